@@ -1,0 +1,504 @@
+// CommEngine: native RCCL gradient all-reduce engine (one per process group, one GPU per process).
+//
+// Replaces the reference's Python collective layer:
+//   * ring_allreduce        /root/reference/src/allreduce.py:45-98   (Gloo isend/recv, CPU buffers)
+//   * ring_allreduce_gpu    /root/reference/src/allreduce.py:100-170 (NCCL pairwise-broadcast emulation)
+//   * central_allreduce     /root/reference/src/allreduce.py:9-43
+//   * built_in_allreduce    /root/reference/src/allreduce.py:5-7
+//   * ReduceImmediatelly    /root/reference/src/reducers.py:6-19 (put = reduce in the send thread)
+// and the OurDist send/receive threads (/root/reference/src/ourdist.py:102-132): instead of two
+// Python threads and queues, every bucket becomes a short sequence on a dedicated high-priority
+// HIP stream: wait(grad-ready event) -> [pack kernel] -> collective -> [unpack kernel] -> record
+// done event. The compute stream joins on the last done event in sync_gradients(); the CPU never
+// blocks on communication.
+//
+// Algorithms (all average in place when `average`):
+//   BUILTIN  ncclAllReduce(ncclAvg/ncclSum) — RCCL chooses its own channels over xGMI.
+//   RING     reference ring schedule (reduce-scatter then all-gather, N-1 steps each) on
+//            ncclSend/ncclRecv, split over C channels; channel c walks its own ring order, so with
+//            7 edge-disjoint Hamiltonian rings every xGMI link of an 8-GPU node carries 1/7 of the
+//            bucket concurrently. C = 1 is exactly the reference algorithm.
+//   DIRECT   two-shot over all peers: grouped P2P scatter of chunk j to peer j, one k-way reduce
+//            kernel, grouped P2P all-gather. 2 network phases, all 7 links busy in both.
+//   CENTRAL  parameter server: root receives N-1 full copies, one k-way reduce kernel, sends back.
+//   RSAG     ncclReduceScatter + ncclAllGather (RCCL's native two-shot).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "dla_bindings.h"
+#include "dla_kernels.h"
+#include "dla_tables.h"
+
+namespace dla {
+
+#define DLA_NCCL_CHECK(expr)                                                                  \
+  do {                                                                                        \
+    ncclResult_t _r = (expr);                                                                 \
+    if (_r != ncclSuccess) {                                                                  \
+      throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(_r) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__) + " (" #expr ")");   \
+    }                                                                                         \
+  } while (0)
+
+#define DLA_HIP_THROW(expr)                                                                  \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) {                                                                  \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                   \
+    }                                                                                        \
+  } while (0)
+
+enum Algo : int { kBuiltin = 0, kRing = 1, kDirect = 2, kCentral = 3, kRsAg = 4 };
+
+static ncclDataType_t nccl_dtype(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return ncclFloat32;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kHalf: return ncclFloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kLong: return ncclInt64;
+    case at::kInt: return ncclInt32;
+    case at::kByte: return ncclUint8;
+    default: TORCH_CHECK(false, "CommEngine: unsupported dtype ", t.scalar_type());
+  }
+  return ncclFloat32;
+}
+
+class CommEngine {
+ public:
+  CommEngine(int rank, int world, pybind11::bytes unique_id, int device, std::vector<std::vector<int>> rings)
+      : rank_(rank), world_(world), device_(device), rings_(std::move(rings)) {
+    std::string id = unique_id;
+    TORCH_CHECK(id.size() == sizeof(ncclUniqueId), "CommEngine: bad unique id size");
+    std::memcpy(&uid_, id.data(), sizeof(ncclUniqueId));
+    c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
+    // High-priority stream from torch's pool so the caching allocator knows it.
+    stream_ = std::make_unique<c10::hip::HIPStream>(c10::hip::getStreamFromPool(/*isHighPriority=*/true, device_));
+    {
+      pybind11::gil_scoped_release nogil;
+      DLA_NCCL_CHECK(ncclCommInitRank(&comm_, world_, uid_, rank_));
+    }
+    if (rings_.empty()) {
+      std::vector<int> r(world_);
+      for (int i = 0; i < world_; ++i) r[i] = i;
+      rings_.push_back(r);
+    }
+    for (auto& r : rings_) {
+      TORCH_CHECK((int)r.size() == world_, "CommEngine: ring order must list every rank once");
+      std::vector<int> pos(world_, -1);
+      for (int i = 0; i < world_; ++i) {
+        TORCH_CHECK(r[i] >= 0 && r[i] < world_ && pos[r[i]] < 0, "CommEngine: ring is not a permutation");
+        pos[r[i]] = i;
+      }
+      ring_pos_.push_back(pos);
+    }
+    DLA_HIP_THROW(hipEventCreateWithFlags(&last_done_, hipEventDisableTiming));
+  }
+
+  ~CommEngine() {
+    if (comm_) {
+      hipStreamSynchronize(stream_->stream());
+      ncclCommDestroy(comm_);
+    }
+    for (auto& e : timing_events_) hipEventDestroy(e);
+    for (auto& e : ready_pool_) hipEventDestroy(e);
+    if (last_done_) hipEventDestroy(last_done_);
+  }
+
+  static pybind11::bytes get_unique_id() {
+    ncclUniqueId id;
+    DLA_NCCL_CHECK(ncclGetUniqueId(&id));
+    return pybind11::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
+  }
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  int num_rings() const { return (int)rings_.size(); }
+
+  // ---------------------------------------------------------------------------------------
+  // Stream plumbing
+  // ---------------------------------------------------------------------------------------
+  // Make the comm stream wait for everything already queued on the caller's current stream.
+  void join_current() {
+    hipStream_t cur = c10::hip::getCurrentHIPStream(device_).stream();
+    hipEvent_t ev = next_ready_event();
+    DLA_HIP_THROW(hipEventRecord(ev, cur));
+    DLA_HIP_THROW(hipStreamWaitEvent(stream_->stream(), ev, 0));
+  }
+
+  // Make the caller's current stream wait for all communication enqueued so far.
+  void wait_on_current() {
+    hipStream_t cur = c10::hip::getCurrentHIPStream(device_).stream();
+    DLA_HIP_THROW(hipEventRecord(last_done_, stream_->stream()));
+    DLA_HIP_THROW(hipStreamWaitEvent(cur, last_done_, 0));
+  }
+
+  void synchronize() {
+    pybind11::gil_scoped_release nogil;
+    DLA_HIP_THROW(hipStreamSynchronize(stream_->stream()));
+  }
+
+  uintptr_t stream_handle() const { return reinterpret_cast<uintptr_t>(stream_->stream()); }
+
+  // ---------------------------------------------------------------------------------------
+  // Collectives. Each call enqueues onto the comm stream after joining the caller's stream.
+  // ---------------------------------------------------------------------------------------
+  void allreduce(at::Tensor flat, int algo, bool average) {
+    check(flat);
+    c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
+    join_current();
+    pybind11::gil_scoped_release nogil;
+    timed([&] { allreduce_on_stream(flat, algo, average); });
+  }
+
+  // Fused bucket path: [pack grads] -> all-reduce -> [unpack], all on the comm stream.
+  // `table` is null when the gradients already live in `flat` (bucket-view mode).
+  void bucket_allreduce(at::Tensor flat, int algo, bool average, PackTable* table, double pack_scale,
+                        double unpack_scale) {
+    check(flat);
+    c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
+    join_current();
+    pybind11::gil_scoped_release nogil;
+    hipStream_t s = stream_->stream();
+    if (table) table->pack_on(flat, pack_scale, s);
+    timed([&] { allreduce_on_stream(flat, algo, average); });
+    if (table) table->unpack_on(flat, unpack_scale, s);
+  }
+
+  void broadcast(at::Tensor t, int root) {
+    check(t);
+    c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
+    join_current();
+    pybind11::gil_scoped_release nogil;
+    DLA_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), root, comm_, stream_->stream()));
+  }
+
+  void allgather(at::Tensor out, at::Tensor in) {
+    check(out);
+    check(in);
+    TORCH_CHECK(out.numel() == in.numel() * world_, "allgather: out must hold world * in elements");
+    c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
+    join_current();
+    pybind11::gil_scoped_release nogil;
+    DLA_NCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype(in), comm_, stream_->stream()));
+  }
+
+  // ---------------------------------------------------------------------------------------
+  // Comm-stream timing (true communication ms, SURVEY.md §7.3 hard part 6).
+  // ---------------------------------------------------------------------------------------
+  void set_timing(bool on) { timing_ = on; }
+  // Returns the summed elapsed ms of all timed collectives since the last call, then resets.
+  double consume_comm_ms() {
+    pybind11::gil_scoped_release nogil;
+    double total = 0.0;
+    DLA_HIP_THROW(hipStreamSynchronize(stream_->stream()));
+    for (size_t i = 0; i + 1 < used_timing_; i += 2) {
+      float ms = 0.f;
+      DLA_HIP_THROW(hipEventElapsedTime(&ms, timing_events_[i], timing_events_[i + 1]));
+      total += ms;
+    }
+    used_timing_ = 0;
+    return total;
+  }
+
+ private:
+  void check(const at::Tensor& t) {
+    TORCH_CHECK(t.is_cuda() && t.device().index() == device_, "CommEngine: tensor must live on cuda:", device_);
+    TORCH_CHECK(t.is_contiguous(), "CommEngine: tensor must be contiguous");
+  }
+
+  hipEvent_t next_ready_event() {
+    // Events are recycled round-robin; a pool of 512 is far more than the buckets in flight.
+    if (ready_pool_.size() < 512) {
+      hipEvent_t e;
+      DLA_HIP_THROW(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ready_pool_.push_back(e);
+      return e;
+    }
+    hipEvent_t e = ready_pool_[ready_next_];
+    ready_next_ = (ready_next_ + 1) % ready_pool_.size();
+    return e;
+  }
+
+  template <typename F>
+  void timed(F&& f) {
+    if (!timing_) {
+      f();
+      return;
+    }
+    while (timing_events_.size() < used_timing_ + 2) {
+      hipEvent_t e;
+      DLA_HIP_THROW(hipEventCreate(&e));
+      timing_events_.push_back(e);
+    }
+    DLA_HIP_THROW(hipEventRecord(timing_events_[used_timing_], stream_->stream()));
+    f();
+    DLA_HIP_THROW(hipEventRecord(timing_events_[used_timing_ + 1], stream_->stream()));
+    used_timing_ += 2;
+  }
+
+  void* scratch(size_t bytes) {
+    if (scratch_.defined() && (size_t)scratch_.numel() >= bytes) return scratch_.data_ptr();
+    // Grow geometrically; the old buffer may still be in use by queued work, so keep the
+    // allocator informed through record_stream semantics: we simply keep the previous buffer
+    // alive until the stream drains.
+    if (scratch_.defined()) {
+      DLA_HIP_THROW(hipStreamSynchronize(stream_->stream()));
+    }
+    size_t want = std::max(bytes, (size_t)(scratch_.defined() ? scratch_.numel() * 2 : (64 << 20)));
+    c10::hip::HIPStreamGuard sg(*stream_);  // allocate on the comm stream: the allocator tracks it there
+    scratch_ = at::empty({(int64_t)want}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, device_));
+    return scratch_.data_ptr();
+  }
+
+  void scale_on_stream(void* data, int64_t n, int dt, float s) {
+    if (s != 1.f) launch_scale(data, n, dt, s, stream_->stream());
+  }
+
+  void allreduce_on_stream(const at::Tensor& flat, int algo, bool average) {
+    const int64_t n = flat.numel();
+    if (n == 0) return;
+    hipStream_t st = stream_->stream();
+    const ncclDataType_t ndt = nccl_dtype(flat);
+    const int dt = (flat.scalar_type() == at::kBFloat16) ? kBF16 : kF32;
+    TORCH_CHECK(algo == kBuiltin || algo == kRsAg || flat.scalar_type() == at::kFloat ||
+                    flat.scalar_type() == at::kBFloat16,
+                "custom all-reduce algorithms support fp32/bf16 only");
+    if (world_ == 1) {  // reference short-circuit (allreduce.py:18-19,55-56)
+      return;
+    }
+    const float avg = average ? 1.f / (float)world_ : 1.f;
+    switch (algo) {
+      case kBuiltin:
+        DLA_NCCL_CHECK(ncclAllReduce(flat.data_ptr(), flat.data_ptr(), n, ndt, average ? ncclAvg : ncclSum, comm_, st));
+        break;
+      case kRsAg: {
+        const size_t esz = flat.element_size();
+        const int64_t per = (n + world_ - 1) / world_;
+        // pad to world*per in scratch
+        char* buf = static_cast<char*>(scratch((size_t)per * world_ * esz * 2));
+        char* full = buf;
+        char* mine = buf + (size_t)per * world_ * esz;
+        DLA_HIP_THROW(hipMemsetAsync(full + n * esz, 0, (per * world_ - n) * esz, st));
+        DLA_HIP_THROW(hipMemcpyAsync(full, flat.data_ptr(), n * esz, hipMemcpyDeviceToDevice, st));
+        DLA_NCCL_CHECK(ncclReduceScatter(full, mine, per, ndt, average ? ncclAvg : ncclSum, comm_, st));
+        DLA_NCCL_CHECK(ncclAllGather(mine, full, per, ndt, comm_, st));
+        DLA_HIP_THROW(hipMemcpyAsync(flat.data_ptr(), full, n * esz, hipMemcpyDeviceToDevice, st));
+        break;
+      }
+      case kRing:
+        ring(flat, dt, avg);
+        break;
+      case kDirect:
+        direct(flat, dt, avg);
+        break;
+      case kCentral:
+        central(flat, dt, avg);
+        break;
+      default:
+        TORCH_CHECK(false, "CommEngine: unknown algorithm ", algo);
+    }
+  }
+
+  // Chunk geometry shared by ring/direct: `parts` contiguous slices of at most `per` elements,
+  // every slice start aligned to 64 elements (256 B fp32) for vectorised reduce kernels.
+  static void split(int64_t n, int parts, std::vector<int64_t>& off, std::vector<int64_t>& len) {
+    int64_t per = (n + parts - 1) / parts;
+    per = (per + 63) / 64 * 64;
+    off.resize(parts);
+    len.resize(parts);
+    for (int i = 0; i < parts; ++i) {
+      off[i] = std::min(n, (int64_t)i * per);
+      len[i] = std::max<int64_t>(0, std::min(n, off[i] + per) - off[i]);
+    }
+  }
+
+  void ring(const at::Tensor& flat, int dt, float avg) {
+    hipStream_t st = stream_->stream();
+    const ncclDataType_t ndt = nccl_dtype(flat);
+    const size_t esz = flat.element_size();
+    const int64_t n = flat.numel();
+    const int C = std::max(1, std::min<int>((int)rings_.size(), (int)((n + 4095) / 4096)));
+    const int N = world_;
+    char* base = static_cast<char*>(flat.data_ptr());
+    // channel slices
+    std::vector<int64_t> coff, clen;
+    split(n, C, coff, clen);
+    // per channel chunk geometry + receive scratch (one max-chunk per channel)
+    std::vector<std::vector<int64_t>> off(C), len(C);
+    int64_t maxchunk = 0;
+    for (int c = 0; c < C; ++c) {
+      split(clen[c], N, off[c], len[c]);
+      for (auto l : len[c]) maxchunk = std::max(maxchunk, l);
+    }
+    char* rbuf = static_cast<char*>(scratch((size_t)maxchunk * esz * C + 256 * C));
+    auto rb = [&](int c) { return rbuf + (size_t)c * ((size_t)maxchunk * esz + 256); };
+
+    // Reduce-scatter: step i sends chunk (pos - i) to the right neighbour, receives chunk
+    // (pos - i - 1) from the left and adds it in (allreduce.py:69-77).
+    for (int phase = 0; phase < 2; ++phase) {
+      for (int i = 0; i < N - 1; ++i) {
+        DLA_NCCL_CHECK(ncclGroupStart());
+        for (int c = 0; c < C; ++c) {
+          const auto& ring = rings_[c];
+          const int pos = ring_pos_[c][rank_];
+          const int right = ring[(pos + 1) % N], left = ring[(pos - 1 + N) % N];
+          const int to_send = ((pos - i + (phase ? 1 : 0)) % N + N) % N;
+          const int to_recv = ((to_send - 1) % N + N) % N;
+          char* cbase = base + (size_t)coff[c] * esz;
+          if (len[c][to_send] > 0)
+            DLA_NCCL_CHECK(ncclSend(cbase + off[c][to_send] * esz, len[c][to_send], ndt, right, comm_, st));
+          if (len[c][to_recv] > 0) {
+            void* dst = phase == 0 ? (void*)rb(c) : (void*)(cbase + off[c][to_recv] * esz);  // AG receives in place
+            DLA_NCCL_CHECK(ncclRecv(dst, len[c][to_recv], ndt, left, comm_, st));
+          }
+        }
+        DLA_NCCL_CHECK(ncclGroupEnd());
+        if (phase == 0) {
+          for (int c = 0; c < C; ++c) {
+            const int pos = ring_pos_[c][rank_];
+            const int to_send = ((pos - i) % N + N) % N;
+            const int to_recv = ((to_send - 1) % N + N) % N;
+            if (len[c][to_recv] == 0) continue;
+            char* dst = base + (size_t)(coff[c] + off[c][to_recv]) * esz;
+            ReduceSrcs rs{};
+            rs.count = 1;
+            rs.ptr[0] = rb(c);
+            // The fully reduced chunk (last RS step) is scaled by 1/N here, so the all-gather
+            // moves final values and no extra pass over the bucket is needed.
+            const float s = (i == N - 2) ? avg : 1.f;
+            launch_reduce_sum(dst, true, rs, len[c][to_recv], dt, s, st);
+          }
+        }
+      }
+    }
+  }
+
+  void direct(const at::Tensor& flat, int dt, float avg) {
+    hipStream_t st = stream_->stream();
+    const ncclDataType_t ndt = nccl_dtype(flat);
+    const size_t esz = flat.element_size();
+    const int64_t n = flat.numel();
+    const int N = world_;
+    char* base = static_cast<char*>(flat.data_ptr());
+    std::vector<int64_t> off, len;
+    split(n, N, off, len);
+    int64_t maxchunk = 0;
+    for (auto l : len) maxchunk = std::max(maxchunk, l);
+    const size_t slot = (size_t)maxchunk * esz + 256;
+    char* rbuf = static_cast<char*>(scratch(slot * N));
+    // Phase 1: scatter — my chunk j goes to rank j; I receive everybody's copy of my chunk.
+    DLA_NCCL_CHECK(ncclGroupStart());
+    for (int k = 1; k < N; ++k) {
+      const int peer = (rank_ + k) % N;
+      const int from = (rank_ - k + N) % N;
+      if (len[peer] > 0) DLA_NCCL_CHECK(ncclSend(base + off[peer] * esz, len[peer], ndt, peer, comm_, st));
+      if (len[rank_] > 0) DLA_NCCL_CHECK(ncclRecv(rbuf + slot * k, len[rank_], ndt, from, comm_, st));
+    }
+    DLA_NCCL_CHECK(ncclGroupEnd());
+    // One k-way reduce of my chunk (+ scale), in batches of kMaxReduceSrc sources.
+    if (len[rank_] > 0) {
+      char* mine = base + off[rank_] * esz;
+      int k = 1;
+      while (k < N) {
+        ReduceSrcs rs{};
+        rs.count = 0;
+        while (k < N && rs.count < kMaxReduceSrc) rs.ptr[rs.count++] = rbuf + slot * k++;
+        launch_reduce_sum(mine, true, rs, len[rank_], dt, k >= N ? avg : 1.f, st);
+      }
+    }
+    // Phase 2: all-gather — send my reduced chunk to everybody, receive theirs in place.
+    DLA_NCCL_CHECK(ncclGroupStart());
+    for (int k = 1; k < N; ++k) {
+      const int peer = (rank_ + k) % N;
+      const int from = (rank_ - k + N) % N;
+      if (len[rank_] > 0) DLA_NCCL_CHECK(ncclSend(base + off[rank_] * esz, len[rank_], ndt, peer, comm_, st));
+      if (len[from] > 0) DLA_NCCL_CHECK(ncclRecv(base + off[from] * esz, len[from], ndt, from, comm_, st));
+    }
+    DLA_NCCL_CHECK(ncclGroupEnd());
+  }
+
+  void central(const at::Tensor& flat, int dt, float avg) {
+    hipStream_t st = stream_->stream();
+    const ncclDataType_t ndt = nccl_dtype(flat);
+    const size_t esz = flat.element_size();
+    const int64_t n = flat.numel();
+    const int N = world_;
+    void* data = flat.data_ptr();
+    if (rank_ == 0) {
+      const size_t slot = (size_t)n * esz + 256;
+      char* rbuf = static_cast<char*>(scratch(slot * (N - 1)));
+      DLA_NCCL_CHECK(ncclGroupStart());
+      for (int r = 1; r < N; ++r) DLA_NCCL_CHECK(ncclRecv(rbuf + slot * (r - 1), n, ndt, r, comm_, st));
+      DLA_NCCL_CHECK(ncclGroupEnd());
+      int r = 1;
+      while (r < N) {  // sum in rank order (allreduce.py:30-32)
+        ReduceSrcs rs{};
+        rs.count = 0;
+        while (r < N && rs.count < kMaxReduceSrc) rs.ptr[rs.count++] = rbuf + slot * (r++ - 1);
+        launch_reduce_sum(data, true, rs, n, dt, r >= N ? avg : 1.f, st);
+      }
+      DLA_NCCL_CHECK(ncclGroupStart());
+      for (int q = 1; q < N; ++q) DLA_NCCL_CHECK(ncclSend(data, n, ndt, q, comm_, st));
+      DLA_NCCL_CHECK(ncclGroupEnd());
+    } else {
+      DLA_NCCL_CHECK(ncclSend(data, n, ndt, 0, comm_, st));
+      DLA_NCCL_CHECK(ncclRecv(data, n, ndt, 0, comm_, st));
+    }
+  }
+
+  int rank_, world_, device_;
+  ncclUniqueId uid_;
+  ncclComm_t comm_ = nullptr;
+  std::unique_ptr<c10::hip::HIPStream> stream_;
+  std::vector<std::vector<int>> rings_;
+  std::vector<std::vector<int>> ring_pos_;
+  at::Tensor scratch_;
+  std::vector<hipEvent_t> ready_pool_;
+  size_t ready_next_ = 0;
+  hipEvent_t last_done_ = nullptr;
+  bool timing_ = false;
+  std::vector<hipEvent_t> timing_events_;
+  size_t used_timing_ = 0;
+};
+
+void bind_comm(pybind11::module& m) {
+  pybind11::class_<CommEngine>(m, "CommEngine")
+      .def(pybind11::init<int, int, pybind11::bytes, int, std::vector<std::vector<int>>>(), pybind11::arg("rank"),
+           pybind11::arg("world"), pybind11::arg("unique_id"), pybind11::arg("device"), pybind11::arg("rings"))
+      .def_static("get_unique_id", &CommEngine::get_unique_id)
+      .def("rank", &CommEngine::rank)
+      .def("world", &CommEngine::world)
+      .def("num_rings", &CommEngine::num_rings)
+      .def("join_current", &CommEngine::join_current)
+      .def("wait_on_current", &CommEngine::wait_on_current)
+      .def("synchronize", &CommEngine::synchronize)
+      .def("stream_handle", &CommEngine::stream_handle)
+      .def("allreduce", &CommEngine::allreduce, pybind11::arg("flat"), pybind11::arg("algo"), pybind11::arg("average"))
+      .def("bucket_allreduce", &CommEngine::bucket_allreduce, pybind11::arg("flat"), pybind11::arg("algo"),
+           pybind11::arg("average"), pybind11::arg("table").none(true), pybind11::arg("pack_scale") = 1.0,
+           pybind11::arg("unpack_scale") = 1.0)
+      .def("broadcast", &CommEngine::broadcast)
+      .def("allgather", &CommEngine::allgather)
+      .def("set_timing", &CommEngine::set_timing)
+      .def("consume_comm_ms", &CommEngine::consume_comm_ms);
+  m.attr("ALGO_BUILTIN") = (int)kBuiltin;
+  m.attr("ALGO_RING") = (int)kRing;
+  m.attr("ALGO_DIRECT") = (int)kDirect;
+  m.attr("ALGO_CENTRAL") = (int)kCentral;
+  m.attr("ALGO_RSAG") = (int)kRsAg;
+}
+
+}  // namespace dla

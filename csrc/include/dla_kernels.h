@@ -1,0 +1,72 @@
+// Host-visible launcher declarations for the distributed_learning_amd HIP kernels.
+// Kernel translation units include only HIP headers; torch/ATen stays in the binding TUs so
+// that kernel files compile in seconds.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dla {
+
+enum DType : int { kF32 = 0, kBF16 = 1 };
+
+// ---- multi-tensor (multi_tensor.hip) --------------------------------------------------------
+struct SgdEntry {
+  float* param;
+  const void* grad;      // float* or bf16*
+  float* momentum;       // may be null when momentum == 0
+  uint16_t* param_bf16;  // optional bf16 shadow copy of the parameter (null = skip)
+  int64_t numel;
+};
+
+struct SgdParams {
+  float lr;
+  float momentum;
+  float dampening;
+  float weight_decay;
+  float grad_scale;
+  int nesterov;
+  int first_step;
+};
+
+struct PackEntry {
+  void* tensor;    // grad tensor (pack source / unpack destination)
+  int64_t numel;
+  int64_t offset;  // element offset inside the flat bucket
+};
+
+int mt_chunk_elems();
+void launch_sgd(const SgdEntry* entries, const int32_t* prefix, int ntensors, int nblocks, int grad_dtype,
+                bool use_momentum, const SgdParams& hp, hipStream_t stream);
+void launch_pack(const PackEntry* entries, const int32_t* prefix, int ntensors, int nblocks, int src_dtype,
+                 int flat_dtype, void* flat, float scale, hipStream_t stream);
+void launch_unpack(const PackEntry* entries, const int32_t* prefix, int ntensors, int nblocks, int flat_dtype,
+                   int dst_dtype, const void* flat, float scale, hipStream_t stream);
+
+// ---- elementwise reductions for the collectives (reduce.hip) --------------------------------
+constexpr int kMaxReduceSrc = 8;
+struct ReduceSrcs {
+  const void* ptr[kMaxReduceSrc];
+  int count;
+};
+// dst[i] = (dst_in ? dst[i] : 0) + sum_k src_k[i], times scale. All operands share dtype.
+void launch_reduce_sum(void* dst, bool accumulate_dst, const ReduceSrcs& srcs, int64_t n, int dtype,
+                       float scale, hipStream_t stream);
+void launch_scale(void* data, int64_t n, int dtype, float scale, hipStream_t stream);
+
+// ---- synthetic data (synthetic.hip) ---------------------------------------------------------
+void launch_uniform_fill(void* out, int64_t n, int dtype, uint64_t seed, uint64_t offset, float lo, float hi,
+                         hipStream_t stream);
+void launch_randint_fill(int64_t* out, int64_t n, int64_t high, uint64_t seed, uint64_t offset,
+                         hipStream_t stream);
+
+// ---- fused log-softmax + NLL (loss.hip) -----------------------------------------------------
+// logits [B, C] (dtype), target [B] int64 (< 0 = ignored). ws: 3*B floats (row lse, row loss,
+// row valid). loss_out[0] = mean loss over valid rows, loss_out[1] = valid row count.
+// Backward: dlogits = (softmax - onehot) * gout / count.
+void launch_xent_fwd(const void* logits, const int64_t* target, float* ws, float* loss_out, int B, int C,
+                     int dtype, hipStream_t stream);
+void launch_xent_bwd(const void* logits, const int64_t* target, const float* ws, const float* loss_out,
+                     const float* gout, void* dlogits, int B, int C, int dtype, hipStream_t stream);
+
+}  // namespace dla

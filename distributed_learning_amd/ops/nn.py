@@ -1,0 +1,52 @@
+"""Model hot-path ops with a selectable backend.
+
+``bn_act(x, bn, relu, residual)`` computes ``act(BN(x) [+ residual])`` — the Conv->BN->ReLU(->add)
+tail of every ResNet/GoogLeNet block. Backends:
+
+* ``"torch"``  — stock PyTorch ops (MIOpen BN, elementwise ReLU/add): the reference behaviour.
+* ``"native"`` — the fused HIP kernel (csrc/kernels/bn_act.hip): one pass to compute the batch
+  statistics, one fused normalise+affine+add+ReLU pass, and a two-pass fused backward; bf16
+  NHWC activations, fp32 statistics.
+
+The backend is process-global (``set_backend``) so a model definition does not change between
+the parity path and the MI355X path.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+_BACKEND = "torch"
+
+
+def set_backend(name: str) -> None:
+    global _BACKEND
+    if name not in ("torch", "native"):
+        raise ValueError(f"unknown ops backend {name!r} (expected 'torch' or 'native')")
+    if name == "native":
+        from . import _ext
+
+        _ext.require()
+    _BACKEND = name
+
+
+def get_backend() -> str:
+    return _BACKEND
+
+
+def _torch_bn_act(x, bn: nn.BatchNorm2d, relu: bool, residual):
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    if relu:
+        y = F.relu(y, inplace=residual is not None)
+    return y
+
+
+def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residual: torch.Tensor | None = None):
+    if _BACKEND == "native" and x.is_cuda:
+        from .bn_act import fused_bn_act
+
+        return fused_bn_act(x, bn, relu, residual)
+    return _torch_bn_act(x, bn, relu, residual)

@@ -1,0 +1,307 @@
+"""All-reduce algorithms over ``torch.distributed`` (Gloo on CPU, RCCL on GPU).
+
+These are the *semantic oracles* and the CPU/Gloo path. On GPU the production path is the native
+RCCL engine (csrc/comm/engine.cpp, :mod:`distributed_learning_amd.parallel.engine`), which runs
+the same schedules from C++ on a dedicated HIP stream; both are tested against
+``dist.all_reduce``.
+
+Every function averages ``send`` in place over the group, like the reference
+(/root/reference/src/allreduce.py):
+
+``builtin``  ``dist.all_reduce(SUM)`` then ``/= N``                      (allreduce.py:5-7)
+``central``  rank 0 gathers N-1 copies, sums in rank order, broadcasts   (allreduce.py:9-43)
+``ring``     reduce-scatter + all-gather with N-1 P2P steps each          (allreduce.py:45-98),
+             generalised to C channels (slices on edge-disjoint ring orders) and to
+             device tensors (the reference's ``ring_allreduce`` always staged through a CPU
+             receive buffer and its GPU variant emulated P2P with pairwise broadcasts,
+             allreduce.py:62,100-170 — native ``batch_isend_irecv`` replaces both).
+``direct``   two-shot: scatter chunk j to rank j from every rank, local k-way sum, all-gather.
+
+Padding: the reference pads short chunk lists with 1-element dummies (allreduce.py:59-60); here
+all ranks compute the same slice geometry and skip empty slices on both sides, so numel < N and
+numel % N != 0 work with no dummy traffic.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _ext
+
+ALIGN = 64
+
+
+# ------------------------------------------------------------------------------------------------
+# geometry helpers
+# ------------------------------------------------------------------------------------------------
+def split_ranges(n: int, parts: int, align: int = ALIGN) -> List[Tuple[int, int]]:
+    """``parts`` contiguous (offset, length) slices of ``n`` elements; starts aligned to ``align``."""
+    per = max(1, -(-n // parts))
+    if per > align:
+        per = -(-per // align) * align
+    out = []
+    for i in range(parts):
+        off = min(n, i * per)
+        out.append((off, max(0, min(n, off + per) - off)))
+    return out
+
+
+def edge_disjoint_rings(n: int, want: int) -> List[List[int]]:
+    """Up to ``want`` directed Hamiltonian cycles of K_n with pairwise-disjoint directed edges.
+
+    For an 8-GPU MI355X node (7 xGMI links per GPU) ``want = 7`` yields 7 rings whose union uses
+    every directed link exactly once, so a C-channel ring keeps all links busy. Deterministic
+    (same answer on every rank). Step rings ``i -> i+s`` (s coprime to n) come first, then a
+    bounded backtracking search for the rest.
+    """
+    if n <= 2:
+        return [list(range(n))]
+    rings: List[List[int]] = []
+    used = set()
+
+    def add(ring):
+        edges = {(ring[i], ring[(i + 1) % n]) for i in range(n)}
+        if edges & used:
+            return False
+        used.update(edges)
+        rings.append(ring)
+        return True
+
+    from math import gcd
+
+    for s in range(1, n):
+        if len(rings) >= want:
+            return rings
+        if gcd(s, n) == 1:
+            add([(i * s) % n for i in range(n)])
+    # backtracking for the remaining cycles (small n only; bounded effort)
+    budget = [200000]
+
+    def search(path, seen):
+        budget[0] -= 1
+        if budget[0] <= 0:
+            return None
+        if len(path) == n:
+            return path if (path[-1], path[0]) not in used else None
+        for v in range(n):
+            if v not in seen and (path[-1], v) not in used:
+                r = search(path + [v], seen | {v})
+                if r:
+                    return r
+        return None
+
+    while len(rings) < want:
+        r = search([0], {0})
+        if not r:
+            break
+        add(r)
+    return rings
+
+
+def _peer_ops(sends, recvs, group):
+    # entries are (tensor, peer) or (tensor, peer, tag); the tag (channel index) keeps messages
+    # between the same pair of ranks matched per channel on Gloo (RCCL matches in issue order).
+    ops = []
+    for e in sends:
+        ops.append(dist.P2POp(dist.isend, e[0], e[1], group, e[2] if len(e) > 2 else 0))
+    for e in recvs:
+        ops.append(dist.P2POp(dist.irecv, e[0], e[1], group, e[2] if len(e) > 2 else 0))
+    return ops
+
+
+def _exchange(sends, recvs, group):
+    """Post all sends/recvs of one step together and wait (deadlock-free in any ring order)."""
+    if not sends and not recvs:
+        return
+    reqs = dist.batch_isend_irecv(_peer_ops(sends, recvs, group))
+    for r in reqs:
+        r.wait()
+
+
+def _add_(dst: torch.Tensor, src: torch.Tensor, scale: float = 1.0):
+    if dst.is_cuda and _ext.available() and dst.dtype in (torch.float32, torch.bfloat16):
+        _ext.require().reduce_sum_(dst, [src], True, scale)
+    else:
+        dst.add_(src)
+        if scale != 1.0:
+            dst.mul_(scale)
+
+
+def _group_ranks(group) -> List[int]:
+    if group is None or group is dist.group.WORLD:
+        return list(range(dist.get_world_size()))
+    return dist.get_process_group_ranks(group)
+
+
+# ------------------------------------------------------------------------------------------------
+# ring primitives on an explicit rank list (used by ring all-reduce and the hierarchical reducer)
+# ------------------------------------------------------------------------------------------------
+class Ring:
+    """Multi-channel ring over the global ranks ``ranks`` (in group order)."""
+
+    def __init__(self, ranks: Sequence[int], group=None, channels: int = 1):
+        self.ranks = list(ranks)
+        self.n = len(self.ranks)
+        self.group = group
+        me = dist.get_rank()
+        self.me = self.ranks.index(me)
+        orders = edge_disjoint_rings(self.n, max(1, channels))
+        # reuse rings if more channels than edge-disjoint cycles were requested
+        self.orders = [orders[c % len(orders)] for c in range(max(1, channels))]
+        self.pos = [order.index(self.me) for order in self.orders]
+
+    def geometry(self, n: int):
+        chan = split_ranges(n, len(self.orders))
+        return [(coff, clen, split_ranges(clen, self.n)) for coff, clen in chan]
+
+    def reduce_scatter_(self, flat: torch.Tensor, scale_last: float = 1.0):
+        """After return, ring position p owns chunk (p+1) % n of every channel, fully reduced."""
+        n = self.n
+        geo = self.geometry(flat.numel())
+        maxc = max((l for _, _, ch in geo for _, l in ch), default=0)
+        rbuf = [flat.new_empty(max(1, maxc)) for _ in geo]
+        for i in range(n - 1):
+            sends, recvs, adds = [], [], []
+            for c, (coff, _, ch) in enumerate(geo):
+                order, pos = self.orders[c], self.pos[c]
+                right, left = self.ranks[order[(pos + 1) % n]], self.ranks[order[(pos - 1) % n]]
+                ts = (pos - i) % n
+                tr = (ts - 1) % n
+                so, sl = ch[ts]
+                ro, rl = ch[tr]
+                if sl:
+                    sends.append((flat[coff + so:coff + so + sl], right, c))
+                if rl:
+                    recvs.append((rbuf[c][:rl], left, c))
+                    adds.append((flat[coff + ro:coff + ro + rl], rbuf[c][:rl]))
+            _exchange(sends, recvs, self.group)
+            s = scale_last if i == n - 2 else 1.0
+            for dst, src in adds:
+                _add_(dst, src, s)
+
+    def all_gather_(self, flat: torch.Tensor):
+        n = self.n
+        geo = self.geometry(flat.numel())
+        for i in range(n - 1):
+            sends, recvs = [], []
+            for c, (coff, _, ch) in enumerate(geo):
+                order, pos = self.orders[c], self.pos[c]
+                right, left = self.ranks[order[(pos + 1) % n]], self.ranks[order[(pos - 1) % n]]
+                ts = (pos - i + 1) % n
+                tr = (ts - 1) % n
+                so, sl = ch[ts]
+                ro, rl = ch[tr]
+                if sl:
+                    sends.append((flat[coff + so:coff + so + sl], right, c))
+                if rl:
+                    recvs.append((flat[coff + ro:coff + ro + rl], left, c))
+            _exchange(sends, recvs, self.group)
+
+    def owned_slices(self, n: int) -> List[Tuple[int, int]]:
+        """(offset, length) of the chunk this rank owns after ``reduce_scatter_``, per channel."""
+        out = []
+        for c, (coff, _, ch) in enumerate(self.geometry(n)):
+            o, l = ch[(self.pos[c] + 1) % self.n]
+            out.append((coff + o, l))
+        return out
+
+
+# ------------------------------------------------------------------------------------------------
+# all-reduce algorithms (average in place)
+# ------------------------------------------------------------------------------------------------
+def built_in_allreduce(send: torch.Tensor, group=None) -> None:
+    size = dist.get_world_size(group)
+    if size <= 1:
+        return
+    if send.is_cuda and dist.get_backend(group) == "nccl":
+        dist.all_reduce(send, op=dist.ReduceOp.AVG, group=group)
+    else:
+        dist.all_reduce(send, op=dist.ReduceOp.SUM, group=group)
+        send.div_(float(size))
+
+
+def ring_allreduce(send: torch.Tensor, group=None, channels: int = 1) -> None:
+    ranks = _group_ranks(group)
+    if len(ranks) <= 1:
+        return
+    ring = Ring(ranks, group, channels)
+    ring.reduce_scatter_(send, scale_last=1.0 / len(ranks))
+    ring.all_gather_(send)
+
+
+def ring_allreduce_gpu(send: torch.Tensor, group=None, channels: int = 1) -> None:
+    """GPU-resident ring (the reference's ``ring_allreduce_gpu`` intent, allreduce.py:100-170)."""
+    ring_allreduce(send, group, channels)
+
+
+def central_allreduce(send: torch.Tensor, group=None) -> None:
+    ranks = _group_ranks(group)
+    n = len(ranks)
+    if n <= 1:
+        return
+    root = ranks[0]
+    if dist.get_rank() == root:
+        bufs = [torch.empty_like(send) for _ in ranks[1:]]
+        _exchange([], list(zip(bufs, ranks[1:])), group)
+        for b in bufs:  # sum in rank order (allreduce.py:30-32)
+            send.add_(b)
+        send.div_(float(n))
+        _exchange([(send, r) for r in ranks[1:]], [], group)
+    else:
+        _exchange([(send, root)], [], group)
+        _exchange([], [(send, root)], group)
+
+
+def direct_allreduce(send: torch.Tensor, group=None) -> None:
+    ranks = _group_ranks(group)
+    n = len(ranks)
+    if n <= 1:
+        return
+    me = ranks.index(dist.get_rank())
+    ch = split_ranges(send.numel(), n)
+    mo, ml = ch[me]
+    bufs = {}
+    sends, recvs = [], []
+    for k in range(1, n):
+        peer, frm = (me + k) % n, (me - k) % n
+        po, pl = ch[peer]
+        if pl:
+            sends.append((send[po:po + pl], ranks[peer]))
+        if ml:
+            bufs[frm] = send.new_empty(ml)
+            recvs.append((bufs[frm], ranks[frm]))
+    _exchange(sends, recvs, group)
+    if ml:
+        mine = send[mo:mo + ml]
+        for frm in sorted(bufs):
+            mine.add_(bufs[frm])
+        mine.div_(float(n))
+    sends, recvs = [], []
+    for k in range(1, n):
+        peer, frm = (me + k) % n, (me - k) % n
+        if ml:
+            sends.append((send[mo:mo + ml], ranks[peer]))
+        fo, fl = ch[frm]
+        if fl:
+            recvs.append((send[fo:fo + fl], ranks[frm]))
+    _exchange(sends, recvs, group)
+
+
+ALGORITHMS: Dict[str, Callable] = {
+    "builtin": built_in_allreduce,
+    "ring": ring_allreduce,
+    "ring_gpu": ring_allreduce_gpu,
+    "central": central_allreduce,
+    "direct": direct_allreduce,
+}
+
+
+def get_algorithm(name: str, channels: int = 1) -> Callable[[torch.Tensor, Optional[object]], None]:
+    if name not in ALGORITHMS:
+        raise ValueError(f"unknown all-reduce algorithm {name!r}; choose from {sorted(ALGORITHMS)}")
+    fn = ALGORITHMS[name]
+    if name.startswith("ring") and channels != 1:
+        return lambda t, group=None: fn(t, group, channels)
+    return fn

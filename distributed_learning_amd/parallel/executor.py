@@ -1,0 +1,164 @@
+"""Bucket executors: where and when a ready bucket's pack -> reduce -> unpack runs.
+
+The reference overlaps communication with backward using two Python threads per worker (send:
+wait bucket event, fuse, ``reducer.put``; receive: ``reducer.get``, unfuse) synchronised by
+``threading.Event``s, with the send thread busy-spinning under the GIL
+(/root/reference/src/ourdist.py:102-132,28-36). Here the same pipeline is expressed per device:
+
+* :class:`NativeStreamExecutor` (GPU, production): the C++ engine enqueues wait(event) ->
+  pack kernel -> RCCL collective -> unpack kernel on its high-priority comm stream straight from
+  the autograd hook; ``finish()`` only makes the compute stream wait on the comm stream — the
+  CPU never blocks.
+* :class:`TorchStreamExecutor` (GPU, torch.distributed collectives on a side stream): same
+  stream/event discipline for the Python algorithms of :mod:`.allreduce`.
+* :class:`ThreadExecutor` (CPU/Gloo): one background thread drains an ordered queue (the
+  reference's send thread, without the spin-wait); ``finish()`` joins the queue.
+* :class:`InlineExecutor`: runs in the caller (sequential F / per-tensor modes, tests).
+"""
+from __future__ import annotations
+
+import queue
+import threading
+from typing import Callable, Optional
+
+import torch
+
+from .bucketing import Bucket
+
+
+class BucketIO:
+    """Host-side pack/unpack of a bucket for the non-native paths."""
+
+    @staticmethod
+    def pack(b: Bucket) -> None:
+        if b.views:  # grads already alias the flat buffer
+            return
+        if b.pack_table is not None:
+            b.pack_table.pack(b.flat, 1.0)
+            return
+        for p, off in zip(b.params, b.offsets):
+            g = p.grad
+            dst = b.flat[off:off + p.numel()]
+            if g is None:
+                dst.zero_()
+            else:
+                dst.copy_(g.reshape(-1))
+
+    @staticmethod
+    def unpack(b: Bucket) -> None:
+        if b.views:
+            return
+        if b.pack_table is not None:
+            b.pack_table.unpack(b.flat, 1.0)
+            return
+        for p, off in zip(b.params, b.offsets):
+            if p.grad is not None:
+                p.grad.view(-1).copy_(b.flat[off:off + p.numel()]) if p.grad.is_contiguous() else \
+                    p.grad.copy_(b.flat[off:off + p.numel()].view_as(p.grad))
+
+
+class Executor:
+    def submit(self, bucket: Bucket) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def finish(self) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def close(self) -> None:
+        pass
+
+
+class InlineExecutor(Executor):
+    def __init__(self, reduce_fn: Callable[[torch.Tensor], None]):
+        self.reduce_fn = reduce_fn
+
+    def submit(self, b: Bucket) -> None:
+        BucketIO.pack(b)
+        self.reduce_fn(b.flat)
+        BucketIO.unpack(b)
+
+    def finish(self) -> None:
+        pass
+
+
+class ThreadExecutor(Executor):
+    """CPU overlap: an ordered worker thread (the reference's send/receive threads in one)."""
+
+    def __init__(self, reduce_fn: Callable[[torch.Tensor], None]):
+        self.reduce_fn = reduce_fn
+        self.q: "queue.Queue[Optional[Bucket]]" = queue.Queue()
+        self.err: Optional[BaseException] = None
+        self.pending = 0
+        self.cv = threading.Condition()
+        self.t = threading.Thread(target=self._run, name="dla-comm", daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while True:
+            b = self.q.get()
+            if b is None:
+                return
+            try:
+                if self.err is None:
+                    BucketIO.pack(b)
+                    self.reduce_fn(b.flat)
+                    BucketIO.unpack(b)
+            except BaseException as e:  # propagate to the training thread in finish()
+                self.err = e
+            finally:
+                with self.cv:
+                    self.pending -= 1
+                    self.cv.notify_all()
+
+    def submit(self, b: Bucket) -> None:
+        with self.cv:
+            self.pending += 1
+        self.q.put(b)
+
+    def finish(self) -> None:
+        with self.cv:
+            while self.pending > 0:
+                self.cv.wait()
+        if self.err is not None:
+            e, self.err = self.err, None
+            raise RuntimeError("gradient communication failed") from e
+
+    def close(self) -> None:
+        self.q.put(None)
+        self.t.join(timeout=10)
+
+
+class TorchStreamExecutor(Executor):
+    """GPU overlap with torch.distributed collectives issued on a dedicated side stream."""
+
+    def __init__(self, reduce_fn: Callable[[torch.Tensor], None], device: torch.device):
+        self.reduce_fn = reduce_fn
+        self.stream = torch.cuda.Stream(device=device, priority=-1)
+
+    def submit(self, b: Bucket) -> None:
+        cur = torch.cuda.current_stream(b.flat.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            BucketIO.pack(b)
+            self.reduce_fn(b.flat)
+            BucketIO.unpack(b)
+
+    def finish(self) -> None:
+        torch.cuda.current_stream().wait_stream(self.stream)
+
+
+class NativeStreamExecutor(Executor):
+    """GPU overlap through the C++ RCCL engine (pack/collective/unpack on its comm stream)."""
+
+    def __init__(self, engine, algorithm: str = "builtin"):
+        self.engine = engine
+        self.algorithm = algorithm
+
+    def submit(self, b: Bucket) -> None:
+        table = None if b.views else b.pack_table
+        if not b.views and table is None:
+            raise RuntimeError("native executor needs grad-as-bucket-view or a native PackTable")
+        self.engine.bucket_allreduce(b.flat, self.algorithm, True, table)
+
+    def finish(self) -> None:
+        self.engine.wait_on_current()

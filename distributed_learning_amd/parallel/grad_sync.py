@@ -1,0 +1,223 @@
+"""GradSync: bucketed, ordered, overlapped gradient averaging — the engine behind every DP wrapper.
+
+Reference mechanics (/root/reference/src/ourdist.py):
+* ``Group`` (13-51): flat buffer per bucket, ``register_hook`` per tensor counting ready grads,
+  an ``Event`` when the bucket is complete, ``fuse``/``unfuse`` copies.
+* ``OurDist`` (53-178): buckets from ``_fusion_grouping_gen``, send/receive threads, unused
+  parameters found by a DFS of the autograd graph at every forward and given
+  ``torch.empty_like`` (uninitialised!) grads, ``sync_gradients`` blocks on an Event.
+
+Fixes and MI355X design:
+1. ``register_post_accumulate_grad_hook`` instead of ``register_hook``: the reference's hook fires
+   *before* AccumulateGrad writes ``.grad`` and papers over it with a spin
+   wait. The post-accumulate hook sees the final gradient; the stream event recorded inside it
+   orders the comm stream behind the kernel that produced it.
+2. Buckets are launched strictly in index order (bucket k only after 0..k-1), so every rank issues
+   identical collective sequences regardless of hook timing — a requirement for RCCL.
+3. ``grad_as_bucket_view`` (GPU default): each ``param.grad`` *is* a strided view of its bucket's
+   flat buffer, so backward accumulates straight into the communication buffer and no pack/unpack
+   pass exists at all; averaging happens inside the collective.
+4. Unused parameters get zero gradients (not ``empty_like``) — by graph walk when
+   ``find_unused_parameters`` (reference semantics), and in any case by ``flush()`` at sync time,
+   which zero-fills and launches whatever never became ready, so a missed parameter can never hang
+   the job.
+5. No CPU blocking on GPU: ``synchronize()`` = compute stream waits on the comm stream.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Callable, Iterable, List, Optional, Sequence, Set
+
+import torch
+
+from ..ops import _ext
+from .bucketing import Bucket, bucketize
+from .executor import (Executor, InlineExecutor, NativeStreamExecutor, ThreadExecutor, TorchStreamExecutor)
+
+
+def find_unused_parameters(output, params: Sequence[torch.Tensor]) -> List[torch.Tensor]:
+    """Parameters not reachable from ``output``'s autograd graph (reference ourdist.py:137-156)."""
+    outs = output if isinstance(output, (list, tuple)) else [output]
+    seen = set()
+    stack = [o.grad_fn for o in outs if isinstance(o, torch.Tensor) and o.grad_fn is not None]
+    reached: Set[int] = set()
+    for fn in stack:
+        seen.add(fn)
+    while stack:
+        fn = stack.pop()
+        var = getattr(fn, "variable", None)
+        if var is not None:
+            reached.add(id(var))
+        for nxt, _ in fn.next_functions:
+            if nxt is not None and nxt not in seen:
+                seen.add(nxt)
+                stack.append(nxt)
+    return [p for p in params if p.requires_grad and id(p) not in reached]
+
+
+class GradSync:
+    """Owns buckets, hooks and an executor for a fixed parameter list."""
+
+    def __init__(self, params: Iterable[torch.Tensor], *, bucket_cap_bytes: int = 25 * 1024 * 1024,
+                 executor: Executor, overlap: bool = True, grad_as_bucket_view: Optional[bool] = None,
+                 comm_dtype: Optional[torch.dtype] = None):
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("GradSync: no parameters require grad")
+        self.device = self.params[0].device
+        self.executor = executor
+        self.overlap = overlap
+        self.comm_dtype = comm_dtype or self.params[0].dtype
+        if grad_as_bucket_view is None:
+            grad_as_bucket_view = self.comm_dtype == self.params[0].dtype
+        if grad_as_bucket_view and self.comm_dtype != self.params[0].dtype:
+            raise ValueError("grad_as_bucket_view requires comm_dtype == parameter dtype")
+        self.grad_as_bucket_view = grad_as_bucket_view
+        self.buckets: List[Bucket] = bucketize(self.params, bucket_cap_bytes)
+        self._owner = {}
+        for b in self.buckets:
+            b.flat = torch.zeros(b.padded_numel, dtype=self.comm_dtype, device=self.device)
+            for j, p in enumerate(b.params):
+                self._owner[id(p)] = (b, j)
+        self._persistent_grads = {}
+        if self.grad_as_bucket_view:
+            self._install_views()
+        elif self.device.type == "cuda":
+            self._install_pack_tables()
+        self._next = 0
+        self._enabled = True
+        self._hooks = []
+        if overlap:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
+        self.step_count = 0
+
+    # -------------------------------------------------------------------------------------------
+    # setup
+    # -------------------------------------------------------------------------------------------
+    def _install_views(self):
+        for b in self.buckets:
+            b.views = []
+            for p, off in zip(b.params, b.offsets):
+                if not p.is_non_overlapping_and_dense():
+                    raise ValueError("grad_as_bucket_view needs dense parameters")
+                v = b.flat[off:off + p.numel()].as_strided(p.shape, p.stride())
+                b.views.append(v)
+                p.grad = v
+
+    def _install_pack_tables(self):
+        """Persistent grad tensors + one native PackTable per bucket (GPU pack mode)."""
+        C = _ext.require()
+        for b in self.buckets:
+            grads = []
+            for p in b.params:
+                g = torch.zeros_like(p)
+                self._persistent_grads[id(p)] = g
+                p.grad = g
+                grads.append(g)
+            b.pack_table = C.PackTable(grads, b.offsets)
+
+    # -------------------------------------------------------------------------------------------
+    # per-step protocol
+    # -------------------------------------------------------------------------------------------
+    def prepare(self) -> None:
+        """Call before backward (the wrappers do it in forward): reset counters, zero buffers."""
+        self._next = 0
+        for b in self.buckets:
+            b.reset()
+        if self.grad_as_bucket_view:
+            for b in self.buckets:
+                for p, v in zip(b.params, b.views):
+                    if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                        p.grad = v
+                b.flat.zero_()
+        elif self._persistent_grads:
+            for p in self.params:
+                g = self._persistent_grads[id(p)]
+                if p.grad is None or p.grad.data_ptr() != g.data_ptr():
+                    p.grad = g
+                g.zero_()
+        else:
+            for p in self.params:
+                if p.grad is not None:
+                    p.grad.zero_()
+
+    def mark_ready(self, params: Iterable[torch.Tensor]) -> None:
+        """Mark parameters that will receive no gradient (unused) as ready with zero grads."""
+        for p in params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            self._ready(p)
+
+    def _on_grad_ready(self, p: torch.Tensor) -> None:
+        if not self._enabled:
+            return
+        b, j = self._owner[id(p)]
+        if self.grad_as_bucket_view and p.grad.data_ptr() != b.views[j].data_ptr():
+            # the user replaced .grad (e.g. set_to_none between prepare and backward): fold it back
+            b.views[j].copy_(p.grad)
+            p.grad = b.views[j]
+        self._ready(p)
+
+    def _ready(self, p: torch.Tensor) -> None:
+        b, _ = self._owner[id(p)]
+        b.ready += 1
+        if b.ready > len(b.params):
+            raise RuntimeError(f"bucket {b.index}: parameter reported ready twice in one step "
+                               "(backward called twice without prepare()/no_sync?)")
+        self._launch_in_order()
+
+    def _launch_in_order(self) -> None:
+        while self._next < len(self.buckets) and self.buckets[self._next].ready == len(self.buckets[self._next].params):
+            b = self.buckets[self._next]
+            b.launched = True
+            self._next += 1
+            self.executor.submit(b)
+
+    def flush(self) -> None:
+        """Launch every bucket that has not been launched (zero-filling missing grads)."""
+        for b in self.buckets[self._next:]:
+            if b.ready < len(b.params):
+                for p in b.params:
+                    if p.grad is None:
+                        p.grad = torch.zeros_like(p)
+                b.ready = len(b.params)
+        self._launch_in_order()
+
+    def synchronize(self) -> None:
+        """All buckets reduced; the caller's stream (GPU) / thread (CPU) may use the grads."""
+        if not self._enabled:
+            return
+        self.flush()
+        self.executor.finish()
+        self.step_count += 1
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulate gradients locally (hooks do not communicate) inside this context."""
+        prev = self._enabled
+        self._enabled = False
+        try:
+            yield
+        finally:
+            self._enabled = prev
+
+    def close(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self.executor.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# executor selection
+# ---------------------------------------------------------------------------------------------
+def make_executor(reducer, device: torch.device, overlap: bool = True) -> Executor:
+    """Pick the executor for a reducer on a device (see executor.py)."""
+    if getattr(reducer, "native", False):
+        return NativeStreamExecutor(reducer.engine, reducer.algorithm)
+    if device.type == "cuda":
+        return TorchStreamExecutor(reducer.reduce, device)
+    if overlap:
+        return ThreadExecutor(reducer.reduce)
+    return InlineExecutor(reducer.reduce)
