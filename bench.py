@@ -1,0 +1,152 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 data-parallel training throughput on MI355X.
+
+BASELINE.json metric: "images/sec (whole node) ResNet-50 synthetic ImageNet at 1/2/4/8 MI355X;
+allreduce ms/step". One process per GPU (torchrun for N > 1, RCCL over xGMI); per-GPU batch is
+fixed (weak scaling). Each timed step is the complete training step of the framework:
+on-device synthetic batch generation (Philox kernel) -> bf16-autocast forward (channels_last)
+-> fused log-softmax+NLL -> backward with bucketed gradient all-reduce overlapped on the C++ RCCL
+engine's comm stream -> fused multi-tensor SGD-momentum update (fp32 master weights).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--algorithm builtin|ring|direct]
+For N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
+           --master-port P bench.py --gpus N --steps K --warmup W
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import distributed_learning_amd as dla  # noqa: E402
+from distributed_learning_amd.data import SyntheticBatches  # noqa: E402
+from distributed_learning_amd.models import get_spec  # noqa: E402
+from distributed_learning_amd.ops import nn as dnn  # noqa: E402
+from distributed_learning_amd.ops.loss import cross_entropy  # noqa: E402
+from distributed_learning_amd.ops.optim import FusedSGD  # noqa: E402
+from distributed_learning_amd.parallel import PipelinedFusedDP, make_reducer  # noqa: E402
+from distributed_learning_amd.parallel import context as ctxmod  # noqa: E402
+
+# Reference throughput at the same device count (GoogLeNet on P100 + Gloo/IPoIB):
+# N=1 the "single"/Ideal run, N>1 the best published real-DP number (PyTorch DDP).
+REFERENCE_IMG_S = {1: 317.5, 2: 573.6, 4: 1096.7, 8: 2040.9, 16: 3703.6}
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch size")
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--algorithm", default="builtin", help="native engine all-reduce: builtin|ring|direct|rsag|central")
+    ap.add_argument("--bucket_mb", type=float, default=25.0)
+    ap.add_argument("--kernels", default=os.environ.get("DLA_KERNELS", "torch"), choices=["torch", "native"])
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--momentum", type=float, default=0.5)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    if "WORLD_SIZE" not in os.environ:
+        os.environ["WORLD_SIZE"] = "1"
+        os.environ["RANK"] = "0"
+        os.environ["LOCAL_RANK"] = "0"
+    c = ctxmod.init(backend="nccl")
+    world, rank = c.world_size, c.rank
+    dev = c.device
+    if a.gpus != world:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
+    torch.backends.cudnn.benchmark = True
+    dnn.set_backend(a.kernels)
+
+    spec = get_spec(a.model)
+    torch.manual_seed(1234)
+    model = spec.build().to(dev).to(memory_format=torch.channels_last)
+    reducer = make_reducer("immediate", a.algorithm, native=True)
+    model = PipelinedFusedDP(model, reducer, int(a.bucket_mb * 1024 * 1024), dev)
+    opt = FusedSGD(model.module.parameters(), lr=a.lr, momentum=a.momentum)
+    data = SyntheticBatches(a.batch, spec.input_shape, spec.num_classes, dev, dtype=torch.float32,
+                            seed=1234, rank=rank, channels_last=True)
+    engine = reducer.engine
+
+    def step():
+        x, y = data.next()
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(x)
+            loss = cross_entropy(out, y)
+        loss.backward()
+        model.sync_gradients()
+        opt.step()
+        return loss
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    engine.consume_comm_ms()
+    engine.set_timing(True)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    comm_ms = engine.consume_comm_ms() / max(1, a.steps)
+    engine.set_timing(False)
+    t = torch.tensor([elapsed, comm_ms], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, comm_ms = float(t[0]), float(t[1])
+    final_loss = float(loss.detach().float())
+    ms = elapsed / a.steps * 1000.0
+    img_s = a.batch * world * a.steps / elapsed
+    ref = REFERENCE_IMG_S.get(world)
+    if rank == 0:
+        rec = {
+            "metric": "images/sec (whole node) ResNet-50 synthetic ImageNet",
+            "value": round(img_s, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(img_s / ref, 3) if ref else None,
+            "dtype": "bf16",
+            "data": "synthetic (on-device Philox uniform images, random labels; random-init weights)",
+            "config": {
+                "model": a.model,
+                "global_batch": a.batch * world,
+                "per_gpu_batch": a.batch,
+                "seq_len": None,
+                "image_size": list(spec.input_shape),
+                "parallelism": f"dp{world}",
+                "allreduce": a.algorithm,
+                "bucket_mb": a.bucket_mb,
+                "kernels": a.kernels,
+                "optimizer": f"fused SGD momentum={a.momentum} (fp32 master weights)",
+            },
+            "allreduce_ms_per_step": round(comm_ms, 3),
+            "final_loss": round(final_loss, 4),
+            "baseline_ref": {"value": ref, "what": "reference best published img/s at this N (GoogLeNet, P100, Gloo)"},
+        }
+        print(json.dumps(rec), flush=True)
+    model.cleanup()
+    ctxmod.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -108,7 +108,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def context() -> DistContext:
+def get_context() -> DistContext:
     if _CTX is None:
         raise RuntimeError("distributed_learning_amd.init() has not been called")
     return _CTX
@@ -133,16 +133,16 @@ def shutdown() -> None:
 
 # Horovod-style accessors ------------------------------------------------------------------------
 def rank() -> int:
-    return context().rank
+    return get_context().rank
 
 
 def size() -> int:
-    return context().world_size
+    return get_context().world_size
 
 
 def local_rank() -> int:
-    return context().local_rank
+    return get_context().local_rank
 
 
 def local_size() -> int:
-    return context().local_world_size
+    return get_context().local_world_size

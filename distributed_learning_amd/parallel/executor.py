@@ -68,6 +68,16 @@ class Executor:
         pass
 
 
+class NullExecutor(Executor):
+    """No communication (single device): buckets are only bookkeeping."""
+
+    def submit(self, b: Bucket) -> None:
+        pass
+
+    def finish(self) -> None:
+        pass
+
+
 class InlineExecutor(Executor):
     def __init__(self, reduce_fn: Callable[[torch.Tensor], None]):
         self.reduce_fn = reduce_fn

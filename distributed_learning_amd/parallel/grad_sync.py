@@ -35,6 +35,17 @@ from .bucketing import Bucket, bucketize
 from .executor import (Executor, InlineExecutor, NativeStreamExecutor, ThreadExecutor, TorchStreamExecutor)
 
 
+def is_dense(t: torch.Tensor) -> bool:
+    """Non-overlapping and dense in some dimension order (contiguous, channels_last, ...)."""
+    dims = sorted((d for d in range(t.dim()) if t.shape[d] != 1), key=lambda d: t.stride(d))
+    expect = 1
+    for d in dims:
+        if t.stride(d) != expect:
+            return False
+        expect *= t.shape[d]
+    return True
+
+
 def find_unused_parameters(output, params: Sequence[torch.Tensor]) -> List[torch.Tensor]:
     """Parameters not reachable from ``output``'s autograd graph (reference ourdist.py:137-156)."""
     outs = output if isinstance(output, (list, tuple)) else [output]
@@ -99,7 +110,7 @@ class GradSync:
         for b in self.buckets:
             b.views = []
             for p, off in zip(b.params, b.offsets):
-                if not p.is_non_overlapping_and_dense():
+                if not is_dense(p):
                     raise ValueError("grad_as_bucket_view needs dense parameters")
                 v = b.flat[off:off + p.numel()].as_strided(p.shape, p.stride())
                 b.views.append(v)

@@ -133,9 +133,9 @@ def make_reducer(kind: str = "immediate", algorithm: str = "ring", *, channels: 
     """Factory used by the experiment runners and the public API."""
     if native:
         if engine is None:
-            from .context import context
+            from .context import get_context
 
-            engine = context().engine()
+            engine = get_context().engine()
         return NativeReducer(engine, algorithm)
     if kind in ("immediate", "1step", "onestep"):
         return ImmediateReducer(algorithm, group, channels)

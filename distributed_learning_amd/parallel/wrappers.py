@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from .executor import NullExecutor
 from .grad_sync import GradSync, find_unused_parameters, make_executor
 from .reducers import Reducer, make_reducer
 
@@ -158,10 +159,22 @@ class WarmupDP(_DPBase):
 
 
 class SingleDevice(_DPBase):
-    """No communication; the 'Ideal' single-device baseline (main.py:239-248)."""
+    """No communication; the 'Ideal' single-device baseline (main.py:239-248).
+
+    Gradients still live in one persistent flat buffer (zeroed by a single memset per step and
+    stable across steps, so the fused optimizer's tensor table is built once)."""
 
     def __init__(self, model, reducer=None, grouping_size: int = 0, grad_buff_device=None):
         super().__init__(model, broadcast=False)
+        self.sync = GradSync(model.parameters(), bucket_cap_bytes=1 << 62, executor=NullExecutor(),
+                             overlap=False, grad_as_bucket_view=True)
+
+    def forward(self, *args, **kw):
+        self.sync.prepare()
+        return self.module(*args, **kw)
+
+    def sync_gradients(self) -> None:
+        self.sync.flush()
 
 
 class TorchDDP(_DPBase):

@@ -1,0 +1,190 @@
+"""The per-worker training loop (reference: ``worker_process``, /root/reference/src/main.py:29-107).
+
+Per batch, identical phase structure and timer names to the reference:
+``batch`` ⊃ ``get_data`` -> ``data2dev`` -> ``zero_grad`` -> ``forward`` (model + loss) -> ``backprop``
+-> ``sync`` (``model.sync_gradients()``) -> ``optimizer_step``, then one row appended with
+``batch_count`` and ``data_len``; at the end ``{exp}_{node}_{worker}_times.csv``,
+``{exp}_{node}_{worker}_loss.txt`` and ``{exp}_config.txt``.
+
+Differences by design:
+* errors propagate (the reference printed and swallowed them, main.py:109-114, which left the
+  node pump blocked forever);
+* the loss line is formatted from device values collected without a per-step host sync (the
+  reference's f-string forced ``.item()`` every batch) unless ``--sync_timers 1``;
+* a device-accurate ``*_device_times.csv`` (HIP events) is written beside the parity CSV;
+* only one process writes ``{exp}_config.txt`` (the reference raced all workers on it);
+* optional checkpoint save/resume (the reference had none).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import time
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import data as D
+from .models import get_spec
+from .ops import nn as dnn
+from .ops.loss import cross_entropy
+from .ops.optim import FusedSGD
+from .timing import EventTimers, Timers
+from .utils.log import Level, print_d
+
+
+def _model_for(config, device):
+    spec = get_spec(config.model_name)
+    torch.manual_seed(config.seed)  # identical init on all ranks (reference main.py:31) ...
+    model = spec.build().to(device)
+    if device.type == "cuda":
+        model = model.to(memory_format=torch.channels_last)
+    return spec, model
+
+
+def _data_for(config, spec, device, rank: int, node_id: int, worker_id: int):
+    if config.random_input or not config.dataset_root or not os.path.isdir(config.dataset_root):
+        if not config.random_input:
+            print_d(f"dataset root {config.dataset_root!r} not found: using synthetic data", Level.WARNING)
+        return D.SyntheticBatches(config.batch_size, spec.input_shape, spec.num_classes, device,
+                                  dtype=torch.float32, seed=config.seed, rank=rank,
+                                  channels_last=device.type == "cuda")
+    ds = D.load_dataset(spec.dataset, config.dataset_root)
+    return D.get_partition_loader(ds, node_id, worker_id, config.node_dev, config.total_dev, config.batch_size)
+
+
+def save_checkpoint(path: str, model: nn.Module, optimizer, step: int, extra: Optional[dict] = None) -> None:
+    """Rank-0 checkpoint: plain ``torch.save`` of state dicts (new functionality vs the reference)."""
+    if dist.is_initialized() and dist.get_rank() != 0:
+        return
+    inner = getattr(model, "module", model)
+    state = {"model": inner.state_dict(), "optimizer": optimizer.state_dict(), "step": step, "extra": extra or {}}
+    tmp = path + ".tmp"
+    torch.save(state, tmp)
+    os.replace(tmp, path)
+
+
+def load_checkpoint(path: str, model: nn.Module, optimizer=None, map_location=None) -> int:
+    """Load on every rank (``weights_only=True``: tensors and plain containers only)."""
+    state = torch.load(path, map_location=map_location or "cpu", weights_only=True)
+    inner = getattr(model, "module", model)
+    inner.load_state_dict(state["model"])
+    if optimizer is not None and "optimizer" in state:
+        optimizer.load_state_dict(state["optimizer"])
+    return int(state.get("step", 0))
+
+
+def worker_process(config, distribute_model: Callable, reducer, experiment_name: str,
+                   node_id: Optional[int] = None, worker_id: Optional[int] = None) -> dict:
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    node_id = rank // max(1, config.node_dev) if node_id is None else node_id
+    worker_id = rank % max(1, config.node_dev) if worker_id is None else worker_id
+    device = torch.device(f"cuda:{torch.cuda.current_device()}") if config.use_gpu else torch.device("cpu")
+    print_d(f"Starting experiment {experiment_name} ({config.experiment}), {datetime.datetime.now()}", Level.INFO)
+    dnn.set_backend(config.kernels if device.type == "cuda" else "torch")
+
+    spec, model = _model_for(config, device)
+    model = distribute_model(model, reducer, config.grouping_size, device)
+    params = list(getattr(model, "module", model).parameters())
+    optimizer = FusedSGD(params, lr=config.lr, momentum=config.momentum, weight_decay=config.weight_decay)
+    start_step = 0
+    if getattr(config, "resume", None):
+        start_step = load_checkpoint(config.resume, model, optimizer, map_location=device)
+        print_d(f"resumed from {config.resume} at step {start_step}", Level.INFO)
+
+    os.makedirs(config.folder, exist_ok=True)
+    if rank == 0:
+        with open(f"{config.folder}/{experiment_name}_config.txt", "w") as f:
+            f.write(str(config))
+    stem = f"{config.folder}/{experiment_name}_{node_id}_{worker_id}"
+    timers = Timers(sync=bool(config.sync_timers))
+    ev = EventTimers() if device.type == "cuda" else None
+    train_set = _data_for(config, spec, device, rank, node_id, worker_id)
+    autocast = torch.autocast("cuda", dtype=torch.bfloat16) if (device.type == "cuda" and config.dtype == "bf16") \
+        else torch.autocast("cpu", enabled=False)
+    model.train()
+
+    losses = []
+    batch_count = 0
+    t_start = time.time()
+    for epoch in range(config.epoch_count):
+        if batch_count >= config.limit_batches:
+            break
+        gen = iter(train_set)
+        while batch_count < config.limit_batches:
+            timers.start("batch")
+            ev and ev.start("batch")
+            timers.start("get_data")
+            nx = next(gen, None)
+            if nx is None:
+                break
+            x, y = nx
+            timers.end("get_data")
+
+            timers.start("data2dev")
+            x = x.to(device, non_blocking=True)
+            y = y.to(device, non_blocking=True)
+            if device.type == "cuda" and x.dim() == 4:
+                x = x.contiguous(memory_format=torch.channels_last)
+            timers.end("data2dev")
+
+            timers.start("zero_grad")
+            optimizer.zero_grad(set_to_none=True)
+            timers.end("zero_grad")
+
+            timers.start("forward")
+            ev and ev.start("forward")
+            with autocast:
+                out = model(x)
+                loss = cross_entropy(out, y)
+            ev and ev.end("forward")
+            timers.end("forward")
+
+            timers.start("backprop")
+            ev and ev.start("backprop")
+            loss.backward()
+            ev and ev.end("backprop")
+            timers.end("backprop")
+
+            timers.start("sync")
+            ev and ev.start("sync")
+            model.sync_gradients()
+            ev and ev.end("sync")
+            timers.end("sync")
+
+            timers.start("optimizer_step")
+            ev and ev.start("optimizer_step")
+            optimizer.step()
+            ev and ev.end("optimizer_step")
+            timers.end("optimizer_step")
+
+            losses.append(loss.detach().float())
+            if config.sync_timers:
+                print_d(f"Worker {node_id}:{worker_id} loss for batch {batch_count}: {losses[-1].item()}", Level.DEBUG)
+            timers.end("batch")
+            ev and ev.end("batch")
+            extra = {"batch_count": batch_count, "data_len": x.size(0)}
+            timers.end_experiment(experiment_name, extra)
+            if ev:
+                ev.end_experiment(experiment_name, extra)
+            batch_count += 1
+
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    wall = time.time() - t_start
+    values = torch.stack(losses).cpu().tolist() if losses else []
+    with open(f"{stem}_loss.txt", "w") as f:
+        for i, v in enumerate(values):
+            f.write(f"Worker {node_id}:{worker_id} loss for batch {i}: {v}\n")
+    rows = timers.rows()
+    timers.writeout(f"{stem}_times.csv")
+    if ev:
+        ev.writeout(f"{stem}_device_times.csv")
+    if getattr(config, "checkpoint", None):
+        save_checkpoint(config.checkpoint, model, optimizer, start_step + batch_count)
+    model.cleanup()
+    if hasattr(reducer, "cleanup"):
+        reducer.cleanup()
+    return {"losses": values, "rows": rows, "wall_s": wall, "batches": batch_count}

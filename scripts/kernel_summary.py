@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 ``--kernel-trace`` CSV over the steady-state training steps only.
+
+The trace of a bench run also contains start-up work (MIOpen find-mode tuning, warm-up steps)
+that dwarfs a training step, so the stock ``kernel_stats.csv`` is useless for step anatomy. Steps
+are delimited by the framework's on-device synthetic-data kernel (one Philox ``uniform_kernel``
+launch per step); the last ``--steps`` steps are aggregated per kernel and per category.
+
+usage: kernel_summary.py TRACE.csv --steps 8 [--out profiles/NAME]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import re
+from collections import defaultdict
+
+CATS = [
+    ("conv_wgrad", re.compile(r"wrw|bwd_weight|BwdWeight|conv_bwd_w", re.I)),
+    ("conv_dgrad", re.compile(r"igemm_bwd|bwd_data|conv_bwd_d|BwdData|naive_conv.*_bwd", re.I)),
+    ("conv_fwd", re.compile(r"igemm_fwd|conv_fwd|ConvFwd|naive_conv.*_fwd|grouped_conv_fwd", re.I)),
+    ("gemm", re.compile(r"gemm|Cijk|dla_gemm", re.I)),
+    ("batchnorm", re.compile(r"BatchNorm|bn_", re.I)),
+    ("dla_bn_act", re.compile(r"bn_act|bnact", re.I)),
+    ("optimizer", re.compile(r"sgd_kernel|multi_tensor|foreach", re.I)),
+    ("comm", re.compile(r"nccl|rccl|reduce_sum_kernel|pack_kernel|unpack_kernel", re.I)),
+    ("loss", re.compile(r"xent|softmax|nll", re.I)),
+    ("data", re.compile(r"uniform_kernel|randint_kernel", re.I)),
+    ("pool", re.compile(r"pool", re.I)),
+    ("elementwise", re.compile(r"elementwise|Functor|threshold|clamp|fill|copy|SubTensor|Tensor", re.I)),
+]
+
+
+def category(name: str) -> str:
+    for c, rx in CATS:
+        if rx.search(name):
+            return c
+    return "other"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--marker", default="uniform_kernel")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    rows = []
+    with open(a.trace) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    marks = [i for i, (_, _, n) in enumerate(rows) if a.marker in n]
+    if len(marks) < a.steps + 1:
+        start = marks[0] if marks else 0
+        nsteps = max(1, len(marks))
+    else:
+        start = marks[-a.steps - 1]
+        nsteps = a.steps
+    end = marks[-1] if len(marks) > a.steps else len(rows)
+    win = rows[start:end] if len(marks) > a.steps else rows[start:]
+    if len(marks) > a.steps:
+        nsteps = a.steps
+    per = defaultdict(lambda: [0, 0])
+    cat = defaultdict(int)
+    busy = 0
+    for s, e, n in win:
+        d = e - s
+        per[n][0] += 1
+        per[n][1] += d
+        cat[category(n)] += d
+        busy += d
+    wall = (win[-1][1] - win[0][0]) if win else 0
+    lines = []
+    lines.append(f"# Kernel summary: {a.trace}\n")
+    lines.append(f"steady-state steps: {nsteps}; GPU wall per step {wall / nsteps / 1e6:.3f} ms; "
+                 f"summed kernel time per step {busy / nsteps / 1e6:.3f} ms\n")
+    lines.append("\n## By category (ms per step)\n\n| category | ms/step | % |\n|---|---:|---:|")
+    for c, d in sorted(cat.items(), key=lambda x: -x[1]):
+        lines.append(f"| {c} | {d / nsteps / 1e6:.3f} | {100 * d / max(1, busy):.1f} |")
+    lines.append("\n## Top kernels\n\n| kernel | calls/step | ms/step | % |\n|---|---:|---:|---:|")
+    for n, (cnt, d) in sorted(per.items(), key=lambda x: -x[1][1])[:40]:
+        short = n if len(n) < 110 else n[:107] + "..."
+        lines.append(f"| `{short}` | {cnt / nsteps:.1f} | {d / nsteps / 1e6:.3f} | {100 * d / max(1, busy):.1f} |")
+    text = "\n".join(lines) + "\n"
+    print(text)
+    if a.out:
+        with open(a.out + ".md", "w") as f:
+            f.write(text)
+
+
+if __name__ == "__main__":
+    main()

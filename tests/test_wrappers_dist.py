@@ -1,0 +1,152 @@
+"""DP wrapper semantics on Gloo ranks: every strategy yields the exact average
+of the per-rank gradients; N ranks x batch b == 1 rank x batch N*b; unused parameters; parameter
+consistency after several optimizer steps; DistributedOptimizer."""
+import pytest
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from dist_util import run
+
+
+class TinyNet(nn.Module):
+    """No BN / dropout so DP-equivalence is exact; an unused branch like GoogLeNet's aux heads."""
+
+    def __init__(self, unused=False):
+        super().__init__()
+        self.conv = nn.Conv2d(3, 8, 3, padding=1)
+        self.fc1 = nn.Linear(8 * 8 * 8, 32)
+        self.fc2 = nn.Linear(32, 10)
+        self.aux = nn.Linear(32, 10) if unused else None
+
+    def forward(self, x):
+        h = torch.relu(self.conv(x)).flatten(1)
+        h = torch.relu(self.fc1(h))
+        if self.aux is not None:
+            _ = self.aux(h)  # computed, not part of the output (unused parameters)
+        return self.fc2(h)
+
+
+def _data(rank, b=4, seed=0):
+    g = torch.Generator().manual_seed(seed * 1000 + rank)
+    return torch.randn(b, 3, 8, 8, generator=g), torch.randint(0, 10, (b,), generator=g)
+
+
+def _grads(rank, world, strategy, grouping, algo):
+    import distributed_learning_amd as dla
+    from distributed_learning_amd.ops.loss import cross_entropy
+
+    torch.manual_seed(0)
+    model = TinyNet(unused=True)
+    red = dla.make_reducer("immediate", algo, channels=2 if algo == "ring" else 1)
+    cls = {"pf": dla.PipelinedFusedDP, "f": dla.SequentialFusedDP, "pt": dla.PerTensorDP}[strategy]
+    w = cls(model, red, grouping, find_unused_parameters=(strategy == "pf"))
+    x, y = _data(rank)
+    loss = cross_entropy(w(x), y)
+    loss.backward()
+    w.sync_gradients()
+    out = {n: p.grad.clone() for n, p in model.named_parameters()}
+    w.cleanup()
+    return out
+
+
+def _local_grads(world):
+    from distributed_learning_amd.ops.loss import cross_entropy
+
+    acc = None
+    for r in range(world):
+        torch.manual_seed(0)
+        m = TinyNet(unused=True)
+        x, y = _data(r)
+        cross_entropy(m(x), y).backward()
+        g = {n: (p.grad.clone() if p.grad is not None else torch.zeros_like(p)) for n, p in m.named_parameters()}
+        acc = g if acc is None else {k: acc[k] + g[k] for k in acc}
+    return {k: v / world for k, v in acc.items()}
+
+
+@pytest.mark.parametrize("strategy,grouping,algo", [
+    ("pf", 25 * 1024 * 1024, "ring"), ("pf", 0, "ring"), ("pf", 2048, "central"), ("pf", 4096, "direct"),
+    ("f", 25 * 1024 * 1024, "ring"), ("pt", 0, "builtin"),
+])
+def test_strategies_average_exactly(strategy, grouping, algo):
+    world = 3
+    res = run(_grads, world, strategy, grouping, algo)
+    ref = _local_grads(world)
+    for r in res:
+        for k in ref:
+            torch.testing.assert_close(r[k], ref[k], rtol=1e-5, atol=1e-6)
+    assert torch.count_nonzero(res[0]["aux.weight"]) == 0  # unused -> zeros, not garbage
+
+
+def _train(rank, world, steps, use_opt_wrapper):
+    import distributed_learning_amd as dla
+    from distributed_learning_amd.ops.loss import cross_entropy
+    from distributed_learning_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(rank)  # deliberately different init: the wrapper must broadcast rank 0's
+    model = TinyNet()
+    if use_opt_wrapper:
+        dla.broadcast_parameters(model.state_dict(), root_rank=0)
+        opt = dla.DistributedOptimizer(FusedSGD(model.parameters(), lr=0.1, momentum=0.5),
+                                       named_parameters=model.named_parameters(), bucket_cap_mb=0.001)
+        dp = model
+    else:
+        dp = dla.PipelinedFusedDP(model, dla.make_reducer("immediate", "ring"), 4096)
+        opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.5)
+    for s in range(steps):
+        x, y = _data(rank, seed=s)
+        opt.zero_grad()
+        loss = cross_entropy(dp(x), y)
+        loss.backward()
+        if not use_opt_wrapper:
+            dp.sync_gradients()
+        opt.step()
+    return {n: p.detach().clone() for n, p in model.named_parameters()}
+
+
+def _train_big_batch(world, steps):
+    from distributed_learning_amd.ops.loss import cross_entropy
+    from distributed_learning_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(0)
+    model = TinyNet()
+    opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.5)
+    for s in range(steps):
+        xs, ys = zip(*[_data(r, seed=s) for r in range(world)])
+        opt.zero_grad()
+        cross_entropy(model(torch.cat(xs)), torch.cat(ys)).backward()
+        opt.step()
+    return {n: p.detach().clone() for n, p in model.named_parameters()}
+
+
+@pytest.mark.parametrize("use_opt_wrapper", [False, True])
+def test_dp_equivalence_and_consistency(use_opt_wrapper):
+    world, steps = 2, 4
+    res = run(_train, world, steps, use_opt_wrapper)
+    for k in res[0]:
+        torch.testing.assert_close(res[0][k], res[1][k], rtol=0, atol=0)  # identical on all ranks
+    big = _train_big_batch(world, steps)
+    for k in big:
+        torch.testing.assert_close(res[0][k], big[k], rtol=1e-4, atol=1e-5)
+
+
+def _hier_train(rank, world):
+    import distributed_learning_amd as dla
+    from distributed_learning_amd.ops.loss import cross_entropy
+
+    torch.manual_seed(0)
+    model = TinyNet()
+    red = dla.make_reducer("hierarchical", "ring", local_size=2)
+    dp = dla.PipelinedFusedDP(model, red, 2048)
+    x, y = _data(rank)
+    cross_entropy(dp(x), y).backward()
+    dp.sync_gradients()
+    return {n: p.grad.clone() for n, p in model.named_parameters()}
+
+
+def test_hierarchical_wrapper():
+    res = run(_hier_train, 4)
+    ref = _local_grads(4)
+    for k in res[0]:
+        torch.testing.assert_close(res[0][k], ref[k].reshape(res[0][k].shape) if k in ref else res[0][k],
+                                   rtol=1e-5, atol=1e-6)
