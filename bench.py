@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--algorithm", default="builtin", help="native engine all-reduce: builtin|ring|direct|rsag|central")
     ap.add_argument("--bucket_mb", type=float, default=25.0)
     ap.add_argument("--kernels", default=os.environ.get("DLA_KERNELS", "torch"), choices=["torch", "native"])
+    ap.add_argument("--precision", default=os.environ.get("DLA_PRECISION", "autocast"), choices=["autocast", "bf16"],
+                    help="autocast: fp32 params + bf16 autocast; bf16: bf16 weights + fp32 master weights in the "
+                         "fused optimizer (no per-step weight casts, bf16 gradients on the wire)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--momentum", type=float, default=0.5)
     return ap.parse_args()
@@ -72,17 +75,21 @@ def main():
     spec = get_spec(a.model)
     torch.manual_seed(1234)
     model = spec.build().to(dev).to(memory_format=torch.channels_last)
+    bf16 = a.precision == "bf16"
+    if bf16:
+        dnn.bf16_weights(model)
     reducer = make_reducer("immediate", a.algorithm, native=True)
     model = PipelinedFusedDP(model, reducer, int(a.bucket_mb * 1024 * 1024), dev)
-    opt = FusedSGD(model.module.parameters(), lr=a.lr, momentum=a.momentum)
-    data = SyntheticBatches(a.batch, spec.input_shape, spec.num_classes, dev, dtype=torch.float32,
+    opt = FusedSGD(model.module.parameters(), lr=a.lr, momentum=a.momentum, master_weights=bf16)
+    data = SyntheticBatches(a.batch, spec.input_shape, spec.num_classes, dev,
+                            dtype=torch.bfloat16 if bf16 else torch.float32,
                             seed=1234, rank=rank, channels_last=True)
     engine = reducer.engine
 
     def step():
         x, y = data.next()
         opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=not bf16):
             out = model(x)
             loss = cross_entropy(out, y)
         loss.backward()
@@ -137,6 +144,7 @@ def main():
                 "allreduce": a.algorithm,
                 "bucket_mb": a.bucket_mb,
                 "kernels": a.kernels,
+                "precision": a.precision,
                 "optimizer": f"fused SGD momentum={a.momentum} (fp32 master weights)",
             },
             "allreduce_ms_per_step": round(comm_ms, 3),

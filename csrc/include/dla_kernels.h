@@ -69,4 +69,15 @@ void launch_xent_fwd(const void* logits, const int64_t* target, float* ws, float
 void launch_xent_bwd(const void* logits, const int64_t* target, const float* ws, const float* loss_out,
                      const float* gout, void* dlogits, int B, int C, int dtype, hipStream_t stream);
 
+// ---- fused BatchNorm + residual + ReLU, NHWC (bn_act.hip) ------------------------------------
+// x/res/y/dy/dx/dres: [M, C] row-major (channels_last activations), C % 8 == 0, 16-byte aligned.
+// ws: 7*C floats (mean, invstd, scale, shift | k1, m1, k2); part: bn_partial_floats(M, C) floats.
+void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks);
+void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int dtype, const float* gamma,
+                   const float* beta, float eps, float momentum, float* running_mean, float* running_var, float* ws,
+                   float* part, bool relu, bool training, hipStream_t stream);
+void launch_bn_bwd(const void* dy, const void* y, const void* x, void* dx, void* dres, int64_t M, int C, int dtype,
+                   const float* gamma, float* ws, float* part, float* dgamma, float* dbeta, bool relu,
+                   hipStream_t stream);
+
 }  // namespace dla

@@ -1,0 +1,365 @@
+// Fused training-mode BatchNorm + (residual add) + (ReLU), forward and backward, NHWC.
+//
+// Replaces the per-block tail Conv -> BN -> (+identity) -> ReLU of ResNet / GoogLeNet, which stock
+// PyTorch runs as MIOpen BN (2 passes fwd, 3 passes bwd) plus separate elementwise add / ReLU /
+// threshold-backward kernels. Activations are channels_last ([M = N*H*W rows, C channels],
+// C contiguous) so a lane owns 8 consecutive channels = one 16-byte bf16 vector.
+//
+// Forward : stats pass  — per-channel shifted sums S=Σ(x-K), Q=Σ(x-K)^2 (K = x[row 0][c], which
+//                         removes the E[x^2]-E[x]^2 cancellation), per-block partials, no atomics;
+//           finalize    — mean / invstd / scale / shift per channel + running-stat update;
+//           apply pass  — y = relu(x*scale + shift [+ res]) in one read-modify-write.
+// Backward: reduce pass — Σdy', Σdy'(x-mean) with dy' = dy * (y > 0) (ReLU mask from the saved
+//                         output, which the next conv keeps alive anyway — no mask tensor);
+//           finalize    — dgamma, dbeta and the two per-channel dx coefficients;
+//           apply pass  — dx = k1*(dy' - m1 - (x-mean)*k2) [and d_residual = dy'].
+// Traffic per element (bf16): fwd 2R+1W (+1R res), bwd 5R+1W (+1W dres) vs ~7 and ~8 passes for
+// the unfused chain. Partials are reduced in a fixed order -> bitwise reproducible.
+#include "dla_common.h"
+#include "dla_kernels.h"
+
+namespace dla {
+
+constexpr int kBNThreads = 256;
+
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16_t> {
+  __device__ __forceinline__ static void load(const bf16_t* p, float (&v)[8]) {
+    const ushort8_t x = *reinterpret_cast<const ushort8_t*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(x[j]);
+  }
+  __device__ __forceinline__ static void store(bf16_t* p, const float (&v)[8]) {
+    ushort8_t x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = f32_to_bf16(v[j]);
+    *reinterpret_cast<ushort8_t*>(p) = x;
+  }
+};
+template <> struct Vec8<float> {
+  __device__ __forceinline__ static void load(const float* p, float (&v)[8]) {
+    const float4_t a = reinterpret_cast<const float4_t*>(p)[0];
+    const float4_t b = reinterpret_cast<const float4_t*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ __forceinline__ static void store(float* p, const float (&v)[8]) {
+    reinterpret_cast<float4_t*>(p)[0] = float4_t{v[0], v[1], v[2], v[3]};
+    reinterpret_cast<float4_t*>(p)[1] = float4_t{v[4], v[5], v[6], v[7]};
+  }
+};
+
+// Block geometry shared by the two reduction passes: the block covers CT = tpr*8 channels
+// (channel tile blockIdx.x) and rows [r0, r1) (row block blockIdx.y); rpi = 256/tpr rows are in
+// flight per iteration, each row segment of a wave-instruction is a contiguous 16*tpr bytes.
+struct RedGeom {
+  int tpr, rpi, ct;
+};
+
+__device__ __forceinline__ void block_rows(int64_t M, int nrb, int64_t& r0, int64_t& r1) {
+  const int64_t per = (M + nrb - 1) / nrb;
+  r0 = (int64_t)blockIdx.y * per;
+  r1 = min(M, r0 + per);
+}
+
+// Reduce 8 channels x 2 sums across the rpi row groups of the block (LDS), then thread row-group 0
+// writes the block partial. `red` holds rpi x ct x 2 floats.
+__device__ __forceinline__ void block_reduce_write(float (&s)[8], float (&q)[8], int tpr, int rpi, int ct, int C,
+                                                   float* __restrict__ part, int c_base, float* red) {
+  const int lane_c = threadIdx.x % tpr;  // channel group within tile
+  const int rg = threadIdx.x / tpr;      // row group
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[(rg * ct + lane_c * 8 + j) * 2 + 0] = s[j];
+    red[(rg * ct + lane_c * 8 + j) * 2 + 1] = q[j];
+  }
+  __syncthreads();
+  // tree over row groups, each thread handles (channel, which) pairs
+  for (int idx = threadIdx.x; idx < ct * 2; idx += kBNThreads) {
+    float acc = 0.f;
+    for (int g = 0; g < rpi; ++g) acc += red[g * ct * 2 + idx];
+    const int c = idx >> 1, w = idx & 1;
+    part[((int64_t)blockIdx.y * C + c_base + c) * 2 + w] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// forward: statistics
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBNThreads) void bn_stats_kernel(const T* __restrict__ x, int64_t M, int C, int nrb,
+                                                              int tpr, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int rpi = kBNThreads / tpr, ct = tpr * 8;
+  const int c_base = blockIdx.x * ct;
+  const int c0 = c_base + (threadIdx.x % tpr) * 8;
+  const int rg = threadIdx.x / tpr;
+  int64_t r0, r1;
+  block_rows(M, nrb, r0, r1);
+  float K[8], s[8], q[8];
+  Vec8<T>::load(x + c0, K);  // shift = row 0 (same for every block)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+  for (int64_t r = r0 + rg; r < r1; r += rpi) {
+    float v[8];
+    Vec8<T>::load(x + r * C + c0, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = v[j] - K[j];
+      s[j] += d;
+      q[j] = fmaf(d, d, q[j]);
+    }
+  }
+  block_reduce_write(s, q, tpr, rpi, ct, C, part, c_base, red);
+}
+
+__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __restrict__ x0, int x_is_bf16,
+                                                                const float* __restrict__ part, int nrb, int64_t M,
+                                                                int C, const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, float eps,
+                                                                float momentum, float* __restrict__ running_mean,
+                                                                float* __restrict__ running_var,
+                                                                float* __restrict__ ws) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float S = 0.f, Q = 0.f;
+  for (int b = 0; b < nrb; ++b) {
+    S += part[((int64_t)b * C + c) * 2 + 0];
+    Q += part[((int64_t)b * C + c) * 2 + 1];
+  }
+  const float K = x_is_bf16 ? bf16_to_f32(reinterpret_cast<const bf16_t*>(x0)[c]) : reinterpret_cast<const float*>(x0)[c];
+  const float inv_m = 1.f / (float)M;
+  const float dm = S * inv_m;
+  const float mean = K + dm;
+  const float var = fmaxf(Q * inv_m - dm * dm, 0.f);
+  const float invstd = rsqrtf(var + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  // ws layout: [0,C) mean  [C,2C) invstd  [2C,3C) scale  [3C,4C) shift
+  ws[c] = mean;
+  ws[C + c] = invstd;
+  ws[2 * C + c] = g * invstd;
+  ws[3 * C + c] = b - mean * g * invstd;
+  if (running_mean) {
+    const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// forward: apply  y = act(x*scale + shift [+ res])
+// ---------------------------------------------------------------------------------------------
+template <typename T, bool kRes, bool kRelu>
+__global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                              T* __restrict__ y, const float* __restrict__ ws,
+                                                              int64_t M, int C, int nrb, int tpr) {
+  // Same tiling as the reduction passes: a thread owns 8 fixed channels for all its rows, so the
+  // per-channel coefficients live in registers (no per-element index math or table reads).
+  const int rpi = kBNThreads / tpr, ct = tpr * 8;
+  const int c0 = blockIdx.x * ct + (threadIdx.x % tpr) * 8;
+  const int rg = threadIdx.x / tpr;
+  int64_t r0, r1;
+  block_rows(M, nrb, r0, r1);
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = ws[2 * C + c0 + j];
+    sh[j] = ws[3 * C + c0 + j];
+  }
+  for (int64_t r = r0 + rg; r < r1; r += rpi) {
+    const int64_t off = r * C + c0;
+    float a[8];
+    Vec8<T>::load(x + off, a);
+    float rv[8];
+    if (kRes) Vec8<T>::load(res + off, rv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float o = fmaf(a[j], sc[j], sh[j]);
+      if (kRes) o += rv[j];
+      if (kRelu) o = fmaxf(o, 0.f);
+      a[j] = o;
+    }
+    Vec8<T>::store(y + off, a);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// backward: reduce  Σdy', Σdy'(x-mean)
+// ---------------------------------------------------------------------------------------------
+template <typename T, bool kRelu>
+__global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                                   const T* __restrict__ x,
+                                                                   const float* __restrict__ ws, int64_t M, int C,
+                                                                   int nrb, int tpr, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int rpi = kBNThreads / tpr, ct = tpr * 8;
+  const int c_base = blockIdx.x * ct;
+  const int c0 = c_base + (threadIdx.x % tpr) * 8;
+  const int rg = threadIdx.x / tpr;
+  int64_t r0, r1;
+  block_rows(M, nrb, r0, r1);
+  float mean[8], s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mean[j] = ws[c0 + j];
+    s[j] = q[j] = 0.f;
+  }
+  for (int64_t r = r0 + rg; r < r1; r += rpi) {
+    float g[8], xv[8];
+    Vec8<T>::load(dy + r * C + c0, g);
+    Vec8<T>::load(x + r * C + c0, xv);
+    if (kRelu) {
+      float yv[8];
+      Vec8<T>::load(y + r * C + c0, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] += g[j];
+      q[j] = fmaf(g[j], xv[j] - mean[j], q[j]);
+    }
+  }
+  block_reduce_write(s, q, tpr, rpi, ct, C, part, c_base, red);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int64_t M,
+                                                              int C, const float* __restrict__ gamma,
+                                                              float* __restrict__ ws, float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float S = 0.f, Q = 0.f;
+  for (int b = 0; b < nrb; ++b) {
+    S += part[((int64_t)b * C + c) * 2 + 0];
+    Q += part[((int64_t)b * C + c) * 2 + 1];
+  }
+  const float invstd = ws[C + c];
+  const float g = gamma ? gamma[c] : 1.f;
+  if (dgamma) dgamma[c] = Q * invstd;
+  if (dbeta) dbeta[c] = S;
+  const float inv_m = 1.f / (float)M;
+  // dx = g*invstd*(dy' - S/M - (x-mean)*invstd^2*Q/M)
+  // ws layout (bwd): [4C,5C) k1 = g*invstd  [5C,6C) m1 = S/M  [6C,7C) k2 = invstd^2*Q/M
+  ws[4 * C + c] = g * invstd;
+  ws[5 * C + c] = S * inv_m;
+  ws[6 * C + c] = invstd * invstd * Q * inv_m;
+}
+
+template <typename T, bool kRelu, bool kDres>
+__global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                                  const T* __restrict__ x,
+                                                                  const float* __restrict__ ws, T* __restrict__ dx,
+                                                                  T* __restrict__ dres, int64_t M, int C, int nrb,
+                                                                  int tpr) {
+  const int rpi = kBNThreads / tpr, ct = tpr * 8;
+  const int c0 = blockIdx.x * ct + (threadIdx.x % tpr) * 8;
+  const int rg = threadIdx.x / tpr;
+  int64_t r0, r1;
+  block_rows(M, nrb, r0, r1);
+  float mean[8], k1[8], m1[8], k2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mean[j] = ws[c0 + j];
+    k1[j] = ws[4 * C + c0 + j];
+    m1[j] = ws[5 * C + c0 + j];
+    k2[j] = ws[6 * C + c0 + j];
+  }
+  for (int64_t r = r0 + rg; r < r1; r += rpi) {
+    const int64_t off = r * C + c0;
+    float g[8], xv[8];
+    Vec8<T>::load(dy + off, g);
+    Vec8<T>::load(x + off, xv);
+    if (kRelu) {
+      float yv[8];
+      Vec8<T>::load(y + off, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+    }
+    if (kDres) Vec8<T>::store(dres + off, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = k1[j] * (g[j] - m1[j] - (xv[j] - mean[j]) * k2[j]);
+    Vec8<T>::store(dx + off, xv);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks = 2048) {
+  int ct = C;
+  if (ct > 512) ct = 512;
+  while (C % ct) ct -= 8;  // C % 8 == 0 guaranteed by the caller
+  *tpr = ct / 8;
+  *nct = C / ct;
+  const int rpi = kBNThreads / *tpr;
+  int64_t want = target_blocks / *nct;  // ~8 workgroups per CU overall
+  if (want < 1) want = 1;
+  int64_t maxrb = (M + rpi - 1) / rpi;
+  // keep >= 4 row iterations per thread so the per-block partial write is amortised
+  int64_t cap = (M + 4 * rpi - 1) / (4 * rpi);
+  if (cap < 1) cap = 1;
+  *nrb = (int)std::max<int64_t>(1, std::min(std::min(want, maxrb), cap));
+}
+
+void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int dtype, const float* gamma,
+                   const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                   float* ws, float* part, bool relu, bool training, hipStream_t stream) {
+  int tpr, nrb, nct;
+  bn_geometry(M, C, &tpr, &nrb, &nct);
+  if (training) {
+    const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
+    if (dtype == kBF16)
+      hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, dim3(nct, nrb), dim3(kBNThreads), lds, stream, (const bf16_t*)x, M, C,
+                         nrb, tpr, part);
+    else
+      hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nct, nrb), dim3(kBNThreads), lds, stream, (const float*)x, M, C,
+                         nrb, tpr, part);
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, x, dtype == kBF16, part,
+                       nrb, M, C, gamma, beta, eps, momentum, running_mean, running_var, ws);
+  }
+  int atpr, anrb, anct;
+  bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
+#define DLA_BN_APPLY(T, R, A)                                                                                      \
+  hipLaunchKernelGGL((bn_apply_kernel<T, R, A>), dim3(anct, anrb), dim3(kBNThreads), 0, stream, (const T*)x,        \
+                     (const T*)res, (T*)y, (const float*)ws, M, C, anrb, atpr)
+  if (dtype == kBF16) {
+    if (res) { if (relu) DLA_BN_APPLY(bf16_t, true, true); else DLA_BN_APPLY(bf16_t, true, false); }
+    else { if (relu) DLA_BN_APPLY(bf16_t, false, true); else DLA_BN_APPLY(bf16_t, false, false); }
+  } else {
+    if (res) { if (relu) DLA_BN_APPLY(float, true, true); else DLA_BN_APPLY(float, true, false); }
+    else { if (relu) DLA_BN_APPLY(float, false, true); else DLA_BN_APPLY(float, false, false); }
+  }
+#undef DLA_BN_APPLY
+}
+
+void launch_bn_bwd(const void* dy, const void* y, const void* x, void* dx, void* dres, int64_t M, int C, int dtype,
+                   const float* gamma, float* ws, float* part, float* dgamma, float* dbeta, bool relu,
+                   hipStream_t stream) {
+  int tpr, nrb, nct;
+  bn_geometry(M, C, &tpr, &nrb, &nct);
+  const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
+#define DLA_BN_RED(T, R)                                                                                          \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, R>), dim3(nct, nrb), dim3(kBNThreads), lds, stream, (const T*)dy,     \
+                     (const T*)y, (const T*)x, (const float*)ws, M, C, nrb, tpr, part)
+  if (dtype == kBF16) { if (relu) DLA_BN_RED(bf16_t, true); else DLA_BN_RED(bf16_t, false); }
+  else { if (relu) DLA_BN_RED(float, true); else DLA_BN_RED(float, false); }
+#undef DLA_BN_RED
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, part, nrb, M, C, gamma, ws,
+                     dgamma, dbeta);
+  int atpr, anrb, anct;
+  bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
+#define DLA_BN_BAPPLY(T, R, D)                                                                                     \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, R, D>), dim3(anct, anrb), dim3(kBNThreads), 0, stream, (const T*)dy,   \
+                     (const T*)y, (const T*)x, (const float*)ws, (T*)dx, (T*)dres, M, C, anrb, atpr)
+  if (dtype == kBF16) {
+    if (dres) { if (relu) DLA_BN_BAPPLY(bf16_t, true, true); else DLA_BN_BAPPLY(bf16_t, false, true); }
+    else { if (relu) DLA_BN_BAPPLY(bf16_t, true, false); else DLA_BN_BAPPLY(bf16_t, false, false); }
+  } else {
+    if (dres) { if (relu) DLA_BN_BAPPLY(float, true, true); else DLA_BN_BAPPLY(float, false, true); }
+    else { if (relu) DLA_BN_BAPPLY(float, true, false); else DLA_BN_BAPPLY(float, false, false); }
+  }
+#undef DLA_BN_BAPPLY
+}
+
+}  // namespace dla

@@ -1,0 +1,86 @@
+"""Autograd wrapper for the fused BatchNorm(+residual)(+ReLU) HIP kernels (csrc/kernels/bn_act.hip).
+
+Used by :func:`distributed_learning_amd.ops.nn.bn_act` when the ``native`` backend is selected.
+Semantics match ``relu(batch_norm(x, training=bn.training) + residual)`` with PyTorch's running
+statistics update (momentum, unbiased running variance). Inputs that the kernel does not cover
+(channel counts not divisible by 8, non-channels_last layouts, cumulative-average momentum) take
+the stock PyTorch path.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _ext
+
+
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu):
+        C = _ext.require()
+        y, ws = C.bn_act_fwd(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.training = training
+        ctx.save_for_backward(x, y, ws, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        if not ctx.training:
+            raise RuntimeError("fused BN backward in eval mode is not supported; use the torch backend")
+        x, y, ws, weight = ctx.saved_tensors
+        C = _ext.require()
+        dx, dres, dg, db = C.bn_act_bwd(dy, y, x, ws, weight, ctx.relu, ctx.has_res)
+        need = ctx.needs_input_grad
+        return (dx, dg if need[1] else None, db if need[2] else None, dres if ctx.has_res else None,
+                None, None, None, None, None, None)
+
+
+# num_batches_tracked increments are batched into one multi-tensor launch per forward instead of
+# 53 one-element kernels (ResNet-50); flushed by the DP wrappers after the model forward.
+_PENDING_COUNTERS: list = []
+
+
+def flush_bn_counters() -> None:
+    if _PENDING_COUNTERS:
+        torch._foreach_add_(_PENDING_COUNTERS, 1)
+        _PENDING_COUNTERS.clear()
+
+
+def supported(x: torch.Tensor, bn: nn.BatchNorm2d, residual) -> bool:
+    if not (x.is_cuda and x.dim() == 4 and x.shape[1] % 8 == 0):
+        return False
+    if x.dtype not in (torch.bfloat16, torch.float32):
+        return False
+    if not x.is_contiguous(memory_format=torch.channels_last) or x.data_ptr() % 16:
+        return False
+    if residual is not None and (residual.dtype != x.dtype or residual.shape != x.shape
+                                 or not residual.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    if bn.training and bn.momentum is None:  # cumulative moving average: torch path
+        return False
+    if bn.weight is not None and bn.weight.dtype != torch.float32:
+        return False
+    return True
+
+
+def fused_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residual: torch.Tensor | None = None):
+    if not supported(x, bn, residual):
+        y = bn(x)
+        if residual is not None:
+            y = y + residual
+        return torch.relu(y) if relu else y
+    if bn.training:
+        training = True
+        rm, rv = (bn.running_mean, bn.running_var) if bn.track_running_stats else (None, None)
+        if bn.track_running_stats:
+            _PENDING_COUNTERS.append(bn.num_batches_tracked)
+            if len(_PENDING_COUNTERS) >= 1024:  # used without a DP wrapper: flush periodically
+                flush_bn_counters()
+    elif bn.track_running_stats:
+        training, rm, rv = False, bn.running_mean, bn.running_var
+    else:
+        training, rm, rv = True, None, None
+    return _BNAct.apply(x, bn.weight, bn.bias, residual, rm, rv, training, float(bn.momentum or 0.0),
+                        float(bn.eps), relu)

@@ -35,6 +35,21 @@ def get_backend() -> str:
     return _BACKEND
 
 
+def bf16_weights(model: nn.Module) -> nn.Module:
+    """Mixed-precision layout: conv/linear weights in bf16, normalisation params/stats in fp32.
+
+    Used with ``FusedSGD(master_weights=True)`` (fp32 masters live in the optimizer), so the
+    forward runs natively in bf16 with no autocast weight casts and gradients leave backward in
+    bf16 (half the all-reduce bytes)."""
+    norm_types = (nn.BatchNorm1d, nn.BatchNorm2d, nn.BatchNorm3d, nn.LayerNorm, nn.GroupNorm)
+    for m in model.modules():
+        if isinstance(m, norm_types):
+            continue
+        for name, p in list(m.named_parameters(recurse=False)):
+            p.data = p.data.to(torch.bfloat16)
+    return model
+
+
 def _torch_bn_act(x, bn: nn.BatchNorm2d, relu: bool, residual):
     y = bn(x)
     if residual is not None:

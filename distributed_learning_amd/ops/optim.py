@@ -20,18 +20,32 @@ from . import _ext
 
 
 class FusedSGD(torch.optim.Optimizer):
+    """SGD(momentum, dampening, nesterov, weight_decay) as one native launch per (grad dtype) group.
+
+    ``master_weights=True``: low-precision (bf16) parameters get an fp32 master copy in the
+    optimizer state; the kernel reads the bf16 gradient, updates master + momentum in fp32 and
+    writes the rounded bf16 parameter back in the same pass (no separate cast kernels, and no
+    autocast weight casts in the forward). fp32 parameters (e.g. BatchNorm) are updated in place.
+    """
+
     def __init__(self, params, lr: float = 0.01, momentum: float = 0.0, dampening: float = 0.0,
-                 weight_decay: float = 0.0, nesterov: bool = False, grad_scale: float = 1.0):
+                 weight_decay: float = 0.0, nesterov: bool = False, grad_scale: float = 1.0,
+                 master_weights: bool = False):
         if nesterov and (momentum <= 0 or dampening != 0):
             raise ValueError("Nesterov momentum requires a momentum and zero dampening")
         defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
                         nesterov=nesterov, grad_scale=grad_scale)
         super().__init__(params, defaults)
+        self.master_weights = master_weights
         self._tables = {}
 
-    def _group_tensors(self, group):
-        ps = [p for p in group["params"] if p.grad is not None]
-        return ps, [p.grad for p in ps]
+    def _master(self, p):
+        if p.dtype == torch.float32 or not self.master_weights:
+            return None
+        st = self.state[p]
+        if "master" not in st:
+            st["master"] = torch.empty_like(p, dtype=torch.float32).copy_(p)
+        return st["master"]
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -40,33 +54,50 @@ class FusedSGD(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         for gi, group in enumerate(self.param_groups):
-            ps, gs = self._group_tensors(group)
+            ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
                 continue
             mom = group["momentum"]
-            native = ps[0].is_cuda and ps[0].dtype == torch.float32 and _ext.available()
-            if ps[0].is_cuda and not native and _ext.gpu_required():
-                _ext.require()
-            first = False
-            bufs: List[Optional[torch.Tensor]] = []
+            # partition by (grad dtype, first-step) so every launch has uniform semantics
+            parts = {}
             for p in ps:
                 st = self.state[p]
-                if mom != 0 and "momentum_buffer" not in st:
-                    st["momentum_buffer"] = torch.zeros_like(p)
-                    first = True
-                bufs.append(st.get("momentum_buffer"))
-            if native:
-                key = (gi, tuple(p.data_ptr() for p in ps), tuple(g.data_ptr() for g in gs))
-                tab = self._tables.get(gi)
-                if tab is None or tab[0] != key:
-                    C = _ext.require()
-                    tab = (key, C.SgdTable(ps, gs, bufs if mom != 0 else [], []))
-                    self._tables[gi] = tab
-                tab[1].step(group["lr"], mom, group["dampening"], group["weight_decay"], group["nesterov"],
-                            group["grad_scale"], first)
-            else:
-                self._reference_step(ps, gs, bufs, group, first)
+                first = mom != 0 and "momentum_buffer" not in st
+                if mom != 0 and first:
+                    st["momentum_buffer"] = torch.zeros_like(p, dtype=torch.float32)
+                parts.setdefault((p.grad.dtype, first), []).append(p)
+            for (gdt, first), plist in parts.items():
+                self._step_part(gi, group, plist, first)
         return loss
+
+    def _step_part(self, gi, group, ps, first):
+        mom = group["momentum"]
+        gs = [p.grad for p in ps]
+        masters = [self._master(p) for p in ps]
+        bufs = [self.state[p].get("momentum_buffer") for p in ps]
+        native = ps[0].is_cuda and _ext.available() and all(
+            (m is not None) or p.dtype == torch.float32 for p, m in zip(ps, masters))
+        if ps[0].is_cuda and not native and _ext.gpu_required() and not _ext.available():
+            _ext.require()
+        if not native:
+            targets = [m if m is not None else p for p, m in zip(ps, masters)]
+            self._reference_step(targets, [g.float() for g in gs], bufs, group, first)
+            for p, m in zip(ps, masters):
+                if m is not None:
+                    p.copy_(m)
+            return
+        fp = [m if m is not None else p for p, m in zip(ps, masters)]
+        shadows = [p for p, m in zip(ps, masters) if m is not None]
+        if shadows and len(shadows) != len(ps):  # mixed within a part cannot happen: grads share dtype
+            raise RuntimeError("FusedSGD: mixed master/non-master parameters in one launch group")
+        key = (gi, first, tuple(t.data_ptr() for t in fp), tuple(g.data_ptr() for g in gs))
+        tab = self._tables.get(key[:2] + (len(fp), gs[0].dtype))
+        if tab is None or tab[0] != key:
+            C = _ext.require()
+            tab = (key, C.SgdTable(fp, gs, bufs if mom != 0 else [], shadows))
+            self._tables[key[:2] + (len(fp), gs[0].dtype)] = tab
+        tab[1].step(group["lr"], mom, group["dampening"], group["weight_decay"], group["nesterov"],
+                    group["grad_scale"], first)
 
     @staticmethod
     def _reference_step(ps, gs, bufs, group, first):

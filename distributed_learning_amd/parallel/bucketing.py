@@ -65,10 +65,37 @@ class Bucket:
         self.launched = False
 
 
+def dtype_fusion_groups(params: Sequence[torch.Tensor], grouping_size: int) -> List[List[torch.Tensor]]:
+    """Greedy fusion with one open bucket per dtype (mixed-precision models: bf16 weights + fp32 BN).
+
+    Walks ``reversed(params)`` like the reference; a parameter joins the open bucket of its dtype,
+    and a bucket is emitted when it closes, so the list order is the order in which buckets become
+    complete during backward. With a single dtype this is exactly :func:`fusion_groups`.
+    """
+    out: List[List[torch.Tensor]] = []
+    open_: dict = {}
+    for p in reversed(list(params)):
+        size = p.element_size() * p.numel()
+        cur = open_.get(p.dtype)
+        if cur is None:
+            open_[p.dtype] = [[p], size]
+        elif cur[1] + size <= grouping_size:
+            cur[0].append(p)
+            cur[1] += size
+        else:
+            out.append(cur[0])
+            open_[p.dtype] = [[p], size]
+    # close the remaining buckets in the order of their last (most recently added) parameter
+    order = {id(p): i for i, p in enumerate(reversed(list(params)))}
+    for group, _ in sorted(open_.values(), key=lambda g: order[id(g[0][-1])]):
+        out.append(group)
+    return out
+
+
 def bucketize(params: Iterable[torch.Tensor], grouping_size: int) -> List[Bucket]:
     params = [p for p in params if p.requires_grad]
     buckets = []
-    for i, group in enumerate(fusion_groups(params, grouping_size)):
+    for i, group in enumerate(dtype_fusion_groups(params, grouping_size)):
         offs, cur = [], 0
         for p in group:
             offs.append(cur)

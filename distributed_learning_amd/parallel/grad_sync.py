@@ -78,16 +78,19 @@ class GradSync:
         self.device = self.params[0].device
         self.executor = executor
         self.overlap = overlap
-        self.comm_dtype = comm_dtype or self.params[0].dtype
+        # comm_dtype=None: every bucket communicates in its parameters' dtype (mixed-precision
+        # models get separate bf16 / fp32 buckets); a dtype here forces a wire format (e.g. bf16
+        # compression of fp32 gradients, Horovod's Compression.fp16 analogue).
+        self.comm_dtype = comm_dtype
         if grad_as_bucket_view is None:
-            grad_as_bucket_view = self.comm_dtype == self.params[0].dtype
-        if grad_as_bucket_view and self.comm_dtype != self.params[0].dtype:
+            grad_as_bucket_view = comm_dtype is None or all(p.dtype == comm_dtype for p in self.params)
+        if grad_as_bucket_view and comm_dtype is not None and any(p.dtype != comm_dtype for p in self.params):
             raise ValueError("grad_as_bucket_view requires comm_dtype == parameter dtype")
         self.grad_as_bucket_view = grad_as_bucket_view
         self.buckets: List[Bucket] = bucketize(self.params, bucket_cap_bytes)
         self._owner = {}
         for b in self.buckets:
-            b.flat = torch.zeros(b.padded_numel, dtype=self.comm_dtype, device=self.device)
+            b.flat = torch.zeros(b.padded_numel, dtype=comm_dtype or b.params[0].dtype, device=self.device)
             for j, p in enumerate(b.params):
                 self._owner[id(p)] = (b, j)
         self._persistent_grads = {}

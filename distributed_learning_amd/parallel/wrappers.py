@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..ops.bn_act import flush_bn_counters
 from .executor import NullExecutor
 from .grad_sync import GradSync, find_unused_parameters, make_executor
 from .reducers import Reducer, make_reducer
@@ -111,6 +112,7 @@ class PipelinedFusedDP(_DPBase):
     def forward(self, *args, **kw):
         self.sync.prepare()
         out = self.module(*args, **kw)
+        flush_bn_counters()
         if self.find_unused and torch.is_grad_enabled():
             if self._unused_cache is None or not self.static_graph:
                 self._unused_cache = find_unused_parameters(out, self.sync.params)
@@ -171,7 +173,9 @@ class SingleDevice(_DPBase):
 
     def forward(self, *args, **kw):
         self.sync.prepare()
-        return self.module(*args, **kw)
+        out = self.module(*args, **kw)
+        flush_bn_counters()
+        return out
 
     def sync_gradients(self) -> None:
         self.sync.flush()

@@ -21,6 +21,8 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 
+from .utils import trace
+
 
 class Timers:
     def __init__(self, sync: bool = False):
@@ -36,9 +38,11 @@ class Timers:
         return time.time() * 1000.0
 
     def start(self, name: str) -> None:
+        trace.push(name)  # roctx range per phase when DLA_TRACE=1
         self._starts[name] = self._now()
 
     def end(self, name: str) -> None:
+        trace.pop()
         dt = self._now() - self._starts[name]
         self._sums[name] = self._sums.get(name, 0.0) + dt
         self._counts[name] = self._counts.get(name, 0) + 1
@@ -82,15 +86,27 @@ class EventTimers:
         self._pending.append((name, self._open.pop(name), ev))
 
     def end_experiment(self, experiment_name: str, extra_fields: Optional[Dict] = None) -> None:
-        row: Dict[str, float] = {}
-        for name, a, b in self._pending:
-            b.synchronize()
-            row[name] = row.get(name, 0.0) + a.elapsed_time(b)
-        row.update(extra_fields or {})
-        self.collected.append((experiment_name, row))
+        # events are resolved lazily (at writeout) so the training loop never blocks on the GPU
+        self.collected.append((experiment_name, (list(self._pending), dict(extra_fields or {}))))
         self._pending = []
 
+    def _resolve(self) -> None:
+        out = []
+        for name, item in self.collected:
+            if isinstance(item, dict):
+                out.append((name, item))
+                continue
+            events, extra = item
+            row: Dict[str, float] = {}
+            for ph, a, b in events:
+                b.synchronize()
+                row[ph] = row.get(ph, 0.0) + a.elapsed_time(b)
+            row.update(extra)
+            out.append((name, row))
+        self.collected = out
+
     def writeout(self, filename: str) -> None:
+        self._resolve()
         if not self.collected:
             return
         keys = list(self.collected[0][1].keys())

@@ -1,0 +1,107 @@
+"""Fused BN(+residual)(+ReLU) kernels vs an fp32 PyTorch reference of the same op (gpu)."""
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+
+def _close_mostly(a, b, rtol, atol, max_frac=1e-5):
+    """bf16 ReLU boundary: a pre-activation within rounding of 0 may take the other branch in the
+    reference; allow a vanishing fraction of such elements, everything else must match."""
+    bad = ~torch.isclose(a, b, rtol=rtol, atol=atol)
+    assert bad.float().mean().item() <= max_frac, (bad.sum().item(), (a - b).abs().max().item())
+
+
+def _ref(x, bn, relu, res):
+    y = bn(x.float())
+    if res is not None:
+        y = y + res.float()
+    return torch.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 256, 7, 7), (2, 2048, 7, 7), (3, 24, 5, 9), (16, 512, 28, 28)])
+@pytest.mark.parametrize("relu,use_res", [(True, False), (True, True), (False, False)])
+def test_bn_act_fwd_bwd(cuda, dtype, shape, relu, use_res):
+    from distributed_learning_amd.ops.bn_act import fused_bn_act
+
+    torch.manual_seed(0)
+    C = shape[1]
+    bn = nn.BatchNorm2d(C).to(cuda)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    bn_ref = nn.BatchNorm2d(C).to(cuda)
+    bn_ref.load_state_dict(bn.state_dict())
+    x = (torch.randn(shape, device=cuda) * 2 + 0.7).to(dtype).contiguous(memory_format=torch.channels_last)
+    res = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last) if use_res else None
+    x1 = x.clone().requires_grad_(True)
+    r1 = res.clone().requires_grad_(True) if use_res else None
+    y = fused_bn_act(x1, bn, relu, r1)
+    x2 = x.float().clone().requires_grad_(True)
+    r2 = res.float().clone().requires_grad_(True) if use_res else None
+    yr = _ref(x2, bn_ref, relu, r2)
+    tol = dict(rtol=2e-2, atol=3e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(bn.running_mean, bn_ref.running_mean, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_var, bn_ref.running_var, rtol=1e-3, atol=1e-4)
+    g = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    y.backward(g)
+    # Reference backward with the kernel's own ReLU mask: a bf16 pre-activation within rounding of
+    # 0 may sit on the other side of the threshold in fp32, which would flip that element's branch
+    # (and move its channel's dgamma by O(1)); using one mask isolates the BN/residual math.
+    bn_ref.running_mean.copy_(bn.running_mean)  # stats already compared; second forward for grads
+    pre = torch.nn.functional.batch_norm(x2, None, None, bn_ref.weight, bn_ref.bias, True, 0.0, bn_ref.eps)
+    if use_res:
+        pre = pre + r2
+    mask = (y.detach().float() > 0).float() if relu else torch.ones_like(pre)
+    (pre * mask * g.float()).sum().backward()
+    _close_mostly(x1.grad.float(), x2.grad, **tol)
+    btol = dict(rtol=2e-2, atol=5e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(bn.weight.grad, bn_ref.weight.grad, **btol)
+    torch.testing.assert_close(bn.bias.grad, bn_ref.bias.grad, **btol)
+    if use_res:
+        _close_mostly(r1.grad.float(), r2.grad, **tol)
+
+
+def test_bn_act_eval_mode(cuda):
+    from distributed_learning_amd.ops.bn_act import fused_bn_act
+
+    bn = nn.BatchNorm2d(64).to(cuda)
+    with torch.no_grad():
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.5, 2)
+    bn.eval()
+    x = torch.randn(4, 64, 8, 8, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = fused_bn_act(x, bn, True, None)
+    torch.testing.assert_close(y.float(), torch.relu(bn(x.float())), rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_resnet50_native_matches_torch_backend(cuda, dtype):
+    """Whole-model check: the native fused BN path and the stock PyTorch path agree (fp32 tightly;
+    bf16 within the drift two different rounding orders accumulate over 53 BN layers)."""
+    from distributed_learning_amd.models import resnet50
+    from distributed_learning_amd.ops import nn as dnn
+
+    torch.manual_seed(0)
+    m1 = resnet50().to(cuda).to(memory_format=torch.channels_last)
+    m2 = resnet50().to(cuda).to(memory_format=torch.channels_last)
+    m2.load_state_dict(m1.state_dict())
+    x = torch.randn(8, 3, 224, 224, device=cuda).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for backend, m in (("native", m1), ("torch", m2)):
+        dnn.set_backend(backend)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+            out = m(x)
+        out.float().pow(2).mean().backward()
+        outs.append((out.float(), m.conv1.weight.grad.float(), m.fc.weight.grad.float(),
+                     m.layer3[2].conv2.weight.grad.float()))
+    dnn.set_backend("torch")
+    lim = 2e-3 if dtype == torch.float32 else 0.25
+    rels = [float((a - b).norm() / b.norm()) for a, b in zip(outs[0], outs[1])]
+    assert max(rels) < lim, rels
+    for a, b in zip(m1.buffers(), m2.buffers()):
+        if a.dtype == torch.float32:
+            torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2)
