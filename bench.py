@@ -21,10 +21,15 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+_ROOT = os.path.dirname(os.path.abspath(__file__))
+# MIOpen find results for these conv shapes on gfx950 ship with the repo, so a fresh box skips the
+# multi-minute exhaustive search (torch.backends.cudnn.benchmark) and starts from tuned solvers.
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_ROOT, "miopen_db"))
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+sys.path.insert(0, _ROOT)
 
 import distributed_learning_amd as dla  # noqa: E402
 from distributed_learning_amd.data import SyntheticBatches  # noqa: E402
@@ -53,6 +58,8 @@ def parse():
     ap.add_argument("--precision", default=os.environ.get("DLA_PRECISION", "autocast"), choices=["autocast", "bf16"],
                     help="autocast: fp32 params + bf16 autocast; bf16: bf16 weights + fp32 master weights in the "
                          "fused optimizer (no per-step weight casts, bf16 gradients on the wire)")
+    ap.add_argument("--conv", default=os.environ.get("DLA_CONV", "miopen"), choices=["miopen", "native"],
+                    help="1x1 convolutions on the native MFMA GEMMs (with fused BN statistics) or MIOpen")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--momentum", type=float, default=0.5)
     return ap.parse_args()
@@ -71,6 +78,7 @@ def main():
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
     torch.backends.cudnn.benchmark = True
     dnn.set_backend(a.kernels)
+    dnn.set_native_conv(a.conv == "native")
 
     spec = get_spec(a.model)
     torch.manual_seed(1234)
@@ -145,6 +153,7 @@ def main():
                 "bucket_mb": a.bucket_mb,
                 "kernels": a.kernels,
                 "precision": a.precision,
+                "conv1x1": a.conv,
                 "optimizer": f"fused SGD momentum={a.momentum} (fp32 master weights)",
             },
             "allreduce_ms_per_step": round(comm_ms, 3),

@@ -75,9 +75,21 @@ void launch_xent_bwd(const void* logits, const int64_t* target, const float* ws,
 void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks);
 void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int dtype, const float* gamma,
                    const float* beta, float eps, float momentum, float* running_mean, float* running_var, float* ws,
-                   float* part, bool relu, bool training, hipStream_t stream);
+                   float* part, bool relu, bool training, hipStream_t stream, const float* ext_part = nullptr,
+                   int ext_nrb = 0);
 void launch_bn_bwd(const void* dy, const void* y, const void* x, void* dx, void* dres, int64_t M, int C, int dtype,
                    const float* gamma, float* ws, float* part, float* dgamma, float* dbeta, bool relu,
                    hipStream_t stream);
+
+// ---- bf16 MFMA GEMMs (gemm.hip) ---------------------------------------------------------------
+// C[M,N] = A[M,K] B[N,K]^T; optional per-column (sum, sumsq) partials stats[ceil(M/128)][N][2].
+// Requires K % 8 == 0, N % 8 == 0, 16-byte aligned rows.
+int gemm_nt_row_block(int M, int N);
+void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
+                    float* stats, hipStream_t stream);
+// out[Mo,No] (= scale * A^T B [+ out]) with A [K, lda>=Mo], B [K, ldb>=No]; partial: splits*Mo*No f32.
+int gemm_tn_splits(int Mo, int No, int K);
+void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, float* partial, int splits, int Mo, int No,
+                    int K, void* out, int out_dtype, float scale, bool accumulate, hipStream_t stream);
 
 }  // namespace dla

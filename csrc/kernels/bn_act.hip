@@ -112,6 +112,48 @@ __global__ __launch_bounds__(kBNThreads) void bn_stats_kernel(const T* __restric
   block_reduce_write(s, q, tpr, rpi, ct, C, part, c_base, red);
 }
 
+// Parallel partial reduction shared by both finalize kernels. A block owns kFinC = 8 channels and
+// gives each channel 32 lanes (half a wave) that stride over the nrb block partials with 4
+// independent accumulators in flight (the loop is latency-bound otherwise: one dependent 8-byte load
+// chain per lane was ~57 us per call at nrb = 2048), then a 32-lane shuffle tree. Fixed order ->
+// bitwise reproducible.
+constexpr int kFinC = 8;
+
+__device__ __forceinline__ bool reduce_partials(const float* __restrict__ part, int nrb, int C, float& S, float& Q,
+                                                int& c) {
+  const int lane32 = threadIdx.x & 31;
+  c = blockIdx.x * kFinC + (threadIdx.x >> 5);
+  float s[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    const float2* p2 = reinterpret_cast<const float2*>(part);
+    int b = lane32;
+    for (; b + 96 < nrb; b += 128) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float2 v = p2[(int64_t)(b + 32 * u) * C + c];
+        s[u] += v.x;
+        q[u] += v.y;
+      }
+    }
+    for (; b < nrb; b += 32) {
+      const float2 v = p2[(int64_t)b * C + c];
+      s[0] += v.x;
+      q[0] += v.y;
+    }
+  }
+  float ss = (s[0] + s[1]) + (s[2] + s[3]);
+  float qq = (q[0] + q[1]) + (q[2] + q[3]);
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) {  // stays inside each 32-lane half of the wave
+    ss += __shfl_xor(ss, off, kWave);
+    qq += __shfl_xor(qq, off, kWave);
+  }
+  if (lane32 != 0 || c >= C) return false;
+  S = ss;
+  Q = qq;
+  return true;
+}
+
 __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __restrict__ x0, int x_is_bf16,
                                                                 const float* __restrict__ part, int nrb, int64_t M,
                                                                 int C, const float* __restrict__ gamma,
@@ -119,14 +161,11 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __re
                                                                 float momentum, float* __restrict__ running_mean,
                                                                 float* __restrict__ running_var,
                                                                 float* __restrict__ ws) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float S = 0.f, Q = 0.f;
-  for (int b = 0; b < nrb; ++b) {
-    S += part[((int64_t)b * C + c) * 2 + 0];
-    Q += part[((int64_t)b * C + c) * 2 + 1];
-  }
-  const float K = x_is_bf16 ? bf16_to_f32(reinterpret_cast<const bf16_t*>(x0)[c]) : reinterpret_cast<const float*>(x0)[c];
+  float S, Q;
+  int c;
+  if (!reduce_partials(part, nrb, C, S, Q, c)) return;
+  const float K = x0 == nullptr ? 0.f
+                  : (x_is_bf16 ? bf16_to_f32(reinterpret_cast<const bf16_t*>(x0)[c]) : reinterpret_cast<const float*>(x0)[c]);
   const float inv_m = 1.f / (float)M;
   const float dm = S * inv_m;
   const float mean = K + dm;
@@ -227,13 +266,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
                                                               int C, const float* __restrict__ gamma,
                                                               float* __restrict__ ws, float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float S = 0.f, Q = 0.f;
-  for (int b = 0; b < nrb; ++b) {
-    S += part[((int64_t)b * C + c) * 2 + 0];
-    Q += part[((int64_t)b * C + c) * 2 + 1];
-  }
+  float S, Q;
+  int c;
+  if (!reduce_partials(part, nrb, C, S, Q, c)) return;
   const float invstd = ws[C + c];
   const float g = gamma ? gamma[c] : 1.f;
   if (dgamma) dgamma[c] = Q * invstd;
@@ -304,10 +339,15 @@ void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_bloc
 
 void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int dtype, const float* gamma,
                    const float* beta, float eps, float momentum, float* running_mean, float* running_var,
-                   float* ws, float* part, bool relu, bool training, hipStream_t stream) {
+                   float* ws, float* part, bool relu, bool training, hipStream_t stream, const float* ext_part,
+                   int ext_nrb) {
   int tpr, nrb, nct;
   bn_geometry(M, C, &tpr, &nrb, &nct);
-  if (training) {
+  if (training && ext_part) {
+    // statistics already produced by the conv GEMM epilogue (unshifted per-row-block partials)
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(256), 0, stream, nullptr, 0, ext_part,
+                       ext_nrb, M, C, gamma, beta, eps, momentum, running_mean, running_var, ws);
+  } else if (training) {
     const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
     if (dtype == kBF16)
       hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, dim3(nct, nrb), dim3(kBNThreads), lds, stream, (const bf16_t*)x, M, C,
@@ -315,7 +355,7 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
     else
       hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nct, nrb), dim3(kBNThreads), lds, stream, (const float*)x, M, C,
                          nrb, tpr, part);
-    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, x, dtype == kBF16, part,
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(256), 0, stream, x, dtype == kBF16, part,
                        nrb, M, C, gamma, beta, eps, momentum, running_mean, running_var, ws);
   }
   int atpr, anrb, anct;
@@ -345,7 +385,7 @@ void launch_bn_bwd(const void* dy, const void* y, const void* x, void* dx, void*
   if (dtype == kBF16) { if (relu) DLA_BN_RED(bf16_t, true); else DLA_BN_RED(bf16_t, false); }
   else { if (relu) DLA_BN_RED(float, true); else DLA_BN_RED(float, false); }
 #undef DLA_BN_RED
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, part, nrb, M, C, gamma, ws,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(256), 0, stream, part, nrb, M, C, gamma, ws,
                      dgamma, dbeta);
   int atpr, anrb, anct;
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);

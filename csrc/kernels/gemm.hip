@@ -1,0 +1,372 @@
+// bf16 MFMA GEMMs for the ResNet 1x1-convolution hot path (channels_last activations).
+//
+// With NHWC activations a 1x1 convolution is a plain GEMM over M = N*H*W rows:
+//   forward  Y[M, Cout]    = X[M, Cin]  * W[Cout, Cin]^T        -> gemm_nt (A = X,  B = W)
+//   dgrad    dX[M, Cin]    = dY[M, Cout] * W[Cout, Cin]         -> gemm_nt (A = dY, B = W^T)
+//   wgrad    dW[Cout, Cin] = dY[M, Cout]^T * X[M, Cin]          -> gemm_tn, split over M
+// The reference runs these as cuDNN/MIOpen convolutions. At ResNet-50 shapes the
+// reduction dim is small (K = 64..2048) so most of these GEMMs sit near the HBM roofline rather than
+// the MFMA roofline; the kernels are built for that regime:
+//   * 256-thread workgroups, 2x2 waves, v_mfma_f32_16x16x32_bf16 (fp32 accumulate), 64-deep K
+//     steps staged through LDS with a register prefetch of the next tile (global loads in flight
+//     while the MFMAs of the current tile run, cdna_hip_programming.md T14), rows padded by 16 B so
+//     the ds_read_b128 fragment reads are bank-conflict free;
+//   * bijective XCD-aware tile remap (T1) so consecutive tiles share an XCD's L2;
+//   * epilogue staged through LDS so the bf16 tile leaves in full 16-byte-per-lane row segments,
+//     with an optional fused per-column (channel) sum / sum-of-squares — the BatchNorm statistics of
+//     the conv output — written as per-row-block partials (no atomics, fixed-order reduction);
+//   * gemm_tn reads k-major operands straight from their natural layout with the gfx950
+//     ds_read_b64_tr_b16 transposing LDS read (T10) and splits the long M reduction over blocks
+//     with fp32 partial slabs + a separate reduction kernel.
+#include "dla_common.h"
+#include "dla_kernels.h"
+
+namespace dla {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kGemmThreads = 256;
+constexpr int kBK = 64;
+
+__device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// C[M,N] = A[M,K] * B[N,K]^T   (all row-major; A, B K-contiguous), bf16 in/out, fp32 accumulate.
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, bool kStats>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                                  const bf16_t* __restrict__ B, int64_t ldb,
+                                                                  bf16_t* __restrict__ C, int64_t ldc, int M, int N,
+                                                                  int K, float* __restrict__ stats) {
+  constexpr int LDS_K = kBK + 8;  // +16 B per row: conflict-free ds_read_b128 fragment reads
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int ACH = BM * kBK / 8 / kGemmThreads;  // 16-byte chunks per thread per A tile
+  constexpr int BCH = BN * kBK / 8 / kGemmThreads;
+  static_assert(ACH >= 1 && BCH >= 1, "tile too small for 256 threads");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem_raw);
+  bf16_t* Bs = As + BM * LDS_K;
+
+  const int nbn = (N + BN - 1) / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int bm = tile / nbn, bn = tile % nbn;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int64_t row0 = (int64_t)bm * BM;
+  const int col0 = bn * BN;
+
+  ushort8_t ra[ACH], rb[BCH];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * kGemmThreads, r = c >> 3, kc = (c & 7) * 8;
+      const int64_t gm = row0 + r;
+      ra[i] = (gm < M && k0 + kc < K) ? *reinterpret_cast<const ushort8_t*>(A + gm * lda + k0 + kc)
+                                      : ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * kGemmThreads, r = c >> 3, kc = (c & 7) * 8;
+      const int gn = col0 + r;
+      rb[i] = (gn < N && k0 + kc < K) ? *reinterpret_cast<const ushort8_t*>(B + (int64_t)gn * ldb + k0 + kc)
+                                      : ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * kGemmThreads;
+      *reinterpret_cast<ushort8_t*>(As + (c >> 3) * LDS_K + (c & 7) * 8) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * kGemmThreads;
+      *reinterpret_cast<ushort8_t*>(Bs + (c >> 3) * LDS_K + (c & 7) * 8) = rb[i];
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (K + kBK - 1) / kBK;
+  gload(0);
+  sstore();
+  __syncthreads();
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) gload((t + 1) * kBK);  // next tile in flight during this tile's MFMAs
+#pragma unroll
+    for (int kk = 0; kk < kBK / 32; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8_t*>(As + (wr * WM + i * 16 + fr) * LDS_K + kk * 32 + fk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bs + (wc * WN + j * 16 + fr) * LDS_K + kk * 32 + fk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    __syncthreads();
+    if (t + 1 < nk) {
+      sstore();
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: bf16 tile -> LDS -> coalesced 16 B stores (+ column statistics) ----
+  constexpr int LDS_C = BN + 8;
+  bf16_t* Cs = reinterpret_cast<bf16_t*>(smem_raw);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wr * WM + i * 16 + (lane >> 4) * 4 + r;  // C/D map: row = 4*(lane>>4)+reg
+        const int n = wc * WN + j * 16 + fr;                    //          col = lane & 15
+        Cs[m * LDS_C + n] = f32_to_bf16(acc[i][j][r]);
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int c = tid; c < BM * CPR; c += kGemmThreads) {
+    const int r = c / CPR, cc = (c % CPR) * 8;
+    const int64_t gm = row0 + r;
+    const int gn = col0 + cc;
+    if (gm < M && gn < N) *reinterpret_cast<ushort8_t*>(C + gm * ldc + gn) = *reinterpret_cast<ushort8_t*>(Cs + r * LDS_C + cc);
+  }
+  if constexpr (kStats) {
+    // per-column sum / sum of squares of the rounded outputs over this tile's valid rows
+    constexpr int RG = kGemmThreads / BN;  // row groups
+    float* red = reinterpret_cast<float*>(smem_raw + BM * LDS_C * sizeof(bf16_t));
+    const int cl = tid % BN, g = tid / BN;
+    float s = 0.f, q = 0.f;
+    if (g < RG) {
+      for (int r = g; r < BM; r += RG) {
+        if (row0 + r < M) {
+          const float v = bf16_to_f32(Cs[r * LDS_C + cl]);
+          s += v;
+          q = fmaf(v, v, q);
+        }
+      }
+      red[(g * BN + cl) * 2 + 0] = s;
+      red[(g * BN + cl) * 2 + 1] = q;
+    }
+    __syncthreads();
+    if (tid < BN && col0 + tid < N) {
+      float S = 0.f, Q = 0.f;
+#pragma unroll
+      for (int gg = 0; gg < RG; ++gg) {
+        S += red[(gg * BN + tid) * 2 + 0];
+        Q += red[(gg * BN + tid) * 2 + 1];
+      }
+      stats[((int64_t)bm * N + col0 + tid) * 2 + 0] = S;
+      stats[((int64_t)bm * N + col0 + tid) * 2 + 1] = Q;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// P[split][Mo, No] = sum_{k in split} A[k][m] * B[k][n]   (A: [K, lda] m-contiguous, B: [K, ldb])
+// fp32 partial slabs; gemm_splitk_reduce sums them.
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_tn_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                                  const bf16_t* __restrict__ B, int64_t ldb,
+                                                                  float* __restrict__ P, int Mo, int No, int K,
+                                                                  int k_per_split) {
+  constexpr int LDS_A = BM + 8, LDS_B = BN + 8;  // rows stay 8-byte aligned for ds_read_b64_tr_b16
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int ACH = kBK * BM / 8 / kGemmThreads, BCH = kBK * BN / 8 / kGemmThreads;
+  static_assert(ACH >= 1 && BCH >= 1, "tile too small");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem_raw);  // [BK][LDS_A]
+  bf16_t* Bs = As + kBK * LDS_A;                     // [BK][LDS_B]
+
+  const int nbn = (No + BN - 1) / BN;
+  const int tile = blockIdx.x;
+  const int bm = tile / nbn, bn = tile % nbn;
+  const int split = blockIdx.y;
+  const int kbeg = split * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int m0 = bm * BM, n0 = bn * BN;
+  constexpr int APR = BM / 8, BPR = BN / 8;  // chunks per k-row
+
+  ushort8_t ra[ACH], rb[BCH];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * kGemmThreads, kr = c / APR, mc = (c % APR) * 8;
+      const int gk = k0 + kr;
+      ra[i] = (gk < kend && m0 + mc < Mo) ? *reinterpret_cast<const ushort8_t*>(A + (int64_t)gk * lda + m0 + mc)
+                                          : ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * kGemmThreads, kr = c / BPR, nc = (c % BPR) * 8;
+      const int gk = k0 + kr;
+      rb[i] = (gk < kend && n0 + nc < No) ? *reinterpret_cast<const ushort8_t*>(B + (int64_t)gk * ldb + n0 + nc)
+                                          : ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * kGemmThreads;
+      *reinterpret_cast<ushort8_t*>(As + (c / APR) * LDS_A + (c % APR) * 8) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * kGemmThreads;
+      *reinterpret_cast<ushort8_t*>(Bs + (c / BPR) * LDS_B + (c % BPR) * 8) = rb[i];
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // transposed fragment reads: in each 16-lane group, lane 4q+p addresses row q, columns 4p..4p+3
+  // of a 4 x 16 block and receives column (lane & 15) of those 4 rows (element q = k).
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int nk = (kend - kbeg + kBK - 1) / kBK;
+  if (nk > 0) {
+    gload(kbeg);
+    sstore();
+    __syncthreads();
+  }
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) gload(kbeg + (t + 1) * kBK);
+#pragma unroll
+    for (int kk = 0; kk < kBK / 32; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+      const int kr = kk * 32 + 8 * g + q;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const bf16_t* base = As + kr * LDS_A + wr * WM + i * 16 + 4 * p;
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4_t*)(base));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4_t*)(base + 4 * LDS_A));
+        const short v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = *reinterpret_cast<const bf16x8_t*>(v);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const bf16_t* base = Bs + kr * LDS_B + wc * WN + j * 16 + 4 * p;
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4_t*)(base));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4_t*)(base + 4 * LDS_B));
+        const short v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(v);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    __syncthreads();
+    if (t + 1 < nk) {
+      sstore();
+      __syncthreads();
+    }
+  }
+  float* Ps = P + (int64_t)split * Mo * No;
+  const int fr = lane & 15;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * WM + i * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wc * WN + j * 16 + fr;
+        if (m < Mo && n < No) Ps[(int64_t)m * No + n] = acc[i][j][r];
+      }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ P, int splits, int64_t n,
+                                                            T* __restrict__ out, float scale, int accumulate) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += P[(int64_t)k * n + i];
+    s *= scale;
+    if (accumulate) s += Cvt<T>::to_f32(out[i]);
+    out[i] = Cvt<T>::from_f32(s);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, bool S>
+static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
+                      int N, int K, float* stats, hipStream_t stream) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  size_t ab = (size_t)(BM + BN) * (kBK + 8) * sizeof(bf16_t);
+  size_t cs = (size_t)BM * (BN + 8) * sizeof(bf16_t) + (S ? (size_t)kGemmThreads / BN * BN * 2 * sizeof(float) : 0);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, S>), dim3(tiles), dim3(kGemmThreads), std::max(ab, cs), stream, A, lda, B,
+                     ldb, C, ldc, M, N, K, stats);
+}
+
+int gemm_nt_row_block(int M, int N) {
+  (void)M;
+  return 128;  // BM of every shipped tile config
+}
+
+void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
+                    float* stats, hipStream_t stream) {
+  const bf16_t* a = (const bf16_t*)A;
+  const bf16_t* b = (const bf16_t*)B;
+  bf16_t* c = (bf16_t*)C;
+  if (N <= 64) {
+    if (stats) launch_nt<128, 64, true>(a, lda, b, ldb, c, ldc, M, N, K, stats, stream);
+    else launch_nt<128, 64, false>(a, lda, b, ldb, c, ldc, M, N, K, stats, stream);
+  } else {
+    if (stats) launch_nt<128, 128, true>(a, lda, b, ldb, c, ldc, M, N, K, stats, stream);
+    else launch_nt<128, 128, false>(a, lda, b, ldb, c, ldc, M, N, K, stats, stream);
+  }
+}
+
+int gemm_tn_splits(int Mo, int No, int K) {
+  const int tiles = ((Mo + 127) / 128) * ((No + 127) / 128);
+  int splits = std::max(1, 1024 / std::max(1, tiles));
+  const int max_splits = std::max(1, (K + 4 * kBK - 1) / (4 * kBK));  // >= 4 K-steps per block
+  return std::min(splits, max_splits);
+}
+
+void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, float* partial, int splits, int Mo, int No,
+                    int K, void* out, int out_dtype, float scale, bool accumulate, hipStream_t stream) {
+  int kps = (K + splits - 1) / splits;
+  kps = (kps + kBK - 1) / kBK * kBK;
+  const int tiles = ((Mo + 127) / 128) * ((No + 127) / 128);
+  const size_t lds = (size_t)kBK * (128 + 8 + 128 + 8) * sizeof(bf16_t);
+  hipLaunchKernelGGL((gemm_tn_kernel<128, 128>), dim3(tiles, splits), dim3(kGemmThreads), lds, stream,
+                     (const bf16_t*)A, lda, (const bf16_t*)B, ldb, partial, Mo, No, K, kps);
+  const int64_t n = (int64_t)Mo * No;
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  if (out_dtype == kF32)
+    hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(grid), dim3(256), 0, stream, partial, splits, n, (float*)out,
+                       scale, (int)accumulate);
+  else
+    hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, dim3(grid), dim3(256), 0, stream, partial, splits, n,
+                       (bf16_t*)out, scale, (int)accumulate);
+}
+
+}  // namespace dla

@@ -30,7 +30,7 @@ static int64_t partial_floats(int64_t M, int C) {
 std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> residual, c10::optional<at::Tensor> weight,
                                    c10::optional<at::Tensor> bias, c10::optional<at::Tensor> running_mean,
                                    c10::optional<at::Tensor> running_var, bool training, double momentum, double eps,
-                                   bool relu) {
+                                   bool relu, c10::optional<at::Tensor> stats) {
   check_act(x, "x");
   const int C = (int)x.size(1);
   const int64_t M = rows_of(x);
@@ -62,11 +62,18 @@ std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> resid
     ws.narrow(0, 2 * C, C).copy_(gm * invstd);
     ws.narrow(0, 3 * C, C).copy_(bt - *running_mean * gm * invstd);
   }
-  at::Tensor part = at::empty({training ? partial_floats(M, C) : 1}, f32);
+  const bool ext = stats.has_value() && stats->defined();
+  if (ext) {
+    TORCH_CHECK(stats->scalar_type() == at::kFloat && stats->is_contiguous() && stats->dim() == 3 &&
+                    stats->size(1) == C && stats->size(2) == 2,
+                "stats must be fp32 [row_blocks, C, 2] partials");
+  }
+  at::Tensor part = at::empty({(training && !ext) ? partial_floats(M, C) : 1}, f32);
   at::Tensor y = at::empty_like(x);
   launch_bn_fwd(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), M, C, dtype_code(x), g, b, (float)eps,
                 (float)momentum, training ? rm : nullptr, training ? rv : nullptr, ws.data_ptr<float>(),
-                part.data_ptr<float>(), relu, training, current_stream(x));
+                part.data_ptr<float>(), relu, training, current_stream(x), ext ? stats->data_ptr<float>() : nullptr,
+                ext ? (int)stats->size(0) : 0);
   return {y, ws};
 }
 
@@ -92,11 +99,55 @@ std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at
   return {dx, dres, dg, db};
 }
 
+static void check_mat(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 2, what, " must be a 2-D GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, what, " must be bf16");
+  TORCH_CHECK(t.stride(1) == 1, what, " must have unit stride in its last dim");
+  TORCH_CHECK(t.size(1) % 8 == 0 && t.stride(0) % 8 == 0, what, ": rows must be multiples of 8 elements");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, what, " must be 16-byte aligned");
+}
+
+// C = A @ B^T (A [M,K], B [N,K]) in bf16 with fp32 accumulation. Optionally returns per-row-block
+// column statistics partials [ceil(M/128), N, 2] (sum, sum of squares of the bf16 outputs).
+std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats) {
+  check_mat(A, "A");
+  check_mat(B, "B");
+  TORCH_CHECK(A.size(1) == B.size(1), "gemm_nt: K mismatch");
+  const int M = (int)A.size(0), N = (int)B.size(0), K = (int)A.size(1);
+  at::Tensor C = at::empty({M, N}, A.options());
+  at::Tensor S;
+  if (stats) S = at::empty({(M + gemm_nt_row_block(M, N) - 1) / gemm_nt_row_block(M, N), N, 2},
+                           A.options().dtype(at::kFloat));
+  if (M > 0 && N > 0)
+    launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K,
+                   stats ? S.data_ptr<float>() : nullptr, current_stream(A));
+  return {C, S};
+}
+
+// out = scale * A^T @ B with A [K, Mo], B [K, No] (reduction over the long row dim, split-K).
+at::Tensor gemm_tn(at::Tensor A, at::Tensor B, c10::ScalarType out_dtype, double scale) {
+  check_mat(A, "A");
+  check_mat(B, "B");
+  TORCH_CHECK(A.size(0) == B.size(0), "gemm_tn: K mismatch");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "gemm_tn: fp32/bf16 output");
+  const int K = (int)A.size(0), Mo = (int)A.size(1), No = (int)B.size(1);
+  at::Tensor out = at::empty({Mo, No}, A.options().dtype(out_dtype));
+  const int splits = gemm_tn_splits(Mo, No, K);
+  at::Tensor part = at::empty({(int64_t)splits * Mo * No}, A.options().dtype(at::kFloat));
+  launch_gemm_tn(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), part.data_ptr<float>(), splits, Mo, No, K,
+                 out.data_ptr(), out_dtype == at::kFloat ? kF32 : kBF16, (float)scale, false, current_stream(A));
+  return out;
+}
+
 void bind_nn(pybind11::module& m) {
+  m.def("gemm_nt", &gemm_nt, "C = A @ B^T (bf16 MFMA), optional fused column statistics", pybind11::arg("A"),
+        pybind11::arg("B"), pybind11::arg("stats") = false);
+  m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),
+        pybind11::arg("out_dtype") = at::kFloat, pybind11::arg("scale") = 1.0);
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC", pybind11::arg("x"),
         pybind11::arg("residual"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"),
         pybind11::arg("running_var"), pybind11::arg("training"), pybind11::arg("momentum"), pybind11::arg("eps"),
-        pybind11::arg("relu"));
+        pybind11::arg("relu"), pybind11::arg("stats") = pybind11::none());
   m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC");
 }
 

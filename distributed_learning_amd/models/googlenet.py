@@ -32,7 +32,7 @@ class BasicConv2d(nn.Module):
         self.bn = nn.BatchNorm2d(cout, eps=0.001)
 
     def forward(self, x):
-        return dnn.bn_act(self.conv(x), self.bn, relu=True)
+        return dnn.conv_bn_act(x, self.conv, self.bn, relu=True)
 
 
 class Inception(nn.Module):

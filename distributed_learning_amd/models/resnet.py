@@ -46,8 +46,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         identity = x if self.downsample is None else self.downsample(x)
-        out = dnn.bn_act(self.conv1(x), self.bn1, relu=True)
-        return dnn.bn_act(self.conv2(out), self.bn2, relu=True, residual=identity)
+        out = dnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        return dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=identity)
 
 
 class Bottleneck(nn.Module):
@@ -66,9 +66,9 @@ class Bottleneck(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         identity = x if self.downsample is None else self.downsample(x)
-        out = dnn.bn_act(self.conv1(x), self.bn1, relu=True)
-        out = dnn.bn_act(self.conv2(out), self.bn2, relu=True)
-        return dnn.bn_act(self.conv3(out), self.bn3, relu=True, residual=identity)
+        out = dnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        out = dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True)
+        return dnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=identity)
 
 
 class Downsample(nn.Sequential):
@@ -78,7 +78,7 @@ class Downsample(nn.Sequential):
         super().__init__(conv1x1(cin, cout, stride), nn.BatchNorm2d(cout))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return dnn.bn_act(self[0](x), self[1], relu=False)
+        return dnn.conv_bn_act(x, self[0], self[1], relu=False)
 
 
 class ResNet(nn.Module):
@@ -123,7 +123,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = dnn.bn_act(self.conv1(x), self.bn1, relu=True)
+        x = dnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
         x = self.maxpool(x)
         x = self.layer1(x)
         x = self.layer2(x)

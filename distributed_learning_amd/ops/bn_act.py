@@ -16,9 +16,10 @@ from . import _ext
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu, stats):
         C = _ext.require()
-        y, ws = C.bn_act_fwd(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu)
+        y, ws = C.bn_act_fwd(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu,
+                             stats)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.training = training
@@ -34,7 +35,7 @@ class _BNAct(torch.autograd.Function):
         dx, dres, dg, db = C.bn_act_bwd(dy, y, x, ws, weight, ctx.relu, ctx.has_res)
         need = ctx.needs_input_grad
         return (dx, dg if need[1] else None, db if need[2] else None, dres if ctx.has_res else None,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 # num_batches_tracked increments are batched into one multi-tensor launch per forward instead of
@@ -65,7 +66,10 @@ def supported(x: torch.Tensor, bn: nn.BatchNorm2d, residual) -> bool:
     return True
 
 
-def fused_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residual: torch.Tensor | None = None):
+def fused_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residual: torch.Tensor | None = None,
+                 stats: torch.Tensor | None = None):
+    """``stats``: optional [row_blocks, C, 2] (sum, sumsq) partials of ``x`` produced by the conv GEMM
+    epilogue (training mode only) — the statistics pass over ``x`` is then skipped."""
     if not supported(x, bn, residual):
         y = bn(x)
         if residual is not None:
@@ -83,4 +87,4 @@ def fused_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residua
     else:
         training, rm, rv = True, None, None
     return _BNAct.apply(x, bn.weight, bn.bias, residual, rm, rv, training, float(bn.momentum or 0.0),
-                        float(bn.eps), relu)
+                        float(bn.eps), relu, stats if training else None)

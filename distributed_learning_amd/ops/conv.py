@@ -1,0 +1,87 @@
+"""1x1 convolutions as native bf16 MFMA GEMMs (csrc/kernels/gemm.hip) on channels_last activations.
+
+For NHWC activations a 1x1 convolution is a GEMM over M = N*H*W rows, so ResNet-50's 36 pointwise
+convs (plus their backward) run on the framework's own MFMA kernels instead of MIOpen:
+
+* forward  ``Y = X W^T``   (``gemm_nt``, optionally emitting the BatchNorm column statistics of Y
+  from the epilogue, so the following fused BN skips its statistics pass),
+* dgrad    ``dX = dY W``   (``gemm_nt`` with the tiny transposed weight),
+* wgrad    ``dW = dY^T X`` (``gemm_tn``, split-K over the N*H*W rows).
+
+Stride-2 1x1 convs (ResNet downsample) subsample the input first. Anything else (non-bf16 inputs,
+odd channel counts, grouped/dilated/padded convs) uses ``F.conv2d``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _ext
+
+
+def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and conv.kernel_size == (1, 1)
+            and conv.padding in ((0, 0), 0) and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and conv.stride in ((1, 1), (2, 2)) and conv.in_channels % 8 == 0 and conv.out_channels % 8 == 0
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels_last -> [N*H*W, C] view."""
+    n, c, h, w = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+class _Conv1x1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, want_stats: bool):
+        C = _ext.require()
+        if stride != 1:
+            x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        w2 = weight.reshape(cout, cin).to(torch.bfloat16).contiguous()
+        y2, stats = C.gemm_nt(_rows(x), w2, want_stats)
+        y = y2.view(n, h, w, cout).permute(0, 3, 1, 2)
+        ctx.save_for_backward(x, w2)
+        ctx.stride = stride
+        ctx.in_hw = None
+        ctx.wdtype = weight.dtype
+        ctx.wshape = weight.shape
+        if stats is not None:
+            ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        C = _ext.require()
+        x, w2 = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        if dy.dtype != torch.bfloat16:
+            dy = dy.to(torch.bfloat16)
+        dy2 = _rows(dy)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx2, _ = C.gemm_nt(dy2, w2.t().contiguous(), False)
+            n, cin, h, w = x.shape
+            dxs = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+            if ctx.stride != 1:
+                H, W = h * ctx.stride, w * ctx.stride
+                dx = torch.zeros((n, cin, H, W), device=dy.device, dtype=dxs.dtype,
+                                 memory_format=torch.channels_last)
+                dx[:, :, ::ctx.stride, ::ctx.stride] = dxs
+            else:
+                dx = dxs
+        if ctx.needs_input_grad[1]:
+            dw = C.gemm_tn(dy2, _rows(x), ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16)
+                           else torch.float32, 1.0).view(ctx.wshape).to(ctx.wdtype)
+        return dx, dw, None, None
+
+
+def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
+    """Returns (y, stats-or-None); stats are [row_blocks, Cout, 2] partial (sum, sumsq)."""
+    if x.shape[2] % conv.stride[0] or x.shape[3] % conv.stride[1]:
+        # odd spatial size with stride 2 (output ceil) — keep F.conv2d semantics exactly
+        return F.conv2d(x, conv.weight.to(x.dtype), None, conv.stride), None
+    return _Conv1x1.apply(x, conv.weight, conv.stride[0], want_stats)

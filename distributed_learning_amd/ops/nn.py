@@ -65,3 +65,38 @@ def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residual: tor
 
         return fused_bn_act(x, bn, relu, residual)
     return _torch_bn_act(x, bn, relu, residual)
+
+
+# 1x1 convolutions on the native MFMA GEMMs (ops/conv.py) — separately switchable so the conv path
+# can be A/B'd against MIOpen while the fused BN stays on.
+_NATIVE_CONV = False
+
+
+def set_native_conv(on: bool) -> None:
+    global _NATIVE_CONV
+    if on:
+        from . import _ext
+
+        _ext.require()
+    _NATIVE_CONV = bool(on)
+
+
+def native_conv() -> bool:
+    return _NATIVE_CONV
+
+
+def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool = True,
+                residual: torch.Tensor | None = None):
+    """``act(BN(conv(x)) [+ residual])``. With the native backend and native convs, a 1x1 conv runs as
+    an MFMA GEMM whose epilogue also produces BN's batch statistics (one pass over the conv output
+    saved)."""
+    if _BACKEND == "native" and _NATIVE_CONV and x.is_cuda:
+        from . import conv as nconv
+        from .bn_act import fused_bn_act, supported as bn_supported
+
+        if nconv.supported(x, conv):
+            y, stats = nconv.conv1x1(x, conv, want_stats=bn.training)
+            if stats is not None and not bn_supported(y, bn, residual):
+                stats = None
+            return fused_bn_act(y, bn, relu, residual, stats)
+    return bn_act(conv(x), bn, relu, residual)

@@ -1,0 +1,52 @@
+"""bf16 MFMA GEMMs vs an fp32 PyTorch reference (gpu)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _C():
+    from distributed_learning_amd.ops import _ext
+
+    return _ext.require()
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 64, 64), (1000, 64, 256), (777, 136, 72), (12544, 512, 2048),
+                                   (4096, 256, 64), (130, 8, 8), (50176, 1024, 256)])
+def test_gemm_nt(cuda, M, N, K):
+    C = _C()
+    torch.manual_seed(0)
+    A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    B = torch.randn(N, K, device=cuda).to(torch.bfloat16)
+    out, stats = C.gemm_nt(A, B, True)
+    ref = A.float() @ B.float().t()
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2 * (K ** 0.5))
+    # fused column statistics of the rounded outputs
+    s = stats.sum(0)
+    o = out.float()
+    torch.testing.assert_close(s[:, 0], o.sum(0), rtol=1e-4, atol=1e-2 * M ** 0.5)
+    torch.testing.assert_close(s[:, 1], (o * o).sum(0), rtol=1e-4, atol=1e-1)
+
+
+def test_gemm_nt_asymmetric_identity(cuda):
+    """A = I with an asymmetric B catches a transposed C/D mapping (cdna_hip_programming.md §3)."""
+    C = _C()
+    n = 128
+    A = torch.eye(n, device=cuda).to(torch.bfloat16)
+    B = (torch.arange(n * n, device=cuda).reshape(n, n) % 251).to(torch.bfloat16)
+    out, _ = C.gemm_nt(A, B, False)
+    torch.testing.assert_close(out.float(), B.float().t())
+
+
+@pytest.mark.parametrize("K,Mo,No", [(802816, 64, 256), (1000, 64, 64), (12544, 512, 2048), (333, 136, 72),
+                                     (50176, 256, 1024)])
+def test_gemm_tn(cuda, K, Mo, No):
+    C = _C()
+    torch.manual_seed(0)
+    A = torch.randn(K, Mo, device=cuda).to(torch.bfloat16)
+    B = torch.randn(K, No, device=cuda).to(torch.bfloat16)
+    out = C.gemm_tn(A, B, torch.float32, 0.5)
+    ref = (A.float().t() @ B.float()) * 0.5
+    torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3 * K ** 0.5)
+    outb = C.gemm_tn(A, B, torch.bfloat16, 1.0)
+    torch.testing.assert_close(outb.float(), ref * 2, rtol=1e-2, atol=2e-3 * K ** 0.5)
