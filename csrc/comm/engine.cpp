@@ -177,6 +177,20 @@ class CommEngine {
     if (table) table->unpack_on(flat, unpack_scale, s);
   }
 
+  // Bucket path for autograd-owned gradients: gather `grads` into `flat` at `offsets` on the comm
+  // stream (by-value list launches, no per-step table upload), then all-reduce `flat` in place.
+  // The caller keeps `grads` alive until the compute stream has joined the comm stream.
+  void bucket_allreduce_list(at::Tensor flat, int algo, bool average, std::vector<at::Tensor> grads,
+                             std::vector<int64_t> offsets) {
+    check(flat);
+    c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
+    join_current();
+    pybind11::gil_scoped_release nogil;
+    hipStream_t s = stream_->stream();
+    pack_tensors_on(grads, offsets, flat, 1.f, s);
+    timed([&] { allreduce_on_stream(flat, algo, average); });
+  }
+
   void broadcast(at::Tensor t, int root) {
     check(t);
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
@@ -490,6 +504,8 @@ void bind_comm(pybind11::module& m) {
       .def("bucket_allreduce", &CommEngine::bucket_allreduce, pybind11::arg("flat"), pybind11::arg("algo"),
            pybind11::arg("average"), pybind11::arg("table").none(true), pybind11::arg("pack_scale") = 1.0,
            pybind11::arg("unpack_scale") = 1.0)
+      .def("bucket_allreduce_list", &CommEngine::bucket_allreduce_list, pybind11::arg("flat"), pybind11::arg("algo"),
+           pybind11::arg("average"), pybind11::arg("grads"), pybind11::arg("offsets"))
       .def("broadcast", &CommEngine::broadcast)
       .def("allgather", &CommEngine::allgather)
       .def("set_timing", &CommEngine::set_timing)

@@ -35,7 +35,25 @@ struct PackEntry {
   int64_t offset;  // element offset inside the flat bucket
 };
 
+// By-value tensor lists (kernel arguments, no device table): one launch covers up to kMaxList
+// tensors; used when tensor addresses change between steps.
+constexpr int kMaxList = 32;
+struct SgdList {
+  int ntensors;
+  int32_t prefix[kMaxList + 1];
+  SgdEntry e[kMaxList];
+};
+struct PackList {
+  int ntensors;
+  int32_t prefix[kMaxList + 1];
+  PackEntry e[kMaxList];
+};
+
 int mt_chunk_elems();
+void launch_sgd_list(const SgdList& list, int nblocks, int grad_dtype, bool use_momentum, const SgdParams& hp,
+                     hipStream_t stream);
+void launch_pack_list(const PackList& list, int nblocks, int src_dtype, int flat_dtype, void* flat, float scale,
+                      hipStream_t stream);
 void launch_sgd(const SgdEntry* entries, const int32_t* prefix, int ntensors, int nblocks, int grad_dtype,
                 bool use_momentum, const SgdParams& hp, hipStream_t stream);
 void launch_pack(const PackEntry* entries, const int32_t* prefix, int ntensors, int nblocks, int src_dtype,
@@ -76,10 +94,12 @@ void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_bloc
 void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int dtype, const float* gamma,
                    const float* beta, float eps, float momentum, float* running_mean, float* running_var, float* ws,
                    float* part, bool relu, bool training, hipStream_t stream, const float* ext_part = nullptr,
-                   int ext_nrb = 0);
-void launch_bn_bwd(const void* dy, const void* y, const void* x, void* dx, void* dres, int64_t M, int C, int dtype,
-                   const float* gamma, float* ws, float* part, float* dgamma, float* dbeta, bool relu,
-                   hipStream_t stream);
+                   int ext_nrb = 0, uint8_t* relu_mask = nullptr);
+// mask_mode: 0 no ReLU, 1 recompute from x (ReLU right after BN), 2 1-bit mask written by the
+// forward (ReLU after the residual add), 3 from the saved output y.
+void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const void* x, void* dx, void* dres,
+                   int64_t M, int C, int dtype, const float* gamma, float* ws, float* part, float* dgamma,
+                   float* dbeta, int mask_mode, hipStream_t stream);
 
 // ---- bf16 MFMA GEMMs (gemm.hip) ---------------------------------------------------------------
 // C[M,N] = A[M,K] B[N,K]^T; optional per-column (sum, sumsq) partials stats[ceil(M/128)][N][2].

@@ -9,7 +9,18 @@ namespace dla {
 int dtype_code(const at::Tensor& t);
 hipStream_t current_stream(const at::Tensor& t);
 void check_dev(const at::Tensor& t, const char* what);
+// Same element order in memory: equal shapes and equal strides on every dimension of size > 1
+// (the strides of size-1 dimensions are arbitrary, e.g. 1x1 conv weights in channels_last).
+inline bool same_layout(const at::Tensor& a, const at::Tensor& b) {
+  if (a.sizes() != b.sizes()) return false;
+  for (int64_t d = 0; d < a.dim(); ++d)
+    if (a.size(d) > 1 && a.stride(d) != b.stride(d)) return false;
+  return true;
+}
 at::Tensor upload(const void* data, size_t bytes, const at::Device& dev);
+// Gathers `ts` into `flat` at element offsets `offs` on stream `st` (by-value list launches).
+void pack_tensors_on(const std::vector<at::Tensor>& ts, const std::vector<int64_t>& offs, const at::Tensor& flat,
+                     float scale, hipStream_t st);
 
 // PackTable: gathers a bucket's gradients into a flat buffer (tensor fusion) and scatters the
 // reduced buffer back, each as ONE multi-tensor launch (csrc/kernels/multi_tensor.hip).

@@ -9,11 +9,12 @@
 //                         removes the E[x^2]-E[x]^2 cancellation), per-block partials, no atomics;
 //           finalize    — mean / invstd / scale / shift per channel + running-stat update;
 //           apply pass  — y = relu(x*scale + shift [+ res]) in one read-modify-write.
-// Backward: reduce pass — Σdy', Σdy'(x-mean) with dy' = dy * (y > 0) (ReLU mask from the saved
-//                         output, which the next conv keeps alive anyway — no mask tensor);
+// Backward: reduce pass — Σdy', Σdy'(x-mean) with dy' = dy * relu'(.): the ReLU branch is
+//                         recomputed from x (ReLU right after BN) or read from a 1-bit mask the
+//                         forward wrote (ReLU after the residual add) — never from the saved y;
 //           finalize    — dgamma, dbeta and the two per-channel dx coefficients;
 //           apply pass  — dx = k1*(dy' - m1 - (x-mean)*k2) [and d_residual = dy'].
-// Traffic per element (bf16): fwd 2R+1W (+1R res), bwd 5R+1W (+1W dres) vs ~7 and ~8 passes for
+// Traffic per element (bf16): fwd 2R+1W (+1R res), bwd 4R+1W (+1W dres, +1/16 R mask) vs ~7 and ~8 passes for
 // the unfused chain. Partials are reduced in a fixed order -> bitwise reproducible.
 #include "dla_common.h"
 #include "dla_kernels.h"
@@ -191,7 +192,8 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __re
 template <typename T, bool kRes, bool kRelu>
 __global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                               T* __restrict__ y, const float* __restrict__ ws,
-                                                              int64_t M, int C, int nrb, int tpr) {
+                                                              int64_t M, int C, int nrb, int tpr,
+                                                              uint8_t* __restrict__ mask) {
   // Same tiling as the reduction passes: a thread owns 8 fixed channels for all its rows, so the
   // per-channel coefficients live in registers (no per-element index math or table reads).
   const int rpi = kBNThreads / tpr, ct = tpr * 8;
@@ -211,22 +213,57 @@ __global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restric
     Vec8<T>::load(x + off, a);
     float rv[8];
     if (kRes) Vec8<T>::load(res + off, rv);
+    uint32_t bits = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float o = fmaf(a[j], sc[j], sh[j]);
       if (kRes) o += rv[j];
-      if (kRelu) o = fmaxf(o, 0.f);
+      if (kRelu) {
+        bits |= (o > 0.f ? 1u : 0u) << j;
+        o = fmaxf(o, 0.f);
+      }
       a[j] = o;
     }
     Vec8<T>::store(y + off, a);
+    // ReLU-after-residual: the backward cannot recompute the branch from x alone, so record it as
+    // one bit per element (1/16 of the bf16 output's bytes) instead of re-reading y.
+    if (kRes && kRelu && mask) mask[off >> 3] = (uint8_t)bits;
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // backward: reduce  Σdy', Σdy'(x-mean)
 // ---------------------------------------------------------------------------------------------
-template <typename T, bool kRelu>
+// ReLU branch in backward, by mask source:
+//   kMaskNone   no ReLU;
+//   kMaskRecomp ReLU directly after BN: recompute x*scale+shift > 0 from x, which the backward reads
+//               anyway (bit-identical to the forward's decision: same fmaf on the same operands);
+//   kMaskBits   ReLU after the residual add: the 1-bit mask the forward wrote;
+//   kMaskY      from the saved output (generic fallback).
+enum : int { kMaskNone = 0, kMaskRecomp = 1, kMaskBits = 2, kMaskY = 3 };
+
+template <typename T, int kMask>
+__device__ __forceinline__ void apply_relu_mask(float (&g)[8], const float (&xv)[8], const float (&sc)[8],
+                                                const float (&sh)[8], const T* __restrict__ y,
+                                                const uint8_t* __restrict__ mask, int64_t off) {
+  if constexpr (kMask == kMaskRecomp) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
+  } else if constexpr (kMask == kMaskBits) {
+    const uint32_t bits = mask[off >> 3];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = ((bits >> j) & 1u) ? g[j] : 0.f;
+  } else if constexpr (kMask == kMaskY) {
+    float yv[8];
+    Vec8<T>::load(y + off, yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+  }
+}
+
+template <typename T, int kMask>
 __global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                                   const uint8_t* __restrict__ mask,
                                                                    const T* __restrict__ x,
                                                                    const float* __restrict__ ws, int64_t M, int C,
                                                                    int nrb, int tpr, float* __restrict__ part) {
@@ -237,22 +274,20 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(const T* __re
   const int rg = threadIdx.x / tpr;
   int64_t r0, r1;
   block_rows(M, nrb, r0, r1);
-  float mean[8], s[8], q[8];
+  float mean[8], sc[8], sh[8], s[8], q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     mean[j] = ws[c0 + j];
+    sc[j] = ws[2 * C + c0 + j];
+    sh[j] = ws[3 * C + c0 + j];
     s[j] = q[j] = 0.f;
   }
   for (int64_t r = r0 + rg; r < r1; r += rpi) {
+    const int64_t off = r * C + c0;
     float g[8], xv[8];
-    Vec8<T>::load(dy + r * C + c0, g);
-    Vec8<T>::load(x + r * C + c0, xv);
-    if (kRelu) {
-      float yv[8];
-      Vec8<T>::load(y + r * C + c0, yv);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
-    }
+    Vec8<T>::load(dy + off, g);
+    Vec8<T>::load(x + off, xv);
+    apply_relu_mask<T, kMask>(g, xv, sc, sh, y, mask, off);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       s[j] += g[j];
@@ -281,8 +316,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   ws[6 * C + c] = invstd * invstd * Q * inv_m;
 }
 
-template <typename T, bool kRelu, bool kDres>
+template <typename T, int kMask, bool kDres>
 __global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                                  const uint8_t* __restrict__ mask,
                                                                   const T* __restrict__ x,
                                                                   const float* __restrict__ ws, T* __restrict__ dx,
                                                                   T* __restrict__ dres, int64_t M, int C, int nrb,
@@ -292,10 +328,12 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(const T* __res
   const int rg = threadIdx.x / tpr;
   int64_t r0, r1;
   block_rows(M, nrb, r0, r1);
-  float mean[8], k1[8], m1[8], k2[8];
+  float mean[8], sc[8], sh[8], k1[8], m1[8], k2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     mean[j] = ws[c0 + j];
+    sc[j] = ws[2 * C + c0 + j];
+    sh[j] = ws[3 * C + c0 + j];
     k1[j] = ws[4 * C + c0 + j];
     m1[j] = ws[5 * C + c0 + j];
     k2[j] = ws[6 * C + c0 + j];
@@ -305,12 +343,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(const T* __res
     float g[8], xv[8];
     Vec8<T>::load(dy + off, g);
     Vec8<T>::load(x + off, xv);
-    if (kRelu) {
-      float yv[8];
-      Vec8<T>::load(y + off, yv);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
-    }
+    apply_relu_mask<T, kMask>(g, xv, sc, sh, y, mask, off);
     if (kDres) Vec8<T>::store(dres + off, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = k1[j] * (g[j] - m1[j] - (xv[j] - mean[j]) * k2[j]);
@@ -340,7 +373,7 @@ void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_bloc
 void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int dtype, const float* gamma,
                    const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                    float* ws, float* part, bool relu, bool training, hipStream_t stream, const float* ext_part,
-                   int ext_nrb) {
+                   int ext_nrb, uint8_t* mask) {
   int tpr, nrb, nct;
   bn_geometry(M, C, &tpr, &nrb, &nct);
   if (training && ext_part) {
@@ -362,7 +395,7 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
 #define DLA_BN_APPLY(T, R, A)                                                                                      \
   hipLaunchKernelGGL((bn_apply_kernel<T, R, A>), dim3(anct, anrb), dim3(kBNThreads), 0, stream, (const T*)x,        \
-                     (const T*)res, (T*)y, (const float*)ws, M, C, anrb, atpr)
+                     (const T*)res, (T*)y, (const float*)ws, M, C, anrb, atpr, mask)
   if (dtype == kBF16) {
     if (res) { if (relu) DLA_BN_APPLY(bf16_t, true, true); else DLA_BN_APPLY(bf16_t, true, false); }
     else { if (relu) DLA_BN_APPLY(bf16_t, false, true); else DLA_BN_APPLY(bf16_t, false, false); }
@@ -373,32 +406,45 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
 #undef DLA_BN_APPLY
 }
 
-void launch_bn_bwd(const void* dy, const void* y, const void* x, void* dx, void* dres, int64_t M, int C, int dtype,
-                   const float* gamma, float* ws, float* part, float* dgamma, float* dbeta, bool relu,
-                   hipStream_t stream) {
+void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const void* x, void* dx, void* dres,
+                   int64_t M, int C, int dtype, const float* gamma, float* ws, float* part, float* dgamma,
+                   float* dbeta, int mask_mode, hipStream_t stream) {
   int tpr, nrb, nct;
   bn_geometry(M, C, &tpr, &nrb, &nct);
   const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
-#define DLA_BN_RED(T, R)                                                                                          \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, R>), dim3(nct, nrb), dim3(kBNThreads), lds, stream, (const T*)dy,     \
-                     (const T*)y, (const T*)x, (const float*)ws, M, C, nrb, tpr, part)
-  if (dtype == kBF16) { if (relu) DLA_BN_RED(bf16_t, true); else DLA_BN_RED(bf16_t, false); }
-  else { if (relu) DLA_BN_RED(float, true); else DLA_BN_RED(float, false); }
+#define DLA_BN_RED(T, K)                                                                                          \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, K>), dim3(nct, nrb), dim3(kBNThreads), lds, stream, (const T*)dy,     \
+                     (const T*)y, mask, (const T*)x, (const float*)ws, M, C, nrb, tpr, part)
+#define DLA_BN_RED_ALL(T)                                 \
+  switch (mask_mode) {                                    \
+    case kMaskRecomp: DLA_BN_RED(T, kMaskRecomp); break;  \
+    case kMaskBits: DLA_BN_RED(T, kMaskBits); break;      \
+    case kMaskY: DLA_BN_RED(T, kMaskY); break;            \
+    default: DLA_BN_RED(T, kMaskNone); break;             \
+  }
+  if (dtype == kBF16) { DLA_BN_RED_ALL(bf16_t) } else { DLA_BN_RED_ALL(float) }
+#undef DLA_BN_RED_ALL
 #undef DLA_BN_RED
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(256), 0, stream, part, nrb, M, C, gamma, ws,
-                     dgamma, dbeta);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(256), 0, stream, part, nrb, M, C,
+                     gamma, ws, dgamma, dbeta);
   int atpr, anrb, anct;
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
-#define DLA_BN_BAPPLY(T, R, D)                                                                                     \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, R, D>), dim3(anct, anrb), dim3(kBNThreads), 0, stream, (const T*)dy,   \
-                     (const T*)y, (const T*)x, (const float*)ws, (T*)dx, (T*)dres, M, C, anrb, atpr)
-  if (dtype == kBF16) {
-    if (dres) { if (relu) DLA_BN_BAPPLY(bf16_t, true, true); else DLA_BN_BAPPLY(bf16_t, false, true); }
-    else { if (relu) DLA_BN_BAPPLY(bf16_t, true, false); else DLA_BN_BAPPLY(bf16_t, false, false); }
-  } else {
-    if (dres) { if (relu) DLA_BN_BAPPLY(float, true, true); else DLA_BN_BAPPLY(float, false, true); }
-    else { if (relu) DLA_BN_BAPPLY(float, true, false); else DLA_BN_BAPPLY(float, false, false); }
+#define DLA_BN_BAPPLY(T, K, D)                                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, K, D>), dim3(anct, anrb), dim3(kBNThreads), 0, stream, (const T*)dy,    \
+                     (const T*)y, mask, (const T*)x, (const float*)ws, (T*)dx, (T*)dres, M, C, anrb, atpr)
+#define DLA_BN_BAPPLY_ALL(T, D)                                 \
+  switch (mask_mode) {                                          \
+    case kMaskRecomp: DLA_BN_BAPPLY(T, kMaskRecomp, D); break;  \
+    case kMaskBits: DLA_BN_BAPPLY(T, kMaskBits, D); break;      \
+    case kMaskY: DLA_BN_BAPPLY(T, kMaskY, D); break;            \
+    default: DLA_BN_BAPPLY(T, kMaskNone, D); break;             \
   }
+  if (dtype == kBF16) {
+    if (dres) { DLA_BN_BAPPLY_ALL(bf16_t, true) } else { DLA_BN_BAPPLY_ALL(bf16_t, false) }
+  } else {
+    if (dres) { DLA_BN_BAPPLY_ALL(float, true) } else { DLA_BN_BAPPLY_ALL(float, false) }
+  }
+#undef DLA_BN_BAPPLY_ALL
 #undef DLA_BN_BAPPLY
 }
 

@@ -126,6 +126,12 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(const bf16_t* 
   // ---- epilogue: bf16 tile -> LDS -> coalesced 16 B stores (+ column statistics) ----
   constexpr int LDS_C = BN + 8;
   bf16_t* Cs = reinterpret_cast<bf16_t*>(smem_raw);
+  // Column statistics straight from the accumulator registers: a lane owns one column of each
+  // 16x16 tile and 4 of its rows, so it sums TM*4 rows per column in registers, then the 4 lane
+  // groups sharing a column combine with two xor-shuffles, and the 2 M-waves through LDS.
+  float cs[TN], cq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) cs[j] = cq[j] = 0.f;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -134,7 +140,13 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(const bf16_t* 
       for (int r = 0; r < 4; ++r) {
         const int m = wr * WM + i * 16 + (lane >> 4) * 4 + r;  // C/D map: row = 4*(lane>>4)+reg
         const int n = wc * WN + j * 16 + fr;                    //          col = lane & 15
-        Cs[m * LDS_C + n] = f32_to_bf16(acc[i][j][r]);
+        const bf16_t h = f32_to_bf16(acc[i][j][r]);
+        Cs[m * LDS_C + n] = h;
+        if constexpr (kStats) {
+          const float v = (row0 + m < M) ? bf16_to_f32(h) : 0.f;  // statistics of the stored values
+          cs[j] += v;
+          cq[j] = fmaf(v, v, cq[j]);
+        }
       }
   __syncthreads();
   constexpr int CPR = BN / 8;
@@ -145,32 +157,23 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(const bf16_t* 
     if (gm < M && gn < N) *reinterpret_cast<ushort8_t*>(C + gm * ldc + gn) = *reinterpret_cast<ushort8_t*>(Cs + r * LDS_C + cc);
   }
   if constexpr (kStats) {
-    // per-column sum / sum of squares of the rounded outputs over this tile's valid rows
-    constexpr int RG = kGemmThreads / BN;  // row groups
-    float* red = reinterpret_cast<float*>(smem_raw + BM * LDS_C * sizeof(bf16_t));
-    const int cl = tid % BN, g = tid / BN;
-    float s = 0.f, q = 0.f;
-    if (g < RG) {
-      for (int r = g; r < BM; r += RG) {
-        if (row0 + r < M) {
-          const float v = bf16_to_f32(Cs[r * LDS_C + cl]);
-          s += v;
-          q = fmaf(v, v, q);
-        }
+    float* red = reinterpret_cast<float*>(smem_raw + BM * LDS_C * sizeof(bf16_t));  // [2 wr][BN][2]
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      cs[j] += __shfl_xor(cs[j], 16, kWave);
+      cq[j] += __shfl_xor(cq[j], 16, kWave);
+      cs[j] += __shfl_xor(cs[j], 32, kWave);
+      cq[j] += __shfl_xor(cq[j], 32, kWave);
+      if (lane < 16) {
+        const int n = wc * WN + j * 16 + fr;
+        red[(wr * BN + n) * 2 + 0] = cs[j];
+        red[(wr * BN + n) * 2 + 1] = cq[j];
       }
-      red[(g * BN + cl) * 2 + 0] = s;
-      red[(g * BN + cl) * 2 + 1] = q;
     }
     __syncthreads();
     if (tid < BN && col0 + tid < N) {
-      float S = 0.f, Q = 0.f;
-#pragma unroll
-      for (int gg = 0; gg < RG; ++gg) {
-        S += red[(gg * BN + tid) * 2 + 0];
-        Q += red[(gg * BN + tid) * 2 + 1];
-      }
-      stats[((int64_t)bm * N + col0 + tid) * 2 + 0] = S;
-      stats[((int64_t)bm * N + col0 + tid) * 2 + 1] = Q;
+      stats[((int64_t)bm * N + col0 + tid) * 2 + 0] = red[tid * 2 + 0] + red[(BN + tid) * 2 + 0];
+      stats[((int64_t)bm * N + col0 + tid) * 2 + 1] = red[tid * 2 + 1] + red[(BN + tid) * 2 + 1];
     }
   }
 }
@@ -299,16 +302,39 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_tn_kernel(const bf16_t* 
       }
 }
 
+// Sums the split-K fp32 slabs: each thread owns 4 consecutive outputs (one 16-byte load per slab)
+// and keeps 4 slabs in flight, so the loop is bandwidth- rather than latency-bound.
 template <typename T>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ P, int splits, int64_t n,
                                                             T* __restrict__ out, float scale, int accumulate) {
+  const int64_t nv = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += P[(int64_t)k * n + i];
-    s *= scale;
-    if (accumulate) s += Cvt<T>::to_f32(out[i]);
-    out[i] = Cvt<T>::from_f32(s);
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    float4_t a0{0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    int k = 0;
+    for (; k + 3 < splits; k += 4) {
+      a0 += reinterpret_cast<const float4_t*>(P + (int64_t)(k + 0) * n)[v];
+      a1 += reinterpret_cast<const float4_t*>(P + (int64_t)(k + 1) * n)[v];
+      a2 += reinterpret_cast<const float4_t*>(P + (int64_t)(k + 2) * n)[v];
+      a3 += reinterpret_cast<const float4_t*>(P + (int64_t)(k + 3) * n)[v];
+    }
+    for (; k < splits; ++k) a0 += reinterpret_cast<const float4_t*>(P + (int64_t)k * n)[v];
+    const float4_t s = ((a0 + a1) + (a2 + a3)) * scale;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float o = s[j];
+      if (accumulate) o += Cvt<T>::to_f32(out[v * 4 + j]);
+      out[v * 4 + j] = Cvt<T>::from_f32(o);
+    }
+  }
+  if (blockIdx.x == 0) {  // tail (n % 4)
+    for (int64_t i = nv * 4 + threadIdx.x; i < n; i += blockDim.x) {
+      float o = 0.f;
+      for (int k = 0; k < splits; ++k) o += P[(int64_t)k * n + i];
+      o *= scale;
+      if (accumulate) o += Cvt<T>::to_f32(out[i]);
+      out[i] = Cvt<T>::from_f32(o);
+    }
   }
 }
 
@@ -345,10 +371,12 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
 }
 
 int gemm_tn_splits(int Mo, int No, int K) {
+  // ~512 workgroups in flight (2 per CU) and >= 16 K-steps per split: enough parallelism for the
+  // long M reduction while keeping the fp32 slab traffic (splits * Mo * No * 4 B) small.
   const int tiles = ((Mo + 127) / 128) * ((No + 127) / 128);
-  int splits = std::max(1, 1024 / std::max(1, tiles));
-  const int max_splits = std::max(1, (K + 4 * kBK - 1) / (4 * kBK));  // >= 4 K-steps per block
-  return std::min(splits, max_splits);
+  int splits = std::max(1, 512 / std::max(1, tiles));
+  const int max_splits = std::max(1, K / (16 * kBK));
+  return std::max(1, std::min(splits, max_splits));
 }
 
 void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, float* partial, int splits, int Mo, int No,
@@ -360,7 +388,7 @@ void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, floa
   hipLaunchKernelGGL((gemm_tn_kernel<128, 128>), dim3(tiles, splits), dim3(kGemmThreads), lds, stream,
                      (const bf16_t*)A, lda, (const bf16_t*)B, ldb, partial, Mo, No, K, kps);
   const int64_t n = (int64_t)Mo * No;
-  const int grid = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n / 4 + 255) / 256, 2048));
   if (out_dtype == kF32)
     hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(grid), dim3(256), 0, stream, partial, splits, n, (float*)out,
                        scale, (int)accumulate);

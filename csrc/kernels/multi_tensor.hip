@@ -38,12 +38,26 @@ __device__ __forceinline__ int find_tensor(const int32_t* __restrict__ prefix, i
 // p -= lr*d. Optionally writes a bf16 shadow copy of the updated parameter.
 // --------------------------------------------------------------------------------------------
 template <typename G, bool kMomentum>
+__device__ __forceinline__ void sgd_body(const SgdEntry& e, int64_t chunk0, const SgdParams& hp);
+
+template <typename G, bool kMomentum>
 __global__ __launch_bounds__(kMTBlock) void sgd_kernel(const SgdEntry* __restrict__ entries,
                                                        const int32_t* __restrict__ prefix, int ntensors,
                                                        SgdParams hp) {
   const int t = find_tensor(prefix, ntensors, blockIdx.x);
-  const SgdEntry e = entries[t];
-  const int64_t chunk0 = (int64_t)(blockIdx.x - prefix[t]) * kMTChunk;
+  sgd_body<G, kMomentum>(entries[t], (int64_t)(blockIdx.x - prefix[t]) * kMTChunk, hp);
+}
+
+// Same update with the tensor list passed BY VALUE in the kernel arguments (no device table): used
+// when gradient pointers change every step (autograd-owned gradients, set_to_none zero_grad).
+template <typename G, bool kMomentum>
+__global__ __launch_bounds__(kMTBlock) void sgd_list_kernel(SgdList list, SgdParams hp) {
+  const int t = find_tensor(list.prefix, list.ntensors, blockIdx.x);
+  sgd_body<G, kMomentum>(list.e[t], (int64_t)(blockIdx.x - list.prefix[t]) * kMTChunk, hp);
+}
+
+template <typename G, bool kMomentum>
+__device__ __forceinline__ void sgd_body(const SgdEntry& e, int64_t chunk0, const SgdParams& hp) {
   const int64_t n = e.numel;
   const int64_t end = min(n, chunk0 + (int64_t)kMTChunk);
   float* __restrict__ p = e.param;
@@ -158,6 +172,16 @@ __global__ __launch_bounds__(kMTBlock) void pack_kernel(const PackEntry* __restr
 }
 
 template <typename S, typename D>
+__global__ __launch_bounds__(kMTBlock) void pack_list_kernel(PackList list, void* __restrict__ flat, float scale) {
+  const int t = find_tensor(list.prefix, list.ntensors, blockIdx.x);
+  const PackEntry& e = list.e[t];
+  const int64_t c0 = (int64_t)(blockIdx.x - list.prefix[t]) * kMTChunk;
+  const int64_t end = min(e.numel, c0 + (int64_t)kMTChunk);
+  copy_scale_range<S, D>(reinterpret_cast<const S*>(e.tensor), reinterpret_cast<D*>(flat) + e.offset, c0, end, scale,
+                         end - c0 == kMTChunk);
+}
+
+template <typename S, typename D>
 __global__ __launch_bounds__(kMTBlock) void unpack_kernel(const PackEntry* __restrict__ entries,
                                                           const int32_t* __restrict__ prefix, int ntensors,
                                                           const void* __restrict__ flat, float scale) {
@@ -187,6 +211,33 @@ void launch_sgd(const SgdEntry* entries, const int32_t* prefix, int ntensors, in
 }
 
 int mt_chunk_elems() { return kMTChunk; }
+
+void launch_sgd_list(const SgdList& list, int nblocks, int grad_dtype, bool use_momentum, const SgdParams& hp,
+                     hipStream_t stream) {
+  if (nblocks <= 0 || list.ntensors <= 0) return;
+  dim3 grid(nblocks), block(kMTBlock);
+  if (grad_dtype == kF32) {
+    if (use_momentum) hipLaunchKernelGGL((sgd_list_kernel<float, true>), grid, block, 0, stream, list, hp);
+    else hipLaunchKernelGGL((sgd_list_kernel<float, false>), grid, block, 0, stream, list, hp);
+  } else {
+    if (use_momentum) hipLaunchKernelGGL((sgd_list_kernel<bf16_t, true>), grid, block, 0, stream, list, hp);
+    else hipLaunchKernelGGL((sgd_list_kernel<bf16_t, false>), grid, block, 0, stream, list, hp);
+  }
+}
+
+void launch_pack_list(const PackList& list, int nblocks, int src_dtype, int flat_dtype, void* flat, float scale,
+                      hipStream_t stream) {
+  if (nblocks <= 0 || list.ntensors <= 0) return;
+  dim3 grid(nblocks), block(kMTBlock);
+  if (src_dtype == kF32 && flat_dtype == kF32)
+    hipLaunchKernelGGL((pack_list_kernel<float, float>), grid, block, 0, stream, list, flat, scale);
+  else if (src_dtype == kF32 && flat_dtype == kBF16)
+    hipLaunchKernelGGL((pack_list_kernel<float, bf16_t>), grid, block, 0, stream, list, flat, scale);
+  else if (src_dtype == kBF16 && flat_dtype == kBF16)
+    hipLaunchKernelGGL((pack_list_kernel<bf16_t, bf16_t>), grid, block, 0, stream, list, flat, scale);
+  else
+    hipLaunchKernelGGL((pack_list_kernel<bf16_t, float>), grid, block, 0, stream, list, flat, scale);
+}
 
 void launch_pack(const PackEntry* entries, const int32_t* prefix, int ntensors, int nblocks, int src_dtype,
                  int flat_dtype, void* flat, float scale, hipStream_t stream) {

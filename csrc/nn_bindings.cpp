@@ -26,7 +26,8 @@ static int64_t partial_floats(int64_t M, int C) {
   return (int64_t)nrb * C * 2;
 }
 
-// Returns (y, ws). ws (7C fp32) carries mean/invstd for backward.
+// Returns (y, ws, mask). ws (7C fp32) carries mean/invstd/scale/shift for backward; mask (uint8,
+// one bit per element) is only produced for ReLU after a residual add in training mode.
 std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> residual, c10::optional<at::Tensor> weight,
                                    c10::optional<at::Tensor> bias, c10::optional<at::Tensor> running_mean,
                                    c10::optional<at::Tensor> running_var, bool training, double momentum, double eps,
@@ -70,22 +71,40 @@ std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> resid
   }
   at::Tensor part = at::empty({(training && !ext) ? partial_floats(M, C) : 1}, f32);
   at::Tensor y = at::empty_like(x);
+  at::Tensor mask;
+  if (training && relu && res) mask = at::empty({(M * C + 7) / 8}, x.options().dtype(at::kByte));
   launch_bn_fwd(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), M, C, dtype_code(x), g, b, (float)eps,
                 (float)momentum, training ? rm : nullptr, training ? rv : nullptr, ws.data_ptr<float>(),
                 part.data_ptr<float>(), relu, training, current_stream(x), ext ? stats->data_ptr<float>() : nullptr,
-                ext ? (int)stats->size(0) : 0);
-  return {y, ws};
+                ext ? (int)stats->size(0) : 0, mask.defined() ? mask.data_ptr<uint8_t>() : nullptr);
+  return {y, ws, mask};
 }
 
-// Returns (dx, dres-or-undefined, dgamma, dbeta).
-std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Tensor ws,
-                                   c10::optional<at::Tensor> weight, bool relu, bool need_dres) {
+// Returns (dx, dres-or-undefined, dgamma, dbeta). mask_mode (see launch_bn_bwd): 0 no ReLU,
+// 1 recompute the ReLU branch from x, 2 use `mask` from bn_act_fwd, 3 use the saved output `y`.
+std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, c10::optional<at::Tensor> mask,
+                                   at::Tensor x, at::Tensor ws, c10::optional<at::Tensor> weight, int64_t mask_mode,
+                                   bool need_dres) {
   dy = dy.dim() == 4 ? dy.contiguous(at::MemoryFormat::ChannelsLast) : dy.contiguous();
   check_act(dy, "dy");
   check_act(x, "x");
-  if (relu) check_act(y, "y");
   const int C = (int)x.size(1);
   const int64_t M = rows_of(x);
+  TORCH_CHECK(mask_mode >= 0 && mask_mode <= 3, "bad mask_mode");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() == 7 * (int64_t)C, "ws must be the 7C fp32 workspace");
+  const void* yp = nullptr;
+  const uint8_t* mp = nullptr;
+  if (mask_mode == 3) {
+    TORCH_CHECK(y.has_value() && y->defined(), "mask_mode 3 needs y");
+    check_act(*y, "y");
+    TORCH_CHECK(y->sizes() == x.sizes() && y->scalar_type() == x.scalar_type(), "y mismatch");
+    yp = y->data_ptr();
+  } else if (mask_mode == 2) {
+    TORCH_CHECK(mask.has_value() && mask->defined() && mask->scalar_type() == at::kByte &&
+                    mask->numel() * 8 >= M * C && mask->is_cuda(),
+                "mask_mode 2 needs the forward's 1-bit mask");
+    mp = mask->data_ptr<uint8_t>();
+  }
   TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "dy dtype must match x");
   auto f32 = x.options().dtype(at::kFloat);
   at::Tensor part = at::empty({partial_floats(M, C)}, f32);
@@ -93,9 +112,9 @@ std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at
   at::Tensor dres = need_dres ? at::empty_like(x) : at::Tensor();
   at::Tensor dg = at::empty({C}, f32), db = at::empty({C}, f32);
   const float* g = (weight.has_value() && weight->defined()) ? weight->data_ptr<float>() : nullptr;
-  launch_bn_bwd(dy.data_ptr(), relu ? y.data_ptr() : nullptr, x.data_ptr(), dx.data_ptr(),
-                need_dres ? dres.data_ptr() : nullptr, M, C, dtype_code(x), g, ws.data_ptr<float>(),
-                part.data_ptr<float>(), dg.data_ptr<float>(), db.data_ptr<float>(), relu, current_stream(x));
+  launch_bn_bwd(dy.data_ptr(), yp, mp, x.data_ptr(), dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr, M, C,
+                dtype_code(x), g, ws.data_ptr<float>(), part.data_ptr<float>(), dg.data_ptr<float>(),
+                db.data_ptr<float>(), (int)mask_mode, current_stream(x));
   return {dx, dres, dg, db};
 }
 
@@ -148,7 +167,9 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("residual"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"),
         pybind11::arg("running_var"), pybind11::arg("training"), pybind11::arg("momentum"), pybind11::arg("eps"),
         pybind11::arg("relu"), pybind11::arg("stats") = pybind11::none());
-  m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC");
+  m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC", pybind11::arg("dy"),
+        pybind11::arg("y"), pybind11::arg("mask"), pybind11::arg("x"), pybind11::arg("ws"), pybind11::arg("weight"),
+        pybind11::arg("mask_mode"), pybind11::arg("need_dres"));
 }
 
 }  // namespace dla

@@ -60,7 +60,7 @@ class SgdTable {
       check_dev(grads_[i], "grad");
       TORCH_CHECK(p.scalar_type() == at::kFloat, "SgdTable: parameters must be fp32 (master weights)");
       TORCH_CHECK(grads_[i].numel() == p.numel(), "SgdTable: grad numel mismatch");
-      TORCH_CHECK(grads_[i].strides() == p.strides(), "SgdTable: grad layout (strides) must match the parameter");
+      TORCH_CHECK(same_layout(grads_[i], p), "SgdTable: grad layout (strides) must match the parameter");
       TORCH_CHECK(dtype_code(grads_[i]) == grad_dtype_, "SgdTable: all grads must share a dtype");
       SgdEntry e{};
       e.param = p.data_ptr<float>();
@@ -69,7 +69,7 @@ class SgdTable {
       if (!moms_.empty()) {
         check_dev(moms_[i], "momentum");
         TORCH_CHECK(moms_[i].numel() == p.numel() && moms_[i].scalar_type() == at::kFloat &&
-                        moms_[i].strides() == p.strides(),
+                        same_layout(moms_[i], p),
                     "SgdTable: momentum buffer must be fp32 with the parameter's layout");
       }
       e.param_bf16 = nullptr;
@@ -105,6 +105,93 @@ class SgdTable {
   at::Tensor entries_, prefix_;
   int ntensors_ = 0, nblocks_ = 0, grad_dtype_ = kF32;
 };
+
+// ------------------------------------------------------------------------------------------
+// By-value list launches (tensor addresses may change every step).
+// ------------------------------------------------------------------------------------------
+void sgd_step_list(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> moms,
+                   std::vector<at::Tensor> shadows, double lr, double momentum, double dampening, double weight_decay,
+                   bool nesterov, double grad_scale, bool first_step) {
+  TORCH_CHECK(params.size() == grads.size(), "sgd_step_list: params/grads size mismatch");
+  TORCH_CHECK(moms.empty() || moms.size() == params.size(), "sgd_step_list: momentum list size mismatch");
+  TORCH_CHECK(shadows.empty() || shadows.size() == params.size(), "sgd_step_list: shadow list size mismatch");
+  if (params.empty()) return;
+  const int gdt = dtype_code(grads[0]);
+  const bool use_m = !moms.empty();
+  const SgdParams hp{(float)lr, (float)momentum, (float)dampening, (float)weight_decay, (float)grad_scale,
+                     nesterov ? 1 : 0, first_step ? 1 : 0};
+  const int chunk = mt_chunk_elems();
+  hipStream_t st = current_stream(params[0]);
+  SgdList list{};
+  int blocks = 0;
+  auto flush = [&]() {
+    if (list.ntensors == 0) return;
+    list.prefix[list.ntensors] = blocks;
+    launch_sgd_list(list, blocks, gdt, use_m, hp, st);
+    list = SgdList{};
+    blocks = 0;
+  };
+  for (size_t i = 0; i < params.size(); ++i) {
+    const at::Tensor& p = params[i];
+    check_dev(p, "param");
+    check_dev(grads[i], "grad");
+    TORCH_CHECK(p.scalar_type() == at::kFloat, "sgd_step_list: parameters/masters must be fp32");
+    TORCH_CHECK(dtype_code(grads[i]) == gdt && same_layout(grads[i], p),
+                "sgd_step_list: grad ", i, " must match its parameter's layout and the list's grad dtype");
+    if (p.numel() == 0) continue;
+    SgdEntry e{};
+    e.param = p.data_ptr<float>();
+    e.grad = grads[i].data_ptr();
+    if (use_m) {
+      TORCH_CHECK(moms[i].scalar_type() == at::kFloat && same_layout(moms[i], p), "bad momentum buffer");
+      e.momentum = moms[i].data_ptr<float>();
+    }
+    if (!shadows.empty()) {
+      TORCH_CHECK(shadows[i].scalar_type() == at::kBFloat16 && same_layout(shadows[i], p), "bad shadow");
+      e.param_bf16 = reinterpret_cast<uint16_t*>(shadows[i].data_ptr());
+    }
+    e.numel = p.numel();
+    list.prefix[list.ntensors] = blocks;
+    list.e[list.ntensors++] = e;
+    blocks += (int)((e.numel + chunk - 1) / chunk);
+    if (list.ntensors == kMaxList) flush();
+  }
+  flush();
+}
+
+void pack_tensors_on(const std::vector<at::Tensor>& ts, const std::vector<int64_t>& offs, const at::Tensor& flat,
+                     float scale, hipStream_t st) {
+  TORCH_CHECK(ts.size() == offs.size(), "pack: tensors/offsets size mismatch");
+  const int fdt = dtype_code(flat);
+  const int chunk = mt_chunk_elems();
+  PackList list{};
+  int blocks = 0, sdt = -1;
+  auto flush = [&]() {
+    if (list.ntensors == 0) return;
+    list.prefix[list.ntensors] = blocks;
+    launch_pack_list(list, blocks, sdt, fdt, flat.data_ptr(), scale, st);
+    list = PackList{};
+    blocks = 0;
+  };
+  for (size_t i = 0; i < ts.size(); ++i) {
+    check_dev(ts[i], "pack tensor");
+    const int d = dtype_code(ts[i]);
+    if (sdt != -1 && d != sdt) flush();
+    sdt = d;
+    TORCH_CHECK(offs[i] >= 0 && offs[i] + ts[i].numel() <= flat.numel(), "pack: slot out of range");
+    if (ts[i].numel() == 0) continue;
+    list.prefix[list.ntensors] = blocks;
+    list.e[list.ntensors++] = PackEntry{ts[i].data_ptr(), ts[i].numel(), offs[i]};
+    blocks += (int)((ts[i].numel() + chunk - 1) / chunk);
+    if (list.ntensors == kMaxList) flush();
+  }
+  flush();
+}
+
+void pack_list(std::vector<at::Tensor> ts, std::vector<int64_t> offs, at::Tensor flat, double scale) {
+  check_dev(flat, "flat");
+  pack_tensors_on(ts, offs, flat, (float)scale, current_stream(flat));
+}
 
 // ------------------------------------------------------------------------------------------
 // PackTable (declared in dla_tables.h).
@@ -180,6 +267,8 @@ void bind_ops(pybind11::module& m) {
       .def("unpack", &PackTable::unpack)
       .def("total_numel", &PackTable::total_numel);
   m.def("reduce_sum_", &reduce_sum_, "dst = scale*([dst] + sum(srcs))");
+  m.def("sgd_step_list", &sgd_step_list, "fused SGD over a by-value tensor list (<= 32 tensors per launch)");
+  m.def("pack_list", &pack_list, "gather tensors into a flat buffer at element offsets (by-value list launch)");
   m.def("scale_", &scale_, "t *= scale");
   m.def("uniform_", &uniform_, "Philox uniform fill");
   m.def("randint_", &randint_, "Philox integer fill in [0, high)");

@@ -14,25 +14,30 @@ import torch.nn as nn
 from . import _ext
 
 
+MASK_NONE, MASK_RECOMPUTE, MASK_BITS, MASK_Y = 0, 1, 2, 3
+
+
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu, stats):
         C = _ext.require()
-        y, ws = C.bn_act_fwd(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu,
-                             stats)
-        ctx.relu = relu
+        y, ws, mask = C.bn_act_fwd(x, residual, weight, bias, running_mean, running_var, training, momentum, eps,
+                                   relu, stats)
         ctx.has_res = residual is not None
         ctx.training = training
-        ctx.save_for_backward(x, y, ws, weight)
+        # ReLU branch for backward: recomputed from x (ReLU right after BN) or the forward's 1-bit
+        # mask (ReLU after the residual add) -- the output y is never re-read.
+        ctx.mask_mode = MASK_NONE if not relu else (MASK_BITS if ctx.has_res else MASK_RECOMPUTE)
+        ctx.save_for_backward(x, ws, weight, mask if mask is not None and mask.numel() else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         if not ctx.training:
             raise RuntimeError("fused BN backward in eval mode is not supported; use the torch backend")
-        x, y, ws, weight = ctx.saved_tensors
+        x, ws, weight, mask = ctx.saved_tensors
         C = _ext.require()
-        dx, dres, dg, db = C.bn_act_bwd(dy, y, x, ws, weight, ctx.relu, ctx.has_res)
+        dx, dres, dg, db = C.bn_act_bwd(dy, None, mask, x, ws, weight, ctx.mask_mode, ctx.has_res)
         need = ctx.needs_input_grad
         return (dx, dg if need[1] else None, db if need[2] else None, dres if ctx.has_res else None,
                 None, None, None, None, None, None, None)

@@ -68,8 +68,8 @@ class _Conv1x1(torch.autograd.Function):
             dxs = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
             if ctx.stride != 1:
                 H, W = h * ctx.stride, w * ctx.stride
-                dx = torch.zeros((n, cin, H, W), device=dy.device, dtype=dxs.dtype,
-                                 memory_format=torch.channels_last)
+                dx = torch.empty((n, cin, H, W), device=dy.device, dtype=dxs.dtype,
+                                 memory_format=torch.channels_last).zero_()
                 dx[:, :, ::ctx.stride, ::ctx.stride] = dxs
             else:
                 dx = dxs

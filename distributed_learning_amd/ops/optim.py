@@ -90,14 +90,11 @@ class FusedSGD(torch.optim.Optimizer):
         shadows = [p for p, m in zip(ps, masters) if m is not None]
         if shadows and len(shadows) != len(ps):  # mixed within a part cannot happen: grads share dtype
             raise RuntimeError("FusedSGD: mixed master/non-master parameters in one launch group")
-        key = (gi, first, tuple(t.data_ptr() for t in fp), tuple(g.data_ptr() for g in gs))
-        tab = self._tables.get(key[:2] + (len(fp), gs[0].dtype))
-        if tab is None or tab[0] != key:
-            C = _ext.require()
-            tab = (key, C.SgdTable(fp, gs, bufs if mom != 0 else [], shadows))
-            self._tables[key[:2] + (len(fp), gs[0].dtype)] = tab
-        tab[1].step(group["lr"], mom, group["dampening"], group["weight_decay"], group["nesterov"],
-                    group["grad_scale"], first)
+        # By-value tensor lists in the kernel arguments (<= 32 tensors per launch): no device table,
+        # so gradients may live anywhere and move every step (autograd-owned, set_to_none, views).
+        _ext.require().sgd_step_list(fp, gs, bufs if mom != 0 else [], shadows, group["lr"], mom,
+                                     group["dampening"], group["weight_decay"], group["nesterov"],
+                                     group["grad_scale"], first)
 
     @staticmethod
     def _reference_step(ps, gs, bufs, group, first):

@@ -71,6 +71,10 @@ class NativeEngine:
                          pack_scale: float = 1.0, unpack_scale: float = 1.0) -> None:
         self.impl.bucket_allreduce(flat, algo_code(algo), average, table, pack_scale, unpack_scale)
 
+    def bucket_allreduce_list(self, flat: torch.Tensor, algo: str, grads, offsets, average: bool = True) -> None:
+        """Gather autograd-owned ``grads`` into ``flat`` at ``offsets`` on the comm stream, then reduce."""
+        self.impl.bucket_allreduce_list(flat, algo_code(algo), average, list(grads), list(offsets))
+
     def broadcast(self, t: torch.Tensor, root: int = 0) -> None:
         self.impl.broadcast(t, root)
 

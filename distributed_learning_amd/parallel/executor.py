@@ -160,11 +160,22 @@ class TorchStreamExecutor(Executor):
 class NativeStreamExecutor(Executor):
     """GPU overlap through the C++ RCCL engine (pack/collective/unpack on its comm stream)."""
 
-    def __init__(self, engine, algorithm: str = "builtin"):
+    supports_steal = True
+
+    def __init__(self, engine, algorithm: str = "builtin", passthrough: Optional[bool] = None):
         self.engine = engine
         self.algorithm = algorithm
+        # one rank: nothing to reduce, gradients stay where autograd put them (tests can force the
+        # full gather/reduce/re-point path with passthrough=False)
+        self.passthrough = (engine.impl.world() == 1) if passthrough is None else passthrough
 
     def submit(self, b: Bucket) -> None:
+        if self.passthrough:
+            return
+        stolen = getattr(b, "stolen", None)
+        if stolen is not None:
+            self.engine.bucket_allreduce_list(b.flat, self.algorithm, [g for g, _ in stolen], [o for _, o in stolen])
+            return
         table = None if b.views else b.pack_table
         if not b.views and table is None:
             raise RuntimeError("native executor needs grad-as-bucket-view or a native PackTable")

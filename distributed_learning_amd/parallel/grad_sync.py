@@ -71,13 +71,27 @@ class GradSync:
 
     def __init__(self, params: Iterable[torch.Tensor], *, bucket_cap_bytes: int = 25 * 1024 * 1024,
                  executor: Executor, overlap: bool = True, grad_as_bucket_view: Optional[bool] = None,
-                 comm_dtype: Optional[torch.dtype] = None):
+                 comm_dtype: Optional[torch.dtype] = None, grad_mode: Optional[str] = None):
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
             raise ValueError("GradSync: no parameters require grad")
         self.device = self.params[0].device
         self.executor = executor
         self.overlap = overlap
+        # Gradient storage modes:
+        #   "steal" (native engine default): .grad is None before backward, AccumulateGrad hands the
+        #           autograd-produced tensor over without a copy; each complete bucket is gathered into
+        #           its flat buffer on the comm stream (one by-value multi-tensor launch) and reduced;
+        #           after sync every .grad is re-pointed at its averaged slot. No memset, no
+        #           accumulate-add kernels. With world size 1 the gradients pass through untouched.
+        #   "view": .grad is a persistent view of the bucket buffer (zeroed each step; autograd adds).
+        #   "pack": persistent .grad tensors packed/unpacked by a device-table kernel.
+        if grad_mode is None:
+            if getattr(executor, "supports_steal", False) and (comm_dtype is None) and grad_as_bucket_view is None:
+                grad_mode = "steal"
+            else:
+                grad_mode = None
+        self.grad_mode = grad_mode
         # comm_dtype=None: every bucket communicates in its parameters' dtype (mixed-precision
         # models get separate bf16 / fp32 buckets); a dtype here forces a wire format (e.g. bf16
         # compression of fp32 gradients, Horovod's Compression.fp16 analogue).
@@ -94,10 +108,20 @@ class GradSync:
             for j, p in enumerate(b.params):
                 self._owner[id(p)] = (b, j)
         self._persistent_grads = {}
-        if self.grad_as_bucket_view:
+        self.passthrough = bool(getattr(executor, "passthrough", False))
+        if self.grad_mode == "steal":
+            self.grad_as_bucket_view = False
+            self._install_views(install=False)
+            for b in self.buckets:
+                b.stolen = []
+        elif self.grad_as_bucket_view:
+            self.grad_mode = "view"
             self._install_views()
         elif self.device.type == "cuda":
+            self.grad_mode = "pack"
             self._install_pack_tables()
+        else:
+            self.grad_mode = "pack"
         self._next = 0
         self._enabled = True
         self._hooks = []
@@ -109,15 +133,16 @@ class GradSync:
     # -------------------------------------------------------------------------------------------
     # setup
     # -------------------------------------------------------------------------------------------
-    def _install_views(self):
+    def _install_views(self, install: bool = True):
         for b in self.buckets:
             b.views = []
             for p, off in zip(b.params, b.offsets):
                 if not is_dense(p):
-                    raise ValueError("grad_as_bucket_view needs dense parameters")
+                    raise ValueError("bucket views need dense parameters")
                 v = b.flat[off:off + p.numel()].as_strided(p.shape, p.stride())
                 b.views.append(v)
-                p.grad = v
+                if install:
+                    p.grad = v
 
     def _install_pack_tables(self):
         """Persistent grad tensors + one native PackTable per bucket (GPU pack mode)."""
@@ -139,7 +164,12 @@ class GradSync:
         self._next = 0
         for b in self.buckets:
             b.reset()
-        if self.grad_as_bucket_view:
+        if self.grad_mode == "steal":
+            for p in self.params:
+                p.grad = None
+            for b in self.buckets:
+                b.stolen = []
+        elif self.grad_as_bucket_view:
             for b in self.buckets:
                 for p, v in zip(b.params, b.views):
                     if p.grad is None or p.grad.data_ptr() != v.data_ptr():
@@ -174,7 +204,13 @@ class GradSync:
         self._ready(p)
 
     def _ready(self, p: torch.Tensor) -> None:
-        b, _ = self._owner[id(p)]
+        b, j = self._owner[id(p)]
+        if self.grad_mode == "steal":
+            g = p.grad
+            if g.dtype != b.flat.dtype or g.stride() != p.stride():
+                g = g.to(b.flat.dtype).as_strided(p.shape, p.stride()) if g.stride() == p.stride() else \
+                    torch.empty_like(p, dtype=b.flat.dtype).copy_(g)
+            b.stolen.append((g, b.offsets[j]))
         b.ready += 1
         if b.ready > len(b.params):
             raise RuntimeError(f"bucket {b.index}: parameter reported ready twice in one step "
@@ -192,9 +228,17 @@ class GradSync:
         """Launch every bucket that has not been launched (zero-filling missing grads)."""
         for b in self.buckets[self._next:]:
             if b.ready < len(b.params):
-                for p in b.params:
-                    if p.grad is None:
-                        p.grad = torch.zeros_like(p)
+                if self.grad_mode == "steal":
+                    recorded = {off for _, off in b.stolen}
+                    for p, off in zip(b.params, b.offsets):
+                        if off not in recorded:
+                            if p.grad is None:
+                                p.grad = torch.zeros_like(p)
+                            self._ready(p)  # records the gradient (no launch: bucket incomplete until the end)
+                else:
+                    for p in b.params:
+                        if p.grad is None:
+                            p.grad = torch.zeros_like(p)
                 b.ready = len(b.params)
         self._launch_in_order()
 
@@ -204,6 +248,11 @@ class GradSync:
             return
         self.flush()
         self.executor.finish()
+        if self.grad_mode == "steal" and not self.passthrough:
+            for b in self.buckets:
+                for p, v in zip(b.params, b.views):
+                    p.grad = v
+                b.stolen = []  # autograd's tensors are released only after the compute stream joined
         self.step_count += 1
 
     @contextlib.contextmanager

@@ -110,3 +110,30 @@ def test_resnet50_native_matches_torch_backend(cuda, dtype):
     floor, factor = (1e-3, 3.0) if dtype == torch.float32 else (2e-2, 5.0)
     for nt, tt in zip(native_vs_torch, torch_vs_torch):
         assert nt <= max(factor * tt, floor), (native_vs_torch, torch_vs_torch)
+
+
+@pytest.mark.parametrize("use_res", [False, True])
+def test_bn_act_mask_modes_agree(cuda, use_res):
+    """The recomputed (ReLU after BN) and bit-mask (ReLU after residual) backward branches must
+    reproduce the saved-output branch (mode 3) bit for bit."""
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    torch.manual_seed(1)
+    shape = (8, 128, 14, 14)
+    cl = dict(memory_format=torch.channels_last)
+    x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(**cl)
+    res = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(**cl) if use_res else None
+    w = torch.rand(128, device=cuda) + 0.5
+    b = torch.rand(128, device=cuda) - 0.5
+    y, ws, mask = C.bn_act_fwd(x, res, w, b, None, None, True, 0.1, 1e-5, True, None)
+    assert (mask is not None) == use_res
+    if use_res:
+        bits = torch.stack([(mask >> j) & 1 for j in range(8)], 1).reshape(-1)[: y.numel()]
+        assert torch.equal(bits.bool(), (y.permute(0, 2, 3, 1).reshape(-1) > 0))
+    dy = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(**cl)
+    ref = C.bn_act_bwd(dy, y, None, x, ws, w, 3, use_res)
+    got = C.bn_act_bwd(dy, None, mask, x, ws, w, 2 if use_res else 1, use_res)
+    for a, g in zip(ref, got):
+        if a is not None:
+            assert torch.equal(a, g)

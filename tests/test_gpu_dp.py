@@ -1,0 +1,100 @@
+"""Single-GPU checks of the GPU data-parallel path (native RCCL engine at world size 1, gpu)."""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def world1(cuda):
+    from distributed_learning_amd.parallel import context as ctx
+
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    os.environ.setdefault("LOCAL_RANK", "0")
+    c = ctx.init(backend="nccl")
+    yield c
+    ctx.shutdown()
+
+
+def _train(model_fn, wrap, steps, bf16):
+    from distributed_learning_amd.data import SyntheticBatches
+    from distributed_learning_amd.ops import nn as dnn
+    from distributed_learning_amd.ops.loss import cross_entropy
+    from distributed_learning_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda:0")
+    m = model_fn().to(dev).to(memory_format=torch.channels_last)
+    if bf16:
+        dnn.bf16_weights(m)
+    w = wrap(m)
+    opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, master_weights=bf16)
+    data = SyntheticBatches(8, (3, 32, 32), 10, dev, dtype=torch.bfloat16 if bf16 else torch.float32,
+                            channels_last=True)
+    losses = []
+    for _ in range(steps):
+        x, y = data.next()
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=not bf16):
+            loss = cross_entropy(w(x), y)
+        loss.backward()
+        w.sync_gradients()
+        opt.step()
+        losses.append(float(loss))
+    return m, losses
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("grouping", [25 * 1024 * 1024, 64 * 1024, 0])
+def test_native_engine_steal_path_matches_single_device(world1, bf16, grouping):
+    """Gather of autograd-owned grads into bucket buffers on the comm stream, the (world-1) RCCL
+    all-reduce and the re-pointing of .grad at the averaged slots must give exactly the single-device
+    update (the same kernels run; only the gradient storage differs)."""
+    from distributed_learning_amd.models import resnet18
+    from distributed_learning_amd.ops import nn as dnn
+    from distributed_learning_amd.parallel import PipelinedFusedDP, SingleDevice, make_reducer
+    from distributed_learning_amd.parallel.executor import NativeStreamExecutor
+
+    dnn.set_backend("native")
+    # MIOpen picks non-deterministic conv algorithms by default (run-to-run differences of ~1e-3
+    # that chaotic SGD amplifies); the comparison needs identical kernels on both sides.
+    det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        def wrap_dp(m):
+            red = make_reducer("immediate", "builtin", native=True)
+            w = PipelinedFusedDP(m, red, grouping, broadcast=False)
+            # force the full multi-rank data path (pack -> collective -> re-point) on one GPU
+            w.sync.executor = NativeStreamExecutor(red.engine, "builtin", passthrough=False)
+            w.sync.passthrough = False
+            assert w.sync.grad_mode == "steal"
+            return w
+
+        m1, l1 = _train(lambda: resnet18(10), wrap_dp, 4, bf16)
+        m2, l2 = _train(lambda: resnet18(10), SingleDevice, 4, bf16)
+    finally:
+        dnn.set_backend("torch")
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
+    assert l1 == pytest.approx(l2, rel=1e-5, abs=1e-5)
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6, msg=n)
+
+
+def test_engine_algorithms_world1(world1):
+    from distributed_learning_amd.parallel.engine import ALGO_CODES, NativeEngine
+
+    eng = NativeEngine.create(dist.group.WORLD, torch.device("cuda:0"))
+    x = torch.randn(100_003, device="cuda:0")
+    for algo in sorted(set(ALGO_CODES)):
+        y = x.clone()
+        eng.allreduce(y, algo, True)
+        eng.wait_on_current()
+        torch.testing.assert_close(y, x)  # world size 1: average == identity
+    eng.set_timing(True)
+    eng.allreduce(x, "builtin", True)
+    assert eng.consume_comm_ms() >= 0.0
+    eng.close()
