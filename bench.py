@@ -54,11 +54,11 @@ def parse():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--algorithm", default="builtin", help="native engine all-reduce: builtin|ring|direct|rsag|central")
     ap.add_argument("--bucket_mb", type=float, default=25.0)
-    ap.add_argument("--kernels", default=os.environ.get("DLA_KERNELS", "torch"), choices=["torch", "native"])
-    ap.add_argument("--precision", default=os.environ.get("DLA_PRECISION", "autocast"), choices=["autocast", "bf16"],
+    ap.add_argument("--kernels", default=os.environ.get("DLA_KERNELS", "native"), choices=["torch", "native"])
+    ap.add_argument("--precision", default=os.environ.get("DLA_PRECISION", "bf16"), choices=["autocast", "bf16"],
                     help="autocast: fp32 params + bf16 autocast; bf16: bf16 weights + fp32 master weights in the "
                          "fused optimizer (no per-step weight casts, bf16 gradients on the wire)")
-    ap.add_argument("--conv", default=os.environ.get("DLA_CONV", "miopen"), choices=["miopen", "native"],
+    ap.add_argument("--conv", default=os.environ.get("DLA_CONV", "native"), choices=["miopen", "native"],
                     help="1x1 convolutions on the native MFMA GEMMs (with fused BN statistics) or MIOpen")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--momentum", type=float, default=0.5)

@@ -40,6 +40,33 @@ template <> struct Cvt<bf16_t> {
   __device__ __forceinline__ static bf16_t from_f32(float v) { return f32_to_bf16(v); }
 };
 
+// 8 consecutive channels = one 16-byte (bf16) or two 16-byte (fp32) accesses, widened to fp32.
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16_t> {
+  __device__ __forceinline__ static void load(const bf16_t* p, float (&v)[8]) {
+    const ushort8_t x = *reinterpret_cast<const ushort8_t*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(x[j]);
+  }
+  __device__ __forceinline__ static void store(bf16_t* p, const float (&v)[8]) {
+    ushort8_t x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = f32_to_bf16(v[j]);
+    *reinterpret_cast<ushort8_t*>(p) = x;
+  }
+};
+template <> struct Vec8<float> {
+  __device__ __forceinline__ static void load(const float* p, float (&v)[8]) {
+    const float4_t a = reinterpret_cast<const float4_t*>(p)[0];
+    const float4_t b = reinterpret_cast<const float4_t*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ __forceinline__ static void store(float* p, const float (&v)[8]) {
+    reinterpret_cast<float4_t*>(p)[0] = float4_t{v[0], v[1], v[2], v[3]};
+    reinterpret_cast<float4_t*>(p)[1] = float4_t{v[4], v[5], v[6], v[7]};
+  }
+};
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);

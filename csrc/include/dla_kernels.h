@@ -101,6 +101,14 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
                    int64_t M, int C, int dtype, const float* gamma, float* ws, float* part, float* dgamma,
                    float* dbeta, int mask_mode, hipStream_t stream);
 
+// ---- max pooling, NHWC (pool.hip) ------------------------------------------------------------
+// x [N,H,W,C], y/pos [N,OH,OW,C] (pos: window position k*ky+kx of the max, 1 byte), C % 8 == 0,
+// N*H*W*C/8 < 2^31. Backward writes every dx element (no zero-fill needed).
+void launch_maxpool_fwd(const void* x, void* y, uint8_t* pos, int N, int H, int W, int C, int OH, int OW, int k,
+                        int s, int p, int dtype, hipStream_t stream);
+void launch_maxpool_bwd(const void* dy, const uint8_t* pos, void* dx, int N, int H, int W, int C, int OH, int OW,
+                        int k, int s, int p, int dtype, hipStream_t stream);
+
 // ---- bf16 MFMA GEMMs (gemm.hip) ---------------------------------------------------------------
 // C[M,N] = A[M,K] B[N,K]^T; optional per-column (sum, sumsq) partials stats[ceil(M/128)][N][2].
 // Requires K % 8 == 0, N % 8 == 0, 16-byte aligned rows.

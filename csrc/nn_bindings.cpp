@@ -158,7 +158,49 @@ at::Tensor gemm_tn(at::Tensor A, at::Tensor B, c10::ScalarType out_dtype, double
   return out;
 }
 
+static int pool_out(int in, int k, int s, int p, bool ceil_mode) {
+  int o = (in + 2 * p - k + (ceil_mode ? s - 1 : 0)) / s + 1;
+  if (ceil_mode && (int64_t)(o - 1) * s >= in + p) --o;  // last window must start inside the input
+  return o;
+}
+
+// NHWC max pooling. Returns (y, pos); pos (uint8, same shape as y) is the window position of each
+// maximum and is only produced when `need_pos` (training).
+std::vector<at::Tensor> maxpool_fwd(at::Tensor x, int64_t k, int64_t s, int64_t p, bool ceil_mode, bool need_pos) {
+  check_act(x, "x");
+  TORCH_CHECK(x.dim() == 4, "maxpool: 4-D input");
+  TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && p >= 0 && 2 * p <= k, "maxpool: unsupported window");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int OH = pool_out(H, (int)k, (int)s, (int)p, ceil_mode), OW = pool_out(W, (int)k, (int)s, (int)p, ceil_mode);
+  TORCH_CHECK(OH > 0 && OW > 0, "maxpool: empty output");
+  TORCH_CHECK((int64_t)N * H * W * (C / 8) < (1LL << 31), "maxpool: tensor too large for 32-bit indexing");
+  auto opts = x.options().memory_format(at::MemoryFormat::ChannelsLast);
+  at::Tensor y = at::empty({N, C, OH, OW}, opts);
+  at::Tensor pos;
+  if (need_pos) pos = at::empty({N, C, OH, OW}, opts.dtype(at::kByte));
+  launch_maxpool_fwd(x.data_ptr(), y.data_ptr(), need_pos ? pos.data_ptr<uint8_t>() : nullptr, N, H, W, C, OH, OW,
+                     (int)k, (int)s, (int)p, dtype_code(x), current_stream(x));
+  return {y, pos};
+}
+
+at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor pos, int64_t H, int64_t W, int64_t k, int64_t s, int64_t p) {
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  check_act(dy, "dy");
+  TORCH_CHECK(pos.scalar_type() == at::kByte && pos.sizes() == dy.sizes() &&
+                  pos.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "maxpool_bwd: pos must be the forward's uint8 positions");
+  const int N = (int)dy.size(0), C = (int)dy.size(1), OH = (int)dy.size(2), OW = (int)dy.size(3);
+  at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_maxpool_bwd(dy.data_ptr(), pos.data_ptr<uint8_t>(), dx.data_ptr(), N, (int)H, (int)W, C, OH, OW, (int)k,
+                     (int)s, (int)p, dtype_code(dy), current_stream(dy));
+  return dx;
+}
+
 void bind_nn(pybind11::module& m) {
+  m.def("maxpool_fwd", &maxpool_fwd, "NHWC max pooling forward (+ argmax window positions)", pybind11::arg("x"),
+        pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("ceil_mode") = false,
+        pybind11::arg("need_pos") = true);
+  m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pooling backward (gather form)");
   m.def("gemm_nt", &gemm_nt, "C = A @ B^T (bf16 MFMA), optional fused column statistics", pybind11::arg("A"),
         pybind11::arg("B"), pybind11::arg("stats") = false);
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),

@@ -23,6 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import nn as dnn
+from ..ops.pool import MaxPool2d
 
 
 class BasicConv2d(nn.Module):
@@ -43,7 +44,7 @@ class Inception(nn.Module):
                                      BasicConv2d(ch3x3red, ch3x3, kernel_size=3, padding=1))
         self.branch3 = nn.Sequential(BasicConv2d(cin, ch5x5red, kernel_size=1),
                                      BasicConv2d(ch5x5red, ch5x5, kernel_size=3, padding=1))
-        self.branch4 = nn.Sequential(nn.MaxPool2d(kernel_size=3, stride=1, padding=1, ceil_mode=True),
+        self.branch4 = nn.Sequential(MaxPool2d(kernel_size=3, stride=1, padding=1, ceil_mode=True),
                                      BasicConv2d(cin, pool_proj, kernel_size=1))
 
     def forward(self, x):
@@ -71,19 +72,19 @@ class GoogLeNet(nn.Module):
         super().__init__()
         self.aux_logits = aux_logits
         self.conv1 = BasicConv2d(3, 64, kernel_size=7, stride=2, padding=3)
-        self.maxpool1 = nn.MaxPool2d(3, stride=2, ceil_mode=True)
+        self.maxpool1 = MaxPool2d(3, stride=2, ceil_mode=True)
         self.conv2 = BasicConv2d(64, 64, kernel_size=1)
         self.conv3 = BasicConv2d(64, 192, kernel_size=3, padding=1)
-        self.maxpool2 = nn.MaxPool2d(3, stride=2, ceil_mode=True)
+        self.maxpool2 = MaxPool2d(3, stride=2, ceil_mode=True)
         self.inception3a = Inception(192, 64, 96, 128, 16, 32, 32)
         self.inception3b = Inception(256, 128, 128, 192, 32, 96, 64)
-        self.maxpool3 = nn.MaxPool2d(3, stride=2, ceil_mode=True)
+        self.maxpool3 = MaxPool2d(3, stride=2, ceil_mode=True)
         self.inception4a = Inception(480, 192, 96, 208, 16, 48, 64)
         self.inception4b = Inception(512, 160, 112, 224, 24, 64, 64)
         self.inception4c = Inception(512, 128, 128, 256, 24, 64, 64)
         self.inception4d = Inception(512, 112, 144, 288, 32, 64, 64)
         self.inception4e = Inception(528, 256, 160, 320, 32, 128, 128)
-        self.maxpool4 = nn.MaxPool2d(2, stride=2, ceil_mode=True)
+        self.maxpool4 = MaxPool2d(2, stride=2, ceil_mode=True)
         self.inception5a = Inception(832, 256, 160, 320, 32, 128, 128)
         self.inception5b = Inception(832, 384, 192, 384, 48, 128, 128)
         if aux_logits:
