@@ -60,6 +60,8 @@ def parse():
                          "fused optimizer (no per-step weight casts, bf16 gradients on the wire)")
     ap.add_argument("--conv", default=os.environ.get("DLA_CONV", "native"), choices=["miopen", "native"],
                     help="1x1 convolutions on the native MFMA GEMMs (with fused BN statistics) or MIOpen")
+    ap.add_argument("--graph", default=os.environ.get("DLA_GRAPH", "off"), choices=["on", "off"],
+                    help="capture the whole training step (data, fwd, bwd, collectives, optimizer) in a HIP graph")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--momentum", type=float, default=0.5)
     return ap.parse_args()
@@ -91,7 +93,7 @@ def main():
     opt = FusedSGD(model.module.parameters(), lr=a.lr, momentum=a.momentum, master_weights=bf16)
     data = SyntheticBatches(a.batch, spec.input_shape, spec.num_classes, dev,
                             dtype=torch.bfloat16 if bf16 else torch.float32,
-                            seed=1234, rank=rank, channels_last=True)
+                            seed=1234, rank=rank, channels_last=True, device_step=a.graph == "on")
     engine = reducer.engine
 
     def step():
@@ -105,11 +107,28 @@ def main():
         opt.step()
         return loss
 
+    graphed = a.graph == "on"
+    comm_ms_eager = None
+    if graphed:
+        from distributed_learning_amd.parallel.graphs import GraphedStep
+
+        # eager steps first: algorithm selection, lazy state, and the comm time of one eager step
+        # (event timers are not recorded inside the graph)
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        engine.consume_comm_ms()
+        engine.set_timing(True)
+        step()
+        torch.cuda.synchronize()
+        engine.set_timing(False)
+        comm_ms_eager = engine.consume_comm_ms()
+        step = GraphedStep(step, warmup=2, device=dev)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
     engine.consume_comm_ms()
-    engine.set_timing(True)
+    engine.set_timing(not graphed)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -119,7 +138,7 @@ def main():
     dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    comm_ms = engine.consume_comm_ms() / max(1, a.steps)
+    comm_ms = engine.consume_comm_ms() / max(1, a.steps) if not graphed else comm_ms_eager
     engine.set_timing(False)
     t = torch.tensor([elapsed, comm_ms], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -154,6 +173,7 @@ def main():
                 "kernels": a.kernels,
                 "precision": a.precision,
                 "conv1x1": a.conv,
+                "hip_graph": graphed,
                 "optimizer": f"fused SGD momentum={a.momentum} (fp32 master weights)",
             },
             "allreduce_ms_per_step": round(comm_ms, 3),
@@ -161,6 +181,19 @@ def main():
             "baseline_ref": {"value": ref, "what": "reference best published img/s at this N (GoogLeNet, P100, Gloo)"},
         }
         print(json.dumps(rec), flush=True)
+    prof_out = os.environ.get("DLA_TORCH_PROF")
+    if prof_out and rank == 0:  # diagnostics only, after the timed region: op -> kernel attribution
+        from torch.profiler import ProfilerActivity, profile
+
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+        with open(prof_out, "w") as f:
+            f.write(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=60, max_name_column_width=90))
+            f.write("\n\n")
+            f.write(prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=40,
+                                                                max_name_column_width=60, max_src_column_width=400))
     model.cleanup()
     ctxmod.shutdown()
 

@@ -73,10 +73,11 @@ void launch_reduce_sum(void* dst, bool accumulate_dst, const ReduceSrcs& srcs, i
 void launch_scale(void* data, int64_t n, int dtype, float scale, hipStream_t stream);
 
 // ---- synthetic data (synthetic.hip) ---------------------------------------------------------
+// Philox stream position = offset [+ (*step) * per_step when `step` (device int64 counter) is set].
 void launch_uniform_fill(void* out, int64_t n, int dtype, uint64_t seed, uint64_t offset, float lo, float hi,
-                         hipStream_t stream);
+                         hipStream_t stream, const int64_t* step = nullptr, uint64_t per_step = 0);
 void launch_randint_fill(int64_t* out, int64_t n, int64_t high, uint64_t seed, uint64_t offset,
-                         hipStream_t stream);
+                         hipStream_t stream, const int64_t* step = nullptr, uint64_t per_step = 0);
 
 // ---- fused log-softmax + NLL (loss.hip) -----------------------------------------------------
 // logits [B, C] (dtype), target [B] int64 (< 0 = ignored). ws: 3*B floats (row lse, row loss,
@@ -110,11 +111,13 @@ void launch_maxpool_bwd(const void* dy, const uint8_t* pos, void* dx, int N, int
                         int k, int s, int p, int dtype, hipStream_t stream);
 
 // ---- bf16 MFMA GEMMs (gemm.hip) ---------------------------------------------------------------
-// C[M,N] = A[M,K] B[N,K]^T; optional per-column (sum, sumsq) partials stats[ceil(M/128)][N][2].
-// Requires K % 8 == 0, N % 8 == 0, 16-byte aligned rows.
+// C[M,N] = A[M,K] B[N,K]^T [+ addend[M,N]] (b_kmajor: B given as [K,N], i.e. C = A B); optional
+// per-column (sum, sumsq) partials stats[ceil(M/128)][N][2]. Requires K % 8 == 0, N % 8 == 0,
+// 16-byte aligned rows.
 int gemm_nt_row_block(int M, int N);
 void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
-                    float* stats, hipStream_t stream);
+                    float* stats, hipStream_t stream, const void* addend = nullptr, int64_t ld_addend = 0,
+                    bool b_kmajor = false);
 // out[Mo,No] (= scale * A^T B [+ out]) with A [K, lda>=Mo], B [K, ldb>=No]; partial: splits*Mo*No f32.
 int gemm_tn_splits(int Mo, int No, int K);
 void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, float* partial, int splits, int Mo, int No,

@@ -34,18 +34,46 @@ __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// k-major tile image for ds_read_b64_tr_b16 (rows = k, W = 64 or 128 columns, unpadded rows).
+// A 32-lane half of a transposed 16x16x32-operand read touches rows {r..r+3, r+8..r+11} x 4
+// consecutive 8-byte chunks; with plain rows those 8 row-blocks share banks (2-way or worse for any
+// constant row pitch). XOR-ing the chunk index with a row-dependent multiple of 4 gives the 8
+// row-blocks disjoint 8-bank windows (conflict-free), keeps every 4-chunk (32 B) group and every
+// 16-byte store contiguous, and the same function addresses stores and reads.
+template <int W>
+__device__ __forceinline__ int tr_off(int row, int col) {  // element offset of (row, col), col % 4 == 0
+  static_assert(W == 64 || W == 128, "tr image width");
+  int sw;
+  if constexpr (W == 128)
+    sw = 4 * ((row & 3) | (((row >> 3) & 1) << 2));  // 32 chunks/row (256 B = 64 banks)
+  else
+    sw = 4 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));  // 16 chunks/row; row parity adds 32 banks
+  return row * W + (((col >> 2) ^ sw) << 2);
+}
+
+__device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* lo_ptr, const bf16_t* hi_ptr) {
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(lo_ptr));
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(hi_ptr));
+  const short v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return *reinterpret_cast<const bf16x8_t*>(v);
+}
+
 // ---------------------------------------------------------------------------------------------
 // C[M,N] = A[M,K] * B[N,K]^T   (all row-major; A, B K-contiguous), bf16 in/out, fp32 accumulate.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, bool kStats>
+// kBT: B is given k-major ([K, N], n-contiguous — e.g. the conv weight for dgrad) and its MFMA
+// fragments are read with the transposing ds_read_b64_tr_b16, so no transposed copy is needed.
+template <int BM, int BN, bool kStats, bool kBT>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                                   const bf16_t* __restrict__ B, int64_t ldb,
                                                                   bf16_t* __restrict__ C, int64_t ldc, int M, int N,
-                                                                  int K, float* __restrict__ stats) {
+                                                                  int K, float* __restrict__ stats,
+                                                                  const bf16_t* __restrict__ D, int64_t ldd) {
   constexpr int LDS_K = kBK + 8;  // +16 B per row: conflict-free ds_read_b128 fragment reads
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int ACH = BM * kBK / 8 / kGemmThreads;  // 16-byte chunks per thread per A tile
   constexpr int BCH = BN * kBK / 8 / kGemmThreads;
+  constexpr int BPR = BN / 8;  // kBT: B tile stored [kBK][BN] in the tr_off image
   static_assert(ACH >= 1 && BCH >= 1, "tile too small for 256 threads");
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem_raw);
@@ -70,10 +98,18 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(const bf16_t* 
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
-      const int c = tid + i * kGemmThreads, r = c >> 3, kc = (c & 7) * 8;
-      const int gn = col0 + r;
-      rb[i] = (gn < N && k0 + kc < K) ? *reinterpret_cast<const ushort8_t*>(B + (int64_t)gn * ldb + k0 + kc)
-                                      : ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      const int c = tid + i * kGemmThreads;
+      if constexpr (kBT) {
+        const int kr = c / BPR, nc = (c % BPR) * 8;
+        const int gk = k0 + kr, gn = col0 + nc;
+        rb[i] = (gk < K && gn < N) ? *reinterpret_cast<const ushort8_t*>(B + (int64_t)gk * ldb + gn)
+                                   : ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      } else {
+        const int r = c >> 3, kc = (c & 7) * 8;
+        const int gn = col0 + r;
+        rb[i] = (gn < N && k0 + kc < K) ? *reinterpret_cast<const ushort8_t*>(B + (int64_t)gn * ldb + k0 + kc)
+                                        : ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      }
     }
   };
   auto sstore = [&]() {
@@ -85,7 +121,10 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(const bf16_t* 
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int c = tid + i * kGemmThreads;
-      *reinterpret_cast<ushort8_t*>(Bs + (c >> 3) * LDS_K + (c & 7) * 8) = rb[i];
+      if constexpr (kBT)
+        *reinterpret_cast<ushort8_t*>(Bs + tr_off<BN>(c / BPR, (c % BPR) * 8)) = rb[i];
+      else
+        *reinterpret_cast<ushort8_t*>(Bs + (c >> 3) * LDS_K + (c & 7) * 8) = rb[i];
     }
   };
 
@@ -95,6 +134,8 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(const bf16_t* 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  // transposed-read lane map (kBT): lane 4q+p of 16-lane group g reads k-row 8g+q, columns 4p..4p+3
+  const int tg = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
   const int nk = (K + kBK - 1) / kBK;
   gload(0);
   sstore();
@@ -109,8 +150,14 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(const bf16_t* 
       for (int i = 0; i < TM; ++i)
         af[i] = *reinterpret_cast<const bf16x8_t*>(As + (wr * WM + i * 16 + fr) * LDS_K + kk * 32 + fk);
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bs + (wc * WN + j * 16 + fr) * LDS_K + kk * 32 + fk);
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (kBT) {
+          const int kr = kk * 32 + 8 * tg + tq, cn = wc * WN + j * 16 + 4 * tp;
+          bfr[j] = tr_frag(Bs + tr_off<BN>(kr, cn), Bs + tr_off<BN>(kr + 4, cn));
+        } else {
+          bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bs + (wc * WN + j * 16 + fr) * LDS_K + kk * 32 + fk);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -154,7 +201,15 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(const bf16_t* 
     const int r = c / CPR, cc = (c % CPR) * 8;
     const int64_t gm = row0 + r;
     const int gn = col0 + cc;
-    if (gm < M && gn < N) *reinterpret_cast<ushort8_t*>(C + gm * ldc + gn) = *reinterpret_cast<ushort8_t*>(Cs + r * LDS_C + cc);
+    if (gm < M && gn < N) {
+      ushort8_t v = *reinterpret_cast<ushort8_t*>(Cs + r * LDS_C + cc);
+      if (D) {  // fused addend (residual-gradient sum): C = bf16(bf16(A B^T) + D), as the unfused add
+        const ushort8_t d = *reinterpret_cast<const ushort8_t*>(D + gm * ldd + gn);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(d[j]));
+      }
+      *reinterpret_cast<ushort8_t*>(C + gm * ldc + gn) = v;
+    }
   }
   if constexpr (kStats) {
     float* red = reinterpret_cast<float*>(smem_raw + BM * LDS_C * sizeof(bf16_t));  // [2 wr][BN][2]
@@ -187,13 +242,13 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_tn_kernel(const bf16_t* 
                                                                   const bf16_t* __restrict__ B, int64_t ldb,
                                                                   float* __restrict__ P, int Mo, int No, int K,
                                                                   int k_per_split) {
-  constexpr int LDS_A = BM + 8, LDS_B = BN + 8;  // rows stay 8-byte aligned for ds_read_b64_tr_b16
+  // both tiles k-major in the swizzled tr_off image (conflict-free transposed reads)
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int ACH = kBK * BM / 8 / kGemmThreads, BCH = kBK * BN / 8 / kGemmThreads;
   static_assert(ACH >= 1 && BCH >= 1, "tile too small");
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  bf16_t* As = reinterpret_cast<bf16_t*>(smem_raw);  // [BK][LDS_A]
-  bf16_t* Bs = As + kBK * LDS_A;                     // [BK][LDS_B]
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem_raw);  // [BK][BM]
+  bf16_t* Bs = As + kBK * BM;                        // [BK][BN]
 
   const int nbn = (No + BN - 1) / BN;
   const int tile = blockIdx.x;
@@ -227,12 +282,12 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_tn_kernel(const bf16_t* 
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int c = tid + i * kGemmThreads;
-      *reinterpret_cast<ushort8_t*>(As + (c / APR) * LDS_A + (c % APR) * 8) = ra[i];
+      *reinterpret_cast<ushort8_t*>(As + tr_off<BM>(c / APR, (c % APR) * 8)) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int c = tid + i * kGemmThreads;
-      *reinterpret_cast<ushort8_t*>(Bs + (c / BPR) * LDS_B + (c % BPR) * 8) = rb[i];
+      *reinterpret_cast<ushort8_t*>(Bs + tr_off<BN>(c / BPR, (c % BPR) * 8)) = rb[i];
     }
   };
 
@@ -259,23 +314,13 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_tn_kernel(const bf16_t* 
       const int kr = kk * 32 + 8 * g + q;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const bf16_t* base = As + kr * LDS_A + wr * WM + i * 16 + 4 * p;
-        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(base));
-        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(base + 4 * LDS_A));
-        const short v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = *reinterpret_cast<const bf16x8_t*>(v);
+        const int cm = wr * WM + i * 16 + 4 * p;
+        af[i] = tr_frag(As + tr_off<BM>(kr, cm), As + tr_off<BM>(kr + 4, cm));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const bf16_t* base = Bs + kr * LDS_B + wc * WN + j * 16 + 4 * p;
-        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(base));
-        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(base + 4 * LDS_B));
-        const short v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = *reinterpret_cast<const bf16x8_t*>(v);
+        const int cn = wc * WN + j * 16 + 4 * p;
+        bfr[j] = tr_frag(Bs + tr_off<BN>(kr, cn), Bs + tr_off<BN>(kr + 4, cn));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -341,14 +386,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // ---------------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, bool S>
+template <int BM, int BN, bool S, bool BT>
 static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
-                      int N, int K, float* stats, hipStream_t stream) {
+                      int N, int K, float* stats, const bf16_t* D, int64_t ldd, hipStream_t stream) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  size_t ab = (size_t)(BM + BN) * (kBK + 8) * sizeof(bf16_t);
+  size_t ab = ((size_t)BM * (kBK + 8) + (BT ? (size_t)kBK * BN : (size_t)BN * (kBK + 8))) * sizeof(bf16_t);
   size_t cs = (size_t)BM * (BN + 8) * sizeof(bf16_t) + (S ? (size_t)kGemmThreads / BN * BN * 2 * sizeof(float) : 0);
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, S>), dim3(tiles), dim3(kGemmThreads), std::max(ab, cs), stream, A, lda, B,
-                     ldb, C, ldc, M, N, K, stats);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, S, BT>), dim3(tiles), dim3(kGemmThreads), std::max(ab, cs), stream, A, lda, B,
+                     ldb, C, ldc, M, N, K, stats, D, ldd);
 }
 
 int gemm_nt_row_block(int M, int N) {
@@ -357,17 +402,21 @@ int gemm_nt_row_block(int M, int N) {
 }
 
 void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
-                    float* stats, hipStream_t stream) {
+                    float* stats, hipStream_t stream, const void* addend, int64_t ld_addend, bool b_kmajor) {
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* b = (const bf16_t*)B;
   bf16_t* c = (bf16_t*)C;
+  const bf16_t* d = (const bf16_t*)addend;
+#define DLA_NT(BN_, S_, BT_) launch_nt<128, BN_, S_, BT_>(a, lda, b, ldb, c, ldc, M, N, K, stats, d, ld_addend, stream)
+#define DLA_NT_BT(BN_, S_) \
+  if (b_kmajor) DLA_NT(BN_, S_, true); else DLA_NT(BN_, S_, false);
   if (N <= 64) {
-    if (stats) launch_nt<128, 64, true>(a, lda, b, ldb, c, ldc, M, N, K, stats, stream);
-    else launch_nt<128, 64, false>(a, lda, b, ldb, c, ldc, M, N, K, stats, stream);
+    if (stats) { DLA_NT_BT(64, true) } else { DLA_NT_BT(64, false) }
   } else {
-    if (stats) launch_nt<128, 128, true>(a, lda, b, ldb, c, ldc, M, N, K, stats, stream);
-    else launch_nt<128, 128, false>(a, lda, b, ldb, c, ldc, M, N, K, stats, stream);
+    if (stats) { DLA_NT_BT(128, true) } else { DLA_NT_BT(128, false) }
   }
+#undef DLA_NT_BT
+#undef DLA_NT
 }
 
 int gemm_tn_splits(int Mo, int No, int K) {
@@ -384,7 +433,7 @@ void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, floa
   int kps = (K + splits - 1) / splits;
   kps = (kps + kBK - 1) / kBK * kBK;
   const int tiles = ((Mo + 127) / 128) * ((No + 127) / 128);
-  const size_t lds = (size_t)kBK * (128 + 8 + 128 + 8) * sizeof(bf16_t);
+  const size_t lds = (size_t)kBK * (128 + 128) * sizeof(bf16_t);
   hipLaunchKernelGGL((gemm_tn_kernel<128, 128>), dim3(tiles, splits), dim3(kGemmThreads), lds, stream,
                      (const bf16_t*)A, lda, (const bf16_t*)B, ldb, partial, Mo, No, K, kps);
   const int64_t n = (int64_t)Mo * No;

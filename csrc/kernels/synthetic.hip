@@ -38,9 +38,17 @@ __device__ __forceinline__ float u32_to_unit(uint32_t x) {  // [0, 1) with 24-bi
   return (x >> 8) * (1.0f / 16777216.0f);
 }
 
+// Stream position: offset + (*step) * per_step when `step` (a device counter) is given — a graph
+// replay then draws a fresh batch each time without any host-side argument change.
+__device__ __forceinline__ uint64_t stream_offset(uint64_t offset, const int64_t* step, uint64_t per_step) {
+  return step ? offset + (uint64_t)(*step) * per_step : offset;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void uniform_kernel(T* __restrict__ out, int64_t n, uint64_t seed, uint64_t offset,
-                                                      float lo, float span) {
+                                                      float lo, float span, const int64_t* __restrict__ step,
+                                                      uint64_t per_step) {
+  offset = stream_offset(offset, step, per_step);
   const int64_t ngroups = (n + 3) / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gi < ngroups; gi += stride) {
@@ -64,7 +72,9 @@ __global__ __launch_bounds__(256) void uniform_kernel(T* __restrict__ out, int64
 }
 
 __global__ __launch_bounds__(256) void randint_kernel(int64_t* __restrict__ out, int64_t n, int64_t high, uint64_t seed,
-                                                      uint64_t offset) {
+                                                      uint64_t offset, const int64_t* __restrict__ step,
+                                                      uint64_t per_step) {
+  offset = stream_offset(offset, step, per_step);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     uint32_t r[4];
@@ -75,21 +85,23 @@ __global__ __launch_bounds__(256) void randint_kernel(int64_t* __restrict__ out,
 }
 
 void launch_uniform_fill(void* out, int64_t n, int dtype, uint64_t seed, uint64_t offset, float lo, float hi,
-                         hipStream_t stream) {
+                         hipStream_t stream, const int64_t* step, uint64_t per_step) {
   if (n <= 0) return;
   int64_t groups = (n + 3) / 4;
   int grid = (int)std::min<int64_t>((groups + 255) / 256, 4096);
   if (dtype == kF32)
-    hipLaunchKernelGGL(uniform_kernel<float>, dim3(grid), dim3(256), 0, stream, (float*)out, n, seed, offset, lo, hi - lo);
+    hipLaunchKernelGGL(uniform_kernel<float>, dim3(grid), dim3(256), 0, stream, (float*)out, n, seed, offset, lo, hi - lo,
+                       step, per_step);
   else
     hipLaunchKernelGGL(uniform_kernel<bf16_t>, dim3(grid), dim3(256), 0, stream, (bf16_t*)out, n, seed, offset, lo,
-                       hi - lo);
+                       hi - lo, step, per_step);
 }
 
-void launch_randint_fill(int64_t* out, int64_t n, int64_t high, uint64_t seed, uint64_t offset, hipStream_t stream) {
+void launch_randint_fill(int64_t* out, int64_t n, int64_t high, uint64_t seed, uint64_t offset, hipStream_t stream,
+                         const int64_t* step, uint64_t per_step) {
   if (n <= 0) return;
   int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
-  hipLaunchKernelGGL(randint_kernel, dim3(grid), dim3(256), 0, stream, out, n, high, seed, offset);
+  hipLaunchKernelGGL(randint_kernel, dim3(grid), dim3(256), 0, stream, out, n, high, seed, offset, step, per_step);
 }
 
 }  // namespace dla

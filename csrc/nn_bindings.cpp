@@ -126,20 +126,27 @@ static void check_mat(const at::Tensor& t, const char* what) {
   TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, what, " must be 16-byte aligned");
 }
 
-// C = A @ B^T (A [M,K], B [N,K]) in bf16 with fp32 accumulation. Optionally returns per-row-block
+// C = A @ B^T (A [M,K], B [N,K]; or C = A @ B with B [K,N] when b_kmajor) in bf16 with fp32 accumulation. Optionally returns per-row-block
 // column statistics partials [ceil(M/128), N, 2] (sum, sum of squares of the bf16 outputs).
-std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats) {
+std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::optional<at::Tensor> addend,
+                                bool b_kmajor) {
   check_mat(A, "A");
   check_mat(B, "B");
-  TORCH_CHECK(A.size(1) == B.size(1), "gemm_nt: K mismatch");
-  const int M = (int)A.size(0), N = (int)B.size(0), K = (int)A.size(1);
+  TORCH_CHECK(A.size(1) == B.size(b_kmajor ? 0 : 1), "gemm_nt: K mismatch");
+  const int M = (int)A.size(0), N = (int)B.size(b_kmajor ? 1 : 0), K = (int)A.size(1);
+  const bool add = addend.has_value() && addend->defined();
+  if (add) {
+    check_mat(*addend, "addend");
+    TORCH_CHECK(addend->size(0) == M && addend->size(1) == N, "gemm_nt: addend must be [M, N]");
+  }
   at::Tensor C = at::empty({M, N}, A.options());
   at::Tensor S;
   if (stats) S = at::empty({(M + gemm_nt_row_block(M, N) - 1) / gemm_nt_row_block(M, N), N, 2},
                            A.options().dtype(at::kFloat));
   if (M > 0 && N > 0)
     launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K,
-                   stats ? S.data_ptr<float>() : nullptr, current_stream(A));
+                   stats ? S.data_ptr<float>() : nullptr, current_stream(A), add ? addend->data_ptr() : nullptr,
+                   add ? addend->stride(0) : 0, b_kmajor);
   return {C, S};
 }
 
@@ -202,7 +209,8 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("need_pos") = true);
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pooling backward (gather form)");
   m.def("gemm_nt", &gemm_nt, "C = A @ B^T (bf16 MFMA), optional fused column statistics", pybind11::arg("A"),
-        pybind11::arg("B"), pybind11::arg("stats") = false);
+        pybind11::arg("B"), pybind11::arg("stats") = false, pybind11::arg("addend") = pybind11::none(),
+        pybind11::arg("b_kmajor") = false);
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),
         pybind11::arg("out_dtype") = at::kFloat, pybind11::arg("scale") = 1.0);
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC", pybind11::arg("x"),

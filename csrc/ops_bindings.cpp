@@ -218,17 +218,27 @@ void scale_(at::Tensor t, double scale) {
   launch_scale(t.data_ptr(), t.numel(), dtype_code(t), (float)scale, current_stream(t));
 }
 
-void uniform_(at::Tensor t, int64_t seed, int64_t offset, double lo, double hi) {
-  check_dev(t, "tensor");
-  launch_uniform_fill(t.data_ptr(), t.numel(), dtype_code(t), (uint64_t)seed, (uint64_t)offset, (float)lo, (float)hi,
-                      current_stream(t));
+static const int64_t* step_ptr(const c10::optional<at::Tensor>& step, const at::Tensor& t) {
+  if (!step.has_value() || !step->defined()) return nullptr;
+  TORCH_CHECK(step->scalar_type() == at::kLong && step->numel() == 1 && step->device() == t.device(),
+              "step must be a one-element int64 tensor on the output's device");
+  return step->data_ptr<int64_t>();
 }
 
-void randint_(at::Tensor t, int64_t high, int64_t seed, int64_t offset) {
+void uniform_(at::Tensor t, int64_t seed, int64_t offset, double lo, double hi, c10::optional<at::Tensor> step,
+              int64_t per_step) {
+  check_dev(t, "tensor");
+  launch_uniform_fill(t.data_ptr(), t.numel(), dtype_code(t), (uint64_t)seed, (uint64_t)offset, (float)lo, (float)hi,
+                      current_stream(t), step_ptr(step, t), (uint64_t)per_step);
+}
+
+void randint_(at::Tensor t, int64_t high, int64_t seed, int64_t offset, c10::optional<at::Tensor> step,
+              int64_t per_step) {
   check_dev(t, "tensor");
   TORCH_CHECK(t.scalar_type() == at::kLong, "randint_: int64 tensor required");
   TORCH_CHECK(high > 0, "randint_: high must be positive");
-  launch_randint_fill(t.data_ptr<int64_t>(), t.numel(), high, (uint64_t)seed, (uint64_t)offset, current_stream(t));
+  launch_randint_fill(t.data_ptr<int64_t>(), t.numel(), high, (uint64_t)seed, (uint64_t)offset, current_stream(t),
+                      step_ptr(step, t), (uint64_t)per_step);
 }
 
 std::vector<at::Tensor> xent_fwd(at::Tensor logits, at::Tensor target) {
@@ -270,8 +280,12 @@ void bind_ops(pybind11::module& m) {
   m.def("sgd_step_list", &sgd_step_list, "fused SGD over a by-value tensor list (<= 32 tensors per launch)");
   m.def("pack_list", &pack_list, "gather tensors into a flat buffer at element offsets (by-value list launch)");
   m.def("scale_", &scale_, "t *= scale");
-  m.def("uniform_", &uniform_, "Philox uniform fill");
-  m.def("randint_", &randint_, "Philox integer fill in [0, high)");
+  m.def("uniform_", &uniform_, "Philox uniform fill (stream position offset [+ *step * per_step])",
+        pybind11::arg("t"), pybind11::arg("seed"), pybind11::arg("offset"), pybind11::arg("lo"), pybind11::arg("hi"),
+        pybind11::arg("step") = pybind11::none(), pybind11::arg("per_step") = 0);
+  m.def("randint_", &randint_, "Philox integer fill in [0, high)", pybind11::arg("t"), pybind11::arg("high"),
+        pybind11::arg("seed"), pybind11::arg("offset"), pybind11::arg("step") = pybind11::none(),
+        pybind11::arg("per_step") = 0);
   m.def("xent_fwd", &xent_fwd, "fused log-softmax + NLL forward");
   m.def("xent_bwd", &xent_bwd, "fused log-softmax + NLL backward");
 }

@@ -167,7 +167,7 @@ class SyntheticBatches:
 
     def __init__(self, batch_size: int, shape: Tuple[int, int, int], num_classes: int, device,
                  dtype: torch.dtype = torch.float32, seed: int = 1234, rank: int = 0, identical: bool = False,
-                 channels_last: bool = False, regenerate: bool = True):
+                 channels_last: bool = False, regenerate: bool = True, device_step: bool = False):
         self.batch_size = batch_size
         self.shape = tuple(shape)
         self.num_classes = num_classes
@@ -187,14 +187,26 @@ class SyntheticBatches:
         if self.device.type == "cuda" and not self._native:
             _ext.require()  # fail loudly on a GPU box without the extension
         self._cpu_gen = torch.Generator().manual_seed(self.seed)
+        # device_step: the stream position lives in a device counter advanced by a kernel, so the
+        # generation can be captured in a HIP graph and still draw a new batch on every replay
+        self._step_dev = (torch.zeros((1,), dtype=torch.long, device=self.device)
+                          if device_step and self._native else None)
         self._fill()
+        if self._step_dev is not None:
+            self._step_dev.zero_()  # same stream positions as the host-stepped generator
 
     def _fill(self):
         if self._native:
             C = _ext.require()
             flat = self._x if not self.channels_last else self._x.permute(0, 2, 3, 1)
-            C.uniform_(flat, self.seed, self.step * ((flat.numel() + 3) // 4), 0.0, 1.0)
-            C.randint_(self._y, self.num_classes, self.seed, self.step * self.batch_size)
+            per_x, per_y = (flat.numel() + 3) // 4, self.batch_size
+            if self._step_dev is not None:
+                C.uniform_(flat, self.seed, 0, 0.0, 1.0, self._step_dev, per_x)
+                C.randint_(self._y, self.num_classes, self.seed, 0, self._step_dev, per_y)
+                self._step_dev.add_(1)
+            else:
+                C.uniform_(flat, self.seed, self.step * per_x, 0.0, 1.0)
+                C.randint_(self._y, self.num_classes, self.seed, self.step * per_y)
         else:
             self._x.copy_(torch.rand(self._x.shape, generator=self._cpu_gen).to(self.dtype))
             self._y.copy_(torch.randint(0, self.num_classes, self._y.shape, generator=self._cpu_gen))

@@ -66,8 +66,13 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
-        out = dnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        if self.downsample is None:
+            # identity block: conv1 forwards x as the identity so the two input gradients are
+            # summed inside conv1's dgrad GEMM (native path)
+            out, identity = dnn.conv_bn_act_fork(x, self.conv1, self.bn1, relu=True)
+        else:
+            identity = self.downsample(x)
+            out = dnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
         out = dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True)
         return dnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=identity)
 

@@ -5,7 +5,7 @@ convs (plus their backward) run on the framework's own MFMA kernels instead of M
 
 * forward  ``Y = X W^T``   (``gemm_nt``, optionally emitting the BatchNorm column statistics of Y
   from the epilogue, so the following fused BN skips its statistics pass),
-* dgrad    ``dX = dY W``   (``gemm_nt`` with the tiny transposed weight),
+* dgrad    ``dX = dY W``   (``gemm_nt`` reading W k-major through transposing LDS reads),
 * wgrad    ``dW = dY^T X`` (``gemm_tn``, split-K over the N*H*W rows).
 
 Stride-2 1x1 convs (ResNet downsample) subsample the input first. Anything else (non-bf16 inputs,
@@ -63,7 +63,7 @@ class _Conv1x1(torch.autograd.Function):
         dy2 = _rows(dy)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx2, _ = C.gemm_nt(dy2, w2.t().contiguous(), False)
+            dx2, _ = C.gemm_nt(dy2, w2, False, None, True)
             n, cin, h, w = x.shape
             dxs = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
             if ctx.stride != 1:
@@ -77,6 +77,58 @@ class _Conv1x1(torch.autograd.Function):
             dw = C.gemm_tn(dy2, _rows(x), ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16)
                            else torch.float32, 1.0).view(ctx.wshape).to(ctx.wdtype)
         return dx, dw, None, None
+
+
+class _Conv1x1Fork(torch.autograd.Function):
+    """Stride-1 1x1 conv that also hands its input on as a second output (the block's identity
+    branch). Both gradients of ``x`` then arrive in one backward call, and the identity gradient
+    is added inside the dgrad GEMM's epilogue (``dX = dY W + d_identity``) instead of by a separate
+    elementwise kernel over the block-input tensor (the autograd sum of the two uses of ``x``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, want_stats: bool):
+        C = _ext.require()
+        ctx.set_materialize_grads(False)
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        w2 = weight.reshape(cout, cin).to(torch.bfloat16).contiguous()
+        y2, stats = C.gemm_nt(_rows(x), w2, want_stats)
+        y = y2.view(n, h, w, cout).permute(0, 3, 1, 2)
+        ctx.save_for_backward(x, w2)
+        ctx.wdtype = weight.dtype
+        ctx.wshape = weight.shape
+        if stats is not None:
+            ctx.mark_non_differentiable(stats)
+        return y, stats, x
+
+    @staticmethod
+    def backward(ctx, dy, _dstats, dident):
+        C = _ext.require()
+        x, w2 = ctx.saved_tensors
+        n, cin, h, w = x.shape
+        if dident is not None:
+            dident = dident.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
+        if dy is None:
+            return dident, None, None
+        dy = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
+        dy2 = _rows(dy)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx2, _ = C.gemm_nt(dy2, w2, False, None if dident is None else _rows(dident), True)
+            dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            dw = C.gemm_tn(dy2, _rows(x), ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16)
+                           else torch.float32, 1.0).view(ctx.wshape).to(ctx.wdtype)
+        return dx, dw, None
+
+
+def fork_supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    return supported(x, conv) and conv.stride in ((1, 1), 1)
+
+
+def conv1x1_fork(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
+    """Returns (y, stats-or-None, x_alias); use ``x_alias`` as the residual identity."""
+    return _Conv1x1Fork.apply(x, conv.weight, want_stats)
 
 
 def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):

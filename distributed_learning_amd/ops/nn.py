@@ -100,3 +100,21 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
                 stats = None
             return fused_bn_act(y, bn, relu, residual, stats)
     return bn_act(conv(x), bn, relu, residual)
+
+
+def conv_bn_act_fork(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool = True):
+    """``(act(BN(conv(x))), identity)`` for a residual block whose identity branch is ``x`` itself.
+
+    On the native path the returned identity is an alias of ``x`` produced by the same autograd
+    node as the conv, so the block-input gradient (conv dgrad + identity gradient) is summed in
+    the dgrad GEMM epilogue (ops/conv.py::_Conv1x1Fork). Otherwise ``identity is x``."""
+    if _BACKEND == "native" and _NATIVE_CONV and x.is_cuda:
+        from . import conv as nconv
+        from .bn_act import fused_bn_act, supported as bn_supported
+
+        if nconv.fork_supported(x, conv):
+            y, stats, ident = nconv.conv1x1_fork(x, conv, want_stats=bn.training)
+            if stats is not None and not bn_supported(y, bn, None):
+                stats = None
+            return fused_bn_act(y, bn, relu, None, stats), ident
+    return conv_bn_act(x, conv, bn, relu), x

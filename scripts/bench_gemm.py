@@ -51,6 +51,7 @@ for M, Cin, Cout in shapes:
     r["fwd_torch_mm_ms"] = timeit(lambda: X @ W.t())
     r["fwd_miopen_conv_ms"] = timeit(lambda: torch.nn.functional.conv2d(x4, w4))
     r["dgrad_native_ms"] = timeit(lambda: C.gemm_nt(dY, Wt, False))
+    r["dgrad_native_kmajor_ms"] = timeit(lambda: C.gemm_nt(dY, W, False, None, True))
     r["dgrad_torch_mm_ms"] = timeit(lambda: dY @ W)
     r["wgrad_native_ms"] = timeit(lambda: C.gemm_tn(dY, X, torch.float32, 1.0))
     r["wgrad_torch_mm_ms"] = timeit(lambda: dY.t() @ X)

@@ -56,3 +56,35 @@ def test_conv_bn_act_native_vs_torch(cuda):
     torch.testing.assert_close(y.float(), yr, rtol=3e-2, atol=5e-2)
     torch.testing.assert_close(bn.running_mean, bn2.running_mean, rtol=1e-2, atol=1e-3)
     torch.testing.assert_close(bn.running_var, bn2.running_var, rtol=1e-2, atol=1e-3)
+
+
+def test_conv1x1_fork_sums_identity_gradient(cuda):
+    """_Conv1x1Fork: dx = dgrad + d_identity fused in the GEMM epilogue equals the autograd sum of
+    the two uses of x (bitwise: both round the GEMM result to bf16 before the bf16 add)."""
+    from distributed_learning_amd.ops.conv import conv1x1, conv1x1_fork
+
+    torch.manual_seed(0)
+    conv = nn.Conv2d(256, 64, 1, bias=False).to(cuda).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 256, 28, 28, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(4, 64, 28, 28, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gi = torch.randn(4, 256, 28, 28, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    x1 = x.clone().requires_grad_(True)
+    y1, _, ident = conv1x1_fork(x1, conv)
+    assert ident.data_ptr() == x1.data_ptr()
+    torch.autograd.backward([y1, ident], [g, gi])
+    dw1 = conv.weight.grad.clone()
+    conv.weight.grad = None
+
+    x2 = x.clone().requires_grad_(True)
+    y2, _ = conv1x1(x2, conv)
+    torch.autograd.backward([y2, x2 * 1], [g, gi])
+    assert torch.equal(y1, y2)
+    assert torch.equal(x1.grad, x2.grad)
+    assert torch.equal(dw1, conv.weight.grad)
+
+    # identity gradient only (conv output unused) and conv gradient only
+    x3 = x.clone().requires_grad_(True)
+    _, _, ident = conv1x1_fork(x3, conv)
+    ident.backward(gi)
+    assert torch.equal(x3.grad, gi)

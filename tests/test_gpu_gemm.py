@@ -50,3 +50,23 @@ def test_gemm_tn(cuda, K, Mo, No):
     torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3 * K ** 0.5)
     outb = C.gemm_tn(A, B, torch.bfloat16, 1.0)
     torch.testing.assert_close(outb.float(), ref * 2, rtol=1e-2, atol=2e-3 * K ** 0.5)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 64, 256), (777, 136, 72), (12544, 512, 2048), (130, 8, 8),
+                                   (50176, 256, 1024)])
+def test_gemm_nt_kmajor_b_and_addend(cuda, M, N, K):
+    """b_kmajor: C = A @ B with B [K, N] (dgrad with the weight as stored); the fused addend gives
+    bf16(bf16(A @ B) + D) exactly like the unfused add."""
+    C = _C()
+    torch.manual_seed(0)
+    A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    B = torch.randn(K, N, device=cuda).to(torch.bfloat16)
+    D = torch.randn(M, N, device=cuda).to(torch.bfloat16)
+    out, _ = C.gemm_nt(A, B, False, None, True)
+    ref = A.float() @ B.float()
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2 * (K ** 0.5))
+    # same accumulation order as the n-major form -> bitwise equal
+    out_t, _ = C.gemm_nt(A, B.t().contiguous(), False)
+    assert torch.equal(out, out_t)
+    out_d, _ = C.gemm_nt(A, B, False, D, True)
+    assert torch.equal(out_d, out + D)

@@ -1,0 +1,76 @@
+"""Whole-step HIP graph capture (parallel/graphs.py) reproduces eager training (gpu)."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(graphed: bool, steps: int, world1):
+    from distributed_learning_amd.data import SyntheticBatches
+    from distributed_learning_amd.models import resnet18
+    from distributed_learning_amd.ops import nn as dnn
+    from distributed_learning_amd.ops.loss import cross_entropy
+    from distributed_learning_amd.ops.optim import FusedSGD
+    from distributed_learning_amd.parallel import PipelinedFusedDP, make_reducer
+    from distributed_learning_amd.parallel.graphs import GraphedStep
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda:0")
+    m = resnet18(10).to(dev).to(memory_format=torch.channels_last)
+    dnn.bf16_weights(m)
+    w = PipelinedFusedDP(m, make_reducer("immediate", "builtin", native=True), 1 << 20, dev, broadcast=False)
+    opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, master_weights=True)
+    data = SyntheticBatches(16, (3, 32, 32), 10, dev, dtype=torch.bfloat16, channels_last=True, device_step=True)
+
+    def step():
+        x, y = data.next()
+        opt.zero_grad(set_to_none=True)
+        loss = cross_entropy(w(x), y)
+        loss.backward()
+        w.sync_gradients()
+        opt.step()
+        return loss.detach()
+
+    runner = GraphedStep(step, warmup=2, device=dev) if graphed else step
+    losses = []
+    n = steps if graphed else steps + 2  # the graph runner does 2 eager warmup steps first
+    for _ in range(n):
+        losses.append(float(runner()))
+    if graphed:
+        assert runner.captured
+    w.cleanup()
+    return losses, [p.detach().float().clone() for p in m.parameters()]
+
+
+@pytest.fixture(scope="module")
+def world1(cuda):
+    from distributed_learning_amd.parallel import context as ctx
+
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    os.environ.setdefault("LOCAL_RANK", "0")
+    c = ctx.init(backend="nccl")
+    yield c
+    ctx.shutdown()
+
+
+def test_graphed_step_matches_eager(world1):
+    from distributed_learning_amd.ops import nn as dnn
+
+    det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    dnn.set_backend("native")
+    dnn.set_native_conv(True)
+    try:
+        le, pe = _run(False, 5, world1)
+        lg, pg = _run(True, 5, world1)
+    finally:
+        dnn.set_native_conv(False)
+        dnn.set_backend("torch")
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
+    # eager: 7 steps; graphed: 2 eager warmups + 5 replays -> replays are steps 3..7
+    assert lg == pytest.approx(le[2:], rel=1e-5, abs=1e-5)
+    for a, b in zip(pe, pg):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
