@@ -122,5 +122,22 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
 int gemm_tn_splits(int Mo, int No, int K);
 void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, float* partial, int splits, int Mo, int No,
                     int K, void* out, int out_dtype, float scale, bool accumulate, hipStream_t stream);
+// out[n] (= scale * sum_s partial[s][n] [+ out]), fp32 or bf16 out.
+void launch_splitk_reduce(const float* partial, int splits, int64_t n, void* out, int out_dtype, float scale,
+                          bool accumulate, hipStream_t stream);
+
+// ---- implicit-GEMM 3x3 convolutions, pad 1, NHWC bf16 (conv.hip) -----------------------------
+// x [N,H,W,Cin], w [Cout,3,3,Cin], y [N,OH,OW,Cout]; Cin % 64 == 0, Cout % 64 == 0, pixels < 2^24.
+// fwd: stride 1 or 2, optional BN statistics partials stats[ceil(P/128)][Cout][2].
+// dgrad: stride 1 only, dx [N,H,W,Cin] (+ optional addend). wgrad: stride 1 or 2, split-K fp32
+// partials (splits * Cout * 9*Cin floats) reduced into dw [Cout][9*Cin] (fp32 or bf16).
+int conv3x3_row_block();
+void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout, int stride,
+                        float* stats, hipStream_t stream);
+void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
+                          const void* addend, hipStream_t stream);
+int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int stride);
+void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int splits, void* dw, int out_dtype, int N,
+                          int H, int W, int Cin, int Cout, int stride, hipStream_t stream);
 
 }  // namespace dla

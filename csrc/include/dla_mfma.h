@@ -1,0 +1,288 @@
+// Shared bf16 MFMA GEMM machinery (gfx950): operand loaders, LDS images, the register-staged main
+// loop and the epilogues. gemm.hip (1x1 convolutions / plain GEMMs) and conv.hip (implicit-GEMM
+// 3x3 convolutions) instantiate the same main loop with different global-memory loaders, so every
+// conv variant inherits the tuned tile schedule instead of re-implementing it.
+//
+// Block = 256 threads = 2x2 waves; a block computes a BM x BN tile of C with
+// v_mfma_f32_16x16x32_bf16 (fp32 accumulate), kBK = 64 deep K steps staged through LDS with the
+// next step's global loads in flight during the current step's MFMAs (T14 register staging).
+// Operand tiles live in LDS either
+//   * row-major  [W][kBK + 8]  (operand is K-contiguous in memory; fragments by ds_read_b128,
+//                               rows padded by 16 B -> conflict-free), or
+//   * k-major    [kBK][W]      (operand is K-strided; fragments by ds_read_b64_tr_b16 through the
+//                               XOR-swizzled tr_off image -> conflict-free).
+// C/D fragment map of 16x16x32: col = lane & 15, row = 4 * (lane >> 4) + reg.
+#pragma once
+
+#include "dla_common.h"
+
+namespace dla {
+namespace mm {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int kBK = 64;
+
+__device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ ushort8_t zero8() { return ushort8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
+
+// k-major image (rows = k, W = 64 or 128 columns, unpadded rows). A 32-lane half of a transposed
+// 16x16x32-operand read touches rows {r..r+3, r+8..r+11} x 4 consecutive 8-byte chunks; with plain
+// rows those 8 row-blocks share banks (2-way or worse for any constant pitch). XOR-ing the chunk
+// index with a row-dependent multiple of 4 gives them disjoint 8-bank windows, keeps every 32-byte
+// chunk group and every 16-byte store contiguous; stores and reads share this function.
+template <int W>
+__device__ __forceinline__ int tr_off(int row, int col) {  // element offset of (row, col), col % 4 == 0
+  static_assert(W == 64 || W == 128, "tr image width");
+  int sw;
+  if constexpr (W == 128)
+    sw = 4 * ((row & 3) | (((row >> 3) & 1) << 2));  // 32 chunks/row (256 B = 64 banks)
+  else
+    sw = 4 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));  // 16 chunks/row; row parity adds 32 banks
+  return row * W + (((col >> 2) ^ sw) << 2);
+}
+
+__device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* lo_ptr, const bf16_t* hi_ptr) {
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(lo_ptr));
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(hi_ptr));
+  const short v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return *reinterpret_cast<const bf16x8_t*>(v);
+}
+
+template <int W>
+struct TileGeom {
+  static constexpr int CH = W * kBK / 8 / kThreads;  // 16-byte chunks per thread per k-step
+  static_assert(CH >= 1, "tile too small for 256 threads");
+  static constexpr int KPR = W / 8;  // k-major: chunks per k-row
+  // row-major: chunk c -> (row c >> 3, k (c & 7) * 8); k-major: chunk c -> (k c / KPR, col (c % KPR) * 8)
+  static constexpr int kRowElems = W * (kBK + 8);
+  static constexpr int kKElems = kBK * W;
+};
+
+// ---- loaders ------------------------------------------------------------------------------------
+// A loader exposes kKMajor and  ushort8_t load(int i, int k0) const  returning the 8 elements of
+// chunk slot i (chunk id c = tid + i * 256) for the k-step starting at k0, zeros out of range.
+
+// Row-major matrix [rows][K] (K contiguous): A of gemm_nt, B of gemm_nt (weights [N][K]).
+template <int W>
+struct RowLoader {
+  static constexpr bool kKMajor = false;
+  const bf16_t* p;
+  int64_t ld;
+  int64_t row0, rows;
+  int K;
+  __device__ ushort8_t load(int i, int k0) const {
+    const int c = threadIdx.x + i * kThreads, r = c >> 3, kc = (c & 7) * 8;
+    const int64_t gr = row0 + r;
+    return (gr < rows && k0 + kc < K) ? *reinterpret_cast<const ushort8_t*>(p + gr * ld + k0 + kc) : zero8();
+  }
+};
+
+// k-major matrix [K][cols] (cols contiguous): gemm_tn operands, dgrad weights as stored.
+template <int W>
+struct KLoader {
+  static constexpr bool kKMajor = true;
+  const bf16_t* p;
+  int64_t ld;
+  int col0, cols;
+  int kend;
+  __device__ ushort8_t load(int i, int k0) const {
+    const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR, nc = (c % TileGeom<W>::KPR) * 8;
+    const int gk = k0 + kr, gc = col0 + nc;
+    return (gk < kend && gc < cols) ? *reinterpret_cast<const ushort8_t*>(p + (int64_t)gk * ld + gc) : zero8();
+  }
+};
+
+// ---- main loop -----------------------------------------------------------------------------------
+template <int BM, int BN>
+struct Acc {
+  static constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  f32x4_t v[TM][TN];
+  __device__ void zero() {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) v[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+};
+
+template <int BM, int BN, class LA, class LB>
+__host__ __device__ constexpr size_t mainloop_lds_bytes() {
+  return ((LA::kKMajor ? (size_t)kBK * BM : (size_t)BM * (kBK + 8)) +
+          (LB::kKMajor ? (size_t)kBK * BN : (size_t)BN * (kBK + 8))) * sizeof(bf16_t);
+}
+
+template <int W, class L>
+__device__ __forceinline__ void tile_store(bf16_t* s, const ushort8_t (&r)[TileGeom<W>::CH]) {
+#pragma unroll
+  for (int i = 0; i < TileGeom<W>::CH; ++i) {
+    const int c = threadIdx.x + i * kThreads;
+    if constexpr (L::kKMajor)
+      *reinterpret_cast<ushort8_t*>(s + tr_off<W>(c / TileGeom<W>::KPR, (c % TileGeom<W>::KPR) * 8)) = r[i];
+    else
+      *reinterpret_cast<ushort8_t*>(s + (c >> 3) * (kBK + 8) + (c & 7) * 8) = r[i];
+  }
+}
+
+// 16 x 32 operand fragment for MFMA rows/cols [r0, r0 + 16) at k offset kk*32.
+template <int W, class L>
+__device__ __forceinline__ bf16x8_t tile_frag(const bf16_t* s, int r0, int kk) {
+  const int lane = threadIdx.x & 63;
+  if constexpr (L::kKMajor) {
+    // lane 4q+p of 16-lane group g reads k-row 8g+q (and +4), columns r0+4p..+3 (T10)
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int kr = kk * 32 + 8 * g + q, cn = r0 + 4 * p;
+    return tr_frag(s + tr_off<W>(kr, cn), s + tr_off<W>(kr + 4, cn));
+  } else {
+    return *reinterpret_cast<const bf16x8_t*>(s + (r0 + (lane & 15)) * (kBK + 8) + kk * 32 + 8 * (lane >> 4));
+  }
+}
+
+// acc += A[BM rows, k in [kbeg, kend)] * B[BN cols, same k]^T
+template <int BM, int BN, class LA, class LB>
+__device__ __forceinline__ void mainloop(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN>& acc,
+                                         char* smem) {
+  using GA = TileGeom<BM>;
+  using GB = TileGeom<BN>;
+  constexpr int WM = Acc<BM, BN>::WM, WN = Acc<BM, BN>::WN, TM = Acc<BM, BN>::TM, TN = Acc<BM, BN>::TN;
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Bs = As + (LA::kKMajor ? GA::kKElems : GA::kRowElems);
+  const int wid = threadIdx.x >> 6, wr = wid >> 1, wc = wid & 1;
+  ushort8_t ra[GA::CH], rb[GB::CH];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < GA::CH; ++i) ra[i] = la.load(i, k0);
+#pragma unroll
+    for (int i = 0; i < GB::CH; ++i) rb[i] = lb.load(i, k0);
+  };
+  const int nk = (kend - kbeg + kBK - 1) / kBK;
+  if (nk <= 0) return;
+  gload(kbeg);
+  tile_store<BM, LA>(As, ra);
+  tile_store<BN, LB>(Bs, rb);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) gload(kbeg + (t + 1) * kBK);  // next tile in flight during this tile's MFMAs
+#pragma unroll
+    for (int kk = 0; kk < kBK / 32; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = tile_frag<BM, LA>(As, wr * WM + i * 16, kk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = tile_frag<BN, LB>(Bs, wc * WN + j * 16, kk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma16(af[i], bfr[j], acc.v[i][j]);
+    }
+    __syncthreads();
+    if (t + 1 < nk) {
+      tile_store<BM, LA>(As, ra);
+      tile_store<BN, LB>(Bs, rb);
+      __syncthreads();
+    }
+  }
+}
+
+// ---- epilogues -------------------------------------------------------------------------------
+template <int BM, int BN, bool kStats>
+__host__ __device__ constexpr size_t epilogue_lds_bytes() {
+  return (size_t)BM * (BN + 8) * sizeof(bf16_t) + (kStats ? (size_t)4 * BN * sizeof(float) : 0);
+}
+
+// bf16 C tile -> LDS -> coalesced 16-byte row stores, optional fused addend D (C = bf16(bf16(acc) + D),
+// exactly the unfused bf16 add) and optional per-column (sum, sumsq) of the stored values written
+// as the row-block partial stats[bm][N][2] (BatchNorm statistics of the output, no atomics).
+template <int BM, int BN, bool kStats>
+__device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __restrict__ C, int64_t ldc, int64_t M,
+                                              int N, int64_t row0, int col0, int bm, float* __restrict__ stats,
+                                              const bf16_t* __restrict__ D, int64_t ldd, char* smem) {
+  constexpr int WM = Acc<BM, BN>::WM, WN = Acc<BM, BN>::WN, TM = Acc<BM, BN>::TM, TN = Acc<BM, BN>::TN;
+  constexpr int LDS_C = BN + 8;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
+  bf16_t* Cs = reinterpret_cast<bf16_t*>(smem);
+  // statistics from the accumulator registers: a lane owns one column of each 16x16 tile and 4 of
+  // its rows; the 4 lane groups sharing a column combine by xor-shuffles, the 2 M-waves via LDS
+  float cs[TN], cq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) cs[j] = cq[j] = 0.f;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wr * WM + i * 16 + (lane >> 4) * 4 + r;
+        const int n = wc * WN + j * 16 + fr;
+        const bf16_t h = f32_to_bf16(acc.v[i][j][r]);
+        Cs[m * LDS_C + n] = h;
+        if constexpr (kStats) {
+          const float v = (row0 + m < M) ? bf16_to_f32(h) : 0.f;  // statistics of the stored values
+          cs[j] += v;
+          cq[j] = fmaf(v, v, cq[j]);
+        }
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int c = tid; c < BM * CPR; c += kThreads) {
+    const int r = c / CPR, cc = (c % CPR) * 8;
+    const int64_t gm = row0 + r;
+    const int gn = col0 + cc;
+    if (gm < M && gn < N) {
+      ushort8_t v = *reinterpret_cast<ushort8_t*>(Cs + r * LDS_C + cc);
+      if (D) {
+        const ushort8_t d = *reinterpret_cast<const ushort8_t*>(D + gm * ldd + gn);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(d[j]));
+      }
+      *reinterpret_cast<ushort8_t*>(C + gm * ldc + gn) = v;
+    }
+  }
+  if constexpr (kStats) {
+    float* red = reinterpret_cast<float*>(smem + BM * LDS_C * sizeof(bf16_t));  // [2 wr][BN][2]
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      cs[j] += __shfl_xor(cs[j], 16, kWave);
+      cq[j] += __shfl_xor(cq[j], 16, kWave);
+      cs[j] += __shfl_xor(cs[j], 32, kWave);
+      cq[j] += __shfl_xor(cq[j], 32, kWave);
+      if (lane < 16) {
+        const int n = wc * WN + j * 16 + fr;
+        red[(wr * BN + n) * 2 + 0] = cs[j];
+        red[(wr * BN + n) * 2 + 1] = cq[j];
+      }
+    }
+    __syncthreads();
+    if (tid < BN && col0 + tid < N) {
+      stats[((int64_t)bm * N + col0 + tid) * 2 + 0] = red[tid * 2 + 0] + red[(BN + tid) * 2 + 0];
+      stats[((int64_t)bm * N + col0 + tid) * 2 + 1] = red[tid * 2 + 1] + red[(BN + tid) * 2 + 1];
+    }
+  }
+}
+
+// fp32 split-K partial slab P[Mo][No] (row m = M-side index, col n = N-side index)
+template <int BM, int BN>
+__device__ __forceinline__ void epilogue_f32(const Acc<BM, BN>& acc, float* __restrict__ P, int Mo, int No, int m0,
+                                             int n0) {
+  constexpr int WM = Acc<BM, BN>::WM, WN = Acc<BM, BN>::WN, TM = Acc<BM, BN>::TM, TN = Acc<BM, BN>::TN;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * WM + i * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wc * WN + j * 16 + fr;
+        if (m < Mo && n < No) P[(int64_t)m * No + n] = acc.v[i][j][r];
+      }
+}
+
+}  // namespace mm
+}  // namespace dla

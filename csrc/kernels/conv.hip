@@ -1,0 +1,300 @@
+// Implicit-GEMM 3x3 convolutions, NHWC (channels_last) bf16, on the shared MFMA main loop.
+//
+// ResNet-50 spends ~45% of its FLOPs in 3x3 convolutions (the reference leaves them
+// to cuDNN); stock PyTorch runs them through MIOpen, whose backward-weights path also launches
+// zero-fill and cast kernels around every call. Here all three passes are GEMMs whose operand
+// tiles are gathered straight from the activation tensors (no im2col buffer):
+//
+//   forward  Y[p, co]          = sum_{t, ci} X[src(p, t), ci] * W[co, t, ci]      M = P, N = Cout, K = 9*Cin
+//   dgrad    dX[p, ci]         = sum_{t, co} dY[src'(p, t), co] * W[co, t, ci]    M = P, N = Cin,  K = 9*Cout
+//   wgrad    dW[co, (t, ci)]   = sum_p dY[p, co] * X[src(p, t), ci]               split-K over P
+//
+// with p an output pixel (n, oh, ow), t = (kh, kw), src(p, t) = (n, oh*s - 1 + kh, ow*s - 1 + kw)
+// and src'(p, t) = (n, oh + 1 - kh, ow + 1 - kw) (stride-1 transposed conv). Out-of-image taps load
+// zeros (the padding). W is the channels_last weight [Cout][3][3][Cin] = [Cout][9*Cin], so forward
+// reads it K-contiguous (row-major tile), dgrad reads it k-major per tap (transposed LDS reads),
+// and wgrad writes exactly that layout. A 64-deep K step never straddles a tap (Cin, Cout % 64 == 0),
+// so the tap of a k-step is a scalar and each thread's gather address is one add away.
+// The forward epilogue can emit the BatchNorm statistics of Y (as the 1x1 GEMMs do).
+#include "dla_common.h"
+#include "dla_kernels.h"
+#include "dla_mfma.h"
+
+#include <algorithm>
+
+namespace dla {
+
+using namespace mm;
+
+// n / d for n < 2^24, d < 2^16: floor(n * ceil(2^40 / d) / 2^40), 4 VALU ops.
+struct FastDiv {
+  uint32_t d, m_lo, m_hi;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+  const uint64_t m = ((1ull << 40) + d - 1) / d;
+  return FastDiv{d, (uint32_t)m, (uint32_t)(m >> 32)};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m_lo) + n * f.m_hi) >> 8;
+}
+
+struct ConvGeom {
+  int N, H, W, Cin;  // input image (NHWC)
+  int OH, OW, Cout;  // output image
+  int stride;
+  FastDiv fOW, fOH;  // divisors for output-pixel decode
+};
+
+// A operand of forward / dgrad: row = output pixel of this GEMM, K = (tap, channel) with the channel
+// fastest. kFlip: dgrad (source = o + 1 - k), otherwise forward (source = o*s - 1 + k).
+template <int W, bool kFlip>
+struct Im2colRowLoader {
+  static constexpr bool kKMajor = false;
+  static constexpr int CH = TileGeom<W>::CH;
+  const bf16_t* x;
+  int H, Wd, C;  // source image height, width, channels
+  int stride;
+  int32_t pbase[CH];  // n * H * Wd of each slot's pixel, -1 when the pixel is past the end
+  int ih0[CH], iw0[CH];
+  __device__ void init(const ConvGeom& g, int64_t row0, int64_t P, int oh_dim, int ow_dim, const FastDiv& fw,
+                       const FastDiv& fh) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + i * kThreads, r = c >> 3;
+      const int64_t p = row0 + r;
+      if (p < P) {
+        const uint32_t q = fdiv((uint32_t)p, fw);
+        const int ow = (int)p - (int)q * ow_dim;
+        const uint32_t n = fdiv(q, fh);
+        const int oh = (int)q - (int)n * oh_dim;
+        pbase[i] = (int32_t)n * H * Wd;
+        ih0[i] = kFlip ? oh + 1 : oh * stride - 1;
+        iw0[i] = kFlip ? ow + 1 : ow * stride - 1;
+      } else {
+        pbase[i] = -1;
+        ih0[i] = iw0[i] = 0;
+      }
+    }
+    (void)g;
+  }
+  __device__ ushort8_t load(int i, int k0) const {
+    const int tap = k0 / C;  // uniform across the block
+    const int ci = k0 - tap * C + (threadIdx.x & 7) * 8;
+    const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+    const int ih = kFlip ? ih0[i] - kh : ih0[i] + kh;
+    const int iw = kFlip ? iw0[i] - kw : iw0[i] + kw;
+    if (pbase[i] < 0 || tap >= 9 || (unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)Wd) return zero8();
+    return *reinterpret_cast<const ushort8_t*>(x + ((int64_t)pbase[i] + ih * Wd + iw) * C + ci);
+  }
+};
+
+// B operand of dgrad: k = (tap, co) rows, n = ci columns, element W[co][tap][ci] (k-major per tap).
+template <int W>
+struct WeightTapKLoader {
+  static constexpr bool kKMajor = true;
+  const bf16_t* w;
+  int Cout, Cin, col0;
+  __device__ ushort8_t load(int i, int k0) const {
+    const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR, nc = (c % TileGeom<W>::KPR) * 8;
+    const int tap = k0 / Cout;  // uniform
+    const int co = k0 - tap * Cout + kr, ci = col0 + nc;
+    if (tap >= 9 || ci >= Cin) return zero8();
+    return *reinterpret_cast<const ushort8_t*>(w + ((int64_t)co * 9 + tap) * Cin + ci);
+  }
+};
+
+// B operand of wgrad: k = output pixel rows, n = (tap, ci) columns, element X[src(p, tap)][ci].
+template <int W>
+struct Im2colKLoader {
+  static constexpr bool kKMajor = true;
+  static constexpr int CH = TileGeom<W>::CH;
+  const bf16_t* x;
+  ConvGeom g;
+  int kend;
+  int kh[CH], kw[CH], ci[CH];  // per slot: fixed column -> (tap, channel); kh = -100 if out of range
+  __device__ void init(int col0) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + i * kThreads, nc = col0 + (c % TileGeom<W>::KPR) * 8;
+      const int tap = nc / g.Cin;
+      ci[i] = nc - tap * g.Cin;
+      kh[i] = tap < 9 ? tap / 3 : -100;
+      kw[i] = tap - 3 * (tap / 3);
+    }
+  }
+  __device__ ushort8_t load(int i, int k0) const {
+    const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR;
+    const int p = k0 + kr;
+    if (p >= kend || kh[i] < 0) return zero8();
+    const uint32_t q = fdiv((uint32_t)p, g.fOW);
+    const int ow = p - (int)q * g.OW;
+    const uint32_t n = fdiv(q, g.fOH);
+    const int oh = (int)q - (int)n * g.OH;
+    const int ih = oh * g.stride - 1 + kh[i], iw = ow * g.stride - 1 + kw[i];
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return zero8();
+    return *reinterpret_cast<const ushort8_t*>(x + (((int64_t)n * g.H + ih) * g.W + iw) * g.Cin + ci[i]);
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, bool kStats>
+__global__ __launch_bounds__(kThreads, 2) void conv3x3_fwd_kernel(const bf16_t* __restrict__ x,
+                                                                  const bf16_t* __restrict__ w,
+                                                                  bf16_t* __restrict__ y, ConvGeom g,
+                                                                  float* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int64_t P = (int64_t)g.N * g.OH * g.OW;
+  const int nbn = (g.Cout + BN - 1) / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int bm = tile / nbn, bn = tile % nbn;
+  const int64_t row0 = (int64_t)bm * BM;
+  const int col0 = bn * BN;
+  const int K = 9 * g.Cin;
+  Im2colRowLoader<BM, false> la{x, g.H, g.W, g.Cin, g.stride};
+  la.init(g, row0, P, g.OH, g.OW, g.fOW, g.fOH);
+  const RowLoader<BN> lb{w, K, (int64_t)col0, g.Cout, K};
+  Acc<BM, BN> acc;
+  acc.zero();
+  mainloop<BM, BN>(la, lb, 0, K, acc, smem_raw);
+  epilogue_bf16<BM, BN, kStats>(acc, y, g.Cout, P, g.Cout, row0, col0, bm, stats, nullptr, 0, smem_raw);
+}
+
+// stride-1 dgrad: dX (the GEMM's M = input pixels, N = Cin), A = dY gathered with flipped taps
+template <int BM, int BN>
+__global__ __launch_bounds__(kThreads, 2) void conv3x3_dgrad_kernel(const bf16_t* __restrict__ dy,
+                                                                    const bf16_t* __restrict__ w,
+                                                                    bf16_t* __restrict__ dx, ConvGeom g,
+                                                                    const bf16_t* __restrict__ addend) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int64_t P = (int64_t)g.N * g.H * g.W;  // stride 1: OH = H, OW = W
+  const int nbn = (g.Cin + BN - 1) / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int bm = tile / nbn, bn = tile % nbn;
+  const int64_t row0 = (int64_t)bm * BM;
+  const int col0 = bn * BN;
+  const int K = 9 * g.Cout;
+  Im2colRowLoader<BM, true> la{dy, g.OH, g.OW, g.Cout, 1};
+  la.init(g, row0, P, g.H, g.W, g.fOW, g.fOH);  // stride 1: the same divisors (OW == W, OH == H)
+  const WeightTapKLoader<BN> lb{w, g.Cout, g.Cin, col0};
+  Acc<BM, BN> acc;
+  acc.zero();
+  mainloop<BM, BN>(la, lb, 0, K, acc, smem_raw);
+  epilogue_bf16<BM, BN, false>(acc, dx, g.Cin, P, g.Cin, row0, col0, bm, nullptr, addend, g.Cin, smem_raw);
+}
+
+// wgrad partial slabs P[split][Cout][9*Cin]
+template <int BM, int BN>
+__global__ __launch_bounds__(kThreads, 2) void conv3x3_wgrad_kernel(const bf16_t* __restrict__ dy,
+                                                                    const bf16_t* __restrict__ x, ConvGeom g,
+                                                                    float* __restrict__ part, int k_per_split) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int P = g.N * g.OH * g.OW;
+  const int Mo = g.Cout, No = 9 * g.Cin;
+  const int nbn = (No + BN - 1) / BN;
+  const int bm = blockIdx.x / nbn, bn = blockIdx.x % nbn;
+  const int kbeg = blockIdx.y * k_per_split;
+  const int kend = min(P, kbeg + k_per_split);
+  const int m0 = bm * BM, n0 = bn * BN;
+  const KLoader<BM> la{dy, g.Cout, m0, Mo, kend};
+  Im2colKLoader<BN> lb{x, g, kend};
+  lb.init(n0);
+  Acc<BM, BN> acc;
+  acc.zero();
+  mainloop<BM, BN>(la, lb, kbeg, kend, acc, smem_raw);
+  epilogue_f32<BM, BN>(acc, part + (int64_t)blockIdx.y * Mo * No, Mo, No, m0, n0);
+}
+
+// ---------------------------------------------------------------------------------------------
+static ConvGeom make_geom(int N, int H, int W, int Cin, int Cout, int stride) {
+  ConvGeom g;
+  g.N = N;
+  g.H = H;
+  g.W = W;
+  g.Cin = Cin;
+  g.Cout = Cout;
+  g.stride = stride;
+  g.OH = (H + 2 - 3) / stride + 1;
+  g.OW = (W + 2 - 3) / stride + 1;
+  g.fOW = make_fastdiv((uint32_t)g.OW);
+  g.fOH = make_fastdiv((uint32_t)g.OH);
+  return g;
+}
+
+template <int BM, int BN, bool S>
+static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGeom& g, float* stats,
+                       hipStream_t stream) {
+  const int64_t P = (int64_t)g.N * g.OH * g.OW;
+  const int tiles = (int)((P + BM - 1) / BM) * ((g.Cout + BN - 1) / BN);
+  const size_t lds = std::max(mainloop_lds_bytes<BM, BN, Im2colRowLoader<BM, false>, RowLoader<BN>>(),
+                              epilogue_lds_bytes<BM, BN, S>());
+  hipLaunchKernelGGL((conv3x3_fwd_kernel<BM, BN, S>), dim3(tiles), dim3(kThreads), lds, stream, x, w, y, g, stats);
+}
+
+int conv3x3_row_block() { return 128; }
+
+void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout, int stride,
+                        float* stats, hipStream_t stream) {
+  const ConvGeom g = make_geom(N, H, W, Cin, Cout, stride);
+  const bf16_t* xp = (const bf16_t*)x;
+  const bf16_t* wp = (const bf16_t*)w;
+  bf16_t* yp = (bf16_t*)y;
+  if (Cout <= 64) {
+    if (stats) launch_fwd<128, 64, true>(xp, wp, yp, g, stats, stream);
+    else launch_fwd<128, 64, false>(xp, wp, yp, g, stats, stream);
+  } else {
+    if (stats) launch_fwd<128, 128, true>(xp, wp, yp, g, stats, stream);
+    else launch_fwd<128, 128, false>(xp, wp, yp, g, stats, stream);
+  }
+}
+
+template <int BM, int BN>
+static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const ConvGeom& g, const bf16_t* addend,
+                         hipStream_t stream) {
+  const int64_t P = (int64_t)g.N * g.H * g.W;
+  const int tiles = (int)((P + BM - 1) / BM) * ((g.Cin + BN - 1) / BN);
+  const size_t lds = std::max(mainloop_lds_bytes<BM, BN, Im2colRowLoader<BM, true>, WeightTapKLoader<BN>>(),
+                              epilogue_lds_bytes<BM, BN, false>());
+  hipLaunchKernelGGL((conv3x3_dgrad_kernel<BM, BN>), dim3(tiles), dim3(kThreads), lds, stream, dy, w, dx, g, addend);
+}
+
+void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
+                          const void* addend, hipStream_t stream) {
+  const ConvGeom g = make_geom(N, H, W, Cin, Cout, 1);
+  if (Cin <= 64)
+    launch_dgrad<128, 64>((const bf16_t*)dy, (const bf16_t*)w, (bf16_t*)dx, g, (const bf16_t*)addend, stream);
+  else
+    launch_dgrad<128, 128>((const bf16_t*)dy, (const bf16_t*)w, (bf16_t*)dx, g, (const bf16_t*)addend, stream);
+}
+
+int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int stride) {
+  const ConvGeom g = make_geom(N, H, W, Cin, Cout, stride);
+  const int P = g.N * g.OH * g.OW;
+  const int bm = Cout <= 64 ? 64 : 128;
+  const int tiles = ((Cout + bm - 1) / bm) * ((9 * Cin + 127) / 128);
+  const int splits = std::max(1, 512 / std::max(1, tiles));  // ~2 workgroups per CU
+  const int max_splits = std::max(1, P / (8 * kBK));          // >= 8 k-steps per split
+  return std::max(1, std::min(splits, max_splits));
+}
+
+void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int splits, void* dw, int out_dtype,
+                          int N, int H, int W, int Cin, int Cout, int stride, hipStream_t stream) {
+  const ConvGeom g = make_geom(N, H, W, Cin, Cout, stride);
+  const int P = g.N * g.OH * g.OW;
+  int kps = (P + splits - 1) / splits;
+  kps = (kps + kBK - 1) / kBK * kBK;
+  const int Mo = Cout, No = 9 * Cin;
+  if (Cout <= 64) {
+    const int tiles = ((Mo + 63) / 64) * ((No + 127) / 128);
+    const size_t lds = mainloop_lds_bytes<64, 128, KLoader<64>, Im2colKLoader<128>>();
+    hipLaunchKernelGGL((conv3x3_wgrad_kernel<64, 128>), dim3(tiles, splits), dim3(kThreads), lds, stream,
+                       (const bf16_t*)dy, (const bf16_t*)x, g, partial, kps);
+  } else {
+    const int tiles = ((Mo + 127) / 128) * ((No + 127) / 128);
+    const size_t lds = mainloop_lds_bytes<128, 128, KLoader<128>, Im2colKLoader<128>>();
+    hipLaunchKernelGGL((conv3x3_wgrad_kernel<128, 128>), dim3(tiles, splits), dim3(kThreads), lds, stream,
+                       (const bf16_t*)dy, (const bf16_t*)x, g, partial, kps);
+  }
+  launch_splitk_reduce(partial, splits, (int64_t)Mo * No, dw, out_dtype, 1.f, false, stream);
+}
+
+}  // namespace dla

@@ -203,7 +203,81 @@ at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor pos, int64_t H, int64_t W, int6
   return dx;
 }
 
+static void check_conv3(const at::Tensor& x, const at::Tensor& w) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3: x must be a bf16 channels_last 4-D GPU tensor");
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.scalar_type() == at::kBFloat16 && w.size(2) == 3 && w.size(3) == 3 &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3: w must be a bf16 channels_last [Cout, Cin, 3, 3] tensor");
+  TORCH_CHECK(w.size(1) == x.size(1), "conv3x3: channel mismatch");
+  TORCH_CHECK(x.size(1) % 64 == 0 && w.size(0) % 64 == 0, "conv3x3: Cin and Cout must be multiples of 64");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(w.data_ptr()) & 15) == 0,
+              "conv3x3: 16-byte aligned operands required");
+  TORCH_CHECK(x.numel() / x.size(1) < (1 << 24), "conv3x3: too many pixels for 24-bit index math");
+}
+
+// 3x3 / pad 1 convolution forward (stride 1 or 2). Returns (y, stats-or-undefined).
+std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, bool stats) {
+  check_conv3(x, w);
+  TORCH_CHECK(stride == 1 || stride == 2, "conv3x3: stride 1 or 2");
+  const int N = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Cout = (int)w.size(0);
+  const int OH = (H - 1) / (int)stride + 1, OW = (W - 1) / (int)stride + 1;
+  at::Tensor y = at::empty({N, Cout, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor S;
+  const int64_t P = (int64_t)N * OH * OW;
+  if (stats) S = at::empty({(P + conv3x3_row_block() - 1) / conv3x3_row_block(), Cout, 2}, x.options().dtype(at::kFloat));
+  launch_conv3x3_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), N, H, W, Cin, Cout, (int)stride,
+                     stats ? S.data_ptr<float>() : nullptr, current_stream(x));
+  return {y, S};
+}
+
+// stride-1 data gradient (+ optional fused addend, same shape as dx)
+at::Tensor conv3x3_dgrad(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> addend) {
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(1) == w.size(0), "conv3x3_dgrad: dy/w mismatch");
+  const int N = (int)dy.size(0), Cout = (int)w.size(0), Cin = (int)w.size(1), H = (int)dy.size(2), W = (int)dy.size(3);
+  at::Tensor dx = at::empty({N, Cin, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_conv3(dx, w);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0,
+              "conv3x3_dgrad: bf16 aligned dy");
+  const void* add = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    TORCH_CHECK(addend->sizes() == dx.sizes() && addend->scalar_type() == at::kBFloat16 &&
+                    addend->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv3x3_dgrad: addend must match dx");
+    add = addend->data_ptr();
+  }
+  launch_conv3x3_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, add, current_stream(dy));
+  return dx;
+}
+
+// weight gradient, returned as a channels_last [Cout, Cin, 3, 3] tensor of out_dtype
+at::Tensor conv3x3_wgrad(at::Tensor dy, at::Tensor x, int64_t stride, c10::ScalarType out_dtype) {
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 64 == 0,
+              "conv3x3_wgrad: x must be bf16 channels_last with Cin % 64 == 0");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.size(1) % 64 == 0, "conv3x3_wgrad: dy must be bf16, Cout % 64");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "conv3x3_wgrad: fp32/bf16 output");
+  TORCH_CHECK(x.numel() / x.size(1) < (1 << 24), "conv3x3_wgrad: too many pixels");
+  const int N = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Cout = (int)dy.size(1);
+  TORCH_CHECK(dy.size(2) == (H - 1) / stride + 1 && dy.size(3) == (W - 1) / stride + 1, "conv3x3_wgrad: dy shape");
+  const int splits = conv3x3_wgrad_splits(N, H, W, Cin, Cout, (int)stride);
+  at::Tensor part = at::empty({(int64_t)splits * Cout * 9 * Cin}, x.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({Cout, Cin, 3, 3}, x.options().dtype(out_dtype).memory_format(at::MemoryFormat::ChannelsLast));
+  launch_conv3x3_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), splits, dw.data_ptr(),
+                       out_dtype == at::kFloat ? kF32 : kBF16, N, H, W, Cin, Cout, (int)stride, current_stream(x));
+  return dw;
+}
+
 void bind_nn(pybind11::module& m) {
+  m.def("conv3x3_fwd", &conv3x3_fwd, "implicit-GEMM 3x3/pad-1 conv forward (NHWC bf16, MFMA)", pybind11::arg("x"),
+        pybind11::arg("w"), pybind11::arg("stride") = 1, pybind11::arg("stats") = false);
+  m.def("conv3x3_dgrad", &conv3x3_dgrad, "implicit-GEMM 3x3 conv data gradient (stride 1)", pybind11::arg("dy"),
+        pybind11::arg("w"), pybind11::arg("addend") = pybind11::none());
+  m.def("conv3x3_wgrad", &conv3x3_wgrad, "implicit-GEMM 3x3 conv weight gradient (split-K)", pybind11::arg("dy"),
+        pybind11::arg("x"), pybind11::arg("stride") = 1, pybind11::arg("out_dtype") = at::kFloat);
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC max pooling forward (+ argmax window positions)", pybind11::arg("x"),
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("ceil_mode") = false,
         pybind11::arg("need_pos") = true);

@@ -66,13 +66,11 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if self.downsample is None:
-            # identity block: conv1 forwards x as the identity so the two input gradients are
-            # summed inside conv1's dgrad GEMM (native path)
-            out, identity = dnn.conv_bn_act_fork(x, self.conv1, self.bn1, relu=True)
-        else:
-            identity = self.downsample(x)
-            out = dnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        # conv1 forwards x as a second output that feeds the identity branch (or the downsample conv),
+        # so the two gradients of the block input are summed inside conv1's dgrad GEMM epilogue
+        # instead of by an elementwise add (native path; a plain alias otherwise)
+        out, xa = dnn.conv_bn_act_fork(x, self.conv1, self.bn1, relu=True)
+        identity = xa if self.downsample is None else self.downsample(xa)
         out = dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True)
         return dnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=identity)
 

@@ -137,3 +137,67 @@ def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
         # odd spatial size with stride 2 (output ceil) — keep F.conv2d semantics exactly
         return F.conv2d(x, conv.weight.to(x.dtype), None, conv.stride), None
     return _Conv1x1.apply(x, conv.weight, conv.stride[0], want_stats)
+
+
+# ---------------------------------------------------------------------------------------------
+# 3x3 convolutions (csrc/kernels/conv.hip): implicit GEMMs gathered straight from NHWC tensors.
+# Per-pass engine choice from scripts/bench_conv.py at the ResNet-50 bs256 shapes on MI355X
+# (profiles/conv3x3_native_vs_miopen.md): the native weight gradient beats MIOpen's at every shape
+# (and drops MIOpen's zero-fill/cast kernels around it); the forward stays on MIOpen; the native
+# data gradient wins on the 64-channel 56x56 layer.
+# ---------------------------------------------------------------------------------------------
+CONV3_POLICY = {"fwd": "miopen", "dgrad_native_max_cin": 64, "wgrad": "native"}
+
+
+def supported3x3(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and conv.kernel_size == (3, 3)
+            and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and conv.stride in ((1, 1), (2, 2)) and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and x.numel() // x.shape[1] < (1 << 24))
+
+
+class _Conv3x3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, want_stats: bool):
+        C = _ext.require()
+        w = weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        stats = None
+        if CONV3_POLICY["fwd"] == "native" or want_stats:
+            y, stats = C.conv3x3_fwd(x, w, stride, want_stats)
+        else:
+            y = F.conv2d(x, w, None, stride, 1)
+        ctx.save_for_backward(x, w)
+        ctx.stride = stride
+        ctx.wdtype = weight.dtype
+        if stats is not None:
+            ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        C = _ext.require()
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if ctx.stride == 1 and x.shape[1] <= CONV3_POLICY["dgrad_native_max_cin"]:
+                dx = C.conv3x3_dgrad(dy, w)
+            else:
+                dx = torch.ops.aten.convolution_backward(dy, x, w, None, [ctx.stride] * 2, [1, 1], [1, 1], False,
+                                                         [0, 0], 1, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
+            if CONV3_POLICY["wgrad"] == "native":
+                dw = C.conv3x3_wgrad(dy, x, ctx.stride, odt)
+            else:
+                dw = torch.ops.aten.convolution_backward(dy, x, w, None, [ctx.stride] * 2, [1, 1], [1, 1], False,
+                                                         [0, 0], 1, [False, True, False])[1]
+            dw = dw.to(ctx.wdtype)
+        return dx, dw, None, None
+
+
+def conv3x3(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
+    """Returns (y, stats-or-None); stats are [row_blocks, Cout, 2] partial (sum, sumsq) when the
+    native forward ran."""
+    return _Conv3x3.apply(x, conv.weight, conv.stride[0], want_stats)

@@ -99,6 +99,12 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
             if stats is not None and not bn_supported(y, bn, residual):
                 stats = None
             return fused_bn_act(y, bn, relu, residual, stats)
+        if nconv.supported3x3(x, conv):
+            want = bn.training and nconv.CONV3_POLICY["fwd"] == "native"
+            y, stats = nconv.conv3x3(x, conv, want_stats=want)
+            if stats is not None and not bn_supported(y, bn, residual):
+                stats = None
+            return fused_bn_act(y, bn, relu, residual, stats)
     return bn_act(conv(x), bn, relu, residual)
 
 

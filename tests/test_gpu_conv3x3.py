@@ -1,0 +1,67 @@
+"""Implicit-GEMM 3x3 convolution kernels (csrc/kernels/conv.hip) vs fp32 PyTorch convs (gpu)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+
+
+def _C():
+    from distributed_learning_amd.ops import _ext
+
+    return _ext.require()
+
+
+def _rel(a, b):
+    return float((a.float() - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("N,Cin,H,W,Cout,stride", [
+    (2, 64, 56, 56, 64, 1), (2, 128, 28, 28, 128, 1), (1, 256, 14, 14, 256, 1), (4, 512, 7, 7, 512, 1),
+    (2, 128, 56, 56, 128, 2), (2, 64, 9, 13, 128, 1), (3, 128, 11, 7, 64, 2), (2, 256, 28, 28, 256, 2),
+])
+def test_conv3x3_fwd_dgrad_wgrad(cuda, N, Cin, H, W, Cout, stride):
+    C = _C()
+    torch.manual_seed(0)
+    x = torch.randn(N, Cin, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(Cout, Cin, 3, 3, device=cuda) * (2.0 / (9 * Cin)) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, stride, 1)
+    y, stats = C.conv3x3_fwd(x, w, stride, True)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=CL)
+    assert _rel(y, yr) < 1e-2
+    yf = y.float()
+    torch.testing.assert_close(stats.sum(0)[:, 0], yf.sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    torch.testing.assert_close(stats.sum(0)[:, 1], (yf * yf).sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    dy = torch.randn(yr.shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    yr.backward(dy.float())
+    dw = C.conv3x3_wgrad(dy, x, stride, torch.float32)
+    assert dw.shape == w.shape and dw.is_contiguous(memory_format=CL)
+    assert _rel(dw, wr.grad) < 1e-2, _rel(dw, wr.grad)
+    if stride == 1:
+        dx = C.conv3x3_dgrad(dy, w)
+        assert dx.shape == x.shape
+        assert _rel(dx, xr.grad) < 1e-2, _rel(dx, xr.grad)
+        add = torch.randn_like(x)
+        assert torch.equal(C.conv3x3_dgrad(dy, w, add), dx + add)
+
+
+def test_conv3x3_asymmetric_weights(cuda):
+    """One-hot weights per tap catch a flipped / transposed tap order in any of the passes."""
+    C = _C()
+    N, Cin, H, W, Cout = 1, 64, 6, 5, 64
+    x = torch.randn(N, Cin, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    for tap in range(9):
+        w = torch.zeros(Cout, Cin, 3, 3, device=cuda)
+        w[torch.arange(Cout), (torch.arange(Cout) * 7) % Cin, tap // 3, tap % 3] = 1.0
+        w = w.to(torch.bfloat16).contiguous(memory_format=CL)
+        y, _ = C.conv3x3_fwd(x, w, 1, False)
+        torch.testing.assert_close(y.float(), F.conv2d(x.float(), w.float(), None, 1, 1), rtol=0, atol=0)
+        dy = torch.randn(y.shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+        dx = C.conv3x3_dgrad(dy, w)
+        ref = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), 1, 1)
+        torch.testing.assert_close(dx.float(), ref, rtol=1e-2, atol=1e-2)
