@@ -91,7 +91,7 @@ void launch_xent_bwd(const void* logits, const int64_t* target, const float* ws,
 // ---- fused BatchNorm + residual + ReLU, NHWC (bn_act.hip) ------------------------------------
 // x/res/y/dy/dx/dres: [M, C] row-major (channels_last activations), C % 8 == 0, 16-byte aligned.
 // ws: 7*C floats (mean, invstd, scale, shift | k1, m1, k2); part: bn_partial_floats(M, C) floats.
-void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks);
+void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks);  // reduction passes: 1024
 void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int dtype, const float* gamma,
                    const float* beta, float eps, float momentum, float* running_mean, float* running_var, float* ws,
                    float* part, bool relu, bool training, hipStream_t stream, const float* ext_part = nullptr,
@@ -114,10 +114,17 @@ void launch_maxpool_bwd(const void* dy, const uint8_t* pos, void* dx, int N, int
 // C[M,N] = A[M,K] B[N,K]^T [+ addend[M,N]] (b_kmajor: B given as [K,N], i.e. C = A B); optional
 // per-column (sum, sumsq) partials stats[ceil(M/128)][N][2]. Requires K % 8 == 0, N % 8 == 0,
 // 16-byte aligned rows.
-int gemm_nt_row_block(int M, int N);
+// Tile configurations of the MFMA kernels (gemm_nt, conv3x3 fwd/dgrad). kTileAuto picks the
+// largest tile that still yields >= 1024 workgroups (4 per CU), so small-M layers fill the chip.
+enum TileCfg : int { kTileAuto = 0, kTile128x128 = 1, kTile128x64 = 2, kTile64x64 = 3 };
+int pick_tile(int64_t M, int N, int tile);
+inline int tile_bm(int cfg) { return cfg == kTile64x64 ? 64 : 128; }
+inline int tile_bn(int cfg) { return cfg == kTile128x128 ? 128 : 64; }
+// rows of BN-statistics partials ([rows][N][2]) a stats-producing launch writes (one per row tile)
+int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto);
 void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
                     float* stats, hipStream_t stream, const void* addend = nullptr, int64_t ld_addend = 0,
-                    bool b_kmajor = false);
+                    bool b_kmajor = false, int tile = kTileAuto);
 // out[Mo,No] (= scale * A^T B [+ out]) with A [K, lda>=Mo], B [K, ldb>=No]; partial: splits*Mo*No f32.
 int gemm_tn_splits(int Mo, int No, int K);
 void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, float* partial, int splits, int Mo, int No,
@@ -131,11 +138,11 @@ void launch_splitk_reduce(const float* partial, int splits, int64_t n, void* out
 // fwd: stride 1 or 2, optional BN statistics partials stats[ceil(P/128)][Cout][2].
 // dgrad: stride 1 only, dx [N,H,W,Cin] (+ optional addend). wgrad: stride 1 or 2, split-K fp32
 // partials (splits * Cout * 9*Cin floats) reduced into dw [Cout][9*Cin] (fp32 or bf16).
-int conv3x3_row_block();
+int conv3x3_stats_rows(int64_t P, int Cout, int tile = kTileAuto);
 void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout, int stride,
-                        float* stats, hipStream_t stream);
+                        float* stats, hipStream_t stream, int tile = kTileAuto);
 void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
-                          const void* addend, hipStream_t stream);
+                          const void* addend, hipStream_t stream, int tile = kTileAuto);
 int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int stride);
 void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int splits, void* dw, int out_dtype, int N,
                           int H, int W, int Cin, int Cout, int stride, hipStream_t stream);

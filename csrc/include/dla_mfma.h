@@ -193,25 +193,33 @@ __device__ __forceinline__ void mainloop(const LA& la, const LB& lb, int kbeg, i
 // ---- epilogues -------------------------------------------------------------------------------
 template <int BM, int BN, bool kStats>
 __host__ __device__ constexpr size_t epilogue_lds_bytes() {
-  return (size_t)BM * (BN + 8) * sizeof(bf16_t) + (kStats ? (size_t)4 * BN * sizeof(float) : 0);
+  return (size_t)BM * (BN + 8) * sizeof(bf16_t) > (size_t)4 * BN * sizeof(float)
+             ? (size_t)BM * (BN + 8) * sizeof(bf16_t)
+             : (size_t)4 * BN * sizeof(float);
 }
 
+// Column statistics of a block's output tile(s): a lane owns one column of each 16x16 fragment, so
+// each wave keeps TN (sum, sumsq) in registers until stats_flush.
+template <int BM, int BN>
+struct ColStats {
+  float s[Acc<BM, BN>::TN], q[Acc<BM, BN>::TN];
+  __device__ void zero() {
+#pragma unroll
+    for (int j = 0; j < Acc<BM, BN>::TN; ++j) s[j] = q[j] = 0.f;
+  }
+};
+
 // bf16 C tile -> LDS -> coalesced 16-byte row stores, optional fused addend D (C = bf16(bf16(acc) + D),
-// exactly the unfused bf16 add) and optional per-column (sum, sumsq) of the stored values written
-// as the row-block partial stats[bm][N][2] (BatchNorm statistics of the output, no atomics).
+// exactly the unfused bf16 add); with kStats, the stored values' per-column (sum, sumsq) are added
+// to `st` straight from the accumulator registers. Ends with a barrier (LDS free for the next tile).
 template <int BM, int BN, bool kStats>
 __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __restrict__ C, int64_t ldc, int64_t M,
-                                              int N, int64_t row0, int col0, int bm, float* __restrict__ stats,
+                                              int N, int64_t row0, int col0, ColStats<BM, BN>& st,
                                               const bf16_t* __restrict__ D, int64_t ldd, char* smem) {
   constexpr int WM = Acc<BM, BN>::WM, WN = Acc<BM, BN>::WN, TM = Acc<BM, BN>::TM, TN = Acc<BM, BN>::TN;
   constexpr int LDS_C = BN + 8;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
   bf16_t* Cs = reinterpret_cast<bf16_t*>(smem);
-  // statistics from the accumulator registers: a lane owns one column of each 16x16 tile and 4 of
-  // its rows; the 4 lane groups sharing a column combine by xor-shuffles, the 2 M-waves via LDS
-  float cs[TN], cq[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) cs[j] = cq[j] = 0.f;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -224,8 +232,8 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
         Cs[m * LDS_C + n] = h;
         if constexpr (kStats) {
           const float v = (row0 + m < M) ? bf16_to_f32(h) : 0.f;  // statistics of the stored values
-          cs[j] += v;
-          cq[j] = fmaf(v, v, cq[j]);
+          st.s[j] += v;
+          st.q[j] = fmaf(v, v, st.q[j]);
         }
       }
   __syncthreads();
@@ -244,25 +252,34 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
       *reinterpret_cast<ushort8_t*>(C + gm * ldc + gn) = v;
     }
   }
-  if constexpr (kStats) {
-    float* red = reinterpret_cast<float*>(smem + BM * LDS_C * sizeof(bf16_t));  // [2 wr][BN][2]
+  __syncthreads();
+}
+
+// Writes a block's accumulated column statistics as one partial row: out[N][2] at columns col0..
+// (the 4 lane groups sharing a column combine by xor-shuffles, the 2 M-waves through LDS).
+template <int BM, int BN>
+__device__ __forceinline__ void stats_flush(ColStats<BM, BN>& st, float* __restrict__ out, int N, int col0,
+                                            char* smem) {
+  constexpr int WN = Acc<BM, BN>::WN, TN = Acc<BM, BN>::TN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
+  float* red = reinterpret_cast<float*>(smem);  // [2 wr][BN][2]
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      cs[j] += __shfl_xor(cs[j], 16, kWave);
-      cq[j] += __shfl_xor(cq[j], 16, kWave);
-      cs[j] += __shfl_xor(cs[j], 32, kWave);
-      cq[j] += __shfl_xor(cq[j], 32, kWave);
-      if (lane < 16) {
-        const int n = wc * WN + j * 16 + fr;
-        red[(wr * BN + n) * 2 + 0] = cs[j];
-        red[(wr * BN + n) * 2 + 1] = cq[j];
-      }
+  for (int j = 0; j < TN; ++j) {
+    float a = st.s[j], b = st.q[j];
+    a += __shfl_xor(a, 16, kWave);
+    b += __shfl_xor(b, 16, kWave);
+    a += __shfl_xor(a, 32, kWave);
+    b += __shfl_xor(b, 32, kWave);
+    if (lane < 16) {
+      const int n = wc * WN + j * 16 + fr;
+      red[(wr * BN + n) * 2 + 0] = a;
+      red[(wr * BN + n) * 2 + 1] = b;
     }
-    __syncthreads();
-    if (tid < BN && col0 + tid < N) {
-      stats[((int64_t)bm * N + col0 + tid) * 2 + 0] = red[tid * 2 + 0] + red[(BN + tid) * 2 + 0];
-      stats[((int64_t)bm * N + col0 + tid) * 2 + 1] = red[tid * 2 + 1] + red[(BN + tid) * 2 + 1];
-    }
+  }
+  __syncthreads();
+  if (tid < BN && col0 + tid < N) {
+    out[(int64_t)(col0 + tid) * 2 + 0] = red[tid * 2 + 0] + red[(BN + tid) * 2 + 0];
+    out[(int64_t)(col0 + tid) * 2 + 1] = red[tid * 2 + 1] + red[(BN + tid) * 2 + 1];
   }
 }
 

@@ -22,6 +22,9 @@
 namespace dla {
 
 constexpr int kBNThreads = 256;
+// Row blocks of the two reduction passes (stats, backward reduce): 4 workgroups per CU stream at
+// full bandwidth, and <= 1024 partial rows keep the finalize's reduction at ~2 load round trips.
+constexpr int kRedBlocks = 1024;
 
 // Block geometry shared by the two reduction passes: the block covers CT = tpr*8 channels
 // (channel tile blockIdx.x) and rows [r0, r1) (row block blockIdx.y); rpi = 256/tpr rows are in
@@ -87,48 +90,64 @@ __global__ __launch_bounds__(kBNThreads) void bn_stats_kernel(const T* __restric
   block_reduce_write(s, q, tpr, rpi, ct, C, part, c_base, red);
 }
 
-// Parallel partial reduction shared by both finalize kernels. A block owns kFinC = 8 channels and
-// gives each channel 32 lanes (half a wave) that stride over the nrb block partials with 4
-// independent accumulators in flight (the loop is latency-bound otherwise: one dependent 8-byte load
-// chain per lane was ~57 us per call at nrb = 2048), then a 32-lane shuffle tree. Fixed order ->
-// bitwise reproducible.
-constexpr int kFinC = 8;
-
+// Partial reduction shared by both finalize kernels: WPC waves per channel (a 256-thread block owns
+// 4 / WPC channels); each lane strides over the nrb block partials with 8 independent loads in
+// flight, then a 64-lane shuffle tree and (WPC > 1) a fixed-order combine through LDS. The pass is
+// latency-bound (~1 us per dependent round trip): WPC = 1 for the <= 1024 partial rows of the
+// reduction passes, WPC = 4 for the per-128-row-tile partials of the GEMM epilogues.
+// Fixed order -> bitwise reproducible.
+template <int WPC>
 __device__ __forceinline__ bool reduce_partials(const float* __restrict__ part, int nrb, int C, float& S, float& Q,
                                                 int& c) {
-  const int lane32 = threadIdx.x & 31;
-  c = blockIdx.x * kFinC + (threadIdx.x >> 5);
-  float s[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  c = blockIdx.x * (4 / WPC) + wave / WPC;
+  float s[8], q[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s[u] = q[u] = 0.f;
   if (c < C) {
     const float2* p2 = reinterpret_cast<const float2*>(part);
-    int b = lane32;
-    for (; b + 96 < nrb; b += 128) {
+    constexpr int kStride = 64 * WPC;
+    int b = lane + 64 * (wave % WPC);
+    for (; b + 7 * kStride < nrb; b += 8 * kStride) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float2 v = p2[(int64_t)(b + 32 * u) * C + c];
+      for (int u = 0; u < 8; ++u) {
+        const float2 v = p2[(int64_t)(b + kStride * u) * C + c];
         s[u] += v.x;
         q[u] += v.y;
       }
     }
-    for (; b < nrb; b += 32) {
+    for (; b < nrb; b += kStride) {
       const float2 v = p2[(int64_t)b * C + c];
       s[0] += v.x;
       q[0] += v.y;
     }
   }
-  float ss = (s[0] + s[1]) + (s[2] + s[3]);
-  float qq = (q[0] + q[1]) + (q[2] + q[3]);
+  float ss = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  float qq = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+  ss = wave_sum(ss);
+  qq = wave_sum(qq);
+  if constexpr (WPC > 1) {
+    if (lane == 0) {
+      red[0][wave] = ss;
+      red[1][wave] = qq;
+    }
+    __syncthreads();
+    if (wave % WPC != 0) return false;
+    ss = qq = 0.f;
 #pragma unroll
-  for (int off = 16; off > 0; off >>= 1) {  // stays inside each 32-lane half of the wave
-    ss += __shfl_xor(ss, off, kWave);
-    qq += __shfl_xor(qq, off, kWave);
+    for (int w = 0; w < WPC; ++w) {
+      ss += red[0][wave + w];
+      qq += red[1][wave + w];
+    }
   }
-  if (lane32 != 0 || c >= C) return false;
+  if (lane != 0 || c >= C) return false;
   S = ss;
   Q = qq;
   return true;
 }
 
+template <int WPC>
 __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __restrict__ x0, int x_is_bf16,
                                                                 const float* __restrict__ part, int nrb, int64_t M,
                                                                 int C, const float* __restrict__ gamma,
@@ -138,7 +157,7 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __re
                                                                 float* __restrict__ ws) {
   float S, Q;
   int c;
-  if (!reduce_partials(part, nrb, C, S, Q, c)) return;
+  if (!reduce_partials<WPC>(part, nrb, C, S, Q, c)) return;
   const float K = x0 == nullptr ? 0.f
                   : (x_is_bf16 ? bf16_to_f32(reinterpret_cast<const bf16_t*>(x0)[c]) : reinterpret_cast<const float*>(x0)[c]);
   const float inv_m = 1.f / (float)M;
@@ -271,13 +290,14 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(const T* __re
   block_reduce_write(s, q, tpr, rpi, ct, C, part, c_base, red);
 }
 
+template <int WPC>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int64_t M,
                                                               int C, const float* __restrict__ gamma,
                                                               float* __restrict__ ws, float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta) {
   float S, Q;
   int c;
-  if (!reduce_partials(part, nrb, C, S, Q, c)) return;
+  if (!reduce_partials<WPC>(part, nrb, C, S, Q, c)) return;
   const float invstd = ws[C + c];
   const float g = gamma ? gamma[c] : 1.f;
   if (dgamma) dgamma[c] = Q * invstd;
@@ -328,14 +348,14 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(const T* __res
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
-void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks = 2048) {
+void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks = kRedBlocks) {
   int ct = C;
   if (ct > 512) ct = 512;
   while (C % ct) ct -= 8;  // C % 8 == 0 guaranteed by the caller
   *tpr = ct / 8;
   *nct = C / ct;
   const int rpi = kBNThreads / *tpr;
-  int64_t want = target_blocks / *nct;  // ~8 workgroups per CU overall
+  int64_t want = target_blocks / *nct;
   if (want < 1) want = 1;
   int64_t maxrb = (M + rpi - 1) / rpi;
   // keep >= 4 row iterations per thread so the per-block partial write is amortised
@@ -352,8 +372,12 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
   bn_geometry(M, C, &tpr, &nrb, &nct);
   if (training && ext_part) {
     // statistics already produced by the conv GEMM epilogue (unshifted per-row-block partials)
-    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(256), 0, stream, nullptr, 0, ext_part,
-                       ext_nrb, M, C, gamma, beta, eps, momentum, running_mean, running_var, ws);
+    if (ext_nrb > 1024)
+      hipLaunchKernelGGL(bn_stats_finalize_kernel<4>, dim3(C), dim3(256), 0, stream, nullptr, 0, ext_part, ext_nrb, M,
+                         C, gamma, beta, eps, momentum, running_mean, running_var, ws);
+    else
+      hipLaunchKernelGGL(bn_stats_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, nullptr, 0, ext_part,
+                         ext_nrb, M, C, gamma, beta, eps, momentum, running_mean, running_var, ws);
   } else if (training) {
     const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
     if (dtype == kBF16)
@@ -362,7 +386,7 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
     else
       hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nct, nrb), dim3(kBNThreads), lds, stream, (const float*)x, M, C,
                          nrb, tpr, part);
-    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(256), 0, stream, x, dtype == kBF16, part,
+    hipLaunchKernelGGL(bn_stats_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, x, dtype == kBF16, part,
                        nrb, M, C, gamma, beta, eps, momentum, running_mean, running_var, ws);
   }
   int atpr, anrb, anct;
@@ -399,8 +423,8 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
   if (dtype == kBF16) { DLA_BN_RED_ALL(bf16_t) } else { DLA_BN_RED_ALL(float) }
 #undef DLA_BN_RED_ALL
 #undef DLA_BN_RED
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinC - 1) / kFinC), dim3(256), 0, stream, part, nrb, M, C,
-                     gamma, ws, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, part, nrb, M, C, gamma, ws,
+                     dgamma, dbeta);
   int atpr, anrb, anct;
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
 #define DLA_BN_BAPPLY(T, K, D)                                                                                      \

@@ -150,13 +150,16 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_fwd_kernel(const bf16_t* 
   const int64_t row0 = (int64_t)bm * BM;
   const int col0 = bn * BN;
   const int K = 9 * g.Cin;
+  const RowLoader<BN> lb{w, K, (int64_t)col0, g.Cout, K};
   Im2colRowLoader<BM, false> la{x, g.H, g.W, g.Cin, g.stride};
   la.init(g, row0, P, g.OH, g.OW, g.fOW, g.fOH);
-  const RowLoader<BN> lb{w, K, (int64_t)col0, g.Cout, K};
+  ColStats<BM, BN> st;
+  st.zero();
   Acc<BM, BN> acc;
   acc.zero();
   mainloop<BM, BN>(la, lb, 0, K, acc, smem_raw);
-  epilogue_bf16<BM, BN, kStats>(acc, y, g.Cout, P, g.Cout, row0, col0, bm, stats, nullptr, 0, smem_raw);
+  epilogue_bf16<BM, BN, kStats>(acc, y, g.Cout, P, g.Cout, row0, col0, st, nullptr, 0, smem_raw);
+  if constexpr (kStats) stats_flush<BM, BN>(st, stats + (int64_t)bm * g.Cout * 2, g.Cout, col0, smem_raw);
 }
 
 // stride-1 dgrad: dX (the GEMM's M = input pixels, N = Cin), A = dY gathered with flipped taps
@@ -173,13 +176,14 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_dgrad_kernel(const bf16_t
   const int64_t row0 = (int64_t)bm * BM;
   const int col0 = bn * BN;
   const int K = 9 * g.Cout;
+  const WeightTapKLoader<BN> lb{w, g.Cout, g.Cin, col0};
   Im2colRowLoader<BM, true> la{dy, g.OH, g.OW, g.Cout, 1};
   la.init(g, row0, P, g.H, g.W, g.fOW, g.fOH);  // stride 1: the same divisors (OW == W, OH == H)
-  const WeightTapKLoader<BN> lb{w, g.Cout, g.Cin, col0};
+  ColStats<BM, BN> st;
   Acc<BM, BN> acc;
   acc.zero();
   mainloop<BM, BN>(la, lb, 0, K, acc, smem_raw);
-  epilogue_bf16<BM, BN, false>(acc, dx, g.Cin, P, g.Cin, row0, col0, bm, nullptr, addend, g.Cin, smem_raw);
+  epilogue_bf16<BM, BN, false>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, addend, g.Cin, smem_raw);
 }
 
 // wgrad partial slabs P[split][Cout][9*Cin]
@@ -230,21 +234,26 @@ static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGe
   hipLaunchKernelGGL((conv3x3_fwd_kernel<BM, BN, S>), dim3(tiles), dim3(kThreads), lds, stream, x, w, y, g, stats);
 }
 
-int conv3x3_row_block() { return 128; }
+int conv3x3_stats_rows(int64_t P, int Cout, int tile) {
+  const int bm = tile_bm(pick_tile(P, Cout, tile));
+  return (int)((P + bm - 1) / bm);
+}
 
 void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout, int stride,
-                        float* stats, hipStream_t stream) {
+                        float* stats, hipStream_t stream, int tile) {
   const ConvGeom g = make_geom(N, H, W, Cin, Cout, stride);
   const bf16_t* xp = (const bf16_t*)x;
   const bf16_t* wp = (const bf16_t*)w;
   bf16_t* yp = (bf16_t*)y;
-  if (Cout <= 64) {
-    if (stats) launch_fwd<128, 64, true>(xp, wp, yp, g, stats, stream);
-    else launch_fwd<128, 64, false>(xp, wp, yp, g, stats, stream);
-  } else {
-    if (stats) launch_fwd<128, 128, true>(xp, wp, yp, g, stats, stream);
-    else launch_fwd<128, 128, false>(xp, wp, yp, g, stats, stream);
+#define DLA_CF(BM_, BN_)                                                  \
+  if (stats) launch_fwd<BM_, BN_, true>(xp, wp, yp, g, stats, stream);   \
+  else launch_fwd<BM_, BN_, false>(xp, wp, yp, g, stats, stream);
+  switch (pick_tile((int64_t)g.N * g.OH * g.OW, Cout, tile)) {
+    case kTile128x128: DLA_CF(128, 128) break;
+    case kTile128x64: DLA_CF(128, 64) break;
+    default: DLA_CF(64, 64) break;
   }
+#undef DLA_CF
 }
 
 template <int BM, int BN>
@@ -258,12 +267,16 @@ static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const Co
 }
 
 void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
-                          const void* addend, hipStream_t stream) {
+                          const void* addend, hipStream_t stream, int tile) {
   const ConvGeom g = make_geom(N, H, W, Cin, Cout, 1);
-  if (Cin <= 64)
-    launch_dgrad<128, 64>((const bf16_t*)dy, (const bf16_t*)w, (bf16_t*)dx, g, (const bf16_t*)addend, stream);
-  else
-    launch_dgrad<128, 128>((const bf16_t*)dy, (const bf16_t*)w, (bf16_t*)dx, g, (const bf16_t*)addend, stream);
+  const bf16_t* d = (const bf16_t*)dy;
+  const bf16_t* wp = (const bf16_t*)w;
+  const bf16_t* ad = (const bf16_t*)addend;
+  switch (pick_tile((int64_t)N * H * W, Cin, tile)) {
+    case kTile128x128: launch_dgrad<128, 128>(d, wp, (bf16_t*)dx, g, ad, stream); break;
+    case kTile128x64: launch_dgrad<128, 64>(d, wp, (bf16_t*)dx, g, ad, stream); break;
+    default: launch_dgrad<64, 64>(d, wp, (bf16_t*)dx, g, ad, stream); break;
+  }
 }
 
 int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int stride) {

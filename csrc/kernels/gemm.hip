@@ -42,6 +42,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const bf16_t* __re
   const int bm = tile / nbn, bn = tile % nbn;
   const int64_t row0 = (int64_t)bm * BM;
   const int col0 = bn * BN;
+  ColStats<BM, BN> st;
+  st.zero();
   Acc<BM, BN> acc;
   acc.zero();
   const RowLoader<BM> la{A, lda, row0, M, K};
@@ -52,7 +54,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const bf16_t* __re
     const RowLoader<BN> lb{B, ldb, (int64_t)col0, N, K};
     mainloop<BM, BN>(la, lb, 0, K, acc, smem_raw);
   }
-  epilogue_bf16<BM, BN, kStats>(acc, C, ldc, M, N, row0, col0, bm, stats, D, ldd, smem_raw);
+  epilogue_bf16<BM, BN, kStats>(acc, C, ldc, M, N, row0, col0, st, D, ldd, smem_raw);
+  if constexpr (kStats) stats_flush<BM, BN>(st, stats + (int64_t)bm * N * 2, N, col0, smem_raw);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -128,26 +131,37 @@ static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb
                      ldb, C, ldc, M, N, K, stats, D, ldd);
 }
 
-int gemm_nt_row_block(int M, int N) {
-  (void)M;
-  return 128;  // BM of every shipped tile config
+int pick_tile(int64_t M, int N, int tile) {
+  // measured (scripts/bench_gemm.py, bench_conv.py): the 128-row tiles win at every ResNet shape,
+  // including the small-M layers, so the narrow tile is used only when N itself is narrow
+  if (tile != kTileAuto) return tile;
+  return N <= 64 ? kTile128x64 : kTile128x128;
+}
+
+int gemm_nt_stats_rows(int M, int N, int tile) {
+  const int bm = tile_bm(pick_tile(M, N, tile));
+  return (M + bm - 1) / bm;
 }
 
 void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
-                    float* stats, hipStream_t stream, const void* addend, int64_t ld_addend, bool b_kmajor) {
+                    float* stats, hipStream_t stream, const void* addend, int64_t ld_addend, bool b_kmajor, int tile) {
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* b = (const bf16_t*)B;
   bf16_t* c = (bf16_t*)C;
   const bf16_t* d = (const bf16_t*)addend;
-#define DLA_NT(BN_, S_, BT_) launch_nt<128, BN_, S_, BT_>(a, lda, b, ldb, c, ldc, M, N, K, stats, d, ld_addend, stream)
-#define DLA_NT_BT(BN_, S_) \
-  if (b_kmajor) DLA_NT(BN_, S_, true); else DLA_NT(BN_, S_, false);
-  if (N <= 64) {
-    if (stats) { DLA_NT_BT(64, true) } else { DLA_NT_BT(64, false) }
-  } else {
-    if (stats) { DLA_NT_BT(128, true) } else { DLA_NT_BT(128, false) }
+#define DLA_NT(BM_, BN_, S_, BT_) launch_nt<BM_, BN_, S_, BT_>(a, lda, b, ldb, c, ldc, M, N, K, stats, d, ld_addend, stream)
+#define DLA_NT_ST(BM_, BN_)                                \
+  if (stats) {                                             \
+    if (b_kmajor) DLA_NT(BM_, BN_, true, true); else DLA_NT(BM_, BN_, true, false);    \
+  } else {                                                 \
+    if (b_kmajor) DLA_NT(BM_, BN_, false, true); else DLA_NT(BM_, BN_, false, false);  \
   }
-#undef DLA_NT_BT
+  switch (pick_tile(M, N, tile)) {
+    case kTile128x128: DLA_NT_ST(128, 128) break;
+    case kTile128x64: DLA_NT_ST(128, 64) break;
+    default: DLA_NT_ST(64, 64) break;
+  }
+#undef DLA_NT_ST
 #undef DLA_NT
 }
 

@@ -22,7 +22,7 @@ static int64_t rows_of(const at::Tensor& t) { return t.numel() / t.size(1); }
 
 static int64_t partial_floats(int64_t M, int C) {
   int tpr, nrb, nct;
-  bn_geometry(M, C, &tpr, &nrb, &nct, 2048);
+  bn_geometry(M, C, &tpr, &nrb, &nct, 1024);
   return (int64_t)nrb * C * 2;
 }
 
@@ -129,7 +129,8 @@ static void check_mat(const at::Tensor& t, const char* what) {
 // C = A @ B^T (A [M,K], B [N,K]; or C = A @ B with B [K,N] when b_kmajor) in bf16 with fp32 accumulation. Optionally returns per-row-block
 // column statistics partials [ceil(M/128), N, 2] (sum, sum of squares of the bf16 outputs).
 std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::optional<at::Tensor> addend,
-                                bool b_kmajor) {
+                                bool b_kmajor, int64_t tile) {
+  TORCH_CHECK(tile >= 0 && tile <= 3, "gemm_nt: tile config 0..3");
   check_mat(A, "A");
   check_mat(B, "B");
   TORCH_CHECK(A.size(1) == B.size(b_kmajor ? 0 : 1), "gemm_nt: K mismatch");
@@ -141,12 +142,12 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
   }
   at::Tensor C = at::empty({M, N}, A.options());
   at::Tensor S;
-  if (stats) S = at::empty({(M + gemm_nt_row_block(M, N) - 1) / gemm_nt_row_block(M, N), N, 2},
+  if (stats) S = at::empty({gemm_nt_stats_rows(M, N, (int)tile), N, 2},
                            A.options().dtype(at::kFloat));
   if (M > 0 && N > 0)
     launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K,
                    stats ? S.data_ptr<float>() : nullptr, current_stream(A), add ? addend->data_ptr() : nullptr,
-                   add ? addend->stride(0) : 0, b_kmajor);
+                   add ? addend->stride(0) : 0, b_kmajor, (int)tile);
   return {C, S};
 }
 
@@ -218,7 +219,8 @@ static void check_conv3(const at::Tensor& x, const at::Tensor& w) {
 }
 
 // 3x3 / pad 1 convolution forward (stride 1 or 2). Returns (y, stats-or-undefined).
-std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, bool stats) {
+std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, bool stats, int64_t tile) {
+  TORCH_CHECK(tile >= 0 && tile <= 3, "conv3x3: tile config 0..3");
   check_conv3(x, w);
   TORCH_CHECK(stride == 1 || stride == 2, "conv3x3: stride 1 or 2");
   const int N = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Cout = (int)w.size(0);
@@ -226,14 +228,15 @@ std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, 
   at::Tensor y = at::empty({N, Cout, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor S;
   const int64_t P = (int64_t)N * OH * OW;
-  if (stats) S = at::empty({(P + conv3x3_row_block() - 1) / conv3x3_row_block(), Cout, 2}, x.options().dtype(at::kFloat));
+  if (stats) S = at::empty({conv3x3_stats_rows(P, Cout, (int)tile), Cout, 2}, x.options().dtype(at::kFloat));
   launch_conv3x3_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), N, H, W, Cin, Cout, (int)stride,
-                     stats ? S.data_ptr<float>() : nullptr, current_stream(x));
+                     stats ? S.data_ptr<float>() : nullptr, current_stream(x), (int)tile);
   return {y, S};
 }
 
 // stride-1 data gradient (+ optional fused addend, same shape as dx)
-at::Tensor conv3x3_dgrad(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> addend) {
+at::Tensor conv3x3_dgrad(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> addend, int64_t tile) {
+  TORCH_CHECK(tile >= 0 && tile <= 3, "conv3x3: tile config 0..3");
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(dy.dim() == 4 && dy.size(1) == w.size(0), "conv3x3_dgrad: dy/w mismatch");
   const int N = (int)dy.size(0), Cout = (int)w.size(0), Cin = (int)w.size(1), H = (int)dy.size(2), W = (int)dy.size(3);
@@ -248,7 +251,8 @@ at::Tensor conv3x3_dgrad(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> 
                 "conv3x3_dgrad: addend must match dx");
     add = addend->data_ptr();
   }
-  launch_conv3x3_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, add, current_stream(dy));
+  launch_conv3x3_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, add, current_stream(dy),
+                       (int)tile);
   return dx;
 }
 
@@ -273,9 +277,9 @@ at::Tensor conv3x3_wgrad(at::Tensor dy, at::Tensor x, int64_t stride, c10::Scala
 
 void bind_nn(pybind11::module& m) {
   m.def("conv3x3_fwd", &conv3x3_fwd, "implicit-GEMM 3x3/pad-1 conv forward (NHWC bf16, MFMA)", pybind11::arg("x"),
-        pybind11::arg("w"), pybind11::arg("stride") = 1, pybind11::arg("stats") = false);
+        pybind11::arg("w"), pybind11::arg("stride") = 1, pybind11::arg("stats") = false, pybind11::arg("tile") = 0);
   m.def("conv3x3_dgrad", &conv3x3_dgrad, "implicit-GEMM 3x3 conv data gradient (stride 1)", pybind11::arg("dy"),
-        pybind11::arg("w"), pybind11::arg("addend") = pybind11::none());
+        pybind11::arg("w"), pybind11::arg("addend") = pybind11::none(), pybind11::arg("tile") = 0);
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "implicit-GEMM 3x3 conv weight gradient (split-K)", pybind11::arg("dy"),
         pybind11::arg("x"), pybind11::arg("stride") = 1, pybind11::arg("out_dtype") = at::kFloat);
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC max pooling forward (+ argmax window positions)", pybind11::arg("x"),
@@ -284,7 +288,7 @@ void bind_nn(pybind11::module& m) {
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pooling backward (gather form)");
   m.def("gemm_nt", &gemm_nt, "C = A @ B^T (bf16 MFMA), optional fused column statistics", pybind11::arg("A"),
         pybind11::arg("B"), pybind11::arg("stats") = false, pybind11::arg("addend") = pybind11::none(),
-        pybind11::arg("b_kmajor") = false);
+        pybind11::arg("b_kmajor") = false, pybind11::arg("tile") = 0);
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),
         pybind11::arg("out_dtype") = at::kFloat, pybind11::arg("scale") = 1.0);
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC", pybind11::arg("x"),

@@ -52,6 +52,9 @@ for M, Cin, Cout in shapes:
     r["fwd_miopen_conv_ms"] = timeit(lambda: torch.nn.functional.conv2d(x4, w4))
     r["dgrad_native_ms"] = timeit(lambda: C.gemm_nt(dY, Wt, False))
     r["dgrad_native_kmajor_ms"] = timeit(lambda: C.gemm_nt(dY, W, False, None, True))
+    for t in (1, 2, 3):
+        r[f"fwd_t{t}"] = timeit(lambda: C.gemm_nt(X, W, True, None, False, t))
+        r[f"dgrad_t{t}"] = timeit(lambda: C.gemm_nt(dY, W, False, None, True, t))
     r["dgrad_torch_mm_ms"] = timeit(lambda: dY @ W)
     r["wgrad_native_ms"] = timeit(lambda: C.gemm_tn(dY, X, torch.float32, 1.0))
     r["wgrad_torch_mm_ms"] = timeit(lambda: dY.t() @ X)

@@ -65,3 +65,17 @@ def test_conv3x3_asymmetric_weights(cuda):
         dx = C.conv3x3_dgrad(dy, w)
         ref = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), 1, 1)
         torch.testing.assert_close(dx.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3])
+def test_conv3x3_tile_configs(cuda, tile):
+    C = _C()
+    torch.manual_seed(0)
+    x = torch.randn(2, 128, 14, 14, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(128, 128, 3, 3, device=cuda) * 0.05).to(torch.bfloat16).contiguous(memory_format=CL)
+    y_ref, s_ref = C.conv3x3_fwd(x, w, 1, True, 1)
+    y, s = C.conv3x3_fwd(x, w, 1, True, tile)
+    assert torch.equal(y, y_ref)
+    torch.testing.assert_close(s.sum(0), s_ref.sum(0), rtol=1e-5, atol=1e-3)
+    dy = torch.randn_like(y)
+    assert torch.equal(C.conv3x3_dgrad(dy, w, None, tile), C.conv3x3_dgrad(dy, w, None, 1))

@@ -70,3 +70,18 @@ def test_gemm_nt_kmajor_b_and_addend(cuda, M, N, K):
     assert torch.equal(out, out_t)
     out_d, _ = C.gemm_nt(A, B, False, D, True)
     assert torch.equal(out_d, out + D)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(1000, 64, 256), (777, 136, 72), (4096, 512, 128)])
+def test_gemm_nt_tile_configs(cuda, tile, M, N, K):
+    C = _C()
+    torch.manual_seed(0)
+    A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    B = torch.randn(N, K, device=cuda).to(torch.bfloat16)
+    out, stats = C.gemm_nt(A, B, True, None, False, tile)
+    ref, _ = C.gemm_nt(A, B, False, None, False, 1)
+    assert torch.equal(out, ref)  # same k order in every tile shape
+    torch.testing.assert_close(stats.sum(0)[:, 0], out.float().sum(0), rtol=1e-4, atol=1e-2 * M ** 0.5)
+    outk, _ = C.gemm_nt(A, B.t().contiguous(), False, None, True, tile)
+    assert torch.equal(outk, ref)
