@@ -116,6 +116,11 @@ void launch_maxpool_bwd(const void* dy, const uint8_t* pos, void* dx, int N, int
 // 16-byte aligned rows.
 // Tile configurations of the MFMA kernels (gemm_nt, conv3x3 fwd/dgrad). kTileAuto picks the
 // largest tile that still yields >= 1024 workgroups (4 per CU), so small-M layers fill the chip.
+// MFMA main-loop pipeline for every GEMM/conv kernel: 0 register staging, 2 / 3 LDS-DMA stages,
+// -1 (default) per shape.
+void set_mfma_pipeline(int p);  // -1 = per-shape auto
+int mfma_pipeline();
+int mfma_pipeline_for(int K);
 enum TileCfg : int { kTileAuto = 0, kTile128x128 = 1, kTile128x64 = 2, kTile64x64 = 3 };
 int pick_tile(int64_t M, int N, int tile);
 inline int tile_bm(int cfg) { return cfg == kTile64x64 ? 64 : 128; }

@@ -38,14 +38,16 @@ __device__ __forceinline__ ushort8_t zero8() { return ushort8_t{0, 0, 0, 0, 0, 0
 // index with a row-dependent multiple of 4 gives them disjoint 8-bank windows, keeps every 32-byte
 // chunk group and every 16-byte store contiguous; stores and reads share this function.
 template <int W>
-__device__ __forceinline__ int tr_off(int row, int col) {  // element offset of (row, col), col % 4 == 0
+__device__ __forceinline__ int tr_sw(int row) {  // XOR applied to the 8-byte chunk index of a row
   static_assert(W == 64 || W == 128, "tr image width");
-  int sw;
   if constexpr (W == 128)
-    sw = 4 * ((row & 3) | (((row >> 3) & 1) << 2));  // 32 chunks/row (256 B = 64 banks)
+    return 4 * ((row & 3) | (((row >> 3) & 1) << 2));  // 32 chunks/row (256 B = 64 banks)
   else
-    sw = 4 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));  // 16 chunks/row; row parity adds 32 banks
-  return row * W + (((col >> 2) ^ sw) << 2);
+    return 4 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));  // 16 chunks/row; row parity adds 32 banks
+}
+template <int W>
+__device__ __forceinline__ int tr_off(int row, int col) {  // element offset of (row, col), col % 4 == 0
+  return row * W + (((col >> 2) ^ tr_sw<W>(row)) << 2);
 }
 
 __device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* lo_ptr, const bf16_t* hi_ptr) {
@@ -65,6 +67,47 @@ struct TileGeom {
   static constexpr int kKElems = kBK * W;
 };
 
+// ---- LDS-DMA (global_load_lds) staging ---------------------------------------------------------
+// With LDS-DMA the tile bytes go HBM/L2 -> LDS without touching VGPRs, so several k-steps can be in
+// flight (the register-staged loop holds exactly one). The DMA writes each wave-instruction's 64 x
+// 16 B lane-linearly (wave-uniform base + 16 * lane): chunk slot c of a tile always lands at byte
+// 16 * c, and the loaders choose WHICH logical 16 B each lane fetches so that this linear image is
+// the swizzled one the fragment reads expect (cdna_hip_programming.md §5 'Async global->LDS copy').
+//   row-major image: row = c >> 3, physical chunk c & 7 holds logical chunk (c & 7) ^ ((row >> 1) & 7)
+//                    (16 rows of a ds_read_b128 fragment hit 16 distinct 16-byte bank slots);
+//   k-major image:   the tr_off image above (row = c / KPR, logical column from the inverse XOR).
+// Out-of-range chunks (tile edges, conv padding) read a zero page instead of being masked.
+static __device__ __attribute__((aligned(64))) uint32_t g_zero_page[16];
+
+__device__ __forceinline__ const void* zero_src() { return g_zero_page; }
+
+__device__ __forceinline__ int rm_glds_kc(int c) { return (((c & 7) ^ ((c >> 4) & 7)) << 3); }  // logical k
+template <int W>
+__device__ __forceinline__ int km_glds_col(int c) {  // logical column of chunk c in the k-major image
+  const int kr = c / TileGeom<W>::KPR;
+  return ((((c % TileGeom<W>::KPR) << 1) ^ tr_sw<W>(kr)) << 2);
+}
+
+// one 16-byte LDS-DMA per lane; lds_byte is the wave-uniform destination of lane 0. The asm hides
+// the load from hipcc's waitcnt bookkeeping (it would drain it with vmcnt(0) before every ds_read);
+// completion is tracked by the explicit vm_wait<N>() + barrier in the main loop. M0 is saved and
+// restored inside the statement (§5.7).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_byte)
+               : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
 // ---- loaders ------------------------------------------------------------------------------------
 // A loader exposes kKMajor and  ushort8_t load(int i, int k0) const  returning the 8 elements of
 // chunk slot i (chunk id c = tid + i * 256) for the k-step starting at k0, zeros out of range.
@@ -82,6 +125,11 @@ struct RowLoader {
     const int64_t gr = row0 + r;
     return (gr < rows && k0 + kc < K) ? *reinterpret_cast<const ushort8_t*>(p + gr * ld + k0 + kc) : zero8();
   }
+  __device__ const void* src(int i, int k0) const {
+    const int c = threadIdx.x + i * kThreads, r = c >> 3, kc = rm_glds_kc(c);
+    const int64_t gr = row0 + r;
+    return (gr < rows && k0 + kc < K) ? (const void*)(p + gr * ld + k0 + kc) : zero_src();
+  }
 };
 
 // k-major matrix [K][cols] (cols contiguous): gemm_tn operands, dgrad weights as stored.
@@ -96,6 +144,11 @@ struct KLoader {
     const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR, nc = (c % TileGeom<W>::KPR) * 8;
     const int gk = k0 + kr, gc = col0 + nc;
     return (gk < kend && gc < cols) ? *reinterpret_cast<const ushort8_t*>(p + (int64_t)gk * ld + gc) : zero8();
+  }
+  __device__ const void* src(int i, int k0) const {
+    const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR;
+    const int gk = k0 + kr, gc = col0 + km_glds_col<W>(c);
+    return (gk < kend && gc < cols) ? (const void*)(p + (int64_t)gk * ld + gc) : zero_src();
   }
 };
 
@@ -188,6 +241,98 @@ __device__ __forceinline__ void mainloop(const LA& la, const LB& lb, int kbeg, i
       __syncthreads();
     }
   }
+}
+
+// 16 x 32 row-major operand fragment from the LDS-DMA image (see the image map above)
+__device__ __forceinline__ bf16x8_t rm_glds_frag(const bf16_t* s, int r0, int kk) {
+  const int lane = threadIdx.x & 63;
+  const int r = r0 + (lane & 15), lc = kk * 4 + (lane >> 4);
+  return *reinterpret_cast<const bf16x8_t*>(s + r * kBK + ((lc ^ ((r >> 1) & 7)) << 3));
+}
+
+template <int W, class L>
+__device__ __forceinline__ bf16x8_t glds_frag(const bf16_t* s, int r0, int kk) {
+  if constexpr (L::kKMajor) return tile_frag<W, L>(s, r0, kk);  // same tr_off image
+  else return rm_glds_frag(s, r0, kk);
+}
+
+template <int BM, int BN, int NS>
+__host__ __device__ constexpr size_t glds_lds_bytes() {
+  return (size_t)NS * (BM + BN) * kBK * sizeof(bf16_t);
+}
+
+// NS-stage LDS-DMA pipeline: tiles t+1 .. t+NS-1 are in flight while tile t is multiplied; one
+// barrier per k-step. Iteration t: wait until this wave's DMAs for tile t are done (the younger
+// stages may stay outstanding: counted vmcnt), barrier (everyone's tile t has landed AND everyone
+// finished tile t-1, whose stage the next DMA overwrites), issue tile t+NS-1, multiply tile t.
+template <int BM, int BN, int NS, class LA, class LB>
+__device__ __forceinline__ void mainloop_glds(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN>& acc,
+                                              char* smem) {
+  static_assert(NS == 2 || NS == 3, "2 or 3 stages");
+  using GA = TileGeom<BM>;
+  using GB = TileGeom<BN>;
+  constexpr int L = GA::CH + GB::CH;  // DMA instructions per wave per tile
+  constexpr int WM = Acc<BM, BN>::WM, WN = Acc<BM, BN>::WN, TM = Acc<BM, BN>::TM, TN = Acc<BM, BN>::TN;
+  constexpr int SA = BM * kBK, SB = BN * kBK;  // elements per stage
+  bf16_t* base = reinterpret_cast<bf16_t*>(smem);
+  const int wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
+  const uint32_t lds0 = lds_addr(smem);
+  const uint32_t wofs = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
+  const int nk = (kend - kbeg + kBK - 1) / kBK;
+  if (nk <= 0) return;
+  auto issue = [&](int t) {
+    const int st = t % NS;
+    const int k0 = kbeg + t * kBK;
+    const uint32_t a_base = lds0 + (uint32_t)(st * (SA + SB)) * 2u + wofs;
+    const uint32_t b_base = a_base + (uint32_t)SA * 2u;
+#pragma unroll
+    for (int i = 0; i < GA::CH; ++i) glds16(la.src(i, k0), a_base + (uint32_t)(i * kThreads * 16));
+#pragma unroll
+    for (int i = 0; i < GB::CH; ++i) glds16(lb.src(i, k0), b_base + (uint32_t)(i * kThreads * 16));
+  };
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) issue(p);
+  for (int t = 0; t < nk; ++t) {
+    if constexpr (NS == 3) {
+      if (t + 1 < nk) vm_wait<L>();
+      else vm_wait<0>();
+    } else {
+      vm_wait<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // no LDS read of tile t above the barrier
+    if (t + NS - 1 < nk) issue(t + NS - 1);
+    const bf16_t* As = base + (t % NS) * (SA + SB);
+    const bf16_t* Bs = As + SA;
+#pragma unroll
+    for (int kk = 0; kk < kBK / 32; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = glds_frag<BM, LA>(As, wr * WM + i * 16, kk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag<BN, LB>(Bs, wc * WN + j * 16, kk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma16(af[i], bfr[j], acc.v[i][j]);
+    }
+  }
+  __syncthreads();  // every wave done with the stages before the epilogue reuses the LDS
+}
+
+// Pipeline selection shared by all MFMA kernels: 0 = register staging (one k-step in flight,
+// 3 blocks/CU), 2 / 3 = LDS-DMA with 2 / 3 stages.
+template <int PIPE, int BM, int BN, class LA, class LB>
+__device__ __forceinline__ void run_mainloop(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN>& acc,
+                                             char* smem) {
+  if constexpr (PIPE == 0) mainloop<BM, BN>(la, lb, kbeg, kend, acc, smem);
+  else mainloop_glds<BM, BN, PIPE>(la, lb, kbeg, kend, acc, smem);
+}
+
+template <int PIPE, int BM, int BN, class LA, class LB>
+__host__ __device__ constexpr size_t run_mainloop_lds_bytes() {
+  return PIPE == 0 ? mainloop_lds_bytes<BM, BN, LA, LB>() : glds_lds_bytes<BM, BN, PIPE>();
 }
 
 // ---- epilogues -------------------------------------------------------------------------------

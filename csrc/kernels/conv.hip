@@ -86,6 +86,15 @@ struct Im2colRowLoader {
     if (pbase[i] < 0 || tap >= 9 || (unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)Wd) return zero8();
     return *reinterpret_cast<const ushort8_t*>(x + ((int64_t)pbase[i] + ih * Wd + iw) * C + ci);
   }
+  __device__ const void* src(int i, int k0) const {
+    const int tap = k0 / C;
+    const int ci = k0 - tap * C + rm_glds_kc(threadIdx.x + i * kThreads);
+    const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+    const int ih = kFlip ? ih0[i] - kh : ih0[i] + kh;
+    const int iw = kFlip ? iw0[i] - kw : iw0[i] + kw;
+    if (pbase[i] < 0 || tap >= 9 || (unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)Wd) return zero_src();
+    return x + ((int64_t)pbase[i] + ih * Wd + iw) * C + ci;
+  }
 };
 
 // B operand of dgrad: k = (tap, co) rows, n = ci columns, element W[co][tap][ci] (k-major per tap).
@@ -101,10 +110,17 @@ struct WeightTapKLoader {
     if (tap >= 9 || ci >= Cin) return zero8();
     return *reinterpret_cast<const ushort8_t*>(w + ((int64_t)co * 9 + tap) * Cin + ci);
   }
+  __device__ const void* src(int i, int k0) const {
+    const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR;
+    const int tap = k0 / Cout;
+    const int co = k0 - tap * Cout + kr, ci = col0 + km_glds_col<W>(c);
+    if (tap >= 9 || ci >= Cin) return zero_src();
+    return w + ((int64_t)co * 9 + tap) * Cin + ci;
+  }
 };
 
 // B operand of wgrad: k = output pixel rows, n = (tap, ci) columns, element X[src(p, tap)][ci].
-template <int W>
+template <int W, bool kGlds>
 struct Im2colKLoader {
   static constexpr bool kKMajor = true;
   static constexpr int CH = TileGeom<W>::CH;
@@ -115,7 +131,8 @@ struct Im2colKLoader {
   __device__ void init(int col0) {
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
-      const int c = threadIdx.x + i * kThreads, nc = col0 + (c % TileGeom<W>::KPR) * 8;
+      const int c = threadIdx.x + i * kThreads;
+      const int nc = col0 + (kGlds ? km_glds_col<W>(c) : (c % TileGeom<W>::KPR) * 8);
       const int tap = nc / g.Cin;
       ci[i] = nc - tap * g.Cin;
       kh[i] = tap < 9 ? tap / 3 : -100;
@@ -134,10 +151,22 @@ struct Im2colKLoader {
     if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return zero8();
     return *reinterpret_cast<const ushort8_t*>(x + (((int64_t)n * g.H + ih) * g.W + iw) * g.Cin + ci[i]);
   }
+  __device__ const void* src(int i, int k0) const {
+    const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR;
+    const int p = k0 + kr;
+    if (p >= kend || kh[i] < 0) return zero_src();
+    const uint32_t q = fdiv((uint32_t)p, g.fOW);
+    const int ow = p - (int)q * g.OW;
+    const uint32_t n = fdiv(q, g.fOH);
+    const int oh = (int)q - (int)n * g.OH;
+    const int ih = oh * g.stride - 1 + kh[i], iw = ow * g.stride - 1 + kw[i];
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return zero_src();
+    return x + (((int64_t)n * g.H + ih) * g.W + iw) * g.Cin + ci[i];
+  }
 };
 
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, bool kStats>
+template <int BM, int BN, bool kStats, int PIPE>
 __global__ __launch_bounds__(kThreads, 2) void conv3x3_fwd_kernel(const bf16_t* __restrict__ x,
                                                                   const bf16_t* __restrict__ w,
                                                                   bf16_t* __restrict__ y, ConvGeom g,
@@ -157,13 +186,13 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_fwd_kernel(const bf16_t* 
   st.zero();
   Acc<BM, BN> acc;
   acc.zero();
-  mainloop<BM, BN>(la, lb, 0, K, acc, smem_raw);
+  run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
   epilogue_bf16<BM, BN, kStats>(acc, y, g.Cout, P, g.Cout, row0, col0, st, nullptr, 0, smem_raw);
   if constexpr (kStats) stats_flush<BM, BN>(st, stats + (int64_t)bm * g.Cout * 2, g.Cout, col0, smem_raw);
 }
 
 // stride-1 dgrad: dX (the GEMM's M = input pixels, N = Cin), A = dY gathered with flipped taps
-template <int BM, int BN>
+template <int BM, int BN, int PIPE>
 __global__ __launch_bounds__(kThreads, 2) void conv3x3_dgrad_kernel(const bf16_t* __restrict__ dy,
                                                                     const bf16_t* __restrict__ w,
                                                                     bf16_t* __restrict__ dx, ConvGeom g,
@@ -182,12 +211,12 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_dgrad_kernel(const bf16_t
   ColStats<BM, BN> st;
   Acc<BM, BN> acc;
   acc.zero();
-  mainloop<BM, BN>(la, lb, 0, K, acc, smem_raw);
+  run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
   epilogue_bf16<BM, BN, false>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, addend, g.Cin, smem_raw);
 }
 
 // wgrad partial slabs P[split][Cout][9*Cin]
-template <int BM, int BN>
+template <int BM, int BN, int PIPE>
 __global__ __launch_bounds__(kThreads, 2) void conv3x3_wgrad_kernel(const bf16_t* __restrict__ dy,
                                                                     const bf16_t* __restrict__ x, ConvGeom g,
                                                                     float* __restrict__ part, int k_per_split) {
@@ -200,11 +229,11 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_wgrad_kernel(const bf16_t
   const int kend = min(P, kbeg + k_per_split);
   const int m0 = bm * BM, n0 = bn * BN;
   const KLoader<BM> la{dy, g.Cout, m0, Mo, kend};
-  Im2colKLoader<BN> lb{x, g, kend};
+  Im2colKLoader<BN, PIPE != 0> lb{x, g, kend};
   lb.init(n0);
   Acc<BM, BN> acc;
   acc.zero();
-  mainloop<BM, BN>(la, lb, kbeg, kend, acc, smem_raw);
+  run_mainloop<PIPE>(la, lb, kbeg, kend, acc, smem_raw);
   epilogue_f32<BM, BN>(acc, part + (int64_t)blockIdx.y * Mo * No, Mo, No, m0, n0);
 }
 
@@ -224,14 +253,24 @@ static ConvGeom make_geom(int N, int H, int W, int Cin, int Cout, int stride) {
   return g;
 }
 
+template <int BM, int BN, bool S, int PIPE>
+static void launch_fwd_p(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGeom& g, float* stats,
+                         hipStream_t stream) {
+  const int64_t P = (int64_t)g.N * g.OH * g.OW;
+  const int tiles = (int)((P + BM - 1) / BM) * ((g.Cout + BN - 1) / BN);
+  const size_t lds = std::max(run_mainloop_lds_bytes<PIPE, BM, BN, Im2colRowLoader<BM, false>, RowLoader<BN>>(),
+                              epilogue_lds_bytes<BM, BN, S>());
+  hipLaunchKernelGGL((conv3x3_fwd_kernel<BM, BN, S, PIPE>), dim3(tiles), dim3(kThreads), lds, stream, x, w, y, g,
+                     stats);
+}
 template <int BM, int BN, bool S>
 static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGeom& g, float* stats,
                        hipStream_t stream) {
-  const int64_t P = (int64_t)g.N * g.OH * g.OW;
-  const int tiles = (int)((P + BM - 1) / BM) * ((g.Cout + BN - 1) / BN);
-  const size_t lds = std::max(mainloop_lds_bytes<BM, BN, Im2colRowLoader<BM, false>, RowLoader<BN>>(),
-                              epilogue_lds_bytes<BM, BN, S>());
-  hipLaunchKernelGGL((conv3x3_fwd_kernel<BM, BN, S>), dim3(tiles), dim3(kThreads), lds, stream, x, w, y, g, stats);
+  switch (mfma_pipeline_for(9 * g.Cin)) {
+    case 0: launch_fwd_p<BM, BN, S, 0>(x, w, y, g, stats, stream); break;
+    case 3: launch_fwd_p<BM, BN, S, 3>(x, w, y, g, stats, stream); break;
+    default: launch_fwd_p<BM, BN, S, 2>(x, w, y, g, stats, stream); break;
+  }
 }
 
 int conv3x3_stats_rows(int64_t P, int Cout, int tile) {
@@ -256,14 +295,24 @@ void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int
 #undef DLA_CF
 }
 
+template <int BM, int BN, int PIPE>
+static void launch_dgrad_p(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const ConvGeom& g, const bf16_t* addend,
+                           hipStream_t stream) {
+  const int64_t P = (int64_t)g.N * g.H * g.W;
+  const int tiles = (int)((P + BM - 1) / BM) * ((g.Cin + BN - 1) / BN);
+  const size_t lds = std::max(run_mainloop_lds_bytes<PIPE, BM, BN, Im2colRowLoader<BM, true>, WeightTapKLoader<BN>>(),
+                              epilogue_lds_bytes<BM, BN, false>());
+  hipLaunchKernelGGL((conv3x3_dgrad_kernel<BM, BN, PIPE>), dim3(tiles), dim3(kThreads), lds, stream, dy, w, dx, g,
+                     addend);
+}
 template <int BM, int BN>
 static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const ConvGeom& g, const bf16_t* addend,
                          hipStream_t stream) {
-  const int64_t P = (int64_t)g.N * g.H * g.W;
-  const int tiles = (int)((P + BM - 1) / BM) * ((g.Cin + BN - 1) / BN);
-  const size_t lds = std::max(mainloop_lds_bytes<BM, BN, Im2colRowLoader<BM, true>, WeightTapKLoader<BN>>(),
-                              epilogue_lds_bytes<BM, BN, false>());
-  hipLaunchKernelGGL((conv3x3_dgrad_kernel<BM, BN>), dim3(tiles), dim3(kThreads), lds, stream, dy, w, dx, g, addend);
+  switch (mfma_pipeline_for(9 * g.Cout)) {
+    case 0: launch_dgrad_p<BM, BN, 0>(dy, w, dx, g, addend, stream); break;
+    case 3: launch_dgrad_p<BM, BN, 3>(dy, w, dx, g, addend, stream); break;
+    default: launch_dgrad_p<BM, BN, 2>(dy, w, dx, g, addend, stream); break;
+  }
 }
 
 void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
@@ -296,17 +345,23 @@ void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int spl
   int kps = (P + splits - 1) / splits;
   kps = (kps + kBK - 1) / kBK * kBK;
   const int Mo = Cout, No = 9 * Cin;
-  if (Cout <= 64) {
-    const int tiles = ((Mo + 63) / 64) * ((No + 127) / 128);
-    const size_t lds = mainloop_lds_bytes<64, 128, KLoader<64>, Im2colKLoader<128>>();
-    hipLaunchKernelGGL((conv3x3_wgrad_kernel<64, 128>), dim3(tiles, splits), dim3(kThreads), lds, stream,
-                       (const bf16_t*)dy, (const bf16_t*)x, g, partial, kps);
-  } else {
-    const int tiles = ((Mo + 127) / 128) * ((No + 127) / 128);
-    const size_t lds = mainloop_lds_bytes<128, 128, KLoader<128>, Im2colKLoader<128>>();
-    hipLaunchKernelGGL((conv3x3_wgrad_kernel<128, 128>), dim3(tiles, splits), dim3(kThreads), lds, stream,
-                       (const bf16_t*)dy, (const bf16_t*)x, g, partial, kps);
+#define DLA_WG(BM_, P_)                                                                                         \
+  hipLaunchKernelGGL((conv3x3_wgrad_kernel<BM_, 128, P_>), dim3(((Mo + BM_ - 1) / BM_) * ((No + 127) / 128), splits), \
+                     dim3(kThreads), (run_mainloop_lds_bytes<P_, BM_, 128, KLoader<BM_>, Im2colKLoader<128, P_ != 0>>()), \
+                     stream, (const bf16_t*)dy, (const bf16_t*)x, g, partial, kps)
+#define DLA_WG_P(BM_)                   \
+  switch (mfma_pipeline_for(kps)) {     \
+    case 0: DLA_WG(BM_, 0); break;      \
+    case 3: DLA_WG(BM_, 3); break;      \
+    default: DLA_WG(BM_, 2); break;     \
   }
+  if (Cout <= 64) {
+    DLA_WG_P(64)
+  } else {
+    DLA_WG_P(128)
+  }
+#undef DLA_WG_P
+#undef DLA_WG
   launch_splitk_reduce(partial, splits, (int64_t)Mo * No, dw, out_dtype, 1.f, false, stream);
 }
 

@@ -30,7 +30,7 @@ using namespace mm;
 // C[M,N] = A[M,K] * B[N,K]^T   (A K-contiguous; B K-contiguous, or k-major [K][N] when kBT),
 // bf16 in/out, fp32 accumulate, optional fused addend and BN-statistics epilogue.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, bool kStats, bool kBT>
+template <int BM, int BN, bool kStats, bool kBT, int PIPE>
 __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               bf16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
@@ -49,10 +49,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const bf16_t* __re
   const RowLoader<BM> la{A, lda, row0, M, K};
   if constexpr (kBT) {
     const KLoader<BN> lb{B, ldb, col0, N, K};
-    mainloop<BM, BN>(la, lb, 0, K, acc, smem_raw);
+    run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
   } else {
     const RowLoader<BN> lb{B, ldb, (int64_t)col0, N, K};
-    mainloop<BM, BN>(la, lb, 0, K, acc, smem_raw);
+    run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
   }
   epilogue_bf16<BM, BN, kStats>(acc, C, ldc, M, N, row0, col0, st, D, ldd, smem_raw);
   if constexpr (kStats) stats_flush<BM, BN>(st, stats + (int64_t)bm * N * 2, N, col0, smem_raw);
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const bf16_t* __re
 // P[split][Mo, No] = sum_{k in split} A[k][m] * B[k][n]   (A: [K, lda] m-contiguous, B: [K, ldb])
 // fp32 partial slabs; splitk_reduce_kernel sums them.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN>
+template <int BM, int BN, int PIPE>
 __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               float* __restrict__ P, int Mo, int No, int K,
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(const bf16_t* __re
   acc.zero();
   const KLoader<BM> la{A, lda, m0, Mo, kend};
   const KLoader<BN> lb{B, ldb, n0, No, kend};
-  mainloop<BM, BN>(la, lb, kbeg, kend, acc, smem_raw);
+  run_mainloop<PIPE>(la, lb, kbeg, kend, acc, smem_raw);
   epilogue_f32<BM, BN>(acc, P + (int64_t)blockIdx.y * Mo * No, Mo, No, m0, n0);
 }
 
@@ -120,15 +120,35 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // ---------------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------------
+// MFMA main-loop pipeline (dla_mfma.h run_mainloop). -1 = per shape, from scripts/bench_gemm.py /
+// bench_conv.py on MI355X: the 2-stage LDS-DMA loop wins once a block runs several k-steps
+// (K >= 256: up to 1.45x at K = 1024-2048; every 3x3 conv, K >= 576); at K <= 128 a block has one or
+// two k-steps, nothing to overlap, and the register-staged loop's third resident block wins.
+// 3 stages (96 KB of LDS, 1 block/CU) never won at ResNet shapes.
+static int g_pipe = -1;
+void set_mfma_pipeline(int p) { g_pipe = (p == 0 || p == 2 || p == 3) ? p : -1; }
+int mfma_pipeline() { return g_pipe; }
+int mfma_pipeline_for(int K) { return g_pipe >= 0 ? g_pipe : (K >= 256 ? 2 : 0); }
+
+template <int BM, int BN, bool S, bool BT, int PIPE>
+static void launch_nt_p(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
+                        int N, int K, float* stats, const bf16_t* D, int64_t ldd, hipStream_t stream) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const size_t ab = BT ? run_mainloop_lds_bytes<PIPE, BM, BN, RowLoader<BM>, KLoader<BN>>()
+                       : run_mainloop_lds_bytes<PIPE, BM, BN, RowLoader<BM>, RowLoader<BN>>();
+  const size_t cs = epilogue_lds_bytes<BM, BN, S>();
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, S, BT, PIPE>), dim3(tiles), dim3(kThreads), std::max(ab, cs), stream, A,
+                     lda, B, ldb, C, ldc, M, N, K, stats, D, ldd);
+}
+
 template <int BM, int BN, bool S, bool BT>
 static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
                       int N, int K, float* stats, const bf16_t* D, int64_t ldd, hipStream_t stream) {
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  const size_t ab = BT ? mainloop_lds_bytes<BM, BN, RowLoader<BM>, KLoader<BN>>()
-                       : mainloop_lds_bytes<BM, BN, RowLoader<BM>, RowLoader<BN>>();
-  const size_t cs = epilogue_lds_bytes<BM, BN, S>();
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, S, BT>), dim3(tiles), dim3(kThreads), std::max(ab, cs), stream, A, lda, B,
-                     ldb, C, ldc, M, N, K, stats, D, ldd);
+  switch (mfma_pipeline_for(K)) {
+    case 0: launch_nt_p<BM, BN, S, BT, 0>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, stream); break;
+    case 3: launch_nt_p<BM, BN, S, BT, 3>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, stream); break;
+    default: launch_nt_p<BM, BN, S, BT, 2>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, stream); break;
+  }
 }
 
 int pick_tile(int64_t M, int N, int tile) {
@@ -179,9 +199,16 @@ void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, floa
   int kps = (K + splits - 1) / splits;
   kps = (kps + kBK - 1) / kBK * kBK;
   const int tiles = ((Mo + 127) / 128) * ((No + 127) / 128);
-  const size_t lds = mainloop_lds_bytes<128, 128, KLoader<128>, KLoader<128>>();
-  hipLaunchKernelGGL((gemm_tn_kernel<128, 128>), dim3(tiles, splits), dim3(kThreads), lds, stream,
-                     (const bf16_t*)A, lda, (const bf16_t*)B, ldb, partial, Mo, No, K, kps);
+#define DLA_TN(P_)                                                                                            \
+  hipLaunchKernelGGL((gemm_tn_kernel<128, 128, P_>), dim3(tiles, splits), dim3(kThreads),                     \
+                     (run_mainloop_lds_bytes<P_, 128, 128, KLoader<128>, KLoader<128>>()), stream, (const bf16_t*)A, \
+                     lda, (const bf16_t*)B, ldb, partial, Mo, No, K, kps)
+  switch (mfma_pipeline_for(kps)) {
+    case 0: DLA_TN(0); break;
+    case 3: DLA_TN(3); break;
+    default: DLA_TN(2); break;
+  }
+#undef DLA_TN
   launch_splitk_reduce(partial, splits, (int64_t)Mo * No, out, out_dtype, scale, accumulate, stream);
 }
 

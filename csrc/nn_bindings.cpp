@@ -276,6 +276,8 @@ at::Tensor conv3x3_wgrad(at::Tensor dy, at::Tensor x, int64_t stride, c10::Scala
 }
 
 void bind_nn(pybind11::module& m) {
+  m.def("set_mfma_pipeline", &set_mfma_pipeline, "MFMA main loop: 0 register staging, 2/3 LDS-DMA stages, -1 per-shape auto");
+  m.def("mfma_pipeline", &mfma_pipeline);
   m.def("conv3x3_fwd", &conv3x3_fwd, "implicit-GEMM 3x3/pad-1 conv forward (NHWC bf16, MFMA)", pybind11::arg("x"),
         pybind11::arg("w"), pybind11::arg("stride") = 1, pybind11::arg("stats") = false, pybind11::arg("tile") = 0);
   m.def("conv3x3_dgrad", &conv3x3_dgrad, "implicit-GEMM 3x3 conv data gradient (stride 1)", pybind11::arg("dy"),

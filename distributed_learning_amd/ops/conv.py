@@ -142,11 +142,12 @@ def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
 # ---------------------------------------------------------------------------------------------
 # 3x3 convolutions (csrc/kernels/conv.hip): implicit GEMMs gathered straight from NHWC tensors.
 # Per-pass engine choice from scripts/bench_conv.py at the ResNet-50 bs256 shapes on MI355X
-# (profiles/conv3x3_native_vs_miopen.md): the native weight gradient beats MIOpen's at every shape
-# (and drops MIOpen's zero-fill/cast kernels around it); the forward stays on MIOpen; the native
-# data gradient wins on the 64-channel 56x56 layer.
+# (profiles/conv3x3_native_vs_miopen.md), with the 2-stage LDS-DMA main loop: the native forward
+# beats MIOpen on 5 of the 7 shapes (and its epilogue yields the BatchNorm statistics, saving a
+# pass over the output), the stride-1 data gradient and the weight gradient win everywhere. MIOpen
+# keeps the 3 stride-2 data gradients.
 # ---------------------------------------------------------------------------------------------
-CONV3_POLICY = {"fwd": "miopen", "dgrad_native_max_cin": 64, "wgrad": "native"}
+CONV3_POLICY = {"fwd": "native", "dgrad_native_max_cin": 1 << 30, "wgrad": "native"}
 
 
 def supported3x3(x: torch.Tensor, conv: nn.Conv2d) -> bool:

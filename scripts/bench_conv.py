@@ -40,10 +40,13 @@ for (N, Cin, H, Cout, stride) in [(256, 64, 56, 64, 1), (256, 128, 56, 128, 2), 
     r["fwd_native"] = timeit(lambda: C.conv3x3_fwd(x, w, stride, False))
     r["fwd_native_stats"] = timeit(lambda: C.conv3x3_fwd(x, w, stride, True))
     r["fwd_miopen"] = timeit(lambda: F.conv2d(x, w, None, stride, 1))
-    for t in (1, 2, 3):
-        r[f"fwd_t{t}"] = timeit(lambda: C.conv3x3_fwd(x, w, stride, True, t))
+    for pipe in (0, 2, 3):
+        C.set_mfma_pipeline(pipe)
+        r[f"fwd_p{pipe}"] = timeit(lambda: C.conv3x3_fwd(x, w, stride, True))
         if stride == 1:
-            r[f"dgrad_t{t}"] = timeit(lambda: C.conv3x3_dgrad(dy, w, None, t))
+            r[f"dgrad_p{pipe}"] = timeit(lambda: C.conv3x3_dgrad(dy, w))
+        r[f"wgrad_p{pipe}"] = timeit(lambda: C.conv3x3_wgrad(dy, x, stride, torch.bfloat16))
+    C.set_mfma_pipeline(-1)
     if stride == 1:
         r["dgrad_native"] = timeit(lambda: C.conv3x3_dgrad(dy, w))
     r["dgrad_miopen"] = timeit(lambda: torch.ops.aten.convolution_backward(

@@ -52,9 +52,12 @@ for M, Cin, Cout in shapes:
     r["fwd_miopen_conv_ms"] = timeit(lambda: torch.nn.functional.conv2d(x4, w4))
     r["dgrad_native_ms"] = timeit(lambda: C.gemm_nt(dY, Wt, False))
     r["dgrad_native_kmajor_ms"] = timeit(lambda: C.gemm_nt(dY, W, False, None, True))
-    for t in (1, 2, 3):
-        r[f"fwd_t{t}"] = timeit(lambda: C.gemm_nt(X, W, True, None, False, t))
-        r[f"dgrad_t{t}"] = timeit(lambda: C.gemm_nt(dY, W, False, None, True, t))
+    for pipe in (0, 2, 3):
+        C.set_mfma_pipeline(pipe)
+        r[f"fwd_p{pipe}"] = timeit(lambda: C.gemm_nt(X, W, True))
+        r[f"dgrad_p{pipe}"] = timeit(lambda: C.gemm_nt(dY, W, False, None, True))
+        r[f"wgrad_p{pipe}"] = timeit(lambda: C.gemm_tn(dY, X, torch.float32, 1.0))
+    C.set_mfma_pipeline(-1)
     r["dgrad_torch_mm_ms"] = timeit(lambda: dY @ W)
     r["wgrad_native_ms"] = timeit(lambda: C.gemm_tn(dY, X, torch.float32, 1.0))
     r["wgrad_torch_mm_ms"] = timeit(lambda: dY.t() @ X)

@@ -79,3 +79,24 @@ def test_conv3x3_tile_configs(cuda, tile):
     torch.testing.assert_close(s.sum(0), s_ref.sum(0), rtol=1e-5, atol=1e-3)
     dy = torch.randn_like(y)
     assert torch.equal(C.conv3x3_dgrad(dy, w, None, tile), C.conv3x3_dgrad(dy, w, None, 1))
+
+
+@pytest.mark.parametrize("pipe", [0, 2, 3])
+def test_conv3x3_pipelines_agree(cuda, pipe):
+    C = _C()
+    torch.manual_seed(0)
+    x = torch.randn(2, 64, 9, 13, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(128, 64, 3, 3, device=cuda) * 0.05).to(torch.bfloat16).contiguous(memory_format=CL)
+    dy = torch.randn(2, 128, 9, 13, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    old = C.mfma_pipeline()
+    try:
+        C.set_mfma_pipeline(0)
+        ref = [C.conv3x3_fwd(x, w, 1, True)[0], C.conv3x3_dgrad(dy, w), C.conv3x3_wgrad(dy, x, 1, torch.float32),
+               C.conv3x3_fwd(x, w, 2, False)[0]]
+        C.set_mfma_pipeline(pipe)
+        got = [C.conv3x3_fwd(x, w, 1, True)[0], C.conv3x3_dgrad(dy, w), C.conv3x3_wgrad(dy, x, 1, torch.float32),
+               C.conv3x3_fwd(x, w, 2, False)[0]]
+    finally:
+        C.set_mfma_pipeline(old)
+    for r, g in zip(ref, got):
+        assert torch.equal(r, g)

@@ -85,3 +85,27 @@ def test_gemm_nt_tile_configs(cuda, tile, M, N, K):
     torch.testing.assert_close(stats.sum(0)[:, 0], out.float().sum(0), rtol=1e-4, atol=1e-2 * M ** 0.5)
     outk, _ = C.gemm_nt(A, B.t().contiguous(), False, None, True, tile)
     assert torch.equal(outk, ref)
+
+
+@pytest.mark.parametrize("pipe", [0, 2, 3])
+def test_mfma_pipelines_agree(cuda, pipe):
+    """Register-staged and LDS-DMA (2/3-stage) main loops: identical results for every kernel
+    family (same MFMA order), including ragged edges and the transposed-read operands."""
+    C = _C()
+    torch.manual_seed(0)
+    A = torch.randn(1000, 200, device=cuda).to(torch.bfloat16)
+    B = torch.randn(136, 200, device=cuda).to(torch.bfloat16)
+    Bk = torch.randn(200, 136, device=cuda).to(torch.bfloat16)
+    T1 = torch.randn(3000, 136, device=cuda).to(torch.bfloat16)
+    T2 = torch.randn(3000, 72, device=cuda).to(torch.bfloat16)
+    old = C.mfma_pipeline()
+    try:
+        C.set_mfma_pipeline(0)
+        ref = [C.gemm_nt(A, B, True)[0], C.gemm_nt(A, Bk, False, None, True)[0], C.gemm_tn(T1, T2)]
+        C.set_mfma_pipeline(pipe)
+        got = [C.gemm_nt(A, B, True)[0], C.gemm_nt(A, Bk, False, None, True)[0], C.gemm_tn(T1, T2)]
+    finally:
+        C.set_mfma_pipeline(old)
+    for r, g in zip(ref, got):
+        assert torch.equal(r, g)
+    torch.testing.assert_close(got[0].float(), A.float() @ B.float().t(), rtol=1e-2, atol=0.15)
