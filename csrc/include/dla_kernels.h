@@ -98,9 +98,11 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
                    int ext_nrb = 0, uint8_t* relu_mask = nullptr);
 // mask_mode: 0 no ReLU, 1 recompute from x (ReLU right after BN), 2 1-bit mask written by the
 // forward (ReLU after the residual add), 3 from the saved output y.
+// ext_part/ext_nrb: the reduction pass's partials were already produced (GEMM epilogue, BnBwdArgs).
 void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const void* x, void* dx, void* dres,
                    int64_t M, int C, int dtype, const float* gamma, float* ws, float* part, float* dgamma,
-                   float* dbeta, int mask_mode, hipStream_t stream);
+                   float* dbeta, int mask_mode, hipStream_t stream, const float* ext_part = nullptr,
+                   int ext_nrb = 0);
 
 // ---- max pooling, NHWC (pool.hip) ------------------------------------------------------------
 // x [N,H,W,C], y/pos [N,OH,OW,C] (pos: window position k*ky+kx of the max, 1 byte), C % 8 == 0,
@@ -127,9 +129,19 @@ inline int tile_bm(int cfg) { return cfg == kTile64x64 ? 64 : 128; }
 inline int tile_bn(int cfg) { return cfg == kTile128x128 ? 128 : 64; }
 // rows of BN-statistics partials ([rows][N][2]) a stats-producing launch writes (one per row tile)
 int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto);
+// BatchNorm-backward reduction fused into a bf16-output GEMM epilogue (the output is the BN's dy):
+// x = the BN input [M, N], ws = its 7N workspace, mask/mode as launch_bn_bwd (0, 1 or 2),
+// part = [stats_rows][N][2] partial (sum dy', sum dy'(x - mean)).
+struct BnBwdArgs {
+  const void* x;
+  const float* ws;
+  const uint8_t* mask;
+  int mode;
+  float* part;
+};
 void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
                     float* stats, hipStream_t stream, const void* addend = nullptr, int64_t ld_addend = 0,
-                    bool b_kmajor = false, int tile = kTileAuto);
+                    bool b_kmajor = false, int tile = kTileAuto, const BnBwdArgs* bn_bwd = nullptr);
 // out[Mo,No] (= scale * A^T B [+ out]) with A [K, lda>=Mo], B [K, ldb>=No]; partial: splits*Mo*No f32.
 int gemm_tn_splits(int Mo, int No, int K);
 void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, float* partial, int splits, int Mo, int No,
@@ -147,7 +159,8 @@ int conv3x3_stats_rows(int64_t P, int Cout, int tile = kTileAuto);
 void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout, int stride,
                         float* stats, hipStream_t stream, int tile = kTileAuto);
 void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
-                          const void* addend, hipStream_t stream, int tile = kTileAuto);
+                          const void* addend, hipStream_t stream, int tile = kTileAuto,
+                          const BnBwdArgs* bn_bwd = nullptr);
 int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int stride);
 void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int splits, void* dw, int out_dtype, int N,
                           int H, int W, int Cin, int Cout, int stride, hipStream_t stream);

@@ -338,9 +338,10 @@ __host__ __device__ constexpr size_t run_mainloop_lds_bytes() {
 // ---- epilogues -------------------------------------------------------------------------------
 template <int BM, int BN, bool kStats>
 __host__ __device__ constexpr size_t epilogue_lds_bytes() {
-  return (size_t)BM * (BN + 8) * sizeof(bf16_t) > (size_t)4 * BN * sizeof(float)
-             ? (size_t)BM * (BN + 8) * sizeof(bf16_t)
-             : (size_t)4 * BN * sizeof(float);
+  // C staging tile; the BN-backward partial combine ([256 / (BN/8)][BN][2] floats = 16 KB) and the
+  // statistics flush reuse the same bytes afterwards
+  return (size_t)BM * (BN + 8) * sizeof(bf16_t) > (size_t)16384 ? (size_t)BM * (BN + 8) * sizeof(bf16_t)
+                                                                 : (size_t)16384;
 }
 
 // Column statistics of a block's output tile(s): a lane owns one column of each 16x16 fragment, so
@@ -357,10 +358,25 @@ struct ColStats {
 // bf16 C tile -> LDS -> coalesced 16-byte row stores, optional fused addend D (C = bf16(bf16(acc) + D),
 // exactly the unfused bf16 add); with kStats, the stored values' per-column (sum, sumsq) are added
 // to `st` straight from the accumulator registers. Ends with a barrier (LDS free for the next tile).
+// BatchNorm-backward statistics of a GEMM output that IS the gradient dy of a fused BN(+ReLU)
+// (the dgrad of the conv that consumes the BN's output): per channel (column) the partial sums of
+// dy' and dy' * (x - mean) over the tile's rows, dy' = dy masked by the BN's ReLU (recomputed from
+// x with the forward's scale/shift, or read from its 1-bit mask) — exactly the BN backward's
+// reduction pass, without re-reading dy from HBM. ws: the BN's 7C workspace (mean | invstd |
+// scale | shift | ...); mode as launch_bn_bwd (0 none, 1 recompute, 2 bits).
+struct BnBwdEpi {
+  const bf16_t* x;
+  const float* ws;
+  const uint8_t* mask;
+  int mode;
+  float* part;  // [row tiles][N][2]
+};
+
 template <int BM, int BN, bool kStats>
 __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __restrict__ C, int64_t ldc, int64_t M,
                                               int N, int64_t row0, int col0, ColStats<BM, BN>& st,
-                                              const bf16_t* __restrict__ D, int64_t ldd, char* smem) {
+                                              const bf16_t* __restrict__ D, int64_t ldd, char* smem,
+                                              const BnBwdEpi* bnb = nullptr, int bm = 0) {
   constexpr int WM = Acc<BM, BN>::WM, WN = Acc<BM, BN>::WN, TM = Acc<BM, BN>::TM, TN = Acc<BM, BN>::TN;
   constexpr int LDS_C = BN + 8;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
@@ -383,7 +399,39 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
       }
   __syncthreads();
   constexpr int CPR = BN / 8;
-  for (int c = tid; c < BM * CPR; c += kThreads) {
+  static_assert(kThreads % CPR == 0, "a thread keeps one 8-column group in the store loop");
+  // BN-backward partials: this thread's 8 columns are fixed (c % CPR) across its rows. The x (and
+  // mask) chunks of all its rows are loaded up front, so those global loads overlap each other and
+  // the C stores instead of each waiting a full round trip inside the loop.
+  constexpr int NIT = BM * CPR / kThreads;
+  static_assert(BM * CPR % kThreads == 0, "whole store-loop iterations");
+  const int my_cc = (tid % CPR) * 8;
+  float bs[8], bq[8], mean[8], sc[8], sh[8];
+  ushort8_t xr[NIT];
+  uint32_t mr[NIT];
+  if (bnb) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bs[j] = bq[j] = 0.f;
+      const int gc = min(col0 + my_cc + j, N - 1);
+      mean[j] = bnb->ws[gc];
+      sc[j] = bnb->ws[2 * N + gc];
+      sh[j] = bnb->ws[3 * N + gc];
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int r = (tid + it * kThreads) / CPR;
+      const int64_t gm = row0 + r;
+      const int gn = col0 + my_cc;
+      const bool ok = gm < M && gn < N;
+      const int64_t off = ok ? gm * ldc + gn : 0;
+      xr[it] = ok ? *reinterpret_cast<const ushort8_t*>(bnb->x + off) : zero8();
+      mr[it] = (ok && bnb->mode == 2) ? (uint32_t)bnb->mask[off >> 3] : 0xffu;
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = tid + it * kThreads;
     const int r = c / CPR, cc = (c % CPR) * 8;
     const int64_t gm = row0 + r;
     const int gn = col0 + cc;
@@ -395,9 +443,39 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
         for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(d[j]));
       }
       *reinterpret_cast<ushort8_t*>(C + gm * ldc + gn) = v;
+      if (bnb) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xf = bf16_to_f32(xr[it][j]);
+          float g = bf16_to_f32(v[j]);
+          if (bnb->mode == 1) g = fmaf(xf, sc[j], sh[j]) > 0.f ? g : 0.f;  // same fmaf as the forward
+          else if (bnb->mode == 2) g = ((mr[it] >> j) & 1u) ? g : 0.f;
+          bs[j] += g;
+          bq[j] = fmaf(g, xf - mean[j], bq[j]);
+        }
+      }
     }
   }
   __syncthreads();
+  if (bnb) {
+    // combine the kThreads / CPR row groups of each column through LDS (the C staging is free now)
+    constexpr int RG = kThreads / CPR;
+    float* red = reinterpret_cast<float*>(smem);  // [RG][BN][2]
+    const int rg = tid / CPR;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(rg * BN + my_cc + j) * 2 + 0] = bs[j];
+      red[(rg * BN + my_cc + j) * 2 + 1] = bq[j];
+    }
+    __syncthreads();
+    for (int idx = tid; idx < BN * 2; idx += kThreads) {
+      float a = 0.f;
+      for (int g = 0; g < RG; ++g) a += red[g * BN * 2 + idx];
+      const int col = idx >> 1;
+      if (col0 + col < N) bnb->part[((int64_t)bm * N + col0 + col) * 2 + (idx & 1)] = a;
+    }
+    __syncthreads();
+  }
 }
 
 // Writes a block's accumulated column statistics as one partial row: out[N][2] at columns col0..

@@ -406,9 +406,18 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
 
 void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const void* x, void* dx, void* dres,
                    int64_t M, int C, int dtype, const float* gamma, float* ws, float* part, float* dgamma,
-                   float* dbeta, int mask_mode, hipStream_t stream) {
+                   float* dbeta, int mask_mode, hipStream_t stream, const float* ext_part, int ext_nrb) {
   int tpr, nrb, nct;
   bn_geometry(M, C, &tpr, &nrb, &nct);
+  if (ext_part) {
+    // reduction pass already fused into the producer GEMM's epilogue
+    if (ext_nrb > 1024)
+      hipLaunchKernelGGL(bn_bwd_finalize_kernel<4>, dim3(C), dim3(256), 0, stream, ext_part, ext_nrb, M, C, gamma, ws,
+                         dgamma, dbeta);
+    else
+      hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, ext_part, ext_nrb, M, C,
+                         gamma, ws, dgamma, dbeta);
+  } else {
   const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
 #define DLA_BN_RED(T, K)                                                                                          \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, K>), dim3(nct, nrb), dim3(kBNThreads), lds, stream, (const T*)dy,     \
@@ -425,6 +434,7 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
 #undef DLA_BN_RED
   hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, part, nrb, M, C, gamma, ws,
                      dgamma, dbeta);
+  }
   int atpr, anrb, anct;
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
 #define DLA_BN_BAPPLY(T, K, D)                                                                                      \

@@ -196,7 +196,7 @@ template <int BM, int BN, int PIPE>
 __global__ __launch_bounds__(kThreads, 2) void conv3x3_dgrad_kernel(const bf16_t* __restrict__ dy,
                                                                     const bf16_t* __restrict__ w,
                                                                     bf16_t* __restrict__ dx, ConvGeom g,
-                                                                    const bf16_t* __restrict__ addend) {
+                                                                    const bf16_t* __restrict__ addend, BnBwdEpi bnb) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int64_t P = (int64_t)g.N * g.H * g.W;  // stride 1: OH = H, OW = W
   const int nbn = (g.Cin + BN - 1) / BN;
@@ -212,7 +212,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_dgrad_kernel(const bf16_t
   Acc<BM, BN> acc;
   acc.zero();
   run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
-  epilogue_bf16<BM, BN, false>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, addend, g.Cin, smem_raw);
+  epilogue_bf16<BM, BN, false>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, addend, g.Cin, smem_raw,
+                               bnb.x ? &bnb : nullptr, bm);
 }
 
 // wgrad partial slabs P[split][Cout][9*Cin]
@@ -297,34 +298,36 @@ void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int
 
 template <int BM, int BN, int PIPE>
 static void launch_dgrad_p(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const ConvGeom& g, const bf16_t* addend,
-                           hipStream_t stream) {
+                           const BnBwdEpi& bnb, hipStream_t stream) {
   const int64_t P = (int64_t)g.N * g.H * g.W;
   const int tiles = (int)((P + BM - 1) / BM) * ((g.Cin + BN - 1) / BN);
   const size_t lds = std::max(run_mainloop_lds_bytes<PIPE, BM, BN, Im2colRowLoader<BM, true>, WeightTapKLoader<BN>>(),
                               epilogue_lds_bytes<BM, BN, false>());
   hipLaunchKernelGGL((conv3x3_dgrad_kernel<BM, BN, PIPE>), dim3(tiles), dim3(kThreads), lds, stream, dy, w, dx, g,
-                     addend);
+                     addend, bnb);
 }
 template <int BM, int BN>
 static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const ConvGeom& g, const bf16_t* addend,
-                         hipStream_t stream) {
+                         const BnBwdEpi& bnb, hipStream_t stream) {
   switch (mfma_pipeline_for(9 * g.Cout)) {
-    case 0: launch_dgrad_p<BM, BN, 0>(dy, w, dx, g, addend, stream); break;
-    case 3: launch_dgrad_p<BM, BN, 3>(dy, w, dx, g, addend, stream); break;
-    default: launch_dgrad_p<BM, BN, 2>(dy, w, dx, g, addend, stream); break;
+    case 0: launch_dgrad_p<BM, BN, 0>(dy, w, dx, g, addend, bnb, stream); break;
+    case 3: launch_dgrad_p<BM, BN, 3>(dy, w, dx, g, addend, bnb, stream); break;
+    default: launch_dgrad_p<BM, BN, 2>(dy, w, dx, g, addend, bnb, stream); break;
   }
 }
 
 void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
-                          const void* addend, hipStream_t stream, int tile) {
+                          const void* addend, hipStream_t stream, int tile, const BnBwdArgs* bn_bwd) {
   const ConvGeom g = make_geom(N, H, W, Cin, Cout, 1);
+  const BnBwdEpi bnb = bn_bwd ? BnBwdEpi{(const bf16_t*)bn_bwd->x, bn_bwd->ws, bn_bwd->mask, bn_bwd->mode, bn_bwd->part}
+                              : BnBwdEpi{nullptr, nullptr, nullptr, 0, nullptr};
   const bf16_t* d = (const bf16_t*)dy;
   const bf16_t* wp = (const bf16_t*)w;
   const bf16_t* ad = (const bf16_t*)addend;
   switch (pick_tile((int64_t)N * H * W, Cin, tile)) {
-    case kTile128x128: launch_dgrad<128, 128>(d, wp, (bf16_t*)dx, g, ad, stream); break;
-    case kTile128x64: launch_dgrad<128, 64>(d, wp, (bf16_t*)dx, g, ad, stream); break;
-    default: launch_dgrad<64, 64>(d, wp, (bf16_t*)dx, g, ad, stream); break;
+    case kTile128x128: launch_dgrad<128, 128>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
+    case kTile128x64: launch_dgrad<128, 64>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
+    default: launch_dgrad<64, 64>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
   }
 }
 

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const bf16_t* __re
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               bf16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
                                                               float* __restrict__ stats, const bf16_t* __restrict__ D,
-                                                              int64_t ldd) {
+                                                              int64_t ldd, BnBwdEpi bnb) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int nbn = (N + BN - 1) / BN;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const bf16_t* __re
     const RowLoader<BN> lb{B, ldb, (int64_t)col0, N, K};
     run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
   }
-  epilogue_bf16<BM, BN, kStats>(acc, C, ldc, M, N, row0, col0, st, D, ldd, smem_raw);
+  epilogue_bf16<BM, BN, kStats>(acc, C, ldc, M, N, row0, col0, st, D, ldd, smem_raw, bnb.x ? &bnb : nullptr, bm);
   if constexpr (kStats) stats_flush<BM, BN>(st, stats + (int64_t)bm * N * 2, N, col0, smem_raw);
 }
 
@@ -132,22 +132,24 @@ int mfma_pipeline_for(int K) { return g_pipe >= 0 ? g_pipe : (K >= 256 ? 2 : 0);
 
 template <int BM, int BN, bool S, bool BT, int PIPE>
 static void launch_nt_p(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
-                        int N, int K, float* stats, const bf16_t* D, int64_t ldd, hipStream_t stream) {
+                        int N, int K, float* stats, const bf16_t* D, int64_t ldd, const BnBwdEpi& bnb,
+                        hipStream_t stream) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const size_t ab = BT ? run_mainloop_lds_bytes<PIPE, BM, BN, RowLoader<BM>, KLoader<BN>>()
                        : run_mainloop_lds_bytes<PIPE, BM, BN, RowLoader<BM>, RowLoader<BN>>();
   const size_t cs = epilogue_lds_bytes<BM, BN, S>();
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, S, BT, PIPE>), dim3(tiles), dim3(kThreads), std::max(ab, cs), stream, A,
-                     lda, B, ldb, C, ldc, M, N, K, stats, D, ldd);
+                     lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb);
 }
 
 template <int BM, int BN, bool S, bool BT>
 static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
-                      int N, int K, float* stats, const bf16_t* D, int64_t ldd, hipStream_t stream) {
+                      int N, int K, float* stats, const bf16_t* D, int64_t ldd, const BnBwdEpi& bnb,
+                      hipStream_t stream) {
   switch (mfma_pipeline_for(K)) {
-    case 0: launch_nt_p<BM, BN, S, BT, 0>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, stream); break;
-    case 3: launch_nt_p<BM, BN, S, BT, 3>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, stream); break;
-    default: launch_nt_p<BM, BN, S, BT, 2>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, stream); break;
+    case 0: launch_nt_p<BM, BN, S, BT, 0>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
+    case 3: launch_nt_p<BM, BN, S, BT, 3>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
+    default: launch_nt_p<BM, BN, S, BT, 2>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
   }
 }
 
@@ -164,12 +166,16 @@ int gemm_nt_stats_rows(int M, int N, int tile) {
 }
 
 void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
-                    float* stats, hipStream_t stream, const void* addend, int64_t ld_addend, bool b_kmajor, int tile) {
+                    float* stats, hipStream_t stream, const void* addend, int64_t ld_addend, bool b_kmajor, int tile,
+                    const BnBwdArgs* bn_bwd) {
+  const BnBwdEpi bnb = bn_bwd ? BnBwdEpi{(const bf16_t*)bn_bwd->x, bn_bwd->ws, bn_bwd->mask, bn_bwd->mode, bn_bwd->part}
+                              : BnBwdEpi{nullptr, nullptr, nullptr, 0, nullptr};
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* b = (const bf16_t*)B;
   bf16_t* c = (bf16_t*)C;
   const bf16_t* d = (const bf16_t*)addend;
-#define DLA_NT(BM_, BN_, S_, BT_) launch_nt<BM_, BN_, S_, BT_>(a, lda, b, ldb, c, ldc, M, N, K, stats, d, ld_addend, stream)
+#define DLA_NT(BM_, BN_, S_, BT_) \
+  launch_nt<BM_, BN_, S_, BT_>(a, lda, b, ldb, c, ldc, M, N, K, stats, d, ld_addend, bnb, stream)
 #define DLA_NT_ST(BM_, BN_)                                \
   if (stats) {                                             \
     if (b_kmajor) DLA_NT(BM_, BN_, true, true); else DLA_NT(BM_, BN_, true, false);    \

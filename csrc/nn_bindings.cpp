@@ -84,7 +84,7 @@ std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> resid
 // 1 recompute the ReLU branch from x, 2 use `mask` from bn_act_fwd, 3 use the saved output `y`.
 std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, c10::optional<at::Tensor> mask,
                                    at::Tensor x, at::Tensor ws, c10::optional<at::Tensor> weight, int64_t mask_mode,
-                                   bool need_dres) {
+                                   bool need_dres, c10::optional<at::Tensor> ext_part) {
   dy = dy.dim() == 4 ? dy.contiguous(at::MemoryFormat::ChannelsLast) : dy.contiguous();
   check_act(dy, "dy");
   check_act(x, "x");
@@ -107,15 +107,40 @@ std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, c
   }
   TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "dy dtype must match x");
   auto f32 = x.options().dtype(at::kFloat);
-  at::Tensor part = at::empty({partial_floats(M, C)}, f32);
+  const bool ext = ext_part.has_value() && ext_part->defined();
+  if (ext)
+    TORCH_CHECK(ext_part->scalar_type() == at::kFloat && ext_part->is_contiguous() && ext_part->dim() == 3 &&
+                    ext_part->size(1) == C && ext_part->size(2) == 2,
+                "ext_part must be fp32 [rows, C, 2] (sum dy', sum dy'(x-mean)) partials");
+  at::Tensor part = at::empty({ext ? 1 : partial_floats(M, C)}, f32);
   at::Tensor dx = at::empty_like(x);
   at::Tensor dres = need_dres ? at::empty_like(x) : at::Tensor();
   at::Tensor dg = at::empty({C}, f32), db = at::empty({C}, f32);
   const float* g = (weight.has_value() && weight->defined()) ? weight->data_ptr<float>() : nullptr;
   launch_bn_bwd(dy.data_ptr(), yp, mp, x.data_ptr(), dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr, M, C,
                 dtype_code(x), g, ws.data_ptr<float>(), part.data_ptr<float>(), dg.data_ptr<float>(),
-                db.data_ptr<float>(), (int)mask_mode, current_stream(x));
+                db.data_ptr<float>(), (int)mask_mode, current_stream(x), ext ? ext_part->data_ptr<float>() : nullptr,
+                ext ? (int)ext_part->size(0) : 0);
   return {dx, dres, dg, db};
+}
+
+// BN-backward epilogue operands (see BnBwdArgs): x_bn is the BN input laid out like the GEMM output.
+static BnBwdArgs make_bn_bwd(const at::Tensor& x_bn, const at::Tensor& ws, const c10::optional<at::Tensor>& mask,
+                             int64_t mode, int64_t M, int64_t N, int64_t rows, at::Tensor& part) {
+  TORCH_CHECK(x_bn.is_cuda() && x_bn.scalar_type() == at::kBFloat16 && x_bn.numel() == M * N &&
+                  (x_bn.dim() == 2 ? x_bn.is_contiguous() : x_bn.is_contiguous(at::MemoryFormat::ChannelsLast)) &&
+                  x_bn.size(1) == N,
+              "bn epilogue: x must be the bf16 BN input with the GEMM output's shape/layout");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() == 7 * N, "bn epilogue: ws must be the 7C workspace");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "bn epilogue: mode 0 (no ReLU), 1 (recompute) or 2 (bit mask)");
+  const uint8_t* mp = nullptr;
+  if (mode == 2) {
+    TORCH_CHECK(mask.has_value() && mask->defined() && mask->scalar_type() == at::kByte && mask->numel() * 8 >= M * N,
+                "bn epilogue: mode 2 needs the forward's bit mask");
+    mp = mask->data_ptr<uint8_t>();
+  }
+  part = at::empty({rows, N, 2}, ws.options());
+  return BnBwdArgs{x_bn.data_ptr(), ws.data_ptr<float>(), mp, (int)mode, part.data_ptr<float>()};
 }
 
 static void check_mat(const at::Tensor& t, const char* what) {
@@ -149,6 +174,27 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
                    stats ? S.data_ptr<float>() : nullptr, current_stream(A), add ? addend->data_ptr() : nullptr,
                    add ? addend->stride(0) : 0, b_kmajor, (int)tile);
   return {C, S};
+}
+
+// gemm_nt whose output is the dy of a fused BN: also returns that BN's backward-reduction partials.
+std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at::Tensor> addend, bool b_kmajor,
+                                   at::Tensor x_bn, at::Tensor ws, c10::optional<at::Tensor> mask, int64_t mode) {
+  check_mat(A, "A");
+  check_mat(B, "B");
+  TORCH_CHECK(A.size(1) == B.size(b_kmajor ? 0 : 1), "gemm_nt_bn: K mismatch");
+  const int M = (int)A.size(0), N = (int)B.size(b_kmajor ? 1 : 0), K = (int)A.size(1);
+  const bool add = addend.has_value() && addend->defined();
+  if (add) {
+    check_mat(*addend, "addend");
+    TORCH_CHECK(addend->size(0) == M && addend->size(1) == N, "gemm_nt_bn: addend must be [M, N]");
+  }
+  at::Tensor C = at::empty({M, N}, A.options());
+  at::Tensor part;
+  const BnBwdArgs bnb = make_bn_bwd(x_bn, ws, mask, mode, M, N, gemm_nt_stats_rows(M, N), part);
+  launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K, nullptr,
+                 current_stream(A), add ? addend->data_ptr() : nullptr, add ? addend->stride(0) : 0, b_kmajor,
+                 kTileAuto, &bnb);
+  return {C, part};
 }
 
 // out = scale * A^T @ B with A [K, Mo], B [K, No] (reduction over the long row dim, split-K).
@@ -256,6 +302,31 @@ at::Tensor conv3x3_dgrad(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> 
   return dx;
 }
 
+// stride-1 3x3 data gradient that is the dy of a fused BN: returns (dx, BN-backward partials)
+std::vector<at::Tensor> conv3x3_dgrad_bn(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> addend,
+                                         at::Tensor x_bn, at::Tensor ws, c10::optional<at::Tensor> mask, int64_t mode) {
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(1) == w.size(0), "conv3x3_dgrad_bn: dy/w mismatch");
+  const int N = (int)dy.size(0), Cout = (int)w.size(0), Cin = (int)w.size(1), H = (int)dy.size(2), W = (int)dy.size(3);
+  at::Tensor dx = at::empty({N, Cin, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_conv3(dx, w);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0,
+              "conv3x3_dgrad_bn: bf16 aligned dy");
+  const void* add = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    TORCH_CHECK(addend->sizes() == dx.sizes() && addend->scalar_type() == at::kBFloat16 &&
+                    addend->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv3x3_dgrad_bn: addend must match dx");
+    add = addend->data_ptr();
+  }
+  const int64_t P = (int64_t)N * H * W;
+  at::Tensor part;
+  const BnBwdArgs bnb = make_bn_bwd(x_bn, ws, mask, mode, P, Cin, conv3x3_stats_rows(P, Cin), part);
+  launch_conv3x3_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, add, current_stream(dy),
+                       kTileAuto, &bnb);
+  return {dx, part};
+}
+
 // weight gradient, returned as a channels_last [Cout, Cin, 3, 3] tensor of out_dtype
 at::Tensor conv3x3_wgrad(at::Tensor dy, at::Tensor x, int64_t stride, c10::ScalarType out_dtype) {
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
@@ -276,6 +347,12 @@ at::Tensor conv3x3_wgrad(at::Tensor dy, at::Tensor x, int64_t stride, c10::Scala
 }
 
 void bind_nn(pybind11::module& m) {
+  m.def("gemm_nt_bn", &gemm_nt_bn, "gemm_nt producing a fused BN's dy plus its backward-reduction partials",
+        pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("addend"), pybind11::arg("b_kmajor"),
+        pybind11::arg("x_bn"), pybind11::arg("ws"), pybind11::arg("mask"), pybind11::arg("mode"));
+  m.def("conv3x3_dgrad_bn", &conv3x3_dgrad_bn, "3x3 dgrad producing a fused BN's dy plus its backward partials",
+        pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("addend"), pybind11::arg("x_bn"), pybind11::arg("ws"),
+        pybind11::arg("mask"), pybind11::arg("mode"));
   m.def("set_mfma_pipeline", &set_mfma_pipeline, "MFMA main loop: 0 register staging, 2/3 LDS-DMA stages, -1 per-shape auto");
   m.def("mfma_pipeline", &mfma_pipeline);
   m.def("conv3x3_fwd", &conv3x3_fwd, "implicit-GEMM 3x3/pad-1 conv forward (NHWC bf16, MFMA)", pybind11::arg("x"),
@@ -299,7 +376,7 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("relu"), pybind11::arg("stats") = pybind11::none());
   m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC", pybind11::arg("dy"),
         pybind11::arg("y"), pybind11::arg("mask"), pybind11::arg("x"), pybind11::arg("ws"), pybind11::arg("weight"),
-        pybind11::arg("mask_mode"), pybind11::arg("need_dres"));
+        pybind11::arg("mask_mode"), pybind11::arg("need_dres"), pybind11::arg("ext_part") = pybind11::none());
 }
 
 }  // namespace dla

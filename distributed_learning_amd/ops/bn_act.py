@@ -17,6 +17,37 @@ from . import _ext
 MASK_NONE, MASK_RECOMPUTE, MASK_BITS, MASK_Y = 0, 1, 2, 3
 
 
+class BNLink:
+    """Hand-off between a fused BN(+ReLU) and the native conv that consumes its output.
+
+    The conv's data-gradient GEMM produces exactly this BN's dy, so its epilogue can also produce
+    the BN backward's reduction partials (sum dy', sum dy'(x - mean)) while dy is still on chip
+    (csrc/include/dla_mfma.h BnBwdEpi); the BN backward then skips its reduction pass over dy and x.
+    The BN uses the partials only if the dy it receives is the very tensor that GEMM wrote — if the
+    output had other consumers, autograd summed their gradients into a new tensor and the normal
+    reduction runs."""
+
+    __slots__ = ("x", "ws", "mask", "mode", "part", "dy_ptr")
+
+    def __init__(self, x, ws, mask, mode):
+        self.x, self.ws, self.mask, self.mode = x, ws, mask, mode
+        self.part = None
+        self.dy_ptr = None
+
+    def publish(self, dy: torch.Tensor, part: torch.Tensor) -> None:
+        self.part, self.dy_ptr = part, dy.data_ptr()
+
+    def take(self, dy: torch.Tensor):
+        part, ptr = self.part, self.dy_ptr
+        self.part = self.dy_ptr = None
+        return part if part is not None and ptr == dy.data_ptr() else None
+
+
+def bn_link_of(t: torch.Tensor):
+    """The BNLink attached to a fused-BN output (None for any other tensor)."""
+    return getattr(t, "_dla_bn", None)
+
+
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu, stats):
@@ -28,7 +59,9 @@ class _BNAct(torch.autograd.Function):
         # ReLU branch for backward: recomputed from x (ReLU right after BN) or the forward's 1-bit
         # mask (ReLU after the residual add) -- the output y is never re-read.
         ctx.mask_mode = MASK_NONE if not relu else (MASK_BITS if ctx.has_res else MASK_RECOMPUTE)
-        ctx.save_for_backward(x, ws, weight, mask if mask is not None and mask.numel() else None)
+        m = mask if mask is not None and mask.numel() else None
+        ctx.save_for_backward(x, ws, weight, m)
+        ctx.link = BNLink(x, ws, m, ctx.mask_mode) if training and x.dtype == torch.bfloat16 else None
         return y
 
     @staticmethod
@@ -37,7 +70,8 @@ class _BNAct(torch.autograd.Function):
             raise RuntimeError("fused BN backward in eval mode is not supported; use the torch backend")
         x, ws, weight, mask = ctx.saved_tensors
         C = _ext.require()
-        dx, dres, dg, db = C.bn_act_bwd(dy, None, mask, x, ws, weight, ctx.mask_mode, ctx.has_res)
+        ext = ctx.link.take(dy) if ctx.link is not None else None
+        dx, dres, dg, db = C.bn_act_bwd(dy, None, mask, x, ws, weight, ctx.mask_mode, ctx.has_res, ext)
         need = ctx.needs_input_grad
         return (dx, dg if need[1] else None, db if need[2] else None, dres if ctx.has_res else None,
                 None, None, None, None, None, None, None)
@@ -91,5 +125,10 @@ def fused_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residua
         training, rm, rv = False, bn.running_mean, bn.running_var
     else:
         training, rm, rv = True, None, None
-    return _BNAct.apply(x, bn.weight, bn.bias, residual, rm, rv, training, float(bn.momentum or 0.0),
-                        float(bn.eps), relu, stats if training else None)
+    y = _BNAct.apply(x, bn.weight, bn.bias, residual, rm, rv, training, float(bn.momentum or 0.0),
+                     float(bn.eps), relu, stats if training else None)
+    if y.grad_fn is not None:
+        link = getattr(y.grad_fn, "link", None)
+        if link is not None:
+            y._dla_bn = link
+    return y

@@ -18,6 +18,17 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _ext
+from .bn_act import bn_link_of as _bn_link_of
+
+# Fuse the backward reduction of a producing BatchNorm into this conv's dgrad epilogue (BNLink).
+# Off by default: measured on MI355X (scripts/bench_gemm.py dgrad_bn*), reading the BN input in the
+# GEMM epilogue costs about as much as the standalone reduction pass it replaces (the epilogue's
+# loads do not overlap the tile's MFMA work), so the fused step was 0.3 ms slower end to end.
+BN_EPILOGUE = False
+
+
+def bn_link_of(x):
+    return _bn_link_of(x) if BN_EPILOGUE else None
 
 
 def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -33,10 +44,20 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
 
 
+def _as_param_layout(dw2: torch.Tensor, shape, stride) -> torch.Tensor:
+    """[Cout, Cin] weight gradient viewed with the parameter's own strides: a 1x1 conv weight is the
+    same memory in contiguous and channels_last form, but a stride mismatch would make autograd /
+    the DP gradient gathering copy it."""
+    return dw2.as_strided(shape, stride)
+
+
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride: int, want_stats: bool):
         C = _ext.require()
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
+        ctx.wstride = weight.stride()
+        ctx.link = bn_link_of(x) if stride == 1 else None
         if stride != 1:
             x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
         n, cin, h, w = x.shape
@@ -55,6 +76,8 @@ class _Conv1x1(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dstats):
+        if dy is None:
+            return None, None, None, None
         C = _ext.require()
         x, w2 = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
@@ -63,7 +86,12 @@ class _Conv1x1(torch.autograd.Function):
         dy2 = _rows(dy)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx2, _ = C.gemm_nt(dy2, w2, False, None, True)
+            link = ctx.link
+            if link is not None:
+                dx2, part = C.gemm_nt_bn(dy2, w2, None, True, _rows(link.x), link.ws, link.mask, link.mode)
+                link.publish(dx2, part)
+            else:
+                dx2, _ = C.gemm_nt(dy2, w2, False, None, True)
             n, cin, h, w = x.shape
             dxs = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
             if ctx.stride != 1:
@@ -74,8 +102,8 @@ class _Conv1x1(torch.autograd.Function):
             else:
                 dx = dxs
         if ctx.needs_input_grad[1]:
-            dw = C.gemm_tn(dy2, _rows(x), ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16)
-                           else torch.float32, 1.0).view(ctx.wshape).to(ctx.wdtype)
+            dw = _as_param_layout(C.gemm_tn(dy2, _rows(x), ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16)
+                                            else torch.float32, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
         return dx, dw, None, None
 
 
@@ -97,6 +125,8 @@ class _Conv1x1Fork(torch.autograd.Function):
         ctx.save_for_backward(x, w2)
         ctx.wdtype = weight.dtype
         ctx.wshape = weight.shape
+        ctx.wstride = weight.stride()
+        ctx.link = bn_link_of(x)
         if stats is not None:
             ctx.mark_non_differentiable(stats)
         return y, stats, x
@@ -114,11 +144,18 @@ class _Conv1x1Fork(torch.autograd.Function):
         dy2 = _rows(dy)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx2, _ = C.gemm_nt(dy2, w2, False, None if dident is None else _rows(dident), True)
+            add = None if dident is None else _rows(dident)
+            link = ctx.link
+            if link is not None:
+                dx2, part = C.gemm_nt_bn(dy2, w2, add, True, _rows(link.x), link.ws, link.mask, link.mode)
+            else:
+                dx2, _ = C.gemm_nt(dy2, w2, False, add, True)
             dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+            if link is not None:
+                link.publish(dx, part)
         if ctx.needs_input_grad[1]:
-            dw = C.gemm_tn(dy2, _rows(x), ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16)
-                           else torch.float32, 1.0).view(ctx.wshape).to(ctx.wdtype)
+            dw = _as_param_layout(C.gemm_tn(dy2, _rows(x), ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16)
+                                            else torch.float32, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
         return dx, dw, None
 
 
@@ -142,7 +179,7 @@ def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
 # ---------------------------------------------------------------------------------------------
 # 3x3 convolutions (csrc/kernels/conv.hip): implicit GEMMs gathered straight from NHWC tensors.
 # Per-pass engine choice from scripts/bench_conv.py at the ResNet-50 bs256 shapes on MI355X
-# (profiles/conv3x3_native_vs_miopen.md), with the 2-stage LDS-DMA main loop: the native forward
+# (profiles/mfma_kernels_vs_libraries.md), with the 2-stage LDS-DMA main loop: the native forward
 # beats MIOpen on 5 of the 7 shapes (and its epilogue yields the BatchNorm statistics, saving a
 # pass over the output), the stride-1 data gradient and the weight gradient win everywhere. MIOpen
 # keeps the 3 stride-2 data gradients.
@@ -162,6 +199,8 @@ class _Conv3x3(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride: int, want_stats: bool):
         C = _ext.require()
+        ctx.set_materialize_grads(False)
+        ctx.link = bn_link_of(x)
         w = weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         stats = None
         if CONV3_POLICY["fwd"] == "native" or want_stats:
@@ -177,13 +216,20 @@ class _Conv3x3(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dstats):
+        if dy is None:
+            return None, None, None, None
         C = _ext.require()
         x, w = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
         dx = dw = None
         if ctx.needs_input_grad[0]:
             if ctx.stride == 1 and x.shape[1] <= CONV3_POLICY["dgrad_native_max_cin"]:
-                dx = C.conv3x3_dgrad(dy, w)
+                link = ctx.link
+                if link is not None:
+                    dx, part = C.conv3x3_dgrad_bn(dy, w, None, link.x, link.ws, link.mask, link.mode)
+                    link.publish(dx, part)
+                else:
+                    dx = C.conv3x3_dgrad(dy, w)
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, [ctx.stride] * 2, [1, 1], [1, 1], False,
                                                          [0, 0], 1, [True, False, False])[0]

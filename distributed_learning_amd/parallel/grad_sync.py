@@ -35,6 +35,14 @@ from .bucketing import Bucket, bucketize
 from .executor import (Executor, InlineExecutor, NativeStreamExecutor, ThreadExecutor, TorchStreamExecutor)
 
 
+def same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Same element order in memory (strides of size-1 dims ignored), both dense: a gradient can be
+    gathered linearly in place of its parameter."""
+    if a.shape != b.shape or not is_dense(a):
+        return False
+    return all(sa == sb for n, sa, sb in zip(a.shape, a.stride(), b.stride()) if n > 1)
+
+
 def is_dense(t: torch.Tensor) -> bool:
     """Non-overlapping and dense in some dimension order (contiguous, channels_last, ...)."""
     dims = sorted((d for d in range(t.dim()) if t.shape[d] != 1), key=lambda d: t.stride(d))
@@ -207,9 +215,8 @@ class GradSync:
         b, j = self._owner[id(p)]
         if self.grad_mode == "steal":
             g = p.grad
-            if g.dtype != b.flat.dtype or g.stride() != p.stride():
-                g = g.to(b.flat.dtype).as_strided(p.shape, p.stride()) if g.stride() == p.stride() else \
-                    torch.empty_like(p, dtype=b.flat.dtype).copy_(g)
+            if g.dtype != b.flat.dtype or not same_layout(g, p):
+                g = g.to(b.flat.dtype) if same_layout(g, p) else torch.empty_like(p, dtype=b.flat.dtype).copy_(g)
             b.stolen.append((g, b.offsets[j]))
         b.ready += 1
         if b.ready > len(b.params):

@@ -52,6 +52,15 @@ for M, Cin, Cout in shapes:
     r["fwd_miopen_conv_ms"] = timeit(lambda: torch.nn.functional.conv2d(x4, w4))
     r["dgrad_native_ms"] = timeit(lambda: C.gemm_nt(dY, Wt, False))
     r["dgrad_native_kmajor_ms"] = timeit(lambda: C.gemm_nt(dY, W, False, None, True))
+    # dgrad whose output is a fused BN's dy: + the BN backward-reduction partials in the epilogue
+    xbn = torch.randn(M, Cin, device=dev).to(torch.bfloat16)
+    wsb = torch.randn(7 * Cin, device=dev)
+    mk = torch.randint(0, 255, ((M * Cin + 7) // 8,), device=dev, dtype=torch.uint8)
+    r["dgrad_bn1_ms"] = timeit(lambda: C.gemm_nt_bn(dY, W, None, True, xbn, wsb, None, 1))
+    r["dgrad_bn2_ms"] = timeit(lambda: C.gemm_nt_bn(dY, W, None, True, xbn, wsb, mk, 2))
+    x4b = xbn.view(256, h, h, Cin).permute(0, 3, 1, 2)
+    ws7 = torch.ones(7 * Cin, device=dev)
+    r["bn_bwd_sep_ms"] = timeit(lambda: C.bn_act_bwd(x4b, None, mk, x4b, ws7, None, 2, True))
     for pipe in (0, 2, 3):
         C.set_mfma_pipeline(pipe)
         r[f"fwd_p{pipe}"] = timeit(lambda: C.gemm_nt(X, W, True))
