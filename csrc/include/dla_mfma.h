@@ -365,18 +365,26 @@ struct ColStats {
 // reduction pass, without re-reading dy from HBM. ws: the BN's 7C workspace (mean | invstd |
 // scale | shift | ...); mode as launch_bn_bwd (0 none, 1 recompute, 2 bits).
 struct BnBwdEpi {
-  const bf16_t* x;
+  const bf16_t* x;  // null: no BN partials
   const float* ws;
   const uint8_t* mask;
   int mode;
   float* part;  // [row tiles][N][2]
+  // 1-bit mask for the fused addend (C = bf16(bf16(acc) + (bit ? D : 0))): the residual gradient
+  // dy * relu'(out) of a fused BN(+residual)+ReLU taken straight from dy and the forward's mask,
+  // so the BN backward never writes it out (null: plain addend)
+  const uint8_t* dmask;
 };
 
-template <int BM, int BN, bool kStats>
+template <int BM, int BN, bool kStats, bool kEpi = false>
 __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __restrict__ C, int64_t ldc, int64_t M,
                                               int N, int64_t row0, int col0, ColStats<BM, BN>& st,
                                               const bf16_t* __restrict__ D, int64_t ldd, char* smem,
-                                              const BnBwdEpi* bnb = nullptr, int bm = 0) {
+                                              const BnBwdEpi* epi = nullptr, int bm = 0) {
+  // kEpi compiles in the BN-backward partials and the masked addend (dgrad kernels only: they cost
+  // VGPRs that would lower the forward kernels' occupancy)
+  const BnBwdEpi* bnb = (kEpi && epi && epi->x) ? epi : nullptr;
+  const uint8_t* __restrict__ dmask = (kEpi && epi) ? epi->dmask : nullptr;
   constexpr int WM = Acc<BM, BN>::WM, WN = Acc<BM, BN>::WN, TM = Acc<BM, BN>::TM, TN = Acc<BM, BN>::TN;
   constexpr int LDS_C = BN + 8;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
@@ -439,8 +447,10 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
       ushort8_t v = *reinterpret_cast<ushort8_t*>(Cs + r * LDS_C + cc);
       if (D) {
         const ushort8_t d = *reinterpret_cast<const ushort8_t*>(D + gm * ldd + gn);
+        const uint32_t db = dmask ? (uint32_t)dmask[(gm * ldd + gn) >> 3] : 0xffu;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(d[j]));
+        for (int j = 0; j < 8; ++j)
+          v[j] = f32_to_bf16(bf16_to_f32(v[j]) + (((db >> j) & 1u) ? bf16_to_f32(d[j]) : 0.f));
       }
       *reinterpret_cast<ushort8_t*>(C + gm * ldc + gn) = v;
       if (bnb) {

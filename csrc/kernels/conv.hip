@@ -212,8 +212,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_dgrad_kernel(const bf16_t
   Acc<BM, BN> acc;
   acc.zero();
   run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
-  epilogue_bf16<BM, BN, false>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, addend, g.Cin, smem_raw,
-                               bnb.x ? &bnb : nullptr, bm);
+  epilogue_bf16<BM, BN, false, true>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, addend, g.Cin, smem_raw, &bnb, bm);
 }
 
 // wgrad partial slabs P[split][Cout][9*Cin]
@@ -319,8 +318,9 @@ static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const Co
 void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
                           const void* addend, hipStream_t stream, int tile, const BnBwdArgs* bn_bwd) {
   const ConvGeom g = make_geom(N, H, W, Cin, Cout, 1);
-  const BnBwdEpi bnb = bn_bwd ? BnBwdEpi{(const bf16_t*)bn_bwd->x, bn_bwd->ws, bn_bwd->mask, bn_bwd->mode, bn_bwd->part}
-                              : BnBwdEpi{nullptr, nullptr, nullptr, 0, nullptr};
+  const BnBwdEpi bnb = bn_bwd ? BnBwdEpi{(const bf16_t*)bn_bwd->x, bn_bwd->ws, bn_bwd->mask, bn_bwd->mode, bn_bwd->part,
+                                         nullptr}
+                              : BnBwdEpi{nullptr, nullptr, nullptr, 0, nullptr, nullptr};
   const bf16_t* d = (const bf16_t*)dy;
   const bf16_t* wp = (const bf16_t*)w;
   const bf16_t* ad = (const bf16_t*)addend;

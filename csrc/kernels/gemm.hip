@@ -54,7 +54,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const bf16_t* __re
     const RowLoader<BN> lb{B, ldb, (int64_t)col0, N, K};
     run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
   }
-  epilogue_bf16<BM, BN, kStats>(acc, C, ldc, M, N, row0, col0, st, D, ldd, smem_raw, bnb.x ? &bnb : nullptr, bm);
+  epilogue_bf16<BM, BN, kStats, !kStats>(acc, C, ldc, M, N, row0, col0, st, D, ldd, smem_raw, &bnb, bm);
   if constexpr (kStats) stats_flush<BM, BN>(st, stats + (int64_t)bm * N * 2, N, col0, smem_raw);
 }
 
@@ -167,9 +167,11 @@ int gemm_nt_stats_rows(int M, int N, int tile) {
 
 void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
                     float* stats, hipStream_t stream, const void* addend, int64_t ld_addend, bool b_kmajor, int tile,
-                    const BnBwdArgs* bn_bwd) {
-  const BnBwdEpi bnb = bn_bwd ? BnBwdEpi{(const bf16_t*)bn_bwd->x, bn_bwd->ws, bn_bwd->mask, bn_bwd->mode, bn_bwd->part}
-                              : BnBwdEpi{nullptr, nullptr, nullptr, 0, nullptr};
+                    const BnBwdArgs* bn_bwd, const uint8_t* addend_mask) {
+  BnBwdEpi bnb = bn_bwd ? BnBwdEpi{(const bf16_t*)bn_bwd->x, bn_bwd->ws, bn_bwd->mask, bn_bwd->mode, bn_bwd->part,
+                                   nullptr}
+                        : BnBwdEpi{nullptr, nullptr, nullptr, 0, nullptr, nullptr};
+  bnb.dmask = addend_mask;
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* b = (const bf16_t*)B;
   bf16_t* c = (bf16_t*)C;
@@ -191,10 +193,15 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
 #undef DLA_NT
 }
 
+// 64-wide tiles for 64-wide operands: a 128-wide tile would spend half (or three quarters, at
+// 64 x 64) of its MFMAs and LDS traffic on zero columns.
+static inline int tn_bm(int Mo) { return Mo <= 64 ? 64 : 128; }
+static inline int tn_bn(int No) { return No <= 64 ? 64 : 128; }
+
 int gemm_tn_splits(int Mo, int No, int K) {
   // ~512 workgroups in flight (2 per CU) and >= 16 K-steps per split: enough parallelism for the
   // long M reduction while keeping the fp32 slab traffic (splits * Mo * No * 4 B) small.
-  const int tiles = ((Mo + 127) / 128) * ((No + 127) / 128);
+  const int tiles = ((Mo + tn_bm(Mo) - 1) / tn_bm(Mo)) * ((No + tn_bn(No) - 1) / tn_bn(No));
   int splits = std::max(1, 512 / std::max(1, tiles));
   const int max_splits = std::max(1, K / (16 * kBK));
   return std::max(1, std::min(splits, max_splits));
@@ -204,16 +211,28 @@ void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, floa
                     int K, void* out, int out_dtype, float scale, bool accumulate, hipStream_t stream) {
   int kps = (K + splits - 1) / splits;
   kps = (kps + kBK - 1) / kBK * kBK;
-  const int tiles = ((Mo + 127) / 128) * ((No + 127) / 128);
-#define DLA_TN(P_)                                                                                            \
-  hipLaunchKernelGGL((gemm_tn_kernel<128, 128, P_>), dim3(tiles, splits), dim3(kThreads),                     \
-                     (run_mainloop_lds_bytes<P_, 128, 128, KLoader<128>, KLoader<128>>()), stream, (const bf16_t*)A, \
+  const int bm = tn_bm(Mo), bn = tn_bn(No);
+  const int tiles = ((Mo + bm - 1) / bm) * ((No + bn - 1) / bn);
+#define DLA_TN(BM_, BN_, P_)                                                                                      \
+  hipLaunchKernelGGL((gemm_tn_kernel<BM_, BN_, P_>), dim3(tiles, splits), dim3(kThreads),                         \
+                     (run_mainloop_lds_bytes<P_, BM_, BN_, KLoader<BM_>, KLoader<BN_>>()), stream, (const bf16_t*)A, \
                      lda, (const bf16_t*)B, ldb, partial, Mo, No, K, kps)
-  switch (mfma_pipeline_for(kps)) {
-    case 0: DLA_TN(0); break;
-    case 3: DLA_TN(3); break;
-    default: DLA_TN(2); break;
+#define DLA_TN_P(BM_, BN_)                 \
+  switch (mfma_pipeline_for(kps)) {        \
+    case 0: DLA_TN(BM_, BN_, 0); break;    \
+    case 3: DLA_TN(BM_, BN_, 3); break;    \
+    default: DLA_TN(BM_, BN_, 2); break;   \
   }
+  if (bm == 64 && bn == 64) {
+    DLA_TN_P(64, 64)
+  } else if (bm == 64) {
+    DLA_TN_P(64, 128)
+  } else if (bn == 64) {
+    DLA_TN_P(128, 64)
+  } else {
+    DLA_TN_P(128, 128)
+  }
+#undef DLA_TN_P
 #undef DLA_TN
   launch_splitk_reduce(partial, splits, (int64_t)Mo * No, out, out_dtype, scale, accumulate, stream);
 }

@@ -153,8 +153,16 @@ static void check_mat(const at::Tensor& t, const char* what) {
 
 // C = A @ B^T (A [M,K], B [N,K]; or C = A @ B with B [K,N] when b_kmajor) in bf16 with fp32 accumulation. Optionally returns per-row-block
 // column statistics partials [ceil(M/128), N, 2] (sum, sum of squares of the bf16 outputs).
+static const uint8_t* addend_mask_ptr(const c10::optional<at::Tensor>& m, int64_t M, int64_t N, bool add) {
+  if (!m.has_value() || !m->defined()) return nullptr;
+  TORCH_CHECK(add, "addend_mask needs an addend");
+  TORCH_CHECK(m->scalar_type() == at::kByte && m->is_cuda() && m->numel() * 8 >= M * N,
+              "addend_mask must be the uint8 1-bit mask of the addend");
+  return m->data_ptr<uint8_t>();
+}
+
 std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::optional<at::Tensor> addend,
-                                bool b_kmajor, int64_t tile) {
+                                bool b_kmajor, int64_t tile, c10::optional<at::Tensor> addend_mask) {
   TORCH_CHECK(tile >= 0 && tile <= 3, "gemm_nt: tile config 0..3");
   check_mat(A, "A");
   check_mat(B, "B");
@@ -172,13 +180,14 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
   if (M > 0 && N > 0)
     launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K,
                    stats ? S.data_ptr<float>() : nullptr, current_stream(A), add ? addend->data_ptr() : nullptr,
-                   add ? addend->stride(0) : 0, b_kmajor, (int)tile);
+                   add ? addend->stride(0) : 0, b_kmajor, (int)tile, nullptr, addend_mask_ptr(addend_mask, M, N, add));
   return {C, S};
 }
 
 // gemm_nt whose output is the dy of a fused BN: also returns that BN's backward-reduction partials.
 std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at::Tensor> addend, bool b_kmajor,
-                                   at::Tensor x_bn, at::Tensor ws, c10::optional<at::Tensor> mask, int64_t mode) {
+                                   at::Tensor x_bn, at::Tensor ws, c10::optional<at::Tensor> mask, int64_t mode,
+                                   c10::optional<at::Tensor> addend_mask) {
   check_mat(A, "A");
   check_mat(B, "B");
   TORCH_CHECK(A.size(1) == B.size(b_kmajor ? 0 : 1), "gemm_nt_bn: K mismatch");
@@ -193,7 +202,7 @@ std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at:
   const BnBwdArgs bnb = make_bn_bwd(x_bn, ws, mask, mode, M, N, gemm_nt_stats_rows(M, N), part);
   launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K, nullptr,
                  current_stream(A), add ? addend->data_ptr() : nullptr, add ? addend->stride(0) : 0, b_kmajor,
-                 kTileAuto, &bnb);
+                 kTileAuto, &bnb, addend_mask_ptr(addend_mask, M, N, add));
   return {C, part};
 }
 
@@ -349,7 +358,8 @@ at::Tensor conv3x3_wgrad(at::Tensor dy, at::Tensor x, int64_t stride, c10::Scala
 void bind_nn(pybind11::module& m) {
   m.def("gemm_nt_bn", &gemm_nt_bn, "gemm_nt producing a fused BN's dy plus its backward-reduction partials",
         pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("addend"), pybind11::arg("b_kmajor"),
-        pybind11::arg("x_bn"), pybind11::arg("ws"), pybind11::arg("mask"), pybind11::arg("mode"));
+        pybind11::arg("x_bn"), pybind11::arg("ws"), pybind11::arg("mask"), pybind11::arg("mode"),
+        pybind11::arg("addend_mask") = pybind11::none());
   m.def("conv3x3_dgrad_bn", &conv3x3_dgrad_bn, "3x3 dgrad producing a fused BN's dy plus its backward partials",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("addend"), pybind11::arg("x_bn"), pybind11::arg("ws"),
         pybind11::arg("mask"), pybind11::arg("mode"));
@@ -367,7 +377,8 @@ void bind_nn(pybind11::module& m) {
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pooling backward (gather form)");
   m.def("gemm_nt", &gemm_nt, "C = A @ B^T (bf16 MFMA), optional fused column statistics", pybind11::arg("A"),
         pybind11::arg("B"), pybind11::arg("stats") = false, pybind11::arg("addend") = pybind11::none(),
-        pybind11::arg("b_kmajor") = false, pybind11::arg("tile") = 0);
+        pybind11::arg("b_kmajor") = false, pybind11::arg("tile") = 0,
+        pybind11::arg("addend_mask") = pybind11::none());
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),
         pybind11::arg("out_dtype") = at::kFloat, pybind11::arg("scale") = 1.0);
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC", pybind11::arg("x"),

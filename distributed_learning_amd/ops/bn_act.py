@@ -43,6 +43,24 @@ class BNLink:
         return part if part is not None and ptr == dy.data_ptr() else None
 
 
+class ResidualLink:
+    """Hand-off from a fused BN(+residual)+ReLU to the conv that forked its identity input.
+
+    The residual's gradient is dy * relu'(out) — dy masked by the forward's 1-bit mask. Instead of
+    the BN backward writing it out (a full tensor write + read), it hands (dy, mask) to the forking
+    conv (ops/conv.py::_Conv1x1Fork), whose dgrad epilogue adds dy where the mask bit is set. Valid
+    only when the residual tensor is that fork's identity output (checked at forward time)."""
+
+    __slots__ = ("dy", "mask")
+
+    def __init__(self):
+        self.dy = self.mask = None
+
+
+def fork_link_of(t):
+    return getattr(t, "_dla_fork", None) if t is not None else None
+
+
 def bn_link_of(t: torch.Tensor):
     """The BNLink attached to a fused-BN output (None for any other tensor)."""
     return getattr(t, "_dla_bn", None)
@@ -50,12 +68,14 @@ def bn_link_of(t: torch.Tensor):
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu, stats):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu, stats,
+                rlink=None):
         C = _ext.require()
         y, ws, mask = C.bn_act_fwd(x, residual, weight, bias, running_mean, running_var, training, momentum, eps,
                                    relu, stats)
         ctx.has_res = residual is not None
         ctx.training = training
+        ctx.rlink = rlink if (rlink is not None and residual is not None and training) else None
         # ReLU branch for backward: recomputed from x (ReLU right after BN) or the forward's 1-bit
         # mask (ReLU after the residual add) -- the output y is never re-read.
         ctx.mask_mode = MASK_NONE if not relu else (MASK_BITS if ctx.has_res else MASK_RECOMPUTE)
@@ -71,10 +91,15 @@ class _BNAct(torch.autograd.Function):
         x, ws, weight, mask = ctx.saved_tensors
         C = _ext.require()
         ext = ctx.link.take(dy) if ctx.link is not None else None
-        dx, dres, dg, db = C.bn_act_bwd(dy, None, mask, x, ws, weight, ctx.mask_mode, ctx.has_res, ext)
+        rl = ctx.rlink
+        dx, dres, dg, db = C.bn_act_bwd(dy, None, mask, x, ws, weight, ctx.mask_mode, ctx.has_res and rl is None, ext)
+        if rl is not None:  # the forking conv adds dy (masked) in its dgrad epilogue
+            rl.dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
+            rl.mask = mask if ctx.mask_mode == MASK_BITS else None
+            dres = None
         need = ctx.needs_input_grad
         return (dx, dg if need[1] else None, db if need[2] else None, dres if ctx.has_res else None,
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
 # num_batches_tracked increments are batched into one multi-tensor launch per forward instead of
@@ -125,8 +150,11 @@ def fused_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residua
         training, rm, rv = False, bn.running_mean, bn.running_var
     else:
         training, rm, rv = True, None, None
+    rlink = fork_link_of(residual)
+    if rlink is not None and residual.dtype != torch.bfloat16:  # the epilogue addend is bf16
+        rlink = None
     y = _BNAct.apply(x, bn.weight, bn.bias, residual, rm, rv, training, float(bn.momentum or 0.0),
-                     float(bn.eps), relu, stats if training else None)
+                     float(bn.eps), relu, stats if training else None, rlink)
     if y.grad_fn is not None:
         link = getattr(y.grad_fn, "link", None)
         if link is not None:

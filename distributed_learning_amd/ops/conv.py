@@ -18,6 +18,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _ext
+from .bn_act import ResidualLink
 from .bn_act import bn_link_of as _bn_link_of
 
 # Fuse the backward reduction of a producing BatchNorm into this conv's dgrad epilogue (BNLink).
@@ -114,9 +115,10 @@ class _Conv1x1Fork(torch.autograd.Function):
     elementwise kernel over the block-input tensor (the autograd sum of the two uses of ``x``)."""
 
     @staticmethod
-    def forward(ctx, x, weight, want_stats: bool):
+    def forward(ctx, x, weight, want_stats: bool, rlink):
         C = _ext.require()
         ctx.set_materialize_grads(False)
+        ctx.rlink = rlink
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         w2 = weight.reshape(cout, cin).to(torch.bfloat16).contiguous()
@@ -136,10 +138,23 @@ class _Conv1x1Fork(torch.autograd.Function):
         C = _ext.require()
         x, w2 = ctx.saved_tensors
         n, cin, h, w = x.shape
+        rl = ctx.rlink
+        amask = None
+        if rl is not None and rl.dy is not None:
+            # identity gradient handed over by the BN(+residual)+ReLU that consumed the identity:
+            # dy where the forward's ReLU bit is set (added in the epilogue below)
+            rdy, rmask = rl.dy, rl.mask
+            rl.dy = rl.mask = None
+            if dident is None:
+                dident, amask = rdy, rmask
+            else:  # the identity had other consumers too: materialise the masked gradient
+                dident = dident + (rdy if rmask is None else rdy * _unpack_bits(rmask, rdy))
         if dident is not None:
             dident = dident.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
         if dy is None:
-            return dident, None, None
+            if amask is not None:
+                dident = dident * _unpack_bits(amask, dident)
+            return dident, None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
         dy2 = _rows(dy)
         dx = dw = None
@@ -147,25 +162,41 @@ class _Conv1x1Fork(torch.autograd.Function):
             add = None if dident is None else _rows(dident)
             link = ctx.link
             if link is not None:
-                dx2, part = C.gemm_nt_bn(dy2, w2, add, True, _rows(link.x), link.ws, link.mask, link.mode)
+                dx2, part = C.gemm_nt_bn(dy2, w2, add, True, _rows(link.x), link.ws, link.mask, link.mode, amask)
             else:
-                dx2, _ = C.gemm_nt(dy2, w2, False, add, True)
+                dx2, _ = C.gemm_nt(dy2, w2, False, add, True, 0, amask)
             dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
             if link is not None:
                 link.publish(dx, part)
         if ctx.needs_input_grad[1]:
             dw = _as_param_layout(C.gemm_tn(dy2, _rows(x), ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16)
                                             else torch.float32, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
-        return dx, dw, None
+        return dx, dw, None, None
+
+
+def _unpack_bits(mask: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+    """Expand a 1-bit mask (element order of `like` in channels_last) to a 0/1 tensor like `like`."""
+    bits = torch.stack([(mask >> j) & 1 for j in range(8)], 1).reshape(-1)[: like.numel()]
+    n, c, h, w = like.shape
+    return bits.view(n, h, w, c).permute(0, 3, 1, 2).to(like.dtype)
 
 
 def fork_supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     return supported(x, conv) and conv.stride in ((1, 1), 1)
 
 
+# Hand the residual gradient of the block's final BN(+residual)+ReLU to the fork as (dy, mask)
+# instead of a materialised tensor (ResidualLink).
+RESIDUAL_HANDOFF = True
+
+
 def conv1x1_fork(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
     """Returns (y, stats-or-None, x_alias); use ``x_alias`` as the residual identity."""
-    return _Conv1x1Fork.apply(x, conv.weight, want_stats)
+    rlink = ResidualLink() if RESIDUAL_HANDOFF and x.requires_grad else None
+    y, stats, xa = _Conv1x1Fork.apply(x, conv.weight, want_stats, rlink)
+    if rlink is not None:
+        xa._dla_fork = rlink
+    return y, stats, xa
 
 
 def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):

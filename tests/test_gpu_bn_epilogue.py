@@ -88,3 +88,37 @@ def test_resnet_blocks_with_and_without_bn_epilogue(cuda):
     # gradients by ~1% typical, a few % on the most sensitive (stem) parameters
     rels = sorted(float((g1[n] - g0[n]).norm() / g0[n].norm().clamp_min(1e-20)) for n in g0)
     assert rels[len(rels) // 2] < 2e-2 and rels[-1] < 0.2, rels[-5:]
+
+
+def test_residual_handoff_is_exact(cuda):
+    """(dy, mask) hand-off from the block's last BN to the forking conv1: bitwise the same gradients
+    as materialising the residual gradient."""
+    from distributed_learning_amd.models import resnet50
+    from distributed_learning_amd.ops import conv as nconv
+    from distributed_learning_amd.ops import nn as dnn
+
+    def run(handoff):
+        torch.manual_seed(0)
+        m = resnet50(10).to(cuda).to(memory_format=CL)
+        dnn.bf16_weights(m)
+        x = torch.randn(4, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+        old = nconv.RESIDUAL_HANDOFF
+        nconv.RESIDUAL_HANDOFF = handoff
+        try:
+            m(x).float().square().mean().backward()
+        finally:
+            nconv.RESIDUAL_HANDOFF = old
+        return {n: p.grad.clone() for n, p in m.named_parameters()}
+
+    det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    dnn.set_backend("native")
+    dnn.set_native_conv(True)
+    try:
+        g1, g0 = run(True), run(False)
+    finally:
+        dnn.set_native_conv(False)
+        dnn.set_backend("torch")
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
+    for n in g0:
+        assert torch.equal(g1[n], g0[n]), n
