@@ -142,7 +142,8 @@ struct BnBwdArgs {
 void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
                     float* stats, hipStream_t stream, const void* addend = nullptr, int64_t ld_addend = 0,
                     bool b_kmajor = false, int tile = kTileAuto, const BnBwdArgs* bn_bwd = nullptr,
-                    const uint8_t* addend_mask = nullptr);  // addend element used iff its mask bit is set
+                    const uint8_t* addend_mask = nullptr,  // addend element used iff its mask bit is set
+                    const void* addend2_s2 = nullptr, int H = 0, int W = 0);  // compact stride-2 addend
 // out[Mo,No] (= scale * A^T B [+ out]) with A [K, lda>=Mo], B [K, ldb>=No]; partial: splits*Mo*No f32.
 int gemm_tn_splits(int Mo, int No, int K);
 void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, float* partial, int splits, int Mo, int No,

@@ -23,6 +23,18 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
+// n / d for n < 2^24, d < 2^16: floor(n * ceil(2^40 / d) / 2^40), 4 VALU ops.
+struct FastDiv {
+  uint32_t d, m_lo, m_hi;
+};
+__host__ __device__ inline FastDiv make_fastdiv(uint32_t d) {
+  const uint64_t m = ((1ull << 40) + d - 1) / d;
+  return FastDiv{d, (uint32_t)m, (uint32_t)(m >> 32)};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m_lo) + n * f.m_hi) >> 8;
+}
+
 constexpr int kThreads = 256;
 constexpr int kBK = 64;
 
@@ -374,6 +386,12 @@ struct BnBwdEpi {
   // dy * relu'(out) of a fused BN(+residual)+ReLU taken straight from dy and the forward's mask,
   // so the BN backward never writes it out (null: plain addend)
   const uint8_t* dmask;
+  // second, stride-2 addend: the gradient of the block input's stride-2 subsample (the downsample
+  // 1x1 conv's input), compact [n][H/2][W/2][N]; added at the even pixels of the [n][H][W] rows of
+  // C (null: none). Replaces a zero-filled full-size scatter of that gradient.
+  const bf16_t* d2;
+  int H, W;
+  FastDiv fW, fH;
 };
 
 template <int BM, int BN, bool kStats, bool kEpi = false>
@@ -385,6 +403,7 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
   // VGPRs that would lower the forward kernels' occupancy)
   const BnBwdEpi* bnb = (kEpi && epi && epi->x) ? epi : nullptr;
   const uint8_t* __restrict__ dmask = (kEpi && epi) ? epi->dmask : nullptr;
+  const bf16_t* __restrict__ d2 = (kEpi && epi) ? epi->d2 : nullptr;
   constexpr int WM = Acc<BM, BN>::WM, WN = Acc<BM, BN>::WN, TM = Acc<BM, BN>::TM, TN = Acc<BM, BN>::TN;
   constexpr int LDS_C = BN + 8;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
@@ -451,6 +470,18 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           v[j] = f32_to_bf16(bf16_to_f32(v[j]) + (((db >> j) & 1u) ? bf16_to_f32(d[j]) : 0.f));
+      }
+      if (d2) {
+        const uint32_t q = fdiv((uint32_t)gm, epi->fW);
+        const int w = (int)gm - (int)q * epi->W;
+        const uint32_t n = fdiv(q, epi->fH);
+        const int h = (int)q - (int)n * epi->H;
+        if (((h | w) & 1) == 0) {
+          const int64_t r2 = ((int64_t)n * (epi->H >> 1) + (h >> 1)) * (epi->W >> 1) + (w >> 1);
+          const ushort8_t e = *reinterpret_cast<const ushort8_t*>(d2 + r2 * ldc + gn);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(e[j]));
+        }
       }
       *reinterpret_cast<ushort8_t*>(C + gm * ldc + gn) = v;
       if (bnb) {

@@ -26,18 +26,6 @@ namespace dla {
 
 using namespace mm;
 
-// n / d for n < 2^24, d < 2^16: floor(n * ceil(2^40 / d) / 2^40), 4 VALU ops.
-struct FastDiv {
-  uint32_t d, m_lo, m_hi;
-};
-static FastDiv make_fastdiv(uint32_t d) {
-  const uint64_t m = ((1ull << 40) + d - 1) / d;
-  return FastDiv{d, (uint32_t)m, (uint32_t)(m >> 32)};
-}
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  return (__umulhi(n, f.m_lo) + n * f.m_hi) >> 8;
-}
-
 struct ConvGeom {
   int N, H, W, Cin;  // input image (NHWC)
   int OH, OW, Cout;  // output image
@@ -318,9 +306,14 @@ static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const Co
 void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
                           const void* addend, hipStream_t stream, int tile, const BnBwdArgs* bn_bwd) {
   const ConvGeom g = make_geom(N, H, W, Cin, Cout, 1);
-  const BnBwdEpi bnb = bn_bwd ? BnBwdEpi{(const bf16_t*)bn_bwd->x, bn_bwd->ws, bn_bwd->mask, bn_bwd->mode, bn_bwd->part,
-                                         nullptr}
-                              : BnBwdEpi{nullptr, nullptr, nullptr, 0, nullptr, nullptr};
+  BnBwdEpi bnb{};
+  if (bn_bwd) {
+    bnb.x = (const bf16_t*)bn_bwd->x;
+    bnb.ws = bn_bwd->ws;
+    bnb.mask = bn_bwd->mask;
+    bnb.mode = bn_bwd->mode;
+    bnb.part = bn_bwd->part;
+  }
   const bf16_t* d = (const bf16_t*)dy;
   const bf16_t* wp = (const bf16_t*)w;
   const bf16_t* ad = (const bf16_t*)addend;

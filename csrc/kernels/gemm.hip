@@ -167,11 +167,23 @@ int gemm_nt_stats_rows(int M, int N, int tile) {
 
 void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
                     float* stats, hipStream_t stream, const void* addend, int64_t ld_addend, bool b_kmajor, int tile,
-                    const BnBwdArgs* bn_bwd, const uint8_t* addend_mask) {
-  BnBwdEpi bnb = bn_bwd ? BnBwdEpi{(const bf16_t*)bn_bwd->x, bn_bwd->ws, bn_bwd->mask, bn_bwd->mode, bn_bwd->part,
-                                   nullptr}
-                        : BnBwdEpi{nullptr, nullptr, nullptr, 0, nullptr, nullptr};
+                    const BnBwdArgs* bn_bwd, const uint8_t* addend_mask, const void* addend2_s2, int H, int W) {
+  BnBwdEpi bnb{};
+  if (bn_bwd) {
+    bnb.x = (const bf16_t*)bn_bwd->x;
+    bnb.ws = bn_bwd->ws;
+    bnb.mask = bn_bwd->mask;
+    bnb.mode = bn_bwd->mode;
+    bnb.part = bn_bwd->part;
+  }
   bnb.dmask = addend_mask;
+  if (addend2_s2) {
+    bnb.d2 = (const bf16_t*)addend2_s2;
+    bnb.H = H;
+    bnb.W = W;
+    bnb.fW = make_fastdiv((uint32_t)W);
+    bnb.fH = make_fastdiv((uint32_t)H);
+  }
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* b = (const bf16_t*)B;
   bf16_t* c = (bf16_t*)C;

@@ -161,8 +161,21 @@ static const uint8_t* addend_mask_ptr(const c10::optional<at::Tensor>& m, int64_
   return m->data_ptr<uint8_t>();
 }
 
+// addend2: the gradient of the block input's stride-2 subsample, [n, C, H/2, W/2] channels_last,
+// added at the even pixels of the [n*H*W, C] output rows (requires even H, W).
+static const void* addend2_ptr(const c10::optional<at::Tensor>& a2, int64_t M, int64_t N, int64_t H, int64_t W) {
+  if (!a2.has_value() || !a2->defined()) return nullptr;
+  TORCH_CHECK(H > 0 && W > 0 && H % 2 == 0 && W % 2 == 0 && M % (H * W) == 0, "addend2: even H, W dividing M");
+  TORCH_CHECK(a2->scalar_type() == at::kBFloat16 && a2->dim() == 4 && a2->size(1) == N && a2->size(2) == H / 2 &&
+                  a2->size(3) == W / 2 && a2->size(0) == M / (H * W) &&
+                  a2->is_contiguous(at::MemoryFormat::ChannelsLast),
+              "addend2 must be the bf16 channels_last [n, C, H/2, W/2] gradient");
+  return a2->data_ptr();
+}
+
 std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::optional<at::Tensor> addend,
-                                bool b_kmajor, int64_t tile, c10::optional<at::Tensor> addend_mask) {
+                                bool b_kmajor, int64_t tile, c10::optional<at::Tensor> addend_mask,
+                                c10::optional<at::Tensor> addend2, int64_t H, int64_t W) {
   TORCH_CHECK(tile >= 0 && tile <= 3, "gemm_nt: tile config 0..3");
   check_mat(A, "A");
   check_mat(B, "B");
@@ -180,14 +193,16 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
   if (M > 0 && N > 0)
     launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K,
                    stats ? S.data_ptr<float>() : nullptr, current_stream(A), add ? addend->data_ptr() : nullptr,
-                   add ? addend->stride(0) : 0, b_kmajor, (int)tile, nullptr, addend_mask_ptr(addend_mask, M, N, add));
+                   add ? addend->stride(0) : 0, b_kmajor, (int)tile, nullptr, addend_mask_ptr(addend_mask, M, N, add),
+                   addend2_ptr(addend2, M, N, H, W), (int)H, (int)W);
   return {C, S};
 }
 
 // gemm_nt whose output is the dy of a fused BN: also returns that BN's backward-reduction partials.
 std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at::Tensor> addend, bool b_kmajor,
                                    at::Tensor x_bn, at::Tensor ws, c10::optional<at::Tensor> mask, int64_t mode,
-                                   c10::optional<at::Tensor> addend_mask) {
+                                   c10::optional<at::Tensor> addend_mask, c10::optional<at::Tensor> addend2, int64_t H,
+                                   int64_t W) {
   check_mat(A, "A");
   check_mat(B, "B");
   TORCH_CHECK(A.size(1) == B.size(b_kmajor ? 0 : 1), "gemm_nt_bn: K mismatch");
@@ -202,7 +217,8 @@ std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at:
   const BnBwdArgs bnb = make_bn_bwd(x_bn, ws, mask, mode, M, N, gemm_nt_stats_rows(M, N), part);
   launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K, nullptr,
                  current_stream(A), add ? addend->data_ptr() : nullptr, add ? addend->stride(0) : 0, b_kmajor,
-                 kTileAuto, &bnb, addend_mask_ptr(addend_mask, M, N, add));
+                 kTileAuto, &bnb, addend_mask_ptr(addend_mask, M, N, add), addend2_ptr(addend2, M, N, H, W), (int)H,
+                 (int)W);
   return {C, part};
 }
 
@@ -359,7 +375,8 @@ void bind_nn(pybind11::module& m) {
   m.def("gemm_nt_bn", &gemm_nt_bn, "gemm_nt producing a fused BN's dy plus its backward-reduction partials",
         pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("addend"), pybind11::arg("b_kmajor"),
         pybind11::arg("x_bn"), pybind11::arg("ws"), pybind11::arg("mask"), pybind11::arg("mode"),
-        pybind11::arg("addend_mask") = pybind11::none());
+        pybind11::arg("addend_mask") = pybind11::none(), pybind11::arg("addend2") = pybind11::none(),
+        pybind11::arg("H") = 0, pybind11::arg("W") = 0);
   m.def("conv3x3_dgrad_bn", &conv3x3_dgrad_bn, "3x3 dgrad producing a fused BN's dy plus its backward partials",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("addend"), pybind11::arg("x_bn"), pybind11::arg("ws"),
         pybind11::arg("mask"), pybind11::arg("mode"));
@@ -378,7 +395,8 @@ void bind_nn(pybind11::module& m) {
   m.def("gemm_nt", &gemm_nt, "C = A @ B^T (bf16 MFMA), optional fused column statistics", pybind11::arg("A"),
         pybind11::arg("B"), pybind11::arg("stats") = false, pybind11::arg("addend") = pybind11::none(),
         pybind11::arg("b_kmajor") = false, pybind11::arg("tile") = 0,
-        pybind11::arg("addend_mask") = pybind11::none());
+        pybind11::arg("addend_mask") = pybind11::none(), pybind11::arg("addend2") = pybind11::none(),
+        pybind11::arg("H") = 0, pybind11::arg("W") = 0);
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),
         pybind11::arg("out_dtype") = at::kFloat, pybind11::arg("scale") = 1.0);
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC", pybind11::arg("x"),

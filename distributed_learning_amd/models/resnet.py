@@ -69,8 +69,14 @@ class Bottleneck(nn.Module):
         # conv1 forwards x as a second output that feeds the identity branch (or the downsample conv),
         # so the two gradients of the block input are summed inside conv1's dgrad GEMM epilogue
         # instead of by an elementwise add (native path; a plain alias otherwise)
-        out, xa = dnn.conv_bn_act_fork(x, self.conv1, self.bn1, relu=True)
-        identity = xa if self.downsample is None else self.downsample(xa)
+        if self.downsample is not None and self.downsample[0].stride == (2, 2):
+            # stride-2 downsample: conv1's fork also yields x[:, :, ::2, ::2], whose compact gradient
+            # it adds at the even pixels in its dgrad epilogue (no zero-filled scatter)
+            out, xa, xs = dnn.conv_bn_act_fork(x, self.conv1, self.bn1, relu=True, subsample=True)
+            identity = self.downsample(xa) if xs is None else self.downsample.forward_presubsampled(xs)
+        else:
+            out, xa = dnn.conv_bn_act_fork(x, self.conv1, self.bn1, relu=True)
+            identity = xa if self.downsample is None else self.downsample(xa)
         out = dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True)
         return dnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=identity)
 
@@ -83,6 +89,10 @@ class Downsample(nn.Sequential):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return dnn.conv_bn_act(x, self[0], self[1], relu=False)
+
+    def forward_presubsampled(self, xs: torch.Tensor) -> torch.Tensor:
+        """Same result for an input already subsampled by the conv's stride."""
+        return dnn.conv_bn_act(xs, self[0], self[1], relu=False, presubsampled=True)
 
 
 class ResNet(nn.Module):

@@ -115,11 +115,14 @@ class _Conv1x1Fork(torch.autograd.Function):
     elementwise kernel over the block-input tensor (the autograd sum of the two uses of ``x``)."""
 
     @staticmethod
-    def forward(ctx, x, weight, want_stats: bool, rlink):
+    def forward(ctx, x, weight, want_stats: bool, rlink, sub: bool = False):
         C = _ext.require()
         ctx.set_materialize_grads(False)
         ctx.rlink = rlink
         n, cin, h, w = x.shape
+        # sub: also hand on the stride-2 subsample of x (the downsample conv's input); its compact
+        # gradient is added at the even pixels inside the dgrad epilogue (no zero-filled scatter)
+        xs = x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last) if sub else None
         cout = weight.shape[0]
         w2 = weight.reshape(cout, cin).to(torch.bfloat16).contiguous()
         y2, stats = C.gemm_nt(_rows(x), w2, want_stats)
@@ -131,13 +134,15 @@ class _Conv1x1Fork(torch.autograd.Function):
         ctx.link = bn_link_of(x)
         if stats is not None:
             ctx.mark_non_differentiable(stats)
-        return y, stats, x
+        return y, stats, x, xs
 
     @staticmethod
-    def backward(ctx, dy, _dstats, dident):
+    def backward(ctx, dy, _dstats, dident, dsub=None):
         C = _ext.require()
         x, w2 = ctx.saved_tensors
         n, cin, h, w = x.shape
+        if dsub is not None:
+            dsub = dsub.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
         rl = ctx.rlink
         amask = None
         if rl is not None and rl.dy is not None:
@@ -154,7 +159,11 @@ class _Conv1x1Fork(torch.autograd.Function):
         if dy is None:
             if amask is not None:
                 dident = dident * _unpack_bits(amask, dident)
-            return dident, None, None, None
+            if dsub is not None:
+                full = torch.zeros_like(x) if dident is None else dident.clone()
+                full[:, :, ::2, ::2] += dsub
+                dident = full
+            return dident, None, None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
         dy2 = _rows(dy)
         dx = dw = None
@@ -162,16 +171,17 @@ class _Conv1x1Fork(torch.autograd.Function):
             add = None if dident is None else _rows(dident)
             link = ctx.link
             if link is not None:
-                dx2, part = C.gemm_nt_bn(dy2, w2, add, True, _rows(link.x), link.ws, link.mask, link.mode, amask)
+                dx2, part = C.gemm_nt_bn(dy2, w2, add, True, _rows(link.x), link.ws, link.mask, link.mode, amask,
+                                         dsub, h, w)
             else:
-                dx2, _ = C.gemm_nt(dy2, w2, False, add, True, 0, amask)
+                dx2, _ = C.gemm_nt(dy2, w2, False, add, True, 0, amask, dsub, h, w)
             dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
             if link is not None:
                 link.publish(dx, part)
         if ctx.needs_input_grad[1]:
             dw = _as_param_layout(C.gemm_tn(dy2, _rows(x), ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16)
                                             else torch.float32, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 def _unpack_bits(mask: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
@@ -190,21 +200,24 @@ def fork_supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
 RESIDUAL_HANDOFF = True
 
 
-def conv1x1_fork(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
-    """Returns (y, stats-or-None, x_alias); use ``x_alias`` as the residual identity."""
+def conv1x1_fork(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False, sub: bool = False):
+    """Returns (y, stats-or-None, x_alias, x_sub-or-None); use ``x_alias`` as the residual identity
+    and ``x_sub`` (= x[:, :, ::2, ::2], with sub) as a stride-2 downsample conv's input."""
     rlink = ResidualLink() if RESIDUAL_HANDOFF and x.requires_grad else None
-    y, stats, xa = _Conv1x1Fork.apply(x, conv.weight, want_stats, rlink)
+    y, stats, xa, xs = _Conv1x1Fork.apply(x, conv.weight, want_stats, rlink, sub)
     if rlink is not None:
         xa._dla_fork = rlink
-    return y, stats, xa
+    return y, stats, xa, xs
 
 
-def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
-    """Returns (y, stats-or-None); stats are [row_blocks, Cout, 2] partial (sum, sumsq)."""
-    if x.shape[2] % conv.stride[0] or x.shape[3] % conv.stride[1]:
+def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False, stride: int | None = None):
+    """Returns (y, stats-or-None); stats are [row_blocks, Cout, 2] partial (sum, sumsq).
+    ``stride`` overrides the module's (1 for an input that is already subsampled)."""
+    s = conv.stride[0] if stride is None else stride
+    if x.shape[2] % s or x.shape[3] % s:
         # odd spatial size with stride 2 (output ceil) — keep F.conv2d semantics exactly
-        return F.conv2d(x, conv.weight.to(x.dtype), None, conv.stride), None
-    return _Conv1x1.apply(x, conv.weight, conv.stride[0], want_stats)
+        return F.conv2d(x, conv.weight.to(x.dtype), None, s), None
+    return _Conv1x1.apply(x, conv.weight, s, want_stats)
 
 
 # ---------------------------------------------------------------------------------------------

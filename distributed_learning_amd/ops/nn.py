@@ -86,16 +86,18 @@ def native_conv() -> bool:
 
 
 def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool = True,
-                residual: torch.Tensor | None = None):
+                residual: torch.Tensor | None = None, presubsampled: bool = False):
     """``act(BN(conv(x)) [+ residual])``. With the native backend and native convs, a 1x1 conv runs as
     an MFMA GEMM whose epilogue also produces BN's batch statistics (one pass over the conv output
-    saved)."""
+    saved). ``presubsampled``: ``x`` is already the stride-2 subsample a strided 1x1 ``conv`` would
+    take (conv_bn_act_fork(..., subsample=True)), so the conv runs with stride 1."""
     if _BACKEND == "native" and _NATIVE_CONV and x.is_cuda:
         from . import conv as nconv
         from .bn_act import fused_bn_act, supported as bn_supported
 
         if nconv.supported(x, conv):
-            y, stats = nconv.conv1x1(x, conv, want_stats=bn.training)
+            stride = 1 if presubsampled else None
+            y, stats = nconv.conv1x1(x, conv, want_stats=bn.training, stride=stride)
             if stats is not None and not bn_supported(y, bn, residual):
                 stats = None
             return fused_bn_act(y, bn, relu, residual, stats)
@@ -105,22 +107,37 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
             if stats is not None and not bn_supported(y, bn, residual):
                 stats = None
             return fused_bn_act(y, bn, relu, residual, stats)
+    if presubsampled:
+        y = F.conv2d(x, conv.weight, conv.bias, 1, conv.padding, conv.dilation, conv.groups)
+        return bn_act(y, bn, relu, residual)
     return bn_act(conv(x), bn, relu, residual)
 
 
-def conv_bn_act_fork(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool = True):
-    """``(act(BN(conv(x))), identity)`` for a residual block whose identity branch is ``x`` itself.
+# conv_bn_act_fork(..., subsample=True) may return the stride-2 subsample (see there); tests flip it
+FORK_SUBSAMPLE = True
+
+
+def conv_bn_act_fork(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool = True,
+                     subsample: bool = False):
+    """``(act(BN(conv(x))), identity[, x_sub])`` for a residual block whose identity branch starts
+    at ``x`` itself.
 
     On the native path the returned identity is an alias of ``x`` produced by the same autograd
     node as the conv, so the block-input gradient (conv dgrad + identity gradient) is summed in
-    the dgrad GEMM epilogue (ops/conv.py::_Conv1x1Fork). Otherwise ``identity is x``."""
+    the dgrad GEMM epilogue (ops/conv.py::_Conv1x1Fork). With ``subsample`` a third output is
+    ``x[:, :, ::2, ::2]`` for a stride-2 downsample conv (``conv_bn_act(..., presubsampled=True)``),
+    whose compact gradient the same epilogue adds at the even pixels; None when the native path
+    does not apply (then subsample inside the downsample conv as usual)."""
     if _BACKEND == "native" and _NATIVE_CONV and x.is_cuda:
         from . import conv as nconv
         from .bn_act import fused_bn_act, supported as bn_supported
 
+        sub_ok = subsample and FORK_SUBSAMPLE and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0
         if nconv.fork_supported(x, conv):
-            y, stats, ident = nconv.conv1x1_fork(x, conv, want_stats=bn.training)
+            y, stats, ident, xs = nconv.conv1x1_fork(x, conv, want_stats=bn.training, sub=sub_ok)
             if stats is not None and not bn_supported(y, bn, None):
                 stats = None
-            return fused_bn_act(y, bn, relu, None, stats), ident
-    return conv_bn_act(x, conv, bn, relu), x
+            out = fused_bn_act(y, bn, relu, None, stats)
+            return (out, ident, xs if sub_ok else None) if subsample else (out, ident)
+    out = conv_bn_act(x, conv, bn, relu)
+    return (out, x, None) if subsample else (out, x)

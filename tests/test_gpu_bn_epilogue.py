@@ -122,3 +122,38 @@ def test_residual_handoff_is_exact(cuda):
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
     for n in g0:
         assert torch.equal(g1[n], g0[n]), n
+
+
+def test_fork_subsample_is_exact(cuda):
+    """Stride-2 downsample fed by the fork's compact subsample (gradient added at even pixels in the
+    dgrad epilogue) == subsampling inside the downsample conv (zero-filled scatter), bitwise."""
+    from distributed_learning_amd.models import resnet50
+    from distributed_learning_amd.ops import nn as dnn
+
+    def run(flag):
+        torch.manual_seed(0)
+        m = resnet50(10).to(cuda).to(memory_format=CL)
+        dnn.bf16_weights(m)
+        x = torch.randn(2, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+        old = dnn.FORK_SUBSAMPLE
+        dnn.FORK_SUBSAMPLE = flag
+        try:
+            out = m(x)
+            out.float().square().mean().backward()
+        finally:
+            dnn.FORK_SUBSAMPLE = old
+        return out.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters()}
+
+    det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    dnn.set_backend("native")
+    dnn.set_native_conv(True)
+    try:
+        (o1, g1), (o0, g0) = run(True), run(False)
+    finally:
+        dnn.set_native_conv(False)
+        dnn.set_backend("torch")
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
+    assert torch.equal(o1, o0)
+    for n in g0:
+        assert torch.equal(g1[n], g0[n]), n

@@ -70,7 +70,7 @@ def test_conv1x1_fork_sums_identity_gradient(cuda):
     gi = torch.randn(4, 256, 28, 28, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
 
     x1 = x.clone().requires_grad_(True)
-    y1, _, ident = conv1x1_fork(x1, conv)
+    y1, _, ident, _ = conv1x1_fork(x1, conv)
     assert ident.data_ptr() == x1.data_ptr()
     torch.autograd.backward([y1, ident], [g, gi])
     dw1 = conv.weight.grad.clone()
@@ -85,6 +85,6 @@ def test_conv1x1_fork_sums_identity_gradient(cuda):
 
     # identity gradient only (conv output unused) and conv gradient only
     x3 = x.clone().requires_grad_(True)
-    _, _, ident = conv1x1_fork(x3, conv)
+    _, _, ident, _ = conv1x1_fork(x3, conv)
     ident.backward(gi)
     assert torch.equal(x3.grad, gi)
