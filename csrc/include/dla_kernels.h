@@ -104,6 +104,15 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
                    float* dbeta, int mask_mode, hipStream_t stream, const float* ext_part = nullptr,
                    int ext_nrb = 0);
 
+// Stem BN(+ReLU)+max-pool fused (bn_act.hip): launch_bn_fwd with y == nullptr computes ws only;
+// then the pooled output + window positions come straight from the BN input x. Backward: the BN
+// passes gather dy from the pooled gradient. x/dx [N,H,W,C] bf16, pooled [N,OH,OW,C].
+void launch_bn_relu_maxpool_fwd(const void* x, const float* ws, void* y, uint8_t* pos, int N, int H, int W, int C,
+                                int OH, int OW, int k, int s, int p, hipStream_t stream);
+void launch_bn_relu_maxpool_bwd(const void* dy_pool, const uint8_t* pos, const void* x, void* dx, int N, int H, int W,
+                                int C, int OH, int OW, int k, int s, int p, const float* gamma, float* ws, float* part,
+                                float* dgamma, float* dbeta, hipStream_t stream);
+
 // ---- max pooling, NHWC (pool.hip) ------------------------------------------------------------
 // x [N,H,W,C], y/pos [N,OH,OW,C] (pos: window position k*ky+kx of the max, 1 byte), C % 8 == 0,
 // N*H*W*C/8 < 2^31. Backward writes every dx element (no zero-fill needed).

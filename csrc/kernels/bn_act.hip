@@ -18,6 +18,9 @@
 // the unfused chain. Partials are reduced in a fixed order -> bitwise reproducible.
 #include "dla_common.h"
 #include "dla_kernels.h"
+#include "dla_mfma.h"
+
+#include <algorithm>
 
 namespace dla {
 
@@ -254,8 +257,48 @@ __device__ __forceinline__ void apply_relu_mask(float (&g)[8], const float (&xv)
   }
 }
 
-template <typename T, int kMask>
-__global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+// Where the backward passes read dy from: the gradient tensor itself, or (stem BN(+ReLU) fused with
+// the 3x3/s2 max-pool that follows it) gathered from the pooled gradient and the forward's 1-byte
+// argmax positions — the full-resolution dy is never written.
+template <typename T>
+struct DirectDy {
+  const T* p;
+  __device__ __forceinline__ void load(int64_t off, int64_t /*r*/, int /*c0*/, int /*C*/, float (&g)[8]) const {
+    Vec8<T>::load(p + off, g);
+  }
+};
+
+struct PoolDy {
+  const bf16_t* dyp;   // pooled gradient [N, OH, OW, C]
+  const uint8_t* pos;  // window position of each pooled max (forward)
+  int H, W, OH, OW, k, s, pad;
+  mm::FastDiv fW, fH;
+  __device__ __forceinline__ void load(int64_t /*off*/, int64_t r, int c0, int C, float (&g)[8]) const {
+    const uint32_t q = mm::fdiv((uint32_t)r, fW);
+    const int w = (int)r - (int)q * W;
+    const uint32_t n = mm::fdiv(q, fH);
+    const int h = (int)q - (int)n * H;
+    const int hp = h + pad, wp = w + pad;
+    const int oh_lo = hp < k - 1 ? 0 : (hp - k + 1 + s - 1) / s, oh_hi = min(OH - 1, hp / s);
+    const int ow_lo = wp < k - 1 ? 0 : (wp - k + 1 + s - 1) / s, ow_hi = min(OW - 1, wp / s);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = 0.f;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh)
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const uint32_t qq = (uint32_t)((hp - oh * s) * k + (wp - ow * s));
+        const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c0;
+        const uint64_t packed = *reinterpret_cast<const uint64_t*>(pos + o);
+        float d[8];
+        Vec8<bf16_t>::load(dyp + o, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (((packed >> (8 * j)) & 0xffu) == qq) g[j] += d[j];
+      }
+  }
+};
+
+template <typename T, int kMask, class DY = DirectDy<T>>
+__global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(DY dy, const T* __restrict__ y,
                                                                    const uint8_t* __restrict__ mask,
                                                                    const T* __restrict__ x,
                                                                    const float* __restrict__ ws, int64_t M, int C,
@@ -278,7 +321,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(const T* __re
   for (int64_t r = r0 + rg; r < r1; r += rpi) {
     const int64_t off = r * C + c0;
     float g[8], xv[8];
-    Vec8<T>::load(dy + off, g);
+    dy.load(off, r, c0, C, g);
     Vec8<T>::load(x + off, xv);
     apply_relu_mask<T, kMask>(g, xv, sc, sh, y, mask, off);
 #pragma unroll
@@ -310,8 +353,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   ws[6 * C + c] = invstd * invstd * Q * inv_m;
 }
 
-template <typename T, int kMask, bool kDres>
-__global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+template <typename T, int kMask, bool kDres, class DY = DirectDy<T>>
+__global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(DY dy, const T* __restrict__ y,
                                                                   const uint8_t* __restrict__ mask,
                                                                   const T* __restrict__ x,
                                                                   const float* __restrict__ ws, T* __restrict__ dx,
@@ -335,7 +378,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(const T* __res
   for (int64_t r = r0 + rg; r < r1; r += rpi) {
     const int64_t off = r * C + c0;
     float g[8], xv[8];
-    Vec8<T>::load(dy + off, g);
+    dy.load(off, r, c0, C, g);
     Vec8<T>::load(x + off, xv);
     apply_relu_mask<T, kMask>(g, xv, sc, sh, y, mask, off);
     if (kDres) Vec8<T>::store(dres + off, g);
@@ -389,6 +432,7 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
     hipLaunchKernelGGL(bn_stats_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, x, dtype == kBF16, part,
                        nrb, M, C, gamma, beta, eps, momentum, running_mean, running_var, ws);
   }
+  if (!y) return;  // statistics only (the fused BN+ReLU+max-pool applies them itself)
   int atpr, anrb, anct;
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
 #define DLA_BN_APPLY(T, R, A)                                                                                      \
@@ -420,7 +464,7 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
   } else {
   const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
 #define DLA_BN_RED(T, K)                                                                                          \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, K>), dim3(nct, nrb), dim3(kBNThreads), lds, stream, (const T*)dy,     \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, K>), dim3(nct, nrb), dim3(kBNThreads), lds, stream, DirectDy<T>{(const T*)dy}, \
                      (const T*)y, mask, (const T*)x, (const float*)ws, M, C, nrb, tpr, part)
 #define DLA_BN_RED_ALL(T)                                 \
   switch (mask_mode) {                                    \
@@ -438,7 +482,7 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
   int atpr, anrb, anct;
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
 #define DLA_BN_BAPPLY(T, K, D)                                                                                      \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, K, D>), dim3(anct, anrb), dim3(kBNThreads), 0, stream, (const T*)dy,    \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, K, D>), dim3(anct, anrb), dim3(kBNThreads), 0, stream, DirectDy<T>{(const T*)dy}, \
                      (const T*)y, mask, (const T*)x, (const float*)ws, (T*)dx, (T*)dres, M, C, anrb, atpr)
 #define DLA_BN_BAPPLY_ALL(T, D)                                 \
   switch (mask_mode) {                                          \
@@ -454,6 +498,95 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
   }
 #undef DLA_BN_BAPPLY_ALL
 #undef DLA_BN_BAPPLY
+}
+
+// ---------------------------------------------------------------------------------------------
+// Stem BN + ReLU + max-pool (ResNet: 112x112x64 -> 56x56x64 at batch 256 = 411 MB -> 103 MB).
+// Forward: the pooled output straight from the conv output, y = max over the window of
+// bf16(relu(x*scale + shift)) with PyTorch's first-max tie rule on those bf16 values, plus the
+// 1-byte window position; the full-resolution activation is never written or re-read.
+// Backward: the BN reduce/apply passes gather dy from the pooled gradient (PoolDy) instead of a
+// materialised full-resolution gradient.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(const bf16_t* __restrict__ x,
+                                                                  const float* __restrict__ ws, bf16_t* __restrict__ y,
+                                                                  uint8_t* __restrict__ pos, int N, int H, int W, int C,
+                                                                  int OH, int OW, int k, int s, int p) {
+  const int cg = C / 8;
+  const int total = N * OH * OW * cg;
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
+    const int c = (t % cg) * 8;
+    int r = t / cg;
+    const int ow = r % OW;
+    r /= OW;
+    const int oh = r % OH;
+    const int n = r / OH;
+    float sc[8], sh[8], best[8];
+    uint32_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = ws[2 * C + c + j];
+      sh[j] = ws[3 * C + c + j];
+      best[j] = -INFINITY;
+      bi[j] = 0;
+    }
+    const int h0 = oh * s - p, w0 = ow * s - p;
+    for (int ky = 0; ky < k; ++ky) {
+      const int h = h0 + ky;
+      if (h < 0 || h >= H) continue;
+      for (int kx = 0; kx < k; ++kx) {
+        const int w = w0 + kx;
+        if (w < 0 || w >= W) continue;
+        float v[8];
+        Vec8<bf16_t>::load(x + (((int64_t)n * H + h) * W + w) * C + c, v);
+        const uint32_t q = (uint32_t)(ky * k + kx);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = bf16_to_f32(f32_to_bf16(fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f)));
+          if (a > best[j] || (a != a && best[j] == best[j])) {
+            best[j] = a;
+            bi[j] = q;
+          }
+        }
+      }
+    }
+    const int64_t off = (((int64_t)n * OH + oh) * OW + ow) * C + c;
+    Vec8<bf16_t>::store(y + off, best);
+    uint64_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) packed |= (uint64_t)bi[j] << (8 * j);
+    *reinterpret_cast<uint64_t*>(pos + off) = packed;
+  }
+}
+
+void launch_bn_relu_maxpool_fwd(const void* x, const float* ws, void* y, uint8_t* pos, int N, int H, int W, int C,
+                                int OH, int OW, int k, int s, int p, hipStream_t stream) {
+  const int64_t work = (int64_t)N * OH * OW * (C / 8);
+  const int nb = (int)std::min<int64_t>((work + 255) / 256, 256 * 32);
+  if (nb == 0) return;
+  hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel, dim3(nb), dim3(256), 0, stream, (const bf16_t*)x, ws, (bf16_t*)y, pos,
+                     N, H, W, C, OH, OW, k, s, p);
+}
+
+void launch_bn_relu_maxpool_bwd(const void* dy_pool, const uint8_t* pos, const void* x, void* dx, int N, int H, int W,
+                                int C, int OH, int OW, int k, int s, int p, const float* gamma, float* ws, float* part,
+                                float* dgamma, float* dbeta, hipStream_t stream) {
+  const int64_t M = (int64_t)N * H * W;
+  PoolDy pd{(const bf16_t*)dy_pool, pos, H, W, OH, OW, k, s, p, mm::make_fastdiv((uint32_t)W),
+            mm::make_fastdiv((uint32_t)H)};
+  int tpr, nrb, nct;
+  bn_geometry(M, C, &tpr, &nrb, &nct);
+  const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16_t, kMaskRecomp, PoolDy>), dim3(nct, nrb), dim3(kBNThreads), lds, stream,
+                     pd, (const bf16_t*)nullptr, (const uint8_t*)nullptr, (const bf16_t*)x, (const float*)ws, M, C, nrb,
+                     tpr, part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, part, nrb, M, C, gamma, ws,
+                     dgamma, dbeta);
+  int atpr, anrb, anct;
+  bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16_t, kMaskRecomp, false, PoolDy>), dim3(anct, anrb), dim3(kBNThreads), 0,
+                     stream, pd, (const bf16_t*)nullptr, (const uint8_t*)nullptr, (const bf16_t*)x, (const float*)ws,
+                     (bf16_t*)dx, (bf16_t*)nullptr, M, C, anrb, atpr);
 }
 
 }  // namespace dla

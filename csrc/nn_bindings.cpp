@@ -237,6 +237,62 @@ at::Tensor gemm_tn(at::Tensor A, at::Tensor B, c10::ScalarType out_dtype, double
   return out;
 }
 
+static int pool_out(int in, int k, int s, int p, bool ceil_mode);
+
+// Stem BatchNorm (training) + ReLU + max-pool: returns (y_pool, ws, pos). x is the BN input
+// (channels_last bf16); y_pool/pos [N, C, OH, OW] channels_last.
+std::vector<at::Tensor> bn_relu_maxpool_fwd(at::Tensor x, c10::optional<at::Tensor> weight,
+                                            c10::optional<at::Tensor> bias, c10::optional<at::Tensor> running_mean,
+                                            c10::optional<at::Tensor> running_var, double momentum, double eps,
+                                            int64_t k, int64_t s, int64_t p) {
+  check_act(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.scalar_type() == at::kBFloat16, "bn_relu_maxpool: bf16 4-D input");
+  TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && p >= 0 && 2 * p <= k, "bn_relu_maxpool: unsupported window");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int64_t M = (int64_t)N * H * W;
+  TORCH_CHECK(M < (1 << 24), "bn_relu_maxpool: too many pixels for 24-bit index math");
+  const int OH = pool_out(H, (int)k, (int)s, (int)p, false), OW = pool_out(W, (int)k, (int)s, (int)p, false);
+  auto f32 = x.options().dtype(at::kFloat);
+  auto fptr = [](const c10::optional<at::Tensor>& t) -> float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "BN parameters/stats must be fp32 contiguous");
+    return t->data_ptr<float>();
+  };
+  at::Tensor ws = at::empty({7 * (int64_t)C}, f32);
+  at::Tensor part = at::empty({partial_floats(M, C)}, f32);
+  launch_bn_fwd(x.data_ptr(), nullptr, nullptr, M, C, kBF16, fptr(weight), fptr(bias), (float)eps, (float)momentum,
+                fptr(running_mean), fptr(running_var), ws.data_ptr<float>(), part.data_ptr<float>(), true, true,
+                current_stream(x));
+  auto opts = x.options().memory_format(at::MemoryFormat::ChannelsLast);
+  at::Tensor y = at::empty({N, C, OH, OW}, opts);
+  at::Tensor pos = at::empty({N, C, OH, OW}, opts.dtype(at::kByte));
+  launch_bn_relu_maxpool_fwd(x.data_ptr(), ws.data_ptr<float>(), y.data_ptr(), pos.data_ptr<uint8_t>(), N, H, W, C, OH,
+                             OW, (int)k, (int)s, (int)p, current_stream(x));
+  return {y, ws, pos};
+}
+
+// Returns (dx, dgamma, dbeta) of the fused stem op, gathering dy from the pooled gradient.
+std::vector<at::Tensor> bn_relu_maxpool_bwd(at::Tensor dy_pool, at::Tensor pos, at::Tensor x, at::Tensor ws,
+                                            c10::optional<at::Tensor> weight, int64_t k, int64_t s, int64_t p) {
+  dy_pool = dy_pool.contiguous(at::MemoryFormat::ChannelsLast).to(at::kBFloat16);
+  check_act(x, "x");
+  TORCH_CHECK(pos.scalar_type() == at::kByte && pos.sizes() == dy_pool.sizes() &&
+                  pos.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "bn_relu_maxpool_bwd: pos must be the forward's positions");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int OH = (int)dy_pool.size(2), OW = (int)dy_pool.size(3);
+  const int64_t M = (int64_t)N * H * W;
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor part = at::empty({partial_floats(M, C)}, f32);
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dg = at::empty({C}, f32), db = at::empty({C}, f32);
+  const float* g = (weight.has_value() && weight->defined()) ? weight->data_ptr<float>() : nullptr;
+  launch_bn_relu_maxpool_bwd(dy_pool.data_ptr(), pos.data_ptr<uint8_t>(), x.data_ptr(), dx.data_ptr(), N, H, W, C, OH,
+                             OW, (int)k, (int)s, (int)p, g, ws.data_ptr<float>(), part.data_ptr<float>(),
+                             dg.data_ptr<float>(), db.data_ptr<float>(), current_stream(x));
+  return {dx, dg, db};
+}
+
 static int pool_out(int in, int k, int s, int p, bool ceil_mode) {
   int o = (in + 2 * p - k + (ceil_mode ? s - 1 : 0)) / s + 1;
   if (ceil_mode && (int64_t)(o - 1) * s >= in + p) --o;  // last window must start inside the input
@@ -388,6 +444,11 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("w"), pybind11::arg("addend") = pybind11::none(), pybind11::arg("tile") = 0);
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "implicit-GEMM 3x3 conv weight gradient (split-K)", pybind11::arg("dy"),
         pybind11::arg("x"), pybind11::arg("stride") = 1, pybind11::arg("out_dtype") = at::kFloat);
+  m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd, "stem BN(train)+ReLU+max-pool forward (pooled output only)",
+        pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"),
+        pybind11::arg("running_var"), pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("k"),
+        pybind11::arg("s"), pybind11::arg("p"));
+  m.def("bn_relu_maxpool_bwd", &bn_relu_maxpool_bwd, "stem BN+ReLU+max-pool backward (dy gathered from the pool)");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC max pooling forward (+ argmax window positions)", pybind11::arg("x"),
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("ceil_mode") = false,
         pybind11::arg("need_pos") = true);

@@ -137,8 +137,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = dnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-        x = self.maxpool(x)
+        x = dnn.conv_bn_act_maxpool(x, self.conv1, self.bn1, self.maxpool)
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)

@@ -113,6 +113,16 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
     return bn_act(conv(x), bn, relu, residual)
 
 
+def conv_bn_act_maxpool(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, pool: nn.Module):
+    """``pool(relu(BN(conv(x))))`` — the ResNet stem. Native path: the BN+ReLU+max-pool runs as one
+    fused op (the 112x112 activation and its gradient are never written)."""
+    if _BACKEND == "native" and x.is_cuda and isinstance(pool, nn.MaxPool2d):
+        from .bn_act import fused_bn_relu_maxpool
+
+        return fused_bn_relu_maxpool(conv(x), bn, pool)
+    return pool(conv_bn_act(x, conv, bn, relu=True))
+
+
 # conv_bn_act_fork(..., subsample=True) may return the stride-2 subsample (see there); tests flip it
 FORK_SUBSAMPLE = True
 

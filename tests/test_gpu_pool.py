@@ -46,3 +46,51 @@ def test_maxpool_nan_propagates(cuda):
     x[0, 3, 1, 1] = float("nan")
     y, _ = _ext.require().maxpool_fwd(x, 2, 2, 0, False, True)
     assert torch.isnan(y[0, 3, 0, 0]) and not torch.isnan(y[0, 2, 0, 0])
+
+
+def test_stem_bn_relu_maxpool_fused_matches_unfused(cuda):
+    """Fused stem op == separate fused-BN+ReLU then max-pool: identical pooled output, running
+    statistics and (up to reduction order) gradients."""
+    import torch.nn as nn
+
+    from distributed_learning_amd.ops import nn as dnn
+    from distributed_learning_amd.ops.bn_act import fused_bn_act, fused_bn_relu_maxpool
+    from distributed_learning_amd.ops.pool import MaxPool2d, max_pool2d
+
+    torch.manual_seed(0)
+    x = torch.randn(4, 64, 30, 30, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    bn1, bn2 = nn.BatchNorm2d(64).to(cuda), nn.BatchNorm2d(64).to(cuda)
+    with torch.no_grad():
+        bn1.weight.uniform_(0.5, 1.5)
+        bn1.bias.uniform_(-0.5, 0.5)
+    bn2.load_state_dict(bn1.state_dict())
+    pool = MaxPool2d(3, 2, 1)
+    dnn.set_backend("native")
+    try:
+        x1 = x.clone().requires_grad_(True)
+        y1 = fused_bn_relu_maxpool(x1, bn1, pool)
+        x2 = x.clone().requires_grad_(True)
+        y2 = max_pool2d(fused_bn_act(x2, bn2, True, None), 3, 2, 1)
+    finally:
+        dnn.set_backend("torch")
+    assert torch.equal(y1, y2)
+    torch.testing.assert_close(bn1.running_mean, bn2.running_mean)
+    torch.testing.assert_close(bn1.running_var, bn2.running_var)
+    g = torch.randn_like(y1)
+    y1.backward(g)
+    y2.backward(g)
+    # fp32 reference with the fused op's own pooling choice (ties broken identically): the fused
+    # backward sums overlapping-window gradients in fp32, the unfused max-pool backward rounds that
+    # sum to bf16 first, so the fused result must be at least as close to fp32
+    xr = x.float().requires_grad_(True)
+    bnr = nn.BatchNorm2d(64).to(cuda)
+    bnr.load_state_dict({k: v for k, v in bn2.state_dict().items()})
+    with torch.no_grad():
+        bnr.weight.copy_(bn1.weight)
+        bnr.bias.copy_(bn1.bias)
+    yr = torch.nn.functional.max_pool2d(torch.relu(bnr(xr)), 3, 2, 1)
+    yr.backward(g.float())
+    err = lambda a, b: float((a.float() - b).norm() / b.norm())  # noqa: E731
+    assert err(bn1.weight.grad, bnr.weight.grad) <= err(bn2.weight.grad, bnr.weight.grad) * 1.5 + 1e-3
+    assert err(bn1.bias.grad, bnr.bias.grad) <= err(bn2.bias.grad, bnr.bias.grad) * 1.5 + 1e-3
+    assert err(x1.grad, xr.grad) <= err(x2.grad, xr.grad) * 1.5 + 1e-3
