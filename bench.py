@@ -43,6 +43,8 @@ from distributed_learning_amd.parallel import context as ctxmod  # noqa: E402
 # Reference throughput at the same device count (GoogLeNet on P100 + Gloo/IPoIB):
 # N=1 the "single"/Ideal run, N>1 the best published real-DP number (PyTorch DDP).
 REFERENCE_IMG_S = {1: 317.5, 2: 573.6, 4: 1096.7, 8: 2040.9, 16: 3703.6}
+MODEL_NAMES = {"resnet50": "ResNet-50", "resnet18": "ResNet-18", "resnet34": "ResNet-34", "resnet101": "ResNet-101",
+               "resnet152": "ResNet-152", "googlenet": "GoogLeNet", "googlenet_noaux": "GoogLeNet"}
 
 
 def parse():
@@ -149,7 +151,7 @@ def main():
     ref = REFERENCE_IMG_S.get(world)
     if rank == 0:
         rec = {
-            "metric": "images/sec (whole node) ResNet-50 synthetic ImageNet",
+            "metric": f"images/sec (whole node) {MODEL_NAMES.get(a.model, a.model)} synthetic ImageNet",
             "value": round(img_s, 2),
             "unit": "images/sec",
             "n_gpus": world,

@@ -132,10 +132,11 @@ void launch_maxpool_bwd(const void* dy, const uint8_t* pos, void* dx, int N, int
 void set_mfma_pipeline(int p);  // -1 = per-shape auto
 int mfma_pipeline();
 int mfma_pipeline_for(int K);
-enum TileCfg : int { kTileAuto = 0, kTile128x128 = 1, kTile128x64 = 2, kTile64x64 = 3 };
+// kTile256x128: 8 waves (512 threads), 3-stage LDS-DMA pipeline, one block per CU.
+enum TileCfg : int { kTileAuto = 0, kTile128x128 = 1, kTile128x64 = 2, kTile64x64 = 3, kTile256x128 = 4 };
 int pick_tile(int64_t M, int N, int tile);
-inline int tile_bm(int cfg) { return cfg == kTile64x64 ? 64 : 128; }
-inline int tile_bn(int cfg) { return cfg == kTile128x128 ? 128 : 64; }
+inline int tile_bm(int cfg) { return cfg == kTile64x64 ? 64 : (cfg == kTile256x128 ? 256 : 128); }
+inline int tile_bn(int cfg) { return (cfg == kTile128x128 || cfg == kTile256x128) ? 128 : 64; }
 // rows of BN-statistics partials ([rows][N][2]) a stats-producing launch writes (one per row tile)
 int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto);
 // BatchNorm-backward reduction fused into a bf16-output GEMM epilogue (the output is the BN's dy):

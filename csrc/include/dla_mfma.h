@@ -3,7 +3,7 @@
 // 3x3 convolutions) instantiate the same main loop with different global-memory loaders, so every
 // conv variant inherits the tuned tile schedule instead of re-implementing it.
 //
-// Block = 256 threads = 2x2 waves; a block computes a BM x BN tile of C with
+// Block = NT threads = (NT/128) x 2 waves (NT = 256: 2x2, NT = 512: 4x2); a block computes a BM x BN tile of C with
 // v_mfma_f32_16x16x32_bf16 (fp32 accumulate), kBK = 64 deep K steps staged through LDS with the
 // next step's global loads in flight during the current step's MFMAs (T14 register staging).
 // Operand tiles live in LDS either
@@ -69,10 +69,10 @@ __device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* lo_ptr, const bf16_t* 
   return *reinterpret_cast<const bf16x8_t*>(v);
 }
 
-template <int W>
+template <int W, int NT = kThreads>
 struct TileGeom {
-  static constexpr int CH = W * kBK / 8 / kThreads;  // 16-byte chunks per thread per k-step
-  static_assert(CH >= 1, "tile too small for 256 threads");
+  static constexpr int CH = W * kBK / 8 / NT;  // 16-byte chunks per thread per k-step
+  static_assert(CH >= 1, "tile too small for the block's threads");
   static constexpr int KPR = W / 8;  // k-major: chunks per k-row
   // row-major: chunk c -> (row c >> 3, k (c & 7) * 8); k-major: chunk c -> (k c / KPR, col (c % KPR) * 8)
   static constexpr int kRowElems = W * (kBK + 8);
@@ -122,52 +122,82 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 
 // ---- loaders ------------------------------------------------------------------------------------
 // A loader exposes kKMajor and  ushort8_t load(int i, int k0) const  returning the 8 elements of
-// chunk slot i (chunk id c = tid + i * 256) for the k-step starting at k0, zeros out of range.
+// chunk slot i (chunk id c = tid + i * NT) for the k-step starting at k0, zeros out of range
+// (register-staged loop), and  src(i, k0)  = the global address of that chunk or the zero page
+// (LDS-DMA loop). prep() runs once per tile before the LDS-DMA loop and hoists everything that
+// does not depend on k0 (row/column bounds, 64-bit row bases), so the per-k-step address of a
+// chunk is one 64-bit add of a wave-uniform offset plus a select.
 
 // Row-major matrix [rows][K] (K contiguous): A of gemm_nt, B of gemm_nt (weights [N][K]).
-template <int W>
+template <int W, int NT = kThreads>
 struct RowLoader {
   static constexpr bool kKMajor = false;
+  static constexpr int kNT = NT;
+  static constexpr int CH = TileGeom<W, NT>::CH;
   const bf16_t* p;
   int64_t ld;
   int64_t row0, rows;
   int K;
+  const bf16_t* sp[CH];
+  int skc[CH];  // logical k offset of the slot, or INT_MAX / 2 when its row is out of range
   __device__ ushort8_t load(int i, int k0) const {
-    const int c = threadIdx.x + i * kThreads, r = c >> 3, kc = (c & 7) * 8;
+    const int c = threadIdx.x + i * NT, r = c >> 3, kc = (c & 7) * 8;
     const int64_t gr = row0 + r;
     return (gr < rows && k0 + kc < K) ? *reinterpret_cast<const ushort8_t*>(p + gr * ld + k0 + kc) : zero8();
   }
+  __device__ void prep() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + i * NT, r = c >> 3, kc = rm_glds_kc(c);
+      const int64_t gr = row0 + r;
+      const bool ok = gr < rows;
+      sp[i] = p + (ok ? gr * ld : 0) + kc;
+      skc[i] = ok ? kc : (1 << 30);
+    }
+  }
   __device__ const void* src(int i, int k0) const {
-    const int c = threadIdx.x + i * kThreads, r = c >> 3, kc = rm_glds_kc(c);
-    const int64_t gr = row0 + r;
-    return (gr < rows && k0 + kc < K) ? (const void*)(p + gr * ld + k0 + kc) : zero_src();
+    return (k0 + skc[i] < K) ? (const void*)(sp[i] + k0) : zero_src();
   }
 };
 
 // k-major matrix [K][cols] (cols contiguous): gemm_tn operands, dgrad weights as stored.
-template <int W>
+template <int W, int NT = kThreads>
 struct KLoader {
   static constexpr bool kKMajor = true;
+  static constexpr int kNT = NT;
+  static constexpr int CH = TileGeom<W, NT>::CH;
   const bf16_t* p;
   int64_t ld;
   int col0, cols;
   int kend;
+  const bf16_t* sp[CH];
+  int skr[CH];  // k row of the slot, or INT_MAX / 2 when its column is out of range
   __device__ ushort8_t load(int i, int k0) const {
-    const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR, nc = (c % TileGeom<W>::KPR) * 8;
+    const int c = threadIdx.x + i * NT, kr = c / TileGeom<W>::KPR, nc = (c % TileGeom<W>::KPR) * 8;
     const int gk = k0 + kr, gc = col0 + nc;
     return (gk < kend && gc < cols) ? *reinterpret_cast<const ushort8_t*>(p + (int64_t)gk * ld + gc) : zero8();
   }
+  __device__ void prep() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + i * NT, kr = c / TileGeom<W>::KPR;
+      const int gc = col0 + km_glds_col<W>(c);
+      const bool ok = gc < cols;
+      sp[i] = p + (int64_t)kr * ld + (ok ? gc : 0);
+      skr[i] = ok ? kr : (1 << 30);
+    }
+  }
   __device__ const void* src(int i, int k0) const {
-    const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR;
-    const int gk = k0 + kr, gc = col0 + km_glds_col<W>(c);
-    return (gk < kend && gc < cols) ? (const void*)(p + (int64_t)gk * ld + gc) : zero_src();
+    return (k0 + skr[i] < kend) ? (const void*)(sp[i] + (int64_t)k0 * ld) : zero_src();
   }
 };
 
 // ---- main loop -----------------------------------------------------------------------------------
-template <int BM, int BN>
+template <int BM, int BN, int NT = kThreads>
 struct Acc {
-  static constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  static constexpr int kNT = NT, WGM = NT / 128;  // waves along M (2 along N)
+  static constexpr int WM = BM / WGM, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  static_assert(TM >= 1 && TN >= 1, "wave tile below one MFMA fragment");
   f32x4_t v[TM][TN];
   __device__ void zero() {
 #pragma unroll
@@ -184,10 +214,10 @@ __host__ __device__ constexpr size_t mainloop_lds_bytes() {
 }
 
 template <int W, class L>
-__device__ __forceinline__ void tile_store(bf16_t* s, const ushort8_t (&r)[TileGeom<W>::CH]) {
+__device__ __forceinline__ void tile_store(bf16_t* s, const ushort8_t (&r)[TileGeom<W, L::kNT>::CH]) {
 #pragma unroll
-  for (int i = 0; i < TileGeom<W>::CH; ++i) {
-    const int c = threadIdx.x + i * kThreads;
+  for (int i = 0; i < TileGeom<W, L::kNT>::CH; ++i) {
+    const int c = threadIdx.x + i * L::kNT;
     if constexpr (L::kKMajor)
       *reinterpret_cast<ushort8_t*>(s + tr_off<W>(c / TileGeom<W>::KPR, (c % TileGeom<W>::KPR) * 8)) = r[i];
     else
@@ -210,12 +240,14 @@ __device__ __forceinline__ bf16x8_t tile_frag(const bf16_t* s, int r0, int kk) {
 }
 
 // acc += A[BM rows, k in [kbeg, kend)] * B[BN cols, same k]^T
-template <int BM, int BN, class LA, class LB>
-__device__ __forceinline__ void mainloop(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN>& acc,
+template <int BM, int BN, int NT, class LA, class LB>
+__device__ __forceinline__ void mainloop(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
                                          char* smem) {
-  using GA = TileGeom<BM>;
-  using GB = TileGeom<BN>;
-  constexpr int WM = Acc<BM, BN>::WM, WN = Acc<BM, BN>::WN, TM = Acc<BM, BN>::TM, TN = Acc<BM, BN>::TN;
+  static_assert(LA::kNT == NT && LB::kNT == NT, "loaders built for another block size");
+  using GA = TileGeom<BM, NT>;
+  using GB = TileGeom<BN, NT>;
+  using AC = Acc<BM, BN, NT>;
+  constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);
   bf16_t* Bs = As + (LA::kKMajor ? GA::kKElems : GA::kRowElems);
   const int wid = threadIdx.x >> 6, wr = wid >> 1, wc = wid & 1;
@@ -277,14 +309,16 @@ __host__ __device__ constexpr size_t glds_lds_bytes() {
 // barrier per k-step. Iteration t: wait until this wave's DMAs for tile t are done (the younger
 // stages may stay outstanding: counted vmcnt), barrier (everyone's tile t has landed AND everyone
 // finished tile t-1, whose stage the next DMA overwrites), issue tile t+NS-1, multiply tile t.
-template <int BM, int BN, int NS, class LA, class LB>
-__device__ __forceinline__ void mainloop_glds(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN>& acc,
+template <int BM, int BN, int NT, int NS, class LA, class LB>
+__device__ __forceinline__ void mainloop_glds(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
                                               char* smem) {
   static_assert(NS == 2 || NS == 3, "2 or 3 stages");
-  using GA = TileGeom<BM>;
-  using GB = TileGeom<BN>;
+  static_assert(LA::kNT == NT && LB::kNT == NT, "loaders built for another block size");
+  using GA = TileGeom<BM, NT>;
+  using GB = TileGeom<BN, NT>;
+  using AC = Acc<BM, BN, NT>;
   constexpr int L = GA::CH + GB::CH;  // DMA instructions per wave per tile
-  constexpr int WM = Acc<BM, BN>::WM, WN = Acc<BM, BN>::WN, TM = Acc<BM, BN>::TM, TN = Acc<BM, BN>::TN;
+  constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
   constexpr int SA = BM * kBK, SB = BN * kBK;  // elements per stage
   bf16_t* base = reinterpret_cast<bf16_t*>(smem);
   const int wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
@@ -292,15 +326,19 @@ __device__ __forceinline__ void mainloop_glds(const LA& la, const LB& lb, int kb
   const uint32_t wofs = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
   const int nk = (kend - kbeg + kBK - 1) / kBK;
   if (nk <= 0) return;
+  LA pa = la;
+  LB pb = lb;
+  pa.prep();
+  pb.prep();
   auto issue = [&](int t) {
     const int st = t % NS;
     const int k0 = kbeg + t * kBK;
     const uint32_t a_base = lds0 + (uint32_t)(st * (SA + SB)) * 2u + wofs;
     const uint32_t b_base = a_base + (uint32_t)SA * 2u;
 #pragma unroll
-    for (int i = 0; i < GA::CH; ++i) glds16(la.src(i, k0), a_base + (uint32_t)(i * kThreads * 16));
+    for (int i = 0; i < GA::CH; ++i) glds16(pa.src(i, k0), a_base + (uint32_t)(i * NT * 16));
 #pragma unroll
-    for (int i = 0; i < GB::CH; ++i) glds16(lb.src(i, k0), b_base + (uint32_t)(i * kThreads * 16));
+    for (int i = 0; i < GB::CH; ++i) glds16(pb.src(i, k0), b_base + (uint32_t)(i * NT * 16));
   };
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
@@ -335,11 +373,11 @@ __device__ __forceinline__ void mainloop_glds(const LA& la, const LB& lb, int kb
 
 // Pipeline selection shared by all MFMA kernels: 0 = register staging (one k-step in flight,
 // 3 blocks/CU), 2 / 3 = LDS-DMA with 2 / 3 stages.
-template <int PIPE, int BM, int BN, class LA, class LB>
-__device__ __forceinline__ void run_mainloop(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN>& acc,
+template <int PIPE, int BM, int BN, int NT, class LA, class LB>
+__device__ __forceinline__ void run_mainloop(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
                                              char* smem) {
-  if constexpr (PIPE == 0) mainloop<BM, BN>(la, lb, kbeg, kend, acc, smem);
-  else mainloop_glds<BM, BN, PIPE>(la, lb, kbeg, kend, acc, smem);
+  if constexpr (PIPE == 0) mainloop<BM, BN, NT>(la, lb, kbeg, kend, acc, smem);
+  else mainloop_glds<BM, BN, NT, PIPE>(la, lb, kbeg, kend, acc, smem);
 }
 
 template <int PIPE, int BM, int BN, class LA, class LB>
@@ -348,22 +386,22 @@ __host__ __device__ constexpr size_t run_mainloop_lds_bytes() {
 }
 
 // ---- epilogues -------------------------------------------------------------------------------
-template <int BM, int BN, bool kStats>
+template <int BM, int BN, bool kStats, int NT = kThreads>
 __host__ __device__ constexpr size_t epilogue_lds_bytes() {
-  // C staging tile; the BN-backward partial combine ([256 / (BN/8)][BN][2] floats = 16 KB) and the
-  // statistics flush reuse the same bytes afterwards
-  return (size_t)BM * (BN + 8) * sizeof(bf16_t) > (size_t)16384 ? (size_t)BM * (BN + 8) * sizeof(bf16_t)
-                                                                 : (size_t)16384;
+  // C staging tile; the BN-backward partial combine ([NT / (BN/8)][BN][2] floats = NT * 64 B) and
+  // the statistics flush reuse the same bytes afterwards
+  return (size_t)BM * (BN + 8) * sizeof(bf16_t) > (size_t)NT * 64 ? (size_t)BM * (BN + 8) * sizeof(bf16_t)
+                                                                  : (size_t)NT * 64;
 }
 
 // Column statistics of a block's output tile(s): a lane owns one column of each 16x16 fragment, so
 // each wave keeps TN (sum, sumsq) in registers until stats_flush.
-template <int BM, int BN>
+template <int BM, int BN, int NT = kThreads>
 struct ColStats {
-  float s[Acc<BM, BN>::TN], q[Acc<BM, BN>::TN];
+  float s[Acc<BM, BN, NT>::TN], q[Acc<BM, BN, NT>::TN];
   __device__ void zero() {
 #pragma unroll
-    for (int j = 0; j < Acc<BM, BN>::TN; ++j) s[j] = q[j] = 0.f;
+    for (int j = 0; j < Acc<BM, BN, NT>::TN; ++j) s[j] = q[j] = 0.f;
   }
 };
 
@@ -394,9 +432,9 @@ struct BnBwdEpi {
   FastDiv fW, fH;
 };
 
-template <int BM, int BN, bool kStats, bool kEpi = false>
-__device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __restrict__ C, int64_t ldc, int64_t M,
-                                              int N, int64_t row0, int col0, ColStats<BM, BN>& st,
+template <int BM, int BN, bool kStats, bool kEpi = false, int NT = kThreads>
+__device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t* __restrict__ C, int64_t ldc,
+                                              int64_t M, int N, int64_t row0, int col0, ColStats<BM, BN, NT>& st,
                                               const bf16_t* __restrict__ D, int64_t ldd, char* smem,
                                               const BnBwdEpi* epi = nullptr, int bm = 0) {
   // kEpi compiles in the BN-backward partials and the masked addend (dgrad kernels only: they cost
@@ -404,7 +442,8 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
   const BnBwdEpi* bnb = (kEpi && epi && epi->x) ? epi : nullptr;
   const uint8_t* __restrict__ dmask = (kEpi && epi) ? epi->dmask : nullptr;
   const bf16_t* __restrict__ d2 = (kEpi && epi) ? epi->d2 : nullptr;
-  constexpr int WM = Acc<BM, BN>::WM, WN = Acc<BM, BN>::WN, TM = Acc<BM, BN>::TM, TN = Acc<BM, BN>::TN;
+  using AC = Acc<BM, BN, NT>;
+  constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
   constexpr int LDS_C = BN + 8;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
   bf16_t* Cs = reinterpret_cast<bf16_t*>(smem);
@@ -426,12 +465,12 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
       }
   __syncthreads();
   constexpr int CPR = BN / 8;
-  static_assert(kThreads % CPR == 0, "a thread keeps one 8-column group in the store loop");
+  static_assert(NT % CPR == 0, "a thread keeps one 8-column group in the store loop");
   // BN-backward partials: this thread's 8 columns are fixed (c % CPR) across its rows. The x (and
   // mask) chunks of all its rows are loaded up front, so those global loads overlap each other and
   // the C stores instead of each waiting a full round trip inside the loop.
-  constexpr int NIT = BM * CPR / kThreads;
-  static_assert(BM * CPR % kThreads == 0, "whole store-loop iterations");
+  constexpr int NIT = BM * CPR / NT;
+  static_assert(BM * CPR % NT == 0, "whole store-loop iterations");
   const int my_cc = (tid % CPR) * 8;
   float bs[8], bq[8], mean[8], sc[8], sh[8];
   ushort8_t xr[NIT];
@@ -447,7 +486,7 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
     }
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      const int r = (tid + it * kThreads) / CPR;
+      const int r = (tid + it * NT) / CPR;
       const int64_t gm = row0 + r;
       const int gn = col0 + my_cc;
       const bool ok = gm < M && gn < N;
@@ -458,7 +497,7 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
   }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
-    const int c = tid + it * kThreads;
+    const int c = tid + it * NT;
     const int r = c / CPR, cc = (c % CPR) * 8;
     const int64_t gm = row0 + r;
     const int gn = col0 + cc;
@@ -499,8 +538,8 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
   }
   __syncthreads();
   if (bnb) {
-    // combine the kThreads / CPR row groups of each column through LDS (the C staging is free now)
-    constexpr int RG = kThreads / CPR;
+    // combine the NT / CPR row groups of each column through LDS (the C staging is free now)
+    constexpr int RG = NT / CPR;
     float* red = reinterpret_cast<float*>(smem);  // [RG][BN][2]
     const int rg = tid / CPR;
 #pragma unroll
@@ -509,7 +548,7 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
       red[(rg * BN + my_cc + j) * 2 + 1] = bq[j];
     }
     __syncthreads();
-    for (int idx = tid; idx < BN * 2; idx += kThreads) {
+    for (int idx = tid; idx < BN * 2; idx += NT) {
       float a = 0.f;
       for (int g = 0; g < RG; ++g) a += red[g * BN * 2 + idx];
       const int col = idx >> 1;
@@ -521,12 +560,13 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN>& acc, bf16_t* __
 
 // Writes a block's accumulated column statistics as one partial row: out[N][2] at columns col0..
 // (the 4 lane groups sharing a column combine by xor-shuffles, the 2 M-waves through LDS).
-template <int BM, int BN>
-__device__ __forceinline__ void stats_flush(ColStats<BM, BN>& st, float* __restrict__ out, int N, int col0,
+template <int BM, int BN, int NT = kThreads>
+__device__ __forceinline__ void stats_flush(ColStats<BM, BN, NT>& st, float* __restrict__ out, int N, int col0,
                                             char* smem) {
-  constexpr int WN = Acc<BM, BN>::WN, TN = Acc<BM, BN>::TN;
+  using AC = Acc<BM, BN, NT>;
+  constexpr int WN = AC::WN, TN = AC::TN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
-  float* red = reinterpret_cast<float*>(smem);  // [2 wr][BN][2]
+  float* red = reinterpret_cast<float*>(smem);  // [WGM wr][BN][2]
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     float a = st.s[j], b = st.q[j];
@@ -542,16 +582,23 @@ __device__ __forceinline__ void stats_flush(ColStats<BM, BN>& st, float* __restr
   }
   __syncthreads();
   if (tid < BN && col0 + tid < N) {
-    out[(int64_t)(col0 + tid) * 2 + 0] = red[tid * 2 + 0] + red[(BN + tid) * 2 + 0];
-    out[(int64_t)(col0 + tid) * 2 + 1] = red[tid * 2 + 1] + red[(BN + tid) * 2 + 1];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int g = 0; g < AC::WGM; ++g) {
+      a += red[(g * BN + tid) * 2 + 0];
+      b += red[(g * BN + tid) * 2 + 1];
+    }
+    out[(int64_t)(col0 + tid) * 2 + 0] = a;
+    out[(int64_t)(col0 + tid) * 2 + 1] = b;
   }
 }
 
 // fp32 split-K partial slab P[Mo][No] (row m = M-side index, col n = N-side index)
-template <int BM, int BN>
-__device__ __forceinline__ void epilogue_f32(const Acc<BM, BN>& acc, float* __restrict__ P, int Mo, int No, int m0,
-                                             int n0) {
-  constexpr int WM = Acc<BM, BN>::WM, WN = Acc<BM, BN>::WN, TM = Acc<BM, BN>::TM, TN = Acc<BM, BN>::TN;
+template <int BM, int BN, int NT = kThreads>
+__device__ __forceinline__ void epilogue_f32(const Acc<BM, BN, NT>& acc, float* __restrict__ P, int Mo, int No,
+                                             int m0, int n0) {
+  using AC = Acc<BM, BN, NT>;
+  constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
 #pragma unroll
   for (int i = 0; i < TM; ++i)

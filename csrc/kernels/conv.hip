@@ -35,20 +35,26 @@ struct ConvGeom {
 
 // A operand of forward / dgrad: row = output pixel of this GEMM, K = (tap, channel) with the channel
 // fastest. kFlip: dgrad (source = o + 1 - k), otherwise forward (source = o*s - 1 + k).
-template <int W, bool kFlip>
+template <int W, bool kFlip, int NT = kThreads>
 struct Im2colRowLoader {
   static constexpr bool kKMajor = false;
-  static constexpr int CH = TileGeom<W>::CH;
+  static constexpr int kNT = NT;
+  static constexpr int CH = TileGeom<W, NT>::CH;
   const bf16_t* x;
   int H, Wd, C;  // source image height, width, channels
   int stride;
   int32_t pbase[CH];  // n * H * Wd of each slot's pixel, -1 when the pixel is past the end
   int ih0[CH], iw0[CH];
+  // LDS-DMA form: the slot's source address at tap (0, 0) and channel base 0, and a 9-bit mask of
+  // the taps that fall inside the image (0 past the end): per k-step one wave-uniform offset
+  // (tap shift + channel base) is added and the tap's bit selects it or the zero page.
+  const bf16_t* sp[CH];
+  uint32_t smask[CH];
   __device__ void init(const ConvGeom& g, int64_t row0, int64_t P, int oh_dim, int ow_dim, const FastDiv& fw,
                        const FastDiv& fh) {
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
-      const int c = threadIdx.x + i * kThreads, r = c >> 3;
+      const int c = threadIdx.x + i * NT, r = c >> 3;
       const int64_t p = row0 + r;
       if (p < P) {
         const uint32_t q = fdiv((uint32_t)p, fw);
@@ -65,6 +71,21 @@ struct Im2colRowLoader {
     }
     (void)g;
   }
+  __device__ void prep() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int kc = rm_glds_kc(threadIdx.x + i * NT);
+      uint32_t m = 0;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int ih = kFlip ? ih0[i] - t / 3 : ih0[i] + t / 3;
+        const int iw = kFlip ? iw0[i] - t % 3 : iw0[i] + t % 3;
+        m |= ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)Wd) ? (1u << t) : 0u;
+      }
+      smask[i] = pbase[i] < 0 ? 0u : m;
+      sp[i] = x + ((int64_t)(pbase[i] < 0 ? 0 : pbase[i]) + (int64_t)ih0[i] * Wd + iw0[i]) * C + kc;
+    }
+  }
   __device__ ushort8_t load(int i, int k0) const {
     const int tap = k0 / C;  // uniform across the block
     const int ci = k0 - tap * C + (threadIdx.x & 7) * 8;
@@ -75,51 +96,62 @@ struct Im2colRowLoader {
     return *reinterpret_cast<const ushort8_t*>(x + ((int64_t)pbase[i] + ih * Wd + iw) * C + ci);
   }
   __device__ const void* src(int i, int k0) const {
-    const int tap = k0 / C;
-    const int ci = k0 - tap * C + rm_glds_kc(threadIdx.x + i * kThreads);
+    const int tap = k0 / C;  // uniform: scalar arithmetic
     const int kh = tap / 3, kw = tap - 3 * (tap / 3);
-    const int ih = kFlip ? ih0[i] - kh : ih0[i] + kh;
-    const int iw = kFlip ? iw0[i] - kw : iw0[i] + kw;
-    if (pbase[i] < 0 || tap >= 9 || (unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)Wd) return zero_src();
-    return x + ((int64_t)pbase[i] + ih * Wd + iw) * C + ci;
+    const int shift = kh * Wd + kw;
+    const int64_t off = (int64_t)(kFlip ? -shift : shift) * C + (k0 - tap * C);
+    return ((smask[i] >> tap) & 1u) ? (const void*)(sp[i] + off) : zero_src();
   }
 };
 
 // B operand of dgrad: k = (tap, co) rows, n = ci columns, element W[co][tap][ci] (k-major per tap).
-template <int W>
+template <int W, int NT = kThreads>
 struct WeightTapKLoader {
   static constexpr bool kKMajor = true;
+  static constexpr int kNT = NT;
+  static constexpr int CH = TileGeom<W, NT>::CH;
   const bf16_t* w;
   int Cout, Cin, col0;
+  const bf16_t* sp[CH];
+  bool sok[CH];
   __device__ ushort8_t load(int i, int k0) const {
-    const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR, nc = (c % TileGeom<W>::KPR) * 8;
+    const int c = threadIdx.x + i * NT, kr = c / TileGeom<W>::KPR, nc = (c % TileGeom<W>::KPR) * 8;
     const int tap = k0 / Cout;  // uniform
     const int co = k0 - tap * Cout + kr, ci = col0 + nc;
     if (tap >= 9 || ci >= Cin) return zero8();
     return *reinterpret_cast<const ushort8_t*>(w + ((int64_t)co * 9 + tap) * Cin + ci);
   }
+  __device__ void prep() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + i * NT, kr = c / TileGeom<W>::KPR;
+      const int ci = col0 + km_glds_col<W>(c);
+      sok[i] = ci < Cin;
+      sp[i] = w + (int64_t)kr * 9 * Cin + (sok[i] ? ci : 0);
+    }
+  }
   __device__ const void* src(int i, int k0) const {
-    const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR;
     const int tap = k0 / Cout;
-    const int co = k0 - tap * Cout + kr, ci = col0 + km_glds_col<W>(c);
-    if (tap >= 9 || ci >= Cin) return zero_src();
-    return w + ((int64_t)co * 9 + tap) * Cin + ci;
+    const int64_t off = ((int64_t)(k0 - tap * Cout) * 9 + tap) * Cin;
+    return sok[i] ? (const void*)(sp[i] + off) : zero_src();
   }
 };
 
 // B operand of wgrad: k = output pixel rows, n = (tap, ci) columns, element X[src(p, tap)][ci].
-template <int W, bool kGlds>
+template <int W, bool kGlds, int NT = kThreads>
 struct Im2colKLoader {
   static constexpr bool kKMajor = true;
-  static constexpr int CH = TileGeom<W>::CH;
+  static constexpr int kNT = NT;
+  static constexpr int CH = TileGeom<W, NT>::CH;
   const bf16_t* x;
   ConvGeom g;
   int kend;
   int kh[CH], kw[CH], ci[CH];  // per slot: fixed column -> (tap, channel); kh = -100 if out of range
+  __device__ void prep() {}
   __device__ void init(int col0) {
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
-      const int c = threadIdx.x + i * kThreads;
+      const int c = threadIdx.x + i * NT;
       const int nc = col0 + (kGlds ? km_glds_col<W>(c) : (c % TileGeom<W>::KPR) * 8);
       const int tap = nc / g.Cin;
       ci[i] = nc - tap * g.Cin;
@@ -128,7 +160,7 @@ struct Im2colKLoader {
     }
   }
   __device__ ushort8_t load(int i, int k0) const {
-    const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR;
+    const int c = threadIdx.x + i * NT, kr = c / TileGeom<W>::KPR;
     const int p = k0 + kr;
     if (p >= kend || kh[i] < 0) return zero8();
     const uint32_t q = fdiv((uint32_t)p, g.fOW);
@@ -140,7 +172,7 @@ struct Im2colKLoader {
     return *reinterpret_cast<const ushort8_t*>(x + (((int64_t)n * g.H + ih) * g.W + iw) * g.Cin + ci[i]);
   }
   __device__ const void* src(int i, int k0) const {
-    const int c = threadIdx.x + i * kThreads, kr = c / TileGeom<W>::KPR;
+    const int c = threadIdx.x + i * NT, kr = c / TileGeom<W>::KPR;
     const int p = k0 + kr;
     if (p >= kend || kh[i] < 0) return zero_src();
     const uint32_t q = fdiv((uint32_t)p, g.fOW);
@@ -154,8 +186,8 @@ struct Im2colKLoader {
 };
 
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, bool kStats, int PIPE>
-__global__ __launch_bounds__(kThreads, 2) void conv3x3_fwd_kernel(const bf16_t* __restrict__ x,
+template <int BM, int BN, bool kStats, int PIPE, int NT>
+__global__ __launch_bounds__(NT, NT == kThreads ? 2 : 1) void conv3x3_fwd_kernel(const bf16_t* __restrict__ x,
                                                                   const bf16_t* __restrict__ w,
                                                                   bf16_t* __restrict__ y, ConvGeom g,
                                                                   float* __restrict__ stats) {
@@ -167,21 +199,21 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_fwd_kernel(const bf16_t* 
   const int64_t row0 = (int64_t)bm * BM;
   const int col0 = bn * BN;
   const int K = 9 * g.Cin;
-  const RowLoader<BN> lb{w, K, (int64_t)col0, g.Cout, K};
-  Im2colRowLoader<BM, false> la{x, g.H, g.W, g.Cin, g.stride};
+  const RowLoader<BN, NT> lb{w, K, (int64_t)col0, g.Cout, K};
+  Im2colRowLoader<BM, false, NT> la{x, g.H, g.W, g.Cin, g.stride};
   la.init(g, row0, P, g.OH, g.OW, g.fOW, g.fOH);
-  ColStats<BM, BN> st;
+  ColStats<BM, BN, NT> st;
   st.zero();
-  Acc<BM, BN> acc;
+  Acc<BM, BN, NT> acc;
   acc.zero();
   run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
-  epilogue_bf16<BM, BN, kStats>(acc, y, g.Cout, P, g.Cout, row0, col0, st, nullptr, 0, smem_raw);
-  if constexpr (kStats) stats_flush<BM, BN>(st, stats + (int64_t)bm * g.Cout * 2, g.Cout, col0, smem_raw);
+  epilogue_bf16<BM, BN, kStats, false, NT>(acc, y, g.Cout, P, g.Cout, row0, col0, st, nullptr, 0, smem_raw);
+  if constexpr (kStats) stats_flush<BM, BN, NT>(st, stats + (int64_t)bm * g.Cout * 2, g.Cout, col0, smem_raw);
 }
 
 // stride-1 dgrad: dX (the GEMM's M = input pixels, N = Cin), A = dY gathered with flipped taps
-template <int BM, int BN, int PIPE>
-__global__ __launch_bounds__(kThreads, 2) void conv3x3_dgrad_kernel(const bf16_t* __restrict__ dy,
+template <int BM, int BN, int PIPE, int NT>
+__global__ __launch_bounds__(NT, NT == kThreads ? 2 : 1) void conv3x3_dgrad_kernel(const bf16_t* __restrict__ dy,
                                                                     const bf16_t* __restrict__ w,
                                                                     bf16_t* __restrict__ dx, ConvGeom g,
                                                                     const bf16_t* __restrict__ addend, BnBwdEpi bnb) {
@@ -193,14 +225,14 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_dgrad_kernel(const bf16_t
   const int64_t row0 = (int64_t)bm * BM;
   const int col0 = bn * BN;
   const int K = 9 * g.Cout;
-  const WeightTapKLoader<BN> lb{w, g.Cout, g.Cin, col0};
-  Im2colRowLoader<BM, true> la{dy, g.OH, g.OW, g.Cout, 1};
+  const WeightTapKLoader<BN, NT> lb{w, g.Cout, g.Cin, col0};
+  Im2colRowLoader<BM, true, NT> la{dy, g.OH, g.OW, g.Cout, 1};
   la.init(g, row0, P, g.H, g.W, g.fOW, g.fOH);  // stride 1: the same divisors (OW == W, OH == H)
-  ColStats<BM, BN> st;
-  Acc<BM, BN> acc;
+  ColStats<BM, BN, NT> st;
+  Acc<BM, BN, NT> acc;
   acc.zero();
   run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
-  epilogue_bf16<BM, BN, false, true>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, addend, g.Cin, smem_raw, &bnb, bm);
+  epilogue_bf16<BM, BN, false, true, NT>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, addend, g.Cin, smem_raw, &bnb, bm);
 }
 
 // wgrad partial slabs P[split][Cout][9*Cin]
@@ -241,23 +273,28 @@ static ConvGeom make_geom(int N, int H, int W, int Cin, int Cout, int stride) {
   return g;
 }
 
-template <int BM, int BN, bool S, int PIPE>
+template <int BM, int BN, bool S, int PIPE, int NT>
 static void launch_fwd_p(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGeom& g, float* stats,
                          hipStream_t stream) {
   const int64_t P = (int64_t)g.N * g.OH * g.OW;
   const int tiles = (int)((P + BM - 1) / BM) * ((g.Cout + BN - 1) / BN);
-  const size_t lds = std::max(run_mainloop_lds_bytes<PIPE, BM, BN, Im2colRowLoader<BM, false>, RowLoader<BN>>(),
-                              epilogue_lds_bytes<BM, BN, S>());
-  hipLaunchKernelGGL((conv3x3_fwd_kernel<BM, BN, S, PIPE>), dim3(tiles), dim3(kThreads), lds, stream, x, w, y, g,
+  const size_t lds =
+      std::max(run_mainloop_lds_bytes<PIPE, BM, BN, Im2colRowLoader<BM, false, NT>, RowLoader<BN, NT>>(),
+               epilogue_lds_bytes<BM, BN, S, NT>());
+  hipLaunchKernelGGL((conv3x3_fwd_kernel<BM, BN, S, PIPE, NT>), dim3(tiles), dim3(NT), lds, stream, x, w, y, g,
                      stats);
 }
 template <int BM, int BN, bool S>
 static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGeom& g, float* stats,
                        hipStream_t stream) {
-  switch (mfma_pipeline_for(9 * g.Cin)) {
-    case 0: launch_fwd_p<BM, BN, S, 0>(x, w, y, g, stats, stream); break;
-    case 3: launch_fwd_p<BM, BN, S, 3>(x, w, y, g, stats, stream); break;
-    default: launch_fwd_p<BM, BN, S, 2>(x, w, y, g, stats, stream); break;
+  if constexpr (BM == 256) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
+    launch_fwd_p<BM, BN, S, 3, 512>(x, w, y, g, stats, stream);
+  } else {
+    switch (mfma_pipeline_for(9 * g.Cin)) {
+      case 0: launch_fwd_p<BM, BN, S, 0, kThreads>(x, w, y, g, stats, stream); break;
+      case 3: launch_fwd_p<BM, BN, S, 3, kThreads>(x, w, y, g, stats, stream); break;
+      default: launch_fwd_p<BM, BN, S, 2, kThreads>(x, w, y, g, stats, stream); break;
+    }
   }
 }
 
@@ -276,6 +313,7 @@ void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int
   if (stats) launch_fwd<BM_, BN_, true>(xp, wp, yp, g, stats, stream);   \
   else launch_fwd<BM_, BN_, false>(xp, wp, yp, g, stats, stream);
   switch (pick_tile((int64_t)g.N * g.OH * g.OW, Cout, tile)) {
+    case kTile256x128: DLA_CF(256, 128) break;
     case kTile128x128: DLA_CF(128, 128) break;
     case kTile128x64: DLA_CF(128, 64) break;
     default: DLA_CF(64, 64) break;
@@ -283,23 +321,28 @@ void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int
 #undef DLA_CF
 }
 
-template <int BM, int BN, int PIPE>
+template <int BM, int BN, int PIPE, int NT>
 static void launch_dgrad_p(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const ConvGeom& g, const bf16_t* addend,
                            const BnBwdEpi& bnb, hipStream_t stream) {
   const int64_t P = (int64_t)g.N * g.H * g.W;
   const int tiles = (int)((P + BM - 1) / BM) * ((g.Cin + BN - 1) / BN);
-  const size_t lds = std::max(run_mainloop_lds_bytes<PIPE, BM, BN, Im2colRowLoader<BM, true>, WeightTapKLoader<BN>>(),
-                              epilogue_lds_bytes<BM, BN, false>());
-  hipLaunchKernelGGL((conv3x3_dgrad_kernel<BM, BN, PIPE>), dim3(tiles), dim3(kThreads), lds, stream, dy, w, dx, g,
+  const size_t lds =
+      std::max(run_mainloop_lds_bytes<PIPE, BM, BN, Im2colRowLoader<BM, true, NT>, WeightTapKLoader<BN, NT>>(),
+               epilogue_lds_bytes<BM, BN, false, NT>());
+  hipLaunchKernelGGL((conv3x3_dgrad_kernel<BM, BN, PIPE, NT>), dim3(tiles), dim3(NT), lds, stream, dy, w, dx, g,
                      addend, bnb);
 }
 template <int BM, int BN>
 static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const ConvGeom& g, const bf16_t* addend,
                          const BnBwdEpi& bnb, hipStream_t stream) {
-  switch (mfma_pipeline_for(9 * g.Cout)) {
-    case 0: launch_dgrad_p<BM, BN, 0>(dy, w, dx, g, addend, bnb, stream); break;
-    case 3: launch_dgrad_p<BM, BN, 3>(dy, w, dx, g, addend, bnb, stream); break;
-    default: launch_dgrad_p<BM, BN, 2>(dy, w, dx, g, addend, bnb, stream); break;
+  if constexpr (BM == 256) {
+    launch_dgrad_p<BM, BN, 3, 512>(dy, w, dx, g, addend, bnb, stream);
+  } else {
+    switch (mfma_pipeline_for(9 * g.Cout)) {
+      case 0: launch_dgrad_p<BM, BN, 0, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
+      case 3: launch_dgrad_p<BM, BN, 3, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
+      default: launch_dgrad_p<BM, BN, 2, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
+    }
   }
 }
 
@@ -318,6 +361,7 @@ void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H,
   const bf16_t* wp = (const bf16_t*)w;
   const bf16_t* ad = (const bf16_t*)addend;
   switch (pick_tile((int64_t)N * H * W, Cin, tile)) {
+    case kTile256x128: launch_dgrad<256, 128>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile128x128: launch_dgrad<128, 128>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile128x64: launch_dgrad<128, 64>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     default: launch_dgrad<64, 64>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;

@@ -30,8 +30,8 @@ using namespace mm;
 // C[M,N] = A[M,K] * B[N,K]^T   (A K-contiguous; B K-contiguous, or k-major [K][N] when kBT),
 // bf16 in/out, fp32 accumulate, optional fused addend and BN-statistics epilogue.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, bool kStats, bool kBT, int PIPE>
-__global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const bf16_t* __restrict__ A, int64_t lda,
+template <int BM, int BN, bool kStats, bool kBT, int PIPE, int NT>
+__global__ __launch_bounds__(NT, NT == kThreads ? 2 : 1) void gemm_nt_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               bf16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
                                                               float* __restrict__ stats, const bf16_t* __restrict__ D,
@@ -42,20 +42,20 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const bf16_t* __re
   const int bm = tile / nbn, bn = tile % nbn;
   const int64_t row0 = (int64_t)bm * BM;
   const int col0 = bn * BN;
-  ColStats<BM, BN> st;
+  ColStats<BM, BN, NT> st;
   st.zero();
-  Acc<BM, BN> acc;
+  Acc<BM, BN, NT> acc;
   acc.zero();
-  const RowLoader<BM> la{A, lda, row0, M, K};
+  const RowLoader<BM, NT> la{A, lda, row0, M, K};
   if constexpr (kBT) {
-    const KLoader<BN> lb{B, ldb, col0, N, K};
+    const KLoader<BN, NT> lb{B, ldb, col0, N, K};
     run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
   } else {
-    const RowLoader<BN> lb{B, ldb, (int64_t)col0, N, K};
+    const RowLoader<BN, NT> lb{B, ldb, (int64_t)col0, N, K};
     run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
   }
-  epilogue_bf16<BM, BN, kStats, !kStats>(acc, C, ldc, M, N, row0, col0, st, D, ldd, smem_raw, &bnb, bm);
-  if constexpr (kStats) stats_flush<BM, BN>(st, stats + (int64_t)bm * N * 2, N, col0, smem_raw);
+  epilogue_bf16<BM, BN, kStats, !kStats, NT>(acc, C, ldc, M, N, row0, col0, st, D, ldd, smem_raw, &bnb, bm);
+  if constexpr (kStats) stats_flush<BM, BN, NT>(st, stats + (int64_t)bm * N * 2, N, col0, smem_raw);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -130,15 +130,15 @@ void set_mfma_pipeline(int p) { g_pipe = (p == 0 || p == 2 || p == 3) ? p : -1; 
 int mfma_pipeline() { return g_pipe; }
 int mfma_pipeline_for(int K) { return g_pipe >= 0 ? g_pipe : (K >= 256 ? 2 : 0); }
 
-template <int BM, int BN, bool S, bool BT, int PIPE>
+template <int BM, int BN, bool S, bool BT, int PIPE, int NT>
 static void launch_nt_p(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
                         int N, int K, float* stats, const bf16_t* D, int64_t ldd, const BnBwdEpi& bnb,
                         hipStream_t stream) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  const size_t ab = BT ? run_mainloop_lds_bytes<PIPE, BM, BN, RowLoader<BM>, KLoader<BN>>()
-                       : run_mainloop_lds_bytes<PIPE, BM, BN, RowLoader<BM>, RowLoader<BN>>();
-  const size_t cs = epilogue_lds_bytes<BM, BN, S>();
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, S, BT, PIPE>), dim3(tiles), dim3(kThreads), std::max(ab, cs), stream, A,
+  const size_t ab = BT ? run_mainloop_lds_bytes<PIPE, BM, BN, RowLoader<BM, NT>, KLoader<BN, NT>>()
+                       : run_mainloop_lds_bytes<PIPE, BM, BN, RowLoader<BM, NT>, RowLoader<BN, NT>>();
+  const size_t cs = epilogue_lds_bytes<BM, BN, S, NT>();
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, S, BT, PIPE, NT>), dim3(tiles), dim3(NT), std::max(ab, cs), stream, A,
                      lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb);
 }
 
@@ -146,10 +146,14 @@ template <int BM, int BN, bool S, bool BT>
 static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
                       int N, int K, float* stats, const bf16_t* D, int64_t ldd, const BnBwdEpi& bnb,
                       hipStream_t stream) {
-  switch (mfma_pipeline_for(K)) {
-    case 0: launch_nt_p<BM, BN, S, BT, 0>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
-    case 3: launch_nt_p<BM, BN, S, BT, 3>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
-    default: launch_nt_p<BM, BN, S, BT, 2>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
+  if constexpr (BM == 256) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
+    launch_nt_p<BM, BN, S, BT, 3, 512>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
+  } else {
+    switch (mfma_pipeline_for(K)) {
+      case 0: launch_nt_p<BM, BN, S, BT, 0, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
+      case 3: launch_nt_p<BM, BN, S, BT, 3, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
+      default: launch_nt_p<BM, BN, S, BT, 2, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
+    }
   }
 }
 
@@ -197,6 +201,7 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
     if (b_kmajor) DLA_NT(BM_, BN_, false, true); else DLA_NT(BM_, BN_, false, false);  \
   }
   switch (pick_tile(M, N, tile)) {
+    case kTile256x128: DLA_NT_ST(256, 128) break;
     case kTile128x128: DLA_NT_ST(128, 128) break;
     case kTile128x64: DLA_NT_ST(128, 64) break;
     default: DLA_NT_ST(64, 64) break;
