@@ -1,4 +1,4 @@
-"""A/B of MFMA tile configurations (dla_kernels.h TileCfg) at the ResNet-50 bs256 shapes, in one
+"""A/B of MFMA tile configurations (operands rotated through 2 GiB of copies: HBM-cold, as in the model) (dla_kernels.h TileCfg) at the ResNet-50 bs256 shapes, in one
 process with interleaved rounds; also checks each variant's output against the default tile's.
 
   python scripts/bench_tiles.py [tiles, default "1,4"]
@@ -31,6 +31,28 @@ def timeit(fn, iters=20):
     return round(s.elapsed_time(e) / iters, 4)
 
 
+ROT_BYTES = 2 << 30  # rotate operand copies through 2 GiB so they are not Infinity-Cache (256 MB) hot
+
+
+def copies(t):
+    n = max(1, min(16, ROT_BYTES // max(1, t.numel() * t.element_size())))
+    return [t] + [t.clone() for _ in range(n - 1)]
+
+
+def timeit_rot(fn, ops, iters=20):
+    """fn(*operand tuple); ops = list of tuples cycled per call."""
+    for i in range(3):
+        fn(*ops[i % len(ops)])
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for i in range(iters):
+        fn(*ops[i % len(ops)])
+    e.record()
+    torch.cuda.synchronize()
+    return round(s.elapsed_time(e) / iters, 4)
+
+
 def rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
 
@@ -44,17 +66,18 @@ for (Cin, H, Cout, stride) in [(64, 56, 64, 1), (128, 56, 128, 2), (128, 28, 128
     dy = torch.randn(N, Cout, OH, OH, device=dev).to(torch.bfloat16).contiguous(memory_format=CL)
     flops = 2 * N * OH * OH * Cout * Cin * 9
     r = {"conv": f"{Cin}x{H}->{Cout}/s{stride}"}
+    xs, dys = copies(x), copies(dy)
     ref_y = C.conv3x3_fwd(x, w, stride, True, tiles[0])
     ref_dx = C.conv3x3_dgrad(dy, w, None, tiles[0]) if stride == 1 else None
     for t in tiles:
         y = C.conv3x3_fwd(x, w, stride, True, t)
-        r[f"fwd_t{t}"] = timeit(lambda: C.conv3x3_fwd(x, w, stride, True, t))
+        r[f"fwd_t{t}"] = timeit_rot(lambda xx: C.conv3x3_fwd(xx, w, stride, True, t), [(c,) for c in xs])
         r[f"fwd_t{t}_TF"] = round(flops / r[f"fwd_t{t}"] / 1e9)
         r[f"fwd_t{t}_err"] = round(rel(y[0], ref_y[0]), 5)
         r[f"stats_t{t}_err"] = round(rel(y[1].sum(0), ref_y[1].sum(0)), 5)
         if stride == 1:
             dx = C.conv3x3_dgrad(dy, w, None, t)
-            r[f"dgrad_t{t}"] = timeit(lambda: C.conv3x3_dgrad(dy, w, None, t))
+            r[f"dgrad_t{t}"] = timeit_rot(lambda d: C.conv3x3_dgrad(d, w, None, t), [(c,) for c in dys])
             r[f"dgrad_t{t}_err"] = round(rel(dx, ref_dx), 5)
     print(json.dumps(r), flush=True)
 
@@ -64,13 +87,14 @@ for M, Cin, Cout in [(802816, 64, 256), (802816, 256, 64), (200704, 512, 128), (
     W = (torch.randn(Cout, Cin, device=dev) * 0.05).to(torch.bfloat16)
     dY = torch.randn(M, Cout, device=dev).to(torch.bfloat16)
     r = {"gemm": f"{M}x{Cin}->{Cout}"}
+    Xs, dYs = copies(X), copies(dY)
     ref = C.gemm_nt(X, W, True, None, False, tiles[0])
     refd = C.gemm_nt(dY, W, False, None, True, tiles[0])[0]
     for t in tiles:
         o = C.gemm_nt(X, W, True, None, False, t)
-        r[f"fwd_t{t}"] = timeit(lambda: C.gemm_nt(X, W, True, None, False, t))
+        r[f"fwd_t{t}"] = timeit_rot(lambda xx: C.gemm_nt(xx, W, True, None, False, t), [(c,) for c in Xs])
         r[f"fwd_t{t}_err"] = round(rel(o[0], ref[0]), 5)
         od = C.gemm_nt(dY, W, False, None, True, t)[0]
-        r[f"dgrad_t{t}"] = timeit(lambda: C.gemm_nt(dY, W, False, None, True, t))
+        r[f"dgrad_t{t}"] = timeit_rot(lambda d: C.gemm_nt(d, W, False, None, True, t), [(c,) for c in dYs])
         r[f"dgrad_t{t}_err"] = round(rel(od, refd), 5)
     print(json.dumps(r), flush=True)

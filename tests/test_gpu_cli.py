@@ -1,0 +1,62 @@
+"""End-to-end reference CLI on one MI355X: ``main.py`` positional args,
+experiment suites, the native engine + kernels, and the reference result artefacts
+(times.csv / loss.txt / config.txt, Appendix A), plus checkpoint / resume."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(tmp_path, model, experiment, *extra, batch=16, batches=3):
+    from dist_util import free_port
+
+    env = dict(os.environ, PYTHONPATH=ROOT, MIOPEN_USER_DB_PATH=os.path.join(ROOT, "miopen_db"))
+    cmd = [sys.executable, "-m", "distributed_learning_amd.main", "1", "0", "1", "1", "127.0.0.1", "lo", model,
+           "/nonexistent", "1", "--experiment", experiment, "--random_input", "1", "--limit_batches", str(batches),
+           "--batch_size", str(batch), "--master_port", str(free_port()), "--results_root", str(tmp_path),
+           "--job_id", "g", *extra]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return tmp_path / f"{experiment}_1_g"
+
+
+def _check(folder, exp, batches=3):
+    assert (folder / f"{exp}_config.txt").read_text().startswith("Namespace(")
+    lines = (folder / f"{exp}_0_0_loss.txt").read_text().splitlines()
+    assert len(lines) == batches and lines[0].startswith("Worker 0:0 loss for batch 0: ")
+    vals = [float(ln.rsplit(": ", 1)[1]) for ln in lines]
+    assert all(v == v and abs(v) < 1e4 for v in vals), vals
+    head = (folder / f"{exp}_0_0_times.csv").read_text().splitlines()[0]
+    assert head.startswith("experiment_name, get_data, data2dev, zero_grad, forward, backprop, sync")
+    return vals
+
+
+def test_cli_experiment2_resnet50(cuda, tmp_path):
+    """1-step suite on the GPU: warm-up, DDP (RCCL), ring P+F and central through the native engine."""
+    folder = _run(tmp_path, "resnet50", "experiment2")
+    for exp in ["warmup", "ddp", "onestep_reduce", "onestep_central"]:
+        _check(folder, exp)
+
+
+def test_cli_experiment1_googlenet(cuda, tmp_path):
+    """2-step suite (node reducer) with the reference's own model: GoogLeNet with unused aux heads."""
+    folder = _run(tmp_path, "imagenet", "experiment1")
+    for exp in ["warmup", "ourdist", "seq_merge", "overlap", "central_node_reduce"]:
+        _check(folder, exp)
+
+
+def test_cli_single_checkpoint_resume(cuda, tmp_path):
+    ck = tmp_path / "ck.pt"
+    folder = _run(tmp_path, "resnet18", "experiment_single", "--checkpoint", str(ck))
+    _check(folder, "single")
+    assert ck.exists()
+    sub = tmp_path / "resume"
+    sub.mkdir()
+    folder2 = _run(sub, "resnet18", "experiment_single", "--resume", str(ck))
+    _check(folder2, "single")
