@@ -28,6 +28,32 @@ constexpr int kBNThreads = 256;
 // Row blocks of the two reduction passes (stats, backward reduce): 4 workgroups per CU stream at
 // full bandwidth, and <= 1024 partial rows keep the finalize's reduction at ~2 load round trips.
 constexpr int kRedBlocks = 1024;
+// Rows per thread per streaming-loop iteration (loads of a group issued back to back).
+constexpr int kUnroll = 4;
+
+// 8 consecutive channels as loaded (bf16: one 16-byte register quad; fp32: two), widened on use. The
+// streaming loops below load a whole group of rows into these before touching any of them, so the
+// group's loads are in flight together (hipcc does not hoist them across the per-row arithmetic).
+template <typename T> struct Raw8;
+template <> struct Raw8<bf16_t> {
+  ushort8_t v;
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const ushort8_t*>(p); }
+  __device__ __forceinline__ void get(float (&f)[8]) const {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = bf16_to_f32(v[j]);
+  }
+};
+template <> struct Raw8<float> {
+  float4_t a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = reinterpret_cast<const float4_t*>(p)[0];
+    b = reinterpret_cast<const float4_t*>(p)[1];
+  }
+  __device__ __forceinline__ void get(float (&f)[8]) const {
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  }
+};
+
 
 // Block geometry shared by the two reduction passes: the block covers CT = tpr*8 channels
 // (channel tile blockIdx.x) and rows [r0, r1) (row block blockIdx.y); rpi = 256/tpr rows are in
@@ -203,7 +229,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restric
     sc[j] = ws[2 * C + c0 + j];
     sh[j] = ws[3 * C + c0 + j];
   }
-  for (int64_t r = r0 + rg; r < r1; r += rpi) {
+  auto row = [&](int64_t r) {
     const int64_t off = r * C + c0;
     float a[8];
     Vec8<T>::load(x + off, a);
@@ -224,7 +250,39 @@ __global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restric
     // ReLU-after-residual: the backward cannot recompute the branch from x alone, so record it as
     // one bit per element (1/16 of the bf16 output's bytes) instead of re-reading y.
     if (kRes && kRelu && mask) mask[off >> 3] = (uint8_t)bits;
+  };
+  int64_t r = r0 + rg;
+  for (; r + (kUnroll - 1) * rpi < r1; r += kUnroll * rpi) {
+    Raw8<T> xr[kUnroll], rr[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int64_t off = (r + u * rpi) * C + c0;
+      xr[u].load(x + off);
+      if (kRes) rr[u].load(res + off);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep every load of the group ahead of its arithmetic
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int64_t off = (r + u * rpi) * C + c0;
+      float a[8], rv[8];
+      xr[u].get(a);
+      if (kRes) rr[u].get(rv);
+      uint32_t bits = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float o = fmaf(a[j], sc[j], sh[j]);
+        if (kRes) o += rv[j];
+        if (kRelu) {
+          bits |= (o > 0.f ? 1u : 0u) << j;
+          o = fmaxf(o, 0.f);
+        }
+        a[j] = o;
+      }
+      Vec8<T>::store(y + off, a);
+      if (kRes && kRelu && mask) mask[off >> 3] = (uint8_t)bits;
+    }
   }
+  for (; r < r1; r += rpi) row(r);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -262,13 +320,17 @@ __device__ __forceinline__ void apply_relu_mask(float (&g)[8], const float (&xv)
 // argmax positions — the full-resolution dy is never written.
 template <typename T>
 struct DirectDy {
+  static constexpr bool kRaw = true;  // plain loads: the grouped streaming loop applies
   const T* p;
+  __device__ __forceinline__ void raw(int64_t off, Raw8<T>& v) const { v.load(p + off); }
   __device__ __forceinline__ void load(int64_t off, int64_t /*r*/, int /*c0*/, int /*C*/, float (&g)[8]) const {
     Vec8<T>::load(p + off, g);
   }
 };
 
 struct PoolDy {
+  static constexpr bool kRaw = false;  // a gather per element: per-row loop
+  __device__ __forceinline__ void raw(int64_t, Raw8<bf16_t>&) const {}
   const bf16_t* dyp;   // pooled gradient [N, OH, OW, C]
   const uint8_t* pos;  // window position of each pooled max (forward)
   int H, W, OH, OW, k, s, pad;
@@ -318,7 +380,9 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(DY dy, const 
     sh[j] = ws[3 * C + c0 + j];
     s[j] = q[j] = 0.f;
   }
-  for (int64_t r = r0 + rg; r < r1; r += rpi) {
+  // kUnroll rows per thread per iteration with no bounds test inside the group, so all their loads
+  // are in flight together (the tail loop takes the < kUnroll leftover rows)
+  auto row = [&](int64_t r) {
     const int64_t off = r * C + c0;
     float g[8], xv[8];
     dy.load(off, r, c0, C, g);
@@ -329,7 +393,38 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(DY dy, const 
       s[j] += g[j];
       q[j] = fmaf(g[j], xv[j] - mean[j], q[j]);
     }
+  };
+  int64_t r = r0 + rg;
+  if constexpr (DY::kRaw && kMask != kMaskY) {
+    for (; r + (kUnroll - 1) * rpi < r1; r += kUnroll * rpi) {
+      Raw8<T> gr[kUnroll], xr[kUnroll];
+      uint32_t mb[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t off = (r + u * rpi) * C + c0;
+        dy.raw(off, gr[u]);
+        xr[u].load(x + off);
+        mb[u] = kMask == kMaskBits ? (uint32_t)mask[off >> 3] : 0xffu;
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep every load of the group ahead of its arithmetic
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        float g[8], xv[8];
+        gr[u].get(g);
+        xr[u].get(xv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          bool keep = true;
+          if constexpr (kMask == kMaskRecomp) keep = fmaf(xv[j], sc[j], sh[j]) > 0.f;
+          if constexpr (kMask == kMaskBits) keep = (mb[u] >> j) & 1u;
+          const float gj = keep ? g[j] : 0.f;
+          s[j] += gj;
+          q[j] = fmaf(gj, xv[j] - mean[j], q[j]);
+        }
+      }
+    }
   }
+  for (; r < r1; r += rpi) row(r);
   block_reduce_write(s, q, tpr, rpi, ct, C, part, c_base, red);
 }
 
@@ -375,7 +470,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(DY dy, const T
     m1[j] = ws[5 * C + c0 + j];
     k2[j] = ws[6 * C + c0 + j];
   }
-  for (int64_t r = r0 + rg; r < r1; r += rpi) {
+  auto row = [&](int64_t r) {
     const int64_t off = r * C + c0;
     float g[8], xv[8];
     dy.load(off, r, c0, C, g);
@@ -385,7 +480,41 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(DY dy, const T
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = k1[j] * (g[j] - m1[j] - (xv[j] - mean[j]) * k2[j]);
     Vec8<T>::store(dx + off, xv);
+  };
+  int64_t r = r0 + rg;
+  if constexpr (DY::kRaw && kMask != kMaskY) {
+    for (; r + (kUnroll - 1) * rpi < r1; r += kUnroll * rpi) {
+      Raw8<T> gr[kUnroll], xr[kUnroll];
+      uint32_t mb[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t off = (r + u * rpi) * C + c0;
+        dy.raw(off, gr[u]);
+        xr[u].load(x + off);
+        mb[u] = kMask == kMaskBits ? (uint32_t)mask[off >> 3] : 0xffu;
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep every load of the group ahead of its arithmetic
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t off = (r + u * rpi) * C + c0;
+        float g[8], xv[8];
+        gr[u].get(g);
+        xr[u].get(xv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          bool keep = true;
+          if constexpr (kMask == kMaskRecomp) keep = fmaf(xv[j], sc[j], sh[j]) > 0.f;
+          if constexpr (kMask == kMaskBits) keep = (mb[u] >> j) & 1u;
+          g[j] = keep ? g[j] : 0.f;
+        }
+        if (kDres) Vec8<T>::store(dres + off, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = k1[j] * (g[j] - m1[j] - (xv[j] - mean[j]) * k2[j]);
+        Vec8<T>::store(dx + off, xv);
+      }
+    }
   }
+  for (; r < r1; r += rpi) row(r);
 }
 
 // ---------------------------------------------------------------------------------------------

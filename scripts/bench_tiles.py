@@ -16,6 +16,8 @@ C = _ext.require()
 dev = torch.device("cuda:0")
 CL = torch.channels_last
 tiles = [int(t) for t in (sys.argv[1] if len(sys.argv) > 1 else "1,4").split(",")]
+if len(sys.argv) > 2:  # force the MFMA main-loop pipeline (0 / 2 / 3) for every variant
+    C.set_mfma_pipeline(int(sys.argv[2]))
 
 
 def timeit(fn, iters=20):
