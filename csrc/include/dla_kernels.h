@@ -173,6 +173,9 @@ void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int
 void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
                           const void* addend, hipStream_t stream, int tile = kTileAuto,
                           const BnBwdArgs* bn_bwd = nullptr);
+// stride-2 data gradient (H, W even): dx [N,H,W,Cin] from dy [N,H/2,W/2,Cout], parity-class GEMMs.
+void launch_conv3x3s2_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
+                            hipStream_t stream);
 int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int stride);
 void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int splits, void* dw, int out_dtype, int N,
                           int H, int W, int Cin, int Cout, int stride, hipStream_t stream);

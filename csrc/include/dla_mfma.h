@@ -432,11 +432,17 @@ struct BnBwdEpi {
   FastDiv fW, fH;
 };
 
-template <int BM, int BN, bool kStats, bool kEpi = false, int NT = kThreads>
+// Output row of GEMM row gm: the identity for every kernel except the stride-2 data gradient, whose
+// GEMM rows are one parity class of the input pixels.
+struct RowIdent {
+  __device__ __forceinline__ int64_t operator()(int64_t gm) const { return gm; }
+};
+
+template <int BM, int BN, bool kStats, bool kEpi = false, int NT = kThreads, class RM = RowIdent>
 __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t* __restrict__ C, int64_t ldc,
                                               int64_t M, int N, int64_t row0, int col0, ColStats<BM, BN, NT>& st,
                                               const bf16_t* __restrict__ D, int64_t ldd, char* smem,
-                                              const BnBwdEpi* epi = nullptr, int bm = 0) {
+                                              const BnBwdEpi* epi = nullptr, int bm = 0, RM rowmap = RM()) {
   // kEpi compiles in the BN-backward partials and the masked addend (dgrad kernels only: they cost
   // VGPRs that would lower the forward kernels' occupancy)
   const BnBwdEpi* bnb = (kEpi && epi && epi->x) ? epi : nullptr;
@@ -522,7 +528,7 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
           for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(e[j]));
         }
       }
-      *reinterpret_cast<ushort8_t*>(C + gm * ldc + gn) = v;
+      *reinterpret_cast<ushort8_t*>(C + rowmap(gm) * ldc + gn) = v;
       if (bnb) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {

@@ -137,6 +137,139 @@ struct WeightTapKLoader {
   }
 };
 
+// ---- stride-2 data gradient ----------------------------------------------------------------------
+// dX of a 3x3 / stride-2 / pad-1 conv with even H, W splits into the 4 parity classes (ph, pw) of the
+// input pixel (ih, iw) = (2a + ph, 2b + pw): only taps with ih + 1 - kh even reach it, at
+// oh = a + dh. Row taps: ph = 0 -> {kh 1, dh 0}; ph = 1 -> {kh 0, dh +1}, {kh 2, dh 0} (columns alike),
+// so class (ph, pw) is a dense implicit GEMM over the OH x OW class image with (1 + ph)(1 + pw) taps
+// (9 in total = exactly the forward's FLOPs, no zero-inserted work). Tap index t of the class:
+// th = t / (1 + pw), tw = t % (1 + pw).
+struct S2Class {
+  int ph, pw;
+  __device__ __forceinline__ int ntaps() const { return (1 + ph) * (1 + pw); }
+  __device__ __forceinline__ void tap(int t, int& kh, int& kw, int& dh, int& dw) const {
+    const int th = t / (1 + pw), tw = t - th * (1 + pw);
+    kh = ph == 0 ? 1 : (th == 0 ? 0 : 2);
+    dh = (ph == 1 && th == 0) ? 1 : 0;
+    kw = pw == 0 ? 1 : (tw == 0 ? 0 : 2);
+    dw = (pw == 1 && tw == 0) ? 1 : 0;
+  }
+};
+
+// A operand: row = class pixel (n, a, b), k = (tap t, output channel co), element dY[n][a+dh][b+dw][co].
+template <int W, int NT = kThreads>
+struct S2DgradRowLoader {
+  static constexpr bool kKMajor = false;
+  static constexpr int kNT = NT;
+  static constexpr int CH = TileGeom<W, NT>::CH;
+  const bf16_t* dy;
+  int OH, OW, C;  // dY image (the class image has the same size), C = Cout
+  S2Class cls;
+  int64_t pix[CH];  // n*OH*OW + a*OW + b of the slot's class pixel, -1 past the end
+  int ra[CH], rb[CH];
+  const bf16_t* sp[CH];
+  uint32_t smask[CH];
+  __device__ void init(int64_t row0, int64_t P, const FastDiv& fw, const FastDiv& fh) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + i * NT, r = c >> 3;
+      const int64_t p = row0 + r;
+      if (p < P) {
+        const uint32_t q = fdiv((uint32_t)p, fw);
+        rb[i] = (int)p - (int)q * OW;
+        const uint32_t n = fdiv(q, fh);
+        ra[i] = (int)q - (int)n * OH;
+        pix[i] = p;
+      } else {
+        pix[i] = -1;
+        ra[i] = rb[i] = 0;
+      }
+    }
+  }
+  __device__ bool tap_ok(int i, int t) const {
+    int kh, kw, dh, dw;
+    cls.tap(t, kh, kw, dh, dw);
+    return pix[i] >= 0 && ra[i] + dh < OH && rb[i] + dw < OW;
+  }
+  __device__ void prep() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int kc = rm_glds_kc(threadIdx.x + i * NT);
+      uint32_t m = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) m |= (t < cls.ntaps() && tap_ok(i, t)) ? (1u << t) : 0u;
+      smask[i] = m;
+      sp[i] = dy + (pix[i] < 0 ? 0 : pix[i]) * C + kc;
+    }
+  }
+  __device__ ushort8_t load(int i, int k0) const {
+    const int t = k0 / C;
+    if (t >= cls.ntaps() || !tap_ok(i, t)) return zero8();
+    int kh, kw, dh, dw;
+    cls.tap(t, kh, kw, dh, dw);
+    return *reinterpret_cast<const ushort8_t*>(dy + (pix[i] + dh * OW + dw) * C + (k0 - t * C) +
+                                               (threadIdx.x & 7) * 8);
+  }
+  __device__ const void* src(int i, int k0) const {
+    const int t = k0 / C;  // uniform
+    int kh, kw, dh, dw;
+    cls.tap(t, kh, kw, dh, dw);
+    const int64_t off = (int64_t)(dh * OW + dw) * C + (k0 - t * C);
+    return ((smask[i] >> t) & 1u) ? (const void*)(sp[i] + off) : zero_src();
+  }
+};
+
+// B operand: k = (tap t, co) rows, n = ci columns, element W[co][kh(t)][kw(t)][ci].
+template <int W, int NT = kThreads>
+struct S2WeightKLoader {
+  static constexpr bool kKMajor = true;
+  static constexpr int kNT = NT;
+  static constexpr int CH = TileGeom<W, NT>::CH;
+  const bf16_t* w;
+  int Cout, Cin, col0;
+  S2Class cls;
+  const bf16_t* sp[CH];
+  bool sok[CH];
+  __device__ ushort8_t load(int i, int k0) const {
+    const int c = threadIdx.x + i * NT, kr = c / TileGeom<W>::KPR, nc = (c % TileGeom<W>::KPR) * 8;
+    const int t = k0 / Cout;
+    int kh, kw, dh, dw;
+    cls.tap(t, kh, kw, dh, dw);
+    const int co = k0 - t * Cout + kr, ci = col0 + nc;
+    if (t >= cls.ntaps() || ci >= Cin) return zero8();
+    return *reinterpret_cast<const ushort8_t*>(w + ((int64_t)co * 9 + kh * 3 + kw) * Cin + ci);
+  }
+  __device__ void prep() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + i * NT, kr = c / TileGeom<W>::KPR;
+      const int ci = col0 + km_glds_col<W>(c);
+      sok[i] = ci < Cin;
+      sp[i] = w + (int64_t)kr * 9 * Cin + (sok[i] ? ci : 0);
+    }
+  }
+  __device__ const void* src(int i, int k0) const {
+    const int t = k0 / Cout;
+    int kh, kw, dh, dw;
+    cls.tap(t, kh, kw, dh, dw);
+    const int64_t off = ((int64_t)(k0 - t * Cout) * 9 + kh * 3 + kw) * Cin;
+    return sok[i] ? (const void*)(sp[i] + off) : zero_src();
+  }
+};
+
+// class row (n, a, b) -> dX row (n, 2a + ph, 2b + pw)
+struct S2RowMap {
+  int OH, OW, ph, pw;
+  FastDiv fw, fh;
+  __device__ __forceinline__ int64_t operator()(int64_t p) const {
+    const uint32_t q = fdiv((uint32_t)p, fw);
+    const int b = (int)p - (int)q * OW;
+    const uint32_t n = fdiv(q, fh);
+    const int a = (int)q - (int)n * OH;
+    return ((int64_t)n * (2 * OH) + 2 * a + ph) * (2 * OW) + 2 * b + pw;
+  }
+};
+
 // B operand of wgrad: k = output pixel rows, n = (tap, ci) columns, element X[src(p, tap)][ci].
 template <int W, bool kGlds, int NT = kThreads>
 struct Im2colKLoader {
@@ -233,6 +366,34 @@ __global__ __launch_bounds__(NT, NT == kThreads ? 2 : 1) void conv3x3_dgrad_kern
   acc.zero();
   run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
   epilogue_bf16<BM, BN, false, true, NT>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, addend, g.Cin, smem_raw, &bnb, bm);
+}
+
+// stride-2 dgrad: all 4 parity classes in one launch (heaviest class first: 4, 2, 2, 1 taps)
+template <int BM, int BN, int PIPE>
+__global__ __launch_bounds__(kThreads, 2) void conv3x3s2_dgrad_kernel(const bf16_t* __restrict__ dy,
+                                                                      const bf16_t* __restrict__ w,
+                                                                      bf16_t* __restrict__ dx, ConvGeom g) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int64_t P = (int64_t)g.N * g.OH * g.OW;  // class image = dY image
+  const int nbn = (g.Cin + BN - 1) / BN;
+  const int per_class = (int)((P + BM - 1) / BM) * nbn;
+  const int cls_slot = blockIdx.x / per_class;  // 0..3 -> class (1,1), (1,0), (0,1), (0,0)
+  const S2Class cls{cls_slot < 2 ? 1 : 0, (cls_slot & 1) == 0 ? 1 : 0};
+  const int tile = xcd_remap(blockIdx.x - cls_slot * per_class, per_class);
+  const int bm = tile / nbn, bn = tile % nbn;
+  const int64_t row0 = (int64_t)bm * BM;
+  const int col0 = bn * BN;
+  const int K = cls.ntaps() * g.Cout;
+  const S2WeightKLoader<BN> lb{w, g.Cout, g.Cin, col0, cls};
+  S2DgradRowLoader<BM> la{dy, g.OH, g.OW, g.Cout, cls};
+  la.init(row0, P, g.fOW, g.fOH);
+  ColStats<BM, BN> st;
+  Acc<BM, BN> acc;
+  acc.zero();
+  run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
+  const S2RowMap rm{g.OH, g.OW, cls.ph, cls.pw, g.fOW, g.fOH};
+  epilogue_bf16<BM, BN, false, false, kThreads, S2RowMap>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, nullptr, 0,
+                                                         smem_raw, nullptr, 0, rm);
 }
 
 // wgrad partial slabs P[split][Cout][9*Cin]
@@ -366,6 +527,27 @@ void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H,
     case kTile128x64: launch_dgrad<128, 64>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     default: launch_dgrad<64, 64>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
   }
+}
+
+void launch_conv3x3s2_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
+                            hipStream_t stream) {
+  const ConvGeom g = make_geom(N, H, W, Cin, Cout, 2);  // OH = H / 2, OW = W / 2 (H, W even)
+  const int64_t P = (int64_t)N * g.OH * g.OW;
+  const int bn = Cin <= 64 ? 64 : 128;
+  const int per_class = (int)((P + 127) / 128) * ((Cin + bn - 1) / bn);
+#define DLA_S2(BN_, P_)                                                                                          \
+  hipLaunchKernelGGL((conv3x3s2_dgrad_kernel<128, BN_, P_>), dim3(4 * per_class), dim3(kThreads),               \
+                     std::max(run_mainloop_lds_bytes<P_, 128, BN_, S2DgradRowLoader<128>, S2WeightKLoader<BN_>>(), \
+                              epilogue_lds_bytes<128, BN_, false>()),                                           \
+                     stream, (const bf16_t*)dy, (const bf16_t*)w, (bf16_t*)dx, g)
+  // the 1-tap class has K = Cout (one or two k-steps at ResNet shapes): one pipeline for all classes
+  const int pipe = mfma_pipeline_for(4 * Cout);
+  if (bn == 64) {
+    if (pipe == 0) DLA_S2(64, 0); else DLA_S2(64, 2);
+  } else {
+    if (pipe == 0) DLA_S2(128, 0); else DLA_S2(128, 2);
+  }
+#undef DLA_S2
 }
 
 int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int stride) {

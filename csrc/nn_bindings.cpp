@@ -383,6 +383,22 @@ at::Tensor conv3x3_dgrad(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> 
   return dx;
 }
 
+// stride-2 3x3 data gradient for an input of even size H x W
+at::Tensor conv3x3s2_dgrad(at::Tensor dy, at::Tensor w, int64_t H, int64_t W) {
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(1) == w.size(0), "conv3x3s2_dgrad: dy/w mismatch");
+  TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && dy.size(2) == H / 2 && dy.size(3) == W / 2,
+              "conv3x3s2_dgrad: needs even H, W and dy = [N, Cout, H/2, W/2]");
+  const int N = (int)dy.size(0), Cout = (int)w.size(0), Cin = (int)w.size(1);
+  at::Tensor dx = at::empty({N, Cin, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_conv3(dx, w);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0,
+              "conv3x3s2_dgrad: bf16 aligned dy");
+  launch_conv3x3s2_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, (int)H, (int)W, Cin, Cout,
+                         current_stream(dy));
+  return dx;
+}
+
 // stride-1 3x3 data gradient that is the dy of a fused BN: returns (dx, BN-backward partials)
 std::vector<at::Tensor> conv3x3_dgrad_bn(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> addend,
                                          at::Tensor x_bn, at::Tensor ws, c10::optional<at::Tensor> mask, int64_t mode) {
@@ -442,6 +458,8 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("w"), pybind11::arg("stride") = 1, pybind11::arg("stats") = false, pybind11::arg("tile") = 0);
   m.def("conv3x3_dgrad", &conv3x3_dgrad, "implicit-GEMM 3x3 conv data gradient (stride 1)", pybind11::arg("dy"),
         pybind11::arg("w"), pybind11::arg("addend") = pybind11::none(), pybind11::arg("tile") = 0);
+  m.def("conv3x3s2_dgrad", &conv3x3s2_dgrad, "implicit-GEMM 3x3 / stride-2 conv data gradient (parity classes)",
+        pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("H"), pybind11::arg("W"));
   m.def("conv3x3_wgrad", &conv3x3_wgrad, "implicit-GEMM 3x3 conv weight gradient (split-K)", pybind11::arg("dy"),
         pybind11::arg("x"), pybind11::arg("stride") = 1, pybind11::arg("out_dtype") = at::kFloat);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd, "stem BN(train)+ReLU+max-pool forward (pooled output only)",

@@ -225,8 +225,8 @@ def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False, stride: 
 # Per-pass engine choice from scripts/bench_conv.py at the ResNet-50 bs256 shapes on MI355X
 # (profiles/mfma_kernels_vs_libraries.md), with the 2-stage LDS-DMA main loop: the native forward
 # beats MIOpen on 5 of the 7 shapes (and its epilogue yields the BatchNorm statistics, saving a
-# pass over the output), the stride-1 data gradient and the weight gradient win everywhere. MIOpen
-# keeps the 3 stride-2 data gradients.
+# pass over the output), the stride-1 data gradient and the weight gradient win everywhere. The
+# stride-2 data gradient runs as 4 parity-class GEMMs (conv3x3s2_dgrad); MIOpen only for odd sizes.
 # ---------------------------------------------------------------------------------------------
 CONV3_POLICY = {"fwd": "native", "dgrad_native_max_cin": 1 << 30, "wgrad": "native"}
 
@@ -274,6 +274,8 @@ class _Conv3x3(torch.autograd.Function):
                     link.publish(dx, part)
                 else:
                     dx = C.conv3x3_dgrad(dy, w)
+            elif ctx.stride == 2 and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0:
+                dx = C.conv3x3s2_dgrad(dy, w, x.shape[2], x.shape[3])
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, [ctx.stride] * 2, [1, 1], [1, 1], False,
                                                          [0, 0], 1, [True, False, False])[0]

@@ -49,6 +49,8 @@ for (N, Cin, H, Cout, stride) in [(256, 64, 56, 64, 1), (256, 128, 56, 128, 2), 
     C.set_mfma_pipeline(-1)
     if stride == 1:
         r["dgrad_native"] = timeit(lambda: C.conv3x3_dgrad(dy, w))
+    else:
+        r["dgrad_native"] = timeit(lambda: C.conv3x3s2_dgrad(dy, w, H, H))
     r["dgrad_miopen"] = timeit(lambda: torch.ops.aten.convolution_backward(
         dy, x, w, None, [stride, stride], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]))
     r["wgrad_native"] = timeit(lambda: C.conv3x3_wgrad(dy, x, stride, torch.bfloat16))

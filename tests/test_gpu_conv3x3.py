@@ -48,6 +48,27 @@ def test_conv3x3_fwd_dgrad_wgrad(cuda, N, Cin, H, W, Cout, stride):
         assert _rel(dx, xr.grad) < 1e-2, _rel(dx, xr.grad)
         add = torch.randn_like(x)
         assert torch.equal(C.conv3x3_dgrad(dy, w, add), dx + add)
+    elif H % 2 == 0 and W % 2 == 0:
+        dx = C.conv3x3s2_dgrad(dy, w, H, W)
+        assert dx.shape == x.shape and dx.is_contiguous(memory_format=CL)
+        assert _rel(dx, xr.grad) < 1e-2, _rel(dx, xr.grad)
+
+
+@pytest.mark.parametrize("N,Cin,H,W,Cout", [(2, 64, 8, 6, 64), (1, 128, 14, 14, 64), (3, 64, 4, 10, 128)])
+def test_conv3x3s2_dgrad_every_tap(cuda, N, Cin, H, W, Cout):
+    """Stride-2 data gradient (parity classes): one-hot weights per tap, exact against fp32."""
+    C = _C()
+    x = torch.randn(N, Cin, H, W, device=cuda)
+    for tap in range(9):
+        w = torch.zeros(Cout, Cin, 3, 3, device=cuda)
+        w[torch.arange(Cout), (torch.arange(Cout) * 5) % Cin, tap // 3, tap % 3] = 1.0
+        xr = x.clone().requires_grad_(True)
+        yr = F.conv2d(xr, w, None, 2, 1)
+        dy = torch.randn(yr.shape, device=cuda).to(torch.bfloat16)
+        yr.backward(dy.float())
+        dx = C.conv3x3s2_dgrad(dy.contiguous(memory_format=CL), w.to(torch.bfloat16).contiguous(memory_format=CL),
+                               H, W)
+        torch.testing.assert_close(dx.float(), xr.grad, rtol=4e-3, atol=1e-6)  # bf16 rounding of 2-term sums
 
 
 def test_conv3x3_asymmetric_weights(cuda):
