@@ -64,6 +64,9 @@ def parse():
                     help="1x1 convolutions on the native MFMA GEMMs (with fused BN statistics) or MIOpen")
     ap.add_argument("--graph", default=os.environ.get("DLA_GRAPH", "off"), choices=["on", "off"],
                     help="capture the whole training step (data, fwd, bwd, collectives, optimizer) in a HIP graph")
+    ap.add_argument("--force_comm", type=int, default=0,
+                    help="1 = run the multi-rank gradient path (gather -> RCCL all-reduce -> re-point) even at "
+                         "one GPU (diagnostic: the per-GPU cost of the N>1 data path without the link time)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--momentum", type=float, default=0.5)
     return ap.parse_args()
@@ -92,6 +95,11 @@ def main():
         dnn.bf16_weights(model)
     reducer = make_reducer("immediate", a.algorithm, native=True)
     model = PipelinedFusedDP(model, reducer, int(a.bucket_mb * 1024 * 1024), dev)
+    if a.force_comm and world == 1:
+        from distributed_learning_amd.parallel.executor import NativeStreamExecutor
+
+        model.sync.executor = NativeStreamExecutor(reducer.engine, a.algorithm, passthrough=False)
+        model.sync.passthrough = False
     opt = FusedSGD(model.module.parameters(), lr=a.lr, momentum=a.momentum, master_weights=bf16)
     data = SyntheticBatches(a.batch, spec.input_shape, spec.num_classes, dev,
                             dtype=torch.bfloat16 if bf16 else torch.float32,
@@ -177,8 +185,10 @@ def main():
                 "conv1x1": a.conv,
                 "hip_graph": graphed,
                 "optimizer": f"fused SGD momentum={a.momentum} (fp32 master weights)",
+                "force_comm": bool(a.force_comm),
             },
             "allreduce_ms_per_step": round(comm_ms, 3),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
             "final_loss": round(final_loss, 4),
             "baseline_ref": {"value": ref, "what": "reference best published img/s at this N (GoogLeNet, P100, Gloo)"},
         }
