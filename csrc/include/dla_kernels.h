@@ -120,6 +120,9 @@ void launch_maxpool_fwd(const void* x, void* y, uint8_t* pos, int N, int H, int 
                         int s, int p, int dtype, hipStream_t stream);
 void launch_maxpool_bwd(const void* dy, const uint8_t* pos, void* dx, int N, int H, int W, int C, int OH, int OW,
                         int k, int s, int p, int dtype, hipStream_t stream);
+// global average pooling over the H*W pixels of NHWC x: y [N, C]; backward dx [N, H, W, C] = dy / HW
+void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, int dtype, hipStream_t stream);
+void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, int dtype, hipStream_t stream);
 
 // ---- bf16 MFMA GEMMs (gemm.hip) ---------------------------------------------------------------
 // C[M,N] = A[M,K] B[N,K]^T [+ addend[M,N]] (b_kmajor: B given as [K,N], i.e. C = A B); optional
@@ -132,11 +135,26 @@ void launch_maxpool_bwd(const void* dy, const uint8_t* pos, void* dx, int N, int
 void set_mfma_pipeline(int p);  // -1 = per-shape auto
 int mfma_pipeline();
 int mfma_pipeline_for(int K);
-// kTile256x128: 8 waves (512 threads), 3-stage LDS-DMA pipeline, one block per CU.
-enum TileCfg : int { kTileAuto = 0, kTile128x128 = 1, kTile128x64 = 2, kTile64x64 = 3, kTile256x128 = 4 };
+// kTile256x128: 8 waves (512 threads) of 64x64, 3-stage LDS-DMA pipeline, one block per CU.
+// kTile256x128w4 / kTile128x256w4: 4 waves of 128x64 / 64x128 (half the LDS fragment reads per
+// MFMA of the 64x64 wave tiles), 3-stage LDS-DMA pipeline (144 KB), one block per CU.
+enum TileCfg : int {
+  kTileAuto = 0,
+  kTile128x128 = 1,
+  kTile128x64 = 2,
+  kTile64x64 = 3,
+  kTile256x128 = 4,
+  kTile256x128w4 = 5,
+  kTile128x256w4 = 6
+};
 int pick_tile(int64_t M, int N, int tile);
-inline int tile_bm(int cfg) { return cfg == kTile64x64 ? 64 : (cfg == kTile256x128 ? 256 : 128); }
-inline int tile_bn(int cfg) { return (cfg == kTile128x128 || cfg == kTile256x128) ? 128 : 64; }
+inline int tile_bm(int cfg) {
+  return cfg == kTile64x64 ? 64 : ((cfg == kTile256x128 || cfg == kTile256x128w4) ? 256 : 128);
+}
+inline int tile_bn(int cfg) {
+  return cfg == kTile128x256w4 ? 256
+                               : ((cfg == kTile128x128 || cfg == kTile256x128 || cfg == kTile256x128w4) ? 128 : 64);
+}
 // rows of BN-statistics partials ([rows][N][2]) a stats-producing launch writes (one per row tile)
 int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto);
 // BatchNorm-backward reduction fused into a bf16-output GEMM epilogue (the output is the BN's dy):
@@ -176,6 +194,17 @@ void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H,
 // stride-2 data gradient (H, W even): dx [N,H,W,Cin] from dy [N,H/2,W/2,Cout], parity-class GEMMs.
 void launch_conv3x3s2_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
                             hipStream_t stream);
+// ---- 7x7 / stride-2 / pad-3 stem conv, Cin = 3 (stem.hip) ------------------------------------------
+// x [N,H,W,3] bf16 -> fold: xs [N,(H+1)/2,(W+1)/2,16] (space-to-depth, 4 zero channels);
+// wpk = packed weight [Cout][256] (k = (th * 4 + tw) * 16 + (ph * 2 + pw) * 3 + c, see stem.hip);
+// y [N,OH,OW,Cout] with optional BN-statistics partials stats[stem_stats_rows(P)][Cout][2].
+int stem_stats_rows(int64_t P);
+void launch_stem_fold(const void* x, void* xs, int N, int H, int W, hipStream_t stream);
+void launch_stem_fwd(const void* xs, const void* wpk, void* y, int N, int H, int W, int Cout, float* stats,
+                     hipStream_t stream);
+int stem_wgrad_splits(int N, int H, int W, int Cout);
+void launch_stem_wgrad(const void* dy, const void* xs, float* partial, int splits, void* dwpk, int out_dtype, int N,
+                       int H, int W, int Cout, hipStream_t stream);
 int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int stride);
 void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int splits, void* dw, int out_dtype, int N,
                           int H, int W, int Cin, int Cout, int stride, hipStream_t stream);

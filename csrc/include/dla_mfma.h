@@ -38,6 +38,13 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
 constexpr int kThreads = 256;
 constexpr int kBK = 64;
 
+// resident blocks per CU a kernel is compiled for: 2 for the 4-wave 128x128-or-smaller tiles
+// (64 KB of 2-stage LDS each), 1 for the 8-wave tiles and the 4-wave 256x128 / 128x256 tiles
+// (3-stage LDS-DMA at 144 KB)
+__host__ __device__ constexpr int blocks_per_cu(int BM, int BN, int NT) {
+  return (NT == kThreads && BM * BN <= 128 * 128) ? 2 : 1;
+}
+
 __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -51,8 +58,10 @@ __device__ __forceinline__ ushort8_t zero8() { return ushort8_t{0, 0, 0, 0, 0, 0
 // chunk group and every 16-byte store contiguous; stores and reads share this function.
 template <int W>
 __device__ __forceinline__ int tr_sw(int row) {  // XOR applied to the 8-byte chunk index of a row
-  static_assert(W == 64 || W == 128, "tr image width");
-  if constexpr (W == 128)
+  static_assert(W == 64 || W == 128 || W == 256, "tr image width");
+  // 256 columns (512 B rows): every row starts on bank 0 as with 128, so the same XOR pattern
+  // (it stays inside each 32-chunk half) keeps the transposed reads conflict-free
+  if constexpr (W >= 128)
     return 4 * ((row & 3) | (((row >> 3) & 1) << 2));  // 32 chunks/row (256 B = 64 banks)
   else
     return 4 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));  // 16 chunks/row; row parity adds 32 banks

@@ -320,7 +320,7 @@ struct Im2colKLoader {
 
 // ---------------------------------------------------------------------------------------------
 template <int BM, int BN, bool kStats, int PIPE, int NT>
-__global__ __launch_bounds__(NT, NT == kThreads ? 2 : 1) void conv3x3_fwd_kernel(const bf16_t* __restrict__ x,
+__global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void conv3x3_fwd_kernel(const bf16_t* __restrict__ x,
                                                                   const bf16_t* __restrict__ w,
                                                                   bf16_t* __restrict__ y, ConvGeom g,
                                                                   float* __restrict__ stats) {
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(NT, NT == kThreads ? 2 : 1) void conv3x3_fwd_kernel
 
 // stride-1 dgrad: dX (the GEMM's M = input pixels, N = Cin), A = dY gathered with flipped taps
 template <int BM, int BN, int PIPE, int NT>
-__global__ __launch_bounds__(NT, NT == kThreads ? 2 : 1) void conv3x3_dgrad_kernel(const bf16_t* __restrict__ dy,
+__global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void conv3x3_dgrad_kernel(const bf16_t* __restrict__ dy,
                                                                     const bf16_t* __restrict__ w,
                                                                     bf16_t* __restrict__ dx, ConvGeom g,
                                                                     const bf16_t* __restrict__ addend, BnBwdEpi bnb) {
@@ -445,11 +445,14 @@ static void launch_fwd_p(const bf16_t* x, const bf16_t* w, bf16_t* y, const Conv
   hipLaunchKernelGGL((conv3x3_fwd_kernel<BM, BN, S, PIPE, NT>), dim3(tiles), dim3(NT), lds, stream, x, w, y, g,
                      stats);
 }
-template <int BM, int BN, bool S>
+template <int BM, int BN, bool S, int NTW = kThreads>
 static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGeom& g, float* stats,
                        hipStream_t stream) {
-  if constexpr (BM == 256) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
+  if constexpr (NTW == 512) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
     launch_fwd_p<BM, BN, S, 3, 512>(x, w, y, g, stats, stream);
+  } else if constexpr (BM * BN > 128 * 128) {  // 4 large waves, one block per CU
+    if (mfma_pipeline() == 2) launch_fwd_p<BM, BN, S, 2, kThreads>(x, w, y, g, stats, stream);
+    else launch_fwd_p<BM, BN, S, 3, kThreads>(x, w, y, g, stats, stream);
   } else {
     switch (mfma_pipeline_for(9 * g.Cin)) {
       case 0: launch_fwd_p<BM, BN, S, 0, kThreads>(x, w, y, g, stats, stream); break;
@@ -470,16 +473,20 @@ void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int
   const bf16_t* xp = (const bf16_t*)x;
   const bf16_t* wp = (const bf16_t*)w;
   bf16_t* yp = (bf16_t*)y;
-#define DLA_CF(BM_, BN_)                                                  \
-  if (stats) launch_fwd<BM_, BN_, true>(xp, wp, yp, g, stats, stream);   \
-  else launch_fwd<BM_, BN_, false>(xp, wp, yp, g, stats, stream);
+#define DLA_CFW(BM_, BN_, NT_)                                                  \
+  if (stats) launch_fwd<BM_, BN_, true, NT_>(xp, wp, yp, g, stats, stream);   \
+  else launch_fwd<BM_, BN_, false, NT_>(xp, wp, yp, g, stats, stream);
+#define DLA_CF(BM_, BN_) DLA_CFW(BM_, BN_, kThreads)
   switch (pick_tile((int64_t)g.N * g.OH * g.OW, Cout, tile)) {
-    case kTile256x128: DLA_CF(256, 128) break;
+    case kTile256x128: DLA_CFW(256, 128, 512) break;
+    case kTile256x128w4: DLA_CF(256, 128) break;
+    case kTile128x256w4: DLA_CF(128, 256) break;
     case kTile128x128: DLA_CF(128, 128) break;
     case kTile128x64: DLA_CF(128, 64) break;
     default: DLA_CF(64, 64) break;
   }
 #undef DLA_CF
+#undef DLA_CFW
 }
 
 template <int BM, int BN, int PIPE, int NT>
@@ -493,11 +500,14 @@ static void launch_dgrad_p(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const 
   hipLaunchKernelGGL((conv3x3_dgrad_kernel<BM, BN, PIPE, NT>), dim3(tiles), dim3(NT), lds, stream, dy, w, dx, g,
                      addend, bnb);
 }
-template <int BM, int BN>
+template <int BM, int BN, int NTW = kThreads>
 static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const ConvGeom& g, const bf16_t* addend,
                          const BnBwdEpi& bnb, hipStream_t stream) {
-  if constexpr (BM == 256) {
+  if constexpr (NTW == 512) {
     launch_dgrad_p<BM, BN, 3, 512>(dy, w, dx, g, addend, bnb, stream);
+  } else if constexpr (BM * BN > 128 * 128) {
+    if (mfma_pipeline() == 2) launch_dgrad_p<BM, BN, 2, kThreads>(dy, w, dx, g, addend, bnb, stream);
+    else launch_dgrad_p<BM, BN, 3, kThreads>(dy, w, dx, g, addend, bnb, stream);
   } else {
     switch (mfma_pipeline_for(9 * g.Cout)) {
       case 0: launch_dgrad_p<BM, BN, 0, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
@@ -522,7 +532,9 @@ void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H,
   const bf16_t* wp = (const bf16_t*)w;
   const bf16_t* ad = (const bf16_t*)addend;
   switch (pick_tile((int64_t)N * H * W, Cin, tile)) {
-    case kTile256x128: launch_dgrad<256, 128>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
+    case kTile256x128: launch_dgrad<256, 128, 512>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
+    case kTile256x128w4: launch_dgrad<256, 128>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
+    case kTile128x256w4: launch_dgrad<128, 256>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile128x128: launch_dgrad<128, 128>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile128x64: launch_dgrad<128, 64>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     default: launch_dgrad<64, 64>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;

@@ -31,7 +31,7 @@ using namespace mm;
 // bf16 in/out, fp32 accumulate, optional fused addend and BN-statistics epilogue.
 // ---------------------------------------------------------------------------------------------
 template <int BM, int BN, bool kStats, bool kBT, int PIPE, int NT>
-__global__ __launch_bounds__(NT, NT == kThreads ? 2 : 1) void gemm_nt_kernel(const bf16_t* __restrict__ A, int64_t lda,
+__global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void gemm_nt_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               bf16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
                                                               float* __restrict__ stats, const bf16_t* __restrict__ D,
@@ -142,12 +142,15 @@ static void launch_nt_p(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t l
                      lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb);
 }
 
-template <int BM, int BN, bool S, bool BT>
+template <int BM, int BN, bool S, bool BT, int NTW = kThreads>
 static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
                       int N, int K, float* stats, const bf16_t* D, int64_t ldd, const BnBwdEpi& bnb,
                       hipStream_t stream) {
-  if constexpr (BM == 256) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
+  if constexpr (NTW == 512) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
     launch_nt_p<BM, BN, S, BT, 3, 512>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
+  } else if constexpr (BM * BN > 128 * 128) {  // 4 large waves, one block per CU: 2 or 3 stages
+    if (mfma_pipeline() == 2) launch_nt_p<BM, BN, S, BT, 2, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
+    else launch_nt_p<BM, BN, S, BT, 3, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
   } else {
     switch (mfma_pipeline_for(K)) {
       case 0: launch_nt_p<BM, BN, S, BT, 0, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
@@ -192,21 +195,25 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
   const bf16_t* b = (const bf16_t*)B;
   bf16_t* c = (bf16_t*)C;
   const bf16_t* d = (const bf16_t*)addend;
-#define DLA_NT(BM_, BN_, S_, BT_) \
-  launch_nt<BM_, BN_, S_, BT_>(a, lda, b, ldb, c, ldc, M, N, K, stats, d, ld_addend, bnb, stream)
-#define DLA_NT_ST(BM_, BN_)                                \
-  if (stats) {                                             \
-    if (b_kmajor) DLA_NT(BM_, BN_, true, true); else DLA_NT(BM_, BN_, true, false);    \
-  } else {                                                 \
-    if (b_kmajor) DLA_NT(BM_, BN_, false, true); else DLA_NT(BM_, BN_, false, false);  \
+#define DLA_NT(BM_, BN_, S_, BT_, NT_) \
+  launch_nt<BM_, BN_, S_, BT_, NT_>(a, lda, b, ldb, c, ldc, M, N, K, stats, d, ld_addend, bnb, stream)
+#define DLA_NT_STW(BM_, BN_, NT_)                                                              \
+  if (stats) {                                                                                 \
+    if (b_kmajor) DLA_NT(BM_, BN_, true, true, NT_); else DLA_NT(BM_, BN_, true, false, NT_);    \
+  } else {                                                                                     \
+    if (b_kmajor) DLA_NT(BM_, BN_, false, true, NT_); else DLA_NT(BM_, BN_, false, false, NT_);  \
   }
+#define DLA_NT_ST(BM_, BN_) DLA_NT_STW(BM_, BN_, kThreads)
   switch (pick_tile(M, N, tile)) {
-    case kTile256x128: DLA_NT_ST(256, 128) break;
+    case kTile256x128: DLA_NT_STW(256, 128, 512) break;
+    case kTile256x128w4: DLA_NT_ST(256, 128) break;
+    case kTile128x256w4: DLA_NT_ST(128, 256) break;
     case kTile128x128: DLA_NT_ST(128, 128) break;
     case kTile128x64: DLA_NT_ST(128, 64) break;
     default: DLA_NT_ST(64, 64) break;
   }
 #undef DLA_NT_ST
+#undef DLA_NT_STW
 #undef DLA_NT
 }
 

@@ -143,4 +143,76 @@ void launch_maxpool_bwd(const void* dy, const uint8_t* pos, void* dx, int N, int
                        (float*)dx, g);
 }
 
+// ---- global average pooling (the ResNet / GoogLeNet head) ------------------------------------------
+// Forward: y[n, c] = mean over the HW pixels of x[n, :, c]. A block owns one image and 512 channels:
+// lane = 8 channels (one 16-byte load per pixel, a wave reads 1 KB contiguous), the 4 waves split the
+// pixels and combine through LDS in a fixed order (deterministic).
+// Backward: dx[n, p, c] = dy[n, c] / HW written straight into the channels_last layout the last
+// block's BN backward reads (torch's expand + copy made it a strided, non-vectorised pass).
+template <typename T>
+__global__ __launch_bounds__(kPoolThreads) void gap_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int HW,
+                                                               int C, float inv) {
+  __shared__ float part[4][64][8];
+  const int n = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    const T* base = x + (int64_t)n * HW * C + c;
+    for (int p = wv; p < HW; p += 4) {
+      float v[8];
+      Vec8<T>::load(base + (int64_t)p * C, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[wv][lane][j] = acc[j];
+  __syncthreads();
+  if (wv == 0 && c < C) {
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = ((part[0][lane][j] + part[1][lane][j]) + (part[2][lane][j] + part[3][lane][j])) * inv;
+    Vec8<T>::store(y + (int64_t)n * C + c, o);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kPoolThreads) void gap_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int HW,
+                                                               int C, float inv, int64_t total) {
+  const int cg = C / 8;
+  for (int64_t t = (int64_t)blockIdx.x * kPoolThreads + threadIdx.x; t < total; t += (int64_t)gridDim.x * kPoolThreads) {
+    const int c = (int)(t % cg) * 8;
+    const int64_t n = t / cg / HW;
+    float v[8];
+    Vec8<T>::load(dy + n * C + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= inv;
+    Vec8<T>::store(dx + t * 8, v);
+  }
+}
+
+void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, int dtype, hipStream_t stream) {
+  const dim3 grid((C / 8 + 63) / 64, N);
+  const float inv = 1.f / (float)HW;
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(gap_fwd_kernel<bf16_t>, grid, dim3(kPoolThreads), 0, stream, (const bf16_t*)x, (bf16_t*)y, HW,
+                       C, inv);
+  else
+    hipLaunchKernelGGL(gap_fwd_kernel<float>, grid, dim3(kPoolThreads), 0, stream, (const float*)x, (float*)y, HW, C,
+                       inv);
+}
+
+void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, int dtype, hipStream_t stream) {
+  const int64_t total = (int64_t)N * HW * (C / 8);
+  const int nb = pool_blocks(total);
+  if (nb == 0) return;
+  const float inv = 1.f / (float)HW;
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(gap_bwd_kernel<bf16_t>, dim3(nb), dim3(kPoolThreads), 0, stream, (const bf16_t*)dy, (bf16_t*)dx,
+                       HW, C, inv, total);
+  else
+    hipLaunchKernelGGL(gap_bwd_kernel<float>, dim3(nb), dim3(kPoolThreads), 0, stream, (const float*)dy, (float*)dx, HW,
+                       C, inv, total);
+}
+
 }  // namespace dla

@@ -176,7 +176,7 @@ static const void* addend2_ptr(const c10::optional<at::Tensor>& a2, int64_t M, i
 std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::optional<at::Tensor> addend,
                                 bool b_kmajor, int64_t tile, c10::optional<at::Tensor> addend_mask,
                                 c10::optional<at::Tensor> addend2, int64_t H, int64_t W) {
-  TORCH_CHECK(tile >= 0 && tile <= 4, "gemm_nt: tile config 0..4");
+  TORCH_CHECK(tile >= 0 && tile <= kTile128x256w4, "gemm_nt: tile config 0..6");
   check_mat(A, "A");
   check_mat(B, "B");
   TORCH_CHECK(A.size(1) == B.size(b_kmajor ? 0 : 1), "gemm_nt: K mismatch");
@@ -244,7 +244,7 @@ static int pool_out(int in, int k, int s, int p, bool ceil_mode);
 std::vector<at::Tensor> bn_relu_maxpool_fwd(at::Tensor x, c10::optional<at::Tensor> weight,
                                             c10::optional<at::Tensor> bias, c10::optional<at::Tensor> running_mean,
                                             c10::optional<at::Tensor> running_var, double momentum, double eps,
-                                            int64_t k, int64_t s, int64_t p) {
+                                            int64_t k, int64_t s, int64_t p, c10::optional<at::Tensor> stats) {
   check_act(x, "x");
   TORCH_CHECK(x.dim() == 4 && x.scalar_type() == at::kBFloat16, "bn_relu_maxpool: bf16 4-D input");
   TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && p >= 0 && 2 * p <= k, "bn_relu_maxpool: unsupported window");
@@ -259,10 +259,16 @@ std::vector<at::Tensor> bn_relu_maxpool_fwd(at::Tensor x, c10::optional<at::Tens
     return t->data_ptr<float>();
   };
   at::Tensor ws = at::empty({7 * (int64_t)C}, f32);
-  at::Tensor part = at::empty({partial_floats(M, C)}, f32);
+  const bool ext = stats.has_value() && stats->defined();
+  if (ext) {
+    TORCH_CHECK(stats->scalar_type() == at::kFloat && stats->is_contiguous() && stats->dim() == 3 &&
+                    stats->size(1) == C && stats->size(2) == 2,
+                "stats must be fp32 [row_blocks, C, 2] partials");
+  }
+  at::Tensor part = at::empty({ext ? 1 : partial_floats(M, C)}, f32);
   launch_bn_fwd(x.data_ptr(), nullptr, nullptr, M, C, kBF16, fptr(weight), fptr(bias), (float)eps, (float)momentum,
                 fptr(running_mean), fptr(running_var), ws.data_ptr<float>(), part.data_ptr<float>(), true, true,
-                current_stream(x));
+                current_stream(x), ext ? stats->data_ptr<float>() : nullptr, ext ? (int)stats->size(0) : 0);
   auto opts = x.options().memory_format(at::MemoryFormat::ChannelsLast);
   at::Tensor y = at::empty({N, C, OH, OW}, opts);
   at::Tensor pos = at::empty({N, C, OH, OW}, opts.dtype(at::kByte));
@@ -331,6 +337,70 @@ at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor pos, int64_t H, int64_t W, int6
   return dx;
 }
 
+// ResNet stem conv (7x7/s2/p3, 3 input channels). Returns (y, stats-or-undefined, xs) with xs the
+// space-to-depth folded input the weight gradient reads.
+std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor wpk, bool want_stats) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.size(1) == 3 && x.scalar_type() == at::kBFloat16 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_fwd: x must be a bf16 channels_last [N, 3, H, W] GPU tensor");
+  TORCH_CHECK(wpk.is_cuda() && wpk.dim() == 2 && wpk.size(1) == 256 && wpk.size(0) % 8 == 0 &&
+                  wpk.scalar_type() == at::kBFloat16 && wpk.is_contiguous() &&
+                  (reinterpret_cast<uintptr_t>(wpk.data_ptr()) & 15) == 0,
+              "stem_fwd: wpk must be the packed bf16 [Cout, 256] weight");
+  const int N = (int)x.size(0), H = (int)x.size(2), W = (int)x.size(3), Cout = (int)wpk.size(0);
+  const int OH = (H + 1) / 2, OW = (W + 1) / 2;  // 7x7 / s2 / p3
+  const int64_t P = (int64_t)N * OH * OW;
+  TORCH_CHECK((int64_t)N * H * W < (1 << 24) && P < (1 << 24), "stem_fwd: too many pixels for 24-bit index math");
+  at::Tensor xs = at::empty({N, OH, OW, 16}, x.options().memory_format(at::MemoryFormat::Contiguous));
+  launch_stem_fold(x.data_ptr(), xs.data_ptr(), N, H, W, current_stream(x));
+  at::Tensor y = at::empty({N, Cout, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor stats;
+  if (want_stats) stats = at::empty({stem_stats_rows(P), Cout, 2}, x.options().dtype(at::kFloat));
+  launch_stem_fwd(xs.data_ptr(), wpk.data_ptr(), y.data_ptr(), N, H, W, Cout,
+                  want_stats ? stats.data_ptr<float>() : nullptr, current_stream(x));
+  return {y, stats, xs};
+}
+
+at::Tensor stem_wgrad(at::Tensor dy, at::Tensor xs, int64_t H, int64_t W, c10::ScalarType out_dtype) {
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(xs.is_cuda() && xs.dim() == 4 && xs.size(3) == 16 && xs.scalar_type() == at::kBFloat16 &&
+                  xs.is_contiguous(),
+              "stem_wgrad: xs must be the forward's folded [N, OH, OW, 16] input");
+  check_act(dy, "dy");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.size(1) % 64 == 0, "stem_wgrad: dy must be bf16, Cout % 64");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "stem_wgrad: fp32/bf16 output");
+  const int N = (int)xs.size(0), Cout = (int)dy.size(1);
+  TORCH_CHECK(xs.size(1) == (H + 1) / 2 && xs.size(2) == (W + 1) / 2, "stem_wgrad: xs / image size mismatch");
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == xs.size(1) && dy.size(3) == xs.size(2), "stem_wgrad: dy shape");
+  const int splits = stem_wgrad_splits(N, (int)H, (int)W, Cout);
+  at::Tensor part = at::empty({(int64_t)splits * Cout * 256}, xs.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({Cout, 256}, xs.options().dtype(out_dtype));
+  launch_stem_wgrad(dy.data_ptr(), xs.data_ptr(), part.data_ptr<float>(), splits, dw.data_ptr(),
+                    out_dtype == at::kFloat ? kF32 : kBF16, N, (int)H, (int)W, Cout, current_stream(xs));
+  return dw;
+}
+
+// Global average pooling: x [N, C, H, W] channels_last -> y [N, C] (the flattened head input).
+at::Tensor gap_fwd(at::Tensor x) {
+  check_act(x, "x");
+  TORCH_CHECK(x.dim() == 4, "global_avg_pool: 4-D input");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "global_avg_pool: bf16 or fp32");
+  const int N = (int)x.size(0), C = (int)x.size(1), HW = (int)(x.size(2) * x.size(3));
+  at::Tensor y = at::empty({N, C}, x.options().memory_format(at::MemoryFormat::Contiguous));
+  if (N > 0 && HW > 0) launch_gap_fwd(x.data_ptr(), y.data_ptr(), N, HW, C, dtype_code(x), current_stream(x));
+  return y;
+}
+
+at::Tensor gap_bwd(at::Tensor dy, int64_t H, int64_t W) {
+  dy = dy.contiguous();
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 2 && dy.size(1) % 8 == 0, "global_avg_pool_bwd: dy [N, C], C % 8 == 0");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kFloat, "global_avg_pool_bwd: bf16 or fp32");
+  const int N = (int)dy.size(0), C = (int)dy.size(1);
+  at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_gap_bwd(dy.data_ptr(), dx.data_ptr(), N, (int)(H * W), C, dtype_code(dy), current_stream(dy));
+  return dx;
+}
+
 static void check_conv3(const at::Tensor& x, const at::Tensor& w) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -347,7 +417,7 @@ static void check_conv3(const at::Tensor& x, const at::Tensor& w) {
 
 // 3x3 / pad 1 convolution forward (stride 1 or 2). Returns (y, stats-or-undefined).
 std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, bool stats, int64_t tile) {
-  TORCH_CHECK(tile >= 0 && tile <= 4, "conv3x3: tile config 0..4");
+  TORCH_CHECK(tile >= 0 && tile <= kTile128x256w4, "conv3x3: tile config 0..6");
   check_conv3(x, w);
   TORCH_CHECK(stride == 1 || stride == 2, "conv3x3: stride 1 or 2");
   const int N = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Cout = (int)w.size(0);
@@ -363,7 +433,7 @@ std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, 
 
 // stride-1 data gradient (+ optional fused addend, same shape as dx)
 at::Tensor conv3x3_dgrad(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> addend, int64_t tile) {
-  TORCH_CHECK(tile >= 0 && tile <= 4, "conv3x3: tile config 0..4");
+  TORCH_CHECK(tile >= 0 && tile <= kTile128x256w4, "conv3x3: tile config 0..6");
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(dy.dim() == 4 && dy.size(1) == w.size(0), "conv3x3_dgrad: dy/w mismatch");
   const int N = (int)dy.size(0), Cout = (int)w.size(0), Cin = (int)w.size(1), H = (int)dy.size(2), W = (int)dy.size(3);
@@ -465,12 +535,16 @@ void bind_nn(pybind11::module& m) {
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd, "stem BN(train)+ReLU+max-pool forward (pooled output only)",
         pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"),
         pybind11::arg("running_var"), pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("k"),
-        pybind11::arg("s"), pybind11::arg("p"));
+        pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("stats") = pybind11::none());
   m.def("bn_relu_maxpool_bwd", &bn_relu_maxpool_bwd, "stem BN+ReLU+max-pool backward (dy gathered from the pool)");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC max pooling forward (+ argmax window positions)", pybind11::arg("x"),
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("ceil_mode") = false,
         pybind11::arg("need_pos") = true);
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pooling backward (gather form)");
+  m.def("gap_fwd", &gap_fwd, "NHWC global average pooling -> [N, C]");
+  m.def("stem_fwd", &stem_fwd, "7x7/s2/p3 stem conv, 3 input channels (space-to-depth + MFMA implicit GEMM, BN-statistics epilogue)");
+  m.def("stem_wgrad", &stem_wgrad, "7x7/s2/p3 stem conv weight gradient from the folded input (packed [Cout, 256] layout)");
+  m.def("gap_bwd", &gap_bwd, "NHWC global average pooling backward (channels_last dx)");
   m.def("gemm_nt", &gemm_nt, "C = A @ B^T (bf16 MFMA), optional fused column statistics", pybind11::arg("A"),
         pybind11::arg("B"), pybind11::arg("stats") = false, pybind11::arg("addend") = pybind11::none(),
         pybind11::arg("b_kmajor") = false, pybind11::arg("tile") = 0,

@@ -23,7 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import nn as dnn
-from ..ops.pool import MaxPool2d
+from ..ops.pool import MaxPool2d, global_avg_pool
 
 
 class BasicConv2d(nn.Module):
@@ -114,8 +114,7 @@ class GoogLeNet(nn.Module):
         x = self.maxpool4(x)
         x = self.inception5a(x)
         x = self.inception5b(x)
-        x = self.avgpool(x)
-        x = torch.flatten(x, 1)
+        x = global_avg_pool(x) if isinstance(self.avgpool, nn.AdaptiveAvgPool2d) else torch.flatten(self.avgpool(x), 1)
         x = self.dropout(x)
         x = self.fc(x)
         # Reference semantics: only output[0] (main logits) enters the loss (network.py:41).

@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import nn as dnn
-from ..ops.pool import MaxPool2d
+from ..ops.pool import MaxPool2d, global_avg_pool
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -142,8 +142,7 @@ class ResNet(nn.Module):
         x = self.layer2(x)
         x = self.layer3(x)
         x = self.layer4(x)
-        x = self.avgpool(x)
-        x = torch.flatten(x, 1)
+        x = global_avg_pool(x) if isinstance(self.avgpool, nn.AdaptiveAvgPool2d) else torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 
 

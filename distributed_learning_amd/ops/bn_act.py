@@ -167,9 +167,10 @@ class _BNReluPool(torch.autograd.Function):
     activation and its gradient are never materialised."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p, stats=None):
         C = _ext.require()
-        y, ws, pos = C.bn_relu_maxpool_fwd(x, weight, bias, running_mean, running_var, momentum, eps, k, s, p)
+        y, ws, pos = C.bn_relu_maxpool_fwd(x, weight, bias, running_mean, running_var, momentum, eps, k, s, p,
+                                           stats)
         ctx.save_for_backward(x, ws, weight, pos)
         ctx.geom = (k, s, p)
         return y
@@ -180,13 +181,14 @@ class _BNReluPool(torch.autograd.Function):
         k, s, p = ctx.geom
         dx, dg, db = _ext.require().bn_relu_maxpool_bwd(dy, pos, x, ws, weight, k, s, p)
         need = ctx.needs_input_grad
-        return dx, dg if need[1] else None, db if need[2] else None, None, None, None, None, None, None, None
+        return dx, dg if need[1] else None, db if need[2] else None, None, None, None, None, None, None, None, None
 
 
-def fused_bn_relu_maxpool(x: torch.Tensor, bn: nn.BatchNorm2d, pool: nn.MaxPool2d):
+def fused_bn_relu_maxpool(x: torch.Tensor, bn: nn.BatchNorm2d, pool: nn.MaxPool2d, stats=None):
     """``pool(relu(bn(x)))`` with the fused kernels when they apply (training-mode BN with running
     stats or none, bf16 channels_last, square window, no dilation/ceil/indices); otherwise the
-    separate fused BN+ReLU and max-pool ops."""
+    separate fused BN+ReLU and max-pool ops. ``stats``: the producing conv's [rows, C, 2] (sum, sumsq)
+    partials of ``x`` (the statistics pass over x is skipped)."""
     from .pool import _pair_same, max_pool2d
 
     k, s, p = _pair_same(pool.kernel_size), _pair_same(pool.stride or pool.kernel_size), _pair_same(pool.padding)
@@ -195,9 +197,9 @@ def fused_bn_relu_maxpool(x: torch.Tensor, bn: nn.BatchNorm2d, pool: nn.MaxPool2
           and not pool.return_indices and 1 <= k <= 15 and 2 * p <= k
           and x.numel() // x.shape[1] < (1 << 24))
     if not ok:
-        return max_pool2d(fused_bn_act(x, bn, True, None), pool.kernel_size, pool.stride, pool.padding,
+        return max_pool2d(fused_bn_act(x, bn, True, None, stats), pool.kernel_size, pool.stride, pool.padding,
                           pool.dilation, pool.ceil_mode)
     rm, rv = (bn.running_mean, bn.running_var) if bn.track_running_stats else (None, None)
     if bn.track_running_stats:
         _PENDING_COUNTERS.append(bn.num_batches_tracked)
-    return _BNReluPool.apply(x, bn.weight, bn.bias, rm, rv, float(bn.momentum), float(bn.eps), k, s, p)
+    return _BNReluPool.apply(x, bn.weight, bn.bias, rm, rv, float(bn.momentum), float(bn.eps), k, s, p, stats)

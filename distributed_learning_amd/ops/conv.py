@@ -294,3 +294,70 @@ def conv3x3(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
     """Returns (y, stats-or-None); stats are [row_blocks, Cout, 2] partial (sum, sumsq) when the
     native forward ran."""
     return _Conv3x3.apply(x, conv.weight, conv.stride[0], want_stats)
+
+
+# ---- ResNet stem: 7x7 / stride 2 / pad 3 conv on 3-channel images (csrc/kernels/stem.hip) ---------
+# The image is folded space-to-depth (2x2 pixels -> 12 channels, padded to 16) and the conv runs as
+# a stride-1 4x4 conv over the fold: K = 16 taps x 16 channels = 256, weight index
+# k = (th * 4 + tw) * 16 + (ph * 2 + pw) * 3 + c  <->  W[co, c, 2 th + ph - 1, 2 tw + pw - 1].
+STEM_K = 256
+
+
+def supported_stem(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and x.shape[1] == 3
+            and conv.kernel_size == (7, 7) and conv.stride == (2, 2) and conv.padding == (3, 3)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None and conv.out_channels % 64 == 0
+            and x.is_contiguous(memory_format=torch.channels_last) and x.numel() // 3 < (1 << 24))
+
+
+def stem_pack_weight(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, 3, 7, 7] -> packed bf16 [Cout, 256] of the folded 4x4 conv (zeros at kh or kw = -1)."""
+    co = w.shape[0]
+    wp = F.pad(w.to(torch.bfloat16), (1, 0, 1, 0))  # [co, 3, 8, 8]: index kh + 1 = 2 th + ph
+    wp = wp.reshape(co, 3, 4, 2, 4, 2).permute(0, 2, 4, 3, 5, 1).reshape(co, 16, 12)  # (th, tw), (ph, pw, c)
+    return F.pad(wp, (0, 4)).reshape(co, STEM_K).contiguous()
+
+
+def stem_unpack_grad(dwp: torch.Tensor) -> torch.Tensor:
+    """Packed [Cout, 256] gradient -> [Cout, 3, 7, 7]."""
+    co = dwp.shape[0]
+    g = dwp.reshape(co, 4, 4, 16)[..., :12].reshape(co, 4, 4, 2, 2, 3)  # th, tw, ph, pw, c
+    g = g.permute(0, 5, 1, 3, 2, 4).reshape(co, 3, 8, 8)  # c, (th, ph), (tw, pw)
+    return g[:, :, 1:, 1:]
+
+
+class _StemConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, want_stats: bool):
+        C = _ext.require()
+        ctx.set_materialize_grads(False)
+        y, stats, xs = C.stem_fwd(x, stem_pack_weight(weight), want_stats)
+        ctx.save_for_backward(xs)
+        ctx.hw = (x.shape[2], x.shape[3])
+        ctx.wdtype = weight.dtype
+        ctx.wfmt = torch.channels_last if weight.is_contiguous(memory_format=torch.channels_last) and \
+            not weight.is_contiguous() else torch.contiguous_format
+        if stats is not None:
+            ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        if dy is None:
+            return None, None, None
+        if ctx.needs_input_grad[0]:
+            raise RuntimeError("native stem conv: no input gradient (the stem input is the data batch)")
+        (xs,) = ctx.saved_tensors
+        dw = None
+        if ctx.needs_input_grad[1]:
+            odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
+            dwp = _ext.require().stem_wgrad(dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16), xs,
+                                            ctx.hw[0], ctx.hw[1], odt)
+            dw = stem_unpack_grad(dwp).to(ctx.wdtype).contiguous(memory_format=ctx.wfmt)
+        return None, dw, None
+
+
+def stem_conv(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
+    """The ResNet stem conv on the native kernels. Returns (y, stats-or-None); stats are the
+    [row_blocks, Cout, 2] (sum, sumsq) partials of y for the fused BatchNorm."""
+    return _StemConv.apply(x, conv.weight, want_stats)

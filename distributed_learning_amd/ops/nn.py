@@ -119,6 +119,12 @@ def conv_bn_act_maxpool(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, po
     if _BACKEND == "native" and x.is_cuda and isinstance(pool, nn.MaxPool2d):
         from .bn_act import fused_bn_relu_maxpool
 
+        if _NATIVE_CONV and not x.requires_grad:
+            from . import conv as nconv
+
+            if nconv.supported_stem(x, conv):  # 7x7/s2 MFMA conv whose epilogue emits BN's statistics
+                y, stats = nconv.stem_conv(x, conv, want_stats=bn.training)
+                return fused_bn_relu_maxpool(y, bn, pool, stats)
         return fused_bn_relu_maxpool(conv(x), bn, pool)
     return pool(conv_bn_act(x, conv, bn, relu=True))
 

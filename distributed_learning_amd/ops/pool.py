@@ -62,3 +62,27 @@ class MaxPool2d(nn.MaxPool2d):
         if self.return_indices:
             return super().forward(x)
         return max_pool2d(x, self.kernel_size, self.stride, self.padding, self.dilation, self.ceil_mode)
+
+
+class _GlobalAvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[2], x.shape[3])
+        return _ext.require().gap_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _ext.require().gap_bwd(dy, *ctx.hw)
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """``flatten(adaptive_avg_pool2d(x, 1), 1)`` -> [N, C]. Native path (channels_last bf16/fp32,
+    C % 8 == 0): one reduction kernel forward, and a backward that writes dy / HW straight into the
+    channels_last layout (torch's expand makes the last block's BN backward copy a strided tensor)."""
+    from .nn import get_backend
+
+    if get_backend() == "native" and x.dim() == 4 and x.is_cuda and x.shape[1] % 8 == 0 and \
+            x.dtype in (torch.bfloat16, torch.float32) and x.is_contiguous(memory_format=torch.channels_last) and \
+            x.data_ptr() % 16 == 0:
+        return _GlobalAvgPool.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

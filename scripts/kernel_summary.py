@@ -48,9 +48,12 @@ def main():
     rows = []
     with open(a.trace) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+            grid = "x".join(r.get(k, "?") for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"))
+            wg = r.get("Workgroup_Size_X", "?")
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], grid, wg,
+                         r.get("LDS_Block_Size", r.get("Lds_Size", "?")), r.get("VGPR_Count", r.get("Arch_VGPR_Count", "?"))))
     rows.sort()
-    marks = [i for i, (_, _, n) in enumerate(rows) if a.marker in n]
+    marks = [i for i, r in enumerate(rows) if a.marker in r[2]]
     if len(marks) < a.steps + 1:
         start = marks[0] if marks else 0
         nsteps = max(1, len(marks))
@@ -64,7 +67,7 @@ def main():
     per = defaultdict(lambda: [0, 0])
     cat = defaultdict(int)
     busy = 0
-    for s, e, n in win:
+    for s, e, n, *_ in win:
         d = e - s
         per[n][0] += 1
         per[n][1] += d
@@ -87,6 +90,14 @@ def main():
     if a.out:
         with open(a.out + ".md", "w") as f:
             f.write(text)
+        # step anatomy: every dispatch of the last steady step, in issue order, with its launch shape
+        last = [i for i, r in enumerate(win) if a.marker in r[2]]
+        one = win[last[-1]:] if last else win
+        with open(a.out + "_dispatches.md", "w") as f:
+            f.write("| # | kernel | grid (threads) | wg | LDS | VGPR | us |\n|---:|---|---|---:|---:|---:|---:|\n")
+            for i, (s0, e0, n, grid, wg, lds, vg) in enumerate(one):
+                short = re.sub(r"\(.*", "", n)[:90]
+                f.write(f"| {i} | `{short}` | {grid} | {wg} | {lds} | {vg} | {(e0 - s0) / 1e3:.1f} |\n")
 
 
 if __name__ == "__main__":

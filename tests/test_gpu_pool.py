@@ -94,3 +94,31 @@ def test_stem_bn_relu_maxpool_fused_matches_unfused(cuda):
     assert err(bn1.weight.grad, bnr.weight.grad) <= err(bn2.weight.grad, bnr.weight.grad) * 1.5 + 1e-3
     assert err(bn1.bias.grad, bnr.bias.grad) <= err(bn2.bias.grad, bnr.bias.grad) * 1.5 + 1e-3
     assert err(x1.grad, xr.grad) <= err(x2.grad, xr.grad) * 1.5 + 1e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(256, 2048, 7, 7), (3, 1024, 7, 7), (2, 520, 5, 3), (4, 8, 1, 1)])
+def test_global_avg_pool_matches_torch(cuda, dtype, shape):
+    """Native global average pool (fwd [N, C] + channels_last backward) vs fp32 adaptive_avg_pool2d."""
+    from distributed_learning_amd.ops import _ext
+    from distributed_learning_amd.ops import nn as dnn
+    from distributed_learning_amd.ops.pool import global_avg_pool
+
+    torch.manual_seed(0)
+    x = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    xr = x.detach().float().clone().requires_grad_(True)
+    dnn.set_backend("native")
+    try:
+        y = global_avg_pool(x)
+        assert y.grad_fn is not None and "GlobalAvgPool" in type(y.grad_fn).__name__  # the native op ran
+    finally:
+        dnn.set_backend("torch")
+    yr = torch.flatten(F.adaptive_avg_pool2d(xr, 1), 1)
+    tol = dict(rtol=1e-2, atol=1e-2) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    g = torch.randn(y.shape, device=cuda).to(dtype)
+    y.backward(g)
+    yr.backward(g.float())
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+    assert _ext.require() is not None
