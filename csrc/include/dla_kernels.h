@@ -96,6 +96,10 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
                    const float* beta, float eps, float momentum, float* running_mean, float* running_var, float* ws,
                    float* part, bool relu, bool training, hipStream_t stream, const float* ext_part = nullptr,
                    int ext_nrb = 0, uint8_t* relu_mask = nullptr);
+// y = act(BN(x) + BN_d(xd)) from the two finalized workspaces (ws, wsd: launch_bn_fwd with y == nullptr);
+// mask as launch_bn_fwd's ReLU-after-residual bit mask.
+void launch_bn_dual_apply(const void* x, const void* xd, void* y, const float* ws, const float* wsd, int64_t M, int C,
+                          int dtype, bool relu, uint8_t* mask, hipStream_t stream);
 // mask_mode: 0 no ReLU, 1 recompute from x (ReLU right after BN), 2 1-bit mask written by the
 // forward (ReLU after the residual add), 3 from the saved output y.
 // ext_part/ext_nrb: the reduction pass's partials were already produced (GEMM epilogue, BnBwdArgs).

@@ -211,11 +211,15 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __re
 // ---------------------------------------------------------------------------------------------
 // forward: apply  y = act(x*scale + shift [+ res])
 // ---------------------------------------------------------------------------------------------
-template <typename T, bool kRes, bool kRelu>
+// kBnRes: the residual is itself a BatchNorm input (the downsample branch of a residual block):
+// y = act(x*scale + shift + (res*scale2 + shift2)) with scale2/shift2 from ws2 — the downsample BN's
+// output is never written and re-read.
+template <typename T, bool kRes, bool kRelu, bool kBnRes = false>
 __global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                               T* __restrict__ y, const float* __restrict__ ws,
                                                               int64_t M, int C, int nrb, int tpr,
-                                                              uint8_t* __restrict__ mask) {
+                                                              uint8_t* __restrict__ mask,
+                                                              const float* __restrict__ ws2 = nullptr) {
   // Same tiling as the reduction passes: a thread owns 8 fixed channels for all its rows, so the
   // per-channel coefficients live in registers (no per-element index math or table reads).
   const int rpi = kBNThreads / tpr, ct = tpr * 8;
@@ -223,11 +227,13 @@ __global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restric
   const int rg = threadIdx.x / tpr;
   int64_t r0, r1;
   block_rows(M, nrb, r0, r1);
-  float sc[8], sh[8];
+  float sc[8], sh[8], sc2[8], sh2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sc[j] = ws[2 * C + c0 + j];
     sh[j] = ws[3 * C + c0 + j];
+    sc2[j] = kBnRes ? ws2[2 * C + c0 + j] : 1.f;
+    sh2[j] = kBnRes ? ws2[3 * C + c0 + j] : 0.f;
   }
   auto row = [&](int64_t r) {
     const int64_t off = r * C + c0;
@@ -239,7 +245,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restric
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float o = fmaf(a[j], sc[j], sh[j]);
-      if (kRes) o += rv[j];
+      if (kRes) o += kBnRes ? fmaf(rv[j], sc2[j], sh2[j]) : rv[j];
       if (kRelu) {
         bits |= (o > 0.f ? 1u : 0u) << j;
         o = fmaxf(o, 0.f);
@@ -271,7 +277,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restric
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float o = fmaf(a[j], sc[j], sh[j]);
-        if (kRes) o += rv[j];
+        if (kRes) o += kBnRes ? fmaf(rv[j], sc2[j], sh2[j]) : rv[j];
         if (kRelu) {
           bits |= (o > 0.f ? 1u : 0u) << j;
           o = fmaxf(o, 0.f);
@@ -345,6 +351,32 @@ struct PoolDy {
     const int ow_lo = wp < k - 1 ? 0 : (wp - k + 1 + s - 1) / s, ow_hi = min(OW - 1, wp / s);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = 0.f;
+    if (k <= 2 * s) {
+      // at most 2 x 2 windows contain the pixel: issue all four (pos, dy) loads before any use so
+      // they are in flight together (the data-dependent loop below serialises them)
+      uint64_t pk[4];
+      ushort8_t dv[4];
+      uint32_t qv[4];
+      bool ok[4];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int oh = oh_hi - a, ow = ow_hi - b, t = a * 2 + b;
+          ok[t] = oh >= oh_lo && ow >= ow_lo;
+          const int ohc = ok[t] ? oh : oh_hi, owc = ok[t] ? ow : ow_hi;
+          qv[t] = (uint32_t)((hp - ohc * s) * k + (wp - owc * s));
+          const int64_t o = (((int64_t)n * OH + max(ohc, 0)) * OW + max(owc, 0)) * C + c0;
+          pk[t] = *reinterpret_cast<const uint64_t*>(pos + o);
+          dv[t] = *reinterpret_cast<const ushort8_t*>(dyp + o);
+        }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (ok[t] && ((pk[t] >> (8 * j)) & 0xffu) == qv[t]) g[j] += bf16_to_f32(dv[t][j]);
+      return;
+    }
     for (int oh = oh_lo; oh <= oh_hi; ++oh)
       for (int ow = ow_lo; ow <= ow_hi; ++ow) {
         const uint32_t qq = (uint32_t)((hp - oh * s) * k + (wp - ow * s));
@@ -575,6 +607,21 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
     else { if (relu) DLA_BN_APPLY(float, false, true); else DLA_BN_APPLY(float, false, false); }
   }
 #undef DLA_BN_APPLY
+}
+
+void launch_bn_dual_apply(const void* x, const void* xd, void* y, const float* ws, const float* wsd, int64_t M, int C,
+                          int dtype, bool relu, uint8_t* mask, hipStream_t stream) {
+  int atpr, anrb, anct;
+  bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
+#define DLA_BN_DUAL(T, A)                                                                                         \
+  hipLaunchKernelGGL((bn_apply_kernel<T, true, A, true>), dim3(anct, anrb), dim3(kBNThreads), 0, stream,          \
+                     (const T*)x, (const T*)xd, (T*)y, ws, M, C, anrb, atpr, mask, wsd)
+  if (dtype == kBF16) {
+    if (relu) DLA_BN_DUAL(bf16_t, true); else DLA_BN_DUAL(bf16_t, false);
+  } else {
+    if (relu) DLA_BN_DUAL(float, true); else DLA_BN_DUAL(float, false);
+  }
+#undef DLA_BN_DUAL
 }
 
 void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const void* x, void* dx, void* dres,

@@ -80,6 +80,53 @@ std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> resid
   return {y, ws, mask};
 }
 
+// Training-mode act(BN(x) + BN_d(xd)) — a residual block whose shortcut is a downsample conv + BN —
+// in one apply pass: the shortcut BN's output is never materialised. Returns (y, ws, wsd, mask);
+// mask (ReLU only) is the 1-bit ReLU mask both backward passes read. stats / statsd: optional
+// [row_blocks, C, 2] partials from the producing convs' epilogues.
+std::vector<at::Tensor> bn_dual_fwd(at::Tensor x, at::Tensor xd, c10::optional<at::Tensor> weight,
+                                    c10::optional<at::Tensor> bias, c10::optional<at::Tensor> running_mean,
+                                    c10::optional<at::Tensor> running_var, c10::optional<at::Tensor> weight_d,
+                                    c10::optional<at::Tensor> bias_d, c10::optional<at::Tensor> running_mean_d,
+                                    c10::optional<at::Tensor> running_var_d, double momentum, double momentum_d,
+                                    double eps, double eps_d, bool relu, c10::optional<at::Tensor> stats,
+                                    c10::optional<at::Tensor> stats_d) {
+  check_act(x, "x");
+  check_act(xd, "xd");
+  TORCH_CHECK(xd.sizes() == x.sizes() && xd.scalar_type() == x.scalar_type(), "bn_dual: x / xd mismatch");
+  const int C = (int)x.size(1);
+  const int64_t M = rows_of(x);
+  auto f32 = x.options().dtype(at::kFloat);
+  auto fptr = [](const c10::optional<at::Tensor>& t) -> float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "BN parameters/stats must be fp32 contiguous");
+    return t->data_ptr<float>();
+  };
+  auto finalize = [&](const at::Tensor& in, const c10::optional<at::Tensor>& g, const c10::optional<at::Tensor>& b,
+                      const c10::optional<at::Tensor>& rm, const c10::optional<at::Tensor>& rv, double mom, double ep,
+                      const c10::optional<at::Tensor>& st) {
+    at::Tensor ws = at::empty({7 * (int64_t)C}, f32);
+    const bool ext = st.has_value() && st->defined();
+    if (ext)
+      TORCH_CHECK(st->scalar_type() == at::kFloat && st->is_contiguous() && st->dim() == 3 && st->size(1) == C &&
+                      st->size(2) == 2,
+                  "stats must be fp32 [row_blocks, C, 2] partials");
+    at::Tensor part = at::empty({ext ? 1 : partial_floats(M, C)}, f32);
+    launch_bn_fwd(in.data_ptr(), nullptr, nullptr, M, C, dtype_code(in), fptr(g), fptr(b), (float)ep, (float)mom,
+                  fptr(rm), fptr(rv), ws.data_ptr<float>(), part.data_ptr<float>(), relu, true, current_stream(in),
+                  ext ? st->data_ptr<float>() : nullptr, ext ? (int)st->size(0) : 0);
+    return ws;
+  };
+  at::Tensor ws = finalize(x, weight, bias, running_mean, running_var, momentum, eps, stats);
+  at::Tensor wsd = finalize(xd, weight_d, bias_d, running_mean_d, running_var_d, momentum_d, eps_d, stats_d);
+  at::Tensor y = at::empty_like(x);
+  at::Tensor mask;
+  if (relu) mask = at::empty({(M * C + 7) / 8}, x.options().dtype(at::kByte));
+  launch_bn_dual_apply(x.data_ptr(), xd.data_ptr(), y.data_ptr(), ws.data_ptr<float>(), wsd.data_ptr<float>(), M, C,
+                       dtype_code(x), relu, relu ? mask.data_ptr<uint8_t>() : nullptr, current_stream(x));
+  return {y, ws, wsd, mask};
+}
+
 // Returns (dx, dres-or-undefined, dgamma, dbeta). mask_mode (see launch_bn_bwd): 0 no ReLU,
 // 1 recompute the ReLU branch from x, 2 use `mask` from bn_act_fwd, 3 use the saved output `y`.
 std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, c10::optional<at::Tensor> mask,
@@ -541,6 +588,7 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("ceil_mode") = false,
         pybind11::arg("need_pos") = true);
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pooling backward (gather form)");
+  m.def("bn_dual_fwd", &bn_dual_fwd, "training act(BN(x) + BN_d(xd)) in one apply pass (downsample residual)");
   m.def("gap_fwd", &gap_fwd, "NHWC global average pooling -> [N, C]");
   m.def("stem_fwd", &stem_fwd, "7x7/s2/p3 stem conv, 3 input channels (space-to-depth + MFMA implicit GEMM, BN-statistics epilogue)");
   m.def("stem_wgrad", &stem_wgrad, "7x7/s2/p3 stem conv weight gradient from the folded input (packed [Cout, 256] layout)");

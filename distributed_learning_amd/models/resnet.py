@@ -46,9 +46,10 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
         out = dnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-        return dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=identity)
+        if self.downsample is not None:  # one apply pass for relu(bn2(conv2) + bn_d(conv_d))
+            return dnn.conv_bn_add_conv_bn_act(out, self.conv2, self.bn2, x, self.downsample[0], self.downsample[1])
+        return dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=x)
 
 
 class Bottleneck(nn.Module):
@@ -73,12 +74,17 @@ class Bottleneck(nn.Module):
             # stride-2 downsample: conv1's fork also yields x[:, :, ::2, ::2], whose compact gradient
             # it adds at the even pixels in its dgrad epilogue (no zero-filled scatter)
             out, xa, xs = dnn.conv_bn_act_fork(x, self.conv1, self.bn1, relu=True, subsample=True)
-            identity = self.downsample(xa) if xs is None else self.downsample.forward_presubsampled(xs)
         else:
             out, xa = dnn.conv_bn_act_fork(x, self.conv1, self.bn1, relu=True)
-            identity = xa if self.downsample is None else self.downsample(xa)
+            xs = None
         out = dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True)
-        return dnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=identity)
+        if self.downsample is None:
+            return dnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=xa)
+        # the shortcut BN is applied inside the block's final apply pass (never materialised)
+        ds_conv, ds_bn = self.downsample[0], self.downsample[1]
+        if xs is not None:
+            return dnn.conv_bn_add_conv_bn_act(out, self.conv3, self.bn3, xs, ds_conv, ds_bn, presubsampled=True)
+        return dnn.conv_bn_add_conv_bn_act(out, self.conv3, self.bn3, xa, ds_conv, ds_bn)
 
 
 class Downsample(nn.Sequential):

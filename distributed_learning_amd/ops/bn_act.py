@@ -102,6 +102,56 @@ class _BNAct(torch.autograd.Function):
                 None, None, None, None, None, None, None, None)
 
 
+class _BNDualAct(torch.autograd.Function):
+    """Training-mode ``act(BN(x) + BN_d(xd))``: a residual block's main branch plus its downsample
+    shortcut. One apply pass reads both pre-BN tensors (the shortcut BN's output is never written);
+    backward runs the two BN backwards from the same dy and 1-bit ReLU mask (no materialised
+    residual gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, xd, weight_d, bias_d, rm, rv, rmd, rvd, momentum, momentum_d, eps, eps_d,
+                relu, stats, stats_d):
+        C = _ext.require()
+        y, ws, wsd, mask = C.bn_dual_fwd(x, xd, weight, bias, rm, rv, weight_d, bias_d, rmd, rvd, momentum,
+                                         momentum_d, eps, eps_d, relu, stats, stats_d)
+        ctx.relu = relu
+        ctx.save_for_backward(x, ws, weight, xd, wsd, weight_d, mask if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, ws, weight, xd, wsd, weight_d, mask = ctx.saved_tensors
+        C = _ext.require()
+        mode = MASK_BITS if ctx.relu else MASK_NONE
+        dx, _, dg, db = C.bn_act_bwd(dy, None, mask, x, ws, weight, mode, False, None)
+        dxd, _, dgd, dbd = C.bn_act_bwd(dy, None, mask, xd, wsd, weight_d, mode, False, None)
+        need = ctx.needs_input_grad
+        return (dx, dg if need[1] else None, db if need[2] else None, dxd, dgd if need[4] else None,
+                dbd if need[5] else None) + (None,) * 11
+
+
+def dual_supported(x: torch.Tensor, bn: nn.BatchNorm2d, xd: torch.Tensor, bnd: nn.BatchNorm2d) -> bool:
+    return (bn.training and bnd.training and x.dtype == xd.dtype and x.shape == xd.shape
+            and supported(x, bn, None) and supported(xd, bnd, None)
+            and bn.momentum is not None and bnd.momentum is not None)
+
+
+def fused_bn_add_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, xd: torch.Tensor, bnd: nn.BatchNorm2d,
+                        relu: bool = True, stats=None, stats_d=None) -> torch.Tensor:
+    """``act(bn(x) + bnd(xd))`` (training mode); falls back to the two-step form when unsupported."""
+    if not dual_supported(x, bn, xd, bnd):
+        return fused_bn_act(x, bn, relu, fused_bn_act(xd, bnd, False, None, stats_d), stats)
+    running = []
+    for b in (bn, bnd):
+        running += [b.running_mean, b.running_var] if b.track_running_stats else [None, None]
+        if b.track_running_stats:
+            _PENDING_COUNTERS.append(b.num_batches_tracked)
+    if len(_PENDING_COUNTERS) >= 1024:
+        flush_bn_counters()
+    return _BNDualAct.apply(x, bn.weight, bn.bias, xd, bnd.weight, bnd.bias, *running, float(bn.momentum),
+                            float(bnd.momentum), float(bn.eps), float(bnd.eps), relu, stats, stats_d)
+
+
 # num_batches_tracked increments are batched into one multi-tensor launch per forward instead of
 # 53 one-element kernels (ResNet-50); flushed by the DP wrappers after the model forward.
 _PENDING_COUNTERS: list = []

@@ -113,6 +113,45 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
     return bn_act(conv(x), bn, relu, residual)
 
 
+def _native_conv_stats(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool, presubsampled: bool = False):
+    """(y, stats-or-None) from a native 1x1 / 3x3 conv, or None when neither applies."""
+    from . import conv as nconv
+
+    if nconv.supported(x, conv):
+        return nconv.conv1x1(x, conv, want_stats=want_stats, stride=1 if presubsampled else None)
+    if not presubsampled and nconv.supported3x3(x, conv):
+        want = want_stats and nconv.CONV3_POLICY["fwd"] == "native"
+        return nconv.conv3x3(x, conv, want_stats=want)
+    return None
+
+
+# act(BN(conv(x)) + BN_d(conv_d(xd))) in one apply pass (bench A/B switch)
+DUAL_RESIDUAL = True
+
+
+def conv_bn_add_conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, xd: torch.Tensor,
+                            conv_d: nn.Conv2d, bn_d: nn.BatchNorm2d, relu: bool = True,
+                            presubsampled: bool = False) -> torch.Tensor:
+    """``act(BN(conv(x)) + BN_d(conv_d(xd)))`` — a residual block's last conv plus its downsample
+    shortcut. Native path: both convs emit their BN statistics and one apply pass reads both conv
+    outputs (the shortcut BN's output is never written). ``presubsampled``: ``xd`` is already the
+    stride-2 subsample the strided ``conv_d`` would take."""
+    if _BACKEND == "native" and _NATIVE_CONV and DUAL_RESIDUAL and x.is_cuda and bn.training and bn_d.training:
+        from .bn_act import dual_supported, fused_bn_add_bn_act
+
+        a = _native_conv_stats(x, conv, True)
+        b = _native_conv_stats(xd, conv_d, True, presubsampled) if a is not None else None
+        if a is not None and b is not None and dual_supported(a[0], bn, b[0], bn_d):
+            return fused_bn_add_bn_act(a[0], bn, b[0], bn_d, relu, a[1], b[1])
+        if a is not None and b is not None:  # convs done; BN the plain way
+            from .bn_act import fused_bn_act
+
+            ident = fused_bn_act(b[0], bn_d, False, None, b[1])
+            return fused_bn_act(a[0], bn, relu, ident, a[1])
+    ident = conv_bn_act(xd, conv_d, bn_d, relu=False, presubsampled=presubsampled)
+    return conv_bn_act(x, conv, bn, relu=relu, residual=ident)
+
+
 def conv_bn_act_maxpool(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, pool: nn.Module):
     """``pool(relu(BN(conv(x))))`` — the ResNet stem. Native path: the BN+ReLU+max-pool runs as one
     fused op (the 112x112 activation and its gradient are never written)."""

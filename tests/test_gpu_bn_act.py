@@ -78,6 +78,51 @@ def test_bn_act_eval_mode(cuda):
     torch.testing.assert_close(y.float(), torch.relu(bn(x.float())), rtol=2e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(8, 256, 14, 14), (2, 2048, 7, 7), (3, 24, 5, 9)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_bn_dual_residual_fwd_bwd(cuda, dtype, shape, relu):
+    """act(BN(x) + BN_d(xd)) in one apply pass (downsample shortcut) vs two fp32 BatchNorms."""
+    from distributed_learning_amd.ops.bn_act import _BNDualAct, fused_bn_add_bn_act
+
+    torch.manual_seed(1)
+    C = shape[1]
+    bns = [nn.BatchNorm2d(C).to(cuda) for _ in range(2)]
+    with torch.no_grad():
+        for b in bns:
+            b.weight.uniform_(0.5, 1.5)
+            b.bias.uniform_(-0.5, 0.5)
+    refs = [nn.BatchNorm2d(C).to(cuda) for _ in range(2)]
+    for r, b in zip(refs, bns):
+        r.load_state_dict(b.state_dict())
+    x = (torch.randn(shape, device=cuda) * 2 + 0.7).to(dtype).contiguous(memory_format=torch.channels_last)
+    xd = (torch.randn(shape, device=cuda) - 0.3).to(dtype).contiguous(memory_format=torch.channels_last)
+    x1, xd1 = x.clone().requires_grad_(True), xd.clone().requires_grad_(True)
+    y = fused_bn_add_bn_act(x1, bns[0], xd1, bns[1], relu)
+    assert isinstance(y.grad_fn, _BNDualAct._backward_cls)  # the fused op ran
+    x2, xd2 = x.float().clone().requires_grad_(True), xd.float().clone().requires_grad_(True)
+    pre_r = refs[0](x2) + refs[1](xd2)
+    yr = torch.relu(pre_r) if relu else pre_r
+    tol = dict(rtol=2e-2, atol=3e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    for b, r in zip(bns, refs):
+        torch.testing.assert_close(b.running_mean, r.running_mean, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(b.running_var, r.running_var, rtol=1e-3, atol=1e-4)
+    g = torch.randn(shape, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    y.backward(g)
+    F = torch.nn.functional
+    pre = F.batch_norm(x2, None, None, refs[0].weight, refs[0].bias, True, 0.0, refs[0].eps) + \
+        F.batch_norm(xd2, None, None, refs[1].weight, refs[1].bias, True, 0.0, refs[1].eps)
+    mask = (y.detach().float() > 0).float() if relu else torch.ones_like(pre)
+    (pre * mask * g.float()).sum().backward()
+    _close_mostly(x1.grad.float(), x2.grad, **tol)
+    _close_mostly(xd1.grad.float(), xd2.grad, **tol)
+    btol = dict(rtol=2e-2, atol=5e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-3)
+    for b, r in zip(bns, refs):
+        torch.testing.assert_close(b.weight.grad, r.weight.grad, **btol)
+        torch.testing.assert_close(b.bias.grad, r.bias.grad, **btol)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_resnet50_native_matches_torch_backend(cuda, dtype):
     """Whole-model check. MIOpen's convolutions are not bitwise reproducible run to run and amplify
