@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--force_comm", type=int, default=0,
                     help="1 = run the multi-rank gradient path (gather -> RCCL all-reduce -> re-point) even at "
                          "one GPU (diagnostic: the per-GPU cost of the N>1 data path without the link time)")
+    ap.add_argument("--wgrad_overlap_rows", type=int, default=None,
+                    help="weight gradients of convs with at most this many output rows run concurrently with "
+                         "their data gradient on a side stream (0 = off; default: ops/conv.py)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--momentum", type=float, default=0.5)
     return ap.parse_args()
@@ -86,6 +89,10 @@ def main():
     torch.backends.cudnn.benchmark = True
     dnn.set_backend(a.kernels)
     dnn.set_native_conv(a.conv == "native")
+    if a.wgrad_overlap_rows is not None:
+        from distributed_learning_amd.ops import conv as nconv
+
+        nconv.WGRAD_OVERLAP_MAX_ROWS = a.wgrad_overlap_rows
 
     spec = get_spec(a.model)
     torch.manual_seed(1234)

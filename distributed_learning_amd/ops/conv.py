@@ -52,6 +52,43 @@ def _as_param_layout(dw2: torch.Tensor, shape, stride) -> torch.Tensor:
     return dw2.as_strided(shape, stride)
 
 
+# Weight gradients of launches that under-fill the chip (ResNet-50 stages 2-4: M = N*H*W <= 200704
+# rows gives <= 1568 128x128 tiles, 1-3 waves of 2 blocks on 256 CUs with a ragged last wave) can run
+# on a side stream, concurrently with the data gradient of the same conv; the compute stream joins
+# the side stream before the next op (event wait, also inside HIP-graph capture). 0 disables.
+# Off by default: measured on MI355X (scripts/wgrad_overlap_sweep.sh, ResNet-50 bs256) the step took
+# 22.75 ms without, 23.36 / 23.51 / 23.33 ms with the overlap up to 50176 / 200704 / 802816 rows —
+# the concurrent GEMMs contend for the same L2 / Infinity Cache and CUs rather than filling gaps.
+WGRAD_OVERLAP_MAX_ROWS = 0
+_SIDE_STREAMS: dict = {}
+
+
+class _SideWork:
+    """``fn()`` on the device's side stream (after the current stream's pending work) when
+    ``rows`` is small enough, else inline; ``result()`` joins and returns its tensor."""
+
+    def __init__(self, fn, rows: int, device: torch.device):
+        self.side = None
+        if WGRAD_OVERLAP_MAX_ROWS and rows <= WGRAD_OVERLAP_MAX_ROWS:
+            cur = torch.cuda.current_stream(device)
+            side = _SIDE_STREAMS.get(device)
+            if side is None:
+                side = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self.out = fn()
+            self.side, self.cur = side, cur
+        else:
+            self.out = fn()
+
+    def result(self):
+        if self.side is not None:
+            self.cur.wait_stream(self.side)
+            if self.out is not None:
+                self.out.record_stream(self.cur)  # allocated on the side stream, used on the current one
+        return self.out
+
+
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride: int, want_stats: bool):
@@ -86,6 +123,11 @@ class _Conv1x1(torch.autograd.Function):
             dy = dy.to(torch.bfloat16)
         dy2 = _rows(dy)
         dx = dw = None
+        wg = None
+        if ctx.needs_input_grad[1]:
+            odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
+            wg = _SideWork(lambda: _as_param_layout(C.gemm_tn(dy2, _rows(x), odt, 1.0).to(ctx.wdtype), ctx.wshape,
+                                                    ctx.wstride), dy2.shape[0], dy.device)
         if ctx.needs_input_grad[0]:
             link = ctx.link
             if link is not None:
@@ -102,9 +144,8 @@ class _Conv1x1(torch.autograd.Function):
                 dx[:, :, ::ctx.stride, ::ctx.stride] = dxs
             else:
                 dx = dxs
-        if ctx.needs_input_grad[1]:
-            dw = _as_param_layout(C.gemm_tn(dy2, _rows(x), ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16)
-                                            else torch.float32, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
+        if wg is not None:
+            dw = wg.result()
         return dx, dw, None, None
 
 
@@ -167,6 +208,11 @@ class _Conv1x1Fork(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
         dy2 = _rows(dy)
         dx = dw = None
+        wg = None
+        if ctx.needs_input_grad[1]:
+            odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
+            wg = _SideWork(lambda: _as_param_layout(C.gemm_tn(dy2, _rows(x), odt, 1.0).to(ctx.wdtype), ctx.wshape,
+                                                    ctx.wstride), dy2.shape[0], dy.device)
         if ctx.needs_input_grad[0]:
             add = None if dident is None else _rows(dident)
             link = ctx.link
@@ -178,9 +224,8 @@ class _Conv1x1Fork(torch.autograd.Function):
             dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
             if link is not None:
                 link.publish(dx, part)
-        if ctx.needs_input_grad[1]:
-            dw = _as_param_layout(C.gemm_tn(dy2, _rows(x), ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16)
-                                            else torch.float32, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
+        if wg is not None:
+            dw = wg.result()
         return dx, dw, None, None, None
 
 
@@ -266,6 +311,19 @@ class _Conv3x3(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
         dx = dw = None
+        wg = None
+        if ctx.needs_input_grad[1]:
+            odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
+
+            def wgrad():
+                if CONV3_POLICY["wgrad"] == "native":
+                    g = C.conv3x3_wgrad(dy, x, ctx.stride, odt)
+                else:
+                    g = torch.ops.aten.convolution_backward(dy, x, w, None, [ctx.stride] * 2, [1, 1], [1, 1], False,
+                                                            [0, 0], 1, [False, True, False])[1]
+                return g.to(ctx.wdtype)
+
+            wg = _SideWork(wgrad, dy.shape[0] * dy.shape[2] * dy.shape[3], dy.device)
         if ctx.needs_input_grad[0]:
             if ctx.stride == 1 and x.shape[1] <= CONV3_POLICY["dgrad_native_max_cin"]:
                 link = ctx.link
@@ -279,14 +337,8 @@ class _Conv3x3(torch.autograd.Function):
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, [ctx.stride] * 2, [1, 1], [1, 1], False,
                                                          [0, 0], 1, [True, False, False])[0]
-        if ctx.needs_input_grad[1]:
-            odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
-            if CONV3_POLICY["wgrad"] == "native":
-                dw = C.conv3x3_wgrad(dy, x, ctx.stride, odt)
-            else:
-                dw = torch.ops.aten.convolution_backward(dy, x, w, None, [ctx.stride] * 2, [1, 1], [1, 1], False,
-                                                         [0, 0], 1, [False, True, False])[1]
-            dw = dw.to(ctx.wdtype)
+        if wg is not None:
+            dw = wg.result()
         return dx, dw, None, None
 
 
