@@ -100,6 +100,12 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
 // mask as launch_bn_fwd's ReLU-after-residual bit mask.
 void launch_bn_dual_apply(const void* x, const void* xd, void* y, const float* ws, const float* wsd, int64_t M, int C,
                           int dtype, bool relu, uint8_t* mask, hipStream_t stream);
+// backward of launch_bn_dual_apply: dx, dxd and both (dgamma, dbeta) from one dy (+ the forward's
+// bit mask, or null without ReLU); part / partd: [bn_geometry rows][C][2] scratch each.
+void launch_bn_dual_bwd(const void* dy, const uint8_t* mask, const void* x, const void* xd, void* dx, void* dxd,
+                        int64_t M, int C, int dtype, const float* gamma, const float* gamma_d, float* ws, float* wsd,
+                        float* part, float* partd, float* dgamma, float* dbeta, float* dgamma_d, float* dbeta_d,
+                        hipStream_t stream);
 // mask_mode: 0 no ReLU, 1 recompute from x (ReLU right after BN), 2 1-bit mask written by the
 // forward (ReLU after the residual add), 3 from the saved output y.
 // ext_part/ext_nrb: the reduction pass's partials were already produced (GEMM epilogue, BnBwdArgs).

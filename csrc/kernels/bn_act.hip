@@ -550,6 +550,152 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(DY dy, const T
 }
 
 // ---------------------------------------------------------------------------------------------
+// backward of act(BN(x) + BN_d(xd)) (the dual apply above): both BNs see the same dy' = dy masked
+// by the ReLU bit, so one reduce pass reads dy (+ mask) once for both, Σdy' is shared, and one apply
+// pass writes dx and dxd — the residual gradient is never materialised and dy is read twice, not 4x.
+// ---------------------------------------------------------------------------------------------
+template <typename T, int kMask>
+__global__ __launch_bounds__(kBNThreads) void bn_bwd_dual_reduce_kernel(const T* __restrict__ dy,
+                                                                        const uint8_t* __restrict__ mask,
+                                                                        const T* __restrict__ x,
+                                                                        const T* __restrict__ xd,
+                                                                        const float* __restrict__ ws,
+                                                                        const float* __restrict__ wsd, int64_t M,
+                                                                        int C, int nrb, int tpr,
+                                                                        float* __restrict__ part,
+                                                                        float* __restrict__ partd) {
+  static_assert(kMask == kMaskNone || kMask == kMaskBits, "dual BN backward: no ReLU or the forward's bit mask");
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int rpi = kBNThreads / tpr, ct = tpr * 8;
+  const int c_base = blockIdx.x * ct;
+  const int c0 = c_base + (threadIdx.x % tpr) * 8;
+  const int rg = threadIdx.x / tpr;
+  int64_t r0, r1;
+  block_rows(M, nrb, r0, r1);
+  float mean[8], meand[8], s[8], q[8], qd[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mean[j] = ws[c0 + j];
+    meand[j] = wsd[c0 + j];
+    s[j] = q[j] = qd[j] = 0.f;
+  }
+  auto accum = [&](const float (&g0)[8], uint32_t mb, const float (&xv)[8], const float (&xdv)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float g = (kMask == kMaskBits && !((mb >> j) & 1u)) ? 0.f : g0[j];
+      s[j] += g;
+      q[j] = fmaf(g, xv[j] - mean[j], q[j]);
+      qd[j] = fmaf(g, xdv[j] - meand[j], qd[j]);
+    }
+  };
+  int64_t r = r0 + rg;
+  for (; r + (kUnroll - 1) * rpi < r1; r += kUnroll * rpi) {
+    Raw8<T> gr[kUnroll], xr[kUnroll], dr[kUnroll];
+    uint32_t mb[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int64_t off = (r + u * rpi) * C + c0;
+      gr[u].load(dy + off);
+      xr[u].load(x + off);
+      dr[u].load(xd + off);
+      mb[u] = kMask == kMaskBits ? (uint32_t)mask[off >> 3] : 0xffu;
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep every load of the group ahead of its arithmetic
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      float g[8], xv[8], xdv[8];
+      gr[u].get(g);
+      xr[u].get(xv);
+      dr[u].get(xdv);
+      accum(g, mb[u], xv, xdv);
+    }
+  }
+  for (; r < r1; r += rpi) {
+    const int64_t off = r * C + c0;
+    float g[8], xv[8], xdv[8];
+    Vec8<T>::load(dy + off, g);
+    Vec8<T>::load(x + off, xv);
+    Vec8<T>::load(xd + off, xdv);
+    accum(g, kMask == kMaskBits ? (uint32_t)mask[off >> 3] : 0xffu, xv, xdv);
+  }
+  float s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s2[j] = s[j];
+  block_reduce_write(s, q, tpr, rpi, ct, C, part, c_base, red);
+  __syncthreads();  // red is reused
+  block_reduce_write(s2, qd, tpr, rpi, ct, C, partd, c_base, red);
+}
+
+template <typename T, int kMask>
+__global__ __launch_bounds__(kBNThreads) void bn_bwd_dual_apply_kernel(const T* __restrict__ dy,
+                                                                       const uint8_t* __restrict__ mask,
+                                                                       const T* __restrict__ x,
+                                                                       const T* __restrict__ xd,
+                                                                       const float* __restrict__ ws,
+                                                                       const float* __restrict__ wsd,
+                                                                       T* __restrict__ dx, T* __restrict__ dxd,
+                                                                       int64_t M, int C, int nrb, int tpr) {
+  static_assert(kMask == kMaskNone || kMask == kMaskBits, "dual BN backward: no ReLU or the forward's bit mask");
+  const int rpi = kBNThreads / tpr, ct = tpr * 8;
+  const int c0 = blockIdx.x * ct + (threadIdx.x % tpr) * 8;
+  const int rg = threadIdx.x / tpr;
+  int64_t r0, r1;
+  block_rows(M, nrb, r0, r1);
+  float mean[8], k1[8], m1[8], k2[8], meand[8], k1d[8], m1d[8], k2d[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mean[j] = ws[c0 + j];
+    k1[j] = ws[4 * C + c0 + j];
+    m1[j] = ws[5 * C + c0 + j];
+    k2[j] = ws[6 * C + c0 + j];
+    meand[j] = wsd[c0 + j];
+    k1d[j] = wsd[4 * C + c0 + j];
+    m1d[j] = wsd[5 * C + c0 + j];
+    k2d[j] = wsd[6 * C + c0 + j];
+  }
+  auto emit = [&](int64_t off, const float (&g0)[8], uint32_t mb, float (&xv)[8], float (&xdv)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float g = (kMask == kMaskBits && !((mb >> j) & 1u)) ? 0.f : g0[j];
+      xv[j] = k1[j] * (g - m1[j] - (xv[j] - mean[j]) * k2[j]);
+      xdv[j] = k1d[j] * (g - m1d[j] - (xdv[j] - meand[j]) * k2d[j]);
+    }
+    Vec8<T>::store(dx + off, xv);
+    Vec8<T>::store(dxd + off, xdv);
+  };
+  int64_t r = r0 + rg;
+  for (; r + (kUnroll - 1) * rpi < r1; r += kUnroll * rpi) {
+    Raw8<T> gr[kUnroll], xr[kUnroll], dr[kUnroll];
+    uint32_t mb[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int64_t off = (r + u * rpi) * C + c0;
+      gr[u].load(dy + off);
+      xr[u].load(x + off);
+      dr[u].load(xd + off);
+      mb[u] = kMask == kMaskBits ? (uint32_t)mask[off >> 3] : 0xffu;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      float g[8], xv[8], xdv[8];
+      gr[u].get(g);
+      xr[u].get(xv);
+      dr[u].get(xdv);
+      emit((r + u * rpi) * C + c0, g, mb[u], xv, xdv);
+    }
+  }
+  for (; r < r1; r += rpi) {
+    const int64_t off = r * C + c0;
+    float g[8], xv[8], xdv[8];
+    Vec8<T>::load(dy + off, g);
+    Vec8<T>::load(x + off, xv);
+    Vec8<T>::load(xd + off, xdv);
+    emit(off, g, kMask == kMaskBits ? (uint32_t)mask[off >> 3] : 0xffu, xv, xdv);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
 void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks = kRedBlocks) {
@@ -763,6 +909,41 @@ void launch_bn_relu_maxpool_bwd(const void* dy_pool, const uint8_t* pos, const v
   hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16_t, kMaskRecomp, false, PoolDy>), dim3(anct, anrb), dim3(kBNThreads), 0,
                      stream, pd, (const bf16_t*)nullptr, (const uint8_t*)nullptr, (const bf16_t*)x, (const float*)ws,
                      (bf16_t*)dx, (bf16_t*)nullptr, M, C, anrb, atpr);
+}
+
+void launch_bn_dual_bwd(const void* dy, const uint8_t* mask, const void* x, const void* xd, void* dx, void* dxd,
+                        int64_t M, int C, int dtype, const float* gamma, const float* gamma_d, float* ws, float* wsd,
+                        float* part, float* partd, float* dgamma, float* dbeta, float* dgamma_d, float* dbeta_d,
+                        hipStream_t stream) {
+  int tpr, nrb, nct;
+  bn_geometry(M, C, &tpr, &nrb, &nct);
+  const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
+  const bool bits = mask != nullptr;
+#define DLA_DUAL_RED(T, K)                                                                                        \
+  hipLaunchKernelGGL((bn_bwd_dual_reduce_kernel<T, K>), dim3(nct, nrb), dim3(kBNThreads), lds, stream, (const T*)dy, \
+                     mask, (const T*)x, (const T*)xd, (const float*)ws, (const float*)wsd, M, C, nrb, tpr, part, partd)
+  if (dtype == kBF16) {
+    if (bits) DLA_DUAL_RED(bf16_t, kMaskBits); else DLA_DUAL_RED(bf16_t, kMaskNone);
+  } else {
+    if (bits) DLA_DUAL_RED(float, kMaskBits); else DLA_DUAL_RED(float, kMaskNone);
+  }
+#undef DLA_DUAL_RED
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, part, nrb, M, C, gamma, ws,
+                     dgamma, dbeta);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, partd, nrb, M, C, gamma_d,
+                     wsd, dgamma_d, dbeta_d);
+  int atpr, anrb, anct;
+  bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
+#define DLA_DUAL_APPLY(T, K)                                                                                      \
+  hipLaunchKernelGGL((bn_bwd_dual_apply_kernel<T, K>), dim3(anct, anrb), dim3(kBNThreads), 0, stream, (const T*)dy, \
+                     mask, (const T*)x, (const T*)xd, (const float*)ws, (const float*)wsd, (T*)dx, (T*)dxd, M, C, anrb, \
+                     atpr)
+  if (dtype == kBF16) {
+    if (bits) DLA_DUAL_APPLY(bf16_t, kMaskBits); else DLA_DUAL_APPLY(bf16_t, kMaskNone);
+  } else {
+    if (bits) DLA_DUAL_APPLY(float, kMaskBits); else DLA_DUAL_APPLY(float, kMaskNone);
+  }
+#undef DLA_DUAL_APPLY
 }
 
 }  // namespace dla

@@ -127,6 +127,39 @@ std::vector<at::Tensor> bn_dual_fwd(at::Tensor x, at::Tensor xd, c10::optional<a
   return {y, ws, wsd, mask};
 }
 
+// Backward of bn_dual_fwd: returns (dx, dgamma, dbeta, dxd, dgamma_d, dbeta_d).
+std::vector<at::Tensor> bn_dual_bwd(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x, at::Tensor ws,
+                                    c10::optional<at::Tensor> weight, at::Tensor xd, at::Tensor wsd,
+                                    c10::optional<at::Tensor> weight_d) {
+  dy = dy.dim() == 4 ? dy.contiguous(at::MemoryFormat::ChannelsLast) : dy.contiguous();
+  check_act(dy, "dy");
+  check_act(x, "x");
+  check_act(xd, "xd");
+  const int C = (int)x.size(1);
+  const int64_t M = rows_of(x);
+  TORCH_CHECK(dy.sizes() == x.sizes() && xd.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type() &&
+                  xd.scalar_type() == x.scalar_type(),
+              "bn_dual_bwd: dy / x / xd mismatch");
+  TORCH_CHECK(ws.numel() == 7 * (int64_t)C && wsd.numel() == 7 * (int64_t)C, "bn_dual_bwd: 7C workspaces");
+  const uint8_t* mp = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->numel() * 8 >= M * C, "bn_dual_bwd: bit mask size");
+    mp = mask->data_ptr<uint8_t>();
+  }
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor part = at::empty({partial_floats(M, C)}, f32), partd = at::empty({partial_floats(M, C)}, f32);
+  at::Tensor dx = at::empty_like(x), dxd = at::empty_like(xd);
+  at::Tensor dg = at::empty({C}, f32), db = at::empty({C}, f32), dgd = at::empty({C}, f32), dbd = at::empty({C}, f32);
+  auto gp = [](const c10::optional<at::Tensor>& w) -> const float* {
+    return (w.has_value() && w->defined()) ? w->data_ptr<float>() : nullptr;
+  };
+  launch_bn_dual_bwd(dy.data_ptr(), mp, x.data_ptr(), xd.data_ptr(), dx.data_ptr(), dxd.data_ptr(), M, C,
+                     dtype_code(x), gp(weight), gp(weight_d), ws.data_ptr<float>(), wsd.data_ptr<float>(),
+                     part.data_ptr<float>(), partd.data_ptr<float>(), dg.data_ptr<float>(), db.data_ptr<float>(),
+                     dgd.data_ptr<float>(), dbd.data_ptr<float>(), current_stream(x));
+  return {dx, dg, db, dxd, dgd, dbd};
+}
+
 // Returns (dx, dres-or-undefined, dgamma, dbeta). mask_mode (see launch_bn_bwd): 0 no ReLU,
 // 1 recompute the ReLU branch from x, 2 use `mask` from bn_act_fwd, 3 use the saved output `y`.
 std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, c10::optional<at::Tensor> mask,
@@ -589,6 +622,7 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("need_pos") = true);
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pooling backward (gather form)");
   m.def("bn_dual_fwd", &bn_dual_fwd, "training act(BN(x) + BN_d(xd)) in one apply pass (downsample residual)");
+  m.def("bn_dual_bwd", &bn_dual_bwd, "backward of bn_dual_fwd (one dy read for both BatchNorms)");
   m.def("gap_fwd", &gap_fwd, "NHWC global average pooling -> [N, C]");
   m.def("stem_fwd", &stem_fwd, "7x7/s2/p3 stem conv, 3 input channels (space-to-depth + MFMA implicit GEMM, BN-statistics epilogue)");
   m.def("stem_wgrad", &stem_wgrad, "7x7/s2/p3 stem conv weight gradient from the folded input (packed [Cout, 256] layout)");

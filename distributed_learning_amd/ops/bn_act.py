@@ -105,8 +105,8 @@ class _BNAct(torch.autograd.Function):
 class _BNDualAct(torch.autograd.Function):
     """Training-mode ``act(BN(x) + BN_d(xd))``: a residual block's main branch plus its downsample
     shortcut. One apply pass reads both pre-BN tensors (the shortcut BN's output is never written);
-    backward runs the two BN backwards from the same dy and 1-bit ReLU mask (no materialised
-    residual gradient)."""
+    backward: one reduce and one apply pass read dy (+ the 1-bit ReLU mask) once for both BNs and
+    write dx and dxd (no materialised residual gradient)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, xd, weight_d, bias_d, rm, rv, rmd, rvd, momentum, momentum_d, eps, eps_d,
@@ -121,10 +121,7 @@ class _BNDualAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, ws, weight, xd, wsd, weight_d, mask = ctx.saved_tensors
-        C = _ext.require()
-        mode = MASK_BITS if ctx.relu else MASK_NONE
-        dx, _, dg, db = C.bn_act_bwd(dy, None, mask, x, ws, weight, mode, False, None)
-        dxd, _, dgd, dbd = C.bn_act_bwd(dy, None, mask, xd, wsd, weight_d, mode, False, None)
+        dx, dg, db, dxd, dgd, dbd = _ext.require().bn_dual_bwd(dy, mask, x, ws, weight, xd, wsd, weight_d)
         need = ctx.needs_input_grad
         return (dx, dg if need[1] else None, db if need[2] else None, dxd, dgd if need[4] else None,
                 dbd if need[5] else None) + (None,) * 11
