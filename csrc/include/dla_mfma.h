@@ -359,6 +359,11 @@ __device__ __forceinline__ void mainloop_glds(const LA& la, const LB& lb, int kb
     } else {
       vm_wait<0>();
     }
+    // every LDS read this wave issued for tile t-1 has RETURNED before the barrier: the DMA issued
+    // right after it overwrites that stage, and with an L2-hot source (the stem's folded image, the
+    // weights) it can land while a read that was merely issued is still queued in the LDS pipeline
+    // (measured: 2 of 30 stem launches read the new tile without this wait)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // no LDS read of tile t above the barrier
     if (t + NS - 1 < nk) issue(t + NS - 1);

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--bucket_mb", type=float, default=1.0)
+    ap.add_argument("--nodp", action="store_true", help="plain model, no DP wrapper / comm stream (diagnosis)")
     a = ap.parse_args()
     os.environ.setdefault("RANK", "0")
     os.environ.setdefault("WORLD_SIZE", "1")
@@ -48,10 +49,15 @@ def main():
     torch.manual_seed(0)
     model = spec.build().to(dev).to(memory_format=torch.channels_last)
     dnn.bf16_weights(model)
-    red = make_reducer("immediate", "builtin", native=True)
-    w = PipelinedFusedDP(model, red, int(a.bucket_mb * 1024 * 1024), dev)
-    w.sync.executor = NativeStreamExecutor(red.engine, "builtin", passthrough=False)
-    w.sync.passthrough = False
+    if a.nodp:
+        w = model
+        w.sync_gradients = lambda: None
+        w.cleanup = lambda: None
+    else:
+        red = make_reducer("immediate", "builtin", native=True)
+        w = PipelinedFusedDP(model, red, int(a.bucket_mb * 1024 * 1024), dev)
+        w.sync.executor = NativeStreamExecutor(red.engine, "builtin", passthrough=False)
+        w.sync.passthrough = False
     opt = FusedSGD(model.parameters(), lr=0.05, momentum=0.9, master_weights=True)
     data = SyntheticBatches(a.batch, spec.input_shape, spec.num_classes, dev, dtype=torch.bfloat16, seed=3,
                             channels_last=True)
