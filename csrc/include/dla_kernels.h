@@ -155,11 +155,13 @@ enum TileCfg : int {
   kTile64x64 = 3,
   kTile256x128 = 4,
   kTile256x128w4 = 5,
-  kTile128x256w4 = 6
+  kTile128x256w4 = 6,
+  kTile256x64 = 7  // 4 waves stacked along M (64 x 64 wave tiles), 2 blocks / CU; opt-in: measured slower
+                   // than 128x64 / 128x128 at every ResNet-50 shape (profiles/tiles_256x64_4x1waves_ab.jsonl)
 };
 int pick_tile(int64_t M, int N, int tile);
 inline int tile_bm(int cfg) {
-  return cfg == kTile64x64 ? 64 : ((cfg == kTile256x128 || cfg == kTile256x128w4) ? 256 : 128);
+  return cfg == kTile64x64 ? 64 : ((cfg == kTile256x128 || cfg == kTile256x128w4 || cfg == kTile256x64) ? 256 : 128);
 }
 inline int tile_bn(int cfg) {
   return cfg == kTile128x256w4 ? 256

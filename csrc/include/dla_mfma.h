@@ -202,10 +202,15 @@ struct KLoader {
 };
 
 // ---- main loop -----------------------------------------------------------------------------------
+// Waves along N of a block: 2 (and NT/128 along M), or 1 for the 256 x 64 tile, whose 4 waves stack
+// along M so each owns a 64 x 64 wave tile like the 128 x 128 tile (a 2 x 2 layout of a 64-wide tile
+// gives 64 x 32 wave tiles: a third more LDS fragment reads per MFMA).
+__host__ __device__ constexpr int waves_n(int BM, int BN, int NT) { return (BN <= 64 && BM >= 256 && NT == 256) ? 1 : 2; }
+
 template <int BM, int BN, int NT = kThreads>
 struct Acc {
-  static constexpr int kNT = NT, WGM = NT / 128;  // waves along M (2 along N)
-  static constexpr int WM = BM / WGM, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  static constexpr int kNT = NT, WGN = waves_n(BM, BN, NT), WGM = NT / 64 / WGN;  // waves along N / M
+  static constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
   static_assert(TM >= 1 && TN >= 1, "wave tile below one MFMA fragment");
   f32x4_t v[TM][TN];
   __device__ void zero() {
@@ -259,7 +264,7 @@ __device__ __forceinline__ void mainloop(const LA& la, const LB& lb, int kbeg, i
   constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);
   bf16_t* Bs = As + (LA::kKMajor ? GA::kKElems : GA::kRowElems);
-  const int wid = threadIdx.x >> 6, wr = wid >> 1, wc = wid & 1;
+  const int wid = threadIdx.x >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN;
   ushort8_t ra[GA::CH], rb[GB::CH];
   auto gload = [&](int k0) {
 #pragma unroll
@@ -330,7 +335,7 @@ __device__ __forceinline__ void mainloop_glds(const LA& la, const LB& lb, int kb
   constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
   constexpr int SA = BM * kBK, SB = BN * kBK;  // elements per stage
   bf16_t* base = reinterpret_cast<bf16_t*>(smem);
-  const int wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
+  const int wave = threadIdx.x >> 6, wr = wave / AC::WGN, wc = wave % AC::WGN;
   const uint32_t lds0 = lds_addr(smem);
   const uint32_t wofs = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
   const int nk = (kend - kbeg + kBK - 1) / kBK;
@@ -465,7 +470,7 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
   using AC = Acc<BM, BN, NT>;
   constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
   constexpr int LDS_C = BN + 8;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN, fr = lane & 15;
   bf16_t* Cs = reinterpret_cast<bf16_t*>(smem);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -585,7 +590,7 @@ __device__ __forceinline__ void stats_flush(ColStats<BM, BN, NT>& st, float* __r
                                             char* smem) {
   using AC = Acc<BM, BN, NT>;
   constexpr int WN = AC::WN, TN = AC::TN;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN, fr = lane & 15;
   float* red = reinterpret_cast<float*>(smem);  // [WGM wr][BN][2]
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -619,7 +624,7 @@ __device__ __forceinline__ void epilogue_f32(const Acc<BM, BN, NT>& acc, float* 
                                              int m0, int n0) {
   using AC = Acc<BM, BN, NT>;
   constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid >> 1, wc = wid & 1, fr = lane & 15;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN, fr = lane & 15;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll

@@ -481,6 +481,7 @@ void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int
     case kTile256x128: DLA_CFW(256, 128, 512) break;
     case kTile256x128w4: DLA_CF(256, 128) break;
     case kTile128x256w4: DLA_CF(128, 256) break;
+    case kTile256x64: DLA_CF(256, 64) break;
     case kTile128x128: DLA_CF(128, 128) break;
     case kTile128x64: DLA_CF(128, 64) break;
     default: DLA_CF(64, 64) break;
@@ -535,6 +536,7 @@ void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H,
     case kTile256x128: launch_dgrad<256, 128, 512>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile256x128w4: launch_dgrad<256, 128>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile128x256w4: launch_dgrad<128, 256>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
+    case kTile256x64: launch_dgrad<256, 64>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile128x128: launch_dgrad<128, 128>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile128x64: launch_dgrad<128, 64>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     default: launch_dgrad<64, 64>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;

@@ -208,6 +208,7 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
     case kTile256x128: DLA_NT_STW(256, 128, 512) break;
     case kTile256x128w4: DLA_NT_ST(256, 128) break;
     case kTile128x256w4: DLA_NT_ST(128, 256) break;
+    case kTile256x64: DLA_NT_ST(256, 64) break;
     case kTile128x128: DLA_NT_ST(128, 128) break;
     case kTile128x64: DLA_NT_ST(128, 64) break;
     default: DLA_NT_ST(64, 64) break;

@@ -256,7 +256,7 @@ static const void* addend2_ptr(const c10::optional<at::Tensor>& a2, int64_t M, i
 std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::optional<at::Tensor> addend,
                                 bool b_kmajor, int64_t tile, c10::optional<at::Tensor> addend_mask,
                                 c10::optional<at::Tensor> addend2, int64_t H, int64_t W) {
-  TORCH_CHECK(tile >= 0 && tile <= kTile128x256w4, "gemm_nt: tile config 0..6");
+  TORCH_CHECK(tile >= 0 && tile <= kTile256x64, "gemm_nt: tile config 0..7");
   check_mat(A, "A");
   check_mat(B, "B");
   TORCH_CHECK(A.size(1) == B.size(b_kmajor ? 0 : 1), "gemm_nt: K mismatch");
@@ -497,7 +497,7 @@ static void check_conv3(const at::Tensor& x, const at::Tensor& w) {
 
 // 3x3 / pad 1 convolution forward (stride 1 or 2). Returns (y, stats-or-undefined).
 std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, bool stats, int64_t tile) {
-  TORCH_CHECK(tile >= 0 && tile <= kTile128x256w4, "conv3x3: tile config 0..6");
+  TORCH_CHECK(tile >= 0 && tile <= kTile256x64, "conv3x3: tile config 0..7");
   check_conv3(x, w);
   TORCH_CHECK(stride == 1 || stride == 2, "conv3x3: stride 1 or 2");
   const int N = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Cout = (int)w.size(0);
@@ -513,7 +513,7 @@ std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, 
 
 // stride-1 data gradient (+ optional fused addend, same shape as dx)
 at::Tensor conv3x3_dgrad(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> addend, int64_t tile) {
-  TORCH_CHECK(tile >= 0 && tile <= kTile128x256w4, "conv3x3: tile config 0..6");
+  TORCH_CHECK(tile >= 0 && tile <= kTile256x64, "conv3x3: tile config 0..7");
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(dy.dim() == 4 && dy.size(1) == w.size(0), "conv3x3_dgrad: dy/w mismatch");
   const int N = (int)dy.size(0), Cout = (int)w.size(0), Cin = (int)w.size(1), H = (int)dy.size(2), W = (int)dy.size(3);
