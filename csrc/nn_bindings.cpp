@@ -430,7 +430,7 @@ std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor wpk, bool want_stats) 
   const int N = (int)x.size(0), H = (int)x.size(2), W = (int)x.size(3), Cout = (int)wpk.size(0);
   const int OH = (H + 1) / 2, OW = (W + 1) / 2;  // 7x7 / s2 / p3
   const int64_t P = (int64_t)N * OH * OW;
-  TORCH_CHECK((int64_t)N * H * W < (1 << 24) && P < (1 << 24), "stem_fwd: too many pixels for 24-bit index math");
+  TORCH_CHECK(P < (1 << 24), "stem_fwd: too many output pixels for 24-bit index math");
   at::Tensor xs = at::empty({N, OH, OW, 16}, x.options().memory_format(at::MemoryFormat::Contiguous));
   launch_stem_fold(x.data_ptr(), xs.data_ptr(), N, H, W, current_stream(x));
   at::Tensor y = at::empty({N, Cout, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -451,6 +451,7 @@ at::Tensor stem_wgrad(at::Tensor dy, at::Tensor xs, int64_t H, int64_t W, c10::S
   TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "stem_wgrad: fp32/bf16 output");
   const int N = (int)xs.size(0), Cout = (int)dy.size(1);
   TORCH_CHECK(xs.size(1) == (H + 1) / 2 && xs.size(2) == (W + 1) / 2, "stem_wgrad: xs / image size mismatch");
+  TORCH_CHECK((int64_t)N * xs.size(1) * xs.size(2) < (1 << 24), "stem_wgrad: too many output pixels");
   TORCH_CHECK(dy.size(0) == N && dy.size(2) == xs.size(1) && dy.size(3) == xs.size(2), "stem_wgrad: dy shape");
   const int splits = stem_wgrad_splits(N, (int)H, (int)W, Cout);
   at::Tensor part = at::empty({(int64_t)splits * Cout * 256}, xs.options().dtype(at::kFloat));

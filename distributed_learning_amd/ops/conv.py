@@ -359,7 +359,8 @@ def supported_stem(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and x.shape[1] == 3
             and conv.kernel_size == (7, 7) and conv.stride == (2, 2) and conv.padding == (3, 3)
             and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None and conv.out_channels % 64 == 0
-            and x.is_contiguous(memory_format=torch.channels_last) and x.numel() // 3 < (1 << 24))
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[0] * ((x.shape[2] + 1) // 2) * ((x.shape[3] + 1) // 2) < (1 << 24))  # output pixels
 
 
 def stem_pack_weight(w: torch.Tensor) -> torch.Tensor:

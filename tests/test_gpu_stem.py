@@ -14,7 +14,8 @@ def _inputs(cuda, n, h, w, cout=64, seed=0):
     return x, wt
 
 
-@pytest.mark.parametrize("shape", [(2, 224, 224), (3, 37, 29), (1, 8, 8), (4, 64, 96)])
+@pytest.mark.parametrize("shape", [(2, 224, 224), (3, 37, 29), (1, 8, 8), (4, 64, 96),
+                                   (340, 224, 224)])  # > 2^24 input pixels (only output pixels are fastdiv'd)
 def test_stem_fwd_and_stats_match_torch(cuda, shape):
     from distributed_learning_amd.ops import _ext
     from distributed_learning_amd.ops.conv import stem_pack_weight
