@@ -13,6 +13,8 @@ odd channel counts, grouped/dilated/padded convs) uses ``F.conv2d``.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -25,7 +27,8 @@ from .bn_act import bn_link_of as _bn_link_of
 # Off by default: measured on MI355X (scripts/bench_gemm.py dgrad_bn*), reading the BN input in the
 # GEMM epilogue costs about as much as the standalone reduction pass it replaces (the epilogue's
 # loads do not overlap the tile's MFMA work), so the fused step was 0.3 ms slower end to end.
-BN_EPILOGUE = False
+# DLA_BN_EPILOGUE=1 turns it on for A/B runs.
+BN_EPILOGUE = os.environ.get("DLA_BN_EPILOGUE", "0") == "1"
 
 
 def bn_link_of(x):
