@@ -92,6 +92,8 @@ void launch_xent_bwd(const void* logits, const int64_t* target, const float* ws,
 // x/res/y/dy/dx/dres: [M, C] row-major (channels_last activations), C % 8 == 0, 16-byte aligned.
 // ws: 7*C floats (mean, invstd, scale, shift | k1, m1, k2); part: bn_partial_floats(M, C) floats.
 void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks);  // reduction passes: 1024
+// rows of fp32 [rows][C][2] scratch launch_bn_fwd's `part` needs to fold ext_nrb epilogue partials (0: none)
+int bn_fold_groups(int ext_nrb);
 void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int dtype, const float* gamma,
                    const float* beta, float eps, float momentum, float* running_mean, float* running_var, float* ws,
                    float* part, bool relu, bool training, hipStream_t stream, const float* ext_part = nullptr,

@@ -176,6 +176,52 @@ __device__ __forceinline__ bool reduce_partials(const float* __restrict__ part, 
   return true;
 }
 
+// First level of the reduction of GEMM-epilogue statistics ([nrb][C][2], one row per 128-row output
+// tile: 12,544 rows for a 56x56 layer at batch 512). Lanes own consecutive channels, so each wave's
+// load is one 512-byte run instead of the 64 scattered lines of the lane-per-row layout of
+// reduce_partials; block (cx, g) folds rows [g * kFoldRows, +kFoldRows) into out[g][C][2] with its
+// 4 waves taking every 4th row and 8 loads in flight per lane. Fixed order -> bitwise reproducible.
+constexpr int kFoldRows = 128;
+
+int bn_fold_groups(int nrb) { return nrb > 1024 ? (nrb + kFoldRows - 1) / kFoldRows : 0; }
+
+__global__ __launch_bounds__(256) void bn_partials_fold_kernel(const float* __restrict__ part, int nrb, int C,
+                                                               float* __restrict__ out) {
+  __shared__ float red[4][64][2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * kFoldRows, r1 = min(nrb, r0 + kFoldRows);
+  float s[8], q[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s[u] = q[u] = 0.f;
+  if (c < C) {
+    const float2* p2 = reinterpret_cast<const float2*>(part);
+    int r = r0 + wave;
+    for (; r + 28 < r1; r += 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float2 v = p2[(int64_t)(r + 4 * u) * C + c];
+        s[u] += v.x;
+        q[u] += v.y;
+      }
+    }
+    for (; r < r1; r += 4) {
+      const float2 v = p2[(int64_t)r * C + c];
+      s[0] += v.x;
+      q[0] += v.y;
+    }
+  }
+  red[wave][lane][0] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  red[wave][lane][1] = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+  __syncthreads();
+  if (wave == 0 && c < C) {
+    float2 o;
+    o.x = (red[0][lane][0] + red[1][lane][0]) + (red[2][lane][0] + red[3][lane][0]);
+    o.y = (red[0][lane][1] + red[1][lane][1]) + (red[2][lane][1] + red[3][lane][1]);
+    reinterpret_cast<float2*>(out)[(int64_t)blockIdx.y * C + c] = o;
+  }
+}
+
 template <int WPC>
 __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __restrict__ x0, int x_is_bf16,
                                                                 const float* __restrict__ part, int nrb, int64_t M,
@@ -722,10 +768,13 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
   bn_geometry(M, C, &tpr, &nrb, &nct);
   if (training && ext_part) {
     // statistics already produced by the conv GEMM epilogue (unshifted per-row-block partials)
-    if (ext_nrb > 1024)
-      hipLaunchKernelGGL(bn_stats_finalize_kernel<4>, dim3(C), dim3(256), 0, stream, nullptr, 0, ext_part, ext_nrb, M,
+    // many tile rows: fold them coalesced into bn_fold_groups() rows of `part` first
+    if (const int g = bn_fold_groups(ext_nrb)) {
+      hipLaunchKernelGGL(bn_partials_fold_kernel, dim3((C + 63) / 64, g), dim3(256), 0, stream, ext_part, ext_nrb, C,
+                         part);
+      hipLaunchKernelGGL(bn_stats_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, nullptr, 0, part, g, M,
                          C, gamma, beta, eps, momentum, running_mean, running_var, ws);
-    else
+    } else
       hipLaunchKernelGGL(bn_stats_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, nullptr, 0, ext_part,
                          ext_nrb, M, C, gamma, beta, eps, momentum, running_mean, running_var, ws);
   } else if (training) {

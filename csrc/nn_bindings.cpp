@@ -20,6 +20,11 @@ static void check_act(const at::Tensor& t, const char* what) {
 
 static int64_t rows_of(const at::Tensor& t) { return t.numel() / t.size(1); }
 
+// launch_bn_fwd scratch for GEMM-epilogue statistics [rows][C][2]: the folded rows (>= 1 float)
+static int64_t ext_part_floats(const c10::optional<at::Tensor>& st, int C) {
+  return std::max<int64_t>(1, (int64_t)bn_fold_groups((int)st->size(0)) * C * 2);
+}
+
 static int64_t partial_floats(int64_t M, int C) {
   int tpr, nrb, nct;
   bn_geometry(M, C, &tpr, &nrb, &nct, 1024);
@@ -69,7 +74,7 @@ std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> resid
                     stats->size(1) == C && stats->size(2) == 2,
                 "stats must be fp32 [row_blocks, C, 2] partials");
   }
-  at::Tensor part = at::empty({(training && !ext) ? partial_floats(M, C) : 1}, f32);
+  at::Tensor part = at::empty({(training && !ext) ? partial_floats(M, C) : ext ? ext_part_floats(stats, C) : 1}, f32);
   at::Tensor y = at::empty_like(x);
   at::Tensor mask;
   if (training && relu && res) mask = at::empty({(M * C + 7) / 8}, x.options().dtype(at::kByte));
@@ -111,7 +116,7 @@ std::vector<at::Tensor> bn_dual_fwd(at::Tensor x, at::Tensor xd, c10::optional<a
       TORCH_CHECK(st->scalar_type() == at::kFloat && st->is_contiguous() && st->dim() == 3 && st->size(1) == C &&
                       st->size(2) == 2,
                   "stats must be fp32 [row_blocks, C, 2] partials");
-    at::Tensor part = at::empty({ext ? 1 : partial_floats(M, C)}, f32);
+    at::Tensor part = at::empty({ext ? ext_part_floats(st, C) : partial_floats(M, C)}, f32);
     launch_bn_fwd(in.data_ptr(), nullptr, nullptr, M, C, dtype_code(in), fptr(g), fptr(b), (float)ep, (float)mom,
                   fptr(rm), fptr(rv), ws.data_ptr<float>(), part.data_ptr<float>(), relu, true, current_stream(in),
                   ext ? st->data_ptr<float>() : nullptr, ext ? (int)st->size(0) : 0);
@@ -345,7 +350,7 @@ std::vector<at::Tensor> bn_relu_maxpool_fwd(at::Tensor x, c10::optional<at::Tens
                     stats->size(1) == C && stats->size(2) == 2,
                 "stats must be fp32 [row_blocks, C, 2] partials");
   }
-  at::Tensor part = at::empty({ext ? 1 : partial_floats(M, C)}, f32);
+  at::Tensor part = at::empty({ext ? ext_part_floats(stats, C) : partial_floats(M, C)}, f32);
   launch_bn_fwd(x.data_ptr(), nullptr, nullptr, M, C, kBF16, fptr(weight), fptr(bias), (float)eps, (float)momentum,
                 fptr(running_mean), fptr(running_var), ws.data_ptr<float>(), part.data_ptr<float>(), true, true,
                 current_stream(x), ext ? stats->data_ptr<float>() : nullptr, ext ? (int)stats->size(0) : 0);

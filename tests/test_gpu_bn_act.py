@@ -182,3 +182,30 @@ def test_bn_act_mask_modes_agree(cuda, use_res):
     for a, g in zip(ref, got):
         if a is not None:
             assert torch.equal(a, g)
+
+
+@pytest.mark.parametrize("rows,C", [(128 * 1025 + 7, 64), (128 * 3001, 96), (128 * 600, 256)])
+def test_bn_fwd_external_stats_fold(cuda, rows, C):
+    """GEMM-epilogue statistics ([tiles, C, 2] per-128-row partials): > 1024 tiles take the coalesced
+    fold pass before the finalize; batch mean / variance / output vs fp64 PyTorch."""
+    from distributed_learning_amd.ops import _ext
+
+    Cx = _ext.require()
+    torch.manual_seed(0)
+    x = (torch.randn(rows, C, device=cuda) * 2 + 0.5).to(torch.bfloat16)
+    xf = x.double()
+    tiles = (rows + 127) // 128
+    pad = torch.zeros(tiles * 128, C, device=cuda, dtype=torch.float64)
+    pad[:rows] = xf
+    t = pad.view(tiles, 128, C)
+    stats = torch.stack([t.sum(1), (t * t).sum(1)], -1).float().contiguous()
+    w = torch.rand(C, device=cuda) + 0.5
+    b = torch.randn(C, device=cuda)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    y, ws, _ = Cx.bn_act_fwd(x, None, w, b, rm, rv, True, 0.1, 1e-5, False, stats)
+    mean, var = xf.mean(0), xf.var(0, unbiased=False)
+    torch.testing.assert_close(ws[:C].double(), mean, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(ws[C:2 * C].double(), (var + 1e-5).rsqrt(), rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(rm.double(), 0.1 * mean, rtol=1e-4, atol=1e-4)
+    ref = (xf - mean) * (var + 1e-5).rsqrt() * w.double() + b.double()
+    torch.testing.assert_close(y.double(), ref, rtol=2e-2, atol=2e-2)
