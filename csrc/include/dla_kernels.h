@@ -91,7 +91,9 @@ void launch_xent_bwd(const void* logits, const int64_t* target, const float* ws,
 // ---- fused BatchNorm + residual + ReLU, NHWC (bn_act.hip) ------------------------------------
 // x/res/y/dy/dx/dres: [M, C] row-major (channels_last activations), C % 8 == 0, 16-byte aligned.
 // ws: 7*C floats (mean, invstd, scale, shift | k1, m1, k2); part: bn_partial_floats(M, C) floats.
-void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks);  // reduction passes: 1024
+void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks);  // <= 0: reduction passes
+// fp32 scratch floats of one reduction pass's partials [rows][C][2] plus their fold rows
+int64_t bn_partial_floats(int64_t M, int C);
 // rows of fp32 [rows][C][2] scratch launch_bn_fwd's `part` needs to fold ext_nrb epilogue partials (0: none)
 int bn_fold_groups(int ext_nrb);
 void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int dtype, const float* gamma,

@@ -222,6 +222,23 @@ __global__ __launch_bounds__(256) void bn_partials_fold_kernel(const float* __re
   }
 }
 
+// Partials the finalize reads: `part` itself (<= 1024 rows), or its coalesced fold written to the
+// scratch rows right after it (part + nrb * C * 2; bn_partial_floats sizes for both).
+static const float* bn_fold_rows(const float* part, int* nrb, int C, hipStream_t stream) {
+  const int g = bn_fold_groups(*nrb);
+  if (!g) return part;
+  float* out = const_cast<float*>(part) + (int64_t)*nrb * C * 2;
+  hipLaunchKernelGGL(bn_partials_fold_kernel, dim3((C + 63) / 64, g), dim3(256), 0, stream, part, *nrb, C, out);
+  *nrb = g;
+  return out;
+}
+
+int64_t bn_partial_floats(int64_t M, int C) {
+  int tpr, nrb, nct;
+  bn_geometry(M, C, &tpr, &nrb, &nct, 0);
+  return ((int64_t)nrb + bn_fold_groups(nrb)) * C * 2;
+}
+
 template <int WPC>
 __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __restrict__ x0, int x_is_bf16,
                                                                 const float* __restrict__ part, int nrb, int64_t M,
@@ -744,7 +761,20 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_dual_apply_kernel(const T* 
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
-void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks = kRedBlocks) {
+// Block target of the reduction passes (statistics / backward reduce): kRedBlocks, or
+// DLA_BN_RED_BLOCKS for A/B runs. Above 1024 partial rows the finalize reads them through
+// bn_partials_fold_kernel (bn_fold_rows).
+int bn_red_blocks() {
+  static const int v = [] {
+    const char* e = std::getenv("DLA_BN_RED_BLOCKS");
+    const int b = e ? std::atoi(e) : 0;
+    return b > 0 ? b : kRedBlocks;
+  }();
+  return v;
+}
+
+void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks) {
+  if (target_blocks <= 0) target_blocks = bn_red_blocks();
   int ct = C;
   if (ct > 512) ct = 512;
   while (C % ct) ct -= 8;  // C % 8 == 0 guaranteed by the caller
@@ -765,7 +795,7 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
                    float* ws, float* part, bool relu, bool training, hipStream_t stream, const float* ext_part,
                    int ext_nrb, uint8_t* mask) {
   int tpr, nrb, nct;
-  bn_geometry(M, C, &tpr, &nrb, &nct);
+  bn_geometry(M, C, &tpr, &nrb, &nct, 0);
   if (training && ext_part) {
     // statistics already produced by the conv GEMM epilogue (unshifted per-row-block partials)
     // many tile rows: fold them coalesced into bn_fold_groups() rows of `part` first
@@ -785,7 +815,8 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
     else
       hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nct, nrb), dim3(kBNThreads), lds, stream, (const float*)x, M, C,
                          nrb, tpr, part);
-    hipLaunchKernelGGL(bn_stats_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, x, dtype == kBF16, part,
+    const float* fp = bn_fold_rows(part, &nrb, C, stream);
+    hipLaunchKernelGGL(bn_stats_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, x, dtype == kBF16, fp,
                        nrb, M, C, gamma, beta, eps, momentum, running_mean, running_var, ws);
   }
   if (!y) return;  // statistics only (the fused BN+ReLU+max-pool applies them itself)
@@ -823,7 +854,7 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
                    int64_t M, int C, int dtype, const float* gamma, float* ws, float* part, float* dgamma,
                    float* dbeta, int mask_mode, hipStream_t stream, const float* ext_part, int ext_nrb) {
   int tpr, nrb, nct;
-  bn_geometry(M, C, &tpr, &nrb, &nct);
+  bn_geometry(M, C, &tpr, &nrb, &nct, 0);
   if (ext_part) {
     // reduction pass already fused into the producer GEMM's epilogue
     if (ext_nrb > 1024)
@@ -847,7 +878,8 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
   if (dtype == kBF16) { DLA_BN_RED_ALL(bf16_t) } else { DLA_BN_RED_ALL(float) }
 #undef DLA_BN_RED_ALL
 #undef DLA_BN_RED
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, part, nrb, M, C, gamma, ws,
+  const float* fp = bn_fold_rows(part, &nrb, C, stream);  // before the launch reads nrb
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, fp, nrb, M, C, gamma, ws,
                      dgamma, dbeta);
   }
   int atpr, anrb, anct;
@@ -946,12 +978,13 @@ void launch_bn_relu_maxpool_bwd(const void* dy_pool, const uint8_t* pos, const v
   PoolDy pd{(const bf16_t*)dy_pool, pos, H, W, OH, OW, k, s, p, mm::make_fastdiv((uint32_t)W),
             mm::make_fastdiv((uint32_t)H)};
   int tpr, nrb, nct;
-  bn_geometry(M, C, &tpr, &nrb, &nct);
+  bn_geometry(M, C, &tpr, &nrb, &nct, 0);
   const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16_t, kMaskRecomp, PoolDy>), dim3(nct, nrb), dim3(kBNThreads), lds, stream,
                      pd, (const bf16_t*)nullptr, (const uint8_t*)nullptr, (const bf16_t*)x, (const float*)ws, M, C, nrb,
                      tpr, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, part, nrb, M, C, gamma, ws,
+  const float* fp = bn_fold_rows(part, &nrb, C, stream);  // before the launch reads nrb
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, fp, nrb, M, C, gamma, ws,
                      dgamma, dbeta);
   int atpr, anrb, anct;
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
@@ -965,7 +998,7 @@ void launch_bn_dual_bwd(const void* dy, const uint8_t* mask, const void* x, cons
                         float* part, float* partd, float* dgamma, float* dbeta, float* dgamma_d, float* dbeta_d,
                         hipStream_t stream) {
   int tpr, nrb, nct;
-  bn_geometry(M, C, &tpr, &nrb, &nct);
+  bn_geometry(M, C, &tpr, &nrb, &nct, 0);
   const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
   const bool bits = mask != nullptr;
 #define DLA_DUAL_RED(T, K)                                                                                        \
@@ -977,9 +1010,12 @@ void launch_bn_dual_bwd(const void* dy, const uint8_t* mask, const void* x, cons
     if (bits) DLA_DUAL_RED(float, kMaskBits); else DLA_DUAL_RED(float, kMaskNone);
   }
 #undef DLA_DUAL_RED
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, part, nrb, M, C, gamma, ws,
+  int fr = nrb, frd = nrb;
+  const float* fp = bn_fold_rows(part, &fr, C, stream);
+  const float* fpd = bn_fold_rows(partd, &frd, C, stream);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, fp, fr, M, C, gamma, ws,
                      dgamma, dbeta);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, partd, nrb, M, C, gamma_d,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, fpd, frd, M, C, gamma_d,
                      wsd, dgamma_d, dbeta_d);
   int atpr, anrb, anct;
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);

@@ -25,11 +25,7 @@ static int64_t ext_part_floats(const c10::optional<at::Tensor>& st, int C) {
   return std::max<int64_t>(1, (int64_t)bn_fold_groups((int)st->size(0)) * C * 2);
 }
 
-static int64_t partial_floats(int64_t M, int C) {
-  int tpr, nrb, nct;
-  bn_geometry(M, C, &tpr, &nrb, &nct, 1024);
-  return (int64_t)nrb * C * 2;
-}
+static int64_t partial_floats(int64_t M, int C) { return bn_partial_floats(M, C); }
 
 // Returns (y, ws, mask). ws (7C fp32) carries mean/invstd/scale/shift for backward; mask (uint8,
 // one bit per element) is only produced for ReLU after a residual add in training mode.
