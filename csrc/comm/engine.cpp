@@ -1,4 +1,5 @@
-// CommEngine: native RCCL gradient all-reduce engine (one per process group, one GPU per process).
+// CommEngine: native RCCL gradient all-reduce engine (one per process group, one GPU per process),
+// plus the single-process virtual-rank executor that runs the same schedules on one GPU.
 //
 // Replaces the reference's Python collective layer:
 //   * ring_allreduce        /root/reference/src/allreduce.py:45-98   (Gloo isend/recv, CPU buffers)
@@ -6,41 +7,51 @@
 //   * central_allreduce     /root/reference/src/allreduce.py:9-43
 //   * built_in_allreduce    /root/reference/src/allreduce.py:5-7
 //   * ReduceImmediatelly    /root/reference/src/reducers.py:6-19 (put = reduce in the send thread)
+//   * NodeAgreggateReducerCPU.pump /root/reference/src/reducers.py:38-69 (2-step, node sum + inter ring)
 // and the OurDist send/receive threads (/root/reference/src/ourdist.py:102-132): instead of two
 // Python threads and queues, every bucket becomes a short sequence on a dedicated high-priority
-// HIP stream: wait(grad-ready event) -> [pack kernel] -> collective -> [unpack kernel] -> record
-// done event. The compute stream joins on the last done event in sync_gradients(); the CPU never
-// blocks on communication.
+// HIP stream: wait(grad-ready event) -> [gather kernel] -> collective Plan -> record done event.
+// The compute stream joins on the comm stream in sync_gradients(); the CPU never blocks on
+// communication.
 //
-// Algorithms (all average in place when `average`):
-//   BUILTIN  ncclAllReduce(ncclAvg/ncclSum) — RCCL chooses its own channels over xGMI.
-//   RING     reference ring schedule (reduce-scatter then all-gather, N-1 steps each) on
-//            ncclSend/ncclRecv, split over C channels; channel c walks its own ring order, so with
-//            7 edge-disjoint Hamiltonian rings every xGMI link of an 8-GPU node carries 1/7 of the
-//            bucket concurrently. C = 1 is exactly the reference algorithm.
-//   DIRECT   two-shot over all peers: grouped P2P scatter of chunk j to peer j, one k-way reduce
-//            kernel, grouped P2P all-gather. 2 network phases, all 7 links busy in both.
-//   CENTRAL  parameter server: root receives N-1 full copies, one k-way reduce kernel, sends back.
-//   RSAG     ncclReduceScatter + ncclAllGather (RCCL's native two-shot).
+// Schedules are Plans (plan.h): built once per (algorithm, bucket size), cached, replayed. The
+// engine executes a Plan's steps as RCCL groups of ncclSend/ncclRecv followed by the reduce
+// kernel (reduce.hip), or as RCCL collectives on the world / intra-node / inter-node
+// communicators (ncclCommSplit). VirtualComm runs the Plans of N ranks in lockstep on one GPU
+// with hipMemcpyAsync as the links (vexec.h), so every algorithm's multi-rank path executes and
+// is checked on a one-GPU box.
+//
+// Failure hygiene: synchronize() polls the stream and ncclCommGetAsyncError
+// with a deadline (DLA_COMM_TIMEOUT_S, default 600 s) and aborts the communicators
+// (ncclCommAbort) on error or timeout instead of blocking forever; the destructor never waits
+// unboundedly on a comm stream whose peer may be dead.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPCachingAllocator.h>
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
-#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "dla_bindings.h"
 #include "dla_kernels.h"
 #include "dla_tables.h"
+#include "plan.h"
+#include "vexec.h"
 
 namespace dla {
+
+using comm::Plan;
+using comm::Topology;
 
 #define DLA_NCCL_CHECK(expr)                                                                  \
   do {                                                                                        \
@@ -60,10 +71,8 @@ namespace dla {
     }                                                                                        \
   } while (0)
 
-enum Algo : int { kBuiltin = 0, kRing = 1, kDirect = 2, kCentral = 3, kRsAg = 4 };
-
-static ncclDataType_t nccl_dtype(const at::Tensor& t) {
-  switch (t.scalar_type()) {
+static ncclDataType_t nccl_dtype_of(at::ScalarType t) {
+  switch (t) {
     case at::kFloat: return ncclFloat32;
     case at::kBFloat16: return ncclBfloat16;
     case at::kHalf: return ncclFloat16;
@@ -71,15 +80,47 @@ static ncclDataType_t nccl_dtype(const at::Tensor& t) {
     case at::kLong: return ncclInt64;
     case at::kInt: return ncclInt32;
     case at::kByte: return ncclUint8;
-    default: TORCH_CHECK(false, "CommEngine: unsupported dtype ", t.scalar_type());
+    default: TORCH_CHECK(false, "CommEngine: unsupported dtype ", t);
   }
   return ncclFloat32;
 }
 
+static Topology make_topology(int rank, int world, std::vector<std::vector<int>> rings, int local_size,
+                              std::vector<std::vector<int>> local_rings, std::vector<std::vector<int>> node_rings) {
+  Topology t;
+  t.world = world;
+  t.rank = rank;
+  t.local_size = (local_size <= 0 || local_size > world) ? world : local_size;
+  t.rings = std::move(rings);
+  t.local_rings = std::move(local_rings);
+  t.node_rings = std::move(node_rings);
+  try {
+    t.validate();
+  } catch (const std::exception& e) {
+    TORCH_CHECK(false, e.what());
+  }
+  return t;
+}
+
+// Plans are float-agnostic; these algorithms need the reduce kernel (fp32 / bf16 only).
+static bool needs_reduce_kernel(int algo) {
+  return algo == comm::kRing || algo == comm::kDirect || algo == comm::kCentral || algo == comm::kHierRing;
+}
+
+static double comm_timeout_s() {
+  const char* e = std::getenv("DLA_COMM_TIMEOUT_S");
+  return e ? std::atof(e) : 600.0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// CommEngine
+// ---------------------------------------------------------------------------------------------
 class CommEngine {
  public:
-  CommEngine(int rank, int world, pybind11::bytes unique_id, int device, std::vector<std::vector<int>> rings)
-      : rank_(rank), world_(world), device_(device), rings_(std::move(rings)) {
+  CommEngine(int rank, int world, pybind11::bytes unique_id, int device, std::vector<std::vector<int>> rings,
+             int local_size, std::vector<std::vector<int>> local_rings, std::vector<std::vector<int>> node_rings)
+      : device_(device),
+        topo_(make_topology(rank, world, std::move(rings), local_size, std::move(local_rings), std::move(node_rings))) {
     std::string id = unique_id;
     TORCH_CHECK(id.size() == sizeof(ncclUniqueId), "CommEngine: bad unique id size");
     std::memcpy(&uid_, id.data(), sizeof(ncclUniqueId));
@@ -88,29 +129,31 @@ class CommEngine {
     stream_ = std::make_unique<c10::hip::HIPStream>(c10::hip::getStreamFromPool(/*isHighPriority=*/true, device_));
     {
       pybind11::gil_scoped_release nogil;
-      DLA_NCCL_CHECK(ncclCommInitRank(&comm_, world_, uid_, rank_));
-    }
-    if (rings_.empty()) {
-      std::vector<int> r(world_);
-      for (int i = 0; i < world_; ++i) r[i] = i;
-      rings_.push_back(r);
-    }
-    for (auto& r : rings_) {
-      TORCH_CHECK((int)r.size() == world_, "CommEngine: ring order must list every rank once");
-      std::vector<int> pos(world_, -1);
-      for (int i = 0; i < world_; ++i) {
-        TORCH_CHECK(r[i] >= 0 && r[i] < world_ && pos[r[i]] < 0, "CommEngine: ring is not a permutation");
-        pos[r[i]] = i;
+      DLA_NCCL_CHECK(ncclCommInitRank(&comm_, world, uid_, rank));
+      const int L = topo_.L(), K = topo_.nodes();
+      // 2-step sub-communicators: ranks of one node (colour = node) and ranks with the same
+      // local index on every node (colour = local index). Collective over the world comm.
+      if (L > 1 && K > 1) {
+        DLA_NCCL_CHECK(ncclCommSplit(comm_, rank / L, rank % L, &intra_, nullptr));
+        DLA_NCCL_CHECK(ncclCommSplit(comm_, rank % L, rank / L, &inter_, nullptr));
       }
-      ring_pos_.push_back(pos);
     }
     DLA_HIP_THROW(hipEventCreateWithFlags(&last_done_, hipEventDisableTiming));
   }
 
   ~CommEngine() {
-    if (comm_) {
-      hipStreamSynchronize(stream_->stream());
-      ncclCommDestroy(comm_);
+    try {
+      if (!aborted_ && comm_) {
+        // bounded wait: a dead peer must not turn teardown into a hang
+        if (!wait_stream(std::min(comm_timeout_s(), 60.0), /*throw_on_fail=*/false)) abort_comms();
+      }
+    } catch (...) {
+      abort_comms();
+    }
+    if (!aborted_) {
+      if (inter_) ncclCommDestroy(inter_);
+      if (intra_) ncclCommDestroy(intra_);
+      if (comm_) ncclCommDestroy(comm_);
     }
     for (auto& e : timing_events_) hipEventDestroy(e);
     for (auto& e : ready_pool_) hipEventDestroy(e);
@@ -123,14 +166,16 @@ class CommEngine {
     return pybind11::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
   }
 
-  int rank() const { return rank_; }
-  int world() const { return world_; }
-  int num_rings() const { return (int)rings_.size(); }
+  int rank() const { return topo_.rank; }
+  int world() const { return topo_.world; }
+  int local_size() const { return topo_.L(); }
+  int num_rings() const { return (int)std::max<size_t>(1, topo_.rings.size()); }
+  void set_accum_fp32(bool on) { accum_fp32_ = on; }
+  bool accum_fp32() const { return accum_fp32_; }
 
   // ---------------------------------------------------------------------------------------
   // Stream plumbing
   // ---------------------------------------------------------------------------------------
-  // Make the comm stream wait for everything already queued on the caller's current stream.
   void join_current() {
     hipStream_t cur = c10::hip::getCurrentHIPStream(device_).stream();
     hipEvent_t ev = next_ready_event();
@@ -138,19 +183,43 @@ class CommEngine {
     DLA_HIP_THROW(hipStreamWaitEvent(stream_->stream(), ev, 0));
   }
 
-  // Make the caller's current stream wait for all communication enqueued so far.
   void wait_on_current() {
     hipStream_t cur = c10::hip::getCurrentHIPStream(device_).stream();
     DLA_HIP_THROW(hipEventRecord(last_done_, stream_->stream()));
     DLA_HIP_THROW(hipStreamWaitEvent(cur, last_done_, 0));
   }
 
+  // Blocks until the comm stream drained; polls RCCL's async error state and aborts the
+  // communicators on error or after the deadline.
   void synchronize() {
     pybind11::gil_scoped_release nogil;
-    DLA_HIP_THROW(hipStreamSynchronize(stream_->stream()));
+    wait_stream(comm_timeout_s(), /*throw_on_fail=*/true);
   }
 
+  // Current RCCL async error state of any communicator ("" = healthy).
+  std::string async_error() {
+    for (ncclComm_t c : {comm_, intra_, inter_}) {
+      if (!c) continue;
+      ncclResult_t r = ncclSuccess;
+      if (ncclCommGetAsyncError(c, &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
+      if (r != ncclSuccess && r != ncclInProgress) return ncclGetErrorString(r);
+    }
+    return "";
+  }
+
+  void abort() { abort_comms(); }
+  bool aborted() const { return aborted_; }
+
   uintptr_t stream_handle() const { return reinterpret_cast<uintptr_t>(stream_->stream()); }
+
+  // Build (and cache) the plans of every bucket size up front and size the scratch buffer for the
+  // largest, so no allocation ever happens mid-backward or inside a HIP-graph capture.
+  void reserve(int algo, std::vector<int64_t> sizes, int dtype) {
+    c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
+    size_t need = 0;
+    for (int64_t n : sizes) need = std::max(need, scratch_bytes(plan_for(algo, n), n, dtype));
+    ensure_scratch(need);
+  }
 
   // ---------------------------------------------------------------------------------------
   // Collectives. Each call enqueues onto the comm stream after joining the caller's stream.
@@ -160,7 +229,7 @@ class CommEngine {
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
     join_current();
     pybind11::gil_scoped_release nogil;
-    timed([&] { allreduce_on_stream(flat, algo, average); });
+    timed([&] { allreduce_on_stream(flat, algo, average, nullptr, nullptr); });
   }
 
   // Fused bucket path: [pack grads] -> all-reduce -> [unpack], all on the comm stream.
@@ -173,12 +242,13 @@ class CommEngine {
     pybind11::gil_scoped_release nogil;
     hipStream_t s = stream_->stream();
     if (table) table->pack_on(flat, pack_scale, s);
-    timed([&] { allreduce_on_stream(flat, algo, average); });
+    timed([&] { allreduce_on_stream(flat, algo, average, nullptr, nullptr); });
     if (table) table->unpack_on(flat, unpack_scale, s);
   }
 
   // Bucket path for autograd-owned gradients: gather `grads` into `flat` at `offsets` on the comm
   // stream (by-value list launches, no per-step table upload), then all-reduce `flat` in place.
+  // With accum_fp32 and a bf16 bucket the gather writes straight into the fp32 staging buffer.
   // The caller keeps `grads` alive until the compute stream has joined the comm stream.
   void bucket_allreduce_list(at::Tensor flat, int algo, bool average, std::vector<at::Tensor> grads,
                              std::vector<int64_t> offsets) {
@@ -186,9 +256,7 @@ class CommEngine {
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
     join_current();
     pybind11::gil_scoped_release nogil;
-    hipStream_t s = stream_->stream();
-    pack_tensors_on(grads, offsets, flat, 1.f, s);
-    timed([&] { allreduce_on_stream(flat, algo, average); });
+    timed([&] { allreduce_on_stream(flat, algo, average, &grads, &offsets); });
   }
 
   void broadcast(at::Tensor t, int root) {
@@ -196,28 +264,31 @@ class CommEngine {
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
     join_current();
     pybind11::gil_scoped_release nogil;
-    DLA_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), root, comm_, stream_->stream()));
+    DLA_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype_of(t.scalar_type()), root, comm_,
+                                 stream_->stream()));
   }
 
   void allgather(at::Tensor out, at::Tensor in) {
     check(out);
     check(in);
-    TORCH_CHECK(out.numel() == in.numel() * world_, "allgather: out must hold world * in elements");
+    TORCH_CHECK(out.numel() == in.numel() * topo_.world, "allgather: out must hold world * in elements");
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
     join_current();
     pybind11::gil_scoped_release nogil;
-    DLA_NCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype(in), comm_, stream_->stream()));
+    DLA_NCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype_of(in.scalar_type()), comm_,
+                                 stream_->stream()));
   }
+
+  std::string describe_plan(int algo, int64_t n) { return comm::describe(plan_for(algo, n)); }
 
   // ---------------------------------------------------------------------------------------
   // Comm-stream timing (true communication ms, SURVEY.md §7.3 hard part 6).
   // ---------------------------------------------------------------------------------------
   void set_timing(bool on) { timing_ = on; }
-  // Returns the summed elapsed ms of all timed collectives since the last call, then resets.
   double consume_comm_ms() {
     pybind11::gil_scoped_release nogil;
     double total = 0.0;
-    DLA_HIP_THROW(hipStreamSynchronize(stream_->stream()));
+    wait_stream(comm_timeout_s(), /*throw_on_fail=*/true);
     for (size_t i = 0; i + 1 < used_timing_; i += 2) {
       float ms = 0.f;
       DLA_HIP_THROW(hipEventElapsedTime(&ms, timing_events_[i], timing_events_[i + 1]));
@@ -229,8 +300,50 @@ class CommEngine {
 
  private:
   void check(const at::Tensor& t) {
+    TORCH_CHECK(!aborted_, "CommEngine: communicator was aborted after an error");
     TORCH_CHECK(t.is_cuda() && t.device().index() == device_, "CommEngine: tensor must live on cuda:", device_);
     TORCH_CHECK(t.is_contiguous(), "CommEngine: tensor must be contiguous");
+  }
+
+  bool wait_stream(double timeout_s, bool throw_on_fail) {
+    if (aborted_) {
+      if (throw_on_fail) throw std::runtime_error("CommEngine: communicator was aborted after an error");
+      return false;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    int spins = 0;
+    while (true) {
+      hipError_t q = hipStreamQuery(stream_->stream());
+      if (q == hipSuccess) return true;
+      if (q != hipErrorNotReady) {
+        abort_comms();
+        if (throw_on_fail) throw std::runtime_error(std::string("CommEngine: comm stream failed: ") + hipGetErrorString(q));
+        return false;
+      }
+      std::string err = async_error();
+      if (!err.empty()) {
+        abort_comms();
+        if (throw_on_fail) throw std::runtime_error("CommEngine: RCCL async error: " + err + " (communicators aborted)");
+        return false;
+      }
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > timeout_s) {
+        abort_comms();
+        if (throw_on_fail)
+          throw std::runtime_error("CommEngine: communication did not complete within " + std::to_string(timeout_s) +
+                                   " s (peer failure?); communicators aborted");
+        return false;
+      }
+      if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(spins > 4096 ? 1000 : 20));
+    }
+  }
+
+  void abort_comms() {
+    if (aborted_) return;
+    aborted_ = true;
+    if (inter_) ncclCommAbort(inter_);
+    if (intra_) ncclCommAbort(intra_);
+    if (comm_) ncclCommAbort(comm_);
   }
 
   hipEvent_t next_ready_event() {
@@ -263,222 +376,147 @@ class CommEngine {
     used_timing_ += 2;
   }
 
-  void* scratch(size_t bytes) {
-    if (scratch_.defined() && (size_t)scratch_.numel() >= bytes) return scratch_.data_ptr();
-    // Grow geometrically; the old buffer may still be in use by queued work, so keep the
-    // allocator informed through record_stream semantics: we simply keep the previous buffer
-    // alive until the stream drains.
-    if (scratch_.defined()) {
-      DLA_HIP_THROW(hipStreamSynchronize(stream_->stream()));
+  const Plan& plan_for(int algo, int64_t n) {
+    auto key = std::make_pair(algo, n);
+    auto it = plans_.find(key);
+    if (it != plans_.end()) return it->second;
+    TORCH_CHECK(algo >= comm::kBuiltin && algo <= comm::kHierColl, "CommEngine: unknown algorithm ", algo);
+    Plan p;
+    try {
+      // plans are built for summation; the average is folded into the last reduce of each phase
+      p = comm::build_plan(algo, topo_, n, 1.f / (float)topo_.world);
+    } catch (const std::exception& e) {
+      TORCH_CHECK(false, e.what());
     }
-    size_t want = std::max(bytes, (size_t)(scratch_.defined() ? scratch_.numel() * 2 : (64 << 20)));
-    c10::hip::HIPStreamGuard sg(*stream_);  // allocate on the comm stream: the allocator tracks it there
+    return plans_.emplace(key, std::move(p)).first->second;
+  }
+
+  bool staged(int algo, int dtype) const { return accum_fp32_ && dtype == kBF16 && topo_.world > 1; }
+
+  size_t scratch_bytes(const Plan& p, int64_t n, int dtype) const {
+    const bool st = staged(p.algo, dtype);
+    const size_t esz = (st || dtype == kF32) ? 4 : 2;
+    return ((size_t)p.scratch_elems + (st ? (size_t)((n + 63) / 64 * 64) : 0)) * esz + 512;
+  }
+
+  void ensure_scratch(size_t bytes) {
+    if (scratch_.defined() && (size_t)scratch_.numel() >= bytes) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    DLA_HIP_THROW(hipStreamIsCapturing(stream_->stream(), &cs));
+    TORCH_CHECK(cs == hipStreamCaptureStatusNone,
+                "CommEngine: scratch must grow during HIP-graph capture; call reserve() with the bucket sizes first");
+    // Allocated with the comm stream current: the caching allocator hands a block freed here only
+    // to later allocations on the same stream, i.e. in stream order after all queued work that
+    // still uses the old buffer — no host synchronisation needed when replacing it.
+    c10::hip::HIPStreamGuard sg(*stream_);
+    size_t want = std::max(bytes, (size_t)(scratch_.defined() ? scratch_.numel() * 2 : (16 << 20)));
     scratch_ = at::empty({(int64_t)want}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, device_));
-    return scratch_.data_ptr();
   }
 
-  void scale_on_stream(void* data, int64_t n, int dt, float s) {
-    if (s != 1.f) launch_scale(data, n, dt, s, stream_->stream());
+  ncclComm_t comm_of(comm::CommId c) const {
+    if (c == comm::kIntra) return intra_ ? intra_ : comm_;
+    if (c == comm::kInter) {
+      TORCH_CHECK(inter_, "CommEngine: inter-node communicator missing");
+      return inter_;
+    }
+    return comm_;
   }
 
-  void allreduce_on_stream(const at::Tensor& flat, int algo, bool average) {
+  void allreduce_on_stream(const at::Tensor& flat, int algo, bool average, const std::vector<at::Tensor>* grads,
+                           const std::vector<int64_t>* offsets) {
     const int64_t n = flat.numel();
-    if (n == 0) return;
     hipStream_t st = stream_->stream();
-    const ncclDataType_t ndt = nccl_dtype(flat);
-    const int dt = (flat.scalar_type() == at::kBFloat16) ? kBF16 : kF32;
-    TORCH_CHECK(algo == kBuiltin || algo == kRsAg || flat.scalar_type() == at::kFloat ||
-                    flat.scalar_type() == at::kBFloat16,
-                "custom all-reduce algorithms support fp32/bf16 only");
-    if (world_ == 1) {  // reference short-circuit (allreduce.py:18-19,55-56)
+    const int dt = flat.scalar_type() == at::kBFloat16 ? kBF16 : kF32;
+    if (needs_reduce_kernel(algo))
+      TORCH_CHECK(flat.scalar_type() == at::kFloat || flat.scalar_type() == at::kBFloat16,
+                  "custom all-reduce algorithms support fp32/bf16 only");
+    if (topo_.world == 1 || n == 0) {  // reference short-circuit (allreduce.py:18-19,55-56)
+      if (grads) pack_tensors_on(*grads, *offsets, flat, 1.f, st);
       return;
     }
-    const float avg = average ? 1.f / (float)world_ : 1.f;
-    switch (algo) {
-      case kBuiltin:
-        DLA_NCCL_CHECK(ncclAllReduce(flat.data_ptr(), flat.data_ptr(), n, ndt, average ? ncclAvg : ncclSum, comm_, st));
-        break;
-      case kRsAg: {
-        const size_t esz = flat.element_size();
-        const int64_t per = (n + world_ - 1) / world_;
-        // pad to world*per in scratch
-        char* buf = static_cast<char*>(scratch((size_t)per * world_ * esz * 2));
-        char* full = buf;
-        char* mine = buf + (size_t)per * world_ * esz;
-        DLA_HIP_THROW(hipMemsetAsync(full + n * esz, 0, (per * world_ - n) * esz, st));
-        DLA_HIP_THROW(hipMemcpyAsync(full, flat.data_ptr(), n * esz, hipMemcpyDeviceToDevice, st));
-        DLA_NCCL_CHECK(ncclReduceScatter(full, mine, per, ndt, average ? ncclAvg : ncclSum, comm_, st));
-        DLA_NCCL_CHECK(ncclAllGather(mine, full, per, ndt, comm_, st));
-        DLA_HIP_THROW(hipMemcpyAsync(flat.data_ptr(), full, n * esz, hipMemcpyDeviceToDevice, st));
-        break;
-      }
-      case kRing:
-        ring(flat, dt, avg);
-        break;
-      case kDirect:
-        direct(flat, dt, avg);
-        break;
-      case kCentral:
-        central(flat, dt, avg);
-        break;
-      default:
-        TORCH_CHECK(false, "CommEngine: unknown algorithm ", algo);
+    const Plan& plan = plan_for(algo, n);
+    const bool stg = staged(algo, dt) && (flat.scalar_type() == at::kBFloat16);
+    ensure_scratch(scratch_bytes(plan, n, dt));
+    char* sbase = static_cast<char*>(scratch_.data_ptr());
+    if (!stg) {
+      if (grads) pack_tensors_on(*grads, *offsets, flat, 1.f, st);
+      run_plan(plan, static_cast<char*>(flat.data_ptr()), sbase, flat.element_size(),
+               nccl_dtype_of(flat.scalar_type()), dt, average, st);
+      return;
     }
-  }
-
-  // Chunk geometry shared by ring/direct: `parts` contiguous slices of at most `per` elements,
-  // every slice start aligned to 64 elements (256 B fp32) for vectorised reduce kernels.
-  static void split(int64_t n, int parts, std::vector<int64_t>& off, std::vector<int64_t>& len) {
-    int64_t per = (n + parts - 1) / parts;
-    per = (per + 63) / 64 * 64;
-    off.resize(parts);
-    len.resize(parts);
-    for (int i = 0; i < parts; ++i) {
-      off[i] = std::min(n, (int64_t)i * per);
-      len[i] = std::max<int64_t>(0, std::min(n, off[i] + per) - off[i]);
-    }
-  }
-
-  void ring(const at::Tensor& flat, int dt, float avg) {
-    hipStream_t st = stream_->stream();
-    const ncclDataType_t ndt = nccl_dtype(flat);
-    const size_t esz = flat.element_size();
-    const int64_t n = flat.numel();
-    const int C = std::max(1, std::min<int>((int)rings_.size(), (int)((n + 4095) / 4096)));
-    const int N = world_;
-    char* base = static_cast<char*>(flat.data_ptr());
-    // channel slices
-    std::vector<int64_t> coff, clen;
-    split(n, C, coff, clen);
-    // per channel chunk geometry + receive scratch (one max-chunk per channel)
-    std::vector<std::vector<int64_t>> off(C), len(C);
-    int64_t maxchunk = 0;
-    for (int c = 0; c < C; ++c) {
-      split(clen[c], N, off[c], len[c]);
-      for (auto l : len[c]) maxchunk = std::max(maxchunk, l);
-    }
-    char* rbuf = static_cast<char*>(scratch((size_t)maxchunk * esz * C + 256 * C));
-    auto rb = [&](int c) { return rbuf + (size_t)c * ((size_t)maxchunk * esz + 256); };
-
-    // Reduce-scatter: step i sends chunk (pos - i) to the right neighbour, receives chunk
-    // (pos - i - 1) from the left and adds it in (allreduce.py:69-77).
-    for (int phase = 0; phase < 2; ++phase) {
-      for (int i = 0; i < N - 1; ++i) {
-        DLA_NCCL_CHECK(ncclGroupStart());
-        for (int c = 0; c < C; ++c) {
-          const auto& ring = rings_[c];
-          const int pos = ring_pos_[c][rank_];
-          const int right = ring[(pos + 1) % N], left = ring[(pos - 1 + N) % N];
-          const int to_send = ((pos - i + (phase ? 1 : 0)) % N + N) % N;
-          const int to_recv = ((to_send - 1) % N + N) % N;
-          char* cbase = base + (size_t)coff[c] * esz;
-          if (len[c][to_send] > 0)
-            DLA_NCCL_CHECK(ncclSend(cbase + off[c][to_send] * esz, len[c][to_send], ndt, right, comm_, st));
-          if (len[c][to_recv] > 0) {
-            void* dst = phase == 0 ? (void*)rb(c) : (void*)(cbase + off[c][to_recv] * esz);  // AG receives in place
-            DLA_NCCL_CHECK(ncclRecv(dst, len[c][to_recv], ndt, left, comm_, st));
-          }
-        }
-        DLA_NCCL_CHECK(ncclGroupEnd());
-        if (phase == 0) {
-          for (int c = 0; c < C; ++c) {
-            const int pos = ring_pos_[c][rank_];
-            const int to_send = ((pos - i) % N + N) % N;
-            const int to_recv = ((to_send - 1) % N + N) % N;
-            if (len[c][to_recv] == 0) continue;
-            char* dst = base + (size_t)(coff[c] + off[c][to_recv]) * esz;
-            ReduceSrcs rs{};
-            rs.count = 1;
-            rs.ptr[0] = rb(c);
-            // The fully reduced chunk (last RS step) is scaled by 1/N here, so the all-gather
-            // moves final values and no extra pass over the bucket is needed.
-            const float s = (i == N - 2) ? avg : 1.f;
-            launch_reduce_sum(dst, true, rs, len[c][to_recv], dt, s, st);
-          }
-        }
-      }
-    }
-  }
-
-  void direct(const at::Tensor& flat, int dt, float avg) {
-    hipStream_t st = stream_->stream();
-    const ncclDataType_t ndt = nccl_dtype(flat);
-    const size_t esz = flat.element_size();
-    const int64_t n = flat.numel();
-    const int N = world_;
-    char* base = static_cast<char*>(flat.data_ptr());
-    std::vector<int64_t> off, len;
-    split(n, N, off, len);
-    int64_t maxchunk = 0;
-    for (auto l : len) maxchunk = std::max(maxchunk, l);
-    const size_t slot = (size_t)maxchunk * esz + 256;
-    char* rbuf = static_cast<char*>(scratch(slot * N));
-    // Phase 1: scatter — my chunk j goes to rank j; I receive everybody's copy of my chunk.
-    DLA_NCCL_CHECK(ncclGroupStart());
-    for (int k = 1; k < N; ++k) {
-      const int peer = (rank_ + k) % N;
-      const int from = (rank_ - k + N) % N;
-      if (len[peer] > 0) DLA_NCCL_CHECK(ncclSend(base + off[peer] * esz, len[peer], ndt, peer, comm_, st));
-      if (len[rank_] > 0) DLA_NCCL_CHECK(ncclRecv(rbuf + slot * k, len[rank_], ndt, from, comm_, st));
-    }
-    DLA_NCCL_CHECK(ncclGroupEnd());
-    // One k-way reduce of my chunk (+ scale), in batches of kMaxReduceSrc sources.
-    if (len[rank_] > 0) {
-      char* mine = base + off[rank_] * esz;
-      int k = 1;
-      while (k < N) {
-        ReduceSrcs rs{};
-        rs.count = 0;
-        while (k < N && rs.count < kMaxReduceSrc) rs.ptr[rs.count++] = rbuf + slot * k++;
-        launch_reduce_sum(mine, true, rs, len[rank_], dt, k >= N ? avg : 1.f, st);
-      }
-    }
-    // Phase 2: all-gather — send my reduced chunk to everybody, receive theirs in place.
-    DLA_NCCL_CHECK(ncclGroupStart());
-    for (int k = 1; k < N; ++k) {
-      const int peer = (rank_ + k) % N;
-      const int from = (rank_ - k + N) % N;
-      if (len[rank_] > 0) DLA_NCCL_CHECK(ncclSend(base + off[rank_] * esz, len[rank_], ndt, peer, comm_, st));
-      if (len[from] > 0) DLA_NCCL_CHECK(ncclRecv(base + off[from] * esz, len[from], ndt, from, comm_, st));
-    }
-    DLA_NCCL_CHECK(ncclGroupEnd());
-  }
-
-  void central(const at::Tensor& flat, int dt, float avg) {
-    hipStream_t st = stream_->stream();
-    const ncclDataType_t ndt = nccl_dtype(flat);
-    const size_t esz = flat.element_size();
-    const int64_t n = flat.numel();
-    const int N = world_;
-    void* data = flat.data_ptr();
-    if (rank_ == 0) {
-      const size_t slot = (size_t)n * esz + 256;
-      char* rbuf = static_cast<char*>(scratch(slot * (N - 1)));
-      DLA_NCCL_CHECK(ncclGroupStart());
-      for (int r = 1; r < N; ++r) DLA_NCCL_CHECK(ncclRecv(rbuf + slot * (r - 1), n, ndt, r, comm_, st));
-      DLA_NCCL_CHECK(ncclGroupEnd());
-      int r = 1;
-      while (r < N) {  // sum in rank order (allreduce.py:30-32)
-        ReduceSrcs rs{};
-        rs.count = 0;
-        while (r < N && rs.count < kMaxReduceSrc) rs.ptr[rs.count++] = rbuf + slot * (r++ - 1);
-        launch_reduce_sum(data, true, rs, n, dt, r >= N ? avg : 1.f, st);
-      }
-      DLA_NCCL_CHECK(ncclGroupStart());
-      for (int q = 1; q < N; ++q) DLA_NCCL_CHECK(ncclSend(data, n, ndt, q, comm_, st));
-      DLA_NCCL_CHECK(ncclGroupEnd());
+    // fp32 accumulation of a bf16 bucket: gather / cast into fp32 staging, reduce in fp32 on the
+    // wire and in the reduce kernels, round to bf16 once at the end.
+    const int64_t n64 = (n + 63) / 64 * 64;
+    char* stage = sbase;
+    if (grads) {
+      at::Tensor sv = at::from_blob(stage, {n}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device_));
+      pack_tensors_on(*grads, *offsets, sv, 1.f, st);
     } else {
-      DLA_NCCL_CHECK(ncclSend(data, n, ndt, 0, comm_, st));
-      DLA_NCCL_CHECK(ncclRecv(data, n, ndt, 0, comm_, st));
+      launch_cast(stage, kF32, flat.data_ptr(), kBF16, n, 1.f, st);
+    }
+    run_plan(plan, stage, sbase + n64 * 4, 4, ncclFloat32, kF32, average, st);
+    launch_cast(flat.data_ptr(), kBF16, stage, kF32, n, 1.f, st);
+  }
+
+  void run_plan(const Plan& p, char* data, char* scratch, size_t esz, ncclDataType_t ndt, int dt, bool average,
+                hipStream_t st) {
+    auto ptr = [&](const comm::Ref& r) { return (r.buf == comm::kData ? data : scratch) + (size_t)r.off * esz; };
+    for (const auto& step : p.steps) {
+      if (step.is_coll()) {
+        const comm::Op& o = step.ops[0];
+        ncclComm_t c = comm_of(o.comm);
+        // plans are built for averaging; a summing call keeps ncclSum
+        const ncclRedOp_t red = (o.average && average) ? ncclAvg : ncclSum;
+        switch (o.coll) {
+          case comm::kAllReduce:
+            DLA_NCCL_CHECK(ncclAllReduce(ptr(o.src[0]), ptr(o.dst), o.count, ndt, red, c, st));
+            break;
+          case comm::kReduceScatter:
+            DLA_NCCL_CHECK(ncclReduceScatter(ptr(o.src[0]), ptr(o.dst), o.count, ndt, red, c, st));
+            break;
+          case comm::kAllGather:
+            DLA_NCCL_CHECK(ncclAllGather(ptr(o.src[0]), ptr(o.dst), o.count, ndt, c, st));
+            break;
+        }
+        continue;
+      }
+      bool group = false;
+      for (const auto& o : step.ops) {
+        if (o.kind == comm::kSend || o.kind == comm::kRecv) {
+          if (!group) {
+            DLA_NCCL_CHECK(ncclGroupStart());
+            group = true;
+          }
+          if (o.kind == comm::kSend)
+            DLA_NCCL_CHECK(ncclSend(ptr(o.src[0]), o.count, ndt, o.peer, comm_, st));
+          else
+            DLA_NCCL_CHECK(ncclRecv(ptr(o.dst), o.count, ndt, o.peer, comm_, st));
+        }
+      }
+      if (group) DLA_NCCL_CHECK(ncclGroupEnd());
+      for (const auto& o : step.ops) {
+        if (o.kind == comm::kReduce) {
+          ReduceSrcs rs{};
+          rs.count = o.nsrc;
+          for (int i = 0; i < o.nsrc; ++i) rs.ptr[i] = ptr(o.src[i]);
+          launch_reduce_sum(ptr(o.dst), o.accumulate, rs, o.count, dt, average ? o.scale : 1.f, st);
+        } else if (o.kind == comm::kCopy) {
+          DLA_HIP_THROW(hipMemcpyAsync(ptr(o.dst), ptr(o.src[0]), (size_t)o.count * esz, hipMemcpyDeviceToDevice, st));
+        } else if (o.kind == comm::kZero) {
+          DLA_HIP_THROW(hipMemsetAsync(ptr(o.dst), 0, (size_t)o.count * esz, st));
+        }
+      }
     }
   }
 
-  int rank_, world_, device_;
+  int device_;
+  Topology topo_;
   ncclUniqueId uid_;
-  ncclComm_t comm_ = nullptr;
+  ncclComm_t comm_ = nullptr, intra_ = nullptr, inter_ = nullptr;
+  bool aborted_ = false;
+  bool accum_fp32_ = false;
   std::unique_ptr<c10::hip::HIPStream> stream_;
-  std::vector<std::vector<int>> rings_;
-  std::vector<std::vector<int>> ring_pos_;
+  std::map<std::pair<int, int64_t>, Plan> plans_;
   at::Tensor scratch_;
   std::vector<hipEvent_t> ready_pool_;
   size_t ready_next_ = 0;
@@ -488,18 +526,167 @@ class CommEngine {
   size_t used_timing_ = 0;
 };
 
+// ---------------------------------------------------------------------------------------------
+// Virtual ranks: N ranks' buffers in one process, links = copies (vexec.h)
+// ---------------------------------------------------------------------------------------------
+struct DeviceBackend {
+  std::vector<char*> data, scratch;
+  size_t esz = 4;
+  int dt = kF32;
+  hipStream_t st = nullptr;
+  at::TensorOptions opts;
+  std::vector<at::Tensor> temps;
+
+  void* ptr(int rank, const comm::Ref& r) {
+    return (r.buf == comm::kData ? data[rank] : scratch[rank]) + (size_t)r.off * esz;
+  }
+  void* offset(void* p, int64_t elems) { return static_cast<char*>(p) + (size_t)elems * esz; }
+  void* temp(int64_t n) {
+    temps.push_back(at::empty({(int64_t)((size_t)n * esz + 256)}, opts));
+    return temps.back().data_ptr();
+  }
+  void copy(void* dst, const void* src, int64_t n) {
+    if (n > 0 && dst != src) DLA_HIP_THROW(hipMemcpyAsync(dst, src, (size_t)n * esz, hipMemcpyDeviceToDevice, st));
+  }
+  void zero(void* dst, int64_t n) {
+    if (n > 0) DLA_HIP_THROW(hipMemsetAsync(dst, 0, (size_t)n * esz, st));
+  }
+  void reduce(void* dst, bool acc, const void* const* srcs, int nsrc, int64_t n, float scale) {
+    ReduceSrcs rs{};
+    rs.count = nsrc;
+    for (int i = 0; i < nsrc; ++i) rs.ptr[i] = srcs[i];
+    launch_reduce_sum(dst, acc, rs, n, dt, scale, st);
+  }
+};
+
+// All-reduce `bufs` (one tensor per virtual rank, same numel / dtype / device) in place with the
+// schedules CommEngine would run for that many ranks. CUDA tensors run on the current stream
+// (copies + reduce kernels); CPU tensors on the host backend. accum_fp32 stages bf16 buffers in
+// fp32 exactly like CommEngine (gather/cast, fp32 plan, round once).
+static void virtual_allreduce(std::vector<at::Tensor> bufs, int algo, bool average, std::vector<std::vector<int>> rings,
+                              int local_size, std::vector<std::vector<int>> local_rings,
+                              std::vector<std::vector<int>> node_rings, bool accum_fp32) {
+  const int N = (int)bufs.size();
+  TORCH_CHECK(N >= 1, "virtual_allreduce: no buffers");
+  const int64_t n = bufs[0].numel();
+  const auto dtype = bufs[0].scalar_type();
+  const bool cuda = bufs[0].is_cuda();
+  for (auto& b : bufs) {
+    TORCH_CHECK(b.numel() == n && b.scalar_type() == dtype && b.device() == bufs[0].device() && b.is_contiguous(),
+                "virtual_allreduce: buffers must share numel, dtype, device and be contiguous");
+  }
+  TORCH_CHECK(dtype == at::kFloat || dtype == at::kBFloat16, "virtual_allreduce: fp32 / bf16 only");
+  TORCH_CHECK(algo >= comm::kBuiltin && algo <= comm::kHierColl, "virtual_allreduce: unknown algorithm ", algo);
+  if (N == 1 || n == 0) return;
+  std::vector<Plan> plans;
+  Topology t0 = make_topology(0, N, rings, local_size, local_rings, node_rings);
+  for (int r = 0; r < N; ++r) {
+    Topology t = t0;
+    t.rank = r;
+    try {
+      plans.push_back(comm::build_plan(algo, t, n, average ? 1.f / (float)N : 1.f));
+    } catch (const std::exception& e) {
+      TORCH_CHECK(false, e.what());
+    }
+  }
+  const bool stage = accum_fp32 && dtype == at::kBFloat16;
+  std::vector<at::Tensor> work = bufs;
+  if (cuda) {
+    c10::hip::HIPGuard guard((c10::DeviceIndex)bufs[0].device().index());
+    hipStream_t st = c10::hip::getCurrentHIPStream(bufs[0].device().index()).stream();
+    if (stage) {
+      for (int r = 0; r < N; ++r) {
+        work[r] = at::empty({n}, bufs[r].options().dtype(at::kFloat));
+        launch_cast(work[r].data_ptr(), kF32, bufs[r].data_ptr(), kBF16, n, 1.f, st);
+      }
+    }
+    DeviceBackend be;
+    be.esz = work[0].element_size();
+    be.dt = work[0].scalar_type() == at::kBFloat16 ? kBF16 : kF32;
+    be.st = st;
+    be.opts = at::TensorOptions().dtype(at::kByte).device(bufs[0].device());
+    std::vector<at::Tensor> scr;
+    for (int r = 0; r < N; ++r) {
+      scr.push_back(at::empty({(int64_t)((size_t)plans[r].scratch_elems * be.esz + 256)}, be.opts));
+      be.data.push_back(static_cast<char*>(work[r].data_ptr()));
+      be.scratch.push_back(static_cast<char*>(scr.back().data_ptr()));
+    }
+    comm::VirtualRun<DeviceBackend> run(plans, t0, be);
+    try {
+      run.run();
+    } catch (const std::exception& e) {
+      TORCH_CHECK(false, e.what());
+    }
+    if (stage)
+      for (int r = 0; r < N; ++r) launch_cast(bufs[r].data_ptr(), kBF16, work[r].data_ptr(), kF32, n, 1.f, st);
+    return;
+  }
+  comm::HostBackend be;
+  std::vector<std::vector<char>> stage_mem, scr;
+  be.bf16 = dtype == at::kBFloat16 && !stage;
+  be.esz = be.bf16 ? 2 : 4;
+  for (int r = 0; r < N; ++r) {
+    if (stage) {
+      stage_mem.emplace_back((size_t)n * 4);
+      float* f = reinterpret_cast<float*>(stage_mem.back().data());
+      const uint16_t* b = static_cast<const uint16_t*>(bufs[r].data_ptr());
+      for (int64_t i = 0; i < n; ++i) f[i] = comm::HostBackend::b2f(b[i]);
+      be.data.push_back(stage_mem.back().data());
+    } else {
+      be.data.push_back(static_cast<char*>(bufs[r].data_ptr()));
+    }
+    scr.emplace_back((size_t)plans[r].scratch_elems * be.esz + 64);
+    be.scratch.push_back(scr.back().data());
+  }
+  comm::VirtualRun<comm::HostBackend> run(plans, t0, be);
+  try {
+    run.run();
+  } catch (const std::exception& e) {
+    TORCH_CHECK(false, e.what());
+  }
+  if (stage) {
+    for (int r = 0; r < N; ++r) {
+      const float* f = reinterpret_cast<const float*>(stage_mem[r].data());
+      uint16_t* b = static_cast<uint16_t*>(bufs[r].data_ptr());
+      for (int64_t i = 0; i < n; ++i) b[i] = comm::HostBackend::f2b(f[i]);
+    }
+  }
+}
+
+static std::string plan_describe(int algo, int rank, int world, int64_t n, std::vector<std::vector<int>> rings,
+                                 int local_size, std::vector<std::vector<int>> local_rings,
+                                 std::vector<std::vector<int>> node_rings, bool average) {
+  Topology t = make_topology(rank, world, std::move(rings), local_size, std::move(local_rings), std::move(node_rings));
+  try {
+    return comm::describe(comm::build_plan(algo, t, n, average ? 1.f / (float)world : 1.f));
+  } catch (const std::exception& e) {
+    TORCH_CHECK(false, e.what());
+  }
+  return "";
+}
+
 void bind_comm(pybind11::module& m) {
+  using VV = std::vector<std::vector<int>>;
   pybind11::class_<CommEngine>(m, "CommEngine")
-      .def(pybind11::init<int, int, pybind11::bytes, int, std::vector<std::vector<int>>>(), pybind11::arg("rank"),
-           pybind11::arg("world"), pybind11::arg("unique_id"), pybind11::arg("device"), pybind11::arg("rings"))
+      .def(pybind11::init<int, int, pybind11::bytes, int, VV, int, VV, VV>(), pybind11::arg("rank"),
+           pybind11::arg("world"), pybind11::arg("unique_id"), pybind11::arg("device"), pybind11::arg("rings"),
+           pybind11::arg("local_size") = 0, pybind11::arg("local_rings") = VV{}, pybind11::arg("node_rings") = VV{})
       .def_static("get_unique_id", &CommEngine::get_unique_id)
       .def("rank", &CommEngine::rank)
       .def("world", &CommEngine::world)
+      .def("local_size", &CommEngine::local_size)
       .def("num_rings", &CommEngine::num_rings)
+      .def("set_accum_fp32", &CommEngine::set_accum_fp32)
+      .def("accum_fp32", &CommEngine::accum_fp32)
       .def("join_current", &CommEngine::join_current)
       .def("wait_on_current", &CommEngine::wait_on_current)
       .def("synchronize", &CommEngine::synchronize)
+      .def("async_error", &CommEngine::async_error)
+      .def("abort", &CommEngine::abort)
+      .def("aborted", &CommEngine::aborted)
       .def("stream_handle", &CommEngine::stream_handle)
+      .def("reserve", &CommEngine::reserve, pybind11::arg("algo"), pybind11::arg("sizes"), pybind11::arg("dtype"))
+      .def("describe_plan", &CommEngine::describe_plan)
       .def("allreduce", &CommEngine::allreduce, pybind11::arg("flat"), pybind11::arg("algo"), pybind11::arg("average"))
       .def("bucket_allreduce", &CommEngine::bucket_allreduce, pybind11::arg("flat"), pybind11::arg("algo"),
            pybind11::arg("average"), pybind11::arg("table").none(true), pybind11::arg("pack_scale") = 1.0,
@@ -510,11 +697,20 @@ void bind_comm(pybind11::module& m) {
       .def("allgather", &CommEngine::allgather)
       .def("set_timing", &CommEngine::set_timing)
       .def("consume_comm_ms", &CommEngine::consume_comm_ms);
-  m.attr("ALGO_BUILTIN") = (int)kBuiltin;
-  m.attr("ALGO_RING") = (int)kRing;
-  m.attr("ALGO_DIRECT") = (int)kDirect;
-  m.attr("ALGO_CENTRAL") = (int)kCentral;
-  m.attr("ALGO_RSAG") = (int)kRsAg;
+  m.def("virtual_allreduce", &virtual_allreduce, "all-reduce N virtual ranks' buffers with the engine's schedules",
+        pybind11::arg("bufs"), pybind11::arg("algo"), pybind11::arg("average") = true, pybind11::arg("rings") = VV{},
+        pybind11::arg("local_size") = 0, pybind11::arg("local_rings") = VV{}, pybind11::arg("node_rings") = VV{},
+        pybind11::arg("accum_fp32") = false);
+  m.def("plan_describe", &plan_describe, pybind11::arg("algo"), pybind11::arg("rank"), pybind11::arg("world"),
+        pybind11::arg("n"), pybind11::arg("rings") = VV{}, pybind11::arg("local_size") = 0,
+        pybind11::arg("local_rings") = VV{}, pybind11::arg("node_rings") = VV{}, pybind11::arg("average") = true);
+  m.attr("ALGO_BUILTIN") = (int)comm::kBuiltin;
+  m.attr("ALGO_RING") = (int)comm::kRing;
+  m.attr("ALGO_DIRECT") = (int)comm::kDirect;
+  m.attr("ALGO_CENTRAL") = (int)comm::kCentral;
+  m.attr("ALGO_RSAG") = (int)comm::kRsAg;
+  m.attr("ALGO_HIER_RING") = (int)comm::kHierRing;
+  m.attr("ALGO_HIER_COLL") = (int)comm::kHierColl;
 }
 
 }  // namespace dla

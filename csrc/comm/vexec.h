@@ -1,0 +1,264 @@
+// Lockstep executor for N virtual ranks inside one process.
+//
+// Runs the N per-rank Plans of one all-reduce step by step: at every step the P2P ops of all
+// ranks are matched (the k-th send from a to b pairs with the k-th receive on b from a, the RCCL
+// matching rule) and become buffer copies — the "links" — then every rank's local reduce / copy /
+// zero ops run with the production reduce kernel. Collective steps (ncclAllReduce /
+// ReduceScatter / AllGather on the world, intra-node or inter-node communicator) are emulated
+// per communicator colour. Any schedule inconsistency — a send without a receive, mismatched
+// lengths, a receive overlapping a buffer the same step sends from, ranks disagreeing on the
+// step structure — throws instead of hanging, which is what a real multi-GPU run would do.
+//
+// The Backend supplies memory and arithmetic: the device backend (engine.cpp) issues
+// hipMemcpyAsync + the reduce kernel of reduce.hip on one stream; the host backend (below) runs
+// the same arithmetic on CPU memory, so the schedules are checked in the CPU test suite too.
+#pragma once
+
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "plan.h"
+
+namespace dla {
+namespace comm {
+
+template <class Backend>
+class VirtualRun {
+ public:
+  VirtualRun(const std::vector<Plan>& plans, const Topology& topo, Backend& be) : plans_(plans), t_(topo), be_(be) {}
+
+  void run() {
+    const int N = (int)plans_.size();
+    if (N != t_.world) fail("need one plan per virtual rank");
+    size_t S = plans_[0].steps.size();
+    for (const auto& p : plans_)
+      if (p.steps.size() != S) fail("ranks disagree on the number of steps");
+    for (size_t s = 0; s < S; ++s) {
+      const bool coll = plans_[0].steps[s].is_coll();
+      for (int r = 1; r < N; ++r)
+        if (plans_[r].steps[s].is_coll() != coll) fail("step " + std::to_string(s) + ": collective on some ranks only");
+      if (coll)
+        run_coll(s);
+      else
+        run_p2p_step(s);
+    }
+  }
+
+ private:
+  [[noreturn]] void fail(const std::string& m) { throw std::runtime_error("virtual ranks: " + m); }
+
+  struct Span {
+    int rank;
+    uint8_t buf;
+    int64_t lo, hi;
+  };
+  static bool overlap(const Span& a, const Span& b) {
+    return a.rank == b.rank && a.buf == b.buf && a.lo < b.hi && b.lo < a.hi;
+  }
+
+  void run_p2p_step(size_t s) {
+    const int N = (int)plans_.size();
+    std::map<std::pair<int, int>, std::deque<const Op*>> sends;  // (from, to) -> sends in issue order
+    std::vector<Span> reads, writes;
+    for (int r = 0; r < N; ++r)
+      for (const Op& o : plans_[r].steps[s].ops) {
+        if (o.kind == kSend) {
+          if (o.peer < 0 || o.peer >= N || o.peer == r) fail("bad send peer");
+          sends[{r, o.peer}].push_back(&o);
+          reads.push_back(Span{r, o.src[0].buf, o.src[0].off, o.src[0].off + o.count});
+        }
+      }
+    struct Xfer {
+      int from, to;
+      const Op *snd, *rcv;
+    };
+    std::vector<Xfer> xfers;
+    for (int r = 0; r < N; ++r)
+      for (const Op& o : plans_[r].steps[s].ops) {
+        if (o.kind != kRecv) continue;
+        auto it = sends.find({o.peer, r});
+        if (it == sends.end() || it->second.empty())
+          fail("step " + std::to_string(s) + ": rank " + std::to_string(r) + " receives from " +
+               std::to_string(o.peer) + " which sends nothing");
+        const Op* snd = it->second.front();
+        it->second.pop_front();
+        if (snd->count != o.count)
+          fail("step " + std::to_string(s) + ": length mismatch " + std::to_string(o.peer) + "->" + std::to_string(r) +
+               " (" + std::to_string(snd->count) + " vs " + std::to_string(o.count) + ")");
+        Span w{r, o.dst.buf, o.dst.off, o.dst.off + o.count};
+        for (const auto& x : writes)
+          if (overlap(x, w)) fail("step " + std::to_string(s) + ": overlapping receives on rank " + std::to_string(r));
+        for (const auto& x : reads)
+          if (overlap(x, w))
+            fail("step " + std::to_string(s) + ": rank " + std::to_string(r) + " receives into a region it sends from");
+        writes.push_back(w);
+        xfers.push_back(Xfer{o.peer, r, snd, &o});
+      }
+    for (const auto& kv : sends)
+      if (!kv.second.empty())
+        fail("step " + std::to_string(s) + ": send " + std::to_string(kv.first.first) + "->" +
+             std::to_string(kv.first.second) + " has no matching receive");
+    // the links
+    for (const auto& x : xfers) be_.copy(be_.ptr(x.to, x.rcv->dst), be_.ptr(x.from, x.snd->src[0]), x.rcv->count);
+    // local ops of every rank
+    for (int r = 0; r < N; ++r)
+      for (const Op& o : plans_[r].steps[s].ops) local(r, o);
+  }
+
+  void local(int r, const Op& o) {
+    switch (o.kind) {
+      case kReduce: {
+        const void* srcs[kPlanMaxSrc];
+        for (int i = 0; i < o.nsrc; ++i) srcs[i] = be_.ptr(r, o.src[i]);
+        be_.reduce(be_.ptr(r, o.dst), o.accumulate, srcs, o.nsrc, o.count, o.scale);
+        break;
+      }
+      case kCopy:
+        be_.copy(be_.ptr(r, o.dst), be_.ptr(r, o.src[0]), o.count);
+        break;
+      case kZero:
+        be_.zero(be_.ptr(r, o.dst), o.count);
+        break;
+      default:
+        break;
+    }
+  }
+
+  // members of rank r's communicator `comm`, in communicator-rank order
+  std::vector<int> members(int r, CommId comm) const {
+    const int N = t_.world, L = t_.L();
+    std::vector<int> m;
+    if (comm == kWorld) {
+      for (int i = 0; i < N; ++i) m.push_back(i);
+    } else if (comm == kIntra) {
+      const int node = r / L;
+      for (int j = 0; j < L; ++j) m.push_back(node * L + j);
+    } else {
+      const int lr = r % L;
+      for (int k = 0; k < N / L; ++k) m.push_back(k * L + lr);
+    }
+    return m;
+  }
+
+  void run_coll(size_t s) {
+    const int N = (int)plans_.size();
+    std::vector<char> done(N, 0);
+    for (int r = 0; r < N; ++r) {
+      if (done[r]) continue;
+      const Op& o0 = plans_[r].steps[s].ops[0];
+      auto m = members(r, o0.comm);
+      for (int q : m) {
+        const Op& o = plans_[q].steps[s].ops[0];
+        if (o.coll != o0.coll || o.comm != o0.comm || o.count != o0.count || o.average != o0.average)
+          fail("step " + std::to_string(s) + ": collective arguments differ between ranks");
+        done[q] = 1;
+      }
+      emulate(s, m, o0);
+    }
+  }
+
+  // Sum `k` member buffers into `dst` (fresh), in member order, batches of kPlanMaxSrc.
+  void sum_into(void* dst, const std::vector<const void*>& srcs, int64_t n, float scale) {
+    size_t i = 0;
+    bool first = true;
+    while (i < srcs.size()) {
+      const void* b[kPlanMaxSrc];
+      int c = 0;
+      while (i < srcs.size() && c < kPlanMaxSrc) b[c++] = srcs[i++];
+      be_.reduce(dst, !first, b, c, n, i >= srcs.size() ? scale : 1.f);
+      first = false;
+    }
+  }
+
+  void emulate(size_t s, const std::vector<int>& m, const Op& o) {
+    const int M = (int)m.size();
+    const int64_t n = o.count;
+    const float sc = o.average ? 1.f / (float)M : 1.f;
+    auto op = [&](int j) -> const Op& { return plans_[m[j]].steps[s].ops[0]; };
+    if (o.coll == kAllReduce) {
+      void* tmp = be_.temp(n);
+      std::vector<const void*> srcs;
+      for (int j = 0; j < M; ++j) srcs.push_back(be_.ptr(m[j], op(j).src[0]));
+      sum_into(tmp, srcs, n, sc);
+      for (int j = 0; j < M; ++j) be_.copy(be_.ptr(m[j], op(j).dst), tmp, n);
+    } else if (o.coll == kReduceScatter) {
+      void* tmp = be_.temp(n * M);
+      for (int j = 0; j < M; ++j) {
+        std::vector<const void*> srcs;
+        for (int i = 0; i < M; ++i) {
+          Ref r = op(i).src[0];
+          r.off += (int64_t)j * n;
+          srcs.push_back(be_.ptr(m[i], r));
+        }
+        sum_into(be_.offset(tmp, (int64_t)j * n), srcs, n, sc);
+      }
+      for (int j = 0; j < M; ++j) be_.copy(be_.ptr(m[j], op(j).dst), be_.offset(tmp, (int64_t)j * n), n);
+    } else {  // all-gather
+      void* tmp = be_.temp(n * M);
+      for (int j = 0; j < M; ++j) be_.copy(be_.offset(tmp, (int64_t)j * n), be_.ptr(m[j], op(j).src[0]), n);
+      for (int i = 0; i < M; ++i) be_.copy(be_.ptr(m[i], op(i).dst), tmp, n * M);
+    }
+  }
+
+  const std::vector<Plan>& plans_;
+  const Topology& t_;
+  Backend& be_;
+};
+
+// Host backend: CPU buffers, fp32 or bf16 (round-to-nearest-even, as v_cvt_pk_bf16_f32).
+struct HostBackend {
+  std::vector<char*> data, scratch;
+  size_t esz = 4;
+  bool bf16 = false;
+  std::vector<std::vector<char>> temps;
+
+  static float b2f(uint16_t v) {
+    uint32_t u = (uint32_t)v << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+  }
+  static uint16_t f2b(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+  }
+  float load(const void* p, int64_t i) const {
+    return bf16 ? b2f(static_cast<const uint16_t*>(p)[i]) : static_cast<const float*>(p)[i];
+  }
+  void store(void* p, int64_t i, float v) const {
+    if (bf16)
+      static_cast<uint16_t*>(p)[i] = f2b(v);
+    else
+      static_cast<float*>(p)[i] = v;
+  }
+  void* ptr(int rank, const Ref& r) { return (r.buf == kData ? data[rank] : scratch[rank]) + (size_t)r.off * esz; }
+  void* offset(void* p, int64_t elems) { return static_cast<char*>(p) + (size_t)elems * esz; }
+  void* temp(int64_t n) {
+    temps.emplace_back((size_t)n * esz + 16);
+    return temps.back().data();
+  }
+  void copy(void* dst, const void* src, int64_t n) {
+    if (n > 0 && dst != src) std::memmove(dst, src, (size_t)n * esz);
+  }
+  void zero(void* dst, int64_t n) {
+    if (n > 0) std::memset(dst, 0, (size_t)n * esz);
+  }
+  void reduce(void* dst, bool acc, const void* const* srcs, int nsrc, int64_t n, float scale) {
+    for (int64_t i = 0; i < n; ++i) {
+      float a = acc ? load(dst, i) : 0.f;
+      for (int s = 0; s < nsrc; ++s) a += load(srcs[s], i);
+      store(dst, i, a * scale);
+    }
+  }
+};
+
+}  // namespace comm
+}  // namespace dla

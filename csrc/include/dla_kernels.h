@@ -71,6 +71,8 @@ struct ReduceSrcs {
 void launch_reduce_sum(void* dst, bool accumulate_dst, const ReduceSrcs& srcs, int64_t n, int dtype,
                        float scale, hipStream_t stream);
 void launch_scale(void* data, int64_t n, int dtype, float scale, hipStream_t stream);
+// dst = scale * src with dtype conversion (fp32 / bf16 either way)
+void launch_cast(void* dst, int dst_dtype, const void* src, int src_dtype, int64_t n, float scale, hipStream_t stream);
 
 // ---- synthetic data (synthetic.hip) ---------------------------------------------------------
 // Philox stream position = offset [+ (*step) * per_step when `step` (device int64 counter) is set].

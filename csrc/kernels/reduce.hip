@@ -112,6 +112,32 @@ void launch_reduce_sum(void* dst, bool accumulate_dst, const ReduceSrcs& srcs, i
   }
 }
 
+// dst = scale * src with a dtype conversion (fp32 <-> bf16): staging of bf16 buckets in fp32 for
+// full-precision accumulation across ranks (CommEngine accum_fp32).
+template <typename D, typename S>
+__global__ __launch_bounds__(kRBlock) void cast_kernel(D* __restrict__ dst, const S* __restrict__ src, int64_t n,
+                                                       float scale) {
+  const int64_t stride = (int64_t)gridDim.x * kRBlock * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * kRBlock + threadIdx.x) * 4; i < n; i += stride) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (i + j < n) dst[i + j] = Cvt<D>::from_f32(Cvt<S>::to_f32(src[i + j]) * scale);
+  }
+}
+
+void launch_cast(void* dst, int dst_dtype, const void* src, int src_dtype, int64_t n, float scale, hipStream_t stream) {
+  if (n <= 0) return;
+  const dim3 g(grid_for((n + 3) / 4)), b(kRBlock);
+  if (dst_dtype == kF32 && src_dtype == kBF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16_t>), g, b, 0, stream, (float*)dst, (const bf16_t*)src, n, scale);
+  else if (dst_dtype == kBF16 && src_dtype == kF32)
+    hipLaunchKernelGGL((cast_kernel<bf16_t, float>), g, b, 0, stream, (bf16_t*)dst, (const float*)src, n, scale);
+  else if (dst_dtype == kF32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), g, b, 0, stream, (float*)dst, (const float*)src, n, scale);
+  else
+    hipLaunchKernelGGL((cast_kernel<bf16_t, bf16_t>), g, b, 0, stream, (bf16_t*)dst, (const bf16_t*)src, n, scale);
+}
+
 void launch_scale(void* data, int64_t n, int dtype, float scale, hipStream_t stream) {
   ReduceSrcs none{};
   none.count = 0;

@@ -56,7 +56,7 @@ def _sources():
 
 def _headers_digest() -> str:
     h = hashlib.sha256()
-    for p in sorted((CSRC / "include").glob("*.h")):
+    for p in sorted((CSRC / "include").glob("*.h")) + sorted((CSRC / "comm").glob("*.h")):
         h.update(p.name.encode())
         h.update(p.read_bytes())
     return h.hexdigest()

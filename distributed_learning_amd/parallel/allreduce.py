@@ -154,7 +154,10 @@ class Ring:
         self.pos = [order.index(self.me) for order in self.orders]
 
     def geometry(self, n: int):
-        chan = split_ranges(n, len(self.orders))
+        # same rule as the C++ plans (csrc/comm/plan.cpp channel_lanes): every channel moves at
+        # least 4096 elements, so small buckets use fewer channels
+        nch = max(1, min(len(self.orders), (n + 4095) // 4096))
+        chan = split_ranges(n, nch)
         return [(coff, clen, split_ranges(clen, self.n)) for coff, clen in chan]
 
     def reduce_scatter_(self, flat: torch.Tensor, scale_last: float = 1.0):

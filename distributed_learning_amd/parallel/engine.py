@@ -7,7 +7,14 @@ computed once (:func:`edge_disjoint_rings`) and handed to C++.
 
 Algorithm names map to the C++ schedules:
 ``builtin`` ncclAllReduce, ``ring`` multi-channel P2P ring, ``direct`` two-shot P2P,
-``central`` parameter server, ``rsag`` ncclReduceScatter+ncclAllGather.
+``central`` parameter server, ``rsag`` ncclReduceScatter+ncclAllGather, ``hier_ring`` the 2-step
+node reducer on P2P rings (intra-node RS -> inter-node ring all-reduce of the owned shard ->
+intra-node AG), ``hier_coll`` the same hierarchy on RCCL collectives over ``ncclCommSplit``
+sub-communicators (reference /root/reference/src/reducers.py:38-69, main.py:129-137).
+
+Every schedule is a cached Plan (csrc/comm/plan.h); :mod:`.virtual` runs the identical plans for
+N virtual ranks inside one process (one GPU or the CPU), which is how the N>1 paths are tested
+on a one-GPU box.
 """
 from __future__ import annotations
 
@@ -26,6 +33,8 @@ ALGO_CODES: Dict[str, str] = {
     "direct": "ALGO_DIRECT",
     "central": "ALGO_CENTRAL",
     "rsag": "ALGO_RSAG",
+    "hier_ring": "ALGO_HIER_RING",
+    "hier_coll": "ALGO_HIER_COLL",
 }
 
 
@@ -35,6 +44,29 @@ def algo_code(name: str) -> int:
         return int(getattr(C, ALGO_CODES[name]))
     except KeyError:
         raise ValueError(f"unknown native all-reduce algorithm {name!r}; choose from {sorted(ALGO_CODES)}") from None
+
+
+def topology(world: int, channels: int = 0, local_size: Optional[int] = None) -> Dict[str, object]:
+    """Ring orders for a group of ``world`` ranks (``local_size`` per node), as the engine takes them.
+
+    Default channel count: one ring per outgoing xGMI link of a fully connected node (n - 1, i.e.
+    7 edge-disjoint rings on an 8-GPU MI355X node)."""
+    import os
+
+    if local_size is None:
+        local_size = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        if local_size <= 0 or local_size > world or world % local_size:
+            local_size = world
+    elif local_size <= 0 or local_size > world or world % local_size:
+        raise ValueError(f"local_size {local_size} does not divide the group size {world}")
+    channels = channels or max(1, min(world, 8) - 1)
+    nodes = world // local_size
+    return {
+        "rings": edge_disjoint_rings(world, channels),
+        "local_size": local_size,
+        "local_rings": edge_disjoint_rings(local_size, min(channels, max(1, local_size - 1))),
+        "node_rings": edge_disjoint_rings(nodes, min(channels, max(1, nodes - 1))),
+    }
 
 
 class NativeEngine:
@@ -47,7 +79,10 @@ class NativeEngine:
         self.channels = channels
 
     @classmethod
-    def create(cls, group=None, device: Optional[torch.device] = None, channels: int = 0) -> "NativeEngine":
+    def create(cls, group=None, device: Optional[torch.device] = None, channels: int = 0,
+               local_size: Optional[int] = None, accum_fp32: Optional[bool] = None) -> "NativeEngine":
+        """``local_size``: ranks per node for the 2-step algorithms (default ``LOCAL_WORLD_SIZE`` or
+        the group size); ``accum_fp32``: reduce bf16 buckets in fp32 (default: on when n > 1)."""
         C = _ext.require()
         group = group if group is not None else dist.group.WORLD
         ranks = dist.get_process_group_ranks(group) if group is not dist.group.WORLD else list(
@@ -55,13 +90,30 @@ class NativeEngine:
         n = len(ranks)
         me = ranks.index(dist.get_rank())
         device = device or torch.device("cuda", torch.cuda.current_device())
-        # Default channel count: one ring per outgoing xGMI link of a fully connected node (n-1).
-        channels = channels or max(1, n - 1)
-        rings = edge_disjoint_rings(n, channels)
+        topo = topology(n, channels, local_size)
         obj: List[object] = [C.CommEngine.get_unique_id() if me == 0 else None]
         dist.broadcast_object_list(obj, src=ranks[0], group=group)
-        impl = C.CommEngine(me, n, obj[0], device.index, rings)
-        return cls(impl, group, device, len(rings))
+        impl = C.CommEngine(me, n, obj[0], device.index, topo["rings"], topo["local_size"], topo["local_rings"],
+                            topo["node_rings"])
+        impl.set_accum_fp32(n > 1 if accum_fp32 is None else bool(accum_fp32))
+        return cls(impl, group, device, len(topo["rings"]))
+
+    # -- setup -------------------------------------------------------------------------------
+    def reserve(self, algo: str, sizes, dtype: torch.dtype) -> None:
+        """Pre-build the plans of these bucket sizes and size the scratch buffer once."""
+        self.impl.reserve(algo_code(algo), [int(s) for s in sizes], 1 if dtype == torch.bfloat16 else 0)
+
+    def set_accum_fp32(self, on: bool) -> None:
+        self.impl.set_accum_fp32(bool(on))
+
+    def describe_plan(self, algo: str, n: int) -> str:
+        return self.impl.describe_plan(algo_code(algo), int(n))
+
+    def async_error(self) -> str:
+        return self.impl.async_error()
+
+    def abort(self) -> None:
+        self.impl.abort()
 
     # -- collectives -------------------------------------------------------------------------
     def allreduce(self, flat: torch.Tensor, algo: str = "builtin", average: bool = True) -> None:
@@ -96,5 +148,8 @@ class NativeEngine:
 
     def close(self) -> None:
         if self.impl is not None:
-            self.impl.synchronize()
-            self.impl = None
+            try:
+                if not self.impl.aborted():
+                    self.impl.synchronize()
+            finally:
+                self.impl = None

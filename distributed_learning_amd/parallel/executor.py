@@ -181,5 +181,15 @@ class NativeStreamExecutor(Executor):
             raise RuntimeError("native executor needs grad-as-bucket-view or a native PackTable")
         self.engine.bucket_allreduce(b.flat, self.algorithm, True, table)
 
+    def reserve(self, buckets) -> None:
+        """Build the engine's plans and size its scratch for these buckets once, at setup."""
+        if self.passthrough:
+            return
+        by_dtype = {}
+        for b in buckets:
+            by_dtype.setdefault(b.flat.dtype, []).append(b.flat.numel())
+        for dt, sizes in by_dtype.items():
+            self.engine.reserve(self.algorithm, sizes, dt)
+
     def finish(self) -> None:
         self.engine.wait_on_current()

@@ -22,6 +22,10 @@ Fixes and MI355X design:
    which zero-fills and launches whatever never became ready, so a missed parameter can never hang
    the job.
 5. No CPU blocking on GPU: ``synchronize()`` = compute stream waits on the comm stream.
+6. Local gradient accumulation: backward passes run under :meth:`GradSync.no_sync` leave their
+   gradients in place (the next ``prepare()`` does not reset them) and the next synchronised
+   backward adds to them before its buckets launch; ``passes_per_step`` > 1 (Horovod's
+   ``backward_passes_per_step``) launches a parameter only on its last backward pass.
 """
 from __future__ import annotations
 
@@ -79,7 +83,8 @@ class GradSync:
 
     def __init__(self, params: Iterable[torch.Tensor], *, bucket_cap_bytes: int = 25 * 1024 * 1024,
                  executor: Executor, overlap: bool = True, grad_as_bucket_view: Optional[bool] = None,
-                 comm_dtype: Optional[torch.dtype] = None, grad_mode: Optional[str] = None):
+                 comm_dtype: Optional[torch.dtype] = None, grad_mode: Optional[str] = None,
+                 passes_per_step: int = 1):
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
             raise ValueError("GradSync: no parameters require grad")
@@ -132,11 +137,18 @@ class GradSync:
             self.grad_mode = "pack"
         self._next = 0
         self._enabled = True
+        self._accum_pending = False  # gradients of no_sync passes are waiting for the synced pass
+        if passes_per_step < 1:
+            raise ValueError("passes_per_step must be >= 1")
+        self.passes_per_step = int(passes_per_step)
+        self._pass_count = {}
         self._hooks = []
         if overlap:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
         self.step_count = 0
+        if hasattr(self.executor, "reserve"):
+            self.executor.reserve(self.buckets)
 
     # -------------------------------------------------------------------------------------------
     # setup
@@ -168,10 +180,19 @@ class GradSync:
     # per-step protocol
     # -------------------------------------------------------------------------------------------
     def prepare(self) -> None:
-        """Call before backward (the wrappers do it in forward): reset counters, zero buffers."""
+        """Call before backward (the wrappers do it in forward): reset counters, zero buffers.
+
+        After backward passes under :meth:`no_sync` the gradients are kept (only the bucket
+        counters reset), so the next backward accumulates onto them."""
         self._next = 0
         for b in self.buckets:
             b.reset()
+        if self._accum_pending:
+            if self.grad_mode == "steal":
+                for b in self.buckets:
+                    b.stolen = []
+            return
+        self._pass_count = {}
         if self.grad_mode == "steal":
             for p in self.params:
                 p.grad = None
@@ -196,6 +217,8 @@ class GradSync:
 
     def mark_ready(self, params: Iterable[torch.Tensor]) -> None:
         """Mark parameters that will receive no gradient (unused) as ready with zero grads."""
+        if not self._enabled:
+            return
         for p in params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
@@ -204,6 +227,11 @@ class GradSync:
     def _on_grad_ready(self, p: torch.Tensor) -> None:
         if not self._enabled:
             return
+        if self.passes_per_step > 1:
+            c = self._pass_count.get(id(p), 0) + 1
+            self._pass_count[id(p)] = c
+            if c % self.passes_per_step:
+                return  # accumulate locally; the last pass of the step launches
         b, j = self._owner[id(p)]
         if self.grad_as_bucket_view and p.grad.data_ptr() != b.views[j].data_ptr():
             # the user replaced .grad (e.g. set_to_none between prepare and backward): fold it back
@@ -260,17 +288,21 @@ class GradSync:
                 for p, v in zip(b.params, b.views):
                     p.grad = v
                 b.stolen = []  # autograd's tensors are released only after the compute stream joined
+        self._accum_pending = False
+        self._pass_count = {}
         self.step_count += 1
 
     @contextlib.contextmanager
     def no_sync(self):
-        """Accumulate gradients locally (hooks do not communicate) inside this context."""
+        """Accumulate gradients locally (hooks do not communicate) inside this context; the next
+        synchronised backward adds to them and reduces the sum."""
         prev = self._enabled
         self._enabled = False
         try:
             yield
         finally:
             self._enabled = prev
+            self._accum_pending = True
 
     def close(self) -> None:
         for h in self._hooks:

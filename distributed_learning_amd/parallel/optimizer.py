@@ -44,11 +44,13 @@ class DistributedOptimizer(torch.optim.Optimizer):
                 native = dev.type == "cuda" and dist.is_initialized() and dist.get_backend() == "nccl"
             reducer = make_reducer("immediate", algorithm, native=native)
         self.reducer = reducer
+        # backward_passes_per_step (Horovod): gradients of that many backward passes accumulate
+        # locally and each parameter's bucket slot becomes ready on its last pass
         self.sync = GradSync(params, bucket_cap_bytes=int(bucket_cap_mb * 1024 * 1024),
                              executor=make_executor(reducer, dev, True), overlap=True,
-                             grad_as_bucket_view=grad_as_bucket_view, comm_dtype=comm_dtype)
+                             grad_as_bucket_view=grad_as_bucket_view, comm_dtype=comm_dtype,
+                             passes_per_step=backward_passes_per_step)
         self.backward_passes_per_step = backward_passes_per_step
-        self._passes = 0
         self.sync.prepare()
 
     # Optimizer protocol ------------------------------------------------------------------------

@@ -150,3 +150,120 @@ def test_hierarchical_wrapper():
     for k in res[0]:
         torch.testing.assert_close(res[0][k], ref[k].reshape(res[0][k].shape) if k in ref else res[0][k],
                                    rtol=1e-5, atol=1e-6)
+
+
+# --- local gradient accumulation (no_sync / backward_passes_per_step) --------------------------
+def _accum(rank, world, k, mode):
+    import distributed_learning_amd as dla
+    from distributed_learning_amd.ops.loss import cross_entropy
+    from distributed_learning_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(0)
+    model = TinyNet()
+    if mode == "wrapper":
+        dp = dla.PipelinedFusedDP(model, dla.make_reducer("immediate", "ring"), 2048)
+        for j in range(k):
+            x, y = _data(rank, seed=10 + j)
+            if j < k - 1:
+                with dp.no_sync():
+                    cross_entropy(dp(x), y).backward()
+            else:
+                cross_entropy(dp(x), y).backward()
+        dp.sync_gradients()
+    else:
+        opt = dla.DistributedOptimizer(FusedSGD(model.parameters(), lr=0.0), named_parameters=model.named_parameters(),
+                                       bucket_cap_mb=0.002, backward_passes_per_step=k)
+        opt.zero_grad()
+        for j in range(k):
+            x, y = _data(rank, seed=10 + j)
+            cross_entropy(model(x), y).backward()
+        opt.synchronize()
+    return {n: p.grad.clone() for n, p in model.named_parameters()}
+
+
+def _accum_ref(world, k):
+    from distributed_learning_amd.ops.loss import cross_entropy
+
+    acc = {}
+    for r in range(world):
+        torch.manual_seed(0)
+        m = TinyNet()
+        for j in range(k):
+            x, y = _data(r, seed=10 + j)
+            cross_entropy(m(x), y).backward()
+        for n, p in m.named_parameters():
+            acc[n] = acc.get(n, 0) + p.grad / world
+    return acc
+
+
+@pytest.mark.parametrize("mode", ["wrapper", "optimizer"])
+def test_local_accumulation_then_sync(mode):
+    """k micro-batches (k-1 under no_sync / backward_passes_per_step=k) reduce the SUM of all k."""
+    world, k = 2, 3
+    res = run(_accum, world, k, mode)
+    ref = _accum_ref(world, k)
+    for r in res:
+        for n in ref:
+            torch.testing.assert_close(r[n], ref[n], rtol=1e-5, atol=1e-6)
+
+
+# --- failure propagation ------------------------------------------------------------------------
+def _dies(rank, world):
+    import os
+    import time
+
+    import distributed_learning_amd as dla
+    from distributed_learning_amd.ops.loss import cross_entropy
+
+    torch.manual_seed(0)
+    model = TinyNet()
+    dp = dla.PipelinedFusedDP(model, dla.make_reducer("immediate", "ring"), 2048)
+    if rank == 1:
+        time.sleep(0.5)
+        os._exit(0)  # peer vanishes mid-job: no collective, no teardown (status 0 so rank 0 is not killed)
+    x, y = _data(rank)
+    t0 = time.time()
+    try:
+        cross_entropy(dp(x), y).backward()
+        dp.sync_gradients()
+    except RuntimeError:
+        return {"raised": True, "s": time.time() - t0}
+    return {"raised": False, "s": time.time() - t0}
+
+
+def test_peer_failure_raises_not_hangs():
+    """A rank that exits must make the survivors fail (non-zero exit) within the PG timeout."""
+    import time
+
+    t0 = time.time()
+    try:
+        res = run(_dies, 2, allow_missing=True)
+    except RuntimeError:  # the survivor exited non-zero: also a correct outcome
+        res = [{"raised": True, "s": 0.0}]
+    assert res[0]["raised"], res
+    assert time.time() - t0 < 120
+
+
+# --- Python Gloo ring == C++ plan executed on virtual ranks, bitwise ----------------------------
+def _py_ring(rank, world, n, ch):
+    from distributed_learning_amd.parallel.allreduce import ring_allreduce
+
+    xs = [torch.randn(n, generator=torch.Generator().manual_seed(97 * r + n)) for r in range(world)]
+    y = xs[rank].clone()
+    ring_allreduce(y, None, ch)
+    return y
+
+
+@pytest.mark.parametrize("n,ch", [(5, 1), (1000, 1), (9001, 2), (100_003, 2)])
+def test_python_ring_equals_native_plan(n, ch):
+    from distributed_learning_amd.ops import _ext
+    from distributed_learning_amd.parallel.virtual import virtual_allreduce
+
+    if not _ext.available():
+        pytest.skip("native extension not built")
+    world = 3
+    res = run(_py_ring, world, n, ch)
+    xs = [torch.randn(n, generator=torch.Generator().manual_seed(97 * r + n)) for r in range(world)]
+    virtual_allreduce(xs, "ring", channels=ch)
+    for r in range(world):
+        assert torch.equal(res[r], xs[r]), (n, ch, r)
