@@ -186,7 +186,6 @@ class SyntheticBatches:
         self._native = self.device.type == "cuda" and _ext.available()
         if self.device.type == "cuda" and not self._native:
             _ext.require()  # fail loudly on a GPU box without the extension
-        self._cpu_gen = torch.Generator().manual_seed(self.seed)
         # device_step: the stream position lives in a device counter advanced by a kernel, so the
         # generation can be captured in a HIP graph and still draw a new batch on every replay
         self._step_dev = (torch.zeros((1,), dtype=torch.long, device=self.device)
@@ -208,8 +207,16 @@ class SyntheticBatches:
                 C.uniform_(flat, self.seed, self.step * per_x, 0.0, 1.0)
                 C.randint_(self._y, self.num_classes, self.seed, self.step * per_y)
         else:
-            self._x.copy_(torch.rand(self._x.shape, generator=self._cpu_gen).to(self.dtype))
-            self._y.copy_(torch.randint(0, self.num_classes, self._y.shape, generator=self._cpu_gen))
+            # one generator per step position, so the stream is seekable (checkpoint resume)
+            g = torch.Generator().manual_seed(self.seed + 1_000_003 * self.step)
+            self._x.copy_(torch.rand(self._x.shape, generator=g).to(self.dtype))
+            self._y.copy_(torch.randint(0, self.num_classes, self._y.shape, generator=g))
+
+    def seek(self, step: int) -> None:
+        """Continue the stream at batch ``step`` (a resumed run draws the batches it has not seen)."""
+        self.step = int(step)
+        if self._step_dev is not None:
+            self._step_dev.fill_(self.step)
 
     def next(self) -> Tuple[torch.Tensor, torch.Tensor]:
         if self.regenerate:

@@ -60,7 +60,12 @@ def save_checkpoint(path: str, model: nn.Module, optimizer, step: int, extra: Op
     if dist.is_initialized() and dist.get_rank() != 0:
         return
     inner = getattr(model, "module", model)
-    state = {"model": inner.state_dict(), "optimizer": optimizer.state_dict(), "step": step, "extra": extra or {}}
+    rng = {"cpu": torch.get_rng_state()}
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        rng["cuda"] = torch.cuda.get_rng_state()
+    # the RNG state makes a resumed run draw the same dropout masks as an uninterrupted one
+    state = {"model": inner.state_dict(), "optimizer": optimizer.state_dict(), "step": step, "extra": extra or {},
+             "rng": rng}
     tmp = path + ".tmp"
     torch.save(state, tmp)
     os.replace(tmp, path)
@@ -73,6 +78,11 @@ def load_checkpoint(path: str, model: nn.Module, optimizer=None, map_location=No
     inner.load_state_dict(state["model"])
     if optimizer is not None and "optimizer" in state:
         optimizer.load_state_dict(state["optimizer"])
+    rng = state.get("rng") or {}
+    if "cpu" in rng:
+        torch.set_rng_state(rng["cpu"].cpu())
+    if "cuda" in rng and torch.cuda.is_available():
+        torch.cuda.set_rng_state(rng["cuda"].cpu())
     return int(state.get("step", 0))
 
 
@@ -107,13 +117,22 @@ def worker_process(config, distribute_model: Callable, reducer, experiment_name:
     model.train()
 
     losses = []
-    batch_count = 0
+    # a resumed run continues the original sequence: batch numbering, and the data stream position
+    batch_count = start_step
+    end_batch = start_step + config.limit_batches
+    skip = 0
+    if isinstance(train_set, D.SyntheticBatches):
+        train_set.seek(start_step)
+    else:
+        skip = start_step
     t_start = time.time()
     for epoch in range(config.epoch_count):
-        if batch_count >= config.limit_batches:
+        if batch_count >= end_batch:
             break
         gen = iter(train_set)
-        while batch_count < config.limit_batches:
+        while skip > 0 and next(gen, None) is not None:
+            skip -= 1
+        while batch_count < end_batch:
             timers.start("batch")
             ev and ev.start("batch")
             timers.start("get_data")
@@ -177,14 +196,15 @@ def worker_process(config, distribute_model: Callable, reducer, experiment_name:
     values = torch.stack(losses).cpu().tolist() if losses else []
     with open(f"{stem}_loss.txt", "w") as f:
         for i, v in enumerate(values):
-            f.write(f"Worker {node_id}:{worker_id} loss for batch {i}: {v}\n")
+            f.write(f"Worker {node_id}:{worker_id} loss for batch {start_step + i}: {v}\n")
     rows = timers.rows()
     timers.writeout(f"{stem}_times.csv")
     if ev:
         ev.writeout(f"{stem}_device_times.csv")
     if getattr(config, "checkpoint", None):
-        save_checkpoint(config.checkpoint, model, optimizer, start_step + batch_count)
+        save_checkpoint(config.checkpoint, model, optimizer, batch_count)
     model.cleanup()
     if hasattr(reducer, "cleanup"):
         reducer.cleanup()
-    return {"losses": values, "rows": rows, "wall_s": wall, "batches": batch_count}
+    return {"losses": values, "rows": rows, "wall_s": wall, "batches": batch_count - start_step,
+            "start_step": start_step}

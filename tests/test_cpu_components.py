@@ -153,3 +153,109 @@ def test_stem_weight_packing_roundtrip_and_fold_equivalence():
     w4 = wp.float().reshape(64, 4, 4, 16).permute(0, 3, 1, 2)  # [co, 16, th, tw]
     got = F.conv2d(F.pad(xs, (2, 1, 2, 1)), w4)
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
+
+
+def _cli(tmp_path, sub, *extra, batches=3):
+    out = tmp_path / sub
+    out.mkdir(exist_ok=True)
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "distributed_learning_amd.main", "1", "0", "1", "1", "127.0.0.1", "lo", "mnist",
+           "/nonexistent", "0", "--experiment", "experiment_single", "--random_input", "1", "--limit_batches",
+           str(batches), "--batch_size", "8", "--master_port", str(__import__("dist_util").free_port()),
+           "--results_root", str(out), "--job_id", "t", *extra]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(out))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return [float(l.rsplit(": ", 1)[1]) for l in (out / "experiment_single_1_t" / "single_0_0_loss.txt").read_text()
+            .splitlines()], (out / "experiment_single_1_t" / "single_0_0_loss.txt").read_text().splitlines()
+
+
+def test_checkpoint_resume_continues_the_run(tmp_path):
+    """6 batches in one run == 3 batches + checkpoint + resumed 3 batches (same data stream, same
+    numbering, same weights)."""
+    full, _ = _cli(tmp_path, "full", batches=6)
+    ck = str(tmp_path / "ck.pt")
+    first, _ = _cli(tmp_path, "a", "--checkpoint", ck, batches=3)
+    second, lines = _cli(tmp_path, "b", "--resume", ck, batches=3)
+    assert lines[0].startswith("Worker 0:0 loss for batch 3: ")
+    assert first == full[:3]
+    assert second == pytest.approx(full[3:], rel=1e-5, abs=1e-6)
+
+
+def test_synthetic_seek():
+    s = SyntheticBatches(4, (3, 8, 8), 10, "cpu")
+    batches = [s.next()[0].clone() for _ in range(4)]
+    t = SyntheticBatches(4, (3, 8, 8), 10, "cpu")
+    t.seek(2)
+    assert torch.equal(t.next()[0], batches[2])
+
+
+# --- offline loaders on tiny fixtures written here (C24) -----------------------------------------
+def test_mnist_idx_loader(tmp_path):
+    import struct
+
+    from distributed_learning_amd.data import get_partition_loader, load_mnist
+
+    d = tmp_path / "mnist" / "MNIST" / "raw"
+    d.mkdir(parents=True)
+    imgs = (torch.arange(20 * 28 * 28) % 256).to(torch.uint8).reshape(20, 28, 28)
+    labels = (torch.arange(20) % 10).to(torch.uint8)
+    with open(d / "train-images-idx3-ubyte", "wb") as f:
+        f.write(struct.pack(">IIII", 0x0803, 20, 28, 28) + imgs.numpy().tobytes())
+    with open(d / "train-labels-idx1-ubyte", "wb") as f:
+        f.write(struct.pack(">II", 0x0801, 20) + labels.numpy().tobytes())
+    ds = load_mnist(str(tmp_path))
+    assert len(ds) == 20
+    x, y = ds[3]
+    assert x.shape == (1, 28, 28) and int(y) == 3
+    torch.testing.assert_close(x, (imgs[3].float() / 255.0 - 0.1307).unsqueeze(0) / 0.3081)
+    # partition semantics (reference data.py:26-68): 2 workers x 2 batches of 4 -> disjoint 8-sample sets
+    seen = []
+    for w in range(2):
+        dl = get_partition_loader(ds, 0, w, 2, 2, batch_size=4, num_workers=0)
+        got = [int(v) for xb, yb in dl for v in yb]
+        assert len(got) == 8
+        seen.append(dl.dataset.index.tolist())
+    assert not set(seen[0]) & set(seen[1])
+
+
+def test_cifar10_binary_loader(tmp_path):
+    from distributed_learning_amd.data import load_cifar10
+
+    d = tmp_path / "cifar-10-batches-bin"
+    d.mkdir()
+    rows = []
+    for i in range(5):
+        rec = torch.zeros(3073, dtype=torch.uint8)
+        rec[0] = i % 10
+        rec[1:] = (torch.arange(3072) + i) % 256
+        rows.append(rec)
+    blob = torch.stack(rows).numpy().tobytes()
+    for i in range(1, 6):
+        (d / f"data_batch_{i}.bin").write_bytes(blob)
+    ds = load_cifar10(str(tmp_path))
+    assert len(ds) == 25
+    x, y = ds[2]
+    assert x.shape == (3, 32, 32) and int(y) == 2
+    raw = ((torch.arange(3072) + 2) % 256).float().reshape(3, 32, 32) / 255.0
+    mean = torch.tensor([0.4914, 0.4822, 0.4465]).view(3, 1, 1)
+    std = torch.tensor([0.2470, 0.2435, 0.2616]).view(3, 1, 1)
+    torch.testing.assert_close(x, (raw - mean) / std)
+
+
+def test_imagefolder_loader(tmp_path):
+    PIL = pytest.importorskip("PIL.Image")
+    from distributed_learning_amd.data import ImageFolder, load_dataset
+
+    root = tmp_path / "ImageFolder"
+    for ci, c in enumerate(["cat", "dog"]):
+        (root / c).mkdir(parents=True)
+        for j in range(2):
+            img = PIL.new("RGB", (300, 260), color=(40 * ci + j, 100, 200))
+            img.save(root / c / f"{j}.png")
+    ds = load_dataset("imagenet", str(tmp_path))
+    assert isinstance(ds, ImageFolder) and ds.classes == ["cat", "dog"] and len(ds) == 4
+    x, y = ds[3]
+    assert x.shape == (3, 224, 224) and y == 1
+    want = (torch.tensor([41, 100, 200]) / 255.0 - torch.tensor([0.485, 0.456, 0.406])) / torch.tensor(
+        [0.229, 0.224, 0.225])
+    torch.testing.assert_close(x[:, 100, 100], want.float(), atol=1e-5, rtol=0)

@@ -26,10 +26,10 @@ def _run(tmp_path, model, experiment, *extra, batch=16, batches=3):
     return tmp_path / f"{experiment}_1_g"
 
 
-def _check(folder, exp, batches=3):
+def _check(folder, exp, batches=3, first=0):
     assert (folder / f"{exp}_config.txt").read_text().startswith("Namespace(")
     lines = (folder / f"{exp}_0_0_loss.txt").read_text().splitlines()
-    assert len(lines) == batches and lines[0].startswith("Worker 0:0 loss for batch 0: ")
+    assert len(lines) == batches and lines[0].startswith(f"Worker 0:0 loss for batch {first}: ")
     vals = [float(ln.rsplit(": ", 1)[1]) for ln in lines]
     assert all(v == v and abs(v) < 1e4 for v in vals), vals
     head = (folder / f"{exp}_0_0_times.csv").read_text().splitlines()[0]
@@ -59,4 +59,4 @@ def test_cli_single_checkpoint_resume(cuda, tmp_path):
     sub = tmp_path / "resume"
     sub.mkdir()
     folder2 = _run(sub, "resnet18", "experiment_single", "--resume", str(ck))
-    _check(folder2, "single")
+    _check(folder2, "single", first=3)  # the resumed run continues the batch sequence
