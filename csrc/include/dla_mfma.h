@@ -390,18 +390,117 @@ __device__ __forceinline__ void mainloop_glds(const LA& la, const LB& lb, int kb
   __syncthreads();  // every wave done with the stages before the epilogue reuses the LDS
 }
 
+// Optional per-k-step loader hook: loaders whose chunk addresses share wave-uniform per-k-step
+// terms (implicit-GEMM taps, weight-tap offsets) compute them once in step(k0), so src() is only
+// an add and a select per chunk instead of re-deriving the tap under an exec-masked branch.
+template <class L>
+__device__ __forceinline__ auto loader_step(L& l, int k0, int) -> decltype(l.step(k0), void()) {
+  l.step(k0);
+}
+template <class L>
+__device__ __forceinline__ void loader_step(L&, int, long) {}
+template <class L>
+__device__ __forceinline__ auto loader_src(const L& l, int i, int, int) -> decltype(l.src2(i)) {
+  return l.src2(i);
+}
+template <class L>
+__device__ __forceinline__ const void* loader_src(const L& l, int i, int k0, long) {
+  return l.src(i, k0);
+}
+
+// NS-stage LDS-DMA pipeline, v2 schedule (PIPE 4 = 2 stages, 5 = 3 stages): the next tile's DMA is
+// split around the two 32-deep MFMA clusters of a k-step (A-tile pieces before the first, B-tile
+// pieces between them) so the DMA issue no longer stalls the head of the k-step, per-k-step loader
+// terms are hoisted (loader_step), and each MFMA cluster runs at s_setprio 1 so a co-resident
+// wave's VALU/DMA issue does not preempt it (cdna_hip_programming.md T5). Same LDS images, same
+// counted-vmcnt + raw-barrier protocol as mainloop_glds.
+template <int BM, int BN, int NT, int NS, class LA, class LB>
+__device__ __forceinline__ void mainloop_glds2(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
+                                               char* smem) {
+  static_assert(NS == 2 || NS == 3, "2 or 3 stages");
+  static_assert(LA::kNT == NT && LB::kNT == NT, "loaders built for another block size");
+  using GA = TileGeom<BM, NT>;
+  using GB = TileGeom<BN, NT>;
+  using AC = Acc<BM, BN, NT>;
+  constexpr int L = GA::CH + GB::CH;  // DMA instructions per wave per tile
+  constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
+  constexpr int SA = BM * kBK, SB = BN * kBK;  // elements per stage
+  bf16_t* base = reinterpret_cast<bf16_t*>(smem);
+  const int wave = threadIdx.x >> 6, wr = wave / AC::WGN, wc = wave % AC::WGN;
+  const uint32_t lds0 = lds_addr(smem);
+  const uint32_t wofs = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
+  const int nk = (kend - kbeg + kBK - 1) / kBK;
+  if (nk <= 0) return;
+  LA pa = la;
+  LB pb = lb;
+  pa.prep();
+  pb.prep();
+  auto issue_a = [&](int t) {
+    const int k0 = kbeg + t * kBK;
+    loader_step(pa, k0, 0);
+    const uint32_t a_base = lds0 + (uint32_t)((t % NS) * (SA + SB)) * 2u + wofs;
+#pragma unroll
+    for (int i = 0; i < GA::CH; ++i) glds16(loader_src(pa, i, k0, 0), a_base + (uint32_t)(i * NT * 16));
+  };
+  auto issue_b = [&](int t) {
+    const int k0 = kbeg + t * kBK;
+    loader_step(pb, k0, 0);
+    const uint32_t b_base = lds0 + (uint32_t)((t % NS) * (SA + SB) + SA) * 2u + wofs;
+#pragma unroll
+    for (int i = 0; i < GB::CH; ++i) glds16(loader_src(pb, i, k0, 0), b_base + (uint32_t)(i * NT * 16));
+  };
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) {
+      issue_a(p);
+      issue_b(p);
+    }
+  for (int t = 0; t < nk; ++t) {
+    if constexpr (NS == 3) {
+      if (t + 1 < nk) vm_wait<L>();
+      else vm_wait<0>();
+    } else {
+      vm_wait<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR on the stage the next DMA overwrites
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const bool more = t + NS - 1 < nk;
+    if (more) issue_a(t + NS - 1);
+    const bf16_t* As = base + (t % NS) * (SA + SB);
+    const bf16_t* Bs = As + SA;
+#pragma unroll
+    for (int kk = 0; kk < kBK / 32; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = glds_frag<BM, LA>(As, wr * WM + i * 16, kk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag<BN, LB>(Bs, wc * WN + j * 16, kk);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma16(af[i], bfr[j], acc.v[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      if (kk == 0 && more) issue_b(t + NS - 1);
+    }
+  }
+  __syncthreads();  // every wave done with the stages before the epilogue reuses the LDS
+}
+
 // Pipeline selection shared by all MFMA kernels: 0 = register staging (one k-step in flight,
-// 3 blocks/CU), 2 / 3 = LDS-DMA with 2 / 3 stages.
+// 3 blocks/CU), 2 / 3 = LDS-DMA with 2 / 3 stages, 4 / 5 = the v2 LDS-DMA schedule with 2 / 3 stages.
 template <int PIPE, int BM, int BN, int NT, class LA, class LB>
 __device__ __forceinline__ void run_mainloop(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
                                              char* smem) {
   if constexpr (PIPE == 0) mainloop<BM, BN, NT>(la, lb, kbeg, kend, acc, smem);
+  else if constexpr (PIPE >= 4) mainloop_glds2<BM, BN, NT, PIPE - 2>(la, lb, kbeg, kend, acc, smem);
   else mainloop_glds<BM, BN, NT, PIPE>(la, lb, kbeg, kend, acc, smem);
 }
 
 template <int PIPE, int BM, int BN, class LA, class LB>
 __host__ __device__ constexpr size_t run_mainloop_lds_bytes() {
-  return PIPE == 0 ? mainloop_lds_bytes<BM, BN, LA, LB>() : glds_lds_bytes<BM, BN, PIPE>();
+  return PIPE == 0 ? mainloop_lds_bytes<BM, BN, LA, LB>() : glds_lds_bytes<BM, BN, (PIPE >= 4 ? PIPE - 2 : PIPE)>();
 }
 
 // ---- epilogues -------------------------------------------------------------------------------

@@ -102,6 +102,20 @@ struct Im2colRowLoader {
     const int64_t off = (int64_t)(kFlip ? -shift : shift) * C + (k0 - tap * C);
     return ((smask[i] >> tap) & 1u) ? (const void*)(sp[i] + off) : zero_src();
   }
+  // v2 pipeline: the tap offset and tap bit of a k-step, once per k-step (src2 = add + select)
+  int64_t koff = 0;
+  uint32_t kbit = 0;
+  __device__ void step(int k0) {
+    const int tap = k0 / C;
+    const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+    const int shift = kh * Wd + kw;
+    koff = (int64_t)(kFlip ? -shift : shift) * C + (k0 - tap * C);
+    kbit = 1u << tap;
+  }
+  __device__ const void* src2(int i) const {
+    const bf16_t* p = sp[i] + koff;
+    return (smask[i] & kbit) ? (const void*)p : zero_src();
+  }
 };
 
 // B operand of dgrad: k = (tap, co) rows, n = ci columns, element W[co][tap][ci] (k-major per tap).
@@ -135,6 +149,12 @@ struct WeightTapKLoader {
     const int64_t off = ((int64_t)(k0 - tap * Cout) * 9 + tap) * Cin;
     return sok[i] ? (const void*)(sp[i] + off) : zero_src();
   }
+  int64_t koff = 0;
+  __device__ void step(int k0) {
+    const int tap = k0 / Cout;
+    koff = ((int64_t)(k0 - tap * Cout) * 9 + tap) * Cin;
+  }
+  __device__ const void* src2(int i) const { return sok[i] ? (const void*)(sp[i] + koff) : zero_src(); }
 };
 
 // ---- stride-2 data gradient ----------------------------------------------------------------------
@@ -457,6 +477,7 @@ static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGe
     switch (mfma_pipeline_for(9 * g.Cin)) {
       case 0: launch_fwd_p<BM, BN, S, 0, kThreads>(x, w, y, g, stats, stream); break;
       case 3: launch_fwd_p<BM, BN, S, 3, kThreads>(x, w, y, g, stats, stream); break;
+      case 4: launch_fwd_p<BM, BN, S, 4, kThreads>(x, w, y, g, stats, stream); break;
       default: launch_fwd_p<BM, BN, S, 2, kThreads>(x, w, y, g, stats, stream); break;
     }
   }
@@ -513,6 +534,7 @@ static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const Co
     switch (mfma_pipeline_for(9 * g.Cout)) {
       case 0: launch_dgrad_p<BM, BN, 0, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
       case 3: launch_dgrad_p<BM, BN, 3, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
+      case 4: launch_dgrad_p<BM, BN, 4, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
       default: launch_dgrad_p<BM, BN, 2, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
     }
   }
@@ -589,6 +611,7 @@ void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int spl
   switch (mfma_pipeline_for(kps)) {     \
     case 0: DLA_WG(BM_, 0); break;      \
     case 3: DLA_WG(BM_, 3); break;      \
+    case 4: DLA_WG(BM_, 4); break;      \
     default: DLA_WG(BM_, 2); break;     \
   }
   if (Cout <= 64) {

@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // two k-steps, nothing to overlap, and the register-staged loop's third resident block wins.
 // 3 stages (96 KB of LDS, 1 block/CU) never won at ResNet shapes.
 static int g_pipe = -1;
-void set_mfma_pipeline(int p) { g_pipe = (p == 0 || p == 2 || p == 3) ? p : -1; }
+void set_mfma_pipeline(int p) { g_pipe = (p == 0 || p == 2 || p == 3 || p == 4 || p == 5) ? p : -1; }
 int mfma_pipeline() { return g_pipe; }
 int mfma_pipeline_for(int K) { return g_pipe >= 0 ? g_pipe : (K >= 256 ? 2 : 0); }
 
@@ -155,6 +155,7 @@ static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb
     switch (mfma_pipeline_for(K)) {
       case 0: launch_nt_p<BM, BN, S, BT, 0, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
       case 3: launch_nt_p<BM, BN, S, BT, 3, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
+      case 4: launch_nt_p<BM, BN, S, BT, 4, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
       default: launch_nt_p<BM, BN, S, BT, 2, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
     }
   }
@@ -246,6 +247,7 @@ void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, floa
   switch (mfma_pipeline_for(kps)) {        \
     case 0: DLA_TN(BM_, BN_, 0); break;    \
     case 3: DLA_TN(BM_, BN_, 3); break;    \
+    case 4: DLA_TN(BM_, BN_, 4); break;    \
     default: DLA_TN(BM_, BN_, 2); break;   \
   }
   if (bm == 64 && bn == 64) {

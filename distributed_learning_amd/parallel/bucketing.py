@@ -9,6 +9,10 @@ oversize tensor gets its own bucket) and ``grouping_size = 0`` yields one parame
 MI355X layout: each bucket owns ONE flat device buffer; every gradient slot starts on a 64-element
 boundary (256 B for fp32), so the pack/unpack/SGD kernels always take their 16-byte vector path
 and gradients can alias the bucket buffer directly (``grad_as_bucket_view``: no pack/unpack copy).
+
+Which cap to use on MI355X is derived, not copied from the reference's 25 MiB: see
+:mod:`.cost_model` (collective time on 7 xGMI links vs the backward time left after each bucket
+becomes ready).
 """
 from __future__ import annotations
 
