@@ -123,6 +123,9 @@ def main():
 
         model.sync.executor = NativeStreamExecutor(reducer.engine, a.algorithm, passthrough=False)
         model.sync.passthrough = False
+        reducer.engine.impl.set_force(True)  # the N>1 data path incl. fp32 staging, as a 1-rank collective
+        reducer.engine.set_accum_fp32(True)
+        model.sync.executor.reserve(model.sync.buckets)
     opt = FusedSGD(model.module.parameters(), lr=a.lr, momentum=a.momentum, master_weights=bf16)
     data = SyntheticBatches(a.batch, spec.input_shape, spec.num_classes, dev,
                             dtype=torch.bfloat16 if bf16 else torch.float32,

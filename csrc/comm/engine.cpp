@@ -171,6 +171,12 @@ class CommEngine {
   int local_size() const { return topo_.L(); }
   int num_rings() const { return (int)std::max<size_t>(1, topo_.rings.size()); }
   void set_accum_fp32(bool on) { accum_fp32_ = on; }
+  // Run the whole N>1 data path (gather, fp32 staging, RCCL collective, cast back) even on one rank
+  // (tests / the bench's --force_comm): at world 1 it becomes a 1-rank ncclAllReduce.
+  void set_force(bool on) {
+    force_ = on;
+    plans_.clear();
+  }
   bool accum_fp32() const { return accum_fp32_; }
 
   // ---------------------------------------------------------------------------------------
@@ -388,10 +394,23 @@ class CommEngine {
     } catch (const std::exception& e) {
       TORCH_CHECK(false, e.what());
     }
+    if (force_ && topo_.world == 1) {
+      // diagnostic single-rank run of the full data path: one ncclAllReduce over the 1-rank comm
+      comm::Step st;
+      comm::Op o;
+      o.kind = comm::kColl;
+      o.coll = comm::kAllReduce;
+      o.comm = comm::kWorld;
+      o.nsrc = 1;
+      o.count = n;
+      o.average = true;
+      st.ops.push_back(o);
+      p.steps.push_back(st);
+    }
     return plans_.emplace(key, std::move(p)).first->second;
   }
 
-  bool staged(int algo, int dtype) const { return accum_fp32_ && dtype == kBF16 && topo_.world > 1; }
+  bool staged(int algo, int dtype) const { return accum_fp32_ && dtype == kBF16 && (topo_.world > 1 || force_); }
 
   size_t scratch_bytes(const Plan& p, int64_t n, int dtype) const {
     const bool st = staged(p.algo, dtype);
@@ -430,7 +449,7 @@ class CommEngine {
     if (needs_reduce_kernel(algo))
       TORCH_CHECK(flat.scalar_type() == at::kFloat || flat.scalar_type() == at::kBFloat16,
                   "custom all-reduce algorithms support fp32/bf16 only");
-    if (topo_.world == 1 || n == 0) {  // reference short-circuit (allreduce.py:18-19,55-56)
+    if ((topo_.world == 1 && !force_) || n == 0) {  // reference short-circuit (allreduce.py:18-19,55-56)
       if (grads) pack_tensors_on(*grads, *offsets, flat, 1.f, st);
       return;
     }
@@ -515,6 +534,7 @@ class CommEngine {
   ncclComm_t comm_ = nullptr, intra_ = nullptr, inter_ = nullptr;
   bool aborted_ = false;
   bool accum_fp32_ = false;
+  bool force_ = false;
   std::unique_ptr<c10::hip::HIPStream> stream_;
   std::map<std::pair<int, int64_t>, Plan> plans_;
   at::Tensor scratch_;
@@ -677,6 +697,7 @@ void bind_comm(pybind11::module& m) {
       .def("local_size", &CommEngine::local_size)
       .def("num_rings", &CommEngine::num_rings)
       .def("set_accum_fp32", &CommEngine::set_accum_fp32)
+      .def("set_force", &CommEngine::set_force)
       .def("accum_fp32", &CommEngine::accum_fp32)
       .def("join_current", &CommEngine::join_current)
       .def("wait_on_current", &CommEngine::wait_on_current)

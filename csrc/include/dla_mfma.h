@@ -49,6 +49,33 @@ __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// MFMA shape of every GEMM / conv main loop (build-time: -DDLA_MFMA_SHAPE=32 selects
+// v_mfma_f32_32x32x16_bf16; default v_mfma_f32_16x16x32_bf16). Same wave tiles and LDS images;
+// a 32x32x16 MFMA issues half as many instructions for the same work, so per k-step a wave leaves
+// 3x more vector-issue slots free for address / epilogue VALU (MI355X_MICROARCH.md cycle table).
+#ifndef DLA_MFMA_SHAPE
+#define DLA_MFMA_SHAPE 16
+#endif
+constexpr int kMS = DLA_MFMA_SHAPE;       // output tile edge of one MFMA
+constexpr int kKS = 512 / kMS;            // K of one MFMA (32 or 16)
+constexpr int kAccN = kMS * kMS / 64;     // fp32 accumulators per lane (4 or 16)
+static_assert(kMS == 16 || kMS == 32, "MFMA shape 16 or 32");
+typedef float accv_t __attribute__((ext_vector_type(kAccN)));
+__device__ __forceinline__ accv_t mfma(const bf16x8_t& a, const bf16x8_t& b, const accv_t& c) {
+#if DLA_MFMA_SHAPE == 16
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+// C/D fragment position of accumulator register `reg` of `lane` (16x16x32: col = lane & 15,
+// row = 4 * (lane >> 4) + reg; 32x32x16: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5))
+__device__ __forceinline__ int acc_row(int lane, int reg) {
+  if constexpr (kMS == 16) return 4 * (lane >> 4) + reg;
+  else return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+}
+__device__ __forceinline__ int acc_col(int lane) { return lane & (kMS - 1); }
+
 __device__ __forceinline__ ushort8_t zero8() { return ushort8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
 
 // k-major image (rows = k, W = 64 or 128 columns, unpadded rows). A 32-lane half of a transposed
@@ -59,6 +86,12 @@ __device__ __forceinline__ ushort8_t zero8() { return ushort8_t{0, 0, 0, 0, 0, 0
 template <int W>
 __device__ __forceinline__ int tr_sw(int row) {  // XOR applied to the 8-byte chunk index of a row
   static_assert(W == 64 || W == 128 || W == 256, "tr image width");
+  if constexpr (kMS == 32) {
+    // 32x32x16 transposed reads: a 32-lane half touches rows {r..r+3} x 8 consecutive chunks; give
+    // the 4 rows disjoint 8-chunk windows (64-B rows pair up in a bank row at W = 64)
+    if constexpr (W >= 128) return 8 * (row & 3);
+    else return 8 * ((row >> 1) & 1);
+  }
   // 256 columns (512 B rows): every row starts on bank 0 as with 128, so the same XOR pattern
   // (it stays inside each 32-chunk half) keeps the transposed reads conflict-free
   if constexpr (W >= 128)
@@ -125,6 +158,69 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// ---- buffer LDS-DMA (buffer_load_dwordx4 ... offen lds) -----------------------------------------
+// The v3 pipeline (PIPE 6 / 7) addresses operands through a buffer resource descriptor: each chunk
+// slot keeps ONE 32-bit byte offset for the whole block (VGPR), the k-step advance is a scalar
+// soffset, and out-of-range slots carry an offset past num_records so the hardware returns zeros.
+// Per k-step a RowLoader / KLoader operand then costs no VALU at all (the global_load_lds form
+// needs a 64-bit add and two selects per chunk), which is what makes the MFMA loop issue-bound
+// otherwise: two 4-wave blocks per CU spend ~1 vector-issue slot of every 2 on address math.
+constexpr uint32_t kOOB = 0x80000000u;  // every operand is < 2 GiB (checked on the host)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// CH slots, LDS destination of slot i = lds + i * STRIDE (wave-uniform), one statement: M0 saved
+// once, written per slot (s_nop 0 before each DMA), restored; s_nop 4 lets a freshly computed
+// scalar soffset settle before the first buffer op reads it.
+template <int CH, int STRIDE>
+__device__ __forceinline__ void bglds(const uint32_t (&vo)[CH], __amdgpu_buffer_rsrc_t srd, uint32_t soff,
+                                      uint32_t lds) {
+  uint32_t keep;
+  if constexpr (CH == 1) {
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep) : "v"(vo[0]), "s"(srd), "s"(lds), "s"(soff) : "memory");
+  } else if constexpr (CH == 2) {
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %3, %5 offen lds\n\t"
+        "s_add_u32 m0, m0, %6\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %5 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep) : "v"(vo[0]), "v"(vo[1]), "s"(srd), "s"(lds), "s"(soff), "i"(STRIDE) : "memory");
+  } else if constexpr (CH == 4) {
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %5, %7 offen lds\n\t"
+        "s_add_u32 m0, m0, %8\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %5, %7 offen lds\n\t"
+        "s_add_u32 m0, m0, %8\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %5, %7 offen lds\n\t"
+        "s_add_u32 m0, m0, %8\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %5, %7 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "s"(srd), "s"(lds), "s"(soff), "i"(STRIDE)
+        : "memory");
+  } else {
+    static_assert(CH == 8, "1, 2, 4 or 8 slots");
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %10\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %9, %11 offen lds\n\t"
+        "s_add_u32 m0, m0, %12\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %9, %11 offen lds\n\t"
+        "s_add_u32 m0, m0, %12\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %9, %11 offen lds\n\t"
+        "s_add_u32 m0, m0, %12\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %9, %11 offen lds\n\t"
+        "s_add_u32 m0, m0, %12\n\ts_nop 0\n\tbuffer_load_dwordx4 %5, %9, %11 offen lds\n\t"
+        "s_add_u32 m0, m0, %12\n\ts_nop 0\n\tbuffer_load_dwordx4 %6, %9, %11 offen lds\n\t"
+        "s_add_u32 m0, m0, %12\n\ts_nop 0\n\tbuffer_load_dwordx4 %7, %9, %11 offen lds\n\t"
+        "s_add_u32 m0, m0, %12\n\ts_nop 0\n\tbuffer_load_dwordx4 %8, %9, %11 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "v"(vo[5]), "v"(vo[6]), "v"(vo[7]),
+          "s"(srd), "s"(lds), "s"(soff), "i"(STRIDE)
+        : "memory");
+  }
+}
+
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
@@ -167,6 +263,23 @@ struct RowLoader {
   __device__ const void* src(int i, int k0) const {
     return (k0 + skc[i] < K) ? (const void*)(sp[i] + k0) : zero_src();
   }
+  // buffer form (PIPE 6/7): byte offset of slot i at k0 = 0; soffset = 2 * k0
+  uint32_t bvo[CH];
+  __amdgpu_buffer_rsrc_t bsrd;
+  __device__ void bprep() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + i * NT, r = c >> 3, kc = rm_glds_kc(c);
+      const int64_t gr = row0 + r;
+      bvo[i] = gr < rows ? (uint32_t)((gr * ld + kc) * 2) : kOOB;
+    }
+    bsrd = make_srd(p, (uint32_t)(rows * ld * 2));
+  }
+  __device__ uint32_t bsoff(int k0) const { return (uint32_t)k0 * 2u; }
+  __device__ bool bcheck(int k0) const { return k0 + kBK > K; }  // K tail: per-slot k bound
+  __device__ uint32_t bvoff_chk(int i, int k0) const {
+    return (k0 + rm_glds_kc(threadIdx.x + i * NT) < K) ? bvo[i] : kOOB;
+  }
 };
 
 // k-major matrix [K][cols] (cols contiguous): gemm_tn operands, dgrad weights as stored.
@@ -199,6 +312,23 @@ struct KLoader {
   __device__ const void* src(int i, int k0) const {
     return (k0 + skr[i] < kend) ? (const void*)(sp[i] + (int64_t)k0 * ld) : zero_src();
   }
+  // buffer form (PIPE 6/7): byte offset of slot i at k0 = 0; soffset = 2 * k0 * ld
+  uint32_t bvo[CH];
+  __amdgpu_buffer_rsrc_t bsrd;
+  __device__ void bprep() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + i * NT, kr = c / TileGeom<W>::KPR;
+      const int gc = col0 + km_glds_col<W>(c);
+      bvo[i] = gc < cols ? (uint32_t)(((int64_t)kr * ld + gc) * 2) : kOOB;
+    }
+    bsrd = make_srd(p, (uint32_t)((int64_t)kend * ld * 2));
+  }
+  __device__ uint32_t bsoff(int k0) const { return (uint32_t)((int64_t)k0 * ld * 2); }
+  __device__ bool bcheck(int k0) const { return k0 + kBK > kend; }
+  __device__ uint32_t bvoff_chk(int i, int k0) const {
+    return (k0 + (threadIdx.x + i * NT) / TileGeom<W>::KPR < kend) ? bvo[i] : kOOB;
+  }
 };
 
 // ---- main loop -----------------------------------------------------------------------------------
@@ -210,14 +340,14 @@ __host__ __device__ constexpr int waves_n(int BM, int BN, int NT) { return (BN <
 template <int BM, int BN, int NT = kThreads>
 struct Acc {
   static constexpr int kNT = NT, WGN = waves_n(BM, BN, NT), WGM = NT / 64 / WGN;  // waves along N / M
-  static constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
+  static constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / kMS, TN = WN / kMS;
   static_assert(TM >= 1 && TN >= 1, "wave tile below one MFMA fragment");
-  f32x4_t v[TM][TN];
+  accv_t v[TM][TN];
   __device__ void zero() {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) v[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < TN; ++j) v[i][j] = accv_t{};
   }
 };
 
@@ -239,17 +369,25 @@ __device__ __forceinline__ void tile_store(bf16_t* s, const ushort8_t (&r)[TileG
   }
 }
 
-// 16 x 32 operand fragment for MFMA rows/cols [r0, r0 + 16) at k offset kk*32.
+// kMS x kKS operand fragment for MFMA rows/cols [r0, r0 + kMS) at k offset kk * kKS.
 template <int W, class L>
 __device__ __forceinline__ bf16x8_t tile_frag(const bf16_t* s, int r0, int kk) {
   const int lane = threadIdx.x & 63;
   if constexpr (L::kKMajor) {
-    // lane 4q+p of 16-lane group g reads k-row 8g+q (and +4), columns r0+4p..+3 (T10)
+    // lane 4q+p of 16-lane group g reads k-rows (kbase + q, + 4), columns c + 4p..+3 (T10)
     const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-    const int kr = kk * 32 + 8 * g + q, cn = r0 + 4 * p;
+    int kr, cn;
+    if constexpr (kMS == 16) {
+      kr = kk * 32 + 8 * g + q;
+      cn = r0 + 4 * p;
+    } else {
+      kr = kk * 16 + 8 * (g >> 1) + q;
+      cn = r0 + 16 * (g & 1) + 4 * p;
+    }
     return tr_frag(s + tr_off<W>(kr, cn), s + tr_off<W>(kr + 4, cn));
   } else {
-    return *reinterpret_cast<const bf16x8_t*>(s + (r0 + (lane & 15)) * (kBK + 8) + kk * 32 + 8 * (lane >> 4));
+    return *reinterpret_cast<const bf16x8_t*>(s + (r0 + (lane & (kMS - 1))) * (kBK + 8) + kk * kKS +
+                                              8 * (lane / kMS));
   }
 }
 
@@ -281,16 +419,16 @@ __device__ __forceinline__ void mainloop(const LA& la, const LB& lb, int kbeg, i
   for (int t = 0; t < nk; ++t) {
     if (t + 1 < nk) gload(kbeg + (t + 1) * kBK);  // next tile in flight during this tile's MFMAs
 #pragma unroll
-    for (int kk = 0; kk < kBK / 32; ++kk) {
+    for (int kk = 0; kk < kBK / kKS; ++kk) {
       bf16x8_t af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = tile_frag<BM, LA>(As, wr * WM + i * 16, kk);
+      for (int i = 0; i < TM; ++i) af[i] = tile_frag<BM, LA>(As, wr * WM + i * kMS, kk);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = tile_frag<BN, LB>(Bs, wc * WN + j * 16, kk);
+      for (int j = 0; j < TN; ++j) bfr[j] = tile_frag<BN, LB>(Bs, wc * WN + j * kMS, kk);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma16(af[i], bfr[j], acc.v[i][j]);
+        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
     }
     __syncthreads();
     if (t + 1 < nk) {
@@ -304,7 +442,7 @@ __device__ __forceinline__ void mainloop(const LA& la, const LB& lb, int kbeg, i
 // 16 x 32 row-major operand fragment from the LDS-DMA image (see the image map above)
 __device__ __forceinline__ bf16x8_t rm_glds_frag(const bf16_t* s, int r0, int kk) {
   const int lane = threadIdx.x & 63;
-  const int r = r0 + (lane & 15), lc = kk * 4 + (lane >> 4);
+  const int r = r0 + (lane & (kMS - 1)), lc = kk * (kKS / 8) + lane / kMS;
   return *reinterpret_cast<const bf16x8_t*>(s + r * kBK + ((lc ^ ((r >> 1) & 7)) << 3));
 }
 
@@ -375,16 +513,16 @@ __device__ __forceinline__ void mainloop_glds(const LA& la, const LB& lb, int kb
     const bf16_t* As = base + (t % NS) * (SA + SB);
     const bf16_t* Bs = As + SA;
 #pragma unroll
-    for (int kk = 0; kk < kBK / 32; ++kk) {
+    for (int kk = 0; kk < kBK / kKS; ++kk) {
       bf16x8_t af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = glds_frag<BM, LA>(As, wr * WM + i * 16, kk);
+      for (int i = 0; i < TM; ++i) af[i] = glds_frag<BM, LA>(As, wr * WM + i * kMS, kk);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag<BN, LB>(Bs, wc * WN + j * 16, kk);
+      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag<BN, LB>(Bs, wc * WN + j * kMS, kk);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma16(af[i], bfr[j], acc.v[i][j]);
+        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
     }
   }
   __syncthreads();  // every wave done with the stages before the epilogue reuses the LDS
@@ -470,17 +608,106 @@ __device__ __forceinline__ void mainloop_glds2(const LA& la, const LB& lb, int k
     const bf16_t* As = base + (t % NS) * (SA + SB);
     const bf16_t* Bs = As + SA;
 #pragma unroll
-    for (int kk = 0; kk < kBK / 32; ++kk) {
+    for (int kk = 0; kk < kBK / kKS; ++kk) {
       bf16x8_t af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = glds_frag<BM, LA>(As, wr * WM + i * 16, kk);
+      for (int i = 0; i < TM; ++i) af[i] = glds_frag<BM, LA>(As, wr * WM + i * kMS, kk);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag<BN, LB>(Bs, wc * WN + j * 16, kk);
+      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag<BN, LB>(Bs, wc * WN + j * kMS, kk);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma16(af[i], bfr[j], acc.v[i][j]);
+        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      if (kk == 0 && more) issue_b(t + NS - 1);
+    }
+  }
+  __syncthreads();  // every wave done with the stages before the epilogue reuses the LDS
+}
+
+// v3 schedule (PIPE 6 = 2 stages, 7 = 3 stages): mainloop_glds2's structure with the buffer-form
+// DMA (bglds): per k-step an operand costs one scalar soffset and, only where a slot can fall out
+// of range this step (K tail, conv padding taps), one select per slot.
+template <class L, int W, int NT>
+__device__ __forceinline__ void bissue(const L& l, int k0, uint32_t lds) {
+  constexpr int CH = TileGeom<W, NT>::CH;
+  uint32_t vo[CH];
+  if (l.bcheck(k0)) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) vo[i] = l.bvoff_chk(i, k0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) vo[i] = l.bvo[i];
+  }
+  bglds<CH, NT * 16>(vo, l.bsrd, (uint32_t)__builtin_amdgcn_readfirstlane(l.bsoff(k0)), lds);
+}
+
+template <int BM, int BN, int NT, int NS, class LA, class LB>
+__device__ __forceinline__ void mainloop_bglds(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
+                                               char* smem) {
+  static_assert(NS == 2 || NS == 3, "2 or 3 stages");
+  static_assert(LA::kNT == NT && LB::kNT == NT, "loaders built for another block size");
+  using GA = TileGeom<BM, NT>;
+  using GB = TileGeom<BN, NT>;
+  using AC = Acc<BM, BN, NT>;
+  constexpr int L = GA::CH + GB::CH;  // DMA instructions per wave per tile
+  constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
+  constexpr int SA = BM * kBK, SB = BN * kBK;  // elements per stage
+  bf16_t* base = reinterpret_cast<bf16_t*>(smem);
+  const int wave = threadIdx.x >> 6, wr = wave / AC::WGN, wc = wave % AC::WGN;
+  const uint32_t lds0 = lds_addr(smem);
+  const uint32_t wofs = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
+  const int nk = (kend - kbeg + kBK - 1) / kBK;
+  if (nk <= 0) return;
+  LA pa = la;
+  LB pb = lb;
+  pa.prep();
+  pb.prep();
+  pa.bprep();
+  pb.bprep();
+  auto issue_a = [&](int t) {
+    const int k0 = kbeg + t * kBK;
+    loader_step(pa, k0, 0);
+    bissue<LA, BM, NT>(pa, k0, lds0 + (uint32_t)((t % NS) * (SA + SB)) * 2u + wofs);
+  };
+  auto issue_b = [&](int t) {
+    const int k0 = kbeg + t * kBK;
+    loader_step(pb, k0, 0);
+    bissue<LB, BN, NT>(pb, k0, lds0 + (uint32_t)((t % NS) * (SA + SB) + SA) * 2u + wofs);
+  };
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) {
+      issue_a(p);
+      issue_b(p);
+    }
+  for (int t = 0; t < nk; ++t) {
+    if constexpr (NS == 3) {
+      if (t + 1 < nk) vm_wait<L>();
+      else vm_wait<0>();
+    } else {
+      vm_wait<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR on the stage the next DMA overwrites
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const bool more = t + NS - 1 < nk;
+    if (more) issue_a(t + NS - 1);
+    const bf16_t* As = base + (t % NS) * (SA + SB);
+    const bf16_t* Bs = As + SA;
+#pragma unroll
+    for (int kk = 0; kk < kBK / kKS; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = glds_frag<BM, LA>(As, wr * WM + i * kMS, kk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag<BN, LB>(Bs, wc * WN + j * kMS, kk);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
       __builtin_amdgcn_s_setprio(0);
       if (kk == 0 && more) issue_b(t + NS - 1);
     }
@@ -489,18 +716,21 @@ __device__ __forceinline__ void mainloop_glds2(const LA& la, const LB& lb, int k
 }
 
 // Pipeline selection shared by all MFMA kernels: 0 = register staging (one k-step in flight,
-// 3 blocks/CU), 2 / 3 = LDS-DMA with 2 / 3 stages, 4 / 5 = the v2 LDS-DMA schedule with 2 / 3 stages.
+// 3 blocks/CU), 2 / 3 = LDS-DMA with 2 / 3 stages, 4 / 5 = the v2 LDS-DMA schedule with 2 / 3 stages,
+// 6 / 7 = the v3 buffer-DMA schedule with 2 / 3 stages (loaders with a buffer form only).
 template <int PIPE, int BM, int BN, int NT, class LA, class LB>
 __device__ __forceinline__ void run_mainloop(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
                                              char* smem) {
   if constexpr (PIPE == 0) mainloop<BM, BN, NT>(la, lb, kbeg, kend, acc, smem);
+  else if constexpr (PIPE >= 6) mainloop_bglds<BM, BN, NT, PIPE - 4>(la, lb, kbeg, kend, acc, smem);
   else if constexpr (PIPE >= 4) mainloop_glds2<BM, BN, NT, PIPE - 2>(la, lb, kbeg, kend, acc, smem);
   else mainloop_glds<BM, BN, NT, PIPE>(la, lb, kbeg, kend, acc, smem);
 }
 
 template <int PIPE, int BM, int BN, class LA, class LB>
 __host__ __device__ constexpr size_t run_mainloop_lds_bytes() {
-  return PIPE == 0 ? mainloop_lds_bytes<BM, BN, LA, LB>() : glds_lds_bytes<BM, BN, (PIPE >= 4 ? PIPE - 2 : PIPE)>();
+  return PIPE == 0 ? mainloop_lds_bytes<BM, BN, LA, LB>()
+                   : glds_lds_bytes<BM, BN, (PIPE >= 6 ? PIPE - 4 : (PIPE >= 4 ? PIPE - 2 : PIPE))>();
 }
 
 // ---- epilogues -------------------------------------------------------------------------------
@@ -569,16 +799,17 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
   using AC = Acc<BM, BN, NT>;
   constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
   constexpr int LDS_C = BN + 8;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN, fr = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN,
+            fr = acc_col(lane);
   bf16_t* Cs = reinterpret_cast<bf16_t*>(smem);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = wr * WM + i * 16 + (lane >> 4) * 4 + r;
-        const int n = wc * WN + j * 16 + fr;
+      for (int r = 0; r < kAccN; ++r) {
+        const int m = wr * WM + i * kMS + acc_row(lane, r);
+        const int n = wc * WN + j * kMS + fr;
         const bf16_t h = f32_to_bf16(acc.v[i][j][r]);
         Cs[m * LDS_C + n] = h;
         if constexpr (kStats) {
@@ -689,17 +920,20 @@ __device__ __forceinline__ void stats_flush(ColStats<BM, BN, NT>& st, float* __r
                                             char* smem) {
   using AC = Acc<BM, BN, NT>;
   constexpr int WN = AC::WN, TN = AC::TN;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN, fr = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN,
+            fr = acc_col(lane);
   float* red = reinterpret_cast<float*>(smem);  // [WGM wr][BN][2]
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     float a = st.s[j], b = st.q[j];
-    a += __shfl_xor(a, 16, kWave);
-    b += __shfl_xor(b, 16, kWave);
+    if constexpr (kMS == 16) {
+      a += __shfl_xor(a, 16, kWave);
+      b += __shfl_xor(b, 16, kWave);
+    }
     a += __shfl_xor(a, 32, kWave);
     b += __shfl_xor(b, 32, kWave);
-    if (lane < 16) {
-      const int n = wc * WN + j * 16 + fr;
+    if (lane < kMS) {
+      const int n = wc * WN + j * kMS + fr;
       red[(wr * BN + n) * 2 + 0] = a;
       red[(wr * BN + n) * 2 + 1] = b;
     }
@@ -723,15 +957,16 @@ __device__ __forceinline__ void epilogue_f32(const Acc<BM, BN, NT>& acc, float* 
                                              int m0, int n0) {
   using AC = Acc<BM, BN, NT>;
   constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN, fr = lane & 15;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN,
+            fr = acc_col(lane);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr * WM + i * 16 + (lane >> 4) * 4 + r;
-        const int n = n0 + wc * WN + j * 16 + fr;
+      for (int r = 0; r < kAccN; ++r) {
+        const int m = m0 + wr * WM + i * kMS + acc_row(lane, r);
+        const int n = n0 + wc * WN + j * kMS + fr;
         if (m < Mo && n < No) P[(int64_t)m * No + n] = acc.v[i][j][r];
       }
 }

@@ -52,6 +52,7 @@ struct Im2colRowLoader {
   uint32_t smask[CH];
   __device__ void init(const ConvGeom& g, int64_t row0, int64_t P, int oh_dim, int ow_dim, const FastDiv& fw,
                        const FastDiv& fh) {
+    N_img = g.N;
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const int c = threadIdx.x + i * NT, r = c >> 3;
@@ -116,6 +117,31 @@ struct Im2colRowLoader {
     const bf16_t* p = sp[i] + koff;
     return (smask[i] & kbit) ? (const void*)p : zero_src();
   }
+  // buffer form (PIPE 6/7). The slot offset is taken at the tap with the smallest address (fwd:
+  // tap (0,0) at (oh*s-1, ow*s-1); dgrad: tap (2,2) at (oh-1, ow-1)) so every tap adds a
+  // non-negative scalar soffset; the descriptor base sits (W+1)*C elements before x so that
+  // pixel (-1, -1) of image 0 still has a non-negative offset. Padding taps select kOOB.
+  uint32_t bvo[CH];
+  __amdgpu_buffer_rsrc_t bsrd;
+  int N_img = 0;
+  __device__ void bprep() {
+    const int64_t bias = (int64_t)(Wd + 1) * C;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int kc = rm_glds_kc(threadIdx.x + i * NT);
+      const int ih = kFlip ? ih0[i] - 2 : ih0[i], iw = kFlip ? iw0[i] - 2 : iw0[i];
+      bvo[i] = pbase[i] < 0 ? kOOB : (uint32_t)((bias + ((int64_t)pbase[i] + (int64_t)ih * Wd + iw) * C + kc) * 2);
+    }
+    bsrd = make_srd(x - bias, (uint32_t)((bias + (int64_t)N_img * H * Wd * C) * 2));
+  }
+  __device__ uint32_t bsoff(int k0) const {
+    const int tap = k0 / C;
+    const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+    const int shift = kFlip ? (2 - kh) * Wd + (2 - kw) : kh * Wd + kw;
+    return (uint32_t)(((int64_t)shift * C + (k0 - tap * C)) * 2);
+  }
+  __device__ bool bcheck(int) const { return true; }
+  __device__ uint32_t bvoff_chk(int i, int) const { return (smask[i] & kbit) ? bvo[i] : kOOB; }
 };
 
 // B operand of dgrad: k = (tap, co) rows, n = ci columns, element W[co][tap][ci] (k-major per tap).
@@ -155,6 +181,24 @@ struct WeightTapKLoader {
     koff = ((int64_t)(k0 - tap * Cout) * 9 + tap) * Cin;
   }
   __device__ const void* src2(int i) const { return sok[i] ? (const void*)(sp[i] + koff) : zero_src(); }
+  // buffer form (PIPE 6/7): element W[co][tap][ci] at ((co * 9 + tap) * Cin + ci) * 2 bytes
+  uint32_t bvo[CH];
+  __amdgpu_buffer_rsrc_t bsrd;
+  __device__ void bprep() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + i * NT, kr = c / TileGeom<W>::KPR;
+      const int ci = col0 + km_glds_col<W>(c);
+      bvo[i] = ci < Cin ? (uint32_t)(((int64_t)kr * 9 * Cin + ci) * 2) : kOOB;
+    }
+    bsrd = make_srd(w, (uint32_t)((int64_t)Cout * 9 * Cin * 2));
+  }
+  __device__ uint32_t bsoff(int k0) const {
+    const int tap = k0 / Cout;
+    return (uint32_t)((((int64_t)(k0 - tap * Cout) * 9 + tap) * Cin) * 2);
+  }
+  __device__ bool bcheck(int) const { return false; }
+  __device__ uint32_t bvoff_chk(int i, int) const { return bvo[i]; }
 };
 
 // ---- stride-2 data gradient ----------------------------------------------------------------------
@@ -469,7 +513,8 @@ template <int BM, int BN, bool S, int NTW = kThreads>
 static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGeom& g, float* stats,
                        hipStream_t stream) {
   if constexpr (NTW == 512) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
-    launch_fwd_p<BM, BN, S, 3, 512>(x, w, y, g, stats, stream);
+    if (mfma_pipeline() == 7) launch_fwd_p<BM, BN, S, 7, 512>(x, w, y, g, stats, stream);
+    else launch_fwd_p<BM, BN, S, 3, 512>(x, w, y, g, stats, stream);
   } else if constexpr (BM * BN > 128 * 128) {  // 4 large waves, one block per CU
     if (mfma_pipeline() == 2) launch_fwd_p<BM, BN, S, 2, kThreads>(x, w, y, g, stats, stream);
     else launch_fwd_p<BM, BN, S, 3, kThreads>(x, w, y, g, stats, stream);
@@ -478,6 +523,7 @@ static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGe
       case 0: launch_fwd_p<BM, BN, S, 0, kThreads>(x, w, y, g, stats, stream); break;
       case 3: launch_fwd_p<BM, BN, S, 3, kThreads>(x, w, y, g, stats, stream); break;
       case 4: launch_fwd_p<BM, BN, S, 4, kThreads>(x, w, y, g, stats, stream); break;
+      case 6: launch_fwd_p<BM, BN, S, 6, kThreads>(x, w, y, g, stats, stream); break;
       default: launch_fwd_p<BM, BN, S, 2, kThreads>(x, w, y, g, stats, stream); break;
     }
   }
@@ -526,7 +572,8 @@ template <int BM, int BN, int NTW = kThreads>
 static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const ConvGeom& g, const bf16_t* addend,
                          const BnBwdEpi& bnb, hipStream_t stream) {
   if constexpr (NTW == 512) {
-    launch_dgrad_p<BM, BN, 3, 512>(dy, w, dx, g, addend, bnb, stream);
+    if (mfma_pipeline() == 7) launch_dgrad_p<BM, BN, 7, 512>(dy, w, dx, g, addend, bnb, stream);
+    else launch_dgrad_p<BM, BN, 3, 512>(dy, w, dx, g, addend, bnb, stream);
   } else if constexpr (BM * BN > 128 * 128) {
     if (mfma_pipeline() == 2) launch_dgrad_p<BM, BN, 2, kThreads>(dy, w, dx, g, addend, bnb, stream);
     else launch_dgrad_p<BM, BN, 3, kThreads>(dy, w, dx, g, addend, bnb, stream);
@@ -535,6 +582,7 @@ static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const Co
       case 0: launch_dgrad_p<BM, BN, 0, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
       case 3: launch_dgrad_p<BM, BN, 3, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
       case 4: launch_dgrad_p<BM, BN, 4, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
+      case 6: launch_dgrad_p<BM, BN, 6, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
       default: launch_dgrad_p<BM, BN, 2, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
     }
   }

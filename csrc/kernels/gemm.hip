@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // two k-steps, nothing to overlap, and the register-staged loop's third resident block wins.
 // 3 stages (96 KB of LDS, 1 block/CU) never won at ResNet shapes.
 static int g_pipe = -1;
-void set_mfma_pipeline(int p) { g_pipe = (p == 0 || p == 2 || p == 3 || p == 4 || p == 5) ? p : -1; }
+void set_mfma_pipeline(int p) { g_pipe = (p == 0 || (p >= 2 && p <= 7)) ? p : -1; }
 int mfma_pipeline() { return g_pipe; }
 int mfma_pipeline_for(int K) { return g_pipe >= 0 ? g_pipe : (K >= 256 ? 2 : 0); }
 
@@ -147,7 +147,8 @@ static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb
                       int N, int K, float* stats, const bf16_t* D, int64_t ldd, const BnBwdEpi& bnb,
                       hipStream_t stream) {
   if constexpr (NTW == 512) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
-    launch_nt_p<BM, BN, S, BT, 3, 512>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
+    if (mfma_pipeline() == 7) launch_nt_p<BM, BN, S, BT, 7, 512>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
+    else launch_nt_p<BM, BN, S, BT, 3, 512>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
   } else if constexpr (BM * BN > 128 * 128) {  // 4 large waves, one block per CU: 2 or 3 stages
     if (mfma_pipeline() == 2) launch_nt_p<BM, BN, S, BT, 2, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
     else launch_nt_p<BM, BN, S, BT, 3, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
@@ -156,6 +157,7 @@ static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb
       case 0: launch_nt_p<BM, BN, S, BT, 0, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
       case 3: launch_nt_p<BM, BN, S, BT, 3, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
       case 4: launch_nt_p<BM, BN, S, BT, 4, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
+      case 6: launch_nt_p<BM, BN, S, BT, 6, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
       default: launch_nt_p<BM, BN, S, BT, 2, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
     }
   }
@@ -248,6 +250,7 @@ void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, floa
     case 0: DLA_TN(BM_, BN_, 0); break;    \
     case 3: DLA_TN(BM_, BN_, 3); break;    \
     case 4: DLA_TN(BM_, BN_, 4); break;    \
+    case 6: DLA_TN(BM_, BN_, 6); break;    \
     default: DLA_TN(BM_, BN_, 2); break;   \
   }
   if (bm == 64 && bn == 64) {

@@ -62,8 +62,8 @@ def _headers_digest() -> str:
     return h.hexdigest()
 
 
-def _flags(kind: str, tdir: Path, incs, abi: int):
-    common = [
+def _flags(kind: str, tdir: Path, incs, abi: int, defines=()):
+    common = [f"-D{d}" for d in defines] + [
         f"--offload-arch={ARCH}",
         "-O3",
         "-std=c++17",
@@ -106,27 +106,32 @@ def _compile_one(src: Path, flags, hdr_digest: str, force: bool, verbose: bool) 
     return obj
 
 
-def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -> Path:
+def build(jobs: int | None = None, force: bool = False, verbose: bool = False, defines=(),
+          out: Path | None = None) -> Path:
+    """Compile and link; ``defines`` (e.g. ``DLA_MFMA_SHAPE=32``) build a variant, linked to ``out``
+    (variants are loaded for A/B runs through ``DLA_EXT_SO=<path>``, see ops/_ext.py)."""
+    out = Path(out) if out is not None else OUT
     tdir, incs, abi = _torch_paths()
     OBJ_DIR.mkdir(parents=True, exist_ok=True)
     kern, binds = _sources()
     hd = _headers_digest()
     jobs = jobs or min(8, (os.cpu_count() or 4))
-    kflags = _flags("kernel", tdir, incs, abi)
-    bflags = _flags("binding", tdir, incs, abi)
+    kflags = _flags("kernel", tdir, incs, abi, defines)
+    bflags = _flags("binding", tdir, incs, abi, defines)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = [ex.submit(_compile_one, s, kflags, hd, force, verbose) for s in kern]
         futs += [ex.submit(_compile_one, s, bflags, hd, force, verbose) for s in binds]
         objs = [f.result() for f in futs]
     tlib = tdir / "lib"
-    link_key = hashlib.sha256("".join(sorted(o.name for o in objs)).encode()).hexdigest()[:16]
-    stamp = OBJ_DIR / f"link-{link_key}.stamp"
-    if OUT.exists() and stamp.exists() and not force:
-        return OUT
+    link_key = hashlib.sha256(("".join(sorted(o.name for o in objs)) + str(out)).encode()).hexdigest()[:16]
+    stamp = OBJ_DIR / f"link-{out.stem}-{link_key}.stamp"
+    if out.exists() and stamp.exists() and not force:
+        return out
+    out.parent.mkdir(parents=True, exist_ok=True)
     # Link against torch's own HIP runtime / RCCL first (same SONAMEs as /opt/rocm), so the
     # extension shares one HIP runtime instance with torch at run time.
     cmd = [
-        _hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(OUT), *map(str, objs),
+        _hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out), *map(str, objs),
         f"-L{tlib}", f"-Wl,-rpath,{tlib}",
         "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
         "-lamdhip64", "-lrccl",
@@ -136,10 +141,10 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    for old in OBJ_DIR.glob("link-*.stamp"):
+    for old in OBJ_DIR.glob(f"link-{out.stem}-*.stamp"):
         old.unlink()
     stamp.touch()
-    return OUT
+    return out
 
 
 def main(argv=None):
@@ -147,8 +152,10 @@ def main(argv=None):
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("-D", "--define", action="append", default=[], help="extra -D for a variant build")
+    ap.add_argument("--out", default=None, help="output .so (variant builds)")
     a = ap.parse_args(argv)
-    out = build(a.jobs, a.force, a.verbose)
+    out = build(a.jobs, a.force, a.verbose, tuple(a.define), a.out)
     print(f"built {out}")
 
 

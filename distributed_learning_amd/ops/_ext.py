@@ -21,7 +21,17 @@ def _load():
     if _C is not None or _ERR is not None:
         return
     try:
-        from .. import _C as mod  # type: ignore[attr-defined]
+        variant = os.environ.get("DLA_EXT_SO")
+        if variant:  # A/B runs of a variant build (python -m distributed_learning_amd._build -D ... --out ...)
+            import importlib.util
+            import sys
+
+            spec = importlib.util.spec_from_file_location("distributed_learning_amd._C", variant)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            sys.modules["distributed_learning_amd._C"] = mod
+        else:
+            from .. import _C as mod  # type: ignore[attr-defined]
 
         _C = mod
     except Exception as e:  # pragma: no cover - depends on build state

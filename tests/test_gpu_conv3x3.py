@@ -102,7 +102,7 @@ def test_conv3x3_tile_configs(cuda, tile):
     assert torch.equal(C.conv3x3_dgrad(dy, w, None, tile), C.conv3x3_dgrad(dy, w, None, 1))
 
 
-@pytest.mark.parametrize("pipe", [0, 2, 3, 4, 5])
+@pytest.mark.parametrize("pipe", [0, 2, 3, 4, 5, 6])
 def test_conv3x3_pipelines_agree(cuda, pipe):
     C = _C()
     torch.manual_seed(0)

@@ -48,9 +48,9 @@ def _train(model_fn, wrap, steps, bf16):
     return m, losses
 
 
-@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("bf16,staged", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("grouping", [25 * 1024 * 1024, 64 * 1024, 0])
-def test_native_engine_steal_path_matches_single_device(world1, bf16, grouping):
+def test_native_engine_steal_path_matches_single_device(world1, bf16, staged, grouping):
     """Gather of autograd-owned grads into bucket buffers on the comm stream, the (world-1) RCCL
     all-reduce and the re-pointing of .grad at the averaged slots must give exactly the single-device
     update (the same kernels run; only the gradient storage differs)."""
@@ -71,6 +71,10 @@ def test_native_engine_steal_path_matches_single_device(world1, bf16, grouping):
             # force the full multi-rank data path (pack -> collective -> re-point) on one GPU
             w.sync.executor = NativeStreamExecutor(red.engine, "builtin", passthrough=False)
             w.sync.passthrough = False
+            if staged:  # the N>1 default: bf16 buckets gathered into fp32 staging, reduced, cast back
+                red.engine.impl.set_force(True)
+                red.engine.set_accum_fp32(True)
+                w.sync.executor.reserve(w.sync.buckets)
             assert w.sync.grad_mode == "steal"
             return w
 

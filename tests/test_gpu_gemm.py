@@ -87,7 +87,7 @@ def test_gemm_nt_tile_configs(cuda, tile, M, N, K):
     assert torch.equal(outk, ref)
 
 
-@pytest.mark.parametrize("pipe", [0, 2, 3, 4, 5])
+@pytest.mark.parametrize("pipe", [0, 2, 3, 4, 5, 6])
 def test_mfma_pipelines_agree(cuda, pipe):
     """Register-staged and LDS-DMA (2/3-stage) main loops: identical results for every kernel
     family (same MFMA order), including ragged edges and the transposed-read operands."""
