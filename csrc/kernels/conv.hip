@@ -21,6 +21,7 @@
 #include "dla_mfma.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace dla {
 
@@ -199,6 +200,115 @@ struct WeightTapKLoader {
   }
   __device__ bool bcheck(int) const { return false; }
   __device__ uint32_t bvoff_chk(int i, int) const { return bvo[i]; }
+};
+
+// ---- any channel count (C % 8 == 0, e.g. GoogLeNet's 16/24/48/96/112/144/160-channel 3x3s) ----------
+// A 64-deep k-step then spans several taps, so the tap of a 16-byte chunk (8 channels, never
+// straddling a tap) is per lane: k = k0 + chunk k offset -> (tap, channel) by a FastDiv. Register
+// staging (PIPE 0) and the global_load_lds pipeline (PIPE 2) use these loaders; same LDS images.
+template <int W, bool kFlip, int NT = kThreads>
+struct Im2colRowLoaderAnyC {
+  static constexpr bool kKMajor = false;
+  static constexpr int kNT = NT;
+  static constexpr int CH = TileGeom<W, NT>::CH;
+  const bf16_t* x;
+  int H, Wd, C;
+  int stride;
+  int32_t pbase[CH];
+  int ih0[CH], iw0[CH];
+  const bf16_t* sp0[CH];  // source pixel of tap (0, 0), channel 0
+  uint32_t smask[CH];
+  FastDiv fC;
+  __device__ void init(const ConvGeom& g, int64_t row0, int64_t P, int oh_dim, int ow_dim, const FastDiv& fw,
+                       const FastDiv& fh) {
+    fC = make_fastdiv((uint32_t)C);
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + i * NT, r = c >> 3;
+      const int64_t p = row0 + r;
+      if (p < P) {
+        const uint32_t q = fdiv((uint32_t)p, fw);
+        const int ow = (int)p - (int)q * ow_dim;
+        const uint32_t n = fdiv(q, fh);
+        const int oh = (int)q - (int)n * oh_dim;
+        pbase[i] = (int32_t)n * H * Wd;
+        ih0[i] = kFlip ? oh + 1 : oh * stride - 1;
+        iw0[i] = kFlip ? ow + 1 : ow * stride - 1;
+      } else {
+        pbase[i] = -1;
+        ih0[i] = iw0[i] = 0;
+      }
+      uint32_t m = 0;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int ih = kFlip ? ih0[i] - t / 3 : ih0[i] + t / 3;
+        const int iw = kFlip ? iw0[i] - t % 3 : iw0[i] + t % 3;
+        m |= ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)Wd) ? (1u << t) : 0u;
+      }
+      smask[i] = pbase[i] < 0 ? 0u : m;
+      sp0[i] = x + ((int64_t)(pbase[i] < 0 ? 0 : pbase[i]) + (int64_t)ih0[i] * Wd + iw0[i]) * C;
+    }
+    (void)g;
+  }
+  __device__ void prep() {}
+  __device__ __forceinline__ const bf16_t* at(int i, int k, bool& ok) const {
+    const int tap = (int)fdiv((uint32_t)k, fC);
+    const int ci = k - tap * C;
+    const int kh = (tap * 11) >> 5, kw = tap - 3 * kh;  // tap / 3 for tap <= 8
+    const int shift = kh * Wd + kw;
+    ok = tap < 9 && ((smask[i] >> tap) & 1u);
+    return sp0[i] + (int64_t)(kFlip ? -shift : shift) * C + ci;
+  }
+  __device__ ushort8_t load(int i, int k0) const {
+    bool ok;
+    const bf16_t* p = at(i, k0 + (threadIdx.x & 7) * 8, ok);
+    return ok ? *reinterpret_cast<const ushort8_t*>(p) : zero8();
+  }
+  __device__ const void* src(int i, int k0) const {
+    bool ok;
+    const bf16_t* p = at(i, k0 + rm_glds_kc(threadIdx.x + i * NT), ok);
+    return ok ? (const void*)p : zero_src();
+  }
+};
+
+// dgrad B operand for any Cout % 8: k-row (tap, co) per lane.
+template <int W, int NT = kThreads>
+struct WeightTapKLoaderAnyC {
+  static constexpr bool kKMajor = true;
+  static constexpr int kNT = NT;
+  static constexpr int CH = TileGeom<W, NT>::CH;
+  const bf16_t* w;
+  int Cout, Cin, col0;
+  const bf16_t* sp[CH];  // column base (ci) of the slot
+  bool sok[CH];
+  FastDiv fCo;
+  __device__ __forceinline__ const bf16_t* at(int k, int ci, bool& ok) const {
+    const int tap = (int)fdiv((uint32_t)k, fCo);
+    const int co = k - tap * Cout;
+    ok = tap < 9 && ci < Cin;
+    return w + ((int64_t)co * 9 + tap) * Cin + ci;
+  }
+  __device__ ushort8_t load(int i, int k0) const {
+    const int c = threadIdx.x + i * NT, kr = c / TileGeom<W>::KPR, nc = (c % TileGeom<W>::KPR) * 8;
+    bool ok;
+    const bf16_t* p = at(k0 + kr, col0 + nc, ok);
+    return ok ? *reinterpret_cast<const ushort8_t*>(p) : zero8();
+  }
+  __device__ void prep() {
+    fCo = make_fastdiv((uint32_t)Cout);
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + i * NT;
+      const int ci = col0 + km_glds_col<W>(c);
+      sok[i] = ci < Cin;
+    }
+  }
+  __device__ const void* src(int i, int k0) const {
+    const int c = threadIdx.x + i * NT, kr = c / TileGeom<W>::KPR;
+    bool ok;
+    const bf16_t* p = at(k0 + kr, col0 + km_glds_col<W>(c), ok);
+    return ok ? (const void*)p : zero_src();
+  }
 };
 
 // ---- stride-2 data gradient ----------------------------------------------------------------------
@@ -396,14 +506,17 @@ __global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void conv3x3_fwd_ker
   const int64_t row0 = (int64_t)bm * BM;
   const int col0 = bn * BN;
   const int K = 9 * g.Cin;
+  // PIPE >= 100: any Cin % 8 (per-lane tap decode), main loop PIPE % 100
+  constexpr bool kAny = PIPE >= 100;
   const RowLoader<BN, NT> lb{w, K, (int64_t)col0, g.Cout, K};
-  Im2colRowLoader<BM, false, NT> la{x, g.H, g.W, g.Cin, g.stride};
+  std::conditional_t<kAny, Im2colRowLoaderAnyC<BM, false, NT>, Im2colRowLoader<BM, false, NT>> la{
+      x, g.H, g.W, g.Cin, g.stride};
   la.init(g, row0, P, g.OH, g.OW, g.fOW, g.fOH);
   ColStats<BM, BN, NT> st;
   st.zero();
   Acc<BM, BN, NT> acc;
   acc.zero();
-  run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
+  run_mainloop<PIPE % 100>(la, lb, 0, K, acc, smem_raw);
   epilogue_bf16<BM, BN, kStats, false, NT>(acc, y, g.Cout, P, g.Cout, row0, col0, st, nullptr, 0, smem_raw);
   if constexpr (kStats) stats_flush<BM, BN, NT>(st, stats + (int64_t)bm * g.Cout * 2, g.Cout, col0, smem_raw);
 }
@@ -422,13 +535,16 @@ __global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void conv3x3_dgrad_k
   const int64_t row0 = (int64_t)bm * BM;
   const int col0 = bn * BN;
   const int K = 9 * g.Cout;
-  const WeightTapKLoader<BN, NT> lb{w, g.Cout, g.Cin, col0};
-  Im2colRowLoader<BM, true, NT> la{dy, g.OH, g.OW, g.Cout, 1};
+  constexpr bool kAny = PIPE >= 100;  // any Cout % 8: per-lane tap decode in both loaders
+  std::conditional_t<kAny, WeightTapKLoaderAnyC<BN, NT>, WeightTapKLoader<BN, NT>> lb{w, g.Cout, g.Cin, col0};
+  if constexpr (kAny) lb.prep();  // the divisor by Cout (the register main loop does not call prep)
+  std::conditional_t<kAny, Im2colRowLoaderAnyC<BM, true, NT>, Im2colRowLoader<BM, true, NT>> la{dy, g.OH, g.OW,
+                                                                                                 g.Cout, 1};
   la.init(g, row0, P, g.H, g.W, g.fOW, g.fOH);  // stride 1: the same divisors (OW == W, OH == H)
   ColStats<BM, BN, NT> st;
   Acc<BM, BN, NT> acc;
   acc.zero();
-  run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
+  run_mainloop<PIPE % 100>(la, lb, 0, K, acc, smem_raw);
   epilogue_bf16<BM, BN, false, true, NT>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, addend, g.Cin, smem_raw, &bnb, bm);
 }
 
@@ -504,7 +620,7 @@ static void launch_fwd_p(const bf16_t* x, const bf16_t* w, bf16_t* y, const Conv
   const int64_t P = (int64_t)g.N * g.OH * g.OW;
   const int tiles = (int)((P + BM - 1) / BM) * ((g.Cout + BN - 1) / BN);
   const size_t lds =
-      std::max(run_mainloop_lds_bytes<PIPE, BM, BN, Im2colRowLoader<BM, false, NT>, RowLoader<BN, NT>>(),
+      std::max(run_mainloop_lds_bytes<PIPE % 100, BM, BN, Im2colRowLoader<BM, false, NT>, RowLoader<BN, NT>>(),
                epilogue_lds_bytes<BM, BN, S, NT>());
   hipLaunchKernelGGL((conv3x3_fwd_kernel<BM, BN, S, PIPE, NT>), dim3(tiles), dim3(NT), lds, stream, x, w, y, g,
                      stats);
@@ -518,6 +634,9 @@ static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGe
   } else if constexpr (BM * BN > 128 * 128) {  // 4 large waves, one block per CU
     if (mfma_pipeline() == 2) launch_fwd_p<BM, BN, S, 2, kThreads>(x, w, y, g, stats, stream);
     else launch_fwd_p<BM, BN, S, 3, kThreads>(x, w, y, g, stats, stream);
+  } else if (g.Cin % 64 != 0) {  // a k-step spans taps: per-lane tap decode (register or LDS-DMA staging)
+    if (mfma_pipeline_for(9 * g.Cin) == 0) launch_fwd_p<BM, BN, S, 100, kThreads>(x, w, y, g, stats, stream);
+    else launch_fwd_p<BM, BN, S, 102, kThreads>(x, w, y, g, stats, stream);
   } else {
     switch (mfma_pipeline_for(9 * g.Cin)) {
       case 0: launch_fwd_p<BM, BN, S, 0, kThreads>(x, w, y, g, stats, stream); break;
@@ -563,7 +682,7 @@ static void launch_dgrad_p(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const 
   const int64_t P = (int64_t)g.N * g.H * g.W;
   const int tiles = (int)((P + BM - 1) / BM) * ((g.Cin + BN - 1) / BN);
   const size_t lds =
-      std::max(run_mainloop_lds_bytes<PIPE, BM, BN, Im2colRowLoader<BM, true, NT>, WeightTapKLoader<BN, NT>>(),
+      std::max(run_mainloop_lds_bytes<PIPE % 100, BM, BN, Im2colRowLoader<BM, true, NT>, WeightTapKLoader<BN, NT>>(),
                epilogue_lds_bytes<BM, BN, false, NT>());
   hipLaunchKernelGGL((conv3x3_dgrad_kernel<BM, BN, PIPE, NT>), dim3(tiles), dim3(NT), lds, stream, dy, w, dx, g,
                      addend, bnb);
@@ -577,6 +696,9 @@ static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const Co
   } else if constexpr (BM * BN > 128 * 128) {
     if (mfma_pipeline() == 2) launch_dgrad_p<BM, BN, 2, kThreads>(dy, w, dx, g, addend, bnb, stream);
     else launch_dgrad_p<BM, BN, 3, kThreads>(dy, w, dx, g, addend, bnb, stream);
+  } else if (g.Cout % 64 != 0) {
+    if (mfma_pipeline_for(9 * g.Cout) == 0) launch_dgrad_p<BM, BN, 100, kThreads>(dy, w, dx, g, addend, bnb, stream);
+    else launch_dgrad_p<BM, BN, 102, kThreads>(dy, w, dx, g, addend, bnb, stream);
   } else {
     switch (mfma_pipeline_for(9 * g.Cout)) {
       case 0: launch_dgrad_p<BM, BN, 0, kThreads>(dy, w, dx, g, addend, bnb, stream); break;

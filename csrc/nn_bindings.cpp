@@ -325,14 +325,17 @@ static int pool_out(int in, int k, int s, int p, bool ceil_mode);
 std::vector<at::Tensor> bn_relu_maxpool_fwd(at::Tensor x, c10::optional<at::Tensor> weight,
                                             c10::optional<at::Tensor> bias, c10::optional<at::Tensor> running_mean,
                                             c10::optional<at::Tensor> running_var, double momentum, double eps,
-                                            int64_t k, int64_t s, int64_t p, c10::optional<at::Tensor> stats) {
+                                            int64_t k, int64_t s, int64_t p, c10::optional<at::Tensor> stats,
+                                            bool ceil_mode) {
   check_act(x, "x");
   TORCH_CHECK(x.dim() == 4 && x.scalar_type() == at::kBFloat16, "bn_relu_maxpool: bf16 4-D input");
   TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && p >= 0 && 2 * p <= k, "bn_relu_maxpool: unsupported window");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
   const int64_t M = (int64_t)N * H * W;
   TORCH_CHECK(M < (1 << 24), "bn_relu_maxpool: too many pixels for 24-bit index math");
-  const int OH = pool_out(H, (int)k, (int)s, (int)p, false), OW = pool_out(W, (int)k, (int)s, (int)p, false);
+  // ceil mode (GoogLeNet) only adds trailing windows that start inside the input; the kernels skip
+  // their out-of-range taps and the backward gather clamps to OH/OW
+  const int OH = pool_out(H, (int)k, (int)s, (int)p, ceil_mode), OW = pool_out(W, (int)k, (int)s, (int)p, ceil_mode);
   auto f32 = x.options().dtype(at::kFloat);
   auto fptr = [](const c10::optional<at::Tensor>& t) -> float* {
     if (!t.has_value() || !t->defined()) return nullptr;
@@ -491,7 +494,7 @@ static void check_conv3(const at::Tensor& x, const at::Tensor& w) {
                   w.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv3x3: w must be a bf16 channels_last [Cout, Cin, 3, 3] tensor");
   TORCH_CHECK(w.size(1) == x.size(1), "conv3x3: channel mismatch");
-  TORCH_CHECK(x.size(1) % 64 == 0 && w.size(0) % 64 == 0, "conv3x3: Cin and Cout must be multiples of 64");
+  TORCH_CHECK(x.size(1) % 8 == 0 && w.size(0) % 8 == 0, "conv3x3: Cin and Cout must be multiples of 8");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(w.data_ptr()) & 15) == 0,
               "conv3x3: 16-byte aligned operands required");
   TORCH_CHECK(x.numel() / x.size(1) < (1 << 24), "conv3x3: too many pixels for 24-bit index math");
@@ -502,6 +505,8 @@ std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, 
   TORCH_CHECK(tile >= 0 && tile <= kTile256x64, "conv3x3: tile config 0..7");
   check_conv3(x, w);
   TORCH_CHECK(stride == 1 || stride == 2, "conv3x3: stride 1 or 2");
+  TORCH_CHECK(x.size(1) % 64 == 0 || tile_bm(tile) * tile_bn(tile) <= 128 * 128,
+              "conv3x3: Cin % 64 != 0 needs a tile of at most 128x128");
   const int N = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Cout = (int)w.size(0);
   const int OH = (H - 1) / (int)stride + 1, OW = (W - 1) / (int)stride + 1;
   at::Tensor y = at::empty({N, Cout, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -521,6 +526,8 @@ at::Tensor conv3x3_dgrad(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> 
   const int N = (int)dy.size(0), Cout = (int)w.size(0), Cin = (int)w.size(1), H = (int)dy.size(2), W = (int)dy.size(3);
   at::Tensor dx = at::empty({N, Cin, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   check_conv3(dx, w);
+  TORCH_CHECK(Cout % 64 == 0 || tile_bm(tile) * tile_bn(tile) <= 128 * 128,
+              "conv3x3_dgrad: Cout % 64 != 0 needs a tile of at most 128x128");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0,
               "conv3x3_dgrad: bf16 aligned dy");
   const void* add = nullptr;
@@ -544,6 +551,7 @@ at::Tensor conv3x3s2_dgrad(at::Tensor dy, at::Tensor w, int64_t H, int64_t W) {
   const int N = (int)dy.size(0), Cout = (int)w.size(0), Cin = (int)w.size(1);
   at::Tensor dx = at::empty({N, Cin, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   check_conv3(dx, w);
+  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "conv3x3s2_dgrad: Cin and Cout must be multiples of 64");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0,
               "conv3x3s2_dgrad: bf16 aligned dy");
   launch_conv3x3s2_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, (int)H, (int)W, Cin, Cout,
@@ -580,9 +588,9 @@ std::vector<at::Tensor> conv3x3_dgrad_bn(at::Tensor dy, at::Tensor w, c10::optio
 at::Tensor conv3x3_wgrad(at::Tensor dy, at::Tensor x, int64_t stride, c10::ScalarType out_dtype) {
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16 &&
-                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 64 == 0,
-              "conv3x3_wgrad: x must be bf16 channels_last with Cin % 64 == 0");
-  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.size(1) % 64 == 0, "conv3x3_wgrad: dy must be bf16, Cout % 64");
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 8 == 0,
+              "conv3x3_wgrad: x must be bf16 channels_last with Cin % 8 == 0");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.size(1) % 8 == 0, "conv3x3_wgrad: dy must be bf16, Cout % 8");
   TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "conv3x3_wgrad: fp32/bf16 output");
   TORCH_CHECK(x.numel() / x.size(1) < (1 << 24), "conv3x3_wgrad: too many pixels");
   const int N = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Cout = (int)dy.size(1);
@@ -617,7 +625,8 @@ void bind_nn(pybind11::module& m) {
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd, "stem BN(train)+ReLU+max-pool forward (pooled output only)",
         pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"),
         pybind11::arg("running_var"), pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("k"),
-        pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("stats") = pybind11::none());
+        pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("stats") = pybind11::none(),
+        pybind11::arg("ceil_mode") = false);
   m.def("bn_relu_maxpool_bwd", &bn_relu_maxpool_bwd, "stem BN+ReLU+max-pool backward (dy gathered from the pool)");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC max pooling forward (+ argmax window positions)", pybind11::arg("x"),
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("ceil_mode") = false,

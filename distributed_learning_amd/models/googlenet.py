@@ -96,11 +96,11 @@ class GoogLeNet(nn.Module):
         self.last_aux = None
 
     def forward(self, x):
-        x = self.conv1(x)
-        x = self.maxpool1(x)
+        # conv + BN + ReLU + ceil-mode max-pool as one fused op on the native path (the full-
+        # resolution activations of conv1 and conv3 are never written)
+        x = dnn.conv_bn_act_maxpool(x, self.conv1.conv, self.conv1.bn, self.maxpool1)
         x = self.conv2(x)
-        x = self.conv3(x)
-        x = self.maxpool2(x)
+        x = dnn.conv_bn_act_maxpool(x, self.conv3.conv, self.conv3.bn, self.maxpool2)
         x = self.inception3a(x)
         x = self.inception3b(x)
         x = self.maxpool3(x)
@@ -117,8 +117,10 @@ class GoogLeNet(nn.Module):
         x = global_avg_pool(x) if isinstance(self.avgpool, nn.AdaptiveAvgPool2d) else torch.flatten(self.avgpool(x), 1)
         x = self.dropout(x)
         x = self.fc(x)
-        # Reference semantics: only output[0] (main logits) enters the loss (network.py:41).
-        self.last_aux = (aux2, aux1)
+        # Reference semantics: only output[0] (main logits) enters the loss (network.py:41). The aux
+        # outputs are kept detached: holding their autograd graph would keep the previous step's
+        # AccumulateGrad nodes alive across iterations (and across a HIP-graph capture boundary).
+        self.last_aux = tuple(a.detach() if a is not None else None for a in (aux2, aux1))
         return x
 
 

@@ -214,10 +214,10 @@ class _BNReluPool(torch.autograd.Function):
     activation and its gradient are never materialised."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p, stats=None):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p, stats=None, ceil=False):
         C = _ext.require()
         y, ws, pos = C.bn_relu_maxpool_fwd(x, weight, bias, running_mean, running_var, momentum, eps, k, s, p,
-                                           stats)
+                                           stats, ceil)
         ctx.save_for_backward(x, ws, weight, pos)
         ctx.geom = (k, s, p)
         return y
@@ -228,19 +228,19 @@ class _BNReluPool(torch.autograd.Function):
         k, s, p = ctx.geom
         dx, dg, db = _ext.require().bn_relu_maxpool_bwd(dy, pos, x, ws, weight, k, s, p)
         need = ctx.needs_input_grad
-        return dx, dg if need[1] else None, db if need[2] else None, None, None, None, None, None, None, None, None
+        return dx, dg if need[1] else None, db if need[2] else None, None, None, None, None, None, None, None, None, None
 
 
 def fused_bn_relu_maxpool(x: torch.Tensor, bn: nn.BatchNorm2d, pool: nn.MaxPool2d, stats=None):
     """``pool(relu(bn(x)))`` with the fused kernels when they apply (training-mode BN with running
-    stats or none, bf16 channels_last, square window, no dilation/ceil/indices); otherwise the
+    stats or none, bf16 channels_last, square window, no dilation/indices; floor or ceil mode); otherwise the
     separate fused BN+ReLU and max-pool ops. ``stats``: the producing conv's [rows, C, 2] (sum, sumsq)
     partials of ``x`` (the statistics pass over x is skipped)."""
     from .pool import _pair_same, max_pool2d
 
     k, s, p = _pair_same(pool.kernel_size), _pair_same(pool.stride or pool.kernel_size), _pair_same(pool.padding)
     ok = (bn.training and bn.momentum is not None and x.dtype == torch.bfloat16 and supported(x, bn, None)
-          and None not in (k, s, p) and _pair_same(pool.dilation) == 1 and not pool.ceil_mode
+          and None not in (k, s, p) and _pair_same(pool.dilation) == 1
           and not pool.return_indices and 1 <= k <= 15 and 2 * p <= k
           and x.numel() // x.shape[1] < (1 << 24))
     if not ok:
@@ -249,4 +249,5 @@ def fused_bn_relu_maxpool(x: torch.Tensor, bn: nn.BatchNorm2d, pool: nn.MaxPool2
     rm, rv = (bn.running_mean, bn.running_var) if bn.track_running_stats else (None, None)
     if bn.track_running_stats:
         _PENDING_COUNTERS.append(bn.num_batches_tracked)
-    return _BNReluPool.apply(x, bn.weight, bn.bias, rm, rv, float(bn.momentum), float(bn.eps), k, s, p, stats)
+    return _BNReluPool.apply(x, bn.weight, bn.bias, rm, rv, float(bn.momentum), float(bn.eps), k, s, p, stats,
+                             bool(pool.ceil_mode))

@@ -282,9 +282,17 @@ CONV3_POLICY = {"fwd": "native", "dgrad_native_max_cin": 1 << 30, "wgrad": "nati
 def supported3x3(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and conv.kernel_size == (3, 3)
             and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
-            and conv.stride in ((1, 1), (2, 2)) and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0
-            and x.is_contiguous(memory_format=torch.channels_last)
+            and _conv3_channels_ok(conv) and x.is_contiguous(memory_format=torch.channels_last)
             and x.numel() // x.shape[1] < (1 << 24))
+
+
+def _conv3_channels_ok(conv: nn.Conv2d) -> bool:
+    """Stride 1: any channel count % 8 (the any-C loaders decode the tap per 8-channel chunk, e.g.
+    GoogLeNet's 16/24/48/96/112/144/160); stride 2: % 64 (the parity-class data gradient)."""
+    ci, co = conv.in_channels, conv.out_channels
+    if conv.stride == (1, 1):
+        return ci % 8 == 0 and co % 8 == 0
+    return conv.stride == (2, 2) and ci % 64 == 0 and co % 64 == 0
 
 
 class _Conv3x3(torch.autograd.Function):

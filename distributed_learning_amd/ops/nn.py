@@ -153,7 +153,7 @@ def conv_bn_add_conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d
 
 
 def conv_bn_act_maxpool(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, pool: nn.Module):
-    """``pool(relu(BN(conv(x))))`` — the ResNet stem. Native path: the BN+ReLU+max-pool runs as one
+    """``pool(relu(BN(conv(x))))`` — the ResNet / GoogLeNet stem. Native path: the BN+ReLU+max-pool runs as one
     fused op (the 112x112 activation and its gradient are never written)."""
     if _BACKEND == "native" and x.is_cuda and isinstance(pool, nn.MaxPool2d):
         from .bn_act import fused_bn_relu_maxpool
@@ -164,6 +164,10 @@ def conv_bn_act_maxpool(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, po
             if nconv.supported_stem(x, conv):  # 7x7/s2 MFMA conv whose epilogue emits BN's statistics
                 y, stats = nconv.stem_conv(x, conv, want_stats=bn.training)
                 return fused_bn_relu_maxpool(y, bn, pool, stats)
+        if _NATIVE_CONV:  # a 1x1 / 3x3 conv before the pool (GoogLeNet's conv3 -> maxpool2)
+            r = _native_conv_stats(x, conv, bn.training)
+            if r is not None:
+                return fused_bn_relu_maxpool(r[0], bn, pool, r[1])
         return fused_bn_relu_maxpool(conv(x), bn, pool)
     return pool(conv_bn_act(x, conv, bn, relu=True))
 

@@ -21,6 +21,10 @@ def _rel(a, b):
 @pytest.mark.parametrize("N,Cin,H,W,Cout,stride", [
     (2, 64, 56, 56, 64, 1), (2, 128, 28, 28, 128, 1), (1, 256, 14, 14, 256, 1), (4, 512, 7, 7, 512, 1),
     (2, 128, 56, 56, 128, 2), (2, 64, 9, 13, 128, 1), (3, 128, 11, 7, 64, 2), (2, 256, 28, 28, 256, 2),
+    # GoogLeNet's Inception 3x3s (any C % 8: a 64-deep k-step spans taps -> per-lane tap decode)
+    (2, 16, 28, 28, 32, 1), (2, 96, 28, 28, 128, 1), (2, 96, 14, 14, 208, 1), (2, 24, 14, 14, 64, 1),
+    (2, 112, 14, 14, 224, 1), (2, 144, 14, 14, 288, 1), (2, 160, 7, 7, 320, 1), (2, 48, 7, 7, 128, 1),
+    (1, 8, 5, 7, 24, 1), (2, 64, 56, 56, 192, 1),
 ])
 def test_conv3x3_fwd_dgrad_wgrad(cuda, N, Cin, H, W, Cout, stride):
     C = _C()
@@ -71,10 +75,11 @@ def test_conv3x3s2_dgrad_every_tap(cuda, N, Cin, H, W, Cout):
         torch.testing.assert_close(dx.float(), xr.grad, rtol=4e-3, atol=1e-6)  # bf16 rounding of 2-term sums
 
 
-def test_conv3x3_asymmetric_weights(cuda):
+@pytest.mark.parametrize("Cin,Cout", [(64, 64), (24, 40), (16, 72)])
+def test_conv3x3_asymmetric_weights(cuda, Cin, Cout):
     """One-hot weights per tap catch a flipped / transposed tap order in any of the passes."""
     C = _C()
-    N, Cin, H, W, Cout = 1, 64, 6, 5, 64
+    N, H, W = 1, 6, 5
     x = torch.randn(N, Cin, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
     for tap in range(9):
         w = torch.zeros(Cout, Cin, 3, 3, device=cuda)
@@ -86,6 +91,9 @@ def test_conv3x3_asymmetric_weights(cuda):
         dx = C.conv3x3_dgrad(dy, w)
         ref = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), 1, 1)
         torch.testing.assert_close(dx.float(), ref, rtol=1e-2, atol=1e-2)
+        dw = C.conv3x3_wgrad(dy, x, 1, torch.float32)
+        refw = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), 1, 1)
+        torch.testing.assert_close(dw.float(), refw, rtol=1e-2, atol=1e-2)
 
 
 @pytest.mark.parametrize("tile", [1, 2, 3])
@@ -103,11 +111,12 @@ def test_conv3x3_tile_configs(cuda, tile):
 
 
 @pytest.mark.parametrize("pipe", [0, 2, 3, 4, 5, 6])
-def test_conv3x3_pipelines_agree(cuda, pipe):
+@pytest.mark.parametrize("cin", [64, 24])
+def test_conv3x3_pipelines_agree(cuda, pipe, cin):
     C = _C()
     torch.manual_seed(0)
-    x = torch.randn(2, 64, 9, 13, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
-    w = (torch.randn(128, 64, 3, 3, device=cuda) * 0.05).to(torch.bfloat16).contiguous(memory_format=CL)
+    x = torch.randn(2, cin, 9, 13, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(128, cin, 3, 3, device=cuda) * 0.05).to(torch.bfloat16).contiguous(memory_format=CL)
     dy = torch.randn(2, 128, 9, 13, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
     old = C.mfma_pipeline()
     try:

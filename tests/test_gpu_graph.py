@@ -7,9 +7,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(graphed: bool, steps: int, world1):
+def _run(graphed: bool, steps: int, world1, arch: str = "resnet18"):
     from distributed_learning_amd.data import SyntheticBatches
-    from distributed_learning_amd.models import resnet18
+    from distributed_learning_amd.models import googlenet, resnet18
     from distributed_learning_amd.ops import nn as dnn
     from distributed_learning_amd.ops.loss import cross_entropy
     from distributed_learning_amd.ops.optim import FusedSGD
@@ -18,11 +18,17 @@ def _run(graphed: bool, steps: int, world1):
 
     torch.manual_seed(0)
     dev = torch.device("cuda:0")
-    m = resnet18(10).to(dev).to(memory_format=torch.channels_last)
+    if arch == "googlenet":  # aux heads computed but unused (zero-filled grads), ceil-mode pools, torch.cat
+        m = googlenet(10).to(dev).to(memory_format=torch.channels_last)
+        m.dropout.p = 0.0  # the main-path dropout would make eager and replayed RNG streams matter
+        shape = (3, 64, 64)
+    else:
+        m = resnet18(10).to(dev).to(memory_format=torch.channels_last)
+        shape = (3, 32, 32)
     dnn.bf16_weights(m)
     w = PipelinedFusedDP(m, make_reducer("immediate", "builtin", native=True), 1 << 20, dev, broadcast=False)
     opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, master_weights=True)
-    data = SyntheticBatches(16, (3, 32, 32), 10, dev, dtype=torch.bfloat16, channels_last=True, device_step=True)
+    data = SyntheticBatches(16, shape, 10, dev, dtype=torch.bfloat16, channels_last=True, device_step=True)
 
     def step():
         x, y = data.next()
@@ -56,7 +62,8 @@ def world1(cuda):
     ctx.shutdown()
 
 
-def test_graphed_step_matches_eager(world1):
+@pytest.mark.parametrize("arch", ["resnet18", "googlenet"])
+def test_graphed_step_matches_eager(world1, arch):
     from distributed_learning_amd.ops import nn as dnn
 
     det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
@@ -64,8 +71,8 @@ def test_graphed_step_matches_eager(world1):
     dnn.set_backend("native")
     dnn.set_native_conv(True)
     try:
-        le, pe = _run(False, 5, world1)
-        lg, pg = _run(True, 5, world1)
+        le, pe = _run(False, 5, world1, arch)
+        lg, pg = _run(True, 5, world1, arch)
     finally:
         dnn.set_native_conv(False)
         dnn.set_backend("torch")

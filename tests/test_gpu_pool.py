@@ -48,9 +48,15 @@ def test_maxpool_nan_propagates(cuda):
     assert torch.isnan(y[0, 3, 0, 0]) and not torch.isnan(y[0, 2, 0, 0])
 
 
-def test_stem_bn_relu_maxpool_fused_matches_unfused(cuda):
+@pytest.mark.parametrize("shape,k,s,p,ceil", [
+    ((4, 64, 30, 30), 3, 2, 1, False),   # ResNet stem
+    ((4, 64, 29, 29), 3, 2, 0, True),    # GoogLeNet maxpool1 (odd size: the ceil window is partial)
+    ((2, 192, 15, 15), 3, 2, 0, True),   # GoogLeNet maxpool2
+    ((2, 64, 14, 14), 3, 2, 0, True),    # ceil mode with an even size
+])
+def test_stem_bn_relu_maxpool_fused_matches_unfused(cuda, shape, k, s, p, ceil):
     """Fused stem op == separate fused-BN+ReLU then max-pool: identical pooled output, running
-    statistics and (up to reduction order) gradients."""
+    statistics and (up to reduction order) gradients; floor and ceil mode."""
     import torch.nn as nn
 
     from distributed_learning_amd.ops import nn as dnn
@@ -58,22 +64,24 @@ def test_stem_bn_relu_maxpool_fused_matches_unfused(cuda):
     from distributed_learning_amd.ops.pool import MaxPool2d, max_pool2d
 
     torch.manual_seed(0)
-    x = torch.randn(4, 64, 30, 30, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    bn1, bn2 = nn.BatchNorm2d(64).to(cuda), nn.BatchNorm2d(64).to(cuda)
+    x = torch.randn(*shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    C = shape[1]
+    bn1, bn2 = nn.BatchNorm2d(C, eps=1e-3).to(cuda), nn.BatchNorm2d(C, eps=1e-3).to(cuda)
     with torch.no_grad():
         bn1.weight.uniform_(0.5, 1.5)
         bn1.bias.uniform_(-0.5, 0.5)
     bn2.load_state_dict(bn1.state_dict())
-    pool = MaxPool2d(3, 2, 1)
+    pool = MaxPool2d(k, s, p, ceil_mode=ceil)
     dnn.set_backend("native")
     try:
         x1 = x.clone().requires_grad_(True)
         y1 = fused_bn_relu_maxpool(x1, bn1, pool)
         x2 = x.clone().requires_grad_(True)
-        y2 = max_pool2d(fused_bn_act(x2, bn2, True, None), 3, 2, 1)
+        y2 = max_pool2d(fused_bn_act(x2, bn2, True, None), k, s, p, ceil_mode=ceil)
     finally:
         dnn.set_backend("torch")
-    assert torch.equal(y1, y2)
+    assert y1.shape == y2.shape and torch.equal(y1, y2)
+    assert y1.grad_fn is not None and "BNReluPool" in type(y1.grad_fn).__name__  # the fused op ran
     torch.testing.assert_close(bn1.running_mean, bn2.running_mean)
     torch.testing.assert_close(bn1.running_var, bn2.running_var)
     g = torch.randn_like(y1)
@@ -83,12 +91,12 @@ def test_stem_bn_relu_maxpool_fused_matches_unfused(cuda):
     # backward sums overlapping-window gradients in fp32, the unfused max-pool backward rounds that
     # sum to bf16 first, so the fused result must be at least as close to fp32
     xr = x.float().requires_grad_(True)
-    bnr = nn.BatchNorm2d(64).to(cuda)
+    bnr = nn.BatchNorm2d(C, eps=1e-3).to(cuda)
     bnr.load_state_dict({k: v for k, v in bn2.state_dict().items()})
     with torch.no_grad():
         bnr.weight.copy_(bn1.weight)
         bnr.bias.copy_(bn1.bias)
-    yr = torch.nn.functional.max_pool2d(torch.relu(bnr(xr)), 3, 2, 1)
+    yr = torch.nn.functional.max_pool2d(torch.relu(bnr(xr)), k, s, p, ceil_mode=ceil)
     yr.backward(g.float())
     err = lambda a, b: float((a.float() - b).norm() / b.norm())  # noqa: E731
     assert err(bn1.weight.grad, bnr.weight.grad) <= err(bn2.weight.grad, bnr.weight.grad) * 1.5 + 1e-3
