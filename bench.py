@@ -56,7 +56,7 @@ def parse():
     # per-step fixed costs amortised), 30 GB of the 288 GB HBM (profiles/batch_sweep_resnet50_n1.jsonl)
     ap.add_argument("--batch", type=int, default=512, help="per-GPU batch size")
     ap.add_argument("--model", default="resnet50")
-    ap.add_argument("--algorithm", default="builtin", help="native engine all-reduce: builtin|ring|direct|rsag|central")
+    ap.add_argument("--algorithm", default="builtin", help="native engine all-reduce: builtin|ring|ring_pipe|direct|rsag|central|hier_ring|hier_coll")
     # 8 MiB of bf16 gradients = 16 MiB of fp32 on the wire (fp32 accumulation at N > 1): the cap the
     # cost model (parallel/cost_model.py) derives for ResNet-50 on an 8-GPU node with the builtin
     # collective (the reference's 25 MiB costs ~30 % more exposed + contended comm there); "auto"

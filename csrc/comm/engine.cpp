@@ -35,6 +35,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -104,7 +105,8 @@ static Topology make_topology(int rank, int world, std::vector<std::vector<int>>
 
 // Plans are float-agnostic; these algorithms need the reduce kernel (fp32 / bf16 only).
 static bool needs_reduce_kernel(int algo) {
-  return algo == comm::kRing || algo == comm::kDirect || algo == comm::kCentral || algo == comm::kHierRing;
+  return algo == comm::kRing || algo == comm::kDirect || algo == comm::kCentral || algo == comm::kHierRing ||
+         algo == comm::kRingPipe;
 }
 
 static double comm_timeout_s() {
@@ -157,6 +159,7 @@ class CommEngine {
     }
     for (auto& e : timing_events_) hipEventDestroy(e);
     for (auto& e : ready_pool_) hipEventDestroy(e);
+    for (auto& e : plan_events_) hipEventDestroy(e);
     if (last_done_) hipEventDestroy(last_done_);
   }
 
@@ -386,7 +389,7 @@ class CommEngine {
     auto key = std::make_pair(algo, n);
     auto it = plans_.find(key);
     if (it != plans_.end()) return it->second;
-    TORCH_CHECK(algo >= comm::kBuiltin && algo <= comm::kHierColl, "CommEngine: unknown algorithm ", algo);
+    TORCH_CHECK(algo >= comm::kBuiltin && algo < comm::kAlgoCount, "CommEngine: unknown algorithm ", algo);
     Plan p;
     try {
       // plans are built for summation; the average is folded into the last reduce of each phase
@@ -477,10 +480,42 @@ class CommEngine {
     launch_cast(flat.data_ptr(), kBF16, stage, kF32, n, 1.f, st);
   }
 
+  hipEvent_t plan_event(size_t i) {
+    while (plan_events_.size() <= i) {
+      hipEvent_t e;
+      DLA_HIP_THROW(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      plan_events_.push_back(e);
+    }
+    return plan_events_[i];
+  }
+
+  hipStream_t side_stream() {
+    if (!side_)
+      side_ = std::make_unique<c10::hip::HIPStream>(c10::hip::getStreamFromPool(/*isHighPriority=*/true, device_));
+    return side_->stream();
+  }
+
+  // Runs a Plan on stream `st`. Local ops of a step whose successor has Step::overlap_prev go to
+  // the side stream, after an event that marks the step's group on `st`, so they run concurrently
+  // with the successor's group; a group waits (event) for the side work of every step before its
+  // predecessor, a step without the flag for all of it, and `st` joins the side stream at the end.
   void run_plan(const Plan& p, char* data, char* scratch, size_t esz, ncclDataType_t ndt, int dt, bool average,
                 hipStream_t st) {
     auto ptr = [&](const comm::Ref& r) { return (r.buf == comm::kData ? data : scratch) + (size_t)r.off * esz; };
-    for (const auto& step : p.steps) {
+    size_t nev = 0;
+    std::vector<hipEvent_t> side_done(p.steps.size(), nullptr);  // recorded on the side stream after step k's locals
+    long side_last = -1, side_joined = -1;                       // newest side step / newest one `st` waited for
+    auto join_side_upto = [&](long k) {
+      for (long j = std::min(k, side_last); j > side_joined; --j)
+        if (side_done[j]) {
+          DLA_HIP_THROW(hipStreamWaitEvent(st, side_done[j], 0));
+          side_joined = j;
+          break;
+        }
+    };
+    for (size_t k = 0; k < p.steps.size(); ++k) {
+      const auto& step = p.steps[k];
+      join_side_upto(step.overlap_prev ? (long)k - 2 : (long)k - 1);
       if (step.is_coll()) {
         const comm::Op& o = step.ops[0];
         ncclComm_t c = comm_of(o.comm);
@@ -513,19 +548,36 @@ class CommEngine {
         }
       }
       if (group) DLA_NCCL_CHECK(ncclGroupEnd());
+      const bool has_local = std::any_of(step.ops.begin(), step.ops.end(), [](const comm::Op& o) {
+        return o.kind == comm::kReduce || o.kind == comm::kCopy || o.kind == comm::kZero;
+      });
+      if (!has_local) continue;
+      hipStream_t ls = st;
+      if (k + 1 < p.steps.size() && p.steps[k + 1].overlap_prev) {
+        ls = side_stream();
+        hipEvent_t g = plan_event(nev++);
+        DLA_HIP_THROW(hipEventRecord(g, st));
+        DLA_HIP_THROW(hipStreamWaitEvent(ls, g, 0));
+      }
       for (const auto& o : step.ops) {
         if (o.kind == comm::kReduce) {
           ReduceSrcs rs{};
           rs.count = o.nsrc;
           for (int i = 0; i < o.nsrc; ++i) rs.ptr[i] = ptr(o.src[i]);
-          launch_reduce_sum(ptr(o.dst), o.accumulate, rs, o.count, dt, average ? o.scale : 1.f, st);
+          launch_reduce_sum(ptr(o.dst), o.accumulate, rs, o.count, dt, average ? o.scale : 1.f, ls);
         } else if (o.kind == comm::kCopy) {
-          DLA_HIP_THROW(hipMemcpyAsync(ptr(o.dst), ptr(o.src[0]), (size_t)o.count * esz, hipMemcpyDeviceToDevice, st));
+          DLA_HIP_THROW(hipMemcpyAsync(ptr(o.dst), ptr(o.src[0]), (size_t)o.count * esz, hipMemcpyDeviceToDevice, ls));
         } else if (o.kind == comm::kZero) {
-          DLA_HIP_THROW(hipMemsetAsync(ptr(o.dst), 0, (size_t)o.count * esz, st));
+          DLA_HIP_THROW(hipMemsetAsync(ptr(o.dst), 0, (size_t)o.count * esz, ls));
         }
       }
+      if (ls != st) {
+        side_done[k] = plan_event(nev++);
+        DLA_HIP_THROW(hipEventRecord(side_done[k], ls));
+        side_last = (long)k;
+      }
     }
+    join_side_upto((long)p.steps.size());
   }
 
   int device_;
@@ -539,6 +591,8 @@ class CommEngine {
   std::map<std::pair<int, int64_t>, Plan> plans_;
   at::Tensor scratch_;
   std::vector<hipEvent_t> ready_pool_;
+  std::vector<hipEvent_t> plan_events_;
+  std::unique_ptr<c10::hip::HIPStream> side_;
   size_t ready_next_ = 0;
   hipEvent_t last_done_ = nullptr;
   bool timing_ = false;
@@ -550,12 +604,51 @@ class CommEngine {
 // Virtual ranks: N ranks' buffers in one process, links = copies (vexec.h)
 // ---------------------------------------------------------------------------------------------
 struct DeviceBackend {
+  static constexpr bool kConcurrent = true;
   std::vector<char*> data, scratch;
   size_t esz = 4;
   int dt = kF32;
-  hipStream_t st = nullptr;
+  hipStream_t st = nullptr;    // current queue of the ops below
+  hipStream_t main = nullptr;  // the caller's stream
+  hipStream_t side = nullptr;  // overlapped local ops (created on first use)
+  std::unique_ptr<c10::hip::HIPStream> side_holder;
+  int device = 0;
+  std::vector<hipEvent_t> events;
+  std::map<size_t, hipEvent_t> side_done;
   at::TensorOptions opts;
   std::vector<at::Tensor> temps;
+
+  ~DeviceBackend() {
+    for (auto e : events) hipEventDestroy(e);
+  }
+  hipEvent_t event() {
+    hipEvent_t e;
+    DLA_HIP_THROW(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    events.push_back(e);
+    return e;
+  }
+  void side_begin() {
+    if (!side) {
+      side_holder = std::make_unique<c10::hip::HIPStream>(c10::hip::getStreamFromPool(true, device));
+      side = side_holder->stream();
+    }
+    hipEvent_t e = event();
+    DLA_HIP_THROW(hipEventRecord(e, main));
+    DLA_HIP_THROW(hipStreamWaitEvent(side, e, 0));
+    st = side;
+  }
+  void side_end(size_t tag) {
+    hipEvent_t e = event();
+    DLA_HIP_THROW(hipEventRecord(e, side));
+    side_done[tag] = e;
+    st = main;
+  }
+  void main_wait(size_t tag) {
+    auto it = side_done.upper_bound(tag);  // newest side batch with a tag <= `tag`
+    if (it == side_done.begin()) return;
+    --it;
+    DLA_HIP_THROW(hipStreamWaitEvent(main, it->second, 0));
+  }
 
   void* ptr(int rank, const comm::Ref& r) {
     return (r.buf == comm::kData ? data[rank] : scratch[rank]) + (size_t)r.off * esz;
@@ -596,7 +689,7 @@ static void virtual_allreduce(std::vector<at::Tensor> bufs, int algo, bool avera
                 "virtual_allreduce: buffers must share numel, dtype, device and be contiguous");
   }
   TORCH_CHECK(dtype == at::kFloat || dtype == at::kBFloat16, "virtual_allreduce: fp32 / bf16 only");
-  TORCH_CHECK(algo >= comm::kBuiltin && algo <= comm::kHierColl, "virtual_allreduce: unknown algorithm ", algo);
+  TORCH_CHECK(algo >= comm::kBuiltin && algo < comm::kAlgoCount, "virtual_allreduce: unknown algorithm ", algo);
   if (N == 1 || n == 0) return;
   std::vector<Plan> plans;
   Topology t0 = make_topology(0, N, rings, local_size, local_rings, node_rings);
@@ -623,7 +716,8 @@ static void virtual_allreduce(std::vector<at::Tensor> bufs, int algo, bool avera
     DeviceBackend be;
     be.esz = work[0].element_size();
     be.dt = work[0].scalar_type() == at::kBFloat16 ? kBF16 : kF32;
-    be.st = st;
+    be.st = be.main = st;
+    be.device = bufs[0].device().index();
     be.opts = at::TensorOptions().dtype(at::kByte).device(bufs[0].device());
     std::vector<at::Tensor> scr;
     for (int r = 0; r < N; ++r) {
@@ -732,6 +826,7 @@ void bind_comm(pybind11::module& m) {
   m.attr("ALGO_RSAG") = (int)comm::kRsAg;
   m.attr("ALGO_HIER_RING") = (int)comm::kHierRing;
   m.attr("ALGO_HIER_COLL") = (int)comm::kHierColl;
+  m.attr("ALGO_RING_PIPE") = (int)comm::kRingPipe;
 }
 
 }  // namespace dla

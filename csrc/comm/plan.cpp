@@ -130,6 +130,56 @@ void append_ring_rs(Plan& p, const std::vector<int>& members, int me, const std:
   }
 }
 
+// Pipelined reduce-scatter: every ring step is issued as two sub-steps, one per half of each
+// lane's chunk. Sub-step (i, h) receives half h into scratch slot h of the lane and reduces it;
+// the group of the next sub-step touches only the other half and the other slot, so it may overlap
+// that reduce (Step::overlap_prev). A half is re-sent / its slot re-filled two sub-steps later,
+// after its reduce has completed.
+void append_ring_rs_pipe(Plan& p, const std::vector<int>& members, int me, const std::vector<Lane>& lanes,
+                         float scale_last) {
+  const int M = (int)members.size();
+  if (M <= 1) return;
+  const size_t C = lanes.size();
+  std::vector<std::vector<int64_t>> off(C), len(C);
+  int64_t slot = 0;
+  for (size_t c = 0; c < C; ++c) {
+    split(lanes[c].len, M, off[c], len[c]);
+    for (auto l : len[c]) slot = std::max(slot, l);
+  }
+  slot = round_up(std::max<int64_t>((slot + 1) / 2, 1), kAlign);  // one half-chunk per slot
+  p.scratch_elems = std::max(p.scratch_elems, slot * (int64_t)C * 2);
+  auto half = [](int64_t l, int h, int64_t& o, int64_t& n) {
+    const int64_t h0 = l > kAlign ? round_up((l + 1) / 2, kAlign) : l;  // first half 64-aligned
+    o = h == 0 ? 0 : std::min(l, h0);
+    n = h == 0 ? std::min(l, h0) : l - std::min(l, h0);
+  };
+  bool first = true;
+  for (int i = 0; i < M - 1; ++i)
+    for (int h = 0; h < 2; ++h) {
+      Step st;
+      std::vector<Op> red;
+      for (size_t c = 0; c < C; ++c) {
+        const auto& order = lanes[c].order;
+        const int pos = (int)(std::find(order.begin(), order.end(), me) - order.begin());
+        const int right = members[order[mod(pos + 1, M)]], left = members[order[mod(pos - 1, M)]];
+        const int ts = mod(pos - i, M), tr = mod(ts - 1, M);
+        int64_t so, sn, ro, rn;
+        half(len[c][ts], h, so, sn);
+        half(len[c][tr], h, ro, rn);
+        const Ref sl = scratch(((int64_t)c * 2 + h) * slot);
+        if (sn > 0) st.ops.push_back(p2p(kSend, right, data(lanes[c].off + off[c][ts] + so), sn));
+        if (rn > 0) {
+          st.ops.push_back(p2p(kRecv, left, sl, rn));
+          red.push_back(reduce_op(data(lanes[c].off + off[c][tr] + ro), {sl}, rn, true, i == M - 2 ? scale_last : 1.f));
+        }
+      }
+      for (auto& o : red) st.ops.push_back(o);
+      st.overlap_prev = !first;
+      first = false;
+      p.steps.push_back(std::move(st));
+    }
+}
+
 void append_ring_ag(Plan& p, const std::vector<int>& members, int me, const std::vector<Lane>& lanes) {
   const int M = (int)members.size();
   if (M <= 1) return;
@@ -285,6 +335,7 @@ const char* algo_name(int algo) {
     case kRsAg: return "rsag";
     case kHierRing: return "hier_ring";
     case kHierColl: return "hier_coll";
+    case kRingPipe: return "ring_pipe";
     default: return "?";
   }
 }
@@ -341,6 +392,13 @@ Plan build_plan(int algo, const Topology& t, int64_t n, float avg) {
       append_ring_allreduce(p, world_members, t.rank, channel_lanes(0, n, orders), avg);
       break;
     }
+    case kRingPipe: {
+      const auto& orders = t.rings.empty() ? identity_ring(N) : t.rings;
+      const auto lanes = channel_lanes(0, n, orders);
+      append_ring_rs_pipe(p, world_members, t.rank, lanes, avg);
+      append_ring_ag(p, world_members, t.rank, lanes);  // first AG step joins every reduce
+      break;
+    }
     case kDirect:
       append_direct(p, world_members, t.rank, 0, n, avg);
       break;
@@ -390,7 +448,7 @@ std::string describe(const Plan& p) {
   std::ostringstream os;
   os << algo_name(p.algo) << " rank " << p.rank << " n " << p.n << " scratch " << p.scratch_elems << "\n";
   for (size_t i = 0; i < p.steps.size(); ++i) {
-    os << "step " << i << ":";
+    os << "step " << i << (p.steps[i].overlap_prev ? " (overlaps prev local)" : "") << ":";
     for (const auto& o : p.steps[i].ops) {
       os << " [" << kinds[o.kind];
       if (o.kind == kSend) os << " ->" << o.peer << " " << ref(o.src[0]);

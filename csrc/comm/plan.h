@@ -36,6 +36,9 @@ enum Algo : int {
   kRsAg = 4,      // ncclReduceScatter + ncclAllGather
   kHierRing = 5,  // 2-step on P2P rings: intra RS -> inter ring AR of owned shards -> intra AG
   kHierColl = 6,  // 2-step on sub-communicators: intra ncclReduceScatter -> inter ncclAllReduce -> intra ncclAllGather
+  kRingPipe = 7,  // ring whose reduce-scatter runs in two half-chunk sub-steps: the reduce kernel of
+                  // one half overlaps the P2P transfer of the other (double-buffered scratch slots)
+  kAlgoCount = 8,
 };
 const char* algo_name(int algo);
 
@@ -67,8 +70,15 @@ struct Op {
 
 // One step: its P2P ops (kSend/kRecv) form one RCCL group; the local ops (reduce/copy/zero) run
 // after the group completed, in order. A collective step holds exactly one kColl op.
+//
+// overlap_prev: this step's P2P group does not touch anything the previous step's local ops read or
+// write, so an executor may run those local ops concurrently with this group (RCCL engine: on a
+// side stream). Local ops of every step before the previous one must have completed before the
+// group starts; a step without the flag waits for all of them. The virtual-rank executor verifies
+// the disjointness and executes the deferred order.
 struct Step {
   std::vector<Op> ops;
+  bool overlap_prev = false;
   bool is_coll() const { return ops.size() == 1 && ops[0].kind == kColl; }
 };
 

@@ -10,8 +10,9 @@
 // step structure — throws instead of hanging, which is what a real multi-GPU run would do.
 //
 // The Backend supplies memory and arithmetic: the device backend (engine.cpp) issues
-// hipMemcpyAsync + the reduce kernel of reduce.hip on one stream; the host backend (below) runs
-// the same arithmetic on CPU memory, so the schedules are checked in the CPU test suite too.
+// hipMemcpyAsync + the reduce kernel of reduce.hip on a main stream (and a side stream for
+// overlapped local ops, kConcurrent); the host backend (below) runs the same arithmetic on CPU
+// memory, so the schedules are checked in the CPU test suite too.
 #pragma once
 
 #include <algorithm>
@@ -38,15 +39,45 @@ class VirtualRun {
     size_t S = plans_[0].steps.size();
     for (const auto& p : plans_)
       if (p.steps.size() != S) fail("ranks disagree on the number of steps");
+    // Step::overlap_prev: the previous step's local ops are deferred until after this step's
+    // transfers (the order a concurrent executor may produce), after checking that the two touch
+    // disjoint memory on every rank.
+    if constexpr (Backend::kConcurrent) {
+      run_concurrent(S);
+      return;
+    }
+    long pending = -1;
+    auto flush = [&]() {
+      if (pending >= 0) run_locals((size_t)pending);
+      pending = -1;
+    };
     for (size_t s = 0; s < S; ++s) {
       const bool coll = plans_[0].steps[s].is_coll();
-      for (int r = 1; r < N; ++r)
+      const bool ovl = plans_[0].steps[s].overlap_prev;
+      for (int r = 1; r < N; ++r) {
         if (plans_[r].steps[s].is_coll() != coll) fail("step " + std::to_string(s) + ": collective on some ranks only");
-      if (coll)
+        if (plans_[r].steps[s].overlap_prev != ovl) fail("step " + std::to_string(s) + ": ranks disagree on overlap");
+      }
+      if (coll) {
+        if (ovl) fail("step " + std::to_string(s) + ": a collective step cannot overlap local ops");
+        flush();
         run_coll(s);
+        continue;
+      }
+      if (ovl) {
+        if (s == 0 || plans_[0].steps[s - 1].is_coll()) fail("step " + std::to_string(s) + ": nothing to overlap");
+        check_disjoint(s - 1, s);
+      } else {
+        flush();
+      }
+      run_transfers(s);
+      flush();  // the deferred local ops of step s-1 run after step s's transfers
+      if (s + 1 < S && plans_[0].steps[s + 1].overlap_prev)
+        pending = (long)s;
       else
-        run_p2p_step(s);
+        run_locals(s);
     }
+    flush();
   }
 
  private:
@@ -61,7 +92,86 @@ class VirtualRun {
     return a.rank == b.rank && a.buf == b.buf && a.lo < b.hi && b.lo < a.hi;
   }
 
-  void run_p2p_step(size_t s) {
+  // A backend with a second queue (the device backend) runs the local ops of a step whose successor
+  // overlaps it on that queue, concurrently with the successor's transfers — the RCCL engine's
+  // order (engine.cpp run_plan): side_begin / side_end(tag) bracket them, main_wait(tag) joins.
+  void run_concurrent(size_t S) {
+    const int N = (int)plans_.size();
+    long side_last = -1, joined = -1;
+    auto join_upto = [&](long k) {
+      const long j = std::min(k, side_last);
+      if (j > joined) {
+        be_.main_wait((size_t)j);
+        joined = j;
+      }
+    };
+    for (size_t s = 0; s < S; ++s) {
+      const bool coll = plans_[0].steps[s].is_coll();
+      const bool ovl = plans_[0].steps[s].overlap_prev;
+      for (int r = 1; r < N; ++r) {
+        if (plans_[r].steps[s].is_coll() != coll) fail("step " + std::to_string(s) + ": collective on some ranks only");
+        if (plans_[r].steps[s].overlap_prev != ovl) fail("step " + std::to_string(s) + ": ranks disagree on overlap");
+      }
+      if (coll) {
+        if (ovl) fail("step " + std::to_string(s) + ": a collective step cannot overlap local ops");
+        join_upto((long)s);
+        run_coll(s);
+        continue;
+      }
+      if (ovl) {
+        if (s == 0 || plans_[0].steps[s - 1].is_coll()) fail("step " + std::to_string(s) + ": nothing to overlap");
+        check_disjoint(s - 1, s);
+        join_upto((long)s - 2);
+      } else {
+        join_upto((long)s - 1);
+      }
+      run_transfers(s);
+      if (s + 1 < S && plans_[0].steps[s + 1].overlap_prev) {
+        be_.side_begin();
+        run_locals(s);
+        be_.side_end(s);
+        side_last = (long)s;
+      } else {
+        run_locals(s);
+      }
+    }
+    join_upto((long)S);
+  }
+
+  // Local ops of step a vs P2P ops of step b, per rank: no write of one may meet a read or write of
+  // the other.
+  void check_disjoint(size_t a, size_t b) {
+    for (int r = 0; r < (int)plans_.size(); ++r) {
+      std::vector<Span> lw, lr, pw, pr;
+      for (const Op& o : plans_[r].steps[a].ops) {
+        if (o.kind == kReduce || o.kind == kCopy || o.kind == kZero) {
+          lw.push_back(Span{r, o.dst.buf, o.dst.off, o.dst.off + o.count});
+          if (o.kind != kZero)
+            for (int i = 0; i < o.nsrc; ++i) lr.push_back(Span{r, o.src[i].buf, o.src[i].off, o.src[i].off + o.count});
+        }
+      }
+      for (const Op& o : plans_[r].steps[b].ops) {
+        if (o.kind == kSend) pr.push_back(Span{r, o.src[0].buf, o.src[0].off, o.src[0].off + o.count});
+        if (o.kind == kRecv) pw.push_back(Span{r, o.dst.buf, o.dst.off, o.dst.off + o.count});
+      }
+      auto any = [](const std::vector<Span>& x, const std::vector<Span>& y) {
+        for (const auto& u : x)
+          for (const auto& v : y)
+            if (overlap(u, v)) return true;
+        return false;
+      };
+      if (any(lw, pw) || any(lw, pr) || any(lr, pw))
+        fail("step " + std::to_string(b) + " overlaps the local ops of step " + std::to_string(a) + " on rank " +
+             std::to_string(r) + " but touches their memory");
+    }
+  }
+
+  void run_locals(size_t s) {
+    for (int r = 0; r < (int)plans_.size(); ++r)
+      for (const Op& o : plans_[r].steps[s].ops) local(r, o);
+  }
+
+  void run_transfers(size_t s) {
     const int N = (int)plans_.size();
     std::map<std::pair<int, int>, std::deque<const Op*>> sends;  // (from, to) -> sends in issue order
     std::vector<Span> reads, writes;
@@ -105,9 +215,6 @@ class VirtualRun {
              std::to_string(kv.first.second) + " has no matching receive");
     // the links
     for (const auto& x : xfers) be_.copy(be_.ptr(x.to, x.rcv->dst), be_.ptr(x.from, x.snd->src[0]), x.rcv->count);
-    // local ops of every rank
-    for (int r = 0; r < N; ++r)
-      for (const Op& o : plans_[r].steps[s].ops) local(r, o);
   }
 
   void local(int r, const Op& o) {
@@ -210,8 +317,10 @@ class VirtualRun {
   Backend& be_;
 };
 
-// Host backend: CPU buffers, fp32 or bf16 (round-to-nearest-even, as v_cvt_pk_bf16_f32).
+// Host backend: CPU buffers, fp32 or bf16 (round-to-nearest-even, as v_cvt_pk_bf16_f32). Serial:
+// overlapped steps run in the deferred order (VirtualRun::run).
 struct HostBackend {
+  static constexpr bool kConcurrent = false;
   std::vector<char*> data, scratch;
   size_t esz = 4;
   bool bf16 = false;

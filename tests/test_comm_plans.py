@@ -17,7 +17,7 @@ from distributed_learning_amd.parallel.virtual import plan_text, virtual_allredu
 
 pytestmark = pytest.mark.skipif(not _ext.available(), reason="native extension not built")
 
-FLAT = ["builtin", "ring", "direct", "central", "rsag"]
+FLAT = ["builtin", "ring", "direct", "central", "rsag", "ring_pipe"]
 HIER = ["hier_ring", "hier_coll"]
 
 
@@ -39,7 +39,7 @@ def _check(bufs, xs, tol_rel):
 @pytest.mark.parametrize("algo", FLAT)
 def test_flat_algorithms_fp32(N, algo):
     for n in [1, 7, 63, 64 * N - 1, 1000, 100_003]:
-        for ch in ([1, 3, 7] if algo == "ring" else [0]):
+        for ch in ([1, 3, 7] if algo in ("ring", "ring_pipe") else [0]):
             xs = _inputs(N, n, torch.float32)
             bufs = [x.clone() for x in xs]
             virtual_allreduce(bufs, algo, channels=ch)
@@ -112,3 +112,26 @@ def test_schedule_errors_are_exceptions():
         C.virtual_allreduce([torch.zeros(10), torch.zeros(11)], C.ALGO_RING)
     with pytest.raises(ValueError):  # world not a multiple of local_size
         virtual_allreduce([torch.zeros(10) for _ in range(6)], "hier_ring", local_size=4)
+
+
+@pytest.mark.parametrize("N", [2, 3, 8])
+def test_ring_pipe_structure_and_bitwise_equal_to_ring(N):
+    """The pipelined ring: reduce-scatter sub-steps flagged to overlap the previous sub-step's
+    reduce (the executor checks they touch disjoint memory and runs the deferred order), the first
+    all-gather step joins them all, and the result equals the plain ring bit for bit (same chunks,
+    same summation order)."""
+    n = 100_003
+    text = plan_text("ring_pipe", 1, N, n, channels=3)
+    steps = [l for l in text.splitlines() if l.startswith("step ")]
+    rs = 2 * (N - 1)
+    assert len(steps) == rs + (N - 1)
+    assert "overlaps" not in steps[0] and all("overlaps" in l for l in steps[1:rs])
+    assert not any("overlaps" in l for l in steps[rs:])
+    for dtype in (torch.float32, torch.bfloat16):
+        xs = _inputs(N, n, dtype, seed=3)
+        a = [x.clone() for x in xs]
+        b = [x.clone() for x in xs]
+        virtual_allreduce(a, "ring", channels=3, accum_fp32=False)
+        virtual_allreduce(b, "ring_pipe", channels=3, accum_fp32=False)
+        for u, v in zip(a, b):
+            assert torch.equal(u, v)

@@ -19,7 +19,7 @@ from distributed_learning_amd.parallel.virtual import VirtualGroup, virtual_allr
 pytestmark = pytest.mark.gpu
 
 DEV = torch.device("cuda", 0)
-ALGOS = ["builtin", "ring", "direct", "central", "rsag", "hier_ring", "hier_coll"]
+ALGOS = ["builtin", "ring", "direct", "central", "rsag", "hier_ring", "hier_coll", "ring_pipe"]
 
 
 def _inputs(N, n, dtype, seed=0):
@@ -38,8 +38,9 @@ def _local(algo, N):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_virtual_ranks_gpu_match_host_and_fp64(N, algo, dtype):
     _ext.require()
-    sizes = [1, 7, 63, 64 * N - 1, 1000, 100_003] + ([4 * 1024 * 1024 + 37] if algo in ("ring", "hier_ring") else [])
-    chans = range(1, 8) if algo == "ring" and N == 8 else [0]
+    sizes = [1, 7, 63, 64 * N - 1, 1000, 100_003] + (
+        [4 * 1024 * 1024 + 37] if algo in ("ring", "hier_ring", "ring_pipe") else [])
+    chans = range(1, 8) if algo in ("ring", "ring_pipe") and N == 8 else [0]
     for n in sizes:
         for ch in chans:
             if ch > 1 and n > 200_000 and ch not in (1, 7):
