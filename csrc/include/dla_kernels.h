@@ -96,12 +96,16 @@ void launch_xent_bwd(const void* logits, const int64_t* target, const float* ws,
 void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks);  // <= 0: reduction passes
 // fp32 scratch floats of one reduction pass's partials [rows][C][2] plus their fold rows
 int64_t bn_partial_floats(int64_t M, int C);
+// reduction-pass block target (0 = DLA_BN_RED_BLOCKS or the default 1024); tests exercise the
+// > 1024-row fold path with it
+void set_bn_red_blocks(int blocks);
+int bn_red_blocks();
 // rows of fp32 [rows][C][2] scratch launch_bn_fwd's `part` needs to fold ext_nrb epilogue partials (0: none)
 int bn_fold_groups(int ext_nrb);
 void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int dtype, const float* gamma,
                    const float* beta, float eps, float momentum, float* running_mean, float* running_var, float* ws,
                    float* part, bool relu, bool training, hipStream_t stream, const float* ext_part = nullptr,
-                   int ext_nrb = 0, uint8_t* relu_mask = nullptr);
+                   int ext_nrb = 0, uint8_t* relu_mask = nullptr, int64_t ldy = 0);
 // y = act(BN(x) + BN_d(xd)) from the two finalized workspaces (ws, wsd: launch_bn_fwd with y == nullptr);
 // mask as launch_bn_fwd's ReLU-after-residual bit mask.
 void launch_bn_dual_apply(const void* x, const void* xd, void* y, const float* ws, const float* wsd, int64_t M, int C,
@@ -118,7 +122,7 @@ void launch_bn_dual_bwd(const void* dy, const uint8_t* mask, const void* x, cons
 void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const void* x, void* dx, void* dres,
                    int64_t M, int C, int dtype, const float* gamma, float* ws, float* part, float* dgamma,
                    float* dbeta, int mask_mode, hipStream_t stream, const float* ext_part = nullptr,
-                   int ext_nrb = 0);
+                   int ext_nrb = 0, int64_t ld_dy = 0);  // ld_dy: dy row stride when dy is a channel slice
 
 // Stem BN(+ReLU)+max-pool fused (bn_act.hip): launch_bn_fwd with y == nullptr computes ws only;
 // then the pooled output + window positions come straight from the BN input x. Backward: the BN

@@ -282,7 +282,10 @@ __global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restric
                                                               T* __restrict__ y, const float* __restrict__ ws,
                                                               int64_t M, int C, int nrb, int tpr,
                                                               uint8_t* __restrict__ mask,
-                                                              const float* __restrict__ ws2 = nullptr) {
+                                                              const float* __restrict__ ws2 = nullptr,
+                                                              int64_t ldy = 0) {
+  // ldy != 0: y is a channel slice of a wider channels_last tensor (row stride ldy), e.g. one
+  // Inception branch written straight into the concatenated block output
   // Same tiling as the reduction passes: a thread owns 8 fixed channels for all its rows, so the
   // per-channel coefficients live in registers (no per-element index math or table reads).
   const int rpi = kBNThreads / tpr, ct = tpr * 8;
@@ -315,7 +318,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restric
       }
       a[j] = o;
     }
-    Vec8<T>::store(y + off, a);
+    Vec8<T>::store(y + (ldy ? r * ldy + c0 : off), a);
     // ReLU-after-residual: the backward cannot recompute the branch from x alone, so record it as
     // one bit per element (1/16 of the bf16 output's bytes) instead of re-reading y.
     if (kRes && kRelu && mask) mask[off >> 3] = (uint8_t)bits;
@@ -347,7 +350,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restric
         }
         a[j] = o;
       }
-      Vec8<T>::store(y + off, a);
+      Vec8<T>::store(y + (ldy ? (r + u * rpi) * ldy + c0 : off), a);
       if (kRes && kRelu && mask) mask[off >> 3] = (uint8_t)bits;
     }
   }
@@ -387,19 +390,23 @@ __device__ __forceinline__ void apply_relu_mask(float (&g)[8], const float (&xv)
 // Where the backward passes read dy from: the gradient tensor itself, or (stem BN(+ReLU) fused with
 // the 3x3/s2 max-pool that follows it) gathered from the pooled gradient and the forward's 1-byte
 // argmax positions — the full-resolution dy is never written.
+// ld != 0: dy is a channel slice of a wider channels_last tensor (row stride ld elements), e.g. one
+// Inception branch's part of the concatenated output gradient — read in place, never copied out.
 template <typename T>
 struct DirectDy {
   static constexpr bool kRaw = true;  // plain loads: the grouped streaming loop applies
   const T* p;
-  __device__ __forceinline__ void raw(int64_t off, Raw8<T>& v) const { v.load(p + off); }
-  __device__ __forceinline__ void load(int64_t off, int64_t /*r*/, int /*c0*/, int /*C*/, float (&g)[8]) const {
-    Vec8<T>::load(p + off, g);
+  int64_t ld = 0;
+  __device__ __forceinline__ const T* at(int64_t off, int64_t r, int c0) const { return p + (ld ? r * ld + c0 : off); }
+  __device__ __forceinline__ void raw(int64_t off, int64_t r, int c0, Raw8<T>& v) const { v.load(at(off, r, c0)); }
+  __device__ __forceinline__ void load(int64_t off, int64_t r, int c0, int /*C*/, float (&g)[8]) const {
+    Vec8<T>::load(at(off, r, c0), g);
   }
 };
 
 struct PoolDy {
   static constexpr bool kRaw = false;  // a gather per element: per-row loop
-  __device__ __forceinline__ void raw(int64_t, Raw8<bf16_t>&) const {}
+  __device__ __forceinline__ void raw(int64_t, int64_t, int, Raw8<bf16_t>&) const {}
   const bf16_t* dyp;   // pooled gradient [N, OH, OW, C]
   const uint8_t* pos;  // window position of each pooled max (forward)
   int H, W, OH, OW, k, s, pad;
@@ -497,7 +504,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(DY dy, const 
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int64_t off = (r + u * rpi) * C + c0;
-        dy.raw(off, gr[u]);
+        dy.raw(off, r + u * rpi, c0, gr[u]);
         xr[u].load(x + off);
         mb[u] = kMask == kMaskBits ? (uint32_t)mask[off >> 3] : 0xffu;
       }
@@ -584,7 +591,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(DY dy, const T
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int64_t off = (r + u * rpi) * C + c0;
-        dy.raw(off, gr[u]);
+        dy.raw(off, r + u * rpi, c0, gr[u]);
         xr[u].load(x + off);
         mb[u] = kMask == kMaskBits ? (uint32_t)mask[off >> 3] : 0xffu;
       }
@@ -762,9 +769,14 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_dual_apply_kernel(const T* 
 // host side
 // ---------------------------------------------------------------------------------------------
 // Block target of the reduction passes (statistics / backward reduce): kRedBlocks, or
-// DLA_BN_RED_BLOCKS for A/B runs. Above 1024 partial rows the finalize reads them through
-// bn_partials_fold_kernel (bn_fold_rows).
+// DLA_BN_RED_BLOCKS / set_bn_red_blocks() for A/B runs and tests. Above 1024 partial rows the
+// statistics and backward-reduce finalizes read them through bn_partials_fold_kernel
+// (bn_fold_rows); GEMM-epilogue backward partials (ext_part) above 1024 rows use the
+// wave-per-channel bn_bwd_finalize_kernel<4> instead.
+static int g_red_blocks = 0;  // 0: not set (environment / default)
+void set_bn_red_blocks(int blocks) { g_red_blocks = blocks > 0 ? blocks : 0; }
 int bn_red_blocks() {
+  if (g_red_blocks > 0) return g_red_blocks;
   static const int v = [] {
     const char* e = std::getenv("DLA_BN_RED_BLOCKS");
     const int b = e ? std::atoi(e) : 0;
@@ -793,7 +805,7 @@ void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_bloc
 void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int dtype, const float* gamma,
                    const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                    float* ws, float* part, bool relu, bool training, hipStream_t stream, const float* ext_part,
-                   int ext_nrb, uint8_t* mask) {
+                   int ext_nrb, uint8_t* mask, int64_t ldy) {
   int tpr, nrb, nct;
   bn_geometry(M, C, &tpr, &nrb, &nct, 0);
   if (training && ext_part) {
@@ -824,7 +836,7 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
 #define DLA_BN_APPLY(T, R, A)                                                                                      \
   hipLaunchKernelGGL((bn_apply_kernel<T, R, A>), dim3(anct, anrb), dim3(kBNThreads), 0, stream, (const T*)x,        \
-                     (const T*)res, (T*)y, (const float*)ws, M, C, anrb, atpr, mask)
+                     (const T*)res, (T*)y, (const float*)ws, M, C, anrb, atpr, mask, nullptr, ldy)
   if (dtype == kBF16) {
     if (res) { if (relu) DLA_BN_APPLY(bf16_t, true, true); else DLA_BN_APPLY(bf16_t, true, false); }
     else { if (relu) DLA_BN_APPLY(bf16_t, false, true); else DLA_BN_APPLY(bf16_t, false, false); }
@@ -852,7 +864,8 @@ void launch_bn_dual_apply(const void* x, const void* xd, void* y, const float* w
 
 void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const void* x, void* dx, void* dres,
                    int64_t M, int C, int dtype, const float* gamma, float* ws, float* part, float* dgamma,
-                   float* dbeta, int mask_mode, hipStream_t stream, const float* ext_part, int ext_nrb) {
+                   float* dbeta, int mask_mode, hipStream_t stream, const float* ext_part, int ext_nrb,
+                   int64_t ld_dy) {
   int tpr, nrb, nct;
   bn_geometry(M, C, &tpr, &nrb, &nct, 0);
   if (ext_part) {
@@ -866,7 +879,7 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
   } else {
   const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
 #define DLA_BN_RED(T, K)                                                                                          \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, K>), dim3(nct, nrb), dim3(kBNThreads), lds, stream, DirectDy<T>{(const T*)dy}, \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, K>), dim3(nct, nrb), dim3(kBNThreads), lds, stream, DirectDy<T>{(const T*)dy, ld_dy}, \
                      (const T*)y, mask, (const T*)x, (const float*)ws, M, C, nrb, tpr, part)
 #define DLA_BN_RED_ALL(T)                                 \
   switch (mask_mode) {                                    \
@@ -885,7 +898,7 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
   int atpr, anrb, anct;
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
 #define DLA_BN_BAPPLY(T, K, D)                                                                                      \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, K, D>), dim3(anct, anrb), dim3(kBNThreads), 0, stream, DirectDy<T>{(const T*)dy}, \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, K, D>), dim3(anct, anrb), dim3(kBNThreads), 0, stream, DirectDy<T>{(const T*)dy, ld_dy}, \
                      (const T*)y, mask, (const T*)x, (const float*)ws, (T*)dx, (T*)dres, M, C, anrb, atpr)
 #define DLA_BN_BAPPLY_ALL(T, D)                                 \
   switch (mask_mode) {                                          \

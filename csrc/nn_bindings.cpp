@@ -32,7 +32,8 @@ static int64_t partial_floats(int64_t M, int C) { return bn_partial_floats(M, C)
 std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> residual, c10::optional<at::Tensor> weight,
                                    c10::optional<at::Tensor> bias, c10::optional<at::Tensor> running_mean,
                                    c10::optional<at::Tensor> running_var, bool training, double momentum, double eps,
-                                   bool relu, c10::optional<at::Tensor> stats) {
+                                   bool relu, c10::optional<at::Tensor> stats, c10::optional<at::Tensor> out,
+                                   int64_t out_channel) {
   check_act(x, "x");
   const int C = (int)x.size(1);
   const int64_t M = rows_of(x);
@@ -71,13 +72,28 @@ std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> resid
                 "stats must be fp32 [row_blocks, C, 2] partials");
   }
   at::Tensor part = at::empty({(training && !ext) ? partial_floats(M, C) : ext ? ext_part_floats(stats, C) : 1}, f32);
-  at::Tensor y = at::empty_like(x);
+  // out: write y into channels [out_channel, out_channel + C) of a wider channels_last tensor (the
+  // concatenated output of an Inception block) instead of a fresh one
+  at::Tensor y;
+  int64_t ldy = 0;
+  if (out.has_value() && out->defined()) {
+    TORCH_CHECK(x.dim() == 4 && out->dim() == 4 && out->is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    out->scalar_type() == x.scalar_type() && out->size(0) == x.size(0) && out->size(2) == x.size(2) &&
+                    out->size(3) == x.size(3) && out->size(1) % 8 == 0 && out_channel % 8 == 0 && out_channel >= 0 &&
+                    out_channel + C <= out->size(1),
+                "bn_act_fwd: out must be a channels_last [N, Ctot, H, W] tensor (Ctot, out_channel % 8 == 0) of x's "
+                "dtype and spatial size holding channels [out_channel, out_channel + C)");
+    y = out->narrow(1, out_channel, C);
+    ldy = out->size(1);
+  } else {
+    y = at::empty_like(x);
+  }
   at::Tensor mask;
   if (training && relu && res) mask = at::empty({(M * C + 7) / 8}, x.options().dtype(at::kByte));
   launch_bn_fwd(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), M, C, dtype_code(x), g, b, (float)eps,
                 (float)momentum, training ? rm : nullptr, training ? rv : nullptr, ws.data_ptr<float>(),
                 part.data_ptr<float>(), relu, training, current_stream(x), ext ? stats->data_ptr<float>() : nullptr,
-                ext ? (int)stats->size(0) : 0, mask.defined() ? mask.data_ptr<uint8_t>() : nullptr);
+                ext ? (int)stats->size(0) : 0, mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, ldy);
   return {y, ws, mask};
 }
 
@@ -166,11 +182,20 @@ std::vector<at::Tensor> bn_dual_bwd(at::Tensor dy, c10::optional<at::Tensor> mas
 std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, c10::optional<at::Tensor> mask,
                                    at::Tensor x, at::Tensor ws, c10::optional<at::Tensor> weight, int64_t mask_mode,
                                    bool need_dres, c10::optional<at::Tensor> ext_part) {
-  dy = dy.dim() == 4 ? dy.contiguous(at::MemoryFormat::ChannelsLast) : dy.contiguous();
-  check_act(dy, "dy");
   check_act(x, "x");
   const int C = (int)x.size(1);
   const int64_t M = rows_of(x);
+  // dy may be a channel slice of a wider channels_last tensor (an Inception branch of the
+  // concatenated output gradient): read in place with its row stride
+  int64_t ld_dy = 0;
+  if (dy.dim() == 4 && x.dim() == 4 && dy.sizes() == x.sizes() && dy.stride(1) == 1 && dy.stride(3) > C &&
+      dy.stride(3) % 8 == 0 && dy.stride(2) == dy.stride(3) * dy.size(3) && dy.stride(0) == dy.stride(2) * dy.size(2) &&
+      (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0 && !need_dres && mask_mode != 3) {
+    ld_dy = dy.stride(3);
+  } else {
+    dy = dy.dim() == 4 ? dy.contiguous(at::MemoryFormat::ChannelsLast) : dy.contiguous();
+    check_act(dy, "dy");
+  }
   TORCH_CHECK(mask_mode >= 0 && mask_mode <= 3, "bad mask_mode");
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() == 7 * (int64_t)C, "ws must be the 7C fp32 workspace");
   const void* yp = nullptr;
@@ -201,7 +226,7 @@ std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, c
   launch_bn_bwd(dy.data_ptr(), yp, mp, x.data_ptr(), dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr, M, C,
                 dtype_code(x), g, ws.data_ptr<float>(), part.data_ptr<float>(), dg.data_ptr<float>(),
                 db.data_ptr<float>(), (int)mask_mode, current_stream(x), ext ? ext_part->data_ptr<float>() : nullptr,
-                ext ? (int)ext_part->size(0) : 0);
+                ext ? (int)ext_part->size(0) : 0, ld_dy);
   return {dx, dres, dg, db};
 }
 
@@ -614,6 +639,8 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("mask"), pybind11::arg("mode"));
   m.def("set_mfma_pipeline", &set_mfma_pipeline, "MFMA main loop: 0 register staging, 2/3 LDS-DMA stages, -1 per-shape auto");
   m.def("mfma_pipeline", &mfma_pipeline);
+  m.def("set_bn_red_blocks", &set_bn_red_blocks, "BN reduction-pass block target (0 = default / DLA_BN_RED_BLOCKS)");
+  m.def("bn_red_blocks", &bn_red_blocks);
   m.def("conv3x3_fwd", &conv3x3_fwd, "implicit-GEMM 3x3/pad-1 conv forward (NHWC bf16, MFMA)", pybind11::arg("x"),
         pybind11::arg("w"), pybind11::arg("stride") = 1, pybind11::arg("stats") = false, pybind11::arg("tile") = 0);
   m.def("conv3x3_dgrad", &conv3x3_dgrad, "implicit-GEMM 3x3 conv data gradient (stride 1)", pybind11::arg("dy"),
@@ -648,7 +675,8 @@ void bind_nn(pybind11::module& m) {
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC", pybind11::arg("x"),
         pybind11::arg("residual"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"),
         pybind11::arg("running_var"), pybind11::arg("training"), pybind11::arg("momentum"), pybind11::arg("eps"),
-        pybind11::arg("relu"), pybind11::arg("stats") = pybind11::none());
+        pybind11::arg("relu"), pybind11::arg("stats") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
+        pybind11::arg("out_channel") = 0);
   m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC", pybind11::arg("dy"),
         pybind11::arg("y"), pybind11::arg("mask"), pybind11::arg("x"), pybind11::arg("ws"), pybind11::arg("weight"),
         pybind11::arg("mask_mode"), pybind11::arg("need_dres"), pybind11::arg("ext_part") = pybind11::none());

@@ -48,6 +48,11 @@ class Inception(nn.Module):
                                      BasicConv2d(cin, pool_proj, kernel_size=1))
 
     def forward(self, x):
+        if dnn.get_backend() == "native" and dnn.native_conv() and x.is_cuda:
+            from ..ops import inception as ninc
+
+            if ninc.supported(self, x):  # no concat copy, no autograd sum of x's four gradients
+                return ninc.inception_forward(self, x)
         return torch.cat([self.branch1(x), self.branch2(x), self.branch3(x), self.branch4(x)], 1)
 
 

@@ -1,0 +1,189 @@
+"""Native Inception block (GoogLeNet, torchvision v0.6 layout) without the concatenation copy and
+without the autograd sum of the block input's four gradients.
+
+A stock Inception block runs, besides its convolutions:
+
+* ``torch.cat`` of the four branch outputs, which copies the whole block output once;
+* in backward, ``cat``'s gradient slices, which each BN backward copies into a contiguous dy;
+* three elementwise adds, which sum the gradients of the four consumers of the block input
+  (autograd accumulation). In the round-2 GoogLeNet profile these were ``CatArrayBatchedCopy``,
+  ``elementwise_kernel`` and ``CUDAFunctor_add`` (profiles/googlenet_bs128_r2k_ksum.md).
+
+Here two autograd nodes replace them:
+
+* :class:`_InceptionFanIn` holds every consumer of ``x``: the three 1x1 convs (branch 1 and the
+  branch 2/3 reductions, MFMA GEMMs with a BN-statistics epilogue) and branch 4's 3x3/s1 ceil-mode
+  max-pool. Its backward starts from the max-pool gradient and adds each conv's data gradient to
+  it through the dgrad GEMM's addend epilogue (``dX = dY_k W_k + dX``), so x's gradient is
+  written once per consumer with no separate sum kernels.
+* :class:`_BNReluConcat` applies the four branch BatchNorm+ReLU passes straight into channel slices
+  of one preallocated NHWC block output (row stride = total channels). Its backward reads each
+  branch's dy in place from the concatenated gradient (strided loads in the BN backward passes).
+
+Reference: the block structure of torchvision's GoogLeNet v0.6, which the reference loads through
+torch.hub (/root/reference/src/network.py:33-54).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _ext
+
+CL = torch.channels_last
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    n, c, h, w = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+class _InceptionFanIn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, w2, w3, k: int, s: int, p: int, ceil: bool):
+        C = _ext.require()
+        ctx.set_materialize_grads(False)
+        n, cin, h, w = x.shape
+        xr = _rows(x)
+        outs, w2ds = [], []
+        for wt in (w1, w2, w3):
+            cout = wt.shape[0]
+            wm = wt.reshape(cout, cin).to(torch.bfloat16).contiguous()
+            y2, st = C.gemm_nt(xr, wm, True)
+            ctx.mark_non_differentiable(st)
+            outs += [y2.view(n, h, w, cout).permute(0, 3, 1, 2), st]
+            w2ds.append(wm)
+        yp, pos = C.maxpool_fwd(x, k, s, p, ceil, True)
+        ctx.save_for_backward(x, *w2ds, pos)
+        ctx.pool = (h, w, k, s, p)
+        ctx.wmeta = [(wt.dtype, wt.shape, wt.stride()) for wt in (w1, w2, w3)]
+        return (*outs, yp)
+
+    @staticmethod
+    def backward(ctx, dy1, _s1, dy2, _s2, dy3, _s3, dyp):
+        C = _ext.require()
+        x, w1, w2, w3, pos = ctx.saved_tensors
+        n, cin, h, w = x.shape
+        xr = _rows(x)
+        H, W, k, s, p = ctx.pool
+        dx = None
+        if ctx.needs_input_grad[0] and dyp is not None:
+            dx = C.maxpool_bwd(dyp.contiguous(memory_format=CL), pos, H, W, k, s, p)
+        dws = [None, None, None]
+        # branch 3 first, then 2, then 1: each data gradient is accumulated into dx by the GEMM epilogue
+        for i, (dy, wm) in reversed(list(enumerate(((dy1, w1), (dy2, w2), (dy3, w3))))):
+            if dy is None:
+                continue
+            dy = dy.contiguous(memory_format=CL)
+            if dy.dtype != torch.bfloat16:
+                dy = dy.to(torch.bfloat16)
+            d2 = _rows(dy)
+            if ctx.needs_input_grad[1 + i]:
+                dt, shape, stride = ctx.wmeta[i]
+                odt = dt if dt in (torch.float32, torch.bfloat16) else torch.float32
+                dws[i] = C.gemm_tn(d2, xr, odt, 1.0).to(dt).as_strided(shape, stride)
+            if ctx.needs_input_grad[0]:
+                add = None if dx is None else _rows(dx.contiguous(memory_format=CL))
+                dx2, _ = C.gemm_nt(d2, wm, False, add, True)
+                dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+        return dx, dws[0], dws[1], dws[2], None, None, None, None
+
+
+class _BNReluConcat(torch.autograd.Function):
+    """act(BN_b(y_b)) for every branch b, written into channel slices of one NHWC output."""
+
+    @staticmethod
+    def forward(ctx, metas, *tensors):
+        C = _ext.require()
+        ys, gs, bs = tensors[0::3], tensors[1::3], tensors[2::3]
+        n, _, h, w = ys[0].shape
+        ctot = sum(y.shape[1] for y in ys)
+        out = torch.empty((n, ctot, h, w), dtype=ys[0].dtype, device=ys[0].device, memory_format=CL)
+        wss, off = [], 0
+        for y, g, b, (rm, rv, mom, eps, st) in zip(ys, gs, bs, metas):
+            _, ws, _ = C.bn_act_fwd(y, None, g, b, rm, rv, True, mom, eps, True, st, out, off)
+            wss.append(ws)
+            off += y.shape[1]
+        ctx.save_for_backward(*ys, *gs, *wss)
+        ctx.nb = len(ys)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        C = _ext.require()
+        nb = ctx.nb
+        saved = ctx.saved_tensors
+        ys, gs, wss = saved[:nb], saved[nb:2 * nb], saved[2 * nb:]
+        dout = dout.contiguous(memory_format=CL)
+        if dout.dtype != ys[0].dtype:
+            dout = dout.to(ys[0].dtype)
+        grads, off = [None], 0
+        for y, g, ws in zip(ys, gs, wss):
+            c = y.shape[1]
+            dx, _, dg, db = C.bn_act_bwd(dout[:, off:off + c], None, None, y, ws, g, 1, False, None)
+            grads += [dx, dg, db]
+            off += c
+        return tuple(grads)
+
+
+def _bn_ok(bn: nn.BatchNorm2d) -> bool:
+    return (bn.training and bn.momentum is not None and bn.track_running_stats and bn.affine
+            and bn.weight.dtype == torch.float32)
+
+
+def supported(block, x: torch.Tensor) -> bool:
+    """The fused path: training-mode BNs with running statistics, bf16 channels_last input, native
+    1x1 / 3x3 convs for every branch conv, channel counts % 8."""
+    from . import conv as nconv
+
+    if not (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=CL)
+            and x.shape[1] % 8 == 0 and x.data_ptr() % 16 == 0):
+        return False
+    pool = block.branch4[0]
+    if not isinstance(pool, nn.MaxPool2d) or pool.return_indices or pool.dilation not in (1, (1, 1)):
+        return False
+    bcs = [block.branch1, block.branch2[0], block.branch2[1], block.branch3[0], block.branch3[1], block.branch4[1]]
+    if not all(_bn_ok(b.bn) and b.conv.out_channels % 8 == 0 for b in bcs):
+        return False
+    return all(nconv.supported(x, b.conv) and b.conv.stride == (1, 1)
+               for b in (block.branch1, block.branch2[0], block.branch3[0]))
+
+
+def inception_forward(block, x: torch.Tensor) -> torch.Tensor:
+    """The block's output on the fused path (:func:`supported` must hold)."""
+    from . import bn_act
+    from .conv import conv1x1, conv3x3, supported as sup1, supported3x3
+
+    pool = block.branch4[0]
+
+    def pair(v):
+        return v[0] if isinstance(v, (tuple, list)) else v
+
+    k, s, p = pair(pool.kernel_size), pair(pool.stride or pool.kernel_size), pair(pool.padding)
+    y1, s1, y2r, s2r, y3r, s3r, yp = _InceptionFanIn.apply(
+        x, block.branch1.conv.weight, block.branch2[0].conv.weight, block.branch3[0].conv.weight, k, s, p,
+        bool(pool.ceil_mode))
+    outs = [(y1, block.branch1.bn, s1)]
+    for red, stats, conv_bn in ((y2r, s2r, block.branch2), (y3r, s3r, block.branch3)):
+        a = bn_act.fused_bn_act(red, conv_bn[0].bn, True, None, stats)
+        c = conv_bn[1].conv
+        if supported3x3(a, c):
+            y, st = conv3x3(a, c, want_stats=True)
+        elif sup1(a, c):
+            y, st = conv1x1(a, c, want_stats=True)
+        else:
+            y, st = c(a), None
+        outs.append((y, conv_bn[1].bn, st))
+    c4 = block.branch4[1].conv
+    y4, st4 = conv1x1(yp, c4, want_stats=True) if sup1(yp, c4) else (c4(yp), None)
+    outs.append((y4, block.branch4[1].bn, st4))
+    metas, tensors = [], []
+    for y, bn, st in outs:
+        if not (y.is_contiguous(memory_format=CL) and y.dtype == torch.bfloat16):
+            y = y.contiguous(memory_format=CL).to(torch.bfloat16)
+        metas.append((bn.running_mean, bn.running_var, float(bn.momentum), float(bn.eps), st))
+        tensors += [y, bn.weight, bn.bias]
+        bn_act._PENDING_COUNTERS.append(bn.num_batches_tracked)
+    if len(bn_act._PENDING_COUNTERS) >= 1024:  # used without a DP wrapper: flush periodically
+        bn_act.flush_bn_counters()
+    return _BNReluConcat.apply(tuple(metas), *tensors)

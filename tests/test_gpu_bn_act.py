@@ -209,3 +209,33 @@ def test_bn_fwd_external_stats_fold(cuda, rows, C):
     torch.testing.assert_close(rm.double(), 0.1 * mean, rtol=1e-4, atol=1e-4)
     ref = (xf - mean) * (var + 1e-5).rsqrt() * w.double() + b.double()
     torch.testing.assert_close(y.double(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.fixture
+def red_blocks_4096():
+    """More than 1024 reduction blocks: the partial rows go through the coalesced fold pass
+    (bn_fold_rows) before every finalize (statistics, backward, pooled backward, dual backward)."""
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    C.set_bn_red_blocks(4096)
+    try:
+        yield
+    finally:
+        C.set_bn_red_blocks(0)
+
+
+@pytest.mark.parametrize("relu,use_res", [(True, False), (True, True), (False, False)])
+def test_bn_fold_path_fwd_bwd(cuda, red_blocks_4096, relu, use_res):
+    from distributed_learning_amd.ops import _ext
+
+    assert _ext.require().bn_red_blocks() == 4096
+    test_bn_act_fwd_bwd(cuda, torch.bfloat16, (64, 64, 64, 64), relu, use_res)
+    test_bn_act_fwd_bwd(cuda, torch.float32, (16, 96, 72, 72), relu, use_res)
+
+
+def test_bn_fold_path_dual_and_pool(cuda, red_blocks_4096):
+    from test_gpu_pool import test_stem_bn_relu_maxpool_fused_matches_unfused
+
+    test_bn_dual_residual_fwd_bwd(cuda, torch.bfloat16, (64, 64, 64, 64), True)
+    test_stem_bn_relu_maxpool_fused_matches_unfused(cuda, (16, 64, 112, 112), 3, 2, 1, False)
