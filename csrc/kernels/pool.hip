@@ -12,6 +12,7 @@
 //           resolved by reading the 1-byte positions instead of re-reading x.
 #include "dla_common.h"
 #include "dla_kernels.h"
+#include "dla_mfma.h"
 
 #include <algorithm>
 
@@ -21,20 +22,43 @@ constexpr int kPoolThreads = 256;
 
 struct PoolGeom {
   int N, H, W, C, OH, OW, k, s, p;
+  mm::FastDiv fcg, fw, fh;  // divisors of the flat index: C/8, width, height (output or input side)
 };
 
-template <typename T>
+// Flat index t -> (n, row, col, channel) of an [N, rows, cols, C] NHWC tensor in 8-channel groups.
+// kFast: multiply-shift division (t < 2^24, host-checked), else hardware integer division.
+template <bool kFast>
+__device__ __forceinline__ void decode(int t, const PoolGeom& g, int cols, int rows, int& n, int& row, int& col,
+                                       int& c) {
+  const int cg = g.C / 8;
+  int q, r;
+  if constexpr (kFast) {
+    q = (int)mm::fdiv((uint32_t)t, g.fcg);
+    c = (t - q * cg) * 8;
+    r = (int)mm::fdiv((uint32_t)q, g.fw);
+    col = q - r * cols;
+    n = (int)mm::fdiv((uint32_t)r, g.fh);
+    row = r - n * rows;
+  } else {
+    q = t / cg;
+    c = (t - q * cg) * 8;
+    r = q / cols;
+    col = q - r * cols;
+    n = r / rows;
+    row = r - n * rows;
+  }
+}
+
+// K > 0: the window size is a compile-time constant (GoogLeNet / ResNet use 3 and 2): all K*K taps
+// are loaded before the first comparison (out-of-range taps read a clamped in-range pixel and are
+// masked to -inf), so the loads are in flight together.
+template <typename T, int K, bool kFast>
 __global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                                    uint8_t* __restrict__ pos, PoolGeom g) {
-  const int cg = g.C / 8;
-  const int total = g.N * g.OH * g.OW * cg;  // < 2^31 (host-checked): 32-bit index math
+  const int total = g.N * g.OH * g.OW * (g.C / 8);  // < 2^31 (host-checked): 32-bit index math
   for (int t = blockIdx.x * kPoolThreads + threadIdx.x; t < total; t += gridDim.x * kPoolThreads) {
-    const int c = (t % cg) * 8;
-    int r = t / cg;
-    const int ow = r % g.OW;
-    r /= g.OW;
-    const int oh = r % g.OH;
-    const int n = r / g.OH;
+    int n, oh, ow, c;
+    decode<kFast>(t, g, g.OW, g.OH, n, oh, ow, c);
     float best[8];
     uint32_t bi[8];
 #pragma unroll
@@ -43,22 +67,42 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_kernel(const T* __re
       bi[j] = 0;
     }
     const int h0 = oh * g.s - g.p, w0 = ow * g.s - g.p;
-    for (int ky = 0; ky < g.k; ++ky) {
-      const int h = h0 + ky;
-      if (h < 0 || h >= g.H) continue;
-      for (int kx = 0; kx < g.k; ++kx) {
-        const int w = w0 + kx;
-        if (w < 0 || w >= g.W) continue;
-        float v[8];
-        Vec8<T>::load(x + (((int64_t)n * g.H + h) * g.W + w) * g.C + c, v);
-        const uint32_t q = (uint32_t)(ky * g.k + kx);
+    const T* img = x + (int64_t)n * g.H * g.W * g.C + c;
+    auto take = [&](const float (&v)[8], uint32_t q) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          // strict '>' keeps the first maximum; a NaN wins and sticks (PyTorch semantics)
-          if (v[j] > best[j] || (v[j] != v[j] && best[j] == best[j])) {
-            best[j] = v[j];
-            bi[j] = q;
-          }
+      for (int j = 0; j < 8; ++j) {
+        // strict '>' keeps the first maximum; a NaN wins and sticks (PyTorch semantics)
+        if (v[j] > best[j] || (v[j] != v[j] && best[j] == best[j])) {
+          best[j] = v[j];
+          bi[j] = q;
+        }
+      }
+    };
+    if constexpr (K > 0) {
+      float v[K * K][8];
+      bool ok[K * K];
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          const int h = h0 + ky, w = w0 + kx, q = ky * K + kx;
+          ok[q] = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+          const int hc = min(max(h, 0), g.H - 1), wc = min(max(w, 0), g.W - 1);
+          Vec8<T>::load(img + ((int64_t)hc * g.W + wc) * g.C, v[q]);
+        }
+#pragma unroll
+      for (int q = 0; q < K * K; ++q)
+        if (ok[q]) take(v[q], (uint32_t)q);
+    } else {
+      for (int ky = 0; ky < g.k; ++ky) {
+        const int h = h0 + ky;
+        if (h < 0 || h >= g.H) continue;
+        for (int kx = 0; kx < g.k; ++kx) {
+          const int w = w0 + kx;
+          if (w < 0 || w >= g.W) continue;
+          float v[8];
+          Vec8<T>::load(img + ((int64_t)h * g.W + w) * g.C, v);
+          take(v, (uint32_t)(ky * g.k + kx));
         }
       }
     }
@@ -73,19 +117,16 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_kernel(const T* __re
   }
 }
 
-template <typename T>
+// Backward, gather form: the windows covering input pixel (h, w) are oh in [oh_lo, oh_hi] (at most
+// ceil(K/s) per axis). R = compile-time bound of windows per axis (0: runtime loops).
+template <typename T, int R, bool kFast>
 __global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_kernel(const T* __restrict__ dy,
                                                                    const uint8_t* __restrict__ pos,
                                                                    T* __restrict__ dx, PoolGeom g) {
-  const int cg = g.C / 8;
-  const int total = g.N * g.H * g.W * cg;
+  const int total = g.N * g.H * g.W * (g.C / 8);
   for (int t = blockIdx.x * kPoolThreads + threadIdx.x; t < total; t += gridDim.x * kPoolThreads) {
-    const int c = (t % cg) * 8;
-    int r = t / cg;
-    const int w = r % g.W;
-    r /= g.W;
-    const int h = r % g.H;
-    const int n = r / g.H;
+    int n, h, w, c;
+    decode<kFast>(t, g, g.W, g.H, n, h, w, c);
     // windows covering (h, w): oh*s - p <= h <= oh*s - p + k - 1
     const int hp = h + g.p, wp = w + g.p;
     const int oh_lo = hp < g.k - 1 ? 0 : (hp - g.k + 1 + g.s - 1) / g.s;
@@ -95,16 +136,41 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_kernel(const T* __re
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        const uint32_t q = (uint32_t)((hp - oh * g.s) * g.k + (wp - ow * g.s));
-        const int64_t off = (((int64_t)n * g.OH + oh) * g.OW + ow) * g.C + c;
-        const uint64_t packed = *reinterpret_cast<const uint64_t*>(pos + off);
-        float d[8];
-        Vec8<T>::load(dy + off, d);
+    const int64_t nbase = (int64_t)n * g.OH * g.OW;
+    if constexpr (R > 0) {
+      uint64_t pk[R * R];
+      float d[R * R][8];
+      uint32_t qv[R * R];
+      bool ok[R * R];
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int b = 0; b < R; ++b) {
+          const int oh = oh_lo + a, ow = ow_lo + b, i = a * R + b;
+          ok[i] = oh <= oh_hi && ow <= ow_hi;
+          const int ohc = ok[i] ? oh : oh_lo, owc = ok[i] ? ow : ow_lo;  // in range whenever any window is
+          qv[i] = (uint32_t)((hp - ohc * g.s) * g.k + (wp - owc * g.s));
+          const int64_t off = (nbase + (int64_t)min(ohc, g.OH - 1) * g.OW + min(owc, g.OW - 1)) * g.C + c;
+          pk[i] = *reinterpret_cast<const uint64_t*>(pos + off);
+          Vec8<T>::load(dy + off, d[i]);
+        }
+#pragma unroll
+      for (int i = 0; i < R * R; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (((packed >> (8 * j)) & 0xffu) == q) acc[j] += d[j];
+          if (ok[i] && ((pk[i] >> (8 * j)) & 0xffu) == qv[i]) acc[j] += d[i][j];
+    } else {
+      for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+        for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+          const uint32_t q = (uint32_t)((hp - oh * g.s) * g.k + (wp - ow * g.s));
+          const int64_t off = (nbase + (int64_t)oh * g.OW + ow) * g.C + c;
+          const uint64_t packed = *reinterpret_cast<const uint64_t*>(pos + off);
+          float dd[8];
+          Vec8<T>::load(dy + off, dd);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (((packed >> (8 * j)) & 0xffu) == q) acc[j] += dd[j];
+        }
       }
     }
     Vec8<T>::store(dx + (((int64_t)n * g.H + h) * g.W + w) * g.C + c, acc);
@@ -119,28 +185,41 @@ static int pool_blocks(int64_t work) {
 
 void launch_maxpool_fwd(const void* x, void* y, uint8_t* pos, int N, int H, int W, int C, int OH, int OW, int k,
                         int s, int p, int dtype, hipStream_t stream) {
-  PoolGeom g{N, H, W, C, OH, OW, k, s, p};
-  const int nb = pool_blocks((int64_t)N * OH * OW * (C / 8));
+  PoolGeom g{N, H, W, C, OH, OW, k, s, p, mm::make_fastdiv(C / 8), mm::make_fastdiv(OW), mm::make_fastdiv(OH)};
+  const int64_t work = (int64_t)N * OH * OW * (C / 8);
+  const int nb = pool_blocks(work);
   if (nb == 0) return;
-  if (dtype == kBF16)
-    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, dim3(nb), dim3(kPoolThreads), 0, stream, (const bf16_t*)x,
-                       (bf16_t*)y, pos, g);
-  else
-    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(nb), dim3(kPoolThreads), 0, stream, (const float*)x,
-                       (float*)y, pos, g);
+  const bool fast = work < (1 << 24);
+#define DLA_MPF(T, K, F) \
+  hipLaunchKernelGGL((maxpool_fwd_kernel<T, K, F>), dim3(nb), dim3(kPoolThreads), 0, stream, (const T*)x, (T*)y, pos, g)
+#define DLA_MPF_K(T)                                                      \
+  if (k == 3) { if (fast) DLA_MPF(T, 3, true); else DLA_MPF(T, 3, false); } \
+  else if (k == 2) { if (fast) DLA_MPF(T, 2, true); else DLA_MPF(T, 2, false); } \
+  else { if (fast) DLA_MPF(T, 0, true); else DLA_MPF(T, 0, false); }
+  if (dtype == kBF16) { DLA_MPF_K(bf16_t) } else { DLA_MPF_K(float) }
+#undef DLA_MPF_K
+#undef DLA_MPF
 }
 
 void launch_maxpool_bwd(const void* dy, const uint8_t* pos, void* dx, int N, int H, int W, int C, int OH, int OW,
                         int k, int s, int p, int dtype, hipStream_t stream) {
-  PoolGeom g{N, H, W, C, OH, OW, k, s, p};
-  const int nb = pool_blocks((int64_t)N * H * W * (C / 8));
+  PoolGeom g{N, H, W, C, OH, OW, k, s, p, mm::make_fastdiv(C / 8), mm::make_fastdiv(W), mm::make_fastdiv(H)};
+  const int64_t work = (int64_t)N * H * W * (C / 8);
+  const int nb = pool_blocks(work);
   if (nb == 0) return;
-  if (dtype == kBF16)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, dim3(nb), dim3(kPoolThreads), 0, stream, (const bf16_t*)dy, pos,
-                       (bf16_t*)dx, g);
-  else
-    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(nb), dim3(kPoolThreads), 0, stream, (const float*)dy, pos,
-                       (float*)dx, g);
+  const bool fast = work < (1 << 24);
+  const int r = (k + s - 1) / s;  // windows per axis covering one input pixel, at most
+#define DLA_MPB(T, R, F)                                                                                        \
+  hipLaunchKernelGGL((maxpool_bwd_kernel<T, R, F>), dim3(nb), dim3(kPoolThreads), 0, stream, (const T*)dy, pos, \
+                     (T*)dx, g)
+#define DLA_MPB_R(T)                                                      \
+  if (r == 3) { if (fast) DLA_MPB(T, 3, true); else DLA_MPB(T, 3, false); } \
+  else if (r == 2) { if (fast) DLA_MPB(T, 2, true); else DLA_MPB(T, 2, false); } \
+  else if (r == 1) { if (fast) DLA_MPB(T, 1, true); else DLA_MPB(T, 1, false); } \
+  else { if (fast) DLA_MPB(T, 0, true); else DLA_MPB(T, 0, false); }
+  if (dtype == kBF16) { DLA_MPB_R(bf16_t) } else { DLA_MPB_R(float) }
+#undef DLA_MPB_R
+#undef DLA_MPB
 }
 
 // ---- global average pooling (the ResNet / GoogLeNet head) ------------------------------------------

@@ -13,6 +13,9 @@ pytestmark = pytest.mark.gpu
     ((2, 480, 28, 28), 3, 1, 1, True),     # inception branch4
     ((2, 832, 14, 14), 2, 2, 0, True),     # GoogLeNet maxpool4
     ((3, 24, 9, 13), 3, 2, 1, False),
+    ((2, 16, 11, 11), 5, 2, 2, False),     # runtime window size (generic path)
+    ((2, 16, 12, 10), 4, 3, 1, True),      # k = 4: generic forward, 2x2-window backward
+    ((40, 256, 128, 128), 3, 1, 1, False),  # > 2^24 work items: hardware-division index path
 ])
 def test_maxpool_matches_torch(cuda, dtype, shape, k, s, p, ceil):
     from distributed_learning_amd.ops import nn as dnn
