@@ -580,13 +580,17 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3s2_dgrad_kernel(const bf16
 template <int BM, int BN, int PIPE>
 __global__ __launch_bounds__(kThreads, 2) void conv3x3_wgrad_kernel(const bf16_t* __restrict__ dy,
                                                                     const bf16_t* __restrict__ x, ConvGeom g,
-                                                                    float* __restrict__ part, int k_per_split) {
+                                                                    float* __restrict__ part, int k_per_split,
+                                                                    int ntiles, int remap) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int P = g.N * g.OH * g.OW;
   const int Mo = g.Cout, No = 9 * g.Cin;
   const int nbn = (No + BN - 1) / BN;
-  const int bm = blockIdx.x / nbn, bn = blockIdx.x % nbn;
-  const int kbeg = blockIdx.y * k_per_split;
+  // tiles of one split (the 9 taps x Cin columns over the same pixels) on one XCD (gemm_tn_kernel)
+  const int lin = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int tile = lin % ntiles, split = lin / ntiles;
+  const int bm = tile / nbn, bn = tile % nbn;
+  const int kbeg = split * k_per_split;
   const int kend = min(P, kbeg + k_per_split);
   const int m0 = bm * BM, n0 = bn * BN;
   const KLoader<BM> la{dy, g.Cout, m0, Mo, kend};
@@ -595,7 +599,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_wgrad_kernel(const bf16_t
   Acc<BM, BN> acc;
   acc.zero();
   run_mainloop<PIPE>(la, lb, kbeg, kend, acc, smem_raw);
-  epilogue_f32<BM, BN>(acc, part + (int64_t)blockIdx.y * Mo * No, Mo, No, m0, n0);
+  epilogue_f32<BM, BN>(acc, part + (int64_t)split * Mo * No, Mo, No, m0, n0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -774,9 +778,10 @@ void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int spl
   kps = (kps + kBK - 1) / kBK * kBK;
   const int Mo = Cout, No = 9 * Cin;
 #define DLA_WG(BM_, P_)                                                                                         \
-  hipLaunchKernelGGL((conv3x3_wgrad_kernel<BM_, 128, P_>), dim3(((Mo + BM_ - 1) / BM_) * ((No + 127) / 128), splits), \
+  hipLaunchKernelGGL((conv3x3_wgrad_kernel<BM_, 128, P_>), dim3(((Mo + BM_ - 1) / BM_) * ((No + 127) / 128) * splits), \
                      dim3(kThreads), (run_mainloop_lds_bytes<P_, BM_, 128, KLoader<BM_>, Im2colKLoader<128, P_ != 0>>()), \
-                     stream, (const bf16_t*)dy, (const bf16_t*)x, g, partial, kps)
+                     stream, (const bf16_t*)dy, (const bf16_t*)x, g, partial, kps,                                  \
+                     ((Mo + BM_ - 1) / BM_) * ((No + 127) / 128), (int)splitk_xcd_remap())
 #define DLA_WG_P(BM_)                   \
   switch (mfma_pipeline_for(kps)) {     \
     case 0: DLA_WG(BM_, 0); break;      \

@@ -18,6 +18,8 @@
 //   * gemm_tn reads k-major operands straight from their natural layout with the gfx950
 //     ds_read_b64_tr_b16 transposing LDS read (T10) and splits the long M reduction over blocks
 //     with fp32 partial slabs + a separate reduction kernel.
+#include <cstdlib>
+
 #include "dla_common.h"
 #include "dla_kernels.h"
 #include "dla_mfma.h"
@@ -66,11 +68,15 @@ template <int BM, int BN, int PIPE>
 __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               float* __restrict__ P, int Mo, int No, int K,
-                                                              int k_per_split) {
+                                                              int k_per_split, int ntiles, int remap) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int nbn = (No + BN - 1) / BN;
-  const int bm = blockIdx.x / nbn, bn = blockIdx.x % nbn;
-  const int kbeg = blockIdx.y * k_per_split;
+  // 1-D grid of tiles x splits; with remap the tiles of one split (which read the same K rows of
+  // both operands) are consecutive logical ids, i.e. co-scheduled on one XCD and its L2
+  const int lin = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int tile = lin % ntiles, split = lin / ntiles;
+  const int bm = tile / nbn, bn = tile % nbn;
+  const int kbeg = split * k_per_split;
   const int kend = min(K, kbeg + k_per_split);
   const int m0 = bm * BM, n0 = bn * BN;
   Acc<BM, BN> acc;
@@ -78,7 +84,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(const bf16_t* __re
   const KLoader<BM> la{A, lda, m0, Mo, kend};
   const KLoader<BN> lb{B, ldb, n0, No, kend};
   run_mainloop<PIPE>(la, lb, kbeg, kend, acc, smem_raw);
-  epilogue_f32<BM, BN>(acc, P + (int64_t)blockIdx.y * Mo * No, Mo, No, m0, n0);
+  epilogue_f32<BM, BN>(acc, P + (int64_t)split * Mo * No, Mo, No, m0, n0);
 }
 
 // Sums the split-K fp32 slabs: each thread owns 4 consecutive outputs (one 16-byte load per slab)
@@ -226,6 +232,15 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
 static inline int tn_bm(int Mo) { return Mo <= 64 ? 64 : 128; }
 static inline int tn_bn(int No) { return No <= 64 ? 64 : 128; }
 
+// XCD-aware ordering of split-K grids (DLA_SPLITK_XCD=0 restores the split-major 2-D order, A/B)
+bool splitk_xcd_remap() {
+  static const bool v = [] {
+    const char* e = std::getenv("DLA_SPLITK_XCD");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 int gemm_tn_splits(int Mo, int No, int K) {
   // ~512 workgroups in flight (2 per CU) and >= 16 K-steps per split: enough parallelism for the
   // long M reduction while keeping the fp32 slab traffic (splits * Mo * No * 4 B) small.
@@ -242,9 +257,9 @@ void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, floa
   const int bm = tn_bm(Mo), bn = tn_bn(No);
   const int tiles = ((Mo + bm - 1) / bm) * ((No + bn - 1) / bn);
 #define DLA_TN(BM_, BN_, P_)                                                                                      \
-  hipLaunchKernelGGL((gemm_tn_kernel<BM_, BN_, P_>), dim3(tiles, splits), dim3(kThreads),                         \
+  hipLaunchKernelGGL((gemm_tn_kernel<BM_, BN_, P_>), dim3(tiles * splits), dim3(kThreads),                      \
                      (run_mainloop_lds_bytes<P_, BM_, BN_, KLoader<BM_>, KLoader<BN_>>()), stream, (const bf16_t*)A, \
-                     lda, (const bf16_t*)B, ldb, partial, Mo, No, K, kps)
+                     lda, (const bf16_t*)B, ldb, partial, Mo, No, K, kps, tiles, (int)splitk_xcd_remap())
 #define DLA_TN_P(BM_, BN_)                 \
   switch (mfma_pipeline_for(kps)) {        \
     case 0: DLA_TN(BM_, BN_, 0); break;    \

@@ -199,12 +199,15 @@ __global__ __launch_bounds__(kThreads, 2) void stem_fwd_kernel(const bf16_t* __r
 template <int BM, int BN, int PIPE>
 __global__ __launch_bounds__(kThreads, 2) void stem_wgrad_kernel(const bf16_t* __restrict__ dy,
                                                                  const bf16_t* __restrict__ xs, StemGeom g, int Cout,
-                                                                 float* __restrict__ part, int k_per_split) {
+                                                                 float* __restrict__ part, int k_per_split,
+                                                                 int ntiles, int remap) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int P = g.N * g.BH * g.BW;
   const int nbn = (kStemK + BN - 1) / BN;
-  const int bm = blockIdx.x / nbn, bn = blockIdx.x % nbn;
-  const int kbeg = blockIdx.y * k_per_split;
+  const int lin = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;  // see gemm_tn_kernel
+  const int tile = lin % ntiles, split = lin / ntiles;
+  const int bm = tile / nbn, bn = tile % nbn;
+  const int kbeg = split * k_per_split;
   const int kend = min(P, kbeg + k_per_split);
   const int m0 = bm * BM, n0 = bn * BN;
   const KLoader<BM> la{dy, Cout, m0, Cout, kend};
@@ -213,7 +216,7 @@ __global__ __launch_bounds__(kThreads, 2) void stem_wgrad_kernel(const bf16_t* _
   Acc<BM, BN> acc;
   acc.zero();
   run_mainloop<PIPE>(la, lb, kbeg, kend, acc, smem_raw);
-  epilogue_f32<BM, BN>(acc, part + (int64_t)blockIdx.y * Cout * kStemK, Cout, kStemK, m0, n0);
+  epilogue_f32<BM, BN>(acc, part + (int64_t)split * Cout * kStemK, Cout, kStemK, m0, n0);
 }
 
 static StemGeom make_stem_geom(int N, int H, int W) {
@@ -273,9 +276,9 @@ void launch_stem_wgrad(const void* dy, const void* xs, float* partial, int split
   const int tiles = ((Cout + 63) / 64) * (kStemK / 128);
   const int pipe = mfma_pipeline_for(kps);
 #define DLA_STEM_WG(P_)                                                                                          \
-  hipLaunchKernelGGL((stem_wgrad_kernel<64, 128, P_>), dim3(tiles, splits), dim3(kThreads),                     \
+  hipLaunchKernelGGL((stem_wgrad_kernel<64, 128, P_>), dim3(tiles * splits), dim3(kThreads),                  \
                      (run_mainloop_lds_bytes<P_, 64, 128, KLoader<64>, StemKLoader<128, P_ != 0>>()), stream,    \
-                     (const bf16_t*)dy, (const bf16_t*)xs, g, Cout, partial, kps)
+                     (const bf16_t*)dy, (const bf16_t*)xs, g, Cout, partial, kps, tiles, (int)splitk_xcd_remap())
   if (pipe == 0) DLA_STEM_WG(0); else DLA_STEM_WG(2);
 #undef DLA_STEM_WG
   launch_splitk_reduce(partial, splits, (int64_t)Cout * kStemK, dwpk, out_dtype, 1.f, false, stream);
