@@ -12,7 +12,9 @@ def _C():
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 64, 64), (1000, 64, 256), (777, 136, 72), (12544, 512, 2048),
-                                   (4096, 256, 64), (130, 8, 8), (50176, 1024, 256)])
+                                   (4096, 256, 64), (130, 8, 8), (50176, 1024, 256),
+                                   # >= 2048 tiles with K <= 256: the persistent short-K kernel
+                                   (262181, 200, 136), (300000, 64, 64), (131072, 512, 128)])
 def test_gemm_nt(cuda, M, N, K):
     C = _C()
     torch.manual_seed(0)
@@ -53,7 +55,7 @@ def test_gemm_tn(cuda, K, Mo, No):
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 64, 256), (777, 136, 72), (12544, 512, 2048), (130, 8, 8),
-                                   (50176, 256, 1024)])
+                                   (50176, 256, 1024), (262181, 200, 136), (300000, 64, 64)])
 def test_gemm_nt_kmajor_b_and_addend(cuda, M, N, K):
     """b_kmajor: C = A @ B with B [K, N] (dgrad with the weight as stored); the fused addend gives
     bf16(bf16(A @ B) + D) exactly like the unfused add."""
