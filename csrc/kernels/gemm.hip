@@ -159,7 +159,11 @@ static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb
     if (mfma_pipeline() == 2) launch_nt_p<BM, BN, S, BT, 2, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
     else launch_nt_p<BM, BN, S, BT, 3, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
   } else {
-    switch (mfma_pipeline_for(K)) {
+    // 1x1-conv GEMMs: register staging (36 KB LDS, 4 blocks / CU) up to K = 512, the 2-stage
+    // LDS-DMA loop (64 KB, 2 blocks / CU) above — per-layer A/B at ResNet-50 bs512 shapes,
+    // profiles/r2t (auto K<256 threshold: 9.58-9.71 ms fwd+dgrad; K<=512: 9.43 ms)
+    const int pipe = mfma_pipeline() >= 0 ? mfma_pipeline() : (K > 512 ? 2 : 0);
+    switch (pipe) {
       case 0: launch_nt_p<BM, BN, S, BT, 0, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
       case 3: launch_nt_p<BM, BN, S, BT, 3, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
       case 4: launch_nt_p<BM, BN, S, BT, 4, kThreads>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream); break;
