@@ -21,6 +21,7 @@
 #include "dla_mfma.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace dla {
@@ -603,6 +604,19 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_wgrad_kernel(const bf16_t
 }
 
 // ---------------------------------------------------------------------------------------------
+// Main loop of the 3x3 kernels when not forced (set_mfma_pipeline): per-layer A/B at ResNet-50
+// bs512 (profiles/r2v): forward and data gradient fastest on the buffer-DMA loop (PIPE 6: 2.62 /
+// 2.83 ms vs 2.69 / 2.95 on PIPE 2), the weight gradient on the v2 schedule (PIPE 4: 3.06 vs 3.20)
+static int conv_pipeline(int K, int deep) {
+  const int forced = mfma_pipeline();
+  if (forced >= 0) return forced;
+  static const int env = [] {  // DLA_CONV_PIPE: one loop for all 3x3 passes (A/B runs)
+    const char* e = std::getenv("DLA_CONV_PIPE");
+    return e ? std::atoi(e) : -1;
+  }();
+  return K >= 256 ? (env >= 0 ? env : deep) : 0;
+}
+
 static ConvGeom make_geom(int N, int H, int W, int Cin, int Cout, int stride) {
   ConvGeom g;
   g.N = N;
@@ -642,7 +656,7 @@ static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGe
     if (mfma_pipeline_for(9 * g.Cin) == 0) launch_fwd_p<BM, BN, S, 100, kThreads>(x, w, y, g, stats, stream);
     else launch_fwd_p<BM, BN, S, 102, kThreads>(x, w, y, g, stats, stream);
   } else {
-    switch (mfma_pipeline_for(9 * g.Cin)) {
+    switch (conv_pipeline(9 * g.Cin, 6)) {
       case 0: launch_fwd_p<BM, BN, S, 0, kThreads>(x, w, y, g, stats, stream); break;
       case 3: launch_fwd_p<BM, BN, S, 3, kThreads>(x, w, y, g, stats, stream); break;
       case 4: launch_fwd_p<BM, BN, S, 4, kThreads>(x, w, y, g, stats, stream); break;
@@ -704,7 +718,7 @@ static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const Co
     if (mfma_pipeline_for(9 * g.Cout) == 0) launch_dgrad_p<BM, BN, 100, kThreads>(dy, w, dx, g, addend, bnb, stream);
     else launch_dgrad_p<BM, BN, 102, kThreads>(dy, w, dx, g, addend, bnb, stream);
   } else {
-    switch (mfma_pipeline_for(9 * g.Cout)) {
+    switch (conv_pipeline(9 * g.Cout, 6)) {
       case 0: launch_dgrad_p<BM, BN, 0, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
       case 3: launch_dgrad_p<BM, BN, 3, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
       case 4: launch_dgrad_p<BM, BN, 4, kThreads>(dy, w, dx, g, addend, bnb, stream); break;
@@ -765,7 +779,7 @@ int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int stride) {
   const int P = g.N * g.OH * g.OW;
   const int bm = Cout <= 64 ? 64 : 128;
   const int tiles = ((Cout + bm - 1) / bm) * ((9 * Cin + 127) / 128);
-  const int splits = std::max(1, 512 / std::max(1, tiles));  // ~2 workgroups per CU
+  const int splits = std::max(1, splitk_target_blocks() / std::max(1, tiles));  // ~2 workgroups per CU
   const int max_splits = std::max(1, P / (8 * kBK));          // >= 8 k-steps per split
   return std::max(1, std::min(splits, max_splits));
 }
@@ -783,7 +797,7 @@ void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int spl
                      stream, (const bf16_t*)dy, (const bf16_t*)x, g, partial, kps,                                  \
                      ((Mo + BM_ - 1) / BM_) * ((No + 127) / 128), (int)splitk_xcd_remap())
 #define DLA_WG_P(BM_)                   \
-  switch (mfma_pipeline_for(kps)) {     \
+  switch (conv_pipeline(kps, 4)) {      \
     case 0: DLA_WG(BM_, 0); break;      \
     case 3: DLA_WG(BM_, 3); break;      \
     case 4: DLA_WG(BM_, 4); break;      \

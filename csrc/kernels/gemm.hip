@@ -245,11 +245,22 @@ bool splitk_xcd_remap() {
   return v;
 }
 
+// Workgroups a split-K weight-gradient launch aims for (tiles x splits): 512 = 2 per CU;
+// DLA_SPLITK_BLOCKS overrides it for A/B runs
+int splitk_target_blocks() {
+  static const int v = [] {
+    const char* e = std::getenv("DLA_SPLITK_BLOCKS");
+    const int b = e ? std::atoi(e) : 0;
+    return b > 0 ? b : 512;
+  }();
+  return v;
+}
+
 int gemm_tn_splits(int Mo, int No, int K) {
   // ~512 workgroups in flight (2 per CU) and >= 16 K-steps per split: enough parallelism for the
   // long M reduction while keeping the fp32 slab traffic (splits * Mo * No * 4 B) small.
   const int tiles = ((Mo + tn_bm(Mo) - 1) / tn_bm(Mo)) * ((No + tn_bn(No) - 1) / tn_bn(No));
-  int splits = std::max(1, 512 / std::max(1, tiles));
+  int splits = std::max(1, splitk_target_blocks() / std::max(1, tiles));
   const int max_splits = std::max(1, K / (16 * kBK));
   return std::max(1, std::min(splits, max_splits));
 }

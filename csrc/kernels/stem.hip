@@ -263,7 +263,7 @@ int stem_wgrad_splits(int N, int H, int W, int Cout) {
   const StemGeom g = make_stem_geom(N, H, W);
   const int P = N * g.BH * g.BW;
   const int tiles = ((Cout + 63) / 64) * (kStemK / 128);
-  const int splits = std::max(1, 512 / tiles);
+  const int splits = std::max(1, splitk_target_blocks() / tiles);
   return std::max(1, std::min(splits, P / (16 * kBK)));
 }
 

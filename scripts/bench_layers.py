@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--pipe", type=int, default=-1, help="force the MFMA main loop (see set_mfma_pipeline)")
+    ap.add_argument("--tile", type=int, default=0, help="force the fwd/dgrad tile config (0 = auto; see TileCfg)")
     a = ap.parse_args()
     C.set_mfma_pipeline(a.pipe)
     B = a.batch
@@ -77,8 +78,8 @@ def main():
             X = torch.randn(M_out, Cin, device=dev).to(torch.bfloat16)
             W = (torch.randn(Cout, Cin, device=dev) * 0.05).to(torch.bfloat16)
             dY = torch.randn(M_out, Cout, device=dev).to(torch.bfloat16)
-            fns = {"fwd": lambda: C.gemm_nt(X, W, True),
-                   "dgrad": lambda: C.gemm_nt(dY, W, False, None, True),
+            fns = {"fwd": lambda: C.gemm_nt(X, W, True, None, False, a.tile),
+                   "dgrad": lambda: C.gemm_nt(dY, W, False, None, True, a.tile),
                    "wgrad": lambda: C.gemm_tn(dY, X, torch.bfloat16, 1.0)}
             byts = {"fwd": (M_out * Cin + M_out * Cout + Cin * Cout) * 2,
                     "dgrad": (M_out * Cout + M_out * Cin + Cin * Cout) * 2,
@@ -88,8 +89,8 @@ def main():
             w = (torch.randn(Cout, Cin, 3, 3, device=dev) * 0.05).to(torch.bfloat16).contiguous(
                 memory_format=torch.channels_last)
             dy = torch.randn(B, Cout, OH, OH, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-            fns = {"fwd": lambda: C.conv3x3_fwd(x, w, s, True),
-                   "dgrad": (lambda: C.conv3x3_dgrad(dy, w)) if s == 1 else (lambda: C.conv3x3s2_dgrad(dy, w, H, H)),
+            fns = {"fwd": lambda: C.conv3x3_fwd(x, w, s, True, a.tile),
+                   "dgrad": (lambda: C.conv3x3_dgrad(dy, w, None, a.tile)) if s == 1 else (lambda: C.conv3x3s2_dgrad(dy, w, H, H)),
                    "wgrad": lambda: C.conv3x3_wgrad(dy, x, s, torch.bfloat16)}
             byts = {"fwd": (M_in * Cin + M_out * Cout + 9 * Cin * Cout) * 2,
                     "dgrad": (M_out * Cout + M_in * Cin + 9 * Cin * Cout) * 2,
