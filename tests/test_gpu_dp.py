@@ -20,7 +20,7 @@ def world1(cuda):
     ctx.shutdown()
 
 
-def _train(model_fn, wrap, steps, bf16):
+def _train(model_fn, wrap, steps, bf16, shape=(3, 32, 32)):
     from distributed_learning_amd.data import SyntheticBatches
     from distributed_learning_amd.ops import nn as dnn
     from distributed_learning_amd.ops.loss import cross_entropy
@@ -33,7 +33,7 @@ def _train(model_fn, wrap, steps, bf16):
         dnn.bf16_weights(m)
     w = wrap(m)
     opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, master_weights=bf16)
-    data = SyntheticBatches(8, (3, 32, 32), 10, dev, dtype=torch.bfloat16 if bf16 else torch.float32,
+    data = SyntheticBatches(8, shape, 10, dev, dtype=torch.bfloat16 if bf16 else torch.float32,
                             channels_last=True)
     losses = []
     for _ in range(steps):
@@ -48,18 +48,24 @@ def _train(model_fn, wrap, steps, bf16):
     return m, losses
 
 
-@pytest.mark.parametrize("bf16,staged", [(False, False), (True, False), (True, True)])
-@pytest.mark.parametrize("grouping", [25 * 1024 * 1024, 64 * 1024, 0])
-def test_native_engine_steal_path_matches_single_device(world1, bf16, staged, grouping):
+@pytest.mark.parametrize("arch,bf16,staged,grouping", [
+    (a, b, s, g) for a in ("resnet18",) for b, s in [(False, False), (True, False), (True, True)]
+    for g in (25 * 1024 * 1024, 64 * 1024, 0)] + [
+    # GoogLeNet: fused Inception blocks, native stem, ceil-mode fused pools, and aux heads whose
+    # parameters get no gradient (zero-filled by GradSync.flush before their bucket is reduced)
+    ("googlenet", True, False, 1024 * 1024), ("googlenet", True, True, 1024 * 1024)])
+def test_native_engine_steal_path_matches_single_device(world1, arch, bf16, staged, grouping):
     """Gather of autograd-owned grads into bucket buffers on the comm stream, the (world-1) RCCL
     all-reduce and the re-pointing of .grad at the averaged slots must give exactly the single-device
     update (the same kernels run; only the gradient storage differs)."""
-    from distributed_learning_amd.models import resnet18
+    from distributed_learning_amd.models import googlenet, resnet18
     from distributed_learning_amd.ops import nn as dnn
     from distributed_learning_amd.parallel import PipelinedFusedDP, SingleDevice, make_reducer
     from distributed_learning_amd.parallel.executor import NativeStreamExecutor
 
     dnn.set_backend("native")
+    native_conv = arch == "googlenet"
+    dnn.set_native_conv(native_conv)
     # MIOpen picks non-deterministic conv algorithms by default (run-to-run differences of ~1e-3
     # that chaotic SGD amplifies); the comparison needs identical kernels on both sides.
     det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
@@ -78,10 +84,13 @@ def test_native_engine_steal_path_matches_single_device(world1, bf16, staged, gr
             assert w.sync.grad_mode == "steal"
             return w
 
-        m1, l1 = _train(lambda: resnet18(10), wrap_dp, 4, bf16)
-        m2, l2 = _train(lambda: resnet18(10), SingleDevice, 4, bf16)
+        build = (lambda: googlenet(10)) if arch == "googlenet" else (lambda: resnet18(10))
+        shape = (3, 64, 64) if arch == "googlenet" else (3, 32, 32)
+        m1, l1 = _train(build, wrap_dp, 4, bf16, shape)
+        m2, l2 = _train(build, SingleDevice, 4, bf16, shape)
     finally:
         dnn.set_backend("torch")
+        dnn.set_native_conv(False)
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
     assert l1 == pytest.approx(l2, rel=1e-5, abs=1e-5)
     for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
