@@ -67,9 +67,9 @@ class InceptionAux(nn.Module):
         x = F.adaptive_avg_pool2d(x, (4, 4))
         x = self.conv(x)
         x = torch.flatten(x, 1)
-        x = F.relu(self.fc1(x), inplace=True)
+        x = F.relu(dnn.linear(x, self.fc1), inplace=True)
         x = F.dropout(x, 0.7, training=self.training)
-        return self.fc2(x)
+        return dnn.linear(x, self.fc2)
 
 
 class GoogLeNet(nn.Module):
@@ -121,7 +121,7 @@ class GoogLeNet(nn.Module):
         x = self.inception5b(x)
         x = global_avg_pool(x) if isinstance(self.avgpool, nn.AdaptiveAvgPool2d) else torch.flatten(self.avgpool(x), 1)
         x = self.dropout(x)
-        x = self.fc(x)
+        x = dnn.linear(x, self.fc)
         # Reference semantics: only output[0] (main logits) enters the loss (network.py:41). The aux
         # outputs are kept detached: holding their autograd graph would keep the previous step's
         # AccumulateGrad nodes alive across iterations (and across a HIP-graph capture boundary).

@@ -149,7 +149,7 @@ class ResNet(nn.Module):
         x = self.layer3(x)
         x = self.layer4(x)
         x = global_avg_pool(x) if isinstance(self.avgpool, nn.AdaptiveAvgPool2d) else torch.flatten(self.avgpool(x), 1)
-        return self.fc(x)
+        return dnn.linear(x, self.fc)
 
 
 def resnet18(num_classes: int = 1000, **kw) -> ResNet:

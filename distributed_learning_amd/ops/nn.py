@@ -85,6 +85,15 @@ def native_conv() -> bool:
     return _NATIVE_CONV
 
 
+def linear(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
+    """``fc(x)``; with the native backend and native convs, on the MFMA GEMMs (ops/linear.py)."""
+    if _BACKEND == "native" and _NATIVE_CONV and x.is_cuda:
+        from .linear import linear as native_linear
+
+        return native_linear(x, fc)
+    return fc(x)
+
+
 def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool = True,
                 residual: torch.Tensor | None = None, presubsampled: bool = False):
     """``act(BN(conv(x)) [+ residual])``. With the native backend and native convs, a 1x1 conv runs as
