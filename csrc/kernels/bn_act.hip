@@ -924,6 +924,7 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
 // Backward: the BN reduce/apply passes gather dy from the pooled gradient (PoolDy) instead of a
 // materialised full-resolution gradient.
 // ---------------------------------------------------------------------------------------------
+template <int K>  // K > 0: compile-time window, all taps loaded before the first comparison
 __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(const bf16_t* __restrict__ x,
                                                                   const float* __restrict__ ws, bf16_t* __restrict__ y,
                                                                   uint8_t* __restrict__ pos, int N, int H, int W, int C,
@@ -947,22 +948,41 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(const bf16_t* 
       bi[j] = 0;
     }
     const int h0 = oh * s - p, w0 = ow * s - p;
-    for (int ky = 0; ky < k; ++ky) {
-      const int h = h0 + ky;
-      if (h < 0 || h >= H) continue;
-      for (int kx = 0; kx < k; ++kx) {
-        const int w = w0 + kx;
-        if (w < 0 || w >= W) continue;
-        float v[8];
-        Vec8<bf16_t>::load(x + (((int64_t)n * H + h) * W + w) * C + c, v);
-        const uint32_t q = (uint32_t)(ky * k + kx);
+    auto take = [&](const float (&v)[8], uint32_t q) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float a = bf16_to_f32(f32_to_bf16(fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f)));
-          if (a > best[j] || (a != a && best[j] == best[j])) {
-            best[j] = a;
-            bi[j] = q;
-          }
+      for (int j = 0; j < 8; ++j) {
+        const float a = bf16_to_f32(f32_to_bf16(fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f)));
+        if (a > best[j] || (a != a && best[j] == best[j])) {
+          best[j] = a;
+          bi[j] = q;
+        }
+      }
+    };
+    if constexpr (K > 0) {
+      float v[K * K][8];
+      bool ok[K * K];
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          const int h = h0 + ky, w = w0 + kx, q = ky * K + kx;
+          ok[q] = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+          const int hc = min(max(h, 0), H - 1), wc = min(max(w, 0), W - 1);
+          Vec8<bf16_t>::load(x + (((int64_t)n * H + hc) * W + wc) * C + c, v[q]);
+        }
+#pragma unroll
+      for (int q = 0; q < K * K; ++q)
+        if (ok[q]) take(v[q], (uint32_t)q);
+    } else {
+      for (int ky = 0; ky < k; ++ky) {
+        const int h = h0 + ky;
+        if (h < 0 || h >= H) continue;
+        for (int kx = 0; kx < k; ++kx) {
+          const int w = w0 + kx;
+          if (w < 0 || w >= W) continue;
+          float v[8];
+          Vec8<bf16_t>::load(x + (((int64_t)n * H + h) * W + w) * C + c, v);
+          take(v, (uint32_t)(ky * k + kx));
         }
       }
     }
@@ -980,8 +1000,12 @@ void launch_bn_relu_maxpool_fwd(const void* x, const float* ws, void* y, uint8_t
   const int64_t work = (int64_t)N * OH * OW * (C / 8);
   const int nb = (int)std::min<int64_t>((work + 255) / 256, 256 * 32);
   if (nb == 0) return;
-  hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel, dim3(nb), dim3(256), 0, stream, (const bf16_t*)x, ws, (bf16_t*)y, pos,
-                     N, H, W, C, OH, OW, k, s, p);
+  if (k == 3)
+    hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<3>, dim3(nb), dim3(256), 0, stream, (const bf16_t*)x, ws, (bf16_t*)y,
+                       pos, N, H, W, C, OH, OW, k, s, p);
+  else
+    hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<0>, dim3(nb), dim3(256), 0, stream, (const bf16_t*)x, ws, (bf16_t*)y,
+                       pos, N, H, W, C, OH, OW, k, s, p);
 }
 
 void launch_bn_relu_maxpool_bwd(const void* dy_pool, const uint8_t* pos, const void* x, void* dx, int N, int H, int W,
