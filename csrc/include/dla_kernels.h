@@ -95,7 +95,8 @@ void launch_xent_bwd(const void* logits, const int64_t* target, const float* ws,
 // ws: 7*C floats (mean, invstd, scale, shift | k1, m1, k2); part: bn_partial_floats(M, C) floats.
 void bn_geometry(int64_t M, int C, int* tpr, int* nrb, int* nct, int target_blocks);  // <= 0: reduction passes
 // fp32 scratch floats of one reduction pass's partials [rows][C][2] plus their fold rows
-int64_t bn_partial_floats(int64_t M, int C);
+int64_t bn_partial_floats(int64_t M, int C, int target_blocks = 0);
+int64_t bn_relu_maxpool_part_floats(int64_t M, int C);  // partials of launch_bn_relu_maxpool_bwd
 // reduction-pass block target (0 = DLA_BN_RED_BLOCKS or the default 1024); tests exercise the
 // > 1024-row fold path with it
 void set_bn_red_blocks(int blocks);

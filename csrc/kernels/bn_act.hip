@@ -233,11 +233,15 @@ static const float* bn_fold_rows(const float* part, int* nrb, int C, hipStream_t
   return out;
 }
 
-int64_t bn_partial_floats(int64_t M, int C) {
+int64_t bn_partial_floats(int64_t M, int C, int target_blocks) {
   int tpr, nrb, nct;
-  bn_geometry(M, C, &tpr, &nrb, &nct, 0);
+  bn_geometry(M, C, &tpr, &nrb, &nct, target_blocks);
   return ((int64_t)nrb + bn_fold_groups(nrb)) * C * 2;
 }
+
+// the quad stem backward reduce runs on M / 4 quads with a 4096-block target (its per-thread work
+// is 4 pixels; the default 1024 blocks leave it latency-bound)
+constexpr int kQuadRedBlocks = 4096;
 
 template <int WPC>
 __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __restrict__ x0, int x_is_bf16,
@@ -1008,10 +1012,160 @@ void launch_bn_relu_maxpool_fwd(const void* x, const float* ws, void* y, uint8_t
                        pos, N, H, W, C, OH, OW, k, s, p);
 }
 
+// ResNet stem geometry (3x3 / stride 2 / pad 1 max-pool over an even H x W): the 2x2 input quad
+// (2j..2j+1, 2i..2i+1) is covered exactly by the windows (j..j+1, i..i+1), so a thread owning a quad
+// loads those 4 windows' (position byte, dy) pairs once for its 4 pixels — the per-pixel gather
+// (PoolDy) issues 4 candidate window loads for every pixel. Window taps of the quad pixels, as
+// (pixel, window) -> tap ky*3+kx with window (oh, ow) covering input rows 2oh-1 .. 2oh+1:
+//   (0,0):(j,i)=4 | (0,1):(j,i)=5,(j,i+1)=3 | (1,0):(j,i)=7,(j+1,i)=1 | (1,1):(j,i)=8,(j,i+1)=6,(j+1,i)=2,(j+1,i+1)=0
+struct StemQuad {
+  const bf16_t* dyp;
+  const uint8_t* pos;
+  int H, W, OH, OW;
+  mm::FastDiv fQW, fQH;  // quads per row (W/2), quad rows (H/2)
+  // dy' of the 4 pixels of quad t (channels c0..c0+7) and their element offsets
+  __device__ __forceinline__ void gather(int64_t t, int c0, int C, float (&g)[4][8], int64_t (&off)[4]) const {
+    const uint32_t q = mm::fdiv((uint32_t)t, fQW);
+    const int i = (int)t - (int)q * (W >> 1);
+    const uint32_t n = mm::fdiv(q, fQH);
+    const int j = (int)q - (int)n * (H >> 1);
+    uint64_t pk[4];
+    float d[4][8];
+    bool ok[4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int oh = j + a, ow = i + b, w = a * 2 + b;
+        ok[w] = oh < OH && ow < OW;
+        const int64_t o = (((int64_t)n * OH + min(oh, OH - 1)) * OW + min(ow, OW - 1)) * C + c0;
+        pk[w] = *reinterpret_cast<const uint64_t*>(pos + o);
+        Vec8<bf16_t>::load(dyp + o, d[w]);
+      }
+    // (pixel, window, tap) triples of the quad
+    constexpr int kPix[9] = {0, 1, 1, 2, 2, 3, 3, 3, 3};
+    constexpr int kWin[9] = {0, 0, 1, 0, 2, 0, 1, 2, 3};
+    constexpr uint32_t kTap[9] = {4, 5, 3, 7, 1, 8, 6, 2, 0};
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[p][e] = 0.f;
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      const int w = kWin[u];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (ok[w] && ((pk[w] >> (8 * e)) & 0xffu) == kTap[u]) g[kPix[u]][e] += d[w][e];
+    }
+    const int64_t base = ((int64_t)n * H + 2 * j) * W + 2 * i;
+    off[0] = base * C + c0;
+    off[1] = (base + 1) * C + c0;
+    off[2] = (base + W) * C + c0;
+    off[3] = (base + W + 1) * C + c0;
+  }
+};
+
+__global__ __launch_bounds__(kBNThreads) void bn_pool_quad_reduce_kernel(StemQuad sq, const bf16_t* __restrict__ x,
+                                                                         const float* __restrict__ ws, int64_t Q,
+                                                                         int C, int nrb, int tpr,
+                                                                         float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int rpi = kBNThreads / tpr, ct = tpr * 8;
+  const int c_base = blockIdx.x * ct;
+  const int c0 = c_base + (threadIdx.x % tpr) * 8;
+  const int rg = threadIdx.x / tpr;
+  int64_t r0, r1;
+  block_rows(Q, nrb, r0, r1);
+  float mean[8], sc[8], sh[8], s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mean[e] = ws[c0 + e];
+    sc[e] = ws[2 * C + c0 + e];
+    sh[e] = ws[3 * C + c0 + e];
+    s[e] = q[e] = 0.f;
+  }
+  for (int64_t t = r0 + rg; t < r1; t += rpi) {
+    float g[4][8], xv[4][8];
+    int64_t off[4];
+    sq.gather(t, c0, C, g, off);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) Vec8<bf16_t>::load(x + off[p], xv[p]);
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gg = fmaf(xv[p][e], sc[e], sh[e]) > 0.f ? g[p][e] : 0.f;  // the forward's ReLU
+        s[e] += gg;
+        q[e] = fmaf(gg, xv[p][e] - mean[e], q[e]);
+      }
+  }
+  block_reduce_write(s, q, tpr, rpi, ct, C, part, c_base, red);
+}
+
+__global__ __launch_bounds__(kBNThreads) void bn_pool_quad_apply_kernel(StemQuad sq, const bf16_t* __restrict__ x,
+                                                                        const float* __restrict__ ws,
+                                                                        bf16_t* __restrict__ dx, int64_t Q, int C,
+                                                                        int nrb, int tpr) {
+  const int rpi = kBNThreads / tpr, ct = tpr * 8;
+  const int c0 = blockIdx.x * ct + (threadIdx.x % tpr) * 8;
+  const int rg = threadIdx.x / tpr;
+  int64_t r0, r1;
+  block_rows(Q, nrb, r0, r1);
+  float mean[8], sc[8], sh[8], k1[8], m1[8], k2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mean[e] = ws[c0 + e];
+    sc[e] = ws[2 * C + c0 + e];
+    sh[e] = ws[3 * C + c0 + e];
+    k1[e] = ws[4 * C + c0 + e];
+    m1[e] = ws[5 * C + c0 + e];
+    k2[e] = ws[6 * C + c0 + e];
+  }
+  for (int64_t t = r0 + rg; t < r1; t += rpi) {
+    float g[4][8], xv[4][8];
+    int64_t off[4];
+    sq.gather(t, c0, C, g, off);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) Vec8<bf16_t>::load(x + off[p], xv[p]);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gg = fmaf(xv[p][e], sc[e], sh[e]) > 0.f ? g[p][e] : 0.f;
+        xv[p][e] = k1[e] * (gg - m1[e] - (xv[p][e] - mean[e]) * k2[e]);
+      }
+      Vec8<bf16_t>::store(dx + off[p], xv[p]);
+    }
+  }
+}
+
+int64_t bn_relu_maxpool_part_floats(int64_t M, int C) {
+  return std::max(bn_partial_floats(M, C), bn_partial_floats(M / 4, C, kQuadRedBlocks));
+}
+
 void launch_bn_relu_maxpool_bwd(const void* dy_pool, const uint8_t* pos, const void* x, void* dx, int N, int H, int W,
                                 int C, int OH, int OW, int k, int s, int p, const float* gamma, float* ws, float* part,
                                 float* dgamma, float* dbeta, hipStream_t stream) {
   const int64_t M = (int64_t)N * H * W;
+  if (k == 3 && s == 2 && p == 1 && H % 2 == 0 && W % 2 == 0 && OH == H / 2 && OW == W / 2) {
+    // quad form (ResNet stem): same partials layout / finalize as the per-pixel passes
+    const int64_t Q = M / 4;
+    StemQuad sq{(const bf16_t*)dy_pool, pos, H, W, OH, OW, mm::make_fastdiv((uint32_t)(W / 2)),
+                mm::make_fastdiv((uint32_t)(H / 2))};
+    int tpr, nrb, nct;
+    bn_geometry(Q, C, &tpr, &nrb, &nct, kQuadRedBlocks);  // part sized by bn_relu_maxpool_part_floats
+    const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
+    hipLaunchKernelGGL(bn_pool_quad_reduce_kernel, dim3(nct, nrb), dim3(kBNThreads), lds, stream, sq, (const bf16_t*)x,
+                       (const float*)ws, Q, C, nrb, tpr, part);
+    const float* fp = bn_fold_rows(part, &nrb, C, stream);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, fp, nrb, M, C, gamma, ws,
+                       dgamma, dbeta);
+    int atpr, anrb, anct;
+    bn_geometry(Q, C, &atpr, &anrb, &anct, 4096);
+    hipLaunchKernelGGL(bn_pool_quad_apply_kernel, dim3(anct, anrb), dim3(kBNThreads), 0, stream, sq, (const bf16_t*)x,
+                       (const float*)ws, (bf16_t*)dx, Q, C, anrb, atpr);
+    return;
+  }
   PoolDy pd{(const bf16_t*)dy_pool, pos, H, W, OH, OW, k, s, p, mm::make_fastdiv((uint32_t)W),
             mm::make_fastdiv((uint32_t)H)};
   int tpr, nrb, nct;

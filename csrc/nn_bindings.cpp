@@ -398,7 +398,7 @@ std::vector<at::Tensor> bn_relu_maxpool_bwd(at::Tensor dy_pool, at::Tensor pos, 
   const int OH = (int)dy_pool.size(2), OW = (int)dy_pool.size(3);
   const int64_t M = (int64_t)N * H * W;
   auto f32 = x.options().dtype(at::kFloat);
-  at::Tensor part = at::empty({partial_floats(M, C)}, f32);
+  at::Tensor part = at::empty({bn_relu_maxpool_part_floats(M, C)}, f32);
   at::Tensor dx = at::empty_like(x);
   at::Tensor dg = at::empty({C}, f32), db = at::empty({C}, f32);
   const float* g = (weight.has_value() && weight->defined()) ? weight->data_ptr<float>() : nullptr;
