@@ -1012,12 +1012,13 @@ void launch_bn_relu_maxpool_fwd(const void* x, const float* ws, void* y, uint8_t
                        pos, N, H, W, C, OH, OW, k, s, p);
 }
 
-// ResNet stem geometry (3x3 / stride 2 / pad 1 max-pool over an even H x W): the 2x2 input quad
-// (2j..2j+1, 2i..2i+1) is covered exactly by the windows (j..j+1, i..i+1), so a thread owning a quad
-// loads those 4 windows' (position byte, dy) pairs once for its 4 pixels — the per-pixel gather
-// (PoolDy) issues 4 candidate window loads for every pixel. Window taps of the quad pixels, as
-// (pixel, window) -> tap ky*3+kx with window (oh, ow) covering input rows 2oh-1 .. 2oh+1:
-//   (0,0):(j,i)=4 | (0,1):(j,i)=5,(j,i+1)=3 | (1,0):(j,i)=7,(j+1,i)=1 | (1,1):(j,i)=8,(j,i+1)=6,(j+1,i)=2,(j+1,i+1)=0
+// 3x3 / stride-2 max-pool over an even H x W (ResNet stem: pad 1; GoogLeNet stem / maxpool2: pad 0,
+// ceil mode): the 2x2 input quad (2j..2j+1, 2i..2i+1) is covered exactly by the windows
+// (j-1+P .. j+P, i-1+P .. i+P), so a thread owning a quad loads those 4 windows' (position byte, dy)
+// pairs once for its 4 pixels — the per-pixel gather (PoolDy) issues 4 candidate window loads for
+// every pixel. Window (oh, ow) covers input rows 2oh-P .. 2oh-P+2; the tap of pixel (h, w) in it is
+// (h - 2oh + P) * 3 + (w - 2ow + P), and a (pixel, window) pair is real when both offsets are 0..2.
+template <int P>
 struct StemQuad {
   const bf16_t* dyp;
   const uint8_t* pos;
@@ -1036,27 +1037,34 @@ struct StemQuad {
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        const int oh = j + a, ow = i + b, w = a * 2 + b;
-        ok[w] = oh < OH && ow < OW;
-        const int64_t o = (((int64_t)n * OH + min(oh, OH - 1)) * OW + min(ow, OW - 1)) * C + c0;
+        const int oh = j - 1 + P + a, ow = i - 1 + P + b, w = a * 2 + b;
+        ok[w] = (unsigned)oh < (unsigned)OH && (unsigned)ow < (unsigned)OW;
+        const int64_t o = (((int64_t)n * OH + min(max(oh, 0), OH - 1)) * OW + min(max(ow, 0), OW - 1)) * C + c0;
         pk[w] = *reinterpret_cast<const uint64_t*>(pos + o);
         Vec8<bf16_t>::load(dyp + o, d[w]);
       }
-    // (pixel, window, tap) triples of the quad
-    constexpr int kPix[9] = {0, 1, 1, 2, 2, 3, 3, 3, 3};
-    constexpr int kWin[9] = {0, 0, 1, 0, 2, 0, 1, 2, 3};
-    constexpr uint32_t kTap[9] = {4, 5, 3, 7, 1, 8, 6, 2, 0};
 #pragma unroll
     for (int p = 0; p < 4; ++p)
 #pragma unroll
       for (int e = 0; e < 8; ++e) g[p][e] = 0.f;
+    // pixel (dh, dw) of the quad in window (a, b): ky = dh - 2a + 2 - P, kx = dw - 2b + 2 - P
 #pragma unroll
-    for (int u = 0; u < 9; ++u) {
-      const int w = kWin[u];
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (ok[w] && ((pk[w] >> (8 * e)) & 0xffu) == kTap[u]) g[kPix[u]][e] += d[w][e];
-    }
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+          for (int dw = 0; dw < 2; ++dw) {
+            constexpr int lo = 0;
+            const int ky = dh - 2 * a + 2 - P, kx = dw - 2 * b + 2 - P;
+            if (ky < lo || ky > 2 || kx < lo || kx > 2) continue;  // compile-time after unrolling
+            const int w = a * 2 + b;
+            const uint32_t tap = (uint32_t)(ky * 3 + kx);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (ok[w] && ((pk[w] >> (8 * e)) & 0xffu) == tap) g[dh * 2 + dw][e] += d[w][e];
+          }
     const int64_t base = ((int64_t)n * H + 2 * j) * W + 2 * i;
     off[0] = base * C + c0;
     off[1] = (base + 1) * C + c0;
@@ -1065,7 +1073,8 @@ struct StemQuad {
   }
 };
 
-__global__ __launch_bounds__(kBNThreads) void bn_pool_quad_reduce_kernel(StemQuad sq, const bf16_t* __restrict__ x,
+template <int P>
+__global__ __launch_bounds__(kBNThreads) void bn_pool_quad_reduce_kernel(StemQuad<P> sq, const bf16_t* __restrict__ x,
                                                                          const float* __restrict__ ws, int64_t Q,
                                                                          int C, int nrb, int tpr,
                                                                          float* __restrict__ part) {
@@ -1102,7 +1111,8 @@ __global__ __launch_bounds__(kBNThreads) void bn_pool_quad_reduce_kernel(StemQua
   block_reduce_write(s, q, tpr, rpi, ct, C, part, c_base, red);
 }
 
-__global__ __launch_bounds__(kBNThreads) void bn_pool_quad_apply_kernel(StemQuad sq, const bf16_t* __restrict__ x,
+template <int P>
+__global__ __launch_bounds__(kBNThreads) void bn_pool_quad_apply_kernel(StemQuad<P> sq, const bf16_t* __restrict__ x,
                                                                         const float* __restrict__ ws,
                                                                         bf16_t* __restrict__ dx, int64_t Q, int C,
                                                                         int nrb, int tpr) {
@@ -1147,23 +1157,29 @@ void launch_bn_relu_maxpool_bwd(const void* dy_pool, const uint8_t* pos, const v
                                 int C, int OH, int OW, int k, int s, int p, const float* gamma, float* ws, float* part,
                                 float* dgamma, float* dbeta, hipStream_t stream) {
   const int64_t M = (int64_t)N * H * W;
-  if (k == 3 && s == 2 && p == 1 && H % 2 == 0 && W % 2 == 0 && OH == H / 2 && OW == W / 2) {
-    // quad form (ResNet stem): same partials layout / finalize as the per-pixel passes
+  // quad form: 3x3 / stride 2 over an even input whose windows all start inside it (pad 1 floor:
+  // OH = H/2; pad 0 ceil: OH = H/2 as well). Same partials layout / finalize as the per-pixel passes.
+  if (k == 3 && s == 2 && (p == 0 || p == 1) && H % 2 == 0 && W % 2 == 0 && OH == H / 2 && OW == W / 2) {
     const int64_t Q = M / 4;
-    StemQuad sq{(const bf16_t*)dy_pool, pos, H, W, OH, OW, mm::make_fastdiv((uint32_t)(W / 2)),
-                mm::make_fastdiv((uint32_t)(H / 2))};
+    const mm::FastDiv fqw = mm::make_fastdiv((uint32_t)(W / 2)), fqh = mm::make_fastdiv((uint32_t)(H / 2));
     int tpr, nrb, nct;
     bn_geometry(Q, C, &tpr, &nrb, &nct, kQuadRedBlocks);  // part sized by bn_relu_maxpool_part_floats
     const size_t lds = (size_t)(kBNThreads / tpr) * tpr * 8 * 2 * sizeof(float);
-    hipLaunchKernelGGL(bn_pool_quad_reduce_kernel, dim3(nct, nrb), dim3(kBNThreads), lds, stream, sq, (const bf16_t*)x,
-                       (const float*)ws, Q, C, nrb, tpr, part);
-    const float* fp = bn_fold_rows(part, &nrb, C, stream);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, fp, nrb, M, C, gamma, ws,
-                       dgamma, dbeta);
     int atpr, anrb, anct;
     bn_geometry(Q, C, &atpr, &anrb, &anct, 4096);
-    hipLaunchKernelGGL(bn_pool_quad_apply_kernel, dim3(anct, anrb), dim3(kBNThreads), 0, stream, sq, (const bf16_t*)x,
-                       (const float*)ws, (bf16_t*)dx, Q, C, anrb, atpr);
+#define DLA_QUAD(P_)                                                                                                  \
+  {                                                                                                                   \
+    StemQuad<P_> sq{(const bf16_t*)dy_pool, pos, H, W, OH, OW, fqw, fqh};                                             \
+    hipLaunchKernelGGL(bn_pool_quad_reduce_kernel<P_>, dim3(nct, nrb), dim3(kBNThreads), lds, stream, sq,            \
+                       (const bf16_t*)x, (const float*)ws, Q, C, nrb, tpr, part);                                     \
+    const float* fp = bn_fold_rows(part, &nrb, C, stream);                                                            \
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, fp, nrb, M, C, gamma, ws, \
+                       dgamma, dbeta);                                                                                \
+    hipLaunchKernelGGL(bn_pool_quad_apply_kernel<P_>, dim3(anct, anrb), dim3(kBNThreads), 0, stream, sq,             \
+                       (const bf16_t*)x, (const float*)ws, (bf16_t*)dx, Q, C, anrb, atpr);                            \
+  }
+    if (p == 1) DLA_QUAD(1) else DLA_QUAD(0)
+#undef DLA_QUAD
     return;
   }
   PoolDy pd{(const bf16_t*)dy_pool, pos, H, W, OH, OW, k, s, p, mm::make_fastdiv((uint32_t)W),
