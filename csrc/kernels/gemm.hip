@@ -123,6 +123,54 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// Small outputs with many splits (a 64x64 weight gradient has 1024 float4 outputs and up to 512
+// slabs): one thread per output would leave a handful of blocks each walking hundreds of slabs
+// one latency at a time (19-36 us per call in profiles/resnet50_bs512_r3f_ksum.md). Here SG thread
+// groups of a block split the slab range (group g sums slabs g, g+SG, ...), then group 0 adds the
+// SG partial sums from LDS in group order, so the result is still fixed-order and run-to-run
+// deterministic.
+template <typename T, int SG>
+__global__ __launch_bounds__(256) void splitk_reduce_sg_kernel(const float* __restrict__ P, int splits, int64_t n,
+                                                               T* __restrict__ out, float scale, int accumulate) {
+  constexpr int kOpb = 256 / SG;  // float4 outputs per block
+  __shared__ float4_t red[SG][kOpb];
+  const int g = threadIdx.x / kOpb, o = threadIdx.x % kOpb;
+  const int64_t nv = n / 4;
+  const int64_t v = (int64_t)blockIdx.x * kOpb + o;
+  float4_t a0{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+  if (v < nv) {
+    int k = g;
+    for (; k + SG < splits; k += 2 * SG) {
+      a0 += reinterpret_cast<const float4_t*>(P + (int64_t)k * n)[v];
+      a1 += reinterpret_cast<const float4_t*>(P + (int64_t)(k + SG) * n)[v];
+    }
+    if (k < splits) a0 += reinterpret_cast<const float4_t*>(P + (int64_t)k * n)[v];
+  }
+  red[g][o] = a0 + a1;
+  __syncthreads();
+  if (g == 0 && v < nv) {
+    float4_t s = red[0][o];
+#pragma unroll
+    for (int j = 1; j < SG; ++j) s += red[j][o];
+    s *= scale;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float r = s[j];
+      if (accumulate) r += Cvt<T>::to_f32(out[v * 4 + j]);
+      out[v * 4 + j] = Cvt<T>::from_f32(r);
+    }
+  }
+  if (blockIdx.x == 0) {  // tail (n % 4)
+    for (int64_t i = nv * 4 + threadIdx.x; i < n; i += blockDim.x) {
+      float r = 0.f;
+      for (int k = 0; k < splits; ++k) r += P[(int64_t)k * n + i];
+      r *= scale;
+      if (accumulate) r += Cvt<T>::to_f32(out[i]);
+      out[i] = Cvt<T>::from_f32(r);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------------
@@ -299,7 +347,38 @@ void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, floa
 
 void launch_splitk_reduce(const float* partial, int splits, int64_t n, void* out, int out_dtype, float scale,
                           bool accumulate, hipStream_t stream) {
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n / 4 + 255) / 256, 2048));
+  const int64_t nv = n / 4;
+  // slab groups per block: the fewest that give >= 512 blocks, at most 64 and at most splits / 2
+  // (DLA_SPLITK_SG=0: one thread per output, for A/B runs)
+  static const bool sg_on = [] {
+    const char* e = std::getenv("DLA_SPLITK_SG");
+    return !(e && e[0] == '0');
+  }();
+  int sg = 1;
+  while (sg_on && sg < 64 && 2 * sg <= splits / 2 && (nv * sg + 255) / 256 < 512) sg *= 2;
+  if (sg > 1) {
+    const int grid = (int)std::max<int64_t>(1, (nv * sg + 255) / 256);
+#define DLA_SKR(SG_)                                                                                              \
+  case SG_:                                                                                                       \
+    if (out_dtype == kF32)                                                                                        \
+      hipLaunchKernelGGL((splitk_reduce_sg_kernel<float, SG_>), dim3(grid), dim3(256), 0, stream, partial, splits, \
+                         n, (float*)out, scale, (int)accumulate);                                                 \
+    else                                                                                                          \
+      hipLaunchKernelGGL((splitk_reduce_sg_kernel<bf16_t, SG_>), dim3(grid), dim3(256), 0, stream, partial,       \
+                         splits, n, (bf16_t*)out, scale, (int)accumulate);                                        \
+    break;
+    switch (sg) {
+      DLA_SKR(2)
+      DLA_SKR(4)
+      DLA_SKR(8)
+      DLA_SKR(16)
+      DLA_SKR(32)
+      DLA_SKR(64)
+    }
+#undef DLA_SKR
+    return;
+  }
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nv + 255) / 256, 2048));
   if (out_dtype == kF32)
     hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(grid), dim3(256), 0, stream, partial, splits, n, (float*)out,
                        scale, (int)accumulate);

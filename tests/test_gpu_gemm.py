@@ -41,7 +41,7 @@ def test_gemm_nt_asymmetric_identity(cuda):
 
 
 @pytest.mark.parametrize("K,Mo,No", [(802816, 64, 256), (1000, 64, 64), (12544, 512, 2048), (333, 136, 72),
-                                     (50176, 256, 1024)])
+                                     (50176, 256, 1024), (131072, 8, 8), (65536, 24, 40), (200704, 64, 64)])
 def test_gemm_tn(cuda, K, Mo, No):
     C = _C()
     torch.manual_seed(0)
