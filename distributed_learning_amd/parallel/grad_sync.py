@@ -20,7 +20,8 @@ Fixes and MI355X design:
 4. Unused parameters get zero gradients (not ``empty_like``) — by graph walk when
    ``find_unused_parameters`` (reference semantics), and in any case by ``flush()`` at sync time,
    which zero-fills and launches whatever never became ready, so a missed parameter can never hang
-   the job.
+   the job. With one rank and a pass-through executor nothing is reduced, so they keep
+   ``grad = None`` (plain-PyTorch semantics; optimizers skip them) and no fill kernels run.
 5. No CPU blocking on GPU: ``synchronize()`` = compute stream waits on the comm stream.
 6. Local gradient accumulation: backward passes run under :meth:`GradSync.no_sync` leave their
    gradients in place (the next ``prepare()`` does not reset them) and the next synchronised
@@ -220,7 +221,7 @@ class GradSync:
         if not self._enabled:
             return
         for p in params:
-            if p.grad is None:
+            if p.grad is None and not self.passthrough:  # one rank: left None (see flush)
                 p.grad = torch.zeros_like(p)
             self._ready(p)
 
@@ -241,7 +242,7 @@ class GradSync:
 
     def _ready(self, p: torch.Tensor) -> None:
         b, j = self._owner[id(p)]
-        if self.grad_mode == "steal":
+        if self.grad_mode == "steal" and p.grad is not None:
             g = p.grad
             if g.dtype != b.flat.dtype or not same_layout(g, p):
                 g = g.to(b.flat.dtype) if same_layout(g, p) else torch.empty_like(p, dtype=b.flat.dtype).copy_(g)
@@ -260,19 +261,23 @@ class GradSync:
             self.executor.submit(b)
 
     def flush(self) -> None:
-        """Launch every bucket that has not been launched (zero-filling missing grads)."""
+        """Launch every bucket that has not been launched (zero-filling missing grads).
+
+        One rank with a pass-through executor reduces nothing, so parameters that got no gradient
+        (GoogLeNet's unused aux heads) keep ``grad = None`` as in plain PyTorch, and optimizers skip
+        them, instead of paying a zero-fill launch per tensor every step."""
         for b in self.buckets[self._next:]:
             if b.ready < len(b.params):
                 if self.grad_mode == "steal":
                     recorded = {off for _, off in b.stolen}
                     for p, off in zip(b.params, b.offsets):
                         if off not in recorded:
-                            if p.grad is None:
+                            if p.grad is None and not self.passthrough:
                                 p.grad = torch.zeros_like(p)
                             self._ready(p)  # records the gradient (no launch: bucket incomplete until the end)
                 else:
                     for p in b.params:
-                        if p.grad is None:
+                        if p.grad is None and not self.passthrough:
                             p.grad = torch.zeros_like(p)
                 b.ready = len(b.params)
         self._launch_in_order()
