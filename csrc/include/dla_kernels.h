@@ -201,9 +201,17 @@ bool splitk_xcd_remap();
 int splitk_target_blocks();  // split-K grids: tiles of one split co-scheduled on one XCD (DLA_SPLITK_XCD=0: off)
 void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, float* partial, int splits, int Mo, int No,
                     int K, void* out, int out_dtype, float scale, bool accumulate, hipStream_t stream);
-// out[n] (= scale * sum_s partial[s][n] [+ out]), fp32 or bf16 out.
+// out[n] (= scale * sum_s partial[s][n] [+ addend] [+ out]), fp32 or bf16 out; addend: bf16 rows of
+// ncol with row stride ld_addend (0 = one broadcast row).
 void launch_splitk_reduce(const float* partial, int splits, int64_t n, void* out, int out_dtype, float scale,
-                          bool accumulate, hipStream_t stream);
+                          bool accumulate, hipStream_t stream, const void* addend = nullptr, int64_t ld_addend = 0,
+                          int ncol = 1);
+// Split-K C[M,N] = A B^T (+ addend) for few output tiles and a long K (fully connected heads):
+// splits > 1 when it applies; partial holds splits * M * N floats.
+int gemm_nt_splitk_splits(int M, int N, int K);
+void launch_gemm_nt_splitk(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, float* partial,
+                           int splits, void* C, int M, int N, int K, const void* addend, int64_t ld_addend,
+                           hipStream_t stream);
 
 // ---- implicit-GEMM 3x3 convolutions, pad 1, NHWC bf16 (conv.hip) -----------------------------
 // x [N,H,W,Cin], w [Cout,3,3,Cin], y [N,OH,OW,Cout]; Cin % 64 == 0, Cout % 64 == 0, pixels < 2^24.

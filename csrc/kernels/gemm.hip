@@ -19,6 +19,7 @@
 //     ds_read_b64_tr_b16 transposing LDS read (T10) and splits the long M reduction over blocks
 //     with fp32 partial slabs + a separate reduction kernel.
 #include <cstdlib>
+#include <type_traits>
 
 #include "dla_common.h"
 #include "dla_kernels.h"
@@ -87,6 +88,38 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(const bf16_t* __re
   epilogue_f32<BM, BN>(acc, P + (int64_t)split * Mo * No, Mo, No, m0, n0);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split-K gemm_nt for few output tiles and a long reduction — the fully connected heads
+// (GoogLeNet aux fc1: M = batch 128, N = 1024, K = 2048 is 8 tiles of 32 k-steps each, 37 us on
+// 8 of 256 CUs). P[split][M, N] = A[:, ks] * B[:, ks]^T, summed (+ the row-broadcast bias addend)
+// by splitk_reduce_sg_kernel.
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, bool kBT, int PIPE>
+__global__ __launch_bounds__(kThreads, 2) void gemm_nt_splitk_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                                     const bf16_t* __restrict__ B, int64_t ldb,
+                                                                     float* __restrict__ P, int M, int N, int K,
+                                                                     int k_per_split, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int nbn = (N + BN - 1) / BN;
+  const int tile = blockIdx.x % ntiles, split = blockIdx.x / ntiles;
+  const int bm = tile / nbn, bn = tile % nbn;
+  const int64_t row0 = (int64_t)bm * BM;
+  const int col0 = bn * BN;
+  const int kbeg = split * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+  Acc<BM, BN> acc;
+  acc.zero();
+  const RowLoader<BM> la{A, lda, row0, M, kend};
+  if constexpr (kBT) {
+    const KLoader<BN> lb{B, ldb, col0, N, kend};
+    run_mainloop<PIPE>(la, lb, kbeg, kend, acc, smem_raw);
+  } else {
+    const RowLoader<BN> lb{B, ldb, (int64_t)col0, N, kend};
+    run_mainloop<PIPE>(la, lb, kbeg, kend, acc, smem_raw);
+  }
+  epilogue_f32<BM, BN>(acc, P + (int64_t)split * M * N, M, N, (int)row0, col0);
+}
+
 // Sums the split-K fp32 slabs: each thread owns 4 consecutive outputs (one 16-byte load per slab)
 // and keeps 4 slabs in flight, so the loop is bandwidth- rather than latency-bound.
 template <typename T>
@@ -129,9 +162,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // groups of a block split the slab range (group g sums slabs g, g+SG, ...), then group 0 adds the
 // SG partial sums from LDS in group order, so the result is still fixed-order and run-to-run
 // deterministic.
+// D (optional): bf16 addend of the [n / ncol, ncol] output with row stride ldd (0: one broadcast row,
+// the bias of a split-K linear layer), added after the scale.
 template <typename T, int SG>
 __global__ __launch_bounds__(256) void splitk_reduce_sg_kernel(const float* __restrict__ P, int splits, int64_t n,
-                                                               T* __restrict__ out, float scale, int accumulate) {
+                                                               T* __restrict__ out, float scale, int accumulate,
+                                                               const bf16_t* __restrict__ D, int64_t ldd, int ncol) {
+  auto addend = [&](int64_t i) -> float {
+    if (D == nullptr) return 0.f;
+    const int64_t r = i / ncol;
+    return bf16_to_f32(D[r * ldd + (i - r * ncol)]);
+  };
   constexpr int kOpb = 256 / SG;  // float4 outputs per block
   __shared__ float4_t red[SG][kOpb];
   const int g = threadIdx.x / kOpb, o = threadIdx.x % kOpb;
@@ -155,7 +196,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_sg_kernel(const float* __re
     s *= scale;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float r = s[j];
+      float r = s[j] + addend(v * 4 + j);
       if (accumulate) r += Cvt<T>::to_f32(out[v * 4 + j]);
       out[v * 4 + j] = Cvt<T>::from_f32(r);
     }
@@ -164,7 +205,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_sg_kernel(const float* __re
     for (int64_t i = nv * 4 + threadIdx.x; i < n; i += blockDim.x) {
       float r = 0.f;
       for (int k = 0; k < splits; ++k) r += P[(int64_t)k * n + i];
-      r *= scale;
+      r = r * scale + addend(i);
       if (accumulate) r += Cvt<T>::to_f32(out[i]);
       out[i] = Cvt<T>::from_f32(r);
     }
@@ -346,7 +387,7 @@ void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, floa
 }
 
 void launch_splitk_reduce(const float* partial, int splits, int64_t n, void* out, int out_dtype, float scale,
-                          bool accumulate, hipStream_t stream) {
+                          bool accumulate, hipStream_t stream, const void* addend, int64_t ld_addend, int ncol) {
   const int64_t nv = n / 4;
   // slab groups per block: the fewest that give >= 512 blocks, at most 64 and at most splits / 2
   // (DLA_SPLITK_SG=0: one thread per output, for A/B runs)
@@ -356,18 +397,20 @@ void launch_splitk_reduce(const float* partial, int splits, int64_t n, void* out
   }();
   int sg = 1;
   while (sg_on && sg < 64 && 2 * sg <= splits / 2 && (nv * sg + 255) / 256 < 512) sg *= 2;
-  if (sg > 1) {
+  const bf16_t* D = (const bf16_t*)addend;
+  if (sg > 1 || D != nullptr) {
     const int grid = (int)std::max<int64_t>(1, (nv * sg + 255) / 256);
 #define DLA_SKR(SG_)                                                                                              \
   case SG_:                                                                                                       \
     if (out_dtype == kF32)                                                                                        \
       hipLaunchKernelGGL((splitk_reduce_sg_kernel<float, SG_>), dim3(grid), dim3(256), 0, stream, partial, splits, \
-                         n, (float*)out, scale, (int)accumulate);                                                 \
+                         n, (float*)out, scale, (int)accumulate, D, ld_addend, ncol);                             \
     else                                                                                                          \
       hipLaunchKernelGGL((splitk_reduce_sg_kernel<bf16_t, SG_>), dim3(grid), dim3(256), 0, stream, partial,       \
-                         splits, n, (bf16_t*)out, scale, (int)accumulate);                                        \
+                         splits, n, (bf16_t*)out, scale, (int)accumulate, D, ld_addend, ncol);                    \
     break;
     switch (sg) {
+      DLA_SKR(1)
       DLA_SKR(2)
       DLA_SKR(4)
       DLA_SKR(8)
@@ -385,6 +428,43 @@ void launch_splitk_reduce(const float* partial, int splits, int64_t n, void* out
   else
     hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, dim3(grid), dim3(256), 0, stream, partial, splits, n,
                        (bf16_t*)out, scale, (int)accumulate);
+}
+
+// Split-K gemm_nt (fully connected heads): few output tiles, long K. 0 / 1 = the tile kernel.
+int gemm_nt_splitk_splits(int M, int N, int K) {
+  const int bn = N <= 64 ? 64 : 128;
+  const int tiles = ((M + 127) / 128) * ((N + bn - 1) / bn);
+  if (tiles >= 128 || K < 512) return 1;
+  // ~256 workgroups, >= 2 k-steps (128) per split
+  return std::max(1, std::min(K / 128, 256 / tiles));
+}
+
+void launch_gemm_nt_splitk(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, float* partial,
+                           int splits, void* C, int M, int N, int K, const void* addend, int64_t ld_addend,
+                           hipStream_t stream) {
+  int kps = (K + splits - 1) / splits;
+  kps = (kps + kBK - 1) / kBK * kBK;
+  splits = (K + kps - 1) / kps;
+  const int bn = N <= 64 ? 64 : 128;
+  const int tiles = ((M + 127) / 128) * ((N + bn - 1) / bn);
+  const bf16_t* a = (const bf16_t*)A;
+  const bf16_t* b = (const bf16_t*)B;
+#define DLA_NTS(BN_, BT_, P_)                                                                                       \
+  hipLaunchKernelGGL((gemm_nt_splitk_kernel<128, BN_, BT_, P_>), dim3(tiles * splits), dim3(kThreads),              \
+                     (run_mainloop_lds_bytes<P_, 128, BN_, RowLoader<128>,                                          \
+                                             std::conditional_t<BT_, KLoader<BN_>, RowLoader<BN_>>>()),              \
+                     stream, a, lda, b, ldb, partial, M, N, K, kps, tiles)
+#define DLA_NTS_P(BN_, BT_)                                     \
+  if (mfma_pipeline_for(kps) == 0) DLA_NTS(BN_, BT_, 0);        \
+  else DLA_NTS(BN_, BT_, 2);
+  if (bn == 64) {
+    if (b_kmajor) { DLA_NTS_P(64, true) } else { DLA_NTS_P(64, false) }
+  } else {
+    if (b_kmajor) { DLA_NTS_P(128, true) } else { DLA_NTS_P(128, false) }
+  }
+#undef DLA_NTS_P
+#undef DLA_NTS
+  launch_splitk_reduce(partial, splits, (int64_t)M * N, C, kBF16, 1.f, false, stream, addend, ld_addend, N);
 }
 
 }  // namespace dla

@@ -279,6 +279,15 @@ static const void* addend2_ptr(const c10::optional<at::Tensor>& a2, int64_t M, i
   return a2->data_ptr();
 }
 
+// DLA_GEMM_SPLITK=0 keeps every gemm_nt on the tile kernel (A/B runs)
+static bool split_k_nt() {
+  static const bool v = [] {
+    const char* e = std::getenv("DLA_GEMM_SPLITK");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::optional<at::Tensor> addend,
                                 bool b_kmajor, int64_t tile, c10::optional<at::Tensor> addend_mask,
                                 c10::optional<at::Tensor> addend2, int64_t H, int64_t W) {
@@ -296,6 +305,16 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
   at::Tensor S;
   if (stats) S = at::empty({gemm_nt_stats_rows(M, N, (int)tile), N, 2},
                            A.options().dtype(at::kFloat));
+  const bool plain = !stats && tile == kTileAuto && !(addend_mask.has_value() && addend_mask->defined()) &&
+                     !(addend2.has_value() && addend2->defined());
+  const int splits = plain && M > 0 && N > 0 && split_k_nt() ? gemm_nt_splitk_splits(M, N, K) : 1;
+  if (splits > 1) {  // few output tiles, long K (fully connected heads): split-K + fp32 slab reduce
+    at::Tensor P = at::empty({(int64_t)splits * M * N}, A.options().dtype(at::kFloat));
+    launch_gemm_nt_splitk(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), b_kmajor, P.data_ptr<float>(), splits,
+                          C.data_ptr(), M, N, K, add ? addend->data_ptr() : nullptr, add ? addend->stride(0) : 0,
+                          current_stream(A));
+    return {C, S};
+  }
   if (M > 0 && N > 0)
     launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K,
                    stats ? S.data_ptr<float>() : nullptr, current_stream(A), add ? addend->data_ptr() : nullptr,
@@ -670,6 +689,8 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("b_kmajor") = false, pybind11::arg("tile") = 0,
         pybind11::arg("addend_mask") = pybind11::none(), pybind11::arg("addend2") = pybind11::none(),
         pybind11::arg("H") = 0, pybind11::arg("W") = 0);
+  m.def("gemm_nt_splitk_splits", [](int64_t M, int64_t N, int64_t K) { return gemm_nt_splitk_splits((int)M, (int)N, (int)K); },
+        "split count gemm_nt uses for this shape (1 = tile kernel)");
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),
         pybind11::arg("out_dtype") = at::kFloat, pybind11::arg("scale") = 1.0);
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC", pybind11::arg("x"),

@@ -111,3 +111,26 @@ def test_mfma_pipelines_agree(cuda, pipe):
     for r, g in zip(ref, got):
         assert torch.equal(r, g)
     torch.testing.assert_close(got[0].float(), A.float() @ B.float().t(), rtol=1e-2, atol=0.15)
+
+
+@pytest.mark.parametrize("M,N,K,kmajor,addend", [(128, 1024, 2048, False, "bias"), (512, 1000, 2048, False, "bias"),
+                                                (512, 2048, 1000, True, None), (300, 136, 1000, True, "rows"),
+                                                (8, 64, 4096, False, "rows")])
+def test_gemm_nt_splitk_heads(cuda, M, N, K, kmajor, addend):
+    """Few output tiles + long K take the split-K path (fp32 slabs, fixed-order reduce with the addend)."""
+    C = _C()
+    assert C.gemm_nt_splitk_splits(M, N, K) > 1
+    torch.manual_seed(0)
+    A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    W = torch.randn(N, K, device=cuda).to(torch.bfloat16)
+    B = W.t().contiguous() if kmajor else W
+    D = None
+    if addend == "bias":
+        D = torch.randn(N, device=cuda).to(torch.bfloat16).expand(M, N)
+    elif addend == "rows":
+        D = torch.randn(M, N, device=cuda).to(torch.bfloat16)
+    y, _ = C.gemm_nt(A, B, False, D, kmajor)
+    ref = A.float() @ W.float().t() + (D.float() if D is not None else 0)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=2e-3 * K ** 0.5)
+    y2, _ = C.gemm_nt(A, B, False, D, kmajor)
+    assert torch.equal(y, y2)  # fixed-order reduction

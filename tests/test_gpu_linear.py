@@ -13,7 +13,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("B,fin,fout,bias", [(2, 2048, 1000, True), (512, 2048, 1000, True), (7, 1024, 1000, True),
-                                             (64, 1024, 1024, False), (130, 128, 16, True)])
+                                             (64, 1024, 1024, False), (130, 128, 16, True),
+                                             (128, 2048, 1024, True), (128, 1024, 1000, True)])
 def test_native_linear_matches_fp32(cuda, B, fin, fout, bias):
     from distributed_learning_amd.ops.linear import linear, supported
 
