@@ -125,6 +125,33 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
                    float* dbeta, int mask_mode, hipStream_t stream, const float* ext_part = nullptr,
                    int ext_nrb = 0, int64_t ld_dy = 0);  // ld_dy: dy row stride when dy is a channel slice
 
+// Grouped training BN+ReLU over the branches of a channel concatenation (bn_act.hip): one launch
+// per pass for up to kMaxBnGroups branches. Forward: part = each branch's [nrb][C][2] epilogue
+// statistics (wpart: fold scratch, bn_fold_groups(nrb) rows), outputs into channels [off, off + C)
+// of out (row stride ldo). Backward: dy read from the same slices of dout; wpart = reduce scratch of
+// bn_group_bwd_rows() rows; dx, dgamma, dbeta per branch. ReLU mask recomputed from x.
+constexpr int kMaxBnGroups = 4;
+struct BnGroups {
+  int n;
+  int begin[kMaxBnGroups + 1];
+  const uint16_t* x[kMaxBnGroups];  // bf16 bits
+  int C[kMaxBnGroups], tpr[kMaxBnGroups], off[kMaxBnGroups], nrb[kMaxBnGroups];
+  const float* part[kMaxBnGroups];
+  float* wpart[kMaxBnGroups];
+  const float* gamma[kMaxBnGroups];
+  const float* beta[kMaxBnGroups];
+  float* rm[kMaxBnGroups];
+  float* rv[kMaxBnGroups];
+  float* ws[kMaxBnGroups];
+  float eps[kMaxBnGroups], mom[kMaxBnGroups];
+  uint16_t* dx[kMaxBnGroups];
+  float* dgamma[kMaxBnGroups];
+  float* dbeta[kMaxBnGroups];
+};
+int bn_group_bwd_rows(int64_t M, const int* C, int n);
+void launch_bn_group_fwd(BnGroups G, void* out, int64_t ldo, int64_t M, hipStream_t stream);
+void launch_bn_group_bwd(BnGroups G, const void* dout, int64_t ldo, int64_t M, hipStream_t stream);
+
 // Stem BN(+ReLU)+max-pool fused (bn_act.hip): launch_bn_fwd with y == nullptr computes ws only;
 // then the pooled output + window positions come straight from the BN input x. Backward: the BN
 // passes gather dy from the pooled gradient. x/dx [N,H,W,C] bf16, pooled [N,OH,OW,C].

@@ -126,11 +126,11 @@ __global__ __launch_bounds__(kBNThreads) void bn_stats_kernel(const T* __restric
 // reduction passes, WPC = 4 for the per-128-row-tile partials of the GEMM epilogues.
 // Fixed order -> bitwise reproducible.
 template <int WPC>
-__device__ __forceinline__ bool reduce_partials(const float* __restrict__ part, int nrb, int C, float& S, float& Q,
-                                                int& c) {
+__device__ __forceinline__ bool reduce_partials(int bx, const float* __restrict__ part, int nrb, int C, float& S,
+                                                float& Q, int& c) {
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  c = blockIdx.x * (4 / WPC) + wave / WPC;
+  c = bx * (4 / WPC) + wave / WPC;
   float s[8], q[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) s[u] = q[u] = 0.f;
@@ -244,7 +244,7 @@ int64_t bn_partial_floats(int64_t M, int C, int target_blocks) {
 constexpr int kQuadRedBlocks = 4096;
 
 template <int WPC>
-__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __restrict__ x0, int x_is_bf16,
+__device__ __forceinline__ void bn_stats_finalize_body(int bx, const void* __restrict__ x0, int x_is_bf16,
                                                                 const float* __restrict__ part, int nrb, int64_t M,
                                                                 int C, const float* __restrict__ gamma,
                                                                 const float* __restrict__ beta, float eps,
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __re
                                                                 float* __restrict__ ws) {
   float S, Q;
   int c;
-  if (!reduce_partials<WPC>(part, nrb, C, S, Q, c)) return;
+  if (!reduce_partials<WPC>(bx, part, nrb, C, S, Q, c)) return;
   const float K = x0 == nullptr ? 0.f
                   : (x_is_bf16 ? bf16_to_f32(reinterpret_cast<const bf16_t*>(x0)[c]) : reinterpret_cast<const float*>(x0)[c]);
   const float inv_m = 1.f / (float)M;
@@ -275,6 +275,15 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __re
   }
 }
 
+template <int WPC>
+__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __restrict__ x0, int x_is_bf16, const float* __restrict__ part,
+                                                                int nrb, int64_t M, int C, const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, float eps, float momentum,
+                                                                float* __restrict__ running_mean,
+                                                                float* __restrict__ running_var, float* __restrict__ ws) {
+  bn_stats_finalize_body<WPC>(blockIdx.x, x0, x_is_bf16, part, nrb, M, C, gamma, beta, eps, momentum, running_mean, running_var, ws);
+}
+
 // ---------------------------------------------------------------------------------------------
 // forward: apply  y = act(x*scale + shift [+ res])
 // ---------------------------------------------------------------------------------------------
@@ -282,18 +291,18 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const void* __re
 // y = act(x*scale + shift + (res*scale2 + shift2)) with scale2/shift2 from ws2 — the downsample BN's
 // output is never written and re-read.
 template <typename T, bool kRes, bool kRelu, bool kBnRes = false>
-__global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
+__device__ __forceinline__ void bn_apply_body(int bx, const T* __restrict__ x, const T* __restrict__ res,
                                                               T* __restrict__ y, const float* __restrict__ ws,
                                                               int64_t M, int C, int nrb, int tpr,
                                                               uint8_t* __restrict__ mask,
-                                                              const float* __restrict__ ws2 = nullptr,
-                                                              int64_t ldy = 0) {
+                                                              const float* __restrict__ ws2,
+                                                              int64_t ldy) {
   // ldy != 0: y is a channel slice of a wider channels_last tensor (row stride ldy), e.g. one
   // Inception branch written straight into the concatenated block output
   // Same tiling as the reduction passes: a thread owns 8 fixed channels for all its rows, so the
   // per-channel coefficients live in registers (no per-element index math or table reads).
   const int rpi = kBNThreads / tpr, ct = tpr * 8;
-  const int c0 = blockIdx.x * ct + (threadIdx.x % tpr) * 8;
+  const int c0 = bx * ct + (threadIdx.x % tpr) * 8;
   const int rg = threadIdx.x / tpr;
   int64_t r0, r1;
   block_rows(M, nrb, r0, r1);
@@ -359,6 +368,14 @@ __global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restric
     }
   }
   for (; r < r1; r += rpi) row(r);
+}
+
+template <typename T, bool kRes, bool kRelu, bool kBnRes = false>
+__global__ __launch_bounds__(kBNThreads) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
+                                                              const float* __restrict__ ws, int64_t M, int C, int nrb,
+                                                              int tpr, uint8_t* __restrict__ mask,
+                                                              const float* __restrict__ ws2 = nullptr, int64_t ldy = 0) {
+  bn_apply_body<T, kRes, kRelu, kBnRes>(blockIdx.x, x, res, y, ws, M, C, nrb, tpr, mask, ws2, ldy);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -466,14 +483,14 @@ struct PoolDy {
 };
 
 template <typename T, int kMask, class DY = DirectDy<T>>
-__global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(DY dy, const T* __restrict__ y,
+__device__ __forceinline__ void bn_bwd_reduce_body(int bx, DY dy, const T* __restrict__ y,
                                                                    const uint8_t* __restrict__ mask,
                                                                    const T* __restrict__ x,
                                                                    const float* __restrict__ ws, int64_t M, int C,
                                                                    int nrb, int tpr, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float red[];
   const int rpi = kBNThreads / tpr, ct = tpr * 8;
-  const int c_base = blockIdx.x * ct;
+  const int c_base = bx * ct;
   const int c0 = c_base + (threadIdx.x % tpr) * 8;
   const int rg = threadIdx.x / tpr;
   int64_t r0, r1;
@@ -534,14 +551,22 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(DY dy, const 
   block_reduce_write(s, q, tpr, rpi, ct, C, part, c_base, red);
 }
 
+template <typename T, int kMask, class DY = DirectDy<T>>
+__global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(DY dy, const T* __restrict__ y, const uint8_t* __restrict__ mask,
+                                                                   const T* __restrict__ x, const float* __restrict__ ws,
+                                                                   int64_t M, int C, int nrb, int tpr,
+                                                                   float* __restrict__ part) {
+  bn_bwd_reduce_body<T, kMask, DY>(blockIdx.x, dy, y, mask, x, ws, M, C, nrb, tpr, part);
+}
+
 template <int WPC>
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int64_t M,
+__device__ __forceinline__ void bn_bwd_finalize_body(int bx, const float* __restrict__ part, int nrb, int64_t M,
                                                               int C, const float* __restrict__ gamma,
                                                               float* __restrict__ ws, float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta) {
   float S, Q;
   int c;
-  if (!reduce_partials<WPC>(part, nrb, C, S, Q, c)) return;
+  if (!reduce_partials<WPC>(bx, part, nrb, C, S, Q, c)) return;
   const float invstd = ws[C + c];
   const float g = gamma ? gamma[c] : 1.f;
   if (dgamma) dgamma[c] = Q * invstd;
@@ -554,15 +579,22 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   ws[6 * C + c] = invstd * invstd * Q * inv_m;
 }
 
+template <int WPC>
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int64_t M, int C,
+                                                              const float* __restrict__ gamma, float* __restrict__ ws,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  bn_bwd_finalize_body<WPC>(blockIdx.x, part, nrb, M, C, gamma, ws, dgamma, dbeta);
+}
+
 template <typename T, int kMask, bool kDres, class DY = DirectDy<T>>
-__global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(DY dy, const T* __restrict__ y,
+__device__ __forceinline__ void bn_bwd_apply_body(int bx, DY dy, const T* __restrict__ y,
                                                                   const uint8_t* __restrict__ mask,
                                                                   const T* __restrict__ x,
                                                                   const float* __restrict__ ws, T* __restrict__ dx,
                                                                   T* __restrict__ dres, int64_t M, int C, int nrb,
                                                                   int tpr) {
   const int rpi = kBNThreads / tpr, ct = tpr * 8;
-  const int c0 = blockIdx.x * ct + (threadIdx.x % tpr) * 8;
+  const int c0 = bx * ct + (threadIdx.x % tpr) * 8;
   const int rg = threadIdx.x / tpr;
   int64_t r0, r1;
   block_rows(M, nrb, r0, r1);
@@ -621,6 +653,14 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(DY dy, const T
     }
   }
   for (; r < r1; r += rpi) row(r);
+}
+
+template <typename T, int kMask, bool kDres, class DY = DirectDy<T>>
+__global__ __launch_bounds__(kBNThreads) void bn_bwd_apply_kernel(DY dy, const T* __restrict__ y, const uint8_t* __restrict__ mask,
+                                                                  const T* __restrict__ x, const float* __restrict__ ws,
+                                                                  T* __restrict__ dx, T* __restrict__ dres, int64_t M,
+                                                                  int C, int nrb, int tpr) {
+  bn_bwd_apply_body<T, kMask, kDres, DY>(blockIdx.x, dy, y, mask, x, ws, dx, dres, M, C, nrb, tpr);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1236,6 +1276,127 @@ void launch_bn_dual_bwd(const void* dy, const uint8_t* mask, const void* x, cons
     if (bits) DLA_DUAL_APPLY(float, kMaskBits); else DLA_DUAL_APPLY(float, kMaskNone);
   }
 #undef DLA_DUAL_APPLY
+}
+
+// ---------------------------------------------------------------------------------------------
+// Grouped BatchNorm+ReLU over the branches of a channel concatenation (an Inception block's four
+// branch BNs, whose outputs are channel slices of one NHWC tensor). One launch per pass for all
+// branches instead of one per branch: at GoogLeNet's 14x14 / 7x7 shapes each per-branch finalize /
+// apply / reduce pass is a few-microsecond launch (profiles/googlenet_bs128_graph_r3o_ksum.md).
+// Block x of a grouped grid belongs to group g for begin[g] <= x < begin[g + 1] and runs the
+// single-tensor body with x - begin[g] as its channel-tile index, so every group computes exactly
+// what its own launch would (same tiles, same fixed-order reductions).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int bn_group_of(const BnGroups& G, int bx) {
+  int g = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxBnGroups; ++i)
+    if (i < G.n && bx >= G.begin[i]) g = i;
+  return g;
+}
+
+__global__ __launch_bounds__(256) void bn_group_stats_finalize_kernel(BnGroups G, int64_t M) {
+  const int g = bn_group_of(G, blockIdx.x);
+  bn_stats_finalize_body<1>(blockIdx.x - G.begin[g], nullptr, 0, G.part[g], G.nrb[g], M, G.C[g], G.gamma[g],
+                            G.beta[g], G.eps[g], G.mom[g], G.rm[g], G.rv[g], G.ws[g]);
+}
+
+__global__ __launch_bounds__(kBNThreads) void bn_group_apply_kernel(BnGroups G, bf16_t* __restrict__ out, int64_t ldo,
+                                                                    int64_t M, int nrb) {
+  const int g = bn_group_of(G, blockIdx.x);
+  bn_apply_body<bf16_t, false, true, false>(blockIdx.x - G.begin[g], G.x[g], nullptr, out + G.off[g], G.ws[g], M,
+                                            G.C[g], nrb, G.tpr[g], nullptr, nullptr, ldo);
+}
+
+__global__ __launch_bounds__(kBNThreads) void bn_group_bwd_reduce_kernel(BnGroups G, const bf16_t* __restrict__ dout,
+                                                                         int64_t ldo, int64_t M, int nrb) {
+  const int g = bn_group_of(G, blockIdx.x);
+  bn_bwd_reduce_body<bf16_t, kMaskRecomp, DirectDy<bf16_t>>(blockIdx.x - G.begin[g], DirectDy<bf16_t>{dout + G.off[g], ldo},
+                                                            nullptr, nullptr, G.x[g], G.ws[g], M, G.C[g], nrb,
+                                                            G.tpr[g], G.wpart[g]);
+}
+
+__global__ __launch_bounds__(256) void bn_group_bwd_finalize_kernel(BnGroups G, int64_t M) {
+  const int g = bn_group_of(G, blockIdx.x);
+  bn_bwd_finalize_body<1>(blockIdx.x - G.begin[g], G.part[g], G.nrb[g], M, G.C[g], G.gamma[g], G.ws[g], G.dgamma[g],
+                          G.dbeta[g]);
+}
+
+__global__ __launch_bounds__(kBNThreads) void bn_group_bwd_apply_kernel(BnGroups G, const bf16_t* __restrict__ dout,
+                                                                        int64_t ldo, int64_t M, int nrb) {
+  const int g = bn_group_of(G, blockIdx.x);
+  bn_bwd_apply_body<bf16_t, kMaskRecomp, false, DirectDy<bf16_t>>(blockIdx.x - G.begin[g],
+                                                                  DirectDy<bf16_t>{dout + G.off[g], ldo}, nullptr,
+                                                                  nullptr, G.x[g], G.ws[g], G.dx[g], nullptr, M, G.C[g],
+                                                                  nrb, G.tpr[g]);
+}
+
+// channel tiles of each group for a pass with this block target; returns the row-block count the
+// groups share (bn_geometry's rule: ~target blocks in all, >= 4 row iterations per thread)
+static int bn_group_tiles(BnGroups& G, int64_t M, int target_blocks) {
+  int nct_tot = 0;
+  int64_t cap = INT64_MAX;
+  for (int g = 0; g < G.n; ++g) {
+    int tpr, nrb, nct;
+    bn_geometry(M, G.C[g], &tpr, &nrb, &nct, target_blocks);
+    G.tpr[g] = tpr;
+    G.begin[g] = nct_tot;
+    nct_tot += nct;
+    const int64_t rpi = kBNThreads / tpr;
+    cap = std::min<int64_t>(cap, (M + 4 * rpi - 1) / (4 * rpi));
+  }
+  G.begin[G.n] = nct_tot;
+  const int64_t want = std::max<int64_t>(1, target_blocks / std::max(1, nct_tot));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, cap));
+}
+
+static void bn_group_finalize_blocks(BnGroups& G) {
+  int b = 0;
+  for (int g = 0; g < G.n; ++g) {
+    G.begin[g] = b;
+    b += (G.C[g] + 3) / 4;
+  }
+  G.begin[G.n] = b;
+}
+
+int bn_group_bwd_rows(int64_t M, const int* C, int n) {
+  BnGroups G{};
+  G.n = n;
+  for (int g = 0; g < n; ++g) G.C[g] = C[g];
+  return bn_group_tiles(G, M, bn_red_blocks() > 1024 ? 1024 : bn_red_blocks());
+}
+
+void launch_bn_group_fwd(BnGroups G, void* out, int64_t ldo, int64_t M, hipStream_t stream) {
+  // epilogue partials of many row tiles: fold each group's rows first (into its wpart scratch)
+  for (int g = 0; g < G.n; ++g) {
+    if (const int fg = bn_fold_groups(G.nrb[g])) {
+      hipLaunchKernelGGL(bn_partials_fold_kernel, dim3((G.C[g] + 63) / 64, fg), dim3(256), 0, stream, G.part[g],
+                         G.nrb[g], G.C[g], G.wpart[g]);
+      G.part[g] = G.wpart[g];
+      G.nrb[g] = fg;
+    }
+  }
+  bn_group_finalize_blocks(G);
+  hipLaunchKernelGGL(bn_group_stats_finalize_kernel, dim3(G.begin[G.n]), dim3(256), 0, stream, G, M);
+  const int nrb = bn_group_tiles(G, M, 4096);
+  hipLaunchKernelGGL(bn_group_apply_kernel, dim3(G.begin[G.n], nrb), dim3(kBNThreads), 0, stream, G, (bf16_t*)out,
+                     ldo, M, nrb);
+}
+
+void launch_bn_group_bwd(BnGroups G, const void* dout, int64_t ldo, int64_t M, hipStream_t stream) {
+  const int nrb = bn_group_tiles(G, M, bn_red_blocks() > 1024 ? 1024 : bn_red_blocks());
+  const size_t lds = (size_t)kBNThreads * 8 * 2 * sizeof(float);  // rpi * ct * 2 floats for any tpr
+  hipLaunchKernelGGL(bn_group_bwd_reduce_kernel, dim3(G.begin[G.n], nrb), dim3(kBNThreads), lds, stream, G,
+                     (const bf16_t*)dout, ldo, M, nrb);
+  for (int g = 0; g < G.n; ++g) {
+    G.part[g] = G.wpart[g];
+    G.nrb[g] = nrb;
+  }
+  bn_group_finalize_blocks(G);
+  hipLaunchKernelGGL(bn_group_bwd_finalize_kernel, dim3(G.begin[G.n]), dim3(256), 0, stream, G, M);
+  const int anrb = bn_group_tiles(G, M, 4096);
+  hipLaunchKernelGGL(bn_group_bwd_apply_kernel, dim3(G.begin[G.n], anrb), dim3(kBNThreads), 0, stream, G,
+                     (const bf16_t*)dout, ldo, M, anrb);
 }
 
 }  // namespace dla

@@ -279,6 +279,121 @@ static const void* addend2_ptr(const c10::optional<at::Tensor>& a2, int64_t M, i
   return a2->data_ptr();
 }
 
+// Grouped training BN+ReLU of an Inception block's branches (launch_bn_group_fwd): each y_g, with
+// its conv epilogue's statistics, normalised into channels [off_g, off_g + C_g) of out (the
+// concatenated NHWC block output). Returns the per-branch 7C workspaces.
+static void check_bn_param(const at::Tensor& t, int64_t C, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == C, what,
+              " must be a contiguous fp32 GPU vector of C elements");
+}
+
+std::vector<at::Tensor> bn_concat_fwd(std::vector<at::Tensor> ys, std::vector<at::Tensor> gammas,
+                                      std::vector<at::Tensor> betas, std::vector<at::Tensor> rms,
+                                      std::vector<at::Tensor> rvs, std::vector<double> moms, std::vector<double> epss,
+                                      std::vector<at::Tensor> stats, at::Tensor out) {
+  const int n = (int)ys.size();
+  TORCH_CHECK(n >= 1 && n <= kMaxBnGroups && (int)gammas.size() == n && (int)betas.size() == n &&
+                  (int)rms.size() == n && (int)rvs.size() == n && (int)moms.size() == n && (int)epss.size() == n &&
+                  (int)stats.size() == n,
+              "bn_concat_fwd: 1..4 branches, one entry per branch in every list");
+  check_act(out, "out");
+  TORCH_CHECK(out.dim() == 4 && out.scalar_type() == at::kBFloat16, "bn_concat_fwd: out must be bf16 [N, Ctot, H, W]");
+  const int64_t M = rows_of(out);
+  auto f32 = out.options().dtype(at::kFloat);
+  BnGroups G{};
+  G.n = n;
+  std::vector<at::Tensor> wss, keep;
+  int off = 0;
+  for (int g = 0; g < n; ++g) {
+    const at::Tensor& y = ys[g];
+    check_act(y, "y");
+    TORCH_CHECK(y.dim() == 4 && y.scalar_type() == at::kBFloat16 && y.size(0) == out.size(0) &&
+                    y.size(2) == out.size(2) && y.size(3) == out.size(3),
+                "bn_concat_fwd: every branch must be bf16 with out's batch and spatial size");
+    const int C = (int)y.size(1);
+    const at::Tensor& st = stats[g];
+    TORCH_CHECK(st.is_cuda() && st.scalar_type() == at::kFloat && st.is_contiguous() && st.dim() == 3 &&
+                    st.size(1) == C && st.size(2) == 2,
+                "bn_concat_fwd: stats must be fp32 [row_blocks, C, 2] epilogue partials");
+    check_bn_param(gammas[g], C, "weight");
+    check_bn_param(betas[g], C, "bias");
+    check_bn_param(rms[g], C, "running_mean");
+    check_bn_param(rvs[g], C, "running_var");
+    at::Tensor ws = at::empty({7 * (int64_t)C}, f32);
+    at::Tensor fold = at::empty({std::max<int64_t>(1, (int64_t)bn_fold_groups((int)st.size(0)) * C * 2)}, f32);
+    G.x[g] = (const uint16_t*)y.data_ptr();
+    G.C[g] = C;
+    G.off[g] = off;
+    G.nrb[g] = (int)st.size(0);
+    G.part[g] = st.data_ptr<float>();
+    G.wpart[g] = fold.data_ptr<float>();
+    G.gamma[g] = gammas[g].data_ptr<float>();
+    G.beta[g] = betas[g].data_ptr<float>();
+    G.rm[g] = rms[g].data_ptr<float>();
+    G.rv[g] = rvs[g].data_ptr<float>();
+    G.ws[g] = ws.data_ptr<float>();
+    G.eps[g] = (float)epss[g];
+    G.mom[g] = (float)moms[g];
+    wss.push_back(ws);
+    keep.push_back(fold);
+    off += C;
+  }
+  TORCH_CHECK(off == out.size(1), "bn_concat_fwd: branch channels must add up to out's channels");
+  if (M > 0) launch_bn_group_fwd(G, out.data_ptr(), out.size(1), M, current_stream(out));
+  return wss;
+}
+
+// Backward of bn_concat_fwd: dy of branch g read in place from channels [off_g, off_g + C_g) of
+// dout; returns [dx_0, dgamma_0, dbeta_0, dx_1, ...].
+std::vector<at::Tensor> bn_concat_bwd(at::Tensor dout, std::vector<at::Tensor> ys, std::vector<at::Tensor> gammas,
+                                      std::vector<at::Tensor> wss) {
+  const int n = (int)ys.size();
+  TORCH_CHECK(n >= 1 && n <= kMaxBnGroups && (int)gammas.size() == n && (int)wss.size() == n,
+              "bn_concat_bwd: 1..4 branches, one entry per branch in every list");
+  check_act(dout, "dout");
+  TORCH_CHECK(dout.dim() == 4 && dout.scalar_type() == at::kBFloat16, "bn_concat_bwd: dout must be bf16 [N, Ctot, H, W]");
+  const int64_t M = rows_of(dout);
+  auto f32 = dout.options().dtype(at::kFloat);
+  BnGroups G{};
+  G.n = n;
+  int Cs[kMaxBnGroups];
+  std::vector<at::Tensor> res;
+  int off = 0;
+  for (int g = 0; g < n; ++g) {
+    const at::Tensor& y = ys[g];
+    check_act(y, "y");
+    TORCH_CHECK(y.dim() == 4 && y.scalar_type() == at::kBFloat16 && y.size(0) == dout.size(0) &&
+                    y.size(2) == dout.size(2) && y.size(3) == dout.size(3),
+                "bn_concat_bwd: every branch must be bf16 with dout's batch and spatial size");
+    const int C = (int)y.size(1);
+    check_bn_param(gammas[g], C, "weight");
+    TORCH_CHECK(wss[g].scalar_type() == at::kFloat && wss[g].numel() == 7 * (int64_t)C, "ws must be the 7C workspace");
+    Cs[g] = C;
+    at::Tensor dx = at::empty_like(y), dg = at::empty({C}, f32), db = at::empty({C}, f32);
+    G.x[g] = (const uint16_t*)y.data_ptr();
+    G.C[g] = C;
+    G.off[g] = off;
+    G.gamma[g] = gammas[g].data_ptr<float>();
+    G.ws[g] = wss[g].data_ptr<float>();
+    G.dx[g] = (uint16_t*)dx.data_ptr();
+    G.dgamma[g] = dg.data_ptr<float>();
+    G.dbeta[g] = db.data_ptr<float>();
+    res.push_back(dx);
+    res.push_back(dg);
+    res.push_back(db);
+    off += C;
+  }
+  TORCH_CHECK(off == dout.size(1), "bn_concat_bwd: branch channels must add up to dout's channels");
+  const int rows = bn_group_bwd_rows(M, Cs, n);
+  std::vector<at::Tensor> keep;
+  for (int g = 0; g < n; ++g) {
+    keep.push_back(at::empty({(int64_t)rows * Cs[g] * 2}, f32));
+    G.wpart[g] = keep.back().data_ptr<float>();
+  }
+  if (M > 0) launch_bn_group_bwd(G, dout.data_ptr(), dout.size(1), M, current_stream(dout));
+  return res;
+}
+
 // DLA_GEMM_SPLITK=0 keeps every gemm_nt on the tile kernel (A/B runs)
 static bool split_k_nt() {
   static const bool v = [] {
@@ -698,6 +813,8 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("running_var"), pybind11::arg("training"), pybind11::arg("momentum"), pybind11::arg("eps"),
         pybind11::arg("relu"), pybind11::arg("stats") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
         pybind11::arg("out_channel") = 0);
+  m.def("bn_concat_fwd", &bn_concat_fwd, "grouped training BN+ReLU of concatenated branches into one NHWC output");
+  m.def("bn_concat_bwd", &bn_concat_bwd, "backward of bn_concat_fwd (dy slices read in place)");
   m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC", pybind11::arg("dy"),
         pybind11::arg("y"), pybind11::arg("mask"), pybind11::arg("x"), pybind11::arg("ws"), pybind11::arg("weight"),
         pybind11::arg("mask_mode"), pybind11::arg("need_dres"), pybind11::arg("ext_part") = pybind11::none());

@@ -19,11 +19,16 @@ Here two autograd nodes replace them:
 * :class:`_BNReluConcat` applies the four branch BatchNorm+ReLU passes straight into channel slices
   of one preallocated NHWC block output (row stride = total channels). Its backward reads each
   branch's dy in place from the concatenated gradient (strided loads in the BN backward passes).
+  The four branches run as one group per pass (``bn_concat_fwd`` / ``bn_concat_bwd``: one
+  finalize + one apply launch forward, one reduce + finalize + apply backward, instead of one chain
+  per branch), which matters at the 14x14 / 7x7 shapes where each pass is a few-microsecond launch.
 
 Reference: the block structure of torchvision's GoogLeNet v0.6, which the reference loads through
 torch.hub (/root/reference/src/network.py:33-54).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn as nn
@@ -99,11 +104,17 @@ class _BNReluConcat(torch.autograd.Function):
         n, _, h, w = ys[0].shape
         ctot = sum(y.shape[1] for y in ys)
         out = torch.empty((n, ctot, h, w), dtype=ys[0].dtype, device=ys[0].device, memory_format=CL)
-        wss, off = [], 0
-        for y, g, b, (rm, rv, mom, eps, st) in zip(ys, gs, bs, metas):
-            _, ws, _ = C.bn_act_fwd(y, None, g, b, rm, rv, True, mom, eps, True, st, out, off)
-            wss.append(ws)
-            off += y.shape[1]
+        ctx.grouped = _grouped_ok(ys, gs, bs, metas)
+        if ctx.grouped:
+            # one finalize + one apply launch for all branches (bn_act.hip, grouped kernels)
+            wss = C.bn_concat_fwd(list(ys), list(gs), list(bs), [m[0] for m in metas], [m[1] for m in metas],
+                                  [m[2] for m in metas], [m[3] for m in metas], [m[4] for m in metas], out)
+        else:
+            wss, off = [], 0
+            for y, g, b, (rm, rv, mom, eps, st) in zip(ys, gs, bs, metas):
+                _, ws, _ = C.bn_act_fwd(y, None, g, b, rm, rv, True, mom, eps, True, st, out, off)
+                wss.append(ws)
+                off += y.shape[1]
         ctx.save_for_backward(*ys, *gs, *wss)
         ctx.nb = len(ys)
         return out
@@ -117,6 +128,8 @@ class _BNReluConcat(torch.autograd.Function):
         dout = dout.contiguous(memory_format=CL)
         if dout.dtype != ys[0].dtype:
             dout = dout.to(ys[0].dtype)
+        if ctx.grouped:
+            return (None, *C.bn_concat_bwd(dout, list(ys), list(gs), list(wss)))
         grads, off = [None], 0
         for y, g, ws in zip(ys, gs, wss):
             c = y.shape[1]
@@ -124,6 +137,22 @@ class _BNReluConcat(torch.autograd.Function):
             grads += [dx, dg, db]
             off += c
         return tuple(grads)
+
+
+# DLA_BN_GROUPED=0 keeps one BN launch chain per branch (A/B runs)
+_GROUPED = os.environ.get("DLA_BN_GROUPED", "1") != "0"
+
+
+def _grouped_ok(ys, gs, bs, metas) -> bool:
+    """The grouped kernels take bf16 branches with epilogue statistics and fp32 BN parameters."""
+    if not _GROUPED or not 1 <= len(ys) <= 4:
+        return False
+    for y, g, b, (rm, rv, _, _, st) in zip(ys, gs, bs, metas):
+        if st is None or y.dtype != torch.bfloat16 or rm is None or rv is None:
+            return False
+        if not all(t.dtype == torch.float32 and t.is_contiguous() for t in (g, b, rm, rv)):
+            return False
+    return True
 
 
 def _bn_ok(bn: nn.BatchNorm2d) -> bool:

@@ -39,6 +39,52 @@ def test_bn_act_into_slice_and_strided_dy(cuda):
             assert torch.equal(u, v)
 
 
+@pytest.mark.parametrize("shape", [(4, 7, 9), (35, 80, 50)])  # the second has > 1024 epilogue row tiles (fold path)
+def test_bn_concat_matches_per_branch(cuda, shape):
+    """Grouped BN+ReLU over concatenated branches == one bn_act_fwd / bn_act_bwd chain per branch."""
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    torch.manual_seed(0)
+    n, h, w = shape
+    chans = [64, 96, 24, 208]
+    ys, sts, gs, bs, rms, rvs = [], [], [], [], [], []
+    for c in chans:
+        a = torch.randn(n * h * w, 32, device=cuda).to(torch.bfloat16)
+        wt = torch.randn(c, 32, device=cuda).to(torch.bfloat16)
+        y2, st = C.gemm_nt(a, wt, True)  # the conv epilogue's statistics, as in the fused block
+        ys.append(y2.view(n, h, w, c).permute(0, 3, 1, 2))
+        sts.append(st)
+        gs.append(torch.rand(c, device=cuda) + 0.5)
+        bs.append(torch.randn(c, device=cuda))
+        rms.append(torch.randn(c, device=cuda))
+        rvs.append(torch.rand(c, device=cuda) + 0.5)
+    ctot = sum(chans)
+    out_g = torch.zeros(n, ctot, h, w, device=cuda, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    out_r = torch.zeros_like(out_g)
+    rm_g, rv_g = [t.clone() for t in rms], [t.clone() for t in rvs]
+    wss_g = C.bn_concat_fwd(ys, gs, bs, rm_g, rv_g, [0.1] * 4, [1e-3] * 4, sts, out_g)
+    wss_r, off = [], 0
+    for i, c in enumerate(chans):
+        _, ws, _ = C.bn_act_fwd(ys[i], None, gs[i], bs[i], rms[i], rvs[i], True, 0.1, 1e-3, True, sts[i], out_r, off)
+        wss_r.append(ws)
+        off += c
+    assert torch.equal(out_g, out_r)
+    for a, b in zip(rm_g + rv_g, rms + rvs):
+        assert torch.equal(a, b)
+    for a, b in zip(wss_g, wss_r):
+        assert torch.equal(a[:4 * a.numel() // 7], b[:4 * b.numel() // 7])
+    dout = torch.randn(n, ctot, h, w, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    got = C.bn_concat_bwd(dout, ys, gs, wss_g)
+    off = 0
+    for i, c in enumerate(chans):
+        dx, _, dg, db = C.bn_act_bwd(dout[:, off:off + c], None, None, ys[i], wss_r[i], gs[i], 1, False, None)
+        gdx, gdg, gdb = got[3 * i:3 * i + 3]
+        assert gdx.shape == dx.shape and gdx.is_contiguous(memory_format=CL)
+        assert _rel(gdx, dx) < 1e-2 and _rel(gdg, dg) < 1e-4 and _rel(gdb, db) < 1e-4, (i, _rel(gdx, dx))
+        off += c
+
+
 def _block():
     from distributed_learning_amd.models.googlenet import Inception
     from distributed_learning_amd.ops import nn as dnn
