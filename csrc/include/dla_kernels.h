@@ -125,17 +125,22 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
                    float* dbeta, int mask_mode, hipStream_t stream, const float* ext_part = nullptr,
                    int ext_nrb = 0, int64_t ld_dy = 0);  // ld_dy: dy row stride when dy is a channel slice
 
-// Grouped training BN+ReLU over the branches of a channel concatenation (bn_act.hip): one launch
-// per pass for up to kMaxBnGroups branches. Forward: part = each branch's [nrb][C][2] epilogue
-// statistics (wpart: fold scratch, bn_fold_groups(nrb) rows), outputs into channels [off, off + C)
-// of out (row stride ldo). Backward: dy read from the same slices of dout; wpart = reduce scratch of
-// bn_group_bwd_rows() rows; dx, dgamma, dbeta per branch. ReLU mask recomputed from x.
+// Grouped training BN+ReLU (bn_act.hip): one launch per pass for up to kMaxBnGroups BatchNorms of
+// the same row count M — the branches of an Inception block. Group g normalises x[g] ([M, C[g]] bf16)
+// into y[g] (row stride ldy[g], 0 = contiguous; a channel slice of the concatenated output, or its
+// own tensor). Forward: part[g] = the [nrb][C][2] conv-epilogue statistics, wpart[g] = fold scratch
+// (bn_fold_groups(nrb) rows). Backward: dy[g] (row stride lddy[g]); with ext, part[g] already holds
+// the dgrad epilogue's reduction partials (nrb[g] rows; wpart[g] = fold scratch), otherwise
+// wpart[g] receives bn_group_bwd_rows() rows of reduce partials. ReLU mask recomputed from x.
 constexpr int kMaxBnGroups = 4;
 struct BnGroups {
   int n;
   int begin[kMaxBnGroups + 1];
   const uint16_t* x[kMaxBnGroups];  // bf16 bits
-  int C[kMaxBnGroups], tpr[kMaxBnGroups], off[kMaxBnGroups], nrb[kMaxBnGroups];
+  uint16_t* y[kMaxBnGroups];
+  const uint16_t* dy[kMaxBnGroups];
+  int64_t ldy[kMaxBnGroups], lddy[kMaxBnGroups];
+  int C[kMaxBnGroups], tpr[kMaxBnGroups], nrb[kMaxBnGroups];
   const float* part[kMaxBnGroups];
   float* wpart[kMaxBnGroups];
   const float* gamma[kMaxBnGroups];
@@ -149,8 +154,8 @@ struct BnGroups {
   float* dbeta[kMaxBnGroups];
 };
 int bn_group_bwd_rows(int64_t M, const int* C, int n);
-void launch_bn_group_fwd(BnGroups G, void* out, int64_t ldo, int64_t M, hipStream_t stream);
-void launch_bn_group_bwd(BnGroups G, const void* dout, int64_t ldo, int64_t M, hipStream_t stream);
+void launch_bn_group_fwd(BnGroups G, int64_t M, hipStream_t stream);
+void launch_bn_group_bwd(BnGroups G, bool ext, int64_t M, hipStream_t stream);
 
 // Stem BN(+ReLU)+max-pool fused (bn_act.hip): launch_bn_fwd with y == nullptr computes ws only;
 // then the pooled output + window positions come straight from the BN input x. Backward: the BN

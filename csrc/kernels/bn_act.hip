@@ -1301,17 +1301,15 @@ __global__ __launch_bounds__(256) void bn_group_stats_finalize_kernel(BnGroups G
                             G.beta[g], G.eps[g], G.mom[g], G.rm[g], G.rv[g], G.ws[g]);
 }
 
-__global__ __launch_bounds__(kBNThreads) void bn_group_apply_kernel(BnGroups G, bf16_t* __restrict__ out, int64_t ldo,
-                                                                    int64_t M, int nrb) {
+__global__ __launch_bounds__(kBNThreads) void bn_group_apply_kernel(BnGroups G, int64_t M, int nrb) {
   const int g = bn_group_of(G, blockIdx.x);
-  bn_apply_body<bf16_t, false, true, false>(blockIdx.x - G.begin[g], G.x[g], nullptr, out + G.off[g], G.ws[g], M,
-                                            G.C[g], nrb, G.tpr[g], nullptr, nullptr, ldo);
+  bn_apply_body<bf16_t, false, true, false>(blockIdx.x - G.begin[g], G.x[g], nullptr, G.y[g], G.ws[g], M, G.C[g],
+                                            nrb, G.tpr[g], nullptr, nullptr, G.ldy[g]);
 }
 
-__global__ __launch_bounds__(kBNThreads) void bn_group_bwd_reduce_kernel(BnGroups G, const bf16_t* __restrict__ dout,
-                                                                         int64_t ldo, int64_t M, int nrb) {
+__global__ __launch_bounds__(kBNThreads) void bn_group_bwd_reduce_kernel(BnGroups G, int64_t M, int nrb) {
   const int g = bn_group_of(G, blockIdx.x);
-  bn_bwd_reduce_body<bf16_t, kMaskRecomp, DirectDy<bf16_t>>(blockIdx.x - G.begin[g], DirectDy<bf16_t>{dout + G.off[g], ldo},
+  bn_bwd_reduce_body<bf16_t, kMaskRecomp, DirectDy<bf16_t>>(blockIdx.x - G.begin[g], DirectDy<bf16_t>{G.dy[g], G.lddy[g]},
                                                             nullptr, nullptr, G.x[g], G.ws[g], M, G.C[g], nrb,
                                                             G.tpr[g], G.wpart[g]);
 }
@@ -1322,11 +1320,10 @@ __global__ __launch_bounds__(256) void bn_group_bwd_finalize_kernel(BnGroups G, 
                           G.dbeta[g]);
 }
 
-__global__ __launch_bounds__(kBNThreads) void bn_group_bwd_apply_kernel(BnGroups G, const bf16_t* __restrict__ dout,
-                                                                        int64_t ldo, int64_t M, int nrb) {
+__global__ __launch_bounds__(kBNThreads) void bn_group_bwd_apply_kernel(BnGroups G, int64_t M, int nrb) {
   const int g = bn_group_of(G, blockIdx.x);
   bn_bwd_apply_body<bf16_t, kMaskRecomp, false, DirectDy<bf16_t>>(blockIdx.x - G.begin[g],
-                                                                  DirectDy<bf16_t>{dout + G.off[g], ldo}, nullptr,
+                                                                  DirectDy<bf16_t>{G.dy[g], G.lddy[g]}, nullptr,
                                                                   nullptr, G.x[g], G.ws[g], G.dx[g], nullptr, M, G.C[g],
                                                                   nrb, G.tpr[g]);
 }
@@ -1366,8 +1363,8 @@ int bn_group_bwd_rows(int64_t M, const int* C, int n) {
   return bn_group_tiles(G, M, bn_red_blocks() > 1024 ? 1024 : bn_red_blocks());
 }
 
-void launch_bn_group_fwd(BnGroups G, void* out, int64_t ldo, int64_t M, hipStream_t stream) {
-  // epilogue partials of many row tiles: fold each group's rows first (into its wpart scratch)
+// epilogue partials of many row tiles: fold each group's rows first (into its wpart scratch)
+static void bn_group_fold(BnGroups& G, hipStream_t stream) {
   for (int g = 0; g < G.n; ++g) {
     if (const int fg = bn_fold_groups(G.nrb[g])) {
       hipLaunchKernelGGL(bn_partials_fold_kernel, dim3((G.C[g] + 63) / 64, fg), dim3(256), 0, stream, G.part[g],
@@ -1376,27 +1373,32 @@ void launch_bn_group_fwd(BnGroups G, void* out, int64_t ldo, int64_t M, hipStrea
       G.nrb[g] = fg;
     }
   }
+}
+
+void launch_bn_group_fwd(BnGroups G, int64_t M, hipStream_t stream) {
+  bn_group_fold(G, stream);
   bn_group_finalize_blocks(G);
   hipLaunchKernelGGL(bn_group_stats_finalize_kernel, dim3(G.begin[G.n]), dim3(256), 0, stream, G, M);
   const int nrb = bn_group_tiles(G, M, 4096);
-  hipLaunchKernelGGL(bn_group_apply_kernel, dim3(G.begin[G.n], nrb), dim3(kBNThreads), 0, stream, G, (bf16_t*)out,
-                     ldo, M, nrb);
+  hipLaunchKernelGGL(bn_group_apply_kernel, dim3(G.begin[G.n], nrb), dim3(kBNThreads), 0, stream, G, M, nrb);
 }
 
-void launch_bn_group_bwd(BnGroups G, const void* dout, int64_t ldo, int64_t M, hipStream_t stream) {
-  const int nrb = bn_group_tiles(G, M, bn_red_blocks() > 1024 ? 1024 : bn_red_blocks());
-  const size_t lds = (size_t)kBNThreads * 8 * 2 * sizeof(float);  // rpi * ct * 2 floats for any tpr
-  hipLaunchKernelGGL(bn_group_bwd_reduce_kernel, dim3(G.begin[G.n], nrb), dim3(kBNThreads), lds, stream, G,
-                     (const bf16_t*)dout, ldo, M, nrb);
-  for (int g = 0; g < G.n; ++g) {
-    G.part[g] = G.wpart[g];
-    G.nrb[g] = nrb;
+void launch_bn_group_bwd(BnGroups G, bool ext, int64_t M, hipStream_t stream) {
+  if (ext) {
+    bn_group_fold(G, stream);  // the dgrad epilogues' partials: one row per 128-row output tile
+  } else {
+    const int nrb = bn_group_tiles(G, M, bn_red_blocks() > 1024 ? 1024 : bn_red_blocks());
+    const size_t lds = (size_t)kBNThreads * 8 * 2 * sizeof(float);  // rpi * ct * 2 floats for any tpr
+    hipLaunchKernelGGL(bn_group_bwd_reduce_kernel, dim3(G.begin[G.n], nrb), dim3(kBNThreads), lds, stream, G, M, nrb);
+    for (int g = 0; g < G.n; ++g) {
+      G.part[g] = G.wpart[g];
+      G.nrb[g] = nrb;
+    }
   }
   bn_group_finalize_blocks(G);
   hipLaunchKernelGGL(bn_group_bwd_finalize_kernel, dim3(G.begin[G.n]), dim3(256), 0, stream, G, M);
   const int anrb = bn_group_tiles(G, M, 4096);
-  hipLaunchKernelGGL(bn_group_bwd_apply_kernel, dim3(G.begin[G.n], anrb), dim3(kBNThreads), 0, stream, G,
-                     (const bf16_t*)dout, ldo, M, anrb);
+  hipLaunchKernelGGL(bn_group_bwd_apply_kernel, dim3(G.begin[G.n], anrb), dim3(kBNThreads), 0, stream, G, M, anrb);
 }
 
 }  // namespace dla

@@ -279,54 +279,54 @@ static const void* addend2_ptr(const c10::optional<at::Tensor>& a2, int64_t M, i
   return a2->data_ptr();
 }
 
-// Grouped training BN+ReLU of an Inception block's branches (launch_bn_group_fwd): each y_g, with
-// its conv epilogue's statistics, normalised into channels [off_g, off_g + C_g) of out (the
-// concatenated NHWC block output). Returns the per-branch 7C workspaces.
+// Grouped training BN+ReLU (launch_bn_group_fwd / _bwd): the BatchNorms of an Inception block's
+// branches, one launch per pass. bn_concat_*: outputs are channel slices of the concatenated NHWC
+// block output (dy read in place from its gradient); bn_group_*: each output its own tensor.
 static void check_bn_param(const at::Tensor& t, int64_t C, const char* what) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == C, what,
               " must be a contiguous fp32 GPU vector of C elements");
 }
 
-std::vector<at::Tensor> bn_concat_fwd(std::vector<at::Tensor> ys, std::vector<at::Tensor> gammas,
-                                      std::vector<at::Tensor> betas, std::vector<at::Tensor> rms,
-                                      std::vector<at::Tensor> rvs, std::vector<double> moms, std::vector<double> epss,
-                                      std::vector<at::Tensor> stats, at::Tensor out) {
+static void check_branch(const at::Tensor& y, const at::Tensor& ref, const char* what) {
+  check_act(y, what);
+  TORCH_CHECK(y.dim() == 4 && y.scalar_type() == at::kBFloat16 && y.size(0) == ref.size(0) &&
+                  y.size(2) == ref.size(2) && y.size(3) == ref.size(3),
+              what, ": every branch must be bf16 [N, C, H, W] channels_last with the same N, H, W");
+}
+
+// forward fields shared by both variants; returns the workspaces (keep: scratch kept alive)
+static std::vector<at::Tensor> group_fwd_fields(BnGroups& G, const std::vector<at::Tensor>& ys,
+                                                const std::vector<at::Tensor>& gammas,
+                                                const std::vector<at::Tensor>& betas, const std::vector<at::Tensor>& rms,
+                                                const std::vector<at::Tensor>& rvs, const std::vector<double>& moms,
+                                                const std::vector<double>& epss, const std::vector<at::Tensor>& stats,
+                                                std::vector<at::Tensor>& keep) {
   const int n = (int)ys.size();
   TORCH_CHECK(n >= 1 && n <= kMaxBnGroups && (int)gammas.size() == n && (int)betas.size() == n &&
                   (int)rms.size() == n && (int)rvs.size() == n && (int)moms.size() == n && (int)epss.size() == n &&
                   (int)stats.size() == n,
-              "bn_concat_fwd: 1..4 branches, one entry per branch in every list");
-  check_act(out, "out");
-  TORCH_CHECK(out.dim() == 4 && out.scalar_type() == at::kBFloat16, "bn_concat_fwd: out must be bf16 [N, Ctot, H, W]");
-  const int64_t M = rows_of(out);
-  auto f32 = out.options().dtype(at::kFloat);
-  BnGroups G{};
+              "grouped BN: 1..4 branches, one entry per branch in every list");
   G.n = n;
-  std::vector<at::Tensor> wss, keep;
-  int off = 0;
+  std::vector<at::Tensor> wss;
   for (int g = 0; g < n; ++g) {
-    const at::Tensor& y = ys[g];
-    check_act(y, "y");
-    TORCH_CHECK(y.dim() == 4 && y.scalar_type() == at::kBFloat16 && y.size(0) == out.size(0) &&
-                    y.size(2) == out.size(2) && y.size(3) == out.size(3),
-                "bn_concat_fwd: every branch must be bf16 with out's batch and spatial size");
-    const int C = (int)y.size(1);
+    check_branch(ys[g], ys[0], "y");
+    const int C = (int)ys[g].size(1);
     const at::Tensor& st = stats[g];
     TORCH_CHECK(st.is_cuda() && st.scalar_type() == at::kFloat && st.is_contiguous() && st.dim() == 3 &&
                     st.size(1) == C && st.size(2) == 2,
-                "bn_concat_fwd: stats must be fp32 [row_blocks, C, 2] epilogue partials");
+                "grouped BN: stats must be fp32 [row_blocks, C, 2] epilogue partials");
     check_bn_param(gammas[g], C, "weight");
     check_bn_param(betas[g], C, "bias");
     check_bn_param(rms[g], C, "running_mean");
     check_bn_param(rvs[g], C, "running_var");
+    auto f32 = ys[g].options().dtype(at::kFloat);
     at::Tensor ws = at::empty({7 * (int64_t)C}, f32);
-    at::Tensor fold = at::empty({std::max<int64_t>(1, (int64_t)bn_fold_groups((int)st.size(0)) * C * 2)}, f32);
-    G.x[g] = (const uint16_t*)y.data_ptr();
+    keep.push_back(at::empty({std::max<int64_t>(1, (int64_t)bn_fold_groups((int)st.size(0)) * C * 2)}, f32));
+    G.x[g] = (const uint16_t*)ys[g].data_ptr();
     G.C[g] = C;
-    G.off[g] = off;
     G.nrb[g] = (int)st.size(0);
     G.part[g] = st.data_ptr<float>();
-    G.wpart[g] = fold.data_ptr<float>();
+    G.wpart[g] = keep.back().data_ptr<float>();
     G.gamma[g] = gammas[g].data_ptr<float>();
     G.beta[g] = betas[g].data_ptr<float>();
     G.rm[g] = rms[g].data_ptr<float>();
@@ -335,44 +335,71 @@ std::vector<at::Tensor> bn_concat_fwd(std::vector<at::Tensor> ys, std::vector<at
     G.eps[g] = (float)epss[g];
     G.mom[g] = (float)moms[g];
     wss.push_back(ws);
-    keep.push_back(fold);
-    off += C;
   }
-  TORCH_CHECK(off == out.size(1), "bn_concat_fwd: branch channels must add up to out's channels");
-  if (M > 0) launch_bn_group_fwd(G, out.data_ptr(), out.size(1), M, current_stream(out));
   return wss;
 }
 
-// Backward of bn_concat_fwd: dy of branch g read in place from channels [off_g, off_g + C_g) of
-// dout; returns [dx_0, dgamma_0, dbeta_0, dx_1, ...].
-std::vector<at::Tensor> bn_concat_bwd(at::Tensor dout, std::vector<at::Tensor> ys, std::vector<at::Tensor> gammas,
-                                      std::vector<at::Tensor> wss) {
+// into channels [off_g, off_g + C_g) of out (the concatenated block output); returns the workspaces
+std::vector<at::Tensor> bn_concat_fwd(std::vector<at::Tensor> ys, std::vector<at::Tensor> gammas,
+                                      std::vector<at::Tensor> betas, std::vector<at::Tensor> rms,
+                                      std::vector<at::Tensor> rvs, std::vector<double> moms, std::vector<double> epss,
+                                      std::vector<at::Tensor> stats, at::Tensor out) {
+  check_act(out, "out");
+  TORCH_CHECK(out.dim() == 4 && out.scalar_type() == at::kBFloat16, "bn_concat_fwd: out must be bf16 [N, Ctot, H, W]");
+  BnGroups G{};
+  std::vector<at::Tensor> keep;
+  auto wss = group_fwd_fields(G, ys, gammas, betas, rms, rvs, moms, epss, stats, keep);
+  int64_t off = 0;
+  for (int g = 0; g < G.n; ++g) {
+    check_branch(ys[g], out, "y");
+    G.y[g] = (uint16_t*)out.data_ptr() + off;
+    G.ldy[g] = out.size(1);
+    off += G.C[g];
+  }
+  TORCH_CHECK(off == out.size(1), "bn_concat_fwd: branch channels must add up to out's channels");
+  const int64_t M = rows_of(out);
+  if (M > 0) launch_bn_group_fwd(G, M, current_stream(out));
+  return wss;
+}
+
+// each branch into its own tensor; returns [a_0 .. a_{n-1}, ws_0 .. ws_{n-1}]
+std::vector<at::Tensor> bn_group_fwd(std::vector<at::Tensor> ys, std::vector<at::Tensor> gammas,
+                                     std::vector<at::Tensor> betas, std::vector<at::Tensor> rms,
+                                     std::vector<at::Tensor> rvs, std::vector<double> moms, std::vector<double> epss,
+                                     std::vector<at::Tensor> stats) {
+  BnGroups G{};
+  std::vector<at::Tensor> keep;
+  auto wss = group_fwd_fields(G, ys, gammas, betas, rms, rvs, moms, epss, stats, keep);
+  std::vector<at::Tensor> res;
+  for (int g = 0; g < G.n; ++g) {
+    res.push_back(at::empty_like(ys[g]));
+    G.y[g] = (uint16_t*)res.back().data_ptr();
+    G.ldy[g] = 0;
+  }
+  const int64_t M = rows_of(ys[0]);
+  if (M > 0) launch_bn_group_fwd(G, M, current_stream(ys[0]));
+  res.insert(res.end(), wss.begin(), wss.end());
+  return res;
+}
+
+// backward fields shared by both variants; returns [dx_0, dgamma_0, dbeta_0, dx_1, ...]
+static std::vector<at::Tensor> group_bwd_fields(BnGroups& G, const std::vector<at::Tensor>& ys,
+                                                const std::vector<at::Tensor>& gammas,
+                                                const std::vector<at::Tensor>& wss) {
   const int n = (int)ys.size();
   TORCH_CHECK(n >= 1 && n <= kMaxBnGroups && (int)gammas.size() == n && (int)wss.size() == n,
-              "bn_concat_bwd: 1..4 branches, one entry per branch in every list");
-  check_act(dout, "dout");
-  TORCH_CHECK(dout.dim() == 4 && dout.scalar_type() == at::kBFloat16, "bn_concat_bwd: dout must be bf16 [N, Ctot, H, W]");
-  const int64_t M = rows_of(dout);
-  auto f32 = dout.options().dtype(at::kFloat);
-  BnGroups G{};
+              "grouped BN backward: 1..4 branches, one entry per branch in every list");
   G.n = n;
-  int Cs[kMaxBnGroups];
   std::vector<at::Tensor> res;
-  int off = 0;
   for (int g = 0; g < n; ++g) {
-    const at::Tensor& y = ys[g];
-    check_act(y, "y");
-    TORCH_CHECK(y.dim() == 4 && y.scalar_type() == at::kBFloat16 && y.size(0) == dout.size(0) &&
-                    y.size(2) == dout.size(2) && y.size(3) == dout.size(3),
-                "bn_concat_bwd: every branch must be bf16 with dout's batch and spatial size");
-    const int C = (int)y.size(1);
+    check_branch(ys[g], ys[0], "y");
+    const int C = (int)ys[g].size(1);
     check_bn_param(gammas[g], C, "weight");
     TORCH_CHECK(wss[g].scalar_type() == at::kFloat && wss[g].numel() == 7 * (int64_t)C, "ws must be the 7C workspace");
-    Cs[g] = C;
-    at::Tensor dx = at::empty_like(y), dg = at::empty({C}, f32), db = at::empty({C}, f32);
-    G.x[g] = (const uint16_t*)y.data_ptr();
+    auto f32 = ys[g].options().dtype(at::kFloat);
+    at::Tensor dx = at::empty_like(ys[g]), dg = at::empty({C}, f32), db = at::empty({C}, f32);
+    G.x[g] = (const uint16_t*)ys[g].data_ptr();
     G.C[g] = C;
-    G.off[g] = off;
     G.gamma[g] = gammas[g].data_ptr<float>();
     G.ws[g] = wss[g].data_ptr<float>();
     G.dx[g] = (uint16_t*)dx.data_ptr();
@@ -381,16 +408,72 @@ std::vector<at::Tensor> bn_concat_bwd(at::Tensor dout, std::vector<at::Tensor> y
     res.push_back(dx);
     res.push_back(dg);
     res.push_back(db);
-    off += C;
   }
-  TORCH_CHECK(off == dout.size(1), "bn_concat_bwd: branch channels must add up to dout's channels");
-  const int rows = bn_group_bwd_rows(M, Cs, n);
-  std::vector<at::Tensor> keep;
-  for (int g = 0; g < n; ++g) {
-    keep.push_back(at::empty({(int64_t)rows * Cs[g] * 2}, f32));
+  return res;
+}
+
+static void group_reduce_scratch(BnGroups& G, int64_t M, std::vector<at::Tensor>& keep, const at::Tensor& like) {
+  int Cs[kMaxBnGroups];
+  for (int g = 0; g < G.n; ++g) Cs[g] = G.C[g];
+  const int rows = bn_group_bwd_rows(M, Cs, G.n);
+  for (int g = 0; g < G.n; ++g) {
+    keep.push_back(at::empty({(int64_t)rows * G.C[g] * 2}, like.options().dtype(at::kFloat)));
     G.wpart[g] = keep.back().data_ptr<float>();
   }
-  if (M > 0) launch_bn_group_bwd(G, dout.data_ptr(), dout.size(1), M, current_stream(dout));
+}
+
+// dy of branch g read in place from channels [off_g, off_g + C_g) of dout
+std::vector<at::Tensor> bn_concat_bwd(at::Tensor dout, std::vector<at::Tensor> ys, std::vector<at::Tensor> gammas,
+                                      std::vector<at::Tensor> wss) {
+  check_act(dout, "dout");
+  TORCH_CHECK(dout.dim() == 4 && dout.scalar_type() == at::kBFloat16, "bn_concat_bwd: dout must be bf16 [N, Ctot, H, W]");
+  BnGroups G{};
+  auto res = group_bwd_fields(G, ys, gammas, wss);
+  int64_t off = 0;
+  for (int g = 0; g < G.n; ++g) {
+    check_branch(ys[g], dout, "y");
+    G.dy[g] = (const uint16_t*)dout.data_ptr() + off;
+    G.lddy[g] = dout.size(1);
+    off += G.C[g];
+  }
+  TORCH_CHECK(off == dout.size(1), "bn_concat_bwd: branch channels must add up to dout's channels");
+  const int64_t M = rows_of(dout);
+  std::vector<at::Tensor> keep;
+  group_reduce_scratch(G, M, keep, dout);
+  if (M > 0) launch_bn_group_bwd(G, false, M, current_stream(dout));
+  return res;
+}
+
+// dys: one gradient per branch; exts: the consumer dgrad epilogues' reduction partials for every
+// branch, or empty (then a grouped reduce pass runs)
+std::vector<at::Tensor> bn_group_bwd(std::vector<at::Tensor> dys, std::vector<at::Tensor> ys,
+                                     std::vector<at::Tensor> gammas, std::vector<at::Tensor> wss,
+                                     std::vector<at::Tensor> exts) {
+  BnGroups G{};
+  auto res = group_bwd_fields(G, ys, gammas, wss);
+  TORCH_CHECK((int)dys.size() == G.n && (exts.empty() || (int)exts.size() == G.n),
+              "bn_group_bwd: one dy (and optionally one partials tensor) per branch");
+  std::vector<at::Tensor> keep;
+  for (int g = 0; g < G.n; ++g) {
+    check_act(dys[g], "dy");
+    TORCH_CHECK(dys[g].sizes() == ys[g].sizes() && dys[g].scalar_type() == at::kBFloat16, "bn_group_bwd: dy must match y");
+    G.dy[g] = (const uint16_t*)dys[g].data_ptr();
+    G.lddy[g] = 0;
+    if (!exts.empty()) {
+      const at::Tensor& e = exts[g];
+      TORCH_CHECK(e.is_cuda() && e.scalar_type() == at::kFloat && e.is_contiguous() && e.dim() == 3 &&
+                      e.size(1) == G.C[g] && e.size(2) == 2,
+                  "bn_group_bwd: partials must be fp32 [rows, C, 2]");
+      G.part[g] = e.data_ptr<float>();
+      G.nrb[g] = (int)e.size(0);
+      keep.push_back(at::empty({std::max<int64_t>(1, (int64_t)bn_fold_groups((int)e.size(0)) * G.C[g] * 2)},
+                               e.options()));
+      G.wpart[g] = keep.back().data_ptr<float>();
+    }
+  }
+  const int64_t M = rows_of(ys[0]);
+  if (exts.empty()) group_reduce_scratch(G, M, keep, ys[0]);
+  if (M > 0) launch_bn_group_bwd(G, !exts.empty(), M, current_stream(ys[0]));
   return res;
 }
 
@@ -815,6 +898,8 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("out_channel") = 0);
   m.def("bn_concat_fwd", &bn_concat_fwd, "grouped training BN+ReLU of concatenated branches into one NHWC output");
   m.def("bn_concat_bwd", &bn_concat_bwd, "backward of bn_concat_fwd (dy slices read in place)");
+  m.def("bn_group_fwd", &bn_group_fwd, "grouped training BN+ReLU of same-size tensors, one output each");
+  m.def("bn_group_bwd", &bn_group_bwd, "backward of bn_group_fwd (optionally from dgrad-epilogue partials)");
   m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC", pybind11::arg("dy"),
         pybind11::arg("y"), pybind11::arg("mask"), pybind11::arg("x"), pybind11::arg("ws"), pybind11::arg("weight"),
         pybind11::arg("mask_mode"), pybind11::arg("need_dres"), pybind11::arg("ext_part") = pybind11::none());

@@ -139,6 +139,43 @@ class _BNReluConcat(torch.autograd.Function):
         return tuple(grads)
 
 
+class _BNReluGroup(torch.autograd.Function):
+    """act(BN_b(y_b)) for same-size tensors that each keep their own output (the 1x1 reductions of
+    branches 2 and 3), one launch per pass. Each output carries a BNLink, so the 3x3 conv consuming
+    it still produces this BN's backward partials in its dgrad epilogue; with all of them present
+    the grouped backward is one finalize + one apply launch."""
+
+    @staticmethod
+    def forward(ctx, metas, *tensors):
+        from .bn_act import BNLink, MASK_RECOMPUTE
+
+        C = _ext.require()
+        ys, gs, bs = tensors[0::3], tensors[1::3], tensors[2::3]
+        n = len(ys)
+        res = C.bn_group_fwd(list(ys), list(gs), list(bs), [m[0] for m in metas], [m[1] for m in metas],
+                             [m[2] for m in metas], [m[3] for m in metas], [m[4] for m in metas])
+        outs, wss = res[:n], res[n:]
+        ctx.save_for_backward(*ys, *gs, *wss)
+        ctx.nb = n
+        ctx.links = [BNLink(y, ws, None, MASK_RECOMPUTE) for y, ws in zip(ys, wss)]
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        C = _ext.require()
+        nb = ctx.nb
+        saved = ctx.saved_tensors
+        ys, gs, wss = saved[:nb], saved[nb:2 * nb], saved[2 * nb:]
+        dys = []
+        for d, y in zip(douts, ys):
+            d = d.contiguous(memory_format=CL)
+            dys.append(d if d.dtype == y.dtype else d.to(y.dtype))
+        exts = [link.take(d) for link, d in zip(ctx.links, dys)]
+        if any(e is None for e in exts):
+            exts = []
+        return (None, *C.bn_group_bwd(dys, list(ys), list(gs), list(wss), exts))
+
+
 # DLA_BN_GROUPED=0 keeps one BN launch chain per branch (A/B runs)
 _GROUPED = os.environ.get("DLA_BN_GROUPED", "1") != "0"
 
@@ -193,8 +230,22 @@ def inception_forward(block, x: torch.Tensor) -> torch.Tensor:
         x, block.branch1.conv.weight, block.branch2[0].conv.weight, block.branch3[0].conv.weight, k, s, p,
         bool(pool.ceil_mode))
     outs = [(y1, block.branch1.bn, s1)]
-    for red, stats, conv_bn in ((y2r, s2r, block.branch2), (y3r, s3r, block.branch3)):
-        a = bn_act.fused_bn_act(red, conv_bn[0].bn, True, None, stats)
+    reds = ((y2r, s2r, block.branch2), (y3r, s3r, block.branch3))
+    rbns = [cb[0].bn for _, _, cb in reds]
+    rmetas = tuple((bn.running_mean, bn.running_var, float(bn.momentum), float(bn.eps), st)
+                   for bn, (_, st, _) in zip(rbns, reds))
+    rys = [r.contiguous(memory_format=CL) for r, _, _ in reds]
+    if _grouped_ok(rys, [bn.weight for bn in rbns], [bn.bias for bn in rbns], rmetas):
+        rt = []
+        for y, bn in zip(rys, rbns):
+            rt += [y, bn.weight, bn.bias]
+            bn_act._PENDING_COUNTERS.append(bn.num_batches_tracked)
+        acts = _BNReluGroup.apply(rmetas, *rt)
+        for i, a in enumerate(acts):
+            a._dla_bn = a.grad_fn.links[i]
+    else:
+        acts = [bn_act.fused_bn_act(red, bn, True, None, stats) for (red, stats, _), bn in zip(reds, rbns)]
+    for a, (_, _, conv_bn) in zip(acts, reds):
         c = conv_bn[1].conv
         if supported3x3(a, c):
             y, st = conv3x3(a, c, want_stats=True)

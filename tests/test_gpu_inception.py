@@ -85,6 +85,53 @@ def test_bn_concat_matches_per_branch(cuda, shape):
         off += c
 
 
+@pytest.mark.parametrize("shape", [(4, 7, 9), (35, 80, 50)])
+def test_bn_group_separate_outputs_with_epilogue_partials(cuda, shape):
+    """bn_group_fwd / bn_group_bwd (the two reduction-branch BNs) == per-branch bn_act_fwd / bn_act_bwd,
+    with the backward's reduction partials coming from the consumer GEMM's dgrad epilogue."""
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    torch.manual_seed(1)
+    n, h, w = shape
+    chans = [96, 16]
+    ys, sts, gs, bs, rms, rvs = [], [], [], [], [], []
+    for c in chans:
+        a = torch.randn(n * h * w, 32, device=cuda).to(torch.bfloat16)
+        wt = torch.randn(c, 32, device=cuda).to(torch.bfloat16)
+        y2, st = C.gemm_nt(a, wt, True)
+        ys.append(y2.view(n, h, w, c).permute(0, 3, 1, 2))
+        sts.append(st)
+        gs.append(torch.rand(c, device=cuda) + 0.5)
+        bs.append(torch.randn(c, device=cuda))
+        rms.append(torch.zeros(c, device=cuda))
+        rvs.append(torch.ones(c, device=cuda))
+    res = C.bn_group_fwd(ys, gs, bs, [t.clone() for t in rms], [t.clone() for t in rvs], [0.1] * 2, [1e-3] * 2, sts)
+    outs, wss = res[:2], res[2:]
+    for i in range(2):
+        y_r, ws_r, _ = C.bn_act_fwd(ys[i], None, gs[i], bs[i], rms[i].clone(), rvs[i].clone(), True, 0.1, 1e-3, True,
+                                    sts[i])
+        assert torch.equal(outs[i], y_r) and outs[i].is_contiguous(memory_format=CL)
+        assert torch.equal(wss[i][:4 * chans[i]], ws_r[:4 * chans[i]])
+    # each BN's dy comes from a consumer GEMM (dgrad of a 1x1 conv) whose epilogue also emits the
+    # BN backward partials (mode 1: ReLU recomputed from the BN input)
+    dys, parts = [], []
+    for i, c in enumerate(chans):
+        g2 = torch.randn(n * h * w, 64, device=cuda).to(torch.bfloat16)
+        wk = torch.randn(64, c, device=cuda).to(torch.bfloat16)
+        dy2, part = C.gemm_nt_bn(g2, wk, None, True, ys[i].permute(0, 2, 3, 1).reshape(-1, c), wss[i], None, 1,
+                                 None, None, 0, 0)
+        dys.append(dy2.view(n, h, w, c).permute(0, 3, 1, 2))
+        parts.append(part)
+    for exts in (parts, []):
+        got = C.bn_group_bwd(dys, ys, gs, [ws.clone() for ws in wss], exts)
+        for i in range(2):
+            dx, _, dg, db = C.bn_act_bwd(dys[i], None, None, ys[i], wss[i].clone(), gs[i], 1, False,
+                                         parts[i] if exts else None)
+            gdx, gdg, gdb = got[3 * i:3 * i + 3]
+            assert _rel(gdx, dx) < 1e-2 and _rel(gdg, dg) < 1e-4 and _rel(gdb, db) < 1e-4, (i, len(exts))
+
+
 def _block():
     from distributed_learning_amd.models.googlenet import Inception
     from distributed_learning_amd.ops import nn as dnn
