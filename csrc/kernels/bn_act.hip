@@ -31,30 +31,6 @@ constexpr int kRedBlocks = 1024;
 // Rows per thread per streaming-loop iteration (loads of a group issued back to back).
 constexpr int kUnroll = 4;
 
-// 8 consecutive channels as loaded (bf16: one 16-byte register quad; fp32: two), widened on use. The
-// streaming loops below load a whole group of rows into these before touching any of them, so the
-// group's loads are in flight together (hipcc does not hoist them across the per-row arithmetic).
-template <typename T> struct Raw8;
-template <> struct Raw8<bf16_t> {
-  ushort8_t v;
-  __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const ushort8_t*>(p); }
-  __device__ __forceinline__ void get(float (&f)[8]) const {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = bf16_to_f32(v[j]);
-  }
-};
-template <> struct Raw8<float> {
-  float4_t a, b;
-  __device__ __forceinline__ void load(const float* p) {
-    a = reinterpret_cast<const float4_t*>(p)[0];
-    b = reinterpret_cast<const float4_t*>(p)[1];
-  }
-  __device__ __forceinline__ void get(float (&f)[8]) const {
-    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
-  }
-};
-
-
 // Block geometry shared by the two reduction passes: the block covers CT = tpr*8 channels
 // (channel tile blockIdx.x) and rows [r0, r1) (row block blockIdx.y); rpi = 256/tpr rows are in
 // flight per iteration, each row segment of a wave-instruction is a contiguous 16*tpr bytes.

@@ -15,6 +15,7 @@
 #include "dla_mfma.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace dla {
 
@@ -90,9 +91,17 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_kernel(const T* __re
           const int hc = min(max(h, 0), g.H - 1), wc = min(max(w, 0), g.W - 1);
           Vec8<T>::load(img + ((int64_t)hc * g.W + wc) * g.C, v[q]);
         }
+      // branch-free: an out-of-range tap becomes -inf, which never wins a strict '>' (as skipping it)
 #pragma unroll
-      for (int q = 0; q < K * K; ++q)
-        if (ok[q]) take(v[q], (uint32_t)q);
+      for (int q = 0; q < K * K; ++q) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float vq = ok[q] ? v[q][j] : -INFINITY;
+          const bool t = !(vq <= best[j]) & (best[j] == best[j]);  // vq > best, or vq NaN and best not
+          best[j] = t ? vq : best[j];
+          bi[j] = t ? (uint32_t)q : bi[j];
+        }
+      }
     } else {
       for (int ky = 0; ky < g.k; ++ky) {
         const int h = h0 + ky;
@@ -113,6 +122,97 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_kernel(const T* __re
 #pragma unroll
       for (int j = 0; j < 8; ++j) packed |= (uint64_t)bi[j] << (8 * j);
       *reinterpret_cast<uint64_t*>(pos + off) = packed;
+    }
+  }
+}
+
+// 3x3 / stride-1 forward (GoogLeNet's Inception branch-4 pools), separable: a thread owns a strip
+// of kStrip3 output rows at one column and 8 channels. It loads the kStrip3 + 2 input rows x 3
+// columns once (27 loads for 7 outputs instead of 63), takes each input row's maximum over its 3
+// columns (value + column), then each output's maximum over 3 of those row maxima. The per-tap
+// compare-and-select work drops from 8 to 2 + 2 per output row shared 3 ways — the generic kernel
+// is VALU-bound here (718 VALU instructions per wave, profiles/r3t).
+// Same result as the row-major scan: strict '>' in both passes picks the first maximum in
+// (ky, kx) order, and a NaN wins and sticks in both passes, so the first NaN in that order wins.
+template <typename T, int RV, bool kFast>
+__global__ __launch_bounds__(kPoolThreads) void maxpool3s1_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                                      uint8_t* __restrict__ pos, PoolGeom g,
+                                                                      int nstrip) {
+  const int total = g.N * nstrip * g.OW * (g.C / 8);  // < 2^31 (host-checked)
+  for (int t = blockIdx.x * kPoolThreads + threadIdx.x; t < total; t += gridDim.x * kPoolThreads) {
+    int n, st, ow, c;
+    decode<kFast>(t, g, g.OW, nstrip, n, st, ow, c);
+    const int oh0 = st * RV;
+    const T* img = x + (int64_t)n * g.H * g.W * g.C + c;
+    int wc[3];
+    bool okc[3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int w = ow - g.p + kx;
+      okc[kx] = (unsigned)w < (unsigned)g.W;
+      wc[kx] = min(max(w, 0), g.W - 1);
+    }
+    // Branch-free: a tap outside the image reads a clamped in-range pixel and is replaced by -inf,
+    // which never wins a strict '>' — the same as skipping it (a real -inf never wins either).
+    // better(v, b) = v > b, or v NaN and b not: !(v <= b) && b == b.
+    auto better = [](float v, float b) { return !(v <= b) & (b == b); };
+    float hb[RV + 2][8];     // each input row's maximum over the window's 3 columns
+    uint32_t hk[RV + 2][8];  // and its column
+#pragma unroll
+    for (int i = 0; i < RV + 2; ++i) {
+      const int h = oh0 - g.p + i;
+      const bool okr = (unsigned)h < (unsigned)g.H;
+      const int hc = min(max(h, 0), g.H - 1);
+      float v[3][8];
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        Vec8<T>::load(img + ((int64_t)hc * g.W + wc[kx]) * g.C, v[kx]);
+        const bool ok = okr && okc[kx];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[kx][j] = ok ? v[kx][j] : -INFINITY;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float b = v[0][j];  // column 0 first: the strict scan from -inf takes it unless it is -inf,
+        uint32_t k = 0;     // and then position 0 is the default anyway
+        const bool t1 = better(v[1][j], b);
+        b = t1 ? v[1][j] : b;
+        k = t1 ? 1u : k;
+        const bool t2 = better(v[2][j], b);
+        b = t2 ? v[2][j] : b;
+        k = t2 ? 2u : k;
+        hb[i][j] = b;
+        hk[i][j] = k;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RV; ++r) {
+      const int oh = oh0 + r;  // input rows r, r+1, r+2 of the strip are its window rows ky = 0, 1, 2
+      float best[8];
+      uint32_t bi[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float b = hb[r][j];
+        uint32_t k = hk[r][j];
+        const bool t1 = better(hb[r + 1][j], b);
+        b = t1 ? hb[r + 1][j] : b;
+        k = t1 ? 3u + hk[r + 1][j] : k;
+        const bool t2 = better(hb[r + 2][j], b);
+        b = t2 ? hb[r + 2][j] : b;
+        k = t2 ? 6u + hk[r + 2][j] : k;
+        best[j] = b;
+        bi[j] = k;
+      }
+      if (oh < g.OH) {
+        const int64_t off = (((int64_t)n * g.OH + oh) * g.OW + ow) * g.C + c;
+        Vec8<T>::store(y + off, best);
+        if (pos) {
+          uint64_t packed = 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) packed |= (uint64_t)bi[j] << (8 * j);
+          *reinterpret_cast<uint64_t*>(pos + off) = packed;
+        }
+      }
     }
   }
 }
@@ -154,11 +254,17 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_kernel(const T* __re
           pk[i] = *reinterpret_cast<const uint64_t*>(pos + off);
           Vec8<T>::load(dy + off, d[i]);
         }
+      // branch-free: a window outside the output matches no tap (0xff); the adds stay in (oh, ow) order
 #pragma unroll
-      for (int i = 0; i < R * R; ++i)
+      for (int i = 0; i < R * R; ++i) {
+        const uint32_t q = ok[i] ? qv[i] : 0xffu;
+        const uint32_t lo = (uint32_t)pk[i], hi = (uint32_t)(pk[i] >> 32);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (ok[i] && ((pk[i] >> (8 * j)) & 0xffu) == qv[i]) acc[j] += d[i][j];
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t byte = ((j < 4 ? lo : hi) >> (8 * (j & 3))) & 0xffu;
+          acc[j] += byte == q ? d[i][j] : 0.f;
+        }
+      }
     } else {
       for (int oh = oh_lo; oh <= oh_hi; ++oh) {
         for (int ow = ow_lo; ow <= ow_hi; ++ow) {
@@ -190,6 +296,28 @@ void launch_maxpool_fwd(const void* x, void* y, uint8_t* pos, int N, int H, int 
   const int nb = pool_blocks(work);
   if (nb == 0) return;
   const bool fast = work < (1 << 24);
+  // 3x3/s1: separable strips of 4 output rows (DLA_POOL3_SEP=0: generic kernel, 7: strips of 7; A/B)
+  static const int sep3 = [] {
+    const char* e = std::getenv("DLA_POOL3_SEP");
+    return e ? std::atoi(e) : 4;
+  }();
+  if (k == 3 && s == 1 && (sep3 == 4 || sep3 == 7)) {
+    const int nstrip = (OH + sep3 - 1) / sep3;
+    PoolGeom gs{N, H, W, C, OH, OW, k, s, p, mm::make_fastdiv(C / 8), mm::make_fastdiv(OW), mm::make_fastdiv(nstrip)};
+    const int64_t swork = (int64_t)N * nstrip * OW * (C / 8);
+    const int snb = pool_blocks(swork);
+    const bool sfast = swork < (1 << 24);
+#define DLA_MPS(T, RV, F)                                                                                         \
+  hipLaunchKernelGGL((maxpool3s1_fwd_kernel<T, RV, F>), dim3(snb), dim3(kPoolThreads), 0, stream, (const T*)x, (T*)y, \
+                     pos, gs, nstrip)
+#define DLA_MPS_RV(T, F) \
+  if (sep3 == 7) DLA_MPS(T, 7, F); else DLA_MPS(T, 4, F);
+    if (dtype == kBF16) { if (sfast) { DLA_MPS_RV(bf16_t, true) } else { DLA_MPS_RV(bf16_t, false) } }
+    else { if (sfast) { DLA_MPS_RV(float, true) } else { DLA_MPS_RV(float, false) } }
+#undef DLA_MPS_RV
+#undef DLA_MPS
+    return;
+  }
 #define DLA_MPF(T, K, F) \
   hipLaunchKernelGGL((maxpool_fwd_kernel<T, K, F>), dim3(nb), dim3(kPoolThreads), 0, stream, (const T*)x, (T*)y, pos, g)
 #define DLA_MPF_K(T)                                                      \

@@ -11,6 +11,8 @@ pytestmark = pytest.mark.gpu
     ((4, 64, 112, 112), 3, 2, 1, False),   # ResNet stem
     ((2, 64, 112, 112), 3, 2, 0, True),    # GoogLeNet maxpool1
     ((2, 480, 28, 28), 3, 1, 1, True),     # inception branch4
+    ((3, 16, 9, 7), 3, 1, 0, False),        # 3x3/s1 strips with remainders, no padding
+    ((2, 24, 1, 5), 3, 1, 1, False),
     ((2, 832, 14, 14), 2, 2, 0, True),     # GoogLeNet maxpool4
     ((3, 24, 9, 13), 3, 2, 1, False),
     ((2, 16, 11, 11), 5, 2, 2, False),     # runtime window size (generic path)
@@ -49,6 +51,37 @@ def test_maxpool_nan_propagates(cuda):
     x[0, 3, 1, 1] = float("nan")
     y, _ = _ext.require().maxpool_fwd(x, 2, 2, 0, False, True)
     assert torch.isnan(y[0, 3, 0, 0]) and not torch.isnan(y[0, 2, 0, 0])
+
+
+def _pool_reference(x, k, s, p):
+    """y and the first-maximum window position in row-major order, NaN winning (first NaN), fp32."""
+    n, c, h, w = x.shape
+    xp = F.pad(x.float(), (p, p, p, p), value=float("-inf"))
+    win = xp.unfold(2, k, s).unfold(3, k, s).reshape(n, c, (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1, k * k)
+    nan = torch.isnan(win)
+    idx = torch.where(nan.any(-1), nan.float().argmax(-1), torch.nan_to_num(win, nan=0.0).argmax(-1))
+    return torch.gather(win, -1, idx.unsqueeze(-1)).squeeze(-1), idx
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,p", [((2, 24, 10, 9), 1), ((3, 16, 7, 7), 0), ((2, 40, 15, 1), 1), ((1, 8, 29, 4), 1)])
+def test_maxpool3s1_ties_nan_inf_positions(cuda, dtype, shape, p):
+    """The separable 3x3/s1 forward: values and 1-byte argmax positions equal the row-major
+    first-maximum scan, with ties, NaNs and -inf in the windows; strips of 7 rows with remainders."""
+    from distributed_learning_amd.ops import _ext
+
+    torch.manual_seed(3)
+    x = torch.randint(0, 4, shape, device=cuda).float()
+    r = torch.rand(shape, device=cuda)
+    x[r < 0.02] = float("nan")
+    x[(r >= 0.02) & (r < 0.05)] = float("-inf")
+    x = x.to(dtype).contiguous(memory_format=torch.channels_last)
+    y, pos = _ext.require().maxpool_fwd(x, 3, 1, p, False, True)
+    yr, ir = _pool_reference(x, 3, 1, p)
+    assert y.shape == yr.shape
+    torch.testing.assert_close(y.float(), yr, rtol=0, atol=0, equal_nan=True)
+    posr = ir.permute(0, 2, 3, 1).reshape(-1).to(torch.uint8)
+    assert torch.equal(pos.permute(0, 2, 3, 1).reshape(-1).cpu(), posr.cpu())
 
 
 @pytest.mark.parametrize("shape,k,s,p,ceil", [
