@@ -944,20 +944,36 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
 // Backward: the BN reduce/apply passes gather dy from the pooled gradient (PoolDy) instead of a
 // materialised full-resolution gradient.
 // ---------------------------------------------------------------------------------------------
-template <int K>  // K > 0: compile-time window, all taps loaded before the first comparison
+// K > 0: compile-time window, all taps loaded before the first comparison.
+// kFast: the flat index is decoded with multiply-shift divisions (total < 2^24, host-checked).
+struct PoolDivs {
+  mm::FastDiv fcg, fow, foh;
+};
+
+template <int K, bool kFast>
 __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(const bf16_t* __restrict__ x,
                                                                   const float* __restrict__ ws, bf16_t* __restrict__ y,
                                                                   uint8_t* __restrict__ pos, int N, int H, int W, int C,
-                                                                  int OH, int OW, int k, int s, int p) {
+                                                                  int OH, int OW, int k, int s, int p, PoolDivs dv) {
   const int cg = C / 8;
   const int total = N * OH * OW * cg;
   for (int t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
-    const int c = (t % cg) * 8;
-    int r = t / cg;
-    const int ow = r % OW;
-    r /= OW;
-    const int oh = r % OH;
-    const int n = r / OH;
+    int c, ow, oh, n;
+    if constexpr (kFast) {
+      const int q = (int)mm::fdiv((uint32_t)t, dv.fcg);
+      c = (t - q * cg) * 8;
+      const int q2 = (int)mm::fdiv((uint32_t)q, dv.fow);
+      ow = q - q2 * OW;
+      n = (int)mm::fdiv((uint32_t)q2, dv.foh);
+      oh = q2 - n * OH;
+    } else {
+      c = (t % cg) * 8;
+      int r = t / cg;
+      ow = r % OW;
+      r /= OW;
+      oh = r % OH;
+      n = r / OH;
+    }
     float sc[8], sh[8], best[8];
     uint32_t bi[8];
 #pragma unroll
@@ -990,9 +1006,27 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(const bf16_t* 
           const int hc = min(max(h, 0), H - 1), wc = min(max(w, 0), W - 1);
           Vec8<bf16_t>::load(x + (((int64_t)n * H + hc) * W + wc) * C + c, v[q]);
         }
+      // Branch-free, in the bf16 bit domain: after the ReLU every value is >= +0 or a positive NaN
+      // (the fma's canonical NaN), whose bf16 patterns order as integers exactly like the floats,
+      // with NaN above everything; an out-of-range tap is -1, below every valid tap. A strict '>'
+      // on these keys picks the first maximum, and the first NaN, of the rounded values — what
+      // max-pooling the stored bf16 BN output gives.
+      int key[8];
 #pragma unroll
-      for (int q = 0; q < K * K; ++q)
-        if (ok[q]) take(v[q], (uint32_t)q);
+      for (int j = 0; j < 8; ++j) key[j] = -1;
+#pragma unroll
+      for (int q = 0; q < K * K; ++q) {
+        const int oor = ok[q] ? 0 : -1;  // OR-ed in: no select the compiler could turn into a branch
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int kq = (int)f32_to_bf16(fmaxf(fmaf(v[q][j], sc[j], sh[j]), 0.f)) | oor;
+          const bool tk = kq > key[j];
+          key[j] = tk ? kq : key[j];
+          bi[j] = tk ? (uint32_t)q : bi[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) best[j] = bf16_to_f32((bf16_t)key[j]);
     } else {
       for (int ky = 0; ky < k; ++ky) {
         const int h = h0 + ky;
@@ -1020,12 +1054,14 @@ void launch_bn_relu_maxpool_fwd(const void* x, const float* ws, void* y, uint8_t
   const int64_t work = (int64_t)N * OH * OW * (C / 8);
   const int nb = (int)std::min<int64_t>((work + 255) / 256, 256 * 32);
   if (nb == 0) return;
-  if (k == 3)
-    hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<3>, dim3(nb), dim3(256), 0, stream, (const bf16_t*)x, ws, (bf16_t*)y,
-                       pos, N, H, W, C, OH, OW, k, s, p);
-  else
-    hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel<0>, dim3(nb), dim3(256), 0, stream, (const bf16_t*)x, ws, (bf16_t*)y,
-                       pos, N, H, W, C, OH, OW, k, s, p);
+  const PoolDivs dv{mm::make_fastdiv(C / 8), mm::make_fastdiv(OW), mm::make_fastdiv(OH)};
+  const bool fast = work < (1 << 24);
+#define DLA_BRMP(K_, F_)                                                                                          \
+  hipLaunchKernelGGL((bn_relu_maxpool_fwd_kernel<K_, F_>), dim3(nb), dim3(256), 0, stream, (const bf16_t*)x, ws,   \
+                     (bf16_t*)y, pos, N, H, W, C, OH, OW, k, s, p, dv)
+  if (k == 3) { if (fast) DLA_BRMP(3, true); else DLA_BRMP(3, false); }
+  else { if (fast) DLA_BRMP(0, true); else DLA_BRMP(0, false); }
+#undef DLA_BRMP
 }
 
 // 3x3 / stride-2 max-pool over an even H x W (ResNet stem: pad 1; GoogLeNet stem / maxpool2: pad 0,
