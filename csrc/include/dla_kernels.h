@@ -126,7 +126,8 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
                    int ext_nrb = 0, int64_t ld_dy = 0);  // ld_dy: dy row stride when dy is a channel slice
 
 // Grouped training BN+ReLU (bn_act.hip): one launch per pass for up to kMaxBnGroups BatchNorms of
-// the same row count M — the branches of an Inception block. Group g normalises x[g] ([M, C[g]] bf16)
+// the same row count M — the branches of an Inception block. Group g normalises x[g] ([M, C[g]] bf16,
+// row stride ldx[g]; its statistics part[g] may be a channel slice of a wider partials tensor, ldp[g])
 // into y[g] (row stride ldy[g], 0 = contiguous; a channel slice of the concatenated output, or its
 // own tensor). Forward: part[g] = the [nrb][C][2] conv-epilogue statistics, wpart[g] = fold scratch
 // (bn_fold_groups(nrb) rows). Backward: dy[g] (row stride lddy[g]); with ext, part[g] already holds
@@ -140,6 +141,8 @@ struct BnGroups {
   uint16_t* y[kMaxBnGroups];
   const uint16_t* dy[kMaxBnGroups];
   int64_t ldy[kMaxBnGroups], lddy[kMaxBnGroups];
+  int64_t ldx[kMaxBnGroups], lddx[kMaxBnGroups];  // row strides of x / dx (0: contiguous [M, C])
+  int ldp[kMaxBnGroups];                          // row stride of part in channels (0: C)
   int C[kMaxBnGroups], tpr[kMaxBnGroups], nrb[kMaxBnGroups];
   const float* part[kMaxBnGroups];
   float* wpart[kMaxBnGroups];

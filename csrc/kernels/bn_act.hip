@@ -103,7 +103,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_stats_kernel(const T* __restric
 // Fixed order -> bitwise reproducible.
 template <int WPC>
 __device__ __forceinline__ bool reduce_partials(int bx, const float* __restrict__ part, int nrb, int C, float& S,
-                                                float& Q, int& c) {
+                                                float& Q, int& c, int ldp = 0) {
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   c = bx * (4 / WPC) + wave / WPC;
@@ -112,18 +112,19 @@ __device__ __forceinline__ bool reduce_partials(int bx, const float* __restrict_
   for (int u = 0; u < 8; ++u) s[u] = q[u] = 0.f;
   if (c < C) {
     const float2* p2 = reinterpret_cast<const float2*>(part);
+    const int64_t ld = ldp ? ldp : C;
     constexpr int kStride = 64 * WPC;
     int b = lane + 64 * (wave % WPC);
     for (; b + 7 * kStride < nrb; b += 8 * kStride) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const float2 v = p2[(int64_t)(b + kStride * u) * C + c];
+        const float2 v = p2[(int64_t)(b + kStride * u) * ld + c];
         s[u] += v.x;
         q[u] += v.y;
       }
     }
     for (; b < nrb; b += kStride) {
-      const float2 v = p2[(int64_t)b * C + c];
+      const float2 v = p2[(int64_t)b * ld + c];
       s[0] += v.x;
       q[0] += v.y;
     }
@@ -162,7 +163,7 @@ constexpr int kFoldRows = 128;
 int bn_fold_groups(int nrb) { return nrb > 1024 ? (nrb + kFoldRows - 1) / kFoldRows : 0; }
 
 __global__ __launch_bounds__(256) void bn_partials_fold_kernel(const float* __restrict__ part, int nrb, int C,
-                                                               float* __restrict__ out) {
+                                                               float* __restrict__ out, int ldp = 0) {
   __shared__ float red[4][64][2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
@@ -172,17 +173,18 @@ __global__ __launch_bounds__(256) void bn_partials_fold_kernel(const float* __re
   for (int u = 0; u < 8; ++u) s[u] = q[u] = 0.f;
   if (c < C) {
     const float2* p2 = reinterpret_cast<const float2*>(part);
+    const int64_t ld = ldp ? ldp : C;
     int r = r0 + wave;
     for (; r + 28 < r1; r += 32) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const float2 v = p2[(int64_t)(r + 4 * u) * C + c];
+        const float2 v = p2[(int64_t)(r + 4 * u) * ld + c];
         s[u] += v.x;
         q[u] += v.y;
       }
     }
     for (; r < r1; r += 4) {
-      const float2 v = p2[(int64_t)r * C + c];
+      const float2 v = p2[(int64_t)r * ld + c];
       s[0] += v.x;
       q[0] += v.y;
     }
@@ -226,10 +228,10 @@ __device__ __forceinline__ void bn_stats_finalize_body(int bx, const void* __res
                                                                 const float* __restrict__ beta, float eps,
                                                                 float momentum, float* __restrict__ running_mean,
                                                                 float* __restrict__ running_var,
-                                                                float* __restrict__ ws) {
+                                                                float* __restrict__ ws, int ldp = 0) {
   float S, Q;
   int c;
-  if (!reduce_partials<WPC>(bx, part, nrb, C, S, Q, c)) return;
+  if (!reduce_partials<WPC>(bx, part, nrb, C, S, Q, c, ldp)) return;
   const float K = x0 == nullptr ? 0.f
                   : (x_is_bf16 ? bf16_to_f32(reinterpret_cast<const bf16_t*>(x0)[c]) : reinterpret_cast<const float*>(x0)[c]);
   const float inv_m = 1.f / (float)M;
@@ -272,7 +274,7 @@ __device__ __forceinline__ void bn_apply_body(int bx, const T* __restrict__ x, c
                                                               int64_t M, int C, int nrb, int tpr,
                                                               uint8_t* __restrict__ mask,
                                                               const float* __restrict__ ws2,
-                                                              int64_t ldy) {
+                                                              int64_t ldy, int64_t ldx = 0) {
   // ldy != 0: y is a channel slice of a wider channels_last tensor (row stride ldy), e.g. one
   // Inception branch written straight into the concatenated block output
   // Same tiling as the reduction passes: a thread owns 8 fixed channels for all its rows, so the
@@ -293,7 +295,7 @@ __device__ __forceinline__ void bn_apply_body(int bx, const T* __restrict__ x, c
   auto row = [&](int64_t r) {
     const int64_t off = r * C + c0;
     float a[8];
-    Vec8<T>::load(x + off, a);
+    Vec8<T>::load(x + (ldx ? r * ldx + c0 : off), a);
     float rv[8];
     if (kRes) Vec8<T>::load(res + off, rv);
     uint32_t bits = 0;
@@ -318,7 +320,7 @@ __device__ __forceinline__ void bn_apply_body(int bx, const T* __restrict__ x, c
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int64_t off = (r + u * rpi) * C + c0;
-      xr[u].load(x + off);
+      xr[u].load(x + (ldx ? (r + u * rpi) * ldx + c0 : off));
       if (kRes) rr[u].load(res + off);
     }
     __builtin_amdgcn_sched_barrier(0);  // keep every load of the group ahead of its arithmetic
@@ -463,7 +465,7 @@ __device__ __forceinline__ void bn_bwd_reduce_body(int bx, DY dy, const T* __res
                                                                    const uint8_t* __restrict__ mask,
                                                                    const T* __restrict__ x,
                                                                    const float* __restrict__ ws, int64_t M, int C,
-                                                                   int nrb, int tpr, float* __restrict__ part) {
+                                                                   int nrb, int tpr, float* __restrict__ part, int64_t ldx = 0) {
   extern __shared__ __attribute__((aligned(16))) float red[];
   const int rpi = kBNThreads / tpr, ct = tpr * 8;
   const int c_base = bx * ct;
@@ -485,7 +487,7 @@ __device__ __forceinline__ void bn_bwd_reduce_body(int bx, DY dy, const T* __res
     const int64_t off = r * C + c0;
     float g[8], xv[8];
     dy.load(off, r, c0, C, g);
-    Vec8<T>::load(x + off, xv);
+    Vec8<T>::load(x + (ldx ? r * ldx + c0 : off), xv);
     apply_relu_mask<T, kMask>(g, xv, sc, sh, y, mask, off);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -502,7 +504,7 @@ __device__ __forceinline__ void bn_bwd_reduce_body(int bx, DY dy, const T* __res
       for (int u = 0; u < kUnroll; ++u) {
         const int64_t off = (r + u * rpi) * C + c0;
         dy.raw(off, r + u * rpi, c0, gr[u]);
-        xr[u].load(x + off);
+        xr[u].load(x + (ldx ? (r + u * rpi) * ldx + c0 : off));
         mb[u] = kMask == kMaskBits ? (uint32_t)mask[off >> 3] : 0xffu;
       }
       __builtin_amdgcn_sched_barrier(0);  // keep every load of the group ahead of its arithmetic
@@ -539,10 +541,10 @@ template <int WPC>
 __device__ __forceinline__ void bn_bwd_finalize_body(int bx, const float* __restrict__ part, int nrb, int64_t M,
                                                               int C, const float* __restrict__ gamma,
                                                               float* __restrict__ ws, float* __restrict__ dgamma,
-                                                              float* __restrict__ dbeta) {
+                                                              float* __restrict__ dbeta, int ldp = 0) {
   float S, Q;
   int c;
-  if (!reduce_partials<WPC>(bx, part, nrb, C, S, Q, c)) return;
+  if (!reduce_partials<WPC>(bx, part, nrb, C, S, Q, c, ldp)) return;
   const float invstd = ws[C + c];
   const float g = gamma ? gamma[c] : 1.f;
   if (dgamma) dgamma[c] = Q * invstd;
@@ -567,8 +569,7 @@ __device__ __forceinline__ void bn_bwd_apply_body(int bx, DY dy, const T* __rest
                                                                   const uint8_t* __restrict__ mask,
                                                                   const T* __restrict__ x,
                                                                   const float* __restrict__ ws, T* __restrict__ dx,
-                                                                  T* __restrict__ dres, int64_t M, int C, int nrb,
-                                                                  int tpr) {
+                                                                  T* __restrict__ dres, int64_t M, int C, int nrb, int tpr, int64_t ldx = 0, int64_t lddx = 0) {
   const int rpi = kBNThreads / tpr, ct = tpr * 8;
   const int c0 = bx * ct + (threadIdx.x % tpr) * 8;
   const int rg = threadIdx.x / tpr;
@@ -588,12 +589,12 @@ __device__ __forceinline__ void bn_bwd_apply_body(int bx, DY dy, const T* __rest
     const int64_t off = r * C + c0;
     float g[8], xv[8];
     dy.load(off, r, c0, C, g);
-    Vec8<T>::load(x + off, xv);
+    Vec8<T>::load(x + (ldx ? r * ldx + c0 : off), xv);
     apply_relu_mask<T, kMask>(g, xv, sc, sh, y, mask, off);
     if (kDres) Vec8<T>::store(dres + off, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = k1[j] * (g[j] - m1[j] - (xv[j] - mean[j]) * k2[j]);
-    Vec8<T>::store(dx + off, xv);
+    Vec8<T>::store(dx + (lddx ? r * lddx + c0 : off), xv);
   };
   int64_t r = r0 + rg;
   if constexpr (DY::kRaw && kMask != kMaskY) {
@@ -604,7 +605,7 @@ __device__ __forceinline__ void bn_bwd_apply_body(int bx, DY dy, const T* __rest
       for (int u = 0; u < kUnroll; ++u) {
         const int64_t off = (r + u * rpi) * C + c0;
         dy.raw(off, r + u * rpi, c0, gr[u]);
-        xr[u].load(x + off);
+        xr[u].load(x + (ldx ? (r + u * rpi) * ldx + c0 : off));
         mb[u] = kMask == kMaskBits ? (uint32_t)mask[off >> 3] : 0xffu;
       }
       __builtin_amdgcn_sched_barrier(0);  // keep every load of the group ahead of its arithmetic
@@ -624,7 +625,7 @@ __device__ __forceinline__ void bn_bwd_apply_body(int bx, DY dy, const T* __rest
         if (kDres) Vec8<T>::store(dres + off, g);
 #pragma unroll
         for (int j = 0; j < 8; ++j) xv[j] = k1[j] * (g[j] - m1[j] - (xv[j] - mean[j]) * k2[j]);
-        Vec8<T>::store(dx + off, xv);
+        Vec8<T>::store(dx + (lddx ? (r + u * rpi) * lddx + c0 : off), xv);
       }
     }
   }
@@ -1310,26 +1311,26 @@ __device__ __forceinline__ int bn_group_of(const BnGroups& G, int bx) {
 __global__ __launch_bounds__(256) void bn_group_stats_finalize_kernel(BnGroups G, int64_t M) {
   const int g = bn_group_of(G, blockIdx.x);
   bn_stats_finalize_body<1>(blockIdx.x - G.begin[g], nullptr, 0, G.part[g], G.nrb[g], M, G.C[g], G.gamma[g],
-                            G.beta[g], G.eps[g], G.mom[g], G.rm[g], G.rv[g], G.ws[g]);
+                            G.beta[g], G.eps[g], G.mom[g], G.rm[g], G.rv[g], G.ws[g], G.ldp[g]);
 }
 
 __global__ __launch_bounds__(kBNThreads) void bn_group_apply_kernel(BnGroups G, int64_t M, int nrb) {
   const int g = bn_group_of(G, blockIdx.x);
   bn_apply_body<bf16_t, false, true, false>(blockIdx.x - G.begin[g], G.x[g], nullptr, G.y[g], G.ws[g], M, G.C[g],
-                                            nrb, G.tpr[g], nullptr, nullptr, G.ldy[g]);
+                                            nrb, G.tpr[g], nullptr, nullptr, G.ldy[g], G.ldx[g]);
 }
 
 __global__ __launch_bounds__(kBNThreads) void bn_group_bwd_reduce_kernel(BnGroups G, int64_t M, int nrb) {
   const int g = bn_group_of(G, blockIdx.x);
   bn_bwd_reduce_body<bf16_t, kMaskRecomp, DirectDy<bf16_t>>(blockIdx.x - G.begin[g], DirectDy<bf16_t>{G.dy[g], G.lddy[g]},
                                                             nullptr, nullptr, G.x[g], G.ws[g], M, G.C[g], nrb,
-                                                            G.tpr[g], G.wpart[g]);
+                                                            G.tpr[g], G.wpart[g], G.ldx[g]);
 }
 
 __global__ __launch_bounds__(256) void bn_group_bwd_finalize_kernel(BnGroups G, int64_t M) {
   const int g = bn_group_of(G, blockIdx.x);
   bn_bwd_finalize_body<1>(blockIdx.x - G.begin[g], G.part[g], G.nrb[g], M, G.C[g], G.gamma[g], G.ws[g], G.dgamma[g],
-                          G.dbeta[g]);
+                          G.dbeta[g], G.ldp[g]);
 }
 
 __global__ __launch_bounds__(kBNThreads) void bn_group_bwd_apply_kernel(BnGroups G, int64_t M, int nrb) {
@@ -1337,7 +1338,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_group_bwd_apply_kernel(BnGroups
   bn_bwd_apply_body<bf16_t, kMaskRecomp, false, DirectDy<bf16_t>>(blockIdx.x - G.begin[g],
                                                                   DirectDy<bf16_t>{G.dy[g], G.lddy[g]}, nullptr,
                                                                   nullptr, G.x[g], G.ws[g], G.dx[g], nullptr, M, G.C[g],
-                                                                  nrb, G.tpr[g]);
+                                                                  nrb, G.tpr[g], G.ldx[g], G.lddx[g]);
 }
 
 // channel tiles of each group for a pass with this block target; returns the row-block count the
@@ -1380,9 +1381,10 @@ static void bn_group_fold(BnGroups& G, hipStream_t stream) {
   for (int g = 0; g < G.n; ++g) {
     if (const int fg = bn_fold_groups(G.nrb[g])) {
       hipLaunchKernelGGL(bn_partials_fold_kernel, dim3((G.C[g] + 63) / 64, fg), dim3(256), 0, stream, G.part[g],
-                         G.nrb[g], G.C[g], G.wpart[g]);
+                         G.nrb[g], G.C[g], G.wpart[g], G.ldp[g]);
       G.part[g] = G.wpart[g];
       G.nrb[g] = fg;
+      G.ldp[g] = 0;
     }
   }
 }
@@ -1405,6 +1407,7 @@ void launch_bn_group_bwd(BnGroups G, bool ext, int64_t M, hipStream_t stream) {
     for (int g = 0; g < G.n; ++g) {
       G.part[g] = G.wpart[g];
       G.nrb[g] = nrb;
+      G.ldp[g] = 0;
     }
   }
   bn_group_finalize_blocks(G);

@@ -287,11 +287,34 @@ static void check_bn_param(const at::Tensor& t, int64_t C, const char* what) {
               " must be a contiguous fp32 GPU vector of C elements");
 }
 
-static void check_branch(const at::Tensor& y, const at::Tensor& ref, const char* what) {
-  check_act(y, what);
-  TORCH_CHECK(y.dim() == 4 && y.scalar_type() == at::kBFloat16 && y.size(0) == ref.size(0) &&
-                  y.size(2) == ref.size(2) && y.size(3) == ref.size(3),
-              what, ": every branch must be bf16 [N, C, H, W] channels_last with the same N, H, W");
+// Row stride of a bf16 channels_last [N, C, H, W] tensor read as [M, C] rows: 0 when contiguous, the
+// wider tensor's channel count when it is a channel slice of one (e.g. one branch of the fused
+// Inception fan-in GEMM output).
+static int64_t cl_row_stride(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.scalar_type() == at::kBFloat16 && t.size(1) % 8 == 0, what,
+              " must be a bf16 [N, C, H, W] GPU tensor with C % 8 == 0");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, what, " must be 16-byte aligned");
+  if (t.is_contiguous(at::MemoryFormat::ChannelsLast)) return 0;
+  const int64_t ld = t.stride(3);
+  TORCH_CHECK(t.stride(1) == 1 && ld > t.size(1) && ld % 8 == 0 && t.stride(2) == ld * t.size(3) &&
+                  t.stride(0) == t.stride(2) * t.size(2),
+              what, " must be channels_last or a channel slice of a channels_last tensor");
+  return ld;
+}
+
+static int64_t check_branch(const at::Tensor& y, const at::Tensor& ref, const char* what) {
+  const int64_t ld = cl_row_stride(y, what);
+  TORCH_CHECK(y.size(0) == ref.size(0) && y.size(2) == ref.size(2) && y.size(3) == ref.size(3), what,
+              ": every branch must have the same N, H, W");
+  return ld;
+}
+
+// [rows, C, 2] fp32 partials, or a channel slice of a wider [rows, Ctot, 2] tensor: row stride in channels
+static int partials_row_stride(const at::Tensor& st, int64_t C, const char* what) {
+  TORCH_CHECK(st.is_cuda() && st.scalar_type() == at::kFloat && st.dim() == 3 && st.size(1) == C && st.size(2) == 2 &&
+                  st.stride(2) == 1 && st.stride(1) == 2 && st.stride(0) % 2 == 0 && st.stride(0) >= 2 * C,
+              what, " must be fp32 [row_blocks, C, 2] partials (or a channel slice of wider ones)");
+  return st.stride(0) == 2 * C ? 0 : (int)(st.stride(0) / 2);
 }
 
 // forward fields shared by both variants; returns the workspaces (keep: scratch kept alive)
@@ -309,12 +332,10 @@ static std::vector<at::Tensor> group_fwd_fields(BnGroups& G, const std::vector<a
   G.n = n;
   std::vector<at::Tensor> wss;
   for (int g = 0; g < n; ++g) {
-    check_branch(ys[g], ys[0], "y");
+    G.ldx[g] = check_branch(ys[g], ys[0], "y");
     const int C = (int)ys[g].size(1);
     const at::Tensor& st = stats[g];
-    TORCH_CHECK(st.is_cuda() && st.scalar_type() == at::kFloat && st.is_contiguous() && st.dim() == 3 &&
-                    st.size(1) == C && st.size(2) == 2,
-                "grouped BN: stats must be fp32 [row_blocks, C, 2] epilogue partials");
+    G.ldp[g] = partials_row_stride(st, C, "grouped BN stats");
     check_bn_param(gammas[g], C, "weight");
     check_bn_param(betas[g], C, "bias");
     check_bn_param(rms[g], C, "running_mean");
@@ -351,7 +372,7 @@ std::vector<at::Tensor> bn_concat_fwd(std::vector<at::Tensor> ys, std::vector<at
   auto wss = group_fwd_fields(G, ys, gammas, betas, rms, rvs, moms, epss, stats, keep);
   int64_t off = 0;
   for (int g = 0; g < G.n; ++g) {
-    check_branch(ys[g], out, "y");
+    (void)check_branch(ys[g], out, "y");
     G.y[g] = (uint16_t*)out.data_ptr() + off;
     G.ldy[g] = out.size(1);
     off += G.C[g];
@@ -372,7 +393,7 @@ std::vector<at::Tensor> bn_group_fwd(std::vector<at::Tensor> ys, std::vector<at:
   auto wss = group_fwd_fields(G, ys, gammas, betas, rms, rvs, moms, epss, stats, keep);
   std::vector<at::Tensor> res;
   for (int g = 0; g < G.n; ++g) {
-    res.push_back(at::empty_like(ys[g]));
+    res.push_back(at::empty(ys[g].sizes(), ys[g].options().memory_format(at::MemoryFormat::ChannelsLast)));
     G.y[g] = (uint16_t*)res.back().data_ptr();
     G.ldy[g] = 0;
   }
@@ -385,19 +406,28 @@ std::vector<at::Tensor> bn_group_fwd(std::vector<at::Tensor> ys, std::vector<at:
 // backward fields shared by both variants; returns [dx_0, dgamma_0, dbeta_0, dx_1, ...]
 static std::vector<at::Tensor> group_bwd_fields(BnGroups& G, const std::vector<at::Tensor>& ys,
                                                 const std::vector<at::Tensor>& gammas,
-                                                const std::vector<at::Tensor>& wss) {
+                                                const std::vector<at::Tensor>& wss,
+                                                const std::vector<at::Tensor>& dx_out = {}) {
   const int n = (int)ys.size();
   TORCH_CHECK(n >= 1 && n <= kMaxBnGroups && (int)gammas.size() == n && (int)wss.size() == n,
               "grouped BN backward: 1..4 branches, one entry per branch in every list");
   G.n = n;
   std::vector<at::Tensor> res;
+  TORCH_CHECK(dx_out.empty() || (int)dx_out.size() == n, "grouped BN backward: one dx output per branch");
   for (int g = 0; g < n; ++g) {
-    check_branch(ys[g], ys[0], "y");
+    G.ldx[g] = check_branch(ys[g], ys[0], "y");
     const int C = (int)ys[g].size(1);
     check_bn_param(gammas[g], C, "weight");
     TORCH_CHECK(wss[g].scalar_type() == at::kFloat && wss[g].numel() == 7 * (int64_t)C, "ws must be the 7C workspace");
     auto f32 = ys[g].options().dtype(at::kFloat);
-    at::Tensor dx = at::empty_like(ys[g]), dg = at::empty({C}, f32), db = at::empty({C}, f32);
+    at::Tensor dx, dg = at::empty({C}, f32), db = at::empty({C}, f32);
+    if (!dx_out.empty()) {  // written into a given (possibly strided) slice, e.g. of the fan-in's dY
+      dx = dx_out[g];
+      G.lddx[g] = check_branch(dx, ys[g], "dx_out");
+      TORCH_CHECK(dx.size(1) == C, "dx_out: channel count of its branch");
+    } else {
+      dx = at::empty(ys[g].sizes(), ys[g].options().memory_format(at::MemoryFormat::ChannelsLast));
+    }
     G.x[g] = (const uint16_t*)ys[g].data_ptr();
     G.C[g] = C;
     G.gamma[g] = gammas[g].data_ptr<float>();
@@ -424,14 +454,16 @@ static void group_reduce_scratch(BnGroups& G, int64_t M, std::vector<at::Tensor>
 
 // dy of branch g read in place from channels [off_g, off_g + C_g) of dout
 std::vector<at::Tensor> bn_concat_bwd(at::Tensor dout, std::vector<at::Tensor> ys, std::vector<at::Tensor> gammas,
-                                      std::vector<at::Tensor> wss) {
+                                      std::vector<at::Tensor> wss, std::vector<at::Tensor> dx_out) {
   check_act(dout, "dout");
   TORCH_CHECK(dout.dim() == 4 && dout.scalar_type() == at::kBFloat16, "bn_concat_bwd: dout must be bf16 [N, Ctot, H, W]");
   BnGroups G{};
-  auto res = group_bwd_fields(G, ys, gammas, wss);
+  std::vector<at::Tensor> outs;
+  for (size_t g = 0; g < dx_out.size(); ++g) outs.push_back(dx_out[g]);
+  auto res = group_bwd_fields(G, ys, gammas, wss, outs);
   int64_t off = 0;
   for (int g = 0; g < G.n; ++g) {
-    check_branch(ys[g], dout, "y");
+    (void)check_branch(ys[g], dout, "y");
     G.dy[g] = (const uint16_t*)dout.data_ptr() + off;
     G.lddy[g] = dout.size(1);
     off += G.C[g];
@@ -448,9 +480,9 @@ std::vector<at::Tensor> bn_concat_bwd(at::Tensor dout, std::vector<at::Tensor> y
 // branch, or empty (then a grouped reduce pass runs)
 std::vector<at::Tensor> bn_group_bwd(std::vector<at::Tensor> dys, std::vector<at::Tensor> ys,
                                      std::vector<at::Tensor> gammas, std::vector<at::Tensor> wss,
-                                     std::vector<at::Tensor> exts) {
+                                     std::vector<at::Tensor> exts, std::vector<at::Tensor> dx_out) {
   BnGroups G{};
-  auto res = group_bwd_fields(G, ys, gammas, wss);
+  auto res = group_bwd_fields(G, ys, gammas, wss, dx_out);
   TORCH_CHECK((int)dys.size() == G.n && (exts.empty() || (int)exts.size() == G.n),
               "bn_group_bwd: one dy (and optionally one partials tensor) per branch");
   std::vector<at::Tensor> keep;
@@ -897,9 +929,13 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("relu"), pybind11::arg("stats") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
         pybind11::arg("out_channel") = 0);
   m.def("bn_concat_fwd", &bn_concat_fwd, "grouped training BN+ReLU of concatenated branches into one NHWC output");
-  m.def("bn_concat_bwd", &bn_concat_bwd, "backward of bn_concat_fwd (dy slices read in place)");
+  m.def("bn_concat_bwd", &bn_concat_bwd, "backward of bn_concat_fwd (dy slices read in place)", pybind11::arg("dout"),
+        pybind11::arg("ys"), pybind11::arg("weights"), pybind11::arg("wss"),
+        pybind11::arg("dx_out") = std::vector<at::Tensor>{});
   m.def("bn_group_fwd", &bn_group_fwd, "grouped training BN+ReLU of same-size tensors, one output each");
-  m.def("bn_group_bwd", &bn_group_bwd, "backward of bn_group_fwd (optionally from dgrad-epilogue partials)");
+  m.def("bn_group_bwd", &bn_group_bwd, "backward of bn_group_fwd (optionally from dgrad-epilogue partials)",
+        pybind11::arg("dys"), pybind11::arg("ys"), pybind11::arg("weights"), pybind11::arg("wss"),
+        pybind11::arg("exts") = std::vector<at::Tensor>{}, pybind11::arg("dx_out") = std::vector<at::Tensor>{});
   m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC", pybind11::arg("dy"),
         pybind11::arg("y"), pybind11::arg("mask"), pybind11::arg("x"), pybind11::arg("ws"), pybind11::arg("weight"),
         pybind11::arg("mask_mode"), pybind11::arg("need_dres"), pybind11::arg("ext_part") = pybind11::none());

@@ -132,6 +132,47 @@ def test_bn_group_separate_outputs_with_epilogue_partials(cuda, shape):
             assert _rel(gdx, dx) < 1e-2 and _rel(gdg, dg) < 1e-4 and _rel(gdb, db) < 1e-4, (i, len(exts))
 
 
+@pytest.mark.parametrize("shape", [(4, 7, 9), (35, 80, 50)])
+def test_bn_group_strided_inputs_and_dx_slices(cuda, shape):
+    """Branch inputs, their statistics and the dx outputs as channel slices of wider tensors (the
+    fused fan-in GEMM's layout) give bit-identical results to the contiguous call."""
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    torch.manual_seed(2)
+    n, h, w = shape
+    chans = [64, 96, 16]
+    ctot = sum(chans)
+    a = torch.randn(n * h * w, 32, device=cuda).to(torch.bfloat16)
+    wt = torch.randn(ctot, 32, device=cuda).to(torch.bfloat16)
+    ycat, scat = C.gemm_nt(a, wt, True)
+    y4 = ycat.view(n, h, w, ctot).permute(0, 3, 1, 2)
+    offs = [0, 64, 160]
+    ys_s = [y4[:, o:o + c] for o, c in zip(offs, chans)]
+    st_s = [scat[:, o:o + c] for o, c in zip(offs, chans)]
+    ys_c = [y.contiguous(memory_format=CL) for y in ys_s]
+    st_c = [st.contiguous() for st in st_s]
+    gs = [torch.rand(c, device=cuda) + 0.5 for c in chans]
+    bs = [torch.randn(c, device=cuda) for c in chans]
+    rm = [torch.zeros(c, device=cuda) for c in chans]
+    rv = [torch.ones(c, device=cuda) for c in chans]
+    args = ([0.1] * 3, [1e-3] * 3)
+    rs = C.bn_group_fwd(ys_s, gs, bs, [t.clone() for t in rm], [t.clone() for t in rv], *args, st_s)
+    rc = C.bn_group_fwd(ys_c, gs, bs, [t.clone() for t in rm], [t.clone() for t in rv], *args, st_c)
+    for i, c in enumerate(chans):
+        assert torch.equal(rs[i], rc[i])
+        assert torch.equal(rs[3 + i][:4 * c], rc[3 + i][:4 * c])  # ws: [mean, invstd, scale, shift | bwd]
+    dys = [torch.randn(n, c, h, w, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL) for c in chans]
+    buf = torch.full((n, ctot, h, w), 7.0, device=cuda, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    outs = [buf[:, o:o + c] for o, c in zip(offs, chans)]
+    gs_ = C.bn_group_bwd(dys, ys_s, gs, rs[3:], [], outs)
+    gc_ = C.bn_group_bwd(dys, ys_c, gs, rc[3:], [])
+    for i in range(3):
+        assert gs_[3 * i].data_ptr() == outs[i].data_ptr()
+        for u, v in zip(gs_[3 * i:3 * i + 3], gc_[3 * i:3 * i + 3]):
+            assert torch.equal(u, v)
+
+
 def _block():
     from distributed_learning_amd.models.googlenet import Inception
     from distributed_learning_amd.ops import nn as dnn
