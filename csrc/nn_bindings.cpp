@@ -535,8 +535,11 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
   at::Tensor S;
   if (stats) S = at::empty({gemm_nt_stats_rows(M, N, (int)tile), N, 2},
                            A.options().dtype(at::kFloat));
+  // split-K only for the fully connected heads' shape class: no epilogue features beyond a bias row
+  // (a full addend is a conv dgrad's residual sum, whose bitwise result must not depend on which
+  // path — tile or split-K — the same sum takes, tests/test_gpu_bn_epilogue.py)
   const bool plain = !stats && tile == kTileAuto && !(addend_mask.has_value() && addend_mask->defined()) &&
-                     !(addend2.has_value() && addend2->defined());
+                     !(addend2.has_value() && addend2->defined()) && (!add || addend->stride(0) == 0);
   const int splits = plain && M > 0 && N > 0 && split_k_nt() ? gemm_nt_splitk_splits(M, N, K) : 1;
   if (splits > 1) {  // few output tiles, long K (fully connected heads): split-K + fp32 slab reduce
     at::Tensor P = at::empty({(int64_t)splits * M * N}, A.options().dtype(at::kFloat));
