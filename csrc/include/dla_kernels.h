@@ -224,6 +224,7 @@ struct BnBwdArgs {
   const uint8_t* mask;
   int mode;
   float* part;
+  int64_t ldx = 0;  // row stride of x when it is a channel slice of a wider tensor (0: the output's)
 };
 void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
                     float* stats, hipStream_t stream, const void* addend = nullptr, int64_t ld_addend = 0,

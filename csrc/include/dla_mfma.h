@@ -764,6 +764,7 @@ struct ColStats {
 // scale | shift | ...); mode as launch_bn_bwd (0 none, 1 recompute, 2 bits).
 struct BnBwdEpi {
   const bf16_t* x;  // null: no BN partials
+  int64_t ldx;      // its row stride (0: ldc, the same layout as the GEMM output)
   const float* ws;
   const uint8_t* mask;
   int mode;
@@ -846,7 +847,8 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
       const int gn = col0 + my_cc;
       const bool ok = gm < M && gn < N;
       const int64_t off = ok ? gm * ldc + gn : 0;
-      xr[it] = ok ? *reinterpret_cast<const ushort8_t*>(bnb->x + off) : zero8();
+      const int64_t xo = (ok && bnb->ldx) ? gm * bnb->ldx + gn : off;
+      xr[it] = ok ? *reinterpret_cast<const ushort8_t*>(bnb->x + xo) : zero8();
       mr[it] = (ok && bnb->mode == 2) ? (uint32_t)bnb->mask[off >> 3] : 0xffu;
     }
   }

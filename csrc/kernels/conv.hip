@@ -734,6 +734,7 @@ void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H,
   BnBwdEpi bnb{};
   if (bn_bwd) {
     bnb.x = (const bf16_t*)bn_bwd->x;
+    bnb.ldx = bn_bwd->ldx;
     bnb.ws = bn_bwd->ws;
     bnb.mask = bn_bwd->mask;
     bnb.mode = bn_bwd->mode;

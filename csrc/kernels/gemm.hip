@@ -280,6 +280,7 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
   BnBwdEpi bnb{};
   if (bn_bwd) {
     bnb.x = (const bf16_t*)bn_bwd->x;
+    bnb.ldx = bn_bwd->ldx;
     bnb.ws = bn_bwd->ws;
     bnb.mask = bn_bwd->mask;
     bnb.mode = bn_bwd->mode;

@@ -20,6 +20,22 @@ static void check_act(const at::Tensor& t, const char* what) {
 
 static int64_t rows_of(const at::Tensor& t) { return t.numel() / t.size(1); }
 
+// Row stride of a bf16 channels_last [N, C, H, W] tensor read as [M, C] rows: 0 when contiguous, the
+// wider tensor's channel count when it is a channel slice of one (e.g. one branch of the fused
+// Inception fan-in GEMM output).
+static int64_t cl_row_stride(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.scalar_type() == at::kBFloat16 && t.size(1) % 8 == 0, what,
+              " must be a bf16 [N, C, H, W] GPU tensor with C % 8 == 0");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, what, " must be 16-byte aligned");
+  if (t.is_contiguous(at::MemoryFormat::ChannelsLast)) return 0;
+  const int64_t ld = t.stride(3);
+  TORCH_CHECK(t.stride(1) == 1 && ld > t.size(1) && ld % 8 == 0 && t.stride(2) == ld * t.size(3) &&
+                  t.stride(0) == t.stride(2) * t.size(2),
+              what, " must be channels_last or a channel slice of a channels_last tensor");
+  return ld;
+}
+
+
 // launch_bn_fwd scratch for GEMM-epilogue statistics [rows][C][2]: the folded rows (>= 1 float)
 static int64_t ext_part_floats(const c10::optional<at::Tensor>& st, int C) {
   return std::max<int64_t>(1, (int64_t)bn_fold_groups((int)st->size(0)) * C * 2);
@@ -233,10 +249,13 @@ std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, c
 // BN-backward epilogue operands (see BnBwdArgs): x_bn is the BN input laid out like the GEMM output.
 static BnBwdArgs make_bn_bwd(const at::Tensor& x_bn, const at::Tensor& ws, const c10::optional<at::Tensor>& mask,
                              int64_t mode, int64_t M, int64_t N, int64_t rows, at::Tensor& part) {
+  int64_t ldx = 0;
+  if (x_bn.dim() == 4 && !x_bn.is_contiguous(at::MemoryFormat::ChannelsLast)) ldx = cl_row_stride(x_bn, "bn epilogue x");
   TORCH_CHECK(x_bn.is_cuda() && x_bn.scalar_type() == at::kBFloat16 && x_bn.numel() == M * N &&
-                  (x_bn.dim() == 2 ? x_bn.is_contiguous() : x_bn.is_contiguous(at::MemoryFormat::ChannelsLast)) &&
+                  (x_bn.dim() == 2 ? x_bn.is_contiguous() : (ldx > 0 || x_bn.is_contiguous(at::MemoryFormat::ChannelsLast))) &&
                   x_bn.size(1) == N,
-              "bn epilogue: x must be the bf16 BN input with the GEMM output's shape/layout");
+              "bn epilogue: x must be the bf16 BN input with the GEMM output's shape (channels_last, or a channel "
+              "slice of a wider channels_last tensor)");
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() == 7 * N, "bn epilogue: ws must be the 7C workspace");
   TORCH_CHECK(mode >= 0 && mode <= 2, "bn epilogue: mode 0 (no ReLU), 1 (recompute) or 2 (bit mask)");
   const uint8_t* mp = nullptr;
@@ -246,7 +265,8 @@ static BnBwdArgs make_bn_bwd(const at::Tensor& x_bn, const at::Tensor& ws, const
     mp = mask->data_ptr<uint8_t>();
   }
   part = at::empty({rows, N, 2}, ws.options());
-  return BnBwdArgs{x_bn.data_ptr(), ws.data_ptr<float>(), mp, (int)mode, part.data_ptr<float>()};
+  TORCH_CHECK(ldx == 0 || mode != 2, "bn epilogue: the bit mask needs a contiguous x");
+  return BnBwdArgs{x_bn.data_ptr(), ws.data_ptr<float>(), mp, (int)mode, part.data_ptr<float>(), ldx};
 }
 
 static void check_mat(const at::Tensor& t, const char* what) {
@@ -285,21 +305,6 @@ static const void* addend2_ptr(const c10::optional<at::Tensor>& a2, int64_t M, i
 static void check_bn_param(const at::Tensor& t, int64_t C, const char* what) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == C, what,
               " must be a contiguous fp32 GPU vector of C elements");
-}
-
-// Row stride of a bf16 channels_last [N, C, H, W] tensor read as [M, C] rows: 0 when contiguous, the
-// wider tensor's channel count when it is a channel slice of one (e.g. one branch of the fused
-// Inception fan-in GEMM output).
-static int64_t cl_row_stride(const at::Tensor& t, const char* what) {
-  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.scalar_type() == at::kBFloat16 && t.size(1) % 8 == 0, what,
-              " must be a bf16 [N, C, H, W] GPU tensor with C % 8 == 0");
-  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, what, " must be 16-byte aligned");
-  if (t.is_contiguous(at::MemoryFormat::ChannelsLast)) return 0;
-  const int64_t ld = t.stride(3);
-  TORCH_CHECK(t.stride(1) == 1 && ld > t.size(1) && ld % 8 == 0 && t.stride(2) == ld * t.size(3) &&
-                  t.stride(0) == t.stride(2) * t.size(2),
-              what, " must be channels_last or a channel slice of a channels_last tensor");
-  return ld;
 }
 
 static int64_t check_branch(const at::Tensor& y, const at::Tensor& ref, const char* what) {

@@ -260,9 +260,8 @@ class _BNReluGroup(torch.autograd.Function):
         ctx.save_for_backward(*ys, *gs, *wss)
         ctx.nb = n
         ctx.dsl = dsl
-        # the consumer conv's dgrad epilogue reads the BN input contiguously: no link for a slice
-        ctx.links = [BNLink(y, ws, None, MASK_RECOMPUTE) if y.is_contiguous(memory_format=CL) else None
-                     for y, ws in zip(ys, wss)]
+        # the consumer conv's dgrad epilogue reads the BN input in place (a slice: its row stride)
+        ctx.links = [BNLink(y, ws, None, MASK_RECOMPUTE) for y, ws in zip(ys, wss)]
         return tuple(outs)
 
     @staticmethod

@@ -173,6 +173,27 @@ def test_bn_group_strided_inputs_and_dx_slices(cuda, shape):
             assert torch.equal(u, v)
 
 
+def test_dgrad_bn_epilogue_reads_strided_bn_input(cuda):
+    """The 3x3 dgrad's BN-backward epilogue reading its BN input as a channel slice (fused fan-in
+    layout) == reading a contiguous copy, bitwise."""
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    torch.manual_seed(4)
+    n, h, w, cin, ctot, off = 4, 14, 14, 96, 176, 64
+    big = torch.randn(n, ctot, h, w, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    xs = big[:, off:off + cin]
+    xc = xs.contiguous(memory_format=CL)
+    ws = torch.cat([torch.randn(cin, device=cuda) * 0.1, torch.rand(cin, device=cuda) + 0.5,
+                    torch.rand(cin, device=cuda) + 0.5, torch.randn(cin, device=cuda) * 0.1,
+                    torch.zeros(3 * cin, device=cuda)])
+    dy = torch.randn(n, 128, h, w, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    wt = torch.randn(128, cin, 3, 3, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    a = C.conv3x3_dgrad_bn(dy, wt, None, xs, ws, None, 1)
+    b = C.conv3x3_dgrad_bn(dy, wt, None, xc, ws, None, 1)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
 def _block():
     from distributed_learning_amd.models.googlenet import Inception
     from distributed_learning_amd.ops import nn as dnn
