@@ -440,10 +440,15 @@ struct PoolDy {
           dv[t] = *reinterpret_cast<const ushort8_t*>(dyp + o);
         }
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t q = ok[t] ? qv[t] : 0xffu;  // branch-free: an out-of-range window matches nothing
+        const uint32_t lo32 = (uint32_t)pk[t], hi32 = (uint32_t)(pk[t] >> 32);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (ok[t] && ((pk[t] >> (8 * j)) & 0xffu) == qv[t]) g[j] += bf16_to_f32(dv[t][j]);
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t byte = ((j < 4 ? lo32 : hi32) >> (8 * (j & 3))) & 0xffu;
+          g[j] += byte == q ? bf16_to_f32(dv[t][j]) : 0.f;
+        }
+      }
       return;
     }
     for (int oh = oh_lo; oh <= oh_hi; ++oh)
@@ -1113,10 +1118,14 @@ struct StemQuad {
             const int ky = dh - 2 * a + 2 - P, kx = dw - 2 * b + 2 - P;
             if (ky < lo || ky > 2 || kx < lo || kx > 2) continue;  // compile-time after unrolling
             const int w = a * 2 + b;
-            const uint32_t tap = (uint32_t)(ky * 3 + kx);
+            // branch-free: a window outside the output matches no tap (0xff)
+            const uint32_t tap = ok[w] ? (uint32_t)(ky * 3 + kx) : 0xffu;
+            const uint32_t lo32 = (uint32_t)pk[w], hi32 = (uint32_t)(pk[w] >> 32);
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-              if (ok[w] && ((pk[w] >> (8 * e)) & 0xffu) == tap) g[dh * 2 + dw][e] += d[w][e];
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t byte = ((e < 4 ? lo32 : hi32) >> (8 * (e & 3))) & 0xffu;
+              g[dh * 2 + dw][e] += byte == tap ? d[w][e] : 0.f;
+            }
           }
     const int64_t base = ((int64_t)n * H + 2 * j) * W + 2 * i;
     off[0] = base * C + c0;
