@@ -178,6 +178,8 @@ void launch_maxpool_bwd(const void* dy, const uint8_t* pos, void* dx, int N, int
                         int k, int s, int p, int dtype, hipStream_t stream);
 // global average pooling over the H*W pixels of NHWC x: y [N, C]; backward dx [N, H, W, C] = dy / HW
 void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, int dtype, hipStream_t stream);
+// y [N, H/2, W/2, C] = x [N, H, W, C] at even (h, w); bf16 NHWC, C % 8 == 0
+void launch_subsample2(const void* x, void* y, int N, int H, int W, int C, hipStream_t stream);
 void launch_gap_bwd(const void* dy, void* dx, int N, int HW, int C, int dtype, hipStream_t stream);
 
 // ---- bf16 MFMA GEMMs (gemm.hip) ---------------------------------------------------------------
@@ -202,19 +204,30 @@ enum TileCfg : int {
   kTile256x128 = 4,
   kTile256x128w4 = 5,
   kTile128x256w4 = 6,
-  kTile256x64 = 7  // 4 waves stacked along M (64 x 64 wave tiles), 2 blocks / CU; opt-in: measured slower
-                   // than 128x64 / 128x128 at every ResNet-50 shape (profiles/tiles_256x64_4x1waves_ab.jsonl)
+  kTile256x64 = 7,  // 4 waves stacked along M (64 x 64 wave tiles), 2 blocks / CU; opt-in: measured slower
+                    // than 128x64 / 128x128 at every ResNet-50 shape (profiles/tiles_256x64_4x1waves_ab.jsonl)
+  // 8 waves (4 x 2) of 64 x 128, 2-stage buffer-DMA pipeline (128 KB LDS), one block per CU: per MAC
+  // 25 % fewer LDS fragment reads than the 64 x 64 wave tiles and half the DMA writes of two 128x128
+  // blocks, for the compute-bound shapes where the 128x128 loop is LDS-bandwidth co-bound
+  kTile256x256 = 8
 };
-int pick_tile(int64_t M, int N, int tile);
+// K: reduction length (0 = unknown); wide_ok: the kernel family can run the 8-wave tiles (3x3 convs
+// need a channel count % 64 on the loaded side)
+int pick_tile(int64_t M, int N, int tile, int K = 0, bool wide_ok = true);
+bool tile256_enabled();  // DLA_TILE256 != 0: 256x256 tiles for the compute-bound fwd / dgrad shapes
+bool tn256_enabled();    // ... and for the split-K weight gradients (also DLA_TN256 != 0)
 inline int tile_bm(int cfg) {
-  return cfg == kTile64x64 ? 64 : ((cfg == kTile256x128 || cfg == kTile256x128w4 || cfg == kTile256x64) ? 256 : 128);
+  return cfg == kTile64x64 ? 64
+                           : ((cfg == kTile256x128 || cfg == kTile256x128w4 || cfg == kTile256x64 || cfg == kTile256x256)
+                                  ? 256
+                                  : 128);
 }
 inline int tile_bn(int cfg) {
-  return cfg == kTile128x256w4 ? 256
-                               : ((cfg == kTile128x128 || cfg == kTile256x128 || cfg == kTile256x128w4) ? 128 : 64);
+  return (cfg == kTile128x256w4 || cfg == kTile256x256) ? 256
+                                                       : ((cfg == kTile128x128 || cfg == kTile256x128 || cfg == kTile256x128w4) ? 128 : 64);
 }
 // rows of BN-statistics partials ([rows][N][2]) a stats-producing launch writes (one per row tile)
-int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto);
+int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto, int K = 0);
 // BatchNorm-backward reduction fused into a bf16-output GEMM epilogue (the output is the BN's dy):
 // x = the BN input [M, N], ws = its 7N workspace, mask/mode as launch_bn_bwd (0, 1 or 2),
 // part = [stats_rows][N][2] partial (sum dy', sum dy'(x - mean)).
@@ -254,7 +267,7 @@ void launch_gemm_nt_splitk(const void* A, int64_t lda, const void* B, int64_t ld
 // fwd: stride 1 or 2, optional BN statistics partials stats[ceil(P/128)][Cout][2].
 // dgrad: stride 1 only, dx [N,H,W,Cin] (+ optional addend). wgrad: stride 1 or 2, split-K fp32
 // partials (splits * Cout * 9*Cin floats) reduced into dw [Cout][9*Cin] (fp32 or bf16).
-int conv3x3_stats_rows(int64_t P, int Cout, int tile = kTileAuto);
+int conv3x3_stats_rows(int64_t P, int Cout, int tile = kTileAuto, int K = 0, bool wide_ok = true);
 void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout, int stride,
                         float* stats, hipStream_t stream, int tile = kTileAuto);
 void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,

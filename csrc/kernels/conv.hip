@@ -578,11 +578,12 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3s2_dgrad_kernel(const bf16
 }
 
 // wgrad partial slabs P[split][Cout][9*Cin]
-template <int BM, int BN, int PIPE>
-__global__ __launch_bounds__(kThreads, 2) void conv3x3_wgrad_kernel(const bf16_t* __restrict__ dy,
-                                                                    const bf16_t* __restrict__ x, ConvGeom g,
-                                                                    float* __restrict__ part, int k_per_split,
-                                                                    int ntiles, int remap) {
+template <int BM, int BN, int PIPE, int NT = kThreads>
+__global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void conv3x3_wgrad_kernel(const bf16_t* __restrict__ dy,
+                                                                                    const bf16_t* __restrict__ x,
+                                                                                    ConvGeom g, float* __restrict__ part,
+                                                                                    int k_per_split, int ntiles,
+                                                                                    int remap) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int P = g.N * g.OH * g.OW;
   const int Mo = g.Cout, No = 9 * g.Cin;
@@ -594,13 +595,13 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_wgrad_kernel(const bf16_t
   const int kbeg = split * k_per_split;
   const int kend = min(P, kbeg + k_per_split);
   const int m0 = bm * BM, n0 = bn * BN;
-  const KLoader<BM> la{dy, g.Cout, m0, Mo, kend};
-  Im2colKLoader<BN, PIPE != 0> lb{x, g, kend};
+  const KLoader<BM, NT> la{dy, g.Cout, m0, Mo, kend};
+  Im2colKLoader<BN, PIPE != 0, NT> lb{x, g, kend};
   lb.init(n0);
-  Acc<BM, BN> acc;
+  Acc<BM, BN, NT> acc;
   acc.zero();
   run_mainloop<PIPE>(la, lb, kbeg, kend, acc, smem_raw);
-  epilogue_f32<BM, BN>(acc, part + (int64_t)split * Mo * No, Mo, No, m0, n0);
+  epilogue_f32<BM, BN, NT>(acc, part + (int64_t)split * Mo * No, Mo, No, m0, n0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -646,7 +647,10 @@ static void launch_fwd_p(const bf16_t* x, const bf16_t* w, bf16_t* y, const Conv
 template <int BM, int BN, bool S, int NTW = kThreads>
 static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGeom& g, float* stats,
                        hipStream_t stream) {
-  if constexpr (NTW == 512) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
+  if constexpr (NTW == 512 && BM * BN > 256 * 128) {  // 256x256: 2 stages fill 128 KB of LDS
+    if (mfma_pipeline() == 2) launch_fwd_p<BM, BN, S, 2, 512>(x, w, y, g, stats, stream);
+    else launch_fwd_p<BM, BN, S, 6, 512>(x, w, y, g, stats, stream);
+  } else if constexpr (NTW == 512) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
     if (mfma_pipeline() == 7) launch_fwd_p<BM, BN, S, 7, 512>(x, w, y, g, stats, stream);
     else launch_fwd_p<BM, BN, S, 3, 512>(x, w, y, g, stats, stream);
   } else if constexpr (BM * BN > 128 * 128) {  // 4 large waves, one block per CU
@@ -666,8 +670,8 @@ static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGe
   }
 }
 
-int conv3x3_stats_rows(int64_t P, int Cout, int tile) {
-  const int bm = tile_bm(pick_tile(P, Cout, tile));
+int conv3x3_stats_rows(int64_t P, int Cout, int tile, int K, bool wide_ok) {
+  const int bm = tile_bm(pick_tile(P, Cout, tile, K, wide_ok));
   return (int)((P + bm - 1) / bm);
 }
 
@@ -681,7 +685,8 @@ void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int
   if (stats) launch_fwd<BM_, BN_, true, NT_>(xp, wp, yp, g, stats, stream);   \
   else launch_fwd<BM_, BN_, false, NT_>(xp, wp, yp, g, stats, stream);
 #define DLA_CF(BM_, BN_) DLA_CFW(BM_, BN_, kThreads)
-  switch (pick_tile((int64_t)g.N * g.OH * g.OW, Cout, tile)) {
+  switch (pick_tile((int64_t)g.N * g.OH * g.OW, Cout, tile, 9 * Cin, Cin % 64 == 0)) {
+    case kTile256x256: DLA_CFW(256, 256, 512) break;
     case kTile256x128: DLA_CFW(256, 128, 512) break;
     case kTile256x128w4: DLA_CF(256, 128) break;
     case kTile128x256w4: DLA_CF(128, 256) break;
@@ -708,7 +713,10 @@ static void launch_dgrad_p(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const 
 template <int BM, int BN, int NTW = kThreads>
 static void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const ConvGeom& g, const bf16_t* addend,
                          const BnBwdEpi& bnb, hipStream_t stream) {
-  if constexpr (NTW == 512) {
+  if constexpr (NTW == 512 && BM * BN > 256 * 128) {
+    if (mfma_pipeline() == 2) launch_dgrad_p<BM, BN, 2, 512>(dy, w, dx, g, addend, bnb, stream);
+    else launch_dgrad_p<BM, BN, 6, 512>(dy, w, dx, g, addend, bnb, stream);
+  } else if constexpr (NTW == 512) {
     if (mfma_pipeline() == 7) launch_dgrad_p<BM, BN, 7, 512>(dy, w, dx, g, addend, bnb, stream);
     else launch_dgrad_p<BM, BN, 3, 512>(dy, w, dx, g, addend, bnb, stream);
   } else if constexpr (BM * BN > 128 * 128) {
@@ -743,7 +751,8 @@ void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H,
   const bf16_t* d = (const bf16_t*)dy;
   const bf16_t* wp = (const bf16_t*)w;
   const bf16_t* ad = (const bf16_t*)addend;
-  switch (pick_tile((int64_t)N * H * W, Cin, tile)) {
+  switch (pick_tile((int64_t)N * H * W, Cin, tile, 9 * Cout, Cout % 64 == 0)) {
+    case kTile256x256: launch_dgrad<256, 256, 512>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile256x128: launch_dgrad<256, 128, 512>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile256x128w4: launch_dgrad<256, 128>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile128x256w4: launch_dgrad<128, 256>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
@@ -775,12 +784,18 @@ void launch_conv3x3s2_dgrad(const void* dy, const void* w, void* dx, int N, int 
 #undef DLA_S2
 }
 
+// 256x256 8-wave weight-gradient tiles (one block per CU) when both output dims are multiples of
+// 256 (Cout and Cin in {256, 512, ...}: the compute-bound 14x14 / 7x7 layers), as for gemm_tn
+static bool wgrad_wide(int Cin, int Cout) { return tn256_enabled() && Cout % 256 == 0 && Cin % 256 == 0; }
+
 int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int stride) {
   const ConvGeom g = make_geom(N, H, W, Cin, Cout, stride);
   const int P = g.N * g.OH * g.OW;
-  const int bm = Cout <= 64 ? 64 : 128;
-  const int tiles = ((Cout + bm - 1) / bm) * ((9 * Cin + 127) / 128);
-  const int splits = std::max(1, splitk_target_blocks() / std::max(1, tiles));  // ~2 workgroups per CU
+  const bool wide = wgrad_wide(Cin, Cout);
+  const int bm = wide ? 256 : (Cout <= 64 ? 64 : 128), bn = wide ? 256 : 128;
+  const int tiles = ((Cout + bm - 1) / bm) * ((9 * Cin + bn - 1) / bn);
+  // ~2 workgroups per CU (one per CU for the 8-wave tiles)
+  const int splits = std::max(1, (wide ? splitk_target_blocks() / 2 : splitk_target_blocks()) / std::max(1, tiles));
   const int max_splits = std::max(1, P / (8 * kBK));          // >= 8 k-steps per split
   return std::max(1, std::min(splits, max_splits));
 }
@@ -804,7 +819,17 @@ void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int spl
     case 4: DLA_WG(BM_, 4); break;      \
     default: DLA_WG(BM_, 2); break;     \
   }
-  if (Cout <= 64) {
+  if (wgrad_wide(Cin, Cout)) {
+    const int nt = (Mo / 256) * (No / 256);
+    const int pipe = conv_pipeline(kps, 4) == 2 ? 2 : 4;
+#define DLA_WG8(P_)                                                                                             \
+  hipLaunchKernelGGL((conv3x3_wgrad_kernel<256, 256, P_, 512>), dim3(nt * splits), dim3(512),                   \
+                     (run_mainloop_lds_bytes<P_, 256, 256, KLoader<256, 512>, Im2colKLoader<256, true, 512>>()), \
+                     stream, (const bf16_t*)dy, (const bf16_t*)x, g, partial, kps, nt, (int)splitk_xcd_remap())
+    if (pipe == 2) DLA_WG8(2);
+    else DLA_WG8(4);
+#undef DLA_WG8
+  } else if (Cout <= 64) {
     DLA_WG_P(64)
   } else {
     DLA_WG_P(128)

@@ -65,11 +65,11 @@ __global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void gemm_nt_kernel(
 // P[split][Mo, No] = sum_{k in split} A[k][m] * B[k][n]   (A: [K, lda] m-contiguous, B: [K, ldb])
 // fp32 partial slabs; splitk_reduce_kernel sums them.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, int PIPE>
-__global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(const bf16_t* __restrict__ A, int64_t lda,
-                                                              const bf16_t* __restrict__ B, int64_t ldb,
-                                                              float* __restrict__ P, int Mo, int No, int K,
-                                                              int k_per_split, int ntiles, int remap) {
+template <int BM, int BN, int PIPE, int NT = kThreads>
+__global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void gemm_tn_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                                              const bf16_t* __restrict__ B, int64_t ldb,
+                                                                              float* __restrict__ P, int Mo, int No, int K,
+                                                                              int k_per_split, int ntiles, int remap) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int nbn = (No + BN - 1) / BN;
   // 1-D grid of tiles x splits; with remap the tiles of one split (which read the same K rows of
@@ -80,12 +80,12 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(const bf16_t* __re
   const int kbeg = split * k_per_split;
   const int kend = min(K, kbeg + k_per_split);
   const int m0 = bm * BM, n0 = bn * BN;
-  Acc<BM, BN> acc;
+  Acc<BM, BN, NT> acc;
   acc.zero();
-  const KLoader<BM> la{A, lda, m0, Mo, kend};
-  const KLoader<BN> lb{B, ldb, n0, No, kend};
+  const KLoader<BM, NT> la{A, lda, m0, Mo, kend};
+  const KLoader<BN, NT> lb{B, ldb, n0, No, kend};
   run_mainloop<PIPE>(la, lb, kbeg, kend, acc, smem_raw);
-  epilogue_f32<BM, BN>(acc, P + (int64_t)split * Mo * No, Mo, No, m0, n0);
+  epilogue_f32<BM, BN, NT>(acc, P + (int64_t)split * Mo * No, Mo, No, m0, n0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -241,7 +241,10 @@ template <int BM, int BN, bool S, bool BT, int NTW = kThreads>
 static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
                       int N, int K, float* stats, const bf16_t* D, int64_t ldd, const BnBwdEpi& bnb,
                       hipStream_t stream) {
-  if constexpr (NTW == 512) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
+  if constexpr (NTW == 512 && BM * BN > 256 * 128) {  // 256x256: 2 stages fill 128 KB of LDS
+    if (mfma_pipeline() == 2) launch_nt_p<BM, BN, S, BT, 2, 512>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
+    else launch_nt_p<BM, BN, S, BT, 6, 512>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
+  } else if constexpr (NTW == 512) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
     if (mfma_pipeline() == 7) launch_nt_p<BM, BN, S, BT, 7, 512>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
     else launch_nt_p<BM, BN, S, BT, 3, 512>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb, stream);
   } else if constexpr (BM * BN > 128 * 128) {  // 4 large waves, one block per CU: 2 or 3 stages
@@ -262,15 +265,29 @@ static void launch_nt(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb
   }
 }
 
-int pick_tile(int64_t M, int N, int tile) {
-  // measured (scripts/bench_gemm.py, bench_conv.py): the 128-row tiles win at every ResNet shape,
-  // including the small-M layers, so the narrow tile is used only when N itself is narrow
+// 256x256 8-wave tiles for the compute-bound shapes (per-layer A/B at ResNet-50 bs512 shapes,
+// profiles/r5a: 3x3 fwd/dgrad at 14x14 and 7x7 -14..-17 %, 1x1 with K >= 1024 -10..-19 %; shorter K or
+// N < 256 is HBM- or LDS-bound and loses up to 2x). At least ~3/4 of the CUs must get a tile.
+// DLA_TILE256=0 restores the 128-row tiles (A/B).
+bool tile256_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DLA_TILE256");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+int pick_tile(int64_t M, int N, int tile, int K, bool wide_ok) {
   if (tile != kTileAuto) return tile;
+  if (wide_ok && tile256_enabled() && K >= 1024 && N % 256 == 0 && ((M + 255) / 256) * (N / 256) >= 192)
+    return kTile256x256;
+  // the 128-row tiles win at every other ResNet shape, including the small-M layers, so the narrow
+  // tile is used only when N itself is narrow (scripts/bench_gemm.py, bench_conv.py)
   return N <= 64 ? kTile128x64 : kTile128x128;
 }
 
-int gemm_nt_stats_rows(int M, int N, int tile) {
-  const int bm = tile_bm(pick_tile(M, N, tile));
+int gemm_nt_stats_rows(int M, int N, int tile, int K) {
+  const int bm = tile_bm(pick_tile(M, N, tile, K));
   return (M + bm - 1) / bm;
 }
 
@@ -307,7 +324,8 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
     if (b_kmajor) DLA_NT(BM_, BN_, false, true, NT_); else DLA_NT(BM_, BN_, false, false, NT_);  \
   }
 #define DLA_NT_ST(BM_, BN_) DLA_NT_STW(BM_, BN_, kThreads)
-  switch (pick_tile(M, N, tile)) {
+  switch (pick_tile(M, N, tile, K)) {
+    case kTile256x256: DLA_NT_STW(256, 256, 512) break;
     case kTile256x128: DLA_NT_STW(256, 128, 512) break;
     case kTile256x128w4: DLA_NT_ST(256, 128) break;
     case kTile128x256w4: DLA_NT_ST(128, 256) break;
@@ -346,11 +364,27 @@ int splitk_target_blocks() {
   return v;
 }
 
+// 256x256 8-wave tiles (one block per CU) for weight gradients whose output dims are both
+// multiples of 256 (the stage-3/4 1x1 convs: compute-bound, like the fwd/dgrad shapes pick_tile
+// sends to kTile256x256); DLA_TILE256=0 turns them off with the other 256x256 tiles
+// (DLA_TN256=0 turns off only these and the 3x3 ones, for A/B)
+bool tn256_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DLA_TN256");
+    return !(e && e[0] == '0');
+  }();
+  return on && tile256_enabled();
+}
+static bool tn_wide(int Mo, int No) { return tn256_enabled() && Mo % 256 == 0 && No % 256 == 0; }
+
 int gemm_tn_splits(int Mo, int No, int K) {
-  // ~512 workgroups in flight (2 per CU) and >= 16 K-steps per split: enough parallelism for the
-  // long M reduction while keeping the fp32 slab traffic (splits * Mo * No * 4 B) small.
-  const int tiles = ((Mo + tn_bm(Mo) - 1) / tn_bm(Mo)) * ((No + tn_bn(No) - 1) / tn_bn(No));
-  int splits = std::max(1, splitk_target_blocks() / std::max(1, tiles));
+  // ~512 workgroups in flight (2 per CU; 256 one-per-CU blocks for the 8-wave tiles) and >= 16
+  // K-steps per split: enough parallelism for the long M reduction while keeping the fp32 slab
+  // traffic (splits * Mo * No * 4 B) small.
+  const bool wide = tn_wide(Mo, No);
+  const int bm = wide ? 256 : tn_bm(Mo), bn = wide ? 256 : tn_bn(No);
+  const int tiles = ((Mo + bm - 1) / bm) * ((No + bn - 1) / bn);
+  int splits = std::max(1, (wide ? splitk_target_blocks() / 2 : splitk_target_blocks()) / std::max(1, tiles));
   const int max_splits = std::max(1, K / (16 * kBK));
   return std::max(1, std::min(splits, max_splits));
 }
@@ -359,21 +393,26 @@ void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, floa
                     int K, void* out, int out_dtype, float scale, bool accumulate, hipStream_t stream) {
   int kps = (K + splits - 1) / splits;
   kps = (kps + kBK - 1) / kBK * kBK;
-  const int bm = tn_bm(Mo), bn = tn_bn(No);
+  const bool wide = tn_wide(Mo, No);
+  const int bm = wide ? 256 : tn_bm(Mo), bn = wide ? 256 : tn_bn(No);
   const int tiles = ((Mo + bm - 1) / bm) * ((No + bn - 1) / bn);
-#define DLA_TN(BM_, BN_, P_)                                                                                      \
-  hipLaunchKernelGGL((gemm_tn_kernel<BM_, BN_, P_>), dim3(tiles * splits), dim3(kThreads),                      \
-                     (run_mainloop_lds_bytes<P_, BM_, BN_, KLoader<BM_>, KLoader<BN_>>()), stream, (const bf16_t*)A, \
-                     lda, (const bf16_t*)B, ldb, partial, Mo, No, K, kps, tiles, (int)splitk_xcd_remap())
-#define DLA_TN_P(BM_, BN_)                 \
-  switch (mfma_pipeline_for(kps)) {        \
-    case 0: DLA_TN(BM_, BN_, 0); break;    \
-    case 3: DLA_TN(BM_, BN_, 3); break;    \
-    case 4: DLA_TN(BM_, BN_, 4); break;    \
-    case 6: DLA_TN(BM_, BN_, 6); break;    \
-    default: DLA_TN(BM_, BN_, 2); break;   \
+#define DLA_TN(BM_, BN_, P_, NT_)                                                                                 \
+  hipLaunchKernelGGL((gemm_tn_kernel<BM_, BN_, P_, NT_>), dim3(tiles * splits), dim3(NT_),                        \
+                     (run_mainloop_lds_bytes<P_, BM_, BN_, KLoader<BM_, NT_>, KLoader<BN_, NT_>>()), stream,        \
+                     (const bf16_t*)A, lda, (const bf16_t*)B, ldb, partial, Mo, No, K, kps, tiles,                 \
+                     (int)splitk_xcd_remap())
+#define DLA_TN_P(BM_, BN_)                            \
+  switch (mfma_pipeline_for(kps)) {                   \
+    case 0: DLA_TN(BM_, BN_, 0, kThreads); break;     \
+    case 3: DLA_TN(BM_, BN_, 3, kThreads); break;     \
+    case 4: DLA_TN(BM_, BN_, 4, kThreads); break;     \
+    case 6: DLA_TN(BM_, BN_, 6, kThreads); break;     \
+    default: DLA_TN(BM_, BN_, 2, kThreads); break;    \
   }
-  if (bm == 64 && bn == 64) {
+  if (wide) {
+    if (mfma_pipeline() == 2) DLA_TN(256, 256, 2, 512);
+    else DLA_TN(256, 256, 6, 512);
+  } else if (bm == 64 && bn == 64) {
     DLA_TN_P(64, 64)
   } else if (bm == 64) {
     DLA_TN_P(64, 128)

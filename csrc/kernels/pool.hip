@@ -398,6 +398,46 @@ __global__ __launch_bounds__(kPoolThreads) void gap_bwd_kernel(const T* __restri
   }
 }
 
+// Stride-2 subsample of an NHWC bf16 activation, y[n][h][w] = x[n][2h][2w] (the input of a ResNet
+// downsample 1x1 conv): 16-byte chunks, 4 chunks per thread with all loads issued before the
+// stores. Replaces torch's strided elementwise copy (3.2 TB/s at the stage-2 shape).
+__global__ __launch_bounds__(kPoolThreads) void subsample2_kernel(const ushort8_t* __restrict__ x,
+                                                                  ushort8_t* __restrict__ y, uint32_t cg,
+                                                                  uint32_t OW, uint32_t OH, int W, int H,
+                                                                  uint32_t total) {
+  // plain 32-bit divisions (a few dozen VALU per 32 bytes moved: free in this HBM-bound copy; the
+  // 24-bit mm::fdiv would overflow at batch 1024)
+  constexpr int U = 4;
+  const uint32_t stride = gridDim.x * kPoolThreads;
+  for (uint32_t t0 = blockIdx.x * kPoolThreads + threadIdx.x; t0 < total; t0 += U * stride) {
+    ushort8_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t t = t0 + u * stride;
+      if (t < total) {
+        const uint32_t pix = t / cg, c = t - pix * cg;
+        const uint32_t q = pix / OW, ow = pix - q * OW;
+        const uint32_t n = q / OH, oh = q - n * OH;
+        v[u] = x[(((uint64_t)n * H + 2 * oh) * W + 2 * ow) * cg + c];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t t = t0 + u * stride;
+      if (t < total) y[t] = v[u];
+    }
+  }
+}
+
+void launch_subsample2(const void* x, void* y, int N, int H, int W, int C, hipStream_t stream) {
+  const int OH = H / 2, OW = W / 2;
+  const uint32_t total = (uint32_t)N * OH * OW * (C / 8);
+  if (total == 0) return;
+  const int nb = (int)std::min<int64_t>(((int64_t)total + 4 * kPoolThreads - 1) / (4 * kPoolThreads), 256 * 32);
+  hipLaunchKernelGGL(subsample2_kernel, dim3(nb), dim3(kPoolThreads), 0, stream, (const ushort8_t*)x, (ushort8_t*)y,
+                     (uint32_t)(C / 8), (uint32_t)OW, (uint32_t)OH, W, H, total);
+}
+
 void launch_gap_fwd(const void* x, void* y, int N, int HW, int C, int dtype, hipStream_t stream) {
   const dim3 grid((C / 8 + 63) / 64, N);
   const float inv = 1.f / (float)HW;

@@ -526,7 +526,7 @@ static bool split_k_nt() {
 std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::optional<at::Tensor> addend,
                                 bool b_kmajor, int64_t tile, c10::optional<at::Tensor> addend_mask,
                                 c10::optional<at::Tensor> addend2, int64_t H, int64_t W) {
-  TORCH_CHECK(tile >= 0 && tile <= kTile256x64, "gemm_nt: tile config 0..7");
+  TORCH_CHECK(tile >= 0 && tile <= kTile256x256, "gemm_nt: tile config 0..8");
   check_mat(A, "A");
   check_mat(B, "B");
   TORCH_CHECK(A.size(1) == B.size(b_kmajor ? 0 : 1), "gemm_nt: K mismatch");
@@ -538,7 +538,7 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
   }
   at::Tensor C = at::empty({M, N}, A.options());
   at::Tensor S;
-  if (stats) S = at::empty({gemm_nt_stats_rows(M, N, (int)tile), N, 2},
+  if (stats) S = at::empty({gemm_nt_stats_rows(M, N, (int)tile, K), N, 2},
                            A.options().dtype(at::kFloat));
   // split-K only for the fully connected heads' shape class: no epilogue features beyond a bias row
   // (a full addend is a conv dgrad's residual sum, whose bitwise result must not depend on which
@@ -577,7 +577,7 @@ std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at:
   }
   at::Tensor C = at::empty({M, N}, A.options());
   at::Tensor part;
-  const BnBwdArgs bnb = make_bn_bwd(x_bn, ws, mask, mode, M, N, gemm_nt_stats_rows(M, N), part);
+  const BnBwdArgs bnb = make_bn_bwd(x_bn, ws, mask, mode, M, N, gemm_nt_stats_rows(M, N, kTileAuto, K), part);
   launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K, nullptr,
                  current_stream(A), add ? addend->data_ptr() : nullptr, add ? addend->stride(0) : 0, b_kmajor,
                  kTileAuto, &bnb, addend_mask_ptr(addend_mask, M, N, add), addend2_ptr(addend2, M, N, H, W), (int)H,
@@ -747,6 +747,20 @@ at::Tensor stem_wgrad(at::Tensor dy, at::Tensor xs, int64_t H, int64_t W, c10::S
   return dw;
 }
 
+// x[:, :, ::2, ::2] of a channels_last bf16 activation as a compact channels_last tensor (the
+// stride-2 downsample conv's input)
+at::Tensor subsample2(at::Tensor x) {
+  check_act(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.scalar_type() == at::kBFloat16 && x.size(1) % 8 == 0 && x.size(2) % 2 == 0 &&
+                  x.size(3) % 2 == 0,
+              "subsample2: bf16 [N, C % 8, even H, even W]");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK((int64_t)N * (H / 2) * (W / 2) * (C / 8) < (1ll << 32), "subsample2: too large");
+  at::Tensor y = at::empty({N, C, H / 2, W / 2}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_subsample2(x.data_ptr(), y.data_ptr(), N, H, W, C, current_stream(x));
+  return y;
+}
+
 // Global average pooling: x [N, C, H, W] channels_last -> y [N, C] (the flattened head input).
 at::Tensor gap_fwd(at::Tensor x) {
   check_act(x, "x");
@@ -784,7 +798,7 @@ static void check_conv3(const at::Tensor& x, const at::Tensor& w) {
 
 // 3x3 / pad 1 convolution forward (stride 1 or 2). Returns (y, stats-or-undefined).
 std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, bool stats, int64_t tile) {
-  TORCH_CHECK(tile >= 0 && tile <= kTile256x64, "conv3x3: tile config 0..7");
+  TORCH_CHECK(tile >= 0 && tile <= kTile256x256, "conv3x3: tile config 0..8");
   check_conv3(x, w);
   TORCH_CHECK(stride == 1 || stride == 2, "conv3x3: stride 1 or 2");
   TORCH_CHECK(x.size(1) % 64 == 0 || tile_bm(tile) * tile_bn(tile) <= 128 * 128,
@@ -794,7 +808,7 @@ std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, 
   at::Tensor y = at::empty({N, Cout, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor S;
   const int64_t P = (int64_t)N * OH * OW;
-  if (stats) S = at::empty({conv3x3_stats_rows(P, Cout, (int)tile), Cout, 2}, x.options().dtype(at::kFloat));
+  if (stats) S = at::empty({conv3x3_stats_rows(P, Cout, (int)tile, 9 * Cin, Cin % 64 == 0), Cout, 2}, x.options().dtype(at::kFloat));
   launch_conv3x3_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), N, H, W, Cin, Cout, (int)stride,
                      stats ? S.data_ptr<float>() : nullptr, current_stream(x), (int)tile);
   return {y, S};
@@ -802,7 +816,7 @@ std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, 
 
 // stride-1 data gradient (+ optional fused addend, same shape as dx)
 at::Tensor conv3x3_dgrad(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> addend, int64_t tile) {
-  TORCH_CHECK(tile >= 0 && tile <= kTile256x64, "conv3x3: tile config 0..7");
+  TORCH_CHECK(tile >= 0 && tile <= kTile256x256, "conv3x3: tile config 0..8");
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(dy.dim() == 4 && dy.size(1) == w.size(0), "conv3x3_dgrad: dy/w mismatch");
   const int N = (int)dy.size(0), Cout = (int)w.size(0), Cin = (int)w.size(1), H = (int)dy.size(2), W = (int)dy.size(3);
@@ -860,7 +874,7 @@ std::vector<at::Tensor> conv3x3_dgrad_bn(at::Tensor dy, at::Tensor w, c10::optio
   }
   const int64_t P = (int64_t)N * H * W;
   at::Tensor part;
-  const BnBwdArgs bnb = make_bn_bwd(x_bn, ws, mask, mode, P, Cin, conv3x3_stats_rows(P, Cin), part);
+  const BnBwdArgs bnb = make_bn_bwd(x_bn, ws, mask, mode, P, Cin, conv3x3_stats_rows(P, Cin, kTileAuto, 9 * Cout, Cout % 64 == 0), part);
   launch_conv3x3_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, add, current_stream(dy),
                        kTileAuto, &bnb);
   return {dx, part};
@@ -919,6 +933,7 @@ void bind_nn(pybind11::module& m) {
   m.def("bn_dual_fwd", &bn_dual_fwd, "training act(BN(x) + BN_d(xd)) in one apply pass (downsample residual)");
   m.def("bn_dual_bwd", &bn_dual_bwd, "backward of bn_dual_fwd (one dy read for both BatchNorms)");
   m.def("gap_fwd", &gap_fwd, "NHWC global average pooling -> [N, C]");
+  m.def("subsample2", &subsample2, "x[:, :, ::2, ::2] of a channels_last bf16 tensor, compact channels_last");
   m.def("stem_fwd", &stem_fwd, "7x7/s2/p3 stem conv, 3 input channels (space-to-depth + MFMA implicit GEMM, BN-statistics epilogue)");
   m.def("stem_wgrad", &stem_wgrad, "7x7/s2/p3 stem conv weight gradient from the folded input (packed [Cout, 256] layout)");
   m.def("gap_bwd", &gap_bwd, "NHWC global average pooling backward (channels_last dx)");

@@ -25,6 +25,8 @@ def _rel(a, b):
     (2, 16, 28, 28, 32, 1), (2, 96, 28, 28, 128, 1), (2, 96, 14, 14, 208, 1), (2, 24, 14, 14, 64, 1),
     (2, 112, 14, 14, 224, 1), (2, 144, 14, 14, 288, 1), (2, 160, 7, 7, 320, 1), (2, 48, 7, 7, 128, 1),
     (1, 8, 5, 7, 24, 1), (2, 64, 56, 56, 192, 1),
+    # 256x256 8-wave tiles: auto-picked fwd / dgrad (>= 192 tiles, K >= 1024) and the wide wgrad
+    (256, 256, 14, 14, 256, 1), (2, 512, 14, 14, 512, 2),
 ])
 def test_conv3x3_fwd_dgrad_wgrad(cuda, N, Cin, H, W, Cout, stride):
     C = _C()
@@ -96,12 +98,13 @@ def test_conv3x3_asymmetric_weights(cuda, Cin, Cout):
         torch.testing.assert_close(dw.float(), refw, rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3])
-def test_conv3x3_tile_configs(cuda, tile):
+@pytest.mark.parametrize("tile", [1, 2, 3, 8])
+@pytest.mark.parametrize("ch", [128, 256])
+def test_conv3x3_tile_configs(cuda, tile, ch):
     C = _C()
     torch.manual_seed(0)
-    x = torch.randn(2, 128, 14, 14, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
-    w = (torch.randn(128, 128, 3, 3, device=cuda) * 0.05).to(torch.bfloat16).contiguous(memory_format=CL)
+    x = torch.randn(3, ch, 14, 14, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(ch, ch, 3, 3, device=cuda) * 0.05).to(torch.bfloat16).contiguous(memory_format=CL)
     y_ref, s_ref = C.conv3x3_fwd(x, w, 1, True, 1)
     y, s = C.conv3x3_fwd(x, w, 1, True, tile)
     assert torch.equal(y, y_ref)

@@ -41,7 +41,7 @@ def test_gemm_nt_asymmetric_identity(cuda):
 
 
 @pytest.mark.parametrize("K,Mo,No", [(802816, 64, 256), (1000, 64, 64), (12544, 512, 2048), (333, 136, 72),
-                                     (50176, 256, 1024), (131072, 8, 8), (65536, 24, 40), (200704, 64, 64)])
+                                     (50176, 256, 1024), (3333, 512, 256), (131072, 8, 8), (65536, 24, 40), (200704, 64, 64)])
 def test_gemm_tn(cuda, K, Mo, No):
     C = _C()
     torch.manual_seed(0)
@@ -74,8 +74,8 @@ def test_gemm_nt_kmajor_b_and_addend(cuda, M, N, K):
     assert torch.equal(out_d, out + D)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3])
-@pytest.mark.parametrize("M,N,K", [(1000, 64, 256), (777, 136, 72), (4096, 512, 128)])
+@pytest.mark.parametrize("tile", [1, 2, 3, 8])
+@pytest.mark.parametrize("M,N,K", [(1000, 64, 256), (777, 136, 72), (4096, 512, 128), (1300, 520, 640)])
 def test_gemm_nt_tile_configs(cuda, tile, M, N, K):
     C = _C()
     torch.manual_seed(0)

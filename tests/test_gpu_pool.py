@@ -166,3 +166,17 @@ def test_global_avg_pool_matches_torch(cuda, dtype, shape):
     assert x.grad.is_contiguous(memory_format=torch.channels_last)
     torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
     assert _ext.require() is not None
+
+
+@pytest.mark.parametrize("shape", [(2, 256, 56, 56), (3, 8, 6, 10), (1, 1024, 14, 14), (1100, 256, 56, 56)])
+def test_subsample2_matches_strided_copy(cuda, shape):
+    """Native stride-2 subsample (downsample-conv input) == x[:, :, ::2, ::2], bitwise; the last shape
+    has > 2^24 16-byte chunks."""
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = C.subsample2(x)
+    ref = x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last)
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.shape == ref.shape
+    assert torch.equal(y, ref)
