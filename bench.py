@@ -52,9 +52,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    # 512 per GPU: 4.6 % more images/s than 256 on one MI355X (stage-3/4 GEMMs fill the 256 CUs better,
-    # per-step fixed costs amortised), 30 GB of the 288 GB HBM (profiles/batch_sweep_resnet50_n1.jsonl)
-    ap.add_argument("--batch", type=int, default=512, help="per-GPU batch size")
+    # 1024 per GPU, sized for the 288 GB of HBM3E (60 GB peak): the stage-3/4 layers (M = batch x 14^2 or
+    # 7^2 rows) fill the 256 CUs better and per-step fixed costs are amortised, +4.3 % images/s over 512
+    # on one MI355X (profiles/r5f/, same box: 512 -> 12,794-12,819, 768 -> 12,994-13,022, 1024 -> 13,347-
+    # 13,367). 1024 is also the largest batch inside the 24-bit pixel-index limits of the stem kernels.
+    ap.add_argument("--batch", type=int, default=1024, help="per-GPU batch size")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--algorithm", default="builtin", help="native engine all-reduce: builtin|ring|ring_pipe|direct|rsag|central|hier_ring|hier_coll")
     # 8 MiB of bf16 gradients = 16 MiB of fp32 on the wire (fp32 accumulation at N > 1): the cap the
