@@ -677,6 +677,10 @@ int conv3x3_stats_rows(int64_t P, int Cout, int tile, int K, bool wide_ok) {
 
 void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int W, int Cin, int Cout, int stride,
                         float* stats, hipStream_t stream, int tile) {
+  if (tile == kTileAuto && halo_conv_eligible(Cin, Cout, W, stride, true)) {
+    launch_conv3x3_halo(x, w, y, N, H, W, stats, stream);
+    return;
+  }
   const ConvGeom g = make_geom(N, H, W, Cin, Cout, stride);
   const bf16_t* xp = (const bf16_t*)x;
   const bf16_t* wp = (const bf16_t*)w;

@@ -1,0 +1,205 @@
+// Halo-tiled 3x3 / stride-1 / pad-1 convolution for 64 -> 64 channels (ResNet stage 1: conv2 of
+// every bottleneck at 56x56), forward with the fused BatchNorm-statistics epilogue; the data
+// gradient is the same convolution with the flipped, transposed weights (nn_bindings.cpp).
+//
+// Why a separate kernel: the implicit-GEMM path (conv.hip) gathers the A operand tap by tap, so
+// every input pixel crosses L2 -> LDS nine times and every 128-row block also streams the whole
+// 64 x 576 weight matrix. At N = 64 that L2 -> LDS traffic (~2.8 GB per pass at batch 512, about
+// the L2-served gather rate of the chip for the whole pass) and not the MFMA work bounds the layer
+// (profiles/r5e/README.md). Here a block is persistent and owns a contiguous run of 128-pixel
+// strips (flat NHWC order):
+//   * the 73.7 KB weight matrix is DMA'd into LDS once per block (9 tap images in the swizzled
+//     row-major LDS-DMA layout of dla_mfma.h, B fragments by ds_read_b128);
+//   * per strip, the flat input range [p0 - W - 1, p0 + 128 + W + 1) (the strip plus one image row
+//     and one pixel of halo on each side, 242 pixels at W = 56) is DMA'd into one of two 32 KB patch
+//     buffers while the previous strip is multiplied: each input pixel crosses L2 -> LDS ~1.9x
+//     instead of 9x;
+//   * A fragments for tap (kh, kw) are the lane's own pixel shifted by kh * W + kw inside the patch
+//     (XOR-swizzled 16-byte chunks: conflict-free ds_read_b128 for any shift); taps that fall
+//     outside the image (or past the tensor) read a zeroed LDS slot instead;
+//   * the epilogue (bf16 tile through LDS + per-strip BN-statistics partial row) is the shared
+//     epilogue_bf16 / stats_flush, so the partial-row layout equals the 128x64 implicit-GEMM tile's.
+// LDS: 72 KB weights + 2 x 32 KB patches + 18 KB epilogue staging + 128 B zero slot = 154 KB: one
+// 4-wave block per CU, 2x2 waves of 64 x 32 (TM = 4, TN = 2), v_mfma_f32_16x16x32_bf16.
+#include <algorithm>
+
+#include "dla_common.h"
+#include "dla_kernels.h"
+#include "dla_mfma.h"
+
+namespace dla {
+
+using namespace mm;
+
+namespace {
+
+constexpr int kHC = 64;                         // channels in and out
+constexpr int kHBM = 128;                       // pixels per strip
+constexpr int kHNT = 256;                       // threads
+constexpr int kHTapImg = kHC * kBK;             // elements per weight tap image (64 x 64)
+constexpr int kHWBytes = 9 * kHTapImg * 2;      // 73,728
+constexpr int kHPatchBytes = 32768;             // >= (128 + 2 W + 2) * 128 B for W <= 63
+constexpr int kHStageBytes = kHBM * (kHC + 8) * 2;  // epilogue staging, 18,432
+constexpr int kHLds = kHWBytes + 2 * kHPatchBytes + kHStageBytes + 128;
+static_assert(kHLds <= 160 * 1024, "halo conv LDS budget");
+static_assert(kMS == 16, "halo conv fragments assume v_mfma_f32_16x16x32_bf16");
+
+__device__ __forceinline__ int hswz(int s) { return s & 7; }  // chunk XOR of patch pixel s
+
+}  // namespace
+
+template <bool kStats>
+__global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __restrict__ x,
+                                                               const bf16_t* __restrict__ w,
+                                                               bf16_t* __restrict__ y, int H, int W, int P,
+                                                               int nstrips, int per_block,
+                                                               float* __restrict__ stats,
+                                                               const bf16_t* __restrict__ addend) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  using AC = Acc<kHBM, kHC, kHNT>;
+  static_assert(AC::TM == 4 && AC::TN == 2 && AC::WM == 64 && AC::WN == 32, "2x2 waves of 64 x 32");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave / AC::WGN, wc = wave % AC::WGN;
+  const int s_begin = blockIdx.x * per_block;
+  const int s_end = min(nstrips, s_begin + per_block);
+  if (s_begin >= s_end) return;
+
+  char* wimg = smem_raw;
+  char* patch0 = smem_raw + kHWBytes;
+  char* stage = patch0 + 2 * kHPatchBytes;
+  char* zslot = stage + kHStageBytes;
+  const uint32_t lds_w = lds_addr(wimg), lds_p0 = lds_addr(patch0);
+  const uint32_t wofs = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
+  if (tid < 8) reinterpret_cast<ushort8_t*>(zslot)[tid] = zero8();
+
+  // weights: 9 tap images [64 co][64 ci], slot c of image t holds row c >> 3, logical k chunk
+  // rm_glds_kc(c) (the swizzle rm_glds_frag reads back)
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * kHNT;
+      const bf16_t* src = w + (int64_t)(c >> 3) * (9 * kHC) + t * kHC + rm_glds_kc(c);
+      glds16(src, lds_w + (uint32_t)(t * kHTapImg * 2 + i * kHNT * 16) + wofs);
+    }
+
+  const int npx = kHBM + 2 * W + 2;  // patch pixels
+  // patch DMA of strip s into buffer b: slot c = pixel c >> 3, physical chunk c & 7 holding logical
+  // chunk (c & 7) ^ hswz(pixel); pixels outside the tensor (and slots past the patch) read zeros
+  auto issue_patch = [&](int s, int b) {
+    const int64_t q0 = (int64_t)s * kHBM - W - 1;
+#pragma unroll
+    for (int i = 0; i < kHPatchBytes / (16 * kHNT); ++i) {
+      const int c = tid + i * kHNT;
+      const int px = c >> 3;
+      const int64_t q = q0 + px;
+      const int lc = (c & 7) ^ hswz(px);
+      const void* src = (px < npx && q >= 0 && q < P) ? (const void*)(x + q * kHC + lc * 8) : zero_src();
+      glds16(src, lds_p0 + (uint32_t)(b * kHPatchBytes + i * kHNT * 16) + wofs);
+    }
+  };
+  issue_patch(s_begin, 0);
+
+  const char* zfrag = zslot + (lane >> 4) * 16;  // zero A fragment (any logical chunk)
+  for (int s = s_begin; s < s_end; ++s) {
+    const int b = (s - s_begin) & 1;
+    if (s == s_begin) vm_wait<0>();
+    else vm_wait<4>();  // this patch's DMA is older than the previous strip's 4 tile stores
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + 1 < s_end) issue_patch(s + 1, b ^ 1);  // that buffer was last read before this barrier
+
+    const int64_t row0 = (int64_t)s * kHBM;
+    // per A fragment: the lane's output pixel, its patch index and the 9-bit tap validity mask
+    int pidx[AC::TM];
+    uint32_t vmask[AC::TM];
+#pragma unroll
+    for (int i = 0; i < AC::TM; ++i) {
+      const int r = wr * AC::WM + i * 16 + (lane & 15);
+      const int64_t p = row0 + r;
+      const int pp = (int)(p < P ? p : 0);
+      const int q = pp / W, ow = pp - q * W, oh = q % H;
+      uint32_t m = 0;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+          if (p < P && (unsigned)(oh + kh - 1) < (unsigned)H && (unsigned)(ow + kw - 1) < (unsigned)W)
+            m |= 1u << (kh * 3 + kw);
+      vmask[i] = m;
+      pidx[i] = r;
+    }
+    const char* pbuf = patch0 + b * kHPatchBytes;
+    AC acc;
+    acc.zero();
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int off = (t / 3) * W + (t % 3);
+      const bf16_t* wt = reinterpret_cast<const bf16_t*>(wimg + t * kHTapImg * 2);
+#pragma unroll
+      for (int kk = 0; kk < kBK / kKS; ++kk) {
+        bf16x8_t af[AC::TM], bfr[AC::TN];
+        const int lc = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < AC::TM; ++i) {
+          const int sp = pidx[i] + off;
+          const char* a = ((vmask[i] >> t) & 1u) ? pbuf + sp * 128 + ((lc ^ hswz(sp)) << 4) : zfrag;
+          af[i] = *reinterpret_cast<const bf16x8_t*>(a);
+        }
+#pragma unroll
+        for (int j = 0; j < AC::TN; ++j) bfr[j] = rm_glds_frag(wt, wc * AC::WN + j * 16, kk);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < AC::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < AC::TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    ColStats<kHBM, kHC, kHNT> st;
+    st.zero();
+    epilogue_bf16<kHBM, kHC, kStats, false, kHNT>(acc, y, kHC, P, kHC, row0, 0, st, addend, kHC, stage);
+    if constexpr (kStats) stats_flush<kHBM, kHC, kHNT>(st, stats + (int64_t)s * kHC * 2, kHC, 0, stage);
+  }
+}
+
+// DLA_HALO: 0 off, 1 (default) data gradient only, 2 forward and data gradient. Per-layer A/B at
+// ResNet-50 bs512 (profiles/r5h): dgrad 0.22 vs 0.23-0.25 ms, forward 0.24 vs 0.23-0.25 ms (neutral):
+// with one 4-wave block per CU the ds_read latency of each tap is exposed, so the 9x lower L2 -> LDS
+// traffic does not turn into a faster forward.
+static int halo_mode() {
+  static const int v = [] {
+    const char* e = std::getenv("DLA_HALO");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
+bool halo_conv_eligible(int Cin, int Cout, int W, int stride, bool fwd) {
+  return halo_mode() >= (fwd ? 2 : 1) && Cin == kHC && Cout == kHC && stride == 1 && W >= 1 &&
+         2 * W + 2 + kHBM <= 256;
+}
+
+void launch_conv3x3_halo(const void* x, const void* w, void* y, int N, int H, int W, float* stats,
+                         hipStream_t stream, const void* addend) {
+  const int64_t P64 = (int64_t)N * H * W;
+  const int P = (int)P64;
+  const int nstrips = (P + kHBM - 1) / kHBM;
+  if (nstrips == 0) return;
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  const int per_block = (nstrips + cus - 1) / cus;
+  const int grid = (nstrips + per_block - 1) / per_block;
+  if (stats)
+    hipLaunchKernelGGL(conv3x3_halo_kernel<true>, dim3(grid), dim3(kHNT), kHLds, stream, (const bf16_t*)x,
+                       (const bf16_t*)w, (bf16_t*)y, H, W, P, nstrips, per_block, stats, (const bf16_t*)addend);
+  else
+    hipLaunchKernelGGL(conv3x3_halo_kernel<false>, dim3(grid), dim3(kHNT), kHLds, stream, (const bf16_t*)x,
+                       (const bf16_t*)w, (bf16_t*)y, H, W, P, nstrips, per_block, stats, (const bf16_t*)addend);
+}
+
+}  // namespace dla

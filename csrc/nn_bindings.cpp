@@ -833,6 +833,12 @@ at::Tensor conv3x3_dgrad(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> 
                 "conv3x3_dgrad: addend must match dx");
     add = addend->data_ptr();
   }
+  if (tile == 0 && halo_conv_eligible(Cout, Cin, W, 1, false)) {
+    // stride-1 data gradient = the forward conv of dy with W'[ci][kh][kw][co] = W[co][2-kh][2-kw][ci]
+    const at::Tensor wt = w.flip({2, 3}).transpose(0, 1).contiguous(at::MemoryFormat::ChannelsLast);
+    launch_conv3x3_halo(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, H, W, nullptr, current_stream(dy), add);
+    return dx;
+  }
   launch_conv3x3_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, add, current_stream(dy),
                        (int)tile);
   return dx;

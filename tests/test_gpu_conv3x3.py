@@ -133,3 +133,45 @@ def test_conv3x3_pipelines_agree(cuda, pipe, cin):
         C.set_mfma_pipeline(old)
     for r, g in zip(ref, got):
         assert torch.equal(r, g)
+
+
+_HALO_SCRIPT = r"""
+import sys, torch, torch.nn.functional as F
+sys.path.insert(0, %r)
+from distributed_learning_amd.ops import _ext
+C = _ext.require()
+CL = torch.channels_last
+dev = torch.device("cuda:0")
+for N, H, W in [(2, 56, 56), (3, 9, 13), (2, 7, 63), (1, 1, 1), (5, 56, 56)]:
+    torch.manual_seed(0)
+    x = torch.randn(N, 64, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(64, 64, 3, 3, device=dev) * 0.05).to(torch.bfloat16).contiguous(memory_format=CL)
+    y, s = C.conv3x3_fwd(x, w, 1, True, 0)           # halo kernel (DLA_HALO=2)
+    y1, s1 = C.conv3x3_fwd(x, w, 1, True, 1)         # forced 128x128 implicit GEMM
+    assert torch.equal(y, y1), (N, H, W)              # same tap / k order -> bitwise
+    torch.testing.assert_close(s.sum(0), s1.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(y.float(), F.conv2d(x.float(), w.float(), None, 1, 1), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(s.sum(0)[:, 0], y.float().sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    dy = torch.randn_like(y)
+    dx = C.conv3x3_dgrad(dy, w)                       # halo kernel, flipped / transposed weights
+    refx = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), 1, 1)
+    torch.testing.assert_close(dx.float(), refx, rtol=1e-2, atol=2e-2)
+    add = torch.randn_like(x)
+    assert torch.equal(C.conv3x3_dgrad(dy, w, add), dx + add)  # fused addend == unfused bf16 add
+print("halo ok")
+"""
+
+
+def test_conv3x3_halo_c64(cuda):
+    """64 -> 64 channel stride-1 3x3 convs on the halo-tiled persistent kernel, forward and data
+    gradient (a fresh process with DLA_HALO=2, the mode is read once): forward bitwise equal to the
+    implicit-GEMM kernel, statistics and the data gradient against fp32 PyTorch."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DLA_HALO="2")
+    r = subprocess.run([sys.executable, "-c", _HALO_SCRIPT % root], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and "halo ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
