@@ -163,6 +163,162 @@ __global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __r
   }
 }
 
+// Variant 2 (two blocks per CU): the 4 waves split the strip's 64 output channels (wave tile 128 x
+// 16, TM = 8 fragments along M), so each wave's B fragments for all 9 taps fit in VGPRs (9 taps x
+// 2 k-halves = 72 VGPRs per lane, loaded once from L2) and a block needs only one 32 KB patch buffer
+// plus the 18 KB epilogue staging: two blocks share a CU and each SIMD holds two waves of different
+// blocks, whose ds_read latencies and epilogues cover each other. Per strip: compute from the patch
+// -> barrier -> DMA of the next strip's patch into the same buffer -> epilogue (its stores are
+// younger than that DMA, so the next strip waits with a counted vmcnt). A wave owns 16 whole
+// columns, so the BN statistics need no cross-wave combine.
+constexpr int kH2Lds = kHPatchBytes + kHStageBytes;
+
+template <bool kStats>
+__global__ __launch_bounds__(kHNT, 2) void conv3x3_halo_rb_kernel(const bf16_t* __restrict__ x,
+                                                                  const bf16_t* __restrict__ w,
+                                                                  bf16_t* __restrict__ y, int H, int W, int P,
+                                                                  int nstrips, int per_block,
+                                                                  float* __restrict__ stats,
+                                                                  const bf16_t* __restrict__ addend) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  constexpr int TM = kHBM / 16;  // 8 fragments along M per wave
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int s_begin = blockIdx.x * per_block;
+  const int s_end = min(nstrips, s_begin + per_block);
+  if (s_begin >= s_end) return;
+
+  char* patch = smem_raw;
+  bf16_t* Cs = reinterpret_cast<bf16_t*>(smem_raw + kHPatchBytes);
+  const uint32_t lds_p = lds_addr(patch);
+  const uint32_t wofs = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
+
+  const int npx = kHBM + 2 * W + 2;
+  auto issue_patch = [&](int s) {
+    const int64_t q0 = (int64_t)s * kHBM - W - 1;
+#pragma unroll
+    for (int i = 0; i < kHPatchBytes / (16 * kHNT); ++i) {
+      const int c = tid + i * kHNT;
+      const int px = c >> 3;
+      const int64_t q = q0 + px;
+      const int lc = (c & 7) ^ hswz(px);
+      const void* src = (px < npx && q >= 0 && q < P) ? (const void*)(x + q * kHC + lc * 8) : zero_src();
+      glds16(src, lds_p + (uint32_t)(i * kHNT * 16) + wofs);
+    }
+  };
+  issue_patch(s_begin);
+  // B fragments (the layout rm_glds_frag returns): lane -> output channel wave * 16 + (lane & 15),
+  // 8 k values at (lane >> 4) * 8 of the tap's 32-deep half kk
+  bf16x8_t bw[9][2];
+  {
+    const bf16_t* wrow = w + (int64_t)(wave * 16 + (lane & 15)) * (9 * kHC) + (lane >> 4) * 8;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bw[t][kk] = *reinterpret_cast<const bf16x8_t*>(wrow + t * kHC + kk * 32);
+  }
+
+  for (int s = s_begin; s < s_end; ++s) {
+    if (s == s_begin) vm_wait<0>();
+    else vm_wait<4>();  // the patch DMA is older than the previous strip's 4 tile stores
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    const int64_t row0 = (int64_t)s * kHBM;
+    uint32_t vmask[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int64_t p = row0 + i * 16 + (lane & 15);
+      const int pp = (int)(p < P ? p : 0);
+      const int q = pp / W, ow = pp - q * W, oh = q % H;
+      uint32_t m = 0;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+          if (p < P && (unsigned)(oh + kh - 1) < (unsigned)H && (unsigned)(ow + kw - 1) < (unsigned)W)
+            m |= 1u << (kh * 3 + kw);
+      vmask[i] = m;
+    }
+    accv_t acc[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i] = accv_t{};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int off = (t / 3) * W + (t % 3);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8_t af[TM];
+        // fragment i reads patch pixel i * 16 + (lane & 15) + off: the swizzle (pixel & 7) does not
+        // depend on i, so all 8 reads share one address plus an immediate offset of i * 2 KB; taps
+        // outside the image are zeroed after the read (the address stays inside the patch)
+        const int sp0 = (lane & 15) + off;
+        const char* a0 = patch + sp0 * 128 + (((kk * 4 + (lane >> 4)) ^ hswz(sp0)) << 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(a0 + i * 2048);
+          af[i] = ((vmask[i] >> t) & 1u) ? v : bf16x8_t{};
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i] = mfma(af[i], bw[t][kk], acc[i]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    // every wave's patch reads have returned before the next strip's DMA overwrites the buffer
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + 1 < s_end) issue_patch(s + 1);
+
+    // epilogue: bf16 tile -> LDS (pitch 72) -> 16-byte row stores (+ addend); per-column statistics of
+    // the stored values straight from the accumulators (a lane owns one column of each fragment)
+    constexpr int LDC = kHC + 8;
+    const int col = wave * 16 + (lane & 15);
+    float cs = 0.f, cq = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < kAccN; ++r) {
+        const int m = i * 16 + acc_row(lane, r);
+        const bf16_t h = f32_to_bf16(acc[i][r]);
+        Cs[m * LDC + col] = h;
+        if constexpr (kStats) {
+          const float v = (row0 + m < P) ? bf16_to_f32(h) : 0.f;
+          cs += v;
+          cq = fmaf(v, v, cq);
+        }
+      }
+    if constexpr (kStats) {
+      cs += __shfl_xor(cs, 16, kWave);
+      cq += __shfl_xor(cq, 16, kWave);
+      cs += __shfl_xor(cs, 32, kWave);
+      cq += __shfl_xor(cq, 32, kWave);
+      if (lane < 16) {
+        stats[((int64_t)s * kHC + col) * 2 + 0] = cs;
+        stats[((int64_t)s * kHC + col) * 2 + 1] = cq;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kHBM * (kHC / 8) / kHNT; ++it) {
+      const int c = tid + it * kHNT;
+      const int r = c >> 3, cc = (c & 7) * 8;
+      const int64_t gm = row0 + r;
+      if (gm < P) {
+        ushort8_t v = *reinterpret_cast<const ushort8_t*>(Cs + r * LDC + cc);
+        if (addend) {
+          const ushort8_t d = *reinterpret_cast<const ushort8_t*>(addend + gm * kHC + cc);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(d[j]));
+        }
+        *reinterpret_cast<ushort8_t*>(y + gm * kHC + cc) = v;
+      }
+    }
+    __syncthreads();  // staging reads done before the next strip's epilogue writes it
+  }
+}
+
 // DLA_HALO: 0 off, 1 (default) data gradient only, 2 forward and data gradient. Per-layer A/B at
 // ResNet-50 bs512 (profiles/r5h): dgrad 0.22 vs 0.23-0.25 ms, forward 0.24 vs 0.23-0.25 ms (neutral):
 // with one 4-wave block per CU the ds_read latency of each tap is exposed, so the 9x lower L2 -> LDS
@@ -192,14 +348,34 @@ void launch_conv3x3_halo(const void* x, const void* w, void* y, int N, int H, in
     hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     return n > 0 ? n : 256;
   }();
-  const int per_block = (nstrips + cus - 1) / cus;
+  // DLA_HALO_V: 1 (default) the one-block-per-CU variant with LDS-resident weights, 2 the two-blocks-
+  // per-CU variant with VGPR-resident weights
+  static const int ver = [] {
+    const char* e = std::getenv("DLA_HALO_V");
+    return e ? std::atoi(e) : 1;
+  }();
+  const int slots = ver == 1 ? cus : 2 * cus;
+  const int per_block = (nstrips + slots - 1) / slots;
   const int grid = (nstrips + per_block - 1) / per_block;
-  if (stats)
-    hipLaunchKernelGGL(conv3x3_halo_kernel<true>, dim3(grid), dim3(kHNT), kHLds, stream, (const bf16_t*)x,
-                       (const bf16_t*)w, (bf16_t*)y, H, W, P, nstrips, per_block, stats, (const bf16_t*)addend);
-  else
-    hipLaunchKernelGGL(conv3x3_halo_kernel<false>, dim3(grid), dim3(kHNT), kHLds, stream, (const bf16_t*)x,
-                       (const bf16_t*)w, (bf16_t*)y, H, W, P, nstrips, per_block, stats, (const bf16_t*)addend);
+  const bf16_t* xp = (const bf16_t*)x;
+  const bf16_t* wp = (const bf16_t*)w;
+  const bf16_t* ap = (const bf16_t*)addend;
+  bf16_t* yp = (bf16_t*)y;
+  if (ver == 1) {
+    if (stats)
+      hipLaunchKernelGGL(conv3x3_halo_kernel<true>, dim3(grid), dim3(kHNT), kHLds, stream, xp, wp, yp, H, W, P,
+                         nstrips, per_block, stats, ap);
+    else
+      hipLaunchKernelGGL(conv3x3_halo_kernel<false>, dim3(grid), dim3(kHNT), kHLds, stream, xp, wp, yp, H, W, P,
+                         nstrips, per_block, stats, ap);
+  } else {
+    if (stats)
+      hipLaunchKernelGGL(conv3x3_halo_rb_kernel<true>, dim3(grid), dim3(kHNT), kH2Lds, stream, xp, wp, yp, H, W,
+                         P, nstrips, per_block, stats, ap);
+    else
+      hipLaunchKernelGGL(conv3x3_halo_rb_kernel<false>, dim3(grid), dim3(kHNT), kH2Lds, stream, xp, wp, yp, H, W,
+                         P, nstrips, per_block, stats, ap);
+  }
 }
 
 }  // namespace dla

@@ -950,6 +950,13 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("H") = 0, pybind11::arg("W") = 0);
   m.def("gemm_nt_splitk_splits", [](int64_t M, int64_t N, int64_t K) { return gemm_nt_splitk_splits((int)M, (int)N, (int)K); },
         "split count gemm_nt uses for this shape (1 = tile kernel)");
+  m.def("pick_tile", [](int64_t M, int64_t N, int64_t K, bool wide_ok) { return pick_tile(M, (int)N, kTileAuto, (int)K, wide_ok); },
+        "tile config the auto policy picks for an M x N GEMM with reduction K (TileCfg: 1 = 128x128, 2 = 128x64, 8 = 256x256)");
+  m.def("gemm_tn_splits", [](int64_t Mo, int64_t No, int64_t K) { return gemm_tn_splits((int)Mo, (int)No, (int)K); },
+        "split-K count of a weight-gradient gemm_tn launch");
+  m.def("halo_conv_eligible", [](int64_t Cin, int64_t Cout, int64_t W, int64_t stride, bool fwd) {
+        return halo_conv_eligible((int)Cin, (int)Cout, (int)W, (int)stride, fwd); },
+        "whether a 3x3 conv pass runs on the halo-tiled kernel (conv_halo.hip) under the current DLA_HALO mode");
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),
         pybind11::arg("out_dtype") = at::kFloat, pybind11::arg("scale") = 1.0);
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC", pybind11::arg("x"),

@@ -162,16 +162,17 @@ print("halo ok")
 """
 
 
-def test_conv3x3_halo_c64(cuda):
+@pytest.mark.parametrize("version", ["1", "2"])
+def test_conv3x3_halo_c64(cuda, version):
     """64 -> 64 channel stride-1 3x3 convs on the halo-tiled persistent kernel, forward and data
-    gradient (a fresh process with DLA_HALO=2, the mode is read once): forward bitwise equal to the
+    gradient, both kernel variants (a fresh process with DLA_HALO=2, read once): forward bitwise equal to the
     implicit-GEMM kernel, statistics and the data gradient against fp32 PyTorch."""
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, DLA_HALO="2")
+    env = dict(os.environ, DLA_HALO="2", DLA_HALO_V=version)
     r = subprocess.run([sys.executable, "-c", _HALO_SCRIPT % root], env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0 and "halo ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
