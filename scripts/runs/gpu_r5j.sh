@@ -13,9 +13,10 @@ for r in 1 2; do
 done
 grep s56_c2 gpurun_out/r5j/layers_v*_r*.jsonl | cut -c1-200
 for i in 1 2; do
-  for h in 2 1 0; do
-    DLA_HALO=$h timeout -k 10 300 python bench.py > gpurun_out/r5j/bench_h${h}_${i}.log 2>&1 || { tail -20 gpurun_out/r5j/bench_h${h}_${i}.log; exit 1; }
-    echo "halo=$h $(grep -o '"value": [0-9.]*' gpurun_out/r5j/bench_h${h}_${i}.log | head -1)" | tee -a gpurun_out/r5j/ab.txt
+  for cfg in "2 2" "2 1" "1 1" "0 1"; do
+    set -- $cfg
+    DLA_HALO=$1 DLA_HALO_V=$2 timeout -k 10 300 python bench.py > gpurun_out/r5j/bench_h$1v$2_${i}.log 2>&1 || { tail -20 gpurun_out/r5j/bench_h$1v$2_${i}.log; exit 1; }
+    echo "halo=$1 v=$2 $(grep -o '"value": [0-9.]*' gpurun_out/r5j/bench_h$1v$2_${i}.log | head -1)" | tee -a gpurun_out/r5j/ab.txt
   done
 done
 bash scripts/gpu_full.sh
