@@ -5,6 +5,8 @@ set -o pipefail
 mkdir -p gpurun_out/r5j
 timeout -k 10 400 python -u -m pytest tests/test_gpu_conv3x3.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r5j/conv_tests.log 2>&1 || { tail -40 gpurun_out/r5j/conv_tests.log; exit 1; }
 tail -1 gpurun_out/r5j/conv_tests.log
+sed 's/\["1"\])  # variant 2/["1", "2"])  # variant 2/' tests/test_gpu_conv3x3.py > tests/_halo_v2_check.py && timeout -k 10 300 python -u -m pytest tests/_halo_v2_check.py -x -q -k halo --timeout 240 --timeout-method thread > gpurun_out/r5j/halo_v2_test.log 2>&1 || { tail -40 gpurun_out/r5j/halo_v2_test.log; exit 1; }
+tail -1 gpurun_out/r5j/halo_v2_test.log
 for r in 1 2; do
   for v in 0 1 2; do
     if [ $v = 0 ]; then H=0; V=2; else H=2; V=$v; fi
