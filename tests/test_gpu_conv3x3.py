@@ -162,7 +162,7 @@ print("halo ok")
 """
 
 
-@pytest.mark.parametrize("version", ["1"])  # variant 2 (DLA_HALO_V=2) joins once measured on the GPU
+@pytest.mark.parametrize("version", ["1", "2"])
 def test_conv3x3_halo_c64(cuda, version):
     """64 -> 64 channel stride-1 3x3 convs on the halo-tiled persistent kernel, forward and data
     gradient, both kernel variants (a fresh process with DLA_HALO=2, read once): forward bitwise equal to the
