@@ -270,7 +270,7 @@ void launch_gemm_nt_splitk(const void* A, int64_t lda, const void* B, int64_t ld
 int conv3x3_stats_rows(int64_t P, int Cout, int tile = kTileAuto, int K = 0, bool wide_ok = true);
 // halo-tiled 64 -> 64 channel 3x3 / stride-1 conv (conv_halo.hip): persistent strips of 128 pixels,
 // weights resident in LDS; stats partial rows as the 128x64 tile (ceil(P / 128)). DLA_HALO: 0 off,
-// 1 (default) data gradient only, 2 also the forward.
+// 1 data gradient only, 2 (default) also the forward.
 bool halo_conv_eligible(int Cin, int Cout, int W, int stride, bool fwd);
 void launch_conv3x3_halo(const void* x, const void* w, void* y, int N, int H, int W, float* stats,
                          hipStream_t stream, const void* addend = nullptr);

@@ -110,13 +110,11 @@ __global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __r
     if (s + 1 < s_end) issue_patch(s + 1, b ^ 1);  // that buffer was last read before this barrier
 
     const int64_t row0 = (int64_t)s * kHBM;
-    // per A fragment: the lane's output pixel, its patch index and the 9-bit tap validity mask
-    int pidx[AC::TM];
+    // per A fragment: the 9-bit tap validity mask of the lane's output pixel
     uint32_t vmask[AC::TM];
 #pragma unroll
     for (int i = 0; i < AC::TM; ++i) {
-      const int r = wr * AC::WM + i * 16 + (lane & 15);
-      const int64_t p = row0 + r;
+      const int64_t p = row0 + wr * AC::WM + i * 16 + (lane & 15);
       const int pp = (int)(p < P ? p : 0);
       const int q = pp / W, ow = pp - q * W, oh = q % H;
       uint32_t m = 0;
@@ -127,7 +125,6 @@ __global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __r
           if (p < P && (unsigned)(oh + kh - 1) < (unsigned)H && (unsigned)(ow + kw - 1) < (unsigned)W)
             m |= 1u << (kh * 3 + kw);
       vmask[i] = m;
-      pidx[i] = r;
     }
     const char* pbuf = patch0 + b * kHPatchBytes;
     AC acc;
@@ -139,12 +136,15 @@ __global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __r
 #pragma unroll
       for (int kk = 0; kk < kBK / kKS; ++kk) {
         bf16x8_t af[AC::TM], bfr[AC::TN];
-        const int lc = kk * 4 + (lane >> 4);
+        // fragment i reads patch pixel wr * 64 + i * 16 + (lane & 15) + off: the chunk swizzle
+        // (pixel & 7) does not depend on i, so every fragment is one base address plus an immediate
+        // offset of i * 2 KB; a padding tap selects a base that lands on the zero slot instead
+        const int sp0 = wr * AC::WM + (lane & 15) + off;
+        const char* a0 = pbuf + sp0 * 128 + (((kk * 4 + (lane >> 4)) ^ hswz(sp0)) << 4);
 #pragma unroll
         for (int i = 0; i < AC::TM; ++i) {
-          const int sp = pidx[i] + off;
-          const char* a = ((vmask[i] >> t) & 1u) ? pbuf + sp * 128 + ((lc ^ hswz(sp)) << 4) : zfrag;
-          af[i] = *reinterpret_cast<const bf16x8_t*>(a);
+          const char* base = ((vmask[i] >> t) & 1u) ? a0 : zfrag - i * 2048;
+          af[i] = *reinterpret_cast<const bf16x8_t*>(base + i * 2048);
         }
 #pragma unroll
         for (int j = 0; j < AC::TN; ++j) bfr[j] = rm_glds_frag(wt, wc * AC::WN + j * 16, kk);
@@ -319,14 +319,14 @@ __global__ __launch_bounds__(kHNT, 2) void conv3x3_halo_rb_kernel(const bf16_t* 
   }
 }
 
-// DLA_HALO: 0 off, 1 (default) data gradient only, 2 forward and data gradient. Per-layer A/B at
-// ResNet-50 bs512 (profiles/r5h): dgrad 0.22 vs 0.23-0.25 ms, forward 0.24 vs 0.23-0.25 ms (neutral):
-// with one 4-wave block per CU the ds_read latency of each tap is exposed, so the 9x lower L2 -> LDS
-// traffic does not turn into a faster forward.
+// DLA_HALO: 0 off, 1 data gradient only, 2 (default) forward and data gradient. Per-layer A/B at
+// ResNet-50 bs512 (profiles/r5l, after trimming the per-fragment address VALU to one base select):
+// dgrad 0.203-0.220 vs 0.228-0.255 ms, forward 0.225-0.234 vs 0.230-0.252 ms; the forward is
+// bitwise equal to the implicit-GEMM kernel (same tap / k order), so the switch changes no numerics.
 static int halo_mode() {
   static const int v = [] {
     const char* e = std::getenv("DLA_HALO");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 2;
   }();
   return v;
 }

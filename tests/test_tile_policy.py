@@ -43,9 +43,10 @@ def test_gemm_tn_splits_targets():
 
 def test_halo_default_policy():
     C = _ext.require()
-    # default mode (DLA_HALO unset in the test process): data gradient only, 64 -> 64, stride 1, W <= 63
+    # default mode (DLA_HALO unset in the test process): forward and data gradient, 64 -> 64, stride 1,
+    # W <= 63
     assert C.halo_conv_eligible(64, 64, 56, 1, False)
-    assert not C.halo_conv_eligible(64, 64, 56, 1, True)
+    assert C.halo_conv_eligible(64, 64, 56, 1, True)
     assert not C.halo_conv_eligible(128, 128, 28, 1, False)
     assert not C.halo_conv_eligible(64, 64, 56, 2, False)
     assert not C.halo_conv_eligible(64, 64, 64, 1, False)
