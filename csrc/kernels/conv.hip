@@ -550,10 +550,11 @@ __global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void conv3x3_dgrad_k
 }
 
 // stride-2 dgrad: all 4 parity classes in one launch (heaviest class first: 4, 2, 2, 1 taps)
-template <int BM, int BN, int PIPE>
-__global__ __launch_bounds__(kThreads, 2) void conv3x3s2_dgrad_kernel(const bf16_t* __restrict__ dy,
-                                                                      const bf16_t* __restrict__ w,
-                                                                      bf16_t* __restrict__ dx, ConvGeom g) {
+template <int BM, int BN, int PIPE, int NT = kThreads>
+__global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void conv3x3s2_dgrad_kernel(const bf16_t* __restrict__ dy,
+                                                                                      const bf16_t* __restrict__ w,
+                                                                                      bf16_t* __restrict__ dx,
+                                                                                      ConvGeom g) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int64_t P = (int64_t)g.N * g.OH * g.OW;  // class image = dY image
   const int nbn = (g.Cin + BN - 1) / BN;
@@ -565,16 +566,16 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3s2_dgrad_kernel(const bf16
   const int64_t row0 = (int64_t)bm * BM;
   const int col0 = bn * BN;
   const int K = cls.ntaps() * g.Cout;
-  const S2WeightKLoader<BN> lb{w, g.Cout, g.Cin, col0, cls};
-  S2DgradRowLoader<BM> la{dy, g.OH, g.OW, g.Cout, cls};
+  const S2WeightKLoader<BN, NT> lb{w, g.Cout, g.Cin, col0, cls};
+  S2DgradRowLoader<BM, NT> la{dy, g.OH, g.OW, g.Cout, cls};
   la.init(row0, P, g.fOW, g.fOH);
-  ColStats<BM, BN> st;
-  Acc<BM, BN> acc;
+  ColStats<BM, BN, NT> st;
+  Acc<BM, BN, NT> acc;
   acc.zero();
   run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
   const S2RowMap rm{g.OH, g.OW, cls.ph, cls.pw, g.fOW, g.fOH};
-  epilogue_bf16<BM, BN, false, false, kThreads, S2RowMap>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, nullptr, 0,
-                                                         smem_raw, nullptr, 0, rm);
+  epilogue_bf16<BM, BN, false, false, NT, S2RowMap>(acc, dx, g.Cin, P, g.Cin, row0, col0, st, nullptr, 0,
+                                                   smem_raw, nullptr, 0, rm);
 }
 
 // wgrad partial slabs P[split][Cout][9*Cin]
@@ -771,6 +772,17 @@ void launch_conv3x3s2_dgrad(const void* dy, const void* w, void* dx, int N, int 
                             hipStream_t stream) {
   const ConvGeom g = make_geom(N, H, W, Cin, Cout, 2);  // OH = H / 2, OW = W / 2 (H, W even)
   const int64_t P = (int64_t)N * g.OH * g.OW;
+  // 256x256 8-wave tiles (2-stage LDS DMA) at the compute-bound 14x14 / 7x7 shapes (Cin % 256, enough
+  // tiles for the chip), as pick_tile does for the stride-1 passes; DLA_TILE256=0 turns them off
+  if (tile256_enabled() && Cin % 256 == 0 && 4 * ((P + 255) / 256) * (Cin / 256) >= 192) {
+    const int pc = (int)((P + 255) / 256) * (Cin / 256);
+    hipLaunchKernelGGL((conv3x3s2_dgrad_kernel<256, 256, 2, 512>), dim3(4 * pc), dim3(512),
+                       std::max(run_mainloop_lds_bytes<2, 256, 256, S2DgradRowLoader<256, 512>,
+                                                       S2WeightKLoader<256, 512>>(),
+                                epilogue_lds_bytes<256, 256, false, 512>()),
+                       stream, (const bf16_t*)dy, (const bf16_t*)w, (bf16_t*)dx, g);
+    return;
+  }
   const int bn = Cin <= 64 ? 64 : 128;
   const int per_class = (int)((P + 127) / 128) * ((Cin + bn - 1) / bn);
 #define DLA_S2(BN_, P_)                                                                                          \
