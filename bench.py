@@ -9,8 +9,13 @@ on-device synthetic batch generation (Philox kernel) -> bf16-autocast forward (c
 engine's comm stream -> fused multi-tensor SGD-momentum update (fp32 master weights).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--algorithm builtin|ring|direct]
-For N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
-           --master-port P bench.py --gpus N --steps K --warmup W
+For N > 1 either launch it under torchrun (python -m torch.distributed.run --nnodes=1 --nproc-per-node N
+--master-addr 127.0.0.1 --master-port P bench.py --gpus N ...), or run ``python bench.py --gpus N`` as a
+plain command: with no WORLD_SIZE in the environment it starts N ranks itself (a torch.distributed.run
+child process, started before this process touches the GPU), relays rank 0's JSON line and exits with the
+children's status. Asking for more GPUs than the node has is an error, never a silent 1-GPU run.
+(Reference launcher: /root/reference/submit.sh:64 ``mpirun -npernode``; rank -> GPU at
+/root/reference/src/main.py:329-331.)
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -18,6 +23,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
+import subprocess
 import sys
 import time
 
@@ -39,6 +46,7 @@ from distributed_learning_amd.ops.loss import cross_entropy  # noqa: E402
 from distributed_learning_amd.ops.optim import FusedSGD  # noqa: E402
 from distributed_learning_amd.parallel import PipelinedFusedDP, make_reducer  # noqa: E402
 from distributed_learning_amd.parallel import context as ctxmod  # noqa: E402
+from distributed_learning_amd.utils import telemetry  # noqa: E402
 
 # Reference throughput at the same device count (GoogLeNet on P100 + Gloo/IPoIB):
 # N=1 the "single"/Ideal run, N>1 the best published real-DP number (PyTorch DDP).
@@ -80,20 +88,90 @@ def parse():
                          "their data gradient on a side stream (0 = off; default: ops/conv.py)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--momentum", type=float, default=0.5)
+    ap.add_argument("--dry_run", type=int, default=0,
+                    help="1 = launcher/rendezvous check only: ranks join a gloo group on the CPU, meet at a "
+                         "barrier and rank 0 prints who joined (no GPU, no model)")
+    ap.add_argument("--launch_timeout", type=float, default=3000.0,
+                    help="self-launch mode: seconds before the rank processes are killed")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a) -> int:
+    """``--gpus N`` without a WORLD_SIZE: start N ranks as a torch.distributed.run child process.
+
+    Runs before anything initialises the GPU in this process (``torch.cuda.device_count()`` does not, on
+    this image). The child inherits stdout, so rank 0's JSON line is relayed as is; the return value is the
+    launcher's exit status (non-zero if any rank failed), 124 on timeout."""
+    if not a.dry_run:
+        ndev = torch.cuda.device_count()
+        if a.gpus > ndev:
+            print(f"error: --gpus {a.gpus} requested but this node has {ndev} GPU(s); refusing to measure fewer",
+                  file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    p = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        rc = p.wait(timeout=a.launch_timeout)
+    except subprocess.TimeoutExpired:
+        print(f"error: ranks did not finish within {a.launch_timeout:.0f} s; killing them", file=sys.stderr, flush=True)
+        os.killpg(p.pid, signal.SIGTERM)
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+        return 124
+    if rc != 0:
+        print(f"error: rank launcher exited with status {rc}", file=sys.stderr, flush=True)
+    return rc
+
+
+def dry_run(a) -> None:
+    """Rendezvous check of the launch path: every rank joins a gloo group and the barrier."""
+    import datetime
+
+    dist.init_process_group("gloo", init_method="env://", timeout=datetime.timedelta(seconds=120))
+    world, rank = dist.get_world_size(), dist.get_rank()
+    joined = [None] * world
+    dist.all_gather_object(joined, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", 0)),
+                                    "pid": os.getpid()})
+    dist.barrier()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "requested": a.gpus, "ranks_joined": joined}), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ:
+        if a.gpus > 1:
+            sys.exit(launch_ranks(a))
         os.environ["WORLD_SIZE"] = "1"
         os.environ["RANK"] = "0"
         os.environ["LOCAL_RANK"] = "0"
+    if a.dry_run:
+        return dry_run(a)
+    if a.gpus != int(os.environ["WORLD_SIZE"]):
+        print(f"error: --gpus {a.gpus} but WORLD_SIZE {os.environ['WORLD_SIZE']}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if a.gpus > torch.cuda.device_count():
+        print(f"error: --gpus {a.gpus} but this node has {torch.cuda.device_count()} GPU(s)", file=sys.stderr, flush=True)
+        sys.exit(2)
     c = ctxmod.init(backend="nccl")
     world, rank = c.world_size, c.rank
     dev = c.device
-    if a.gpus != world:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
     torch.backends.cudnn.benchmark = True
     dnn.set_backend(a.kernels)
     dnn.set_native_conv(a.conv == "native")
@@ -162,20 +240,34 @@ def main():
         engine.set_timing(False)
         comm_ms_eager = engine.consume_comm_ms()
         step = GraphedStep(step, warmup=2, device=dev)
-    for _ in range(a.warmup):
+    tele = {"before_warmup": telemetry.sample(dev.index or 0)}
+    # one event per step boundary (warmup and timed): the per-step GPU-stream time distribution goes into
+    # the record, so a slow first-steps ramp and a uniformly slow box can be told apart
+    wev = [torch.cuda.Event(enable_timing=True) for _ in range(a.warmup + 1)]
+    wev[0].record()
+    for i in range(a.warmup):
         step()
+        wev[i + 1].record()
     torch.cuda.synchronize()
     engine.consume_comm_ms()
     engine.set_timing(not graphed)
+    tele["before_timed"] = telemetry.sample(dev.index or 0)
+    tev = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    tev[0].record()
+    for i in range(a.steps):
         loss = step()
+        tev[i + 1].record()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    tele["after_timed"] = telemetry.sample(dev.index or 0)
+    warm_ms = [wev[i].elapsed_time(wev[i + 1]) for i in range(a.warmup)]
+    step_ms = sorted(tev[i].elapsed_time(tev[i + 1]) for i in range(a.steps))
+    step_seq = [round(tev[i].elapsed_time(tev[i + 1]), 2) for i in range(a.steps)]
     comm_ms = engine.consume_comm_ms() / max(1, a.steps) if not graphed else comm_ms_eager
     engine.set_timing(False)
     t = torch.tensor([elapsed, comm_ms], dtype=torch.float64, device=dev)
@@ -184,7 +276,9 @@ def main():
     final_loss = float(loss.detach().float())
     ms = elapsed / a.steps * 1000.0
     img_s = a.batch * world * a.steps / elapsed
-    ref = REFERENCE_IMG_S.get(world)
+    # the reference publishes fp32 GoogLeNet numbers only: a ratio against a different model or
+    # a lower precision measures nothing, so vs_baseline is null unless model and precision match
+    ref = REFERENCE_IMG_S.get(world) if (a.model.startswith("googlenet") and a.precision == "fp32") else None
     if rank == 0:
         rec = {
             "metric": f"images/sec (whole node) {MODEL_NAMES.get(a.model, a.model)} synthetic ImageNet",
@@ -216,9 +310,16 @@ def main():
                 "force_comm": bool(a.force_comm),
             },
             "allreduce_ms_per_step": round(comm_ms, 3),
+            "comm_world": int(engine.impl.world()),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
             "final_loss": round(final_loss, 4),
-            "baseline_ref": {"value": ref, "what": "reference best published img/s at this N (GoogLeNet, P100, Gloo)"},
+            "baseline_ref": {"value": REFERENCE_IMG_S.get(world),
+                             "what": "reference best published img/s at this N (GoogLeNet fp32, P100, Gloo); "
+                                     "not comparable unless model=googlenet and precision=fp32"},
+            "step_ms": {"p50": round(step_ms[len(step_ms) // 2], 3), "min": round(step_ms[0], 3),
+                        "max": round(step_ms[-1], 3), "seq": step_seq if a.steps <= 200 else None},
+            "warmup_step_ms": [round(x, 2) for x in warm_ms],
+            "telemetry": tele,
         }
         print(json.dumps(rec), flush=True)
     prof_out = os.environ.get("DLA_TORCH_PROF")
