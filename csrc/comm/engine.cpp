@@ -47,6 +47,7 @@
 #include "dla_kernels.h"
 #include "dla_tables.h"
 #include "plan.h"
+#include "plan_exec.h"
 #include "vexec.h"
 
 namespace dla {
@@ -106,7 +107,7 @@ static Topology make_topology(int rank, int world, std::vector<std::vector<int>>
 // Plans are float-agnostic; these algorithms need the reduce kernel (fp32 / bf16 only).
 static bool needs_reduce_kernel(int algo) {
   return algo == comm::kRing || algo == comm::kDirect || algo == comm::kCentral || algo == comm::kHierRing ||
-         algo == comm::kRingPipe;
+         algo == comm::kRingPipe || algo == comm::kHierCentral;
 }
 
 static double comm_timeout_s() {
@@ -159,7 +160,6 @@ class CommEngine {
     }
     for (auto& e : timing_events_) hipEventDestroy(e);
     for (auto& e : ready_pool_) hipEventDestroy(e);
-    for (auto& e : plan_events_) hipEventDestroy(e);
     if (last_done_) hipEventDestroy(last_done_);
   }
 
@@ -416,9 +416,7 @@ class CommEngine {
   bool staged(int algo, int dtype) const { return accum_fp32_ && dtype == kBF16 && (topo_.world > 1 || force_); }
 
   size_t scratch_bytes(const Plan& p, int64_t n, int dtype) const {
-    const bool st = staged(p.algo, dtype);
-    const size_t esz = (st || dtype == kF32) ? 4 : 2;
-    return ((size_t)p.scratch_elems + (st ? (size_t)((n + 63) / 64 * 64) : 0)) * esz + 512;
+    return comm::staged_scratch_bytes(p.scratch_elems, n, staged(p.algo, dtype), dtype);
   }
 
   void ensure_scratch(size_t bytes) {
@@ -435,11 +433,16 @@ class CommEngine {
     scratch_ = at::empty({(int64_t)want}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, device_));
   }
 
+  // Sub-communicators exist only when both levels have more than one member (ctor): with one GPU per
+  // node (L == 1) the inter-node group IS the world, with one node (K == 1) the intra-node group is.
   ncclComm_t comm_of(comm::CommId c) const {
-    if (c == comm::kIntra) return intra_ ? intra_ : comm_;
+    if (c == comm::kIntra) {
+      TORCH_CHECK(intra_ || topo_.nodes() == 1, "CommEngine: intra-node communicator missing");
+      return intra_ ? intra_ : comm_;
+    }
     if (c == comm::kInter) {
-      TORCH_CHECK(inter_, "CommEngine: inter-node communicator missing");
-      return inter_;
+      TORCH_CHECK(inter_ || topo_.L() == 1, "CommEngine: inter-node communicator missing");
+      return inter_ ? inter_ : comm_;
     }
     return comm_;
   }
@@ -459,125 +462,80 @@ class CommEngine {
     const Plan& plan = plan_for(algo, n);
     const bool stg = staged(algo, dt) && (flat.scalar_type() == at::kBFloat16);
     ensure_scratch(scratch_bytes(plan, n, dt));
-    char* sbase = static_cast<char*>(scratch_.data_ptr());
-    if (!stg) {
-      if (grads) pack_tensors_on(*grads, *offsets, flat, 1.f, st);
-      run_plan(plan, static_cast<char*>(flat.data_ptr()), sbase, flat.element_size(),
-               nccl_dtype_of(flat.scalar_type()), dt, average, st);
-      return;
-    }
-    // fp32 accumulation of a bf16 bucket: gather / cast into fp32 staging, reduce in fp32 on the
-    // wire and in the reduce kernels, round to bf16 once at the end.
-    const int64_t n64 = (n + 63) / 64 * 64;
-    char* stage = sbase;
+    const comm::StagedLayout lay =
+        comm::staged_layout(flat.data_ptr(), dt, flat.element_size(), static_cast<char*>(scratch_.data_ptr()), n, stg);
+    // fp32 accumulation of a bf16 bucket: gather / cast into the fp32 staging buffer, reduce in fp32
+    // on the wire and in the reduce kernels, round to bf16 once at the end.
     if (grads) {
-      at::Tensor sv = at::from_blob(stage, {n}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device_));
-      pack_tensors_on(*grads, *offsets, sv, 1.f, st);
-    } else {
-      launch_cast(stage, kF32, flat.data_ptr(), kBF16, n, 1.f, st);
+      at::Tensor dst = stg ? at::from_blob(lay.data, {n}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device_))
+                           : flat;
+      pack_tensors_on(*grads, *offsets, dst, 1.f, st);
+    } else if (stg) {
+      launch_cast(lay.data, kF32, flat.data_ptr(), kBF16, n, 1.f, st);
     }
-    run_plan(plan, stage, sbase + n64 * 4, 4, ncclFloat32, kF32, average, st);
-    launch_cast(flat.data_ptr(), kBF16, stage, kF32, n, 1.f, st);
+    RcclTransport tr{*this, plan, lay, stg ? ncclFloat32 : nccl_dtype_of(flat.scalar_type()), average,
+                     comm::LocalIssuer(lay.dt, lay.esz)};
+    comm::execute_plan(tr, plan, st, plan_events_);
+    if (stg) launch_cast(flat.data_ptr(), kBF16, lay.data, kF32, n, 1.f, st);
   }
 
-  hipEvent_t plan_event(size_t i) {
-    while (plan_events_.size() <= i) {
-      hipEvent_t e;
-      DLA_HIP_THROW(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      plan_events_.push_back(e);
+  // The RCCL transport of plan_exec.h: collectives and P2P groups on this rank's communicators,
+  // local ops through the multi-lane issuer.
+  struct RcclTransport {
+    CommEngine& e;
+    const Plan& p;
+    comm::StagedLayout lay;
+    ncclDataType_t ndt;
+    bool average;
+    comm::LocalIssuer iss;
+    void* ptr(const comm::Ref& r) const { return (r.buf == comm::kData ? lay.data : lay.scratch) + (size_t)r.off * lay.esz; }
+    void coll(size_t k, hipStream_t st) {
+      const comm::Op& o = p.steps[k].ops[0];
+      ncclComm_t c = e.comm_of(o.comm);
+      // plans are built for averaging; a summing call keeps ncclSum
+      const ncclRedOp_t red = (o.average && average) ? ncclAvg : ncclSum;
+      switch (o.coll) {
+        case comm::kAllReduce:
+          DLA_NCCL_CHECK(ncclAllReduce(ptr(o.src[0]), ptr(o.dst), o.count, ndt, red, c, st));
+          break;
+        case comm::kReduceScatter:
+          DLA_NCCL_CHECK(ncclReduceScatter(ptr(o.src[0]), ptr(o.dst), o.count, ndt, red, c, st));
+          break;
+        case comm::kAllGather:
+          DLA_NCCL_CHECK(ncclAllGather(ptr(o.src[0]), ptr(o.dst), o.count, ndt, c, st));
+          break;
+      }
     }
-    return plan_events_[i];
-  }
+    void transfers(size_t k, hipStream_t st) {
+      bool group = false;
+      for (const auto& o : p.steps[k].ops) {
+        if (o.kind != comm::kSend && o.kind != comm::kRecv) continue;
+        if (!group) {
+          DLA_NCCL_CHECK(ncclGroupStart());
+          group = true;
+        }
+        if (o.kind == comm::kSend)
+          DLA_NCCL_CHECK(ncclSend(ptr(o.src[0]), o.count, ndt, o.peer, e.comm_, st));
+        else
+          DLA_NCCL_CHECK(ncclRecv(ptr(o.dst), o.count, ndt, o.peer, e.comm_, st));
+      }
+      if (group) DLA_NCCL_CHECK(ncclGroupEnd());
+    }
+    bool has_local(size_t k) const {
+      return std::any_of(p.steps[k].ops.begin(), p.steps[k].ops.end(), comm::is_local);
+    }
+    void locals(size_t k, hipStream_t ls) {
+      iss.set_stream(ls);
+      comm::issue_locals(p.steps[k], [&](const comm::Ref& r) { return ptr(r); }, iss, average);
+      iss.flush();
+    }
+    hipStream_t side_stream() { return e.side_stream(); }
+  };
 
   hipStream_t side_stream() {
     if (!side_)
       side_ = std::make_unique<c10::hip::HIPStream>(c10::hip::getStreamFromPool(/*isHighPriority=*/true, device_));
     return side_->stream();
-  }
-
-  // Runs a Plan on stream `st`. Local ops of a step whose successor has Step::overlap_prev go to
-  // the side stream, after an event that marks the step's group on `st`, so they run concurrently
-  // with the successor's group; a group waits (event) for the side work of every step before its
-  // predecessor, a step without the flag for all of it, and `st` joins the side stream at the end.
-  void run_plan(const Plan& p, char* data, char* scratch, size_t esz, ncclDataType_t ndt, int dt, bool average,
-                hipStream_t st) {
-    auto ptr = [&](const comm::Ref& r) { return (r.buf == comm::kData ? data : scratch) + (size_t)r.off * esz; };
-    size_t nev = 0;
-    std::vector<hipEvent_t> side_done(p.steps.size(), nullptr);  // recorded on the side stream after step k's locals
-    long side_last = -1, side_joined = -1;                       // newest side step / newest one `st` waited for
-    auto join_side_upto = [&](long k) {
-      for (long j = std::min(k, side_last); j > side_joined; --j)
-        if (side_done[j]) {
-          DLA_HIP_THROW(hipStreamWaitEvent(st, side_done[j], 0));
-          side_joined = j;
-          break;
-        }
-    };
-    for (size_t k = 0; k < p.steps.size(); ++k) {
-      const auto& step = p.steps[k];
-      join_side_upto(step.overlap_prev ? (long)k - 2 : (long)k - 1);
-      if (step.is_coll()) {
-        const comm::Op& o = step.ops[0];
-        ncclComm_t c = comm_of(o.comm);
-        // plans are built for averaging; a summing call keeps ncclSum
-        const ncclRedOp_t red = (o.average && average) ? ncclAvg : ncclSum;
-        switch (o.coll) {
-          case comm::kAllReduce:
-            DLA_NCCL_CHECK(ncclAllReduce(ptr(o.src[0]), ptr(o.dst), o.count, ndt, red, c, st));
-            break;
-          case comm::kReduceScatter:
-            DLA_NCCL_CHECK(ncclReduceScatter(ptr(o.src[0]), ptr(o.dst), o.count, ndt, red, c, st));
-            break;
-          case comm::kAllGather:
-            DLA_NCCL_CHECK(ncclAllGather(ptr(o.src[0]), ptr(o.dst), o.count, ndt, c, st));
-            break;
-        }
-        continue;
-      }
-      bool group = false;
-      for (const auto& o : step.ops) {
-        if (o.kind == comm::kSend || o.kind == comm::kRecv) {
-          if (!group) {
-            DLA_NCCL_CHECK(ncclGroupStart());
-            group = true;
-          }
-          if (o.kind == comm::kSend)
-            DLA_NCCL_CHECK(ncclSend(ptr(o.src[0]), o.count, ndt, o.peer, comm_, st));
-          else
-            DLA_NCCL_CHECK(ncclRecv(ptr(o.dst), o.count, ndt, o.peer, comm_, st));
-        }
-      }
-      if (group) DLA_NCCL_CHECK(ncclGroupEnd());
-      const bool has_local = std::any_of(step.ops.begin(), step.ops.end(), [](const comm::Op& o) {
-        return o.kind == comm::kReduce || o.kind == comm::kCopy || o.kind == comm::kZero;
-      });
-      if (!has_local) continue;
-      hipStream_t ls = st;
-      if (k + 1 < p.steps.size() && p.steps[k + 1].overlap_prev) {
-        ls = side_stream();
-        hipEvent_t g = plan_event(nev++);
-        DLA_HIP_THROW(hipEventRecord(g, st));
-        DLA_HIP_THROW(hipStreamWaitEvent(ls, g, 0));
-      }
-      for (const auto& o : step.ops) {
-        if (o.kind == comm::kReduce) {
-          ReduceSrcs rs{};
-          rs.count = o.nsrc;
-          for (int i = 0; i < o.nsrc; ++i) rs.ptr[i] = ptr(o.src[i]);
-          launch_reduce_sum(ptr(o.dst), o.accumulate, rs, o.count, dt, average ? o.scale : 1.f, ls);
-        } else if (o.kind == comm::kCopy) {
-          DLA_HIP_THROW(hipMemcpyAsync(ptr(o.dst), ptr(o.src[0]), (size_t)o.count * esz, hipMemcpyDeviceToDevice, ls));
-        } else if (o.kind == comm::kZero) {
-          DLA_HIP_THROW(hipMemsetAsync(ptr(o.dst), 0, (size_t)o.count * esz, ls));
-        }
-      }
-      if (ls != st) {
-        side_done[k] = plan_event(nev++);
-        DLA_HIP_THROW(hipEventRecord(side_done[k], ls));
-        side_last = (long)k;
-      }
-    }
-    join_side_upto((long)p.steps.size());
   }
 
   int device_;
@@ -591,7 +549,7 @@ class CommEngine {
   std::map<std::pair<int, int64_t>, Plan> plans_;
   at::Tensor scratch_;
   std::vector<hipEvent_t> ready_pool_;
-  std::vector<hipEvent_t> plan_events_;
+  comm::EventPool plan_events_;
   std::unique_ptr<c10::hip::HIPStream> side_;
   size_t ready_next_ = 0;
   hipEvent_t last_done_ = nullptr;
@@ -603,52 +561,16 @@ class CommEngine {
 // ---------------------------------------------------------------------------------------------
 // Virtual ranks: N ranks' buffers in one process, links = copies (vexec.h)
 // ---------------------------------------------------------------------------------------------
+// Device backend of the virtual ranks: every link copy and local op goes through the engine's
+// LocalIssuer (so one step's transfers of all ranks are one multi-lane copy launch, the way one
+// RCCL group carries them), and the step sequencing is the engine's own execute_plan.
 struct DeviceBackend {
-  static constexpr bool kConcurrent = true;
   std::vector<char*> data, scratch;
   size_t esz = 4;
   int dt = kF32;
-  hipStream_t st = nullptr;    // current queue of the ops below
-  hipStream_t main = nullptr;  // the caller's stream
-  hipStream_t side = nullptr;  // overlapped local ops (created on first use)
-  std::unique_ptr<c10::hip::HIPStream> side_holder;
-  int device = 0;
-  std::vector<hipEvent_t> events;
-  std::map<size_t, hipEvent_t> side_done;
+  comm::LocalIssuer* iss = nullptr;
   at::TensorOptions opts;
   std::vector<at::Tensor> temps;
-
-  ~DeviceBackend() {
-    for (auto e : events) hipEventDestroy(e);
-  }
-  hipEvent_t event() {
-    hipEvent_t e;
-    DLA_HIP_THROW(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    events.push_back(e);
-    return e;
-  }
-  void side_begin() {
-    if (!side) {
-      side_holder = std::make_unique<c10::hip::HIPStream>(c10::hip::getStreamFromPool(true, device));
-      side = side_holder->stream();
-    }
-    hipEvent_t e = event();
-    DLA_HIP_THROW(hipEventRecord(e, main));
-    DLA_HIP_THROW(hipStreamWaitEvent(side, e, 0));
-    st = side;
-  }
-  void side_end(size_t tag) {
-    hipEvent_t e = event();
-    DLA_HIP_THROW(hipEventRecord(e, side));
-    side_done[tag] = e;
-    st = main;
-  }
-  void main_wait(size_t tag) {
-    auto it = side_done.upper_bound(tag);  // newest side batch with a tag <= `tag`
-    if (it == side_done.begin()) return;
-    --it;
-    DLA_HIP_THROW(hipStreamWaitEvent(main, it->second, 0));
-  }
 
   void* ptr(int rank, const comm::Ref& r) {
     return (r.buf == comm::kData ? data[rank] : scratch[rank]) + (size_t)r.off * esz;
@@ -658,27 +580,51 @@ struct DeviceBackend {
     temps.push_back(at::empty({(int64_t)((size_t)n * esz + 256)}, opts));
     return temps.back().data_ptr();
   }
-  void copy(void* dst, const void* src, int64_t n) {
-    if (n > 0 && dst != src) DLA_HIP_THROW(hipMemcpyAsync(dst, src, (size_t)n * esz, hipMemcpyDeviceToDevice, st));
-  }
-  void zero(void* dst, int64_t n) {
-    if (n > 0) DLA_HIP_THROW(hipMemsetAsync(dst, 0, (size_t)n * esz, st));
-  }
+  void copy(void* dst, const void* src, int64_t n) { iss->copy(dst, src, n); }
+  void zero(void* dst, int64_t n) { iss->zero(dst, n); }
   void reduce(void* dst, bool acc, const void* const* srcs, int nsrc, int64_t n, float scale) {
-    ReduceSrcs rs{};
-    rs.count = nsrc;
-    for (int i = 0; i < nsrc; ++i) rs.ptr[i] = srcs[i];
-    launch_reduce_sum(dst, acc, rs, n, dt, scale, st);
+    iss->reduce(dst, acc, srcs, nsrc, n, scale);
+  }
+};
+
+// Transport of plan_exec.h over N virtual ranks: the P2P group of a step becomes the matched copies
+// of all ranks (validated by VirtualRun), collectives are emulated per communicator colour.
+struct VirtualTransport {
+  comm::VirtualRun<DeviceBackend>& run;
+  comm::LocalIssuer& iss;
+  int device;
+  std::unique_ptr<c10::hip::HIPStream> side;
+  void coll(size_t s, hipStream_t st) {
+    iss.set_stream(st);
+    run.coll(s);
+    iss.flush();
+  }
+  void transfers(size_t s, hipStream_t st) {
+    iss.set_stream(st);
+    run.transfers(s);
+    iss.flush();
+  }
+  bool has_local(size_t s) const { return run.has_local(s); }
+  void locals(size_t s, hipStream_t ls) {
+    iss.set_stream(ls);
+    run.locals(s);
+    iss.flush();
+  }
+  hipStream_t side_stream() {
+    if (!side) side = std::make_unique<c10::hip::HIPStream>(c10::hip::getStreamFromPool(true, device));
+    return side->stream();
   }
 };
 
 // All-reduce `bufs` (one tensor per virtual rank, same numel / dtype / device) in place with the
 // schedules CommEngine would run for that many ranks. CUDA tensors run on the current stream
-// (copies + reduce kernels); CPU tensors on the host backend. accum_fp32 stages bf16 buffers in
-// fp32 exactly like CommEngine (gather/cast, fp32 plan, round once).
-static void virtual_allreduce(std::vector<at::Tensor> bufs, int algo, bool average, std::vector<std::vector<int>> rings,
-                              int local_size, std::vector<std::vector<int>> local_rings,
-                              std::vector<std::vector<int>> node_rings, bool accum_fp32) {
+// through the engine's issuing code (execute_plan, LocalIssuer, StagedLayout); CPU tensors on the
+// serial host backend. accum_fp32 stages bf16 buffers in fp32 exactly like CommEngine (cast into
+// the front of each rank's scratch, fp32 plan behind it, round once). Returns the number of kernel
+// launches the local ops and links took (0 on the host).
+static int64_t virtual_allreduce(std::vector<at::Tensor> bufs, int algo, bool average, std::vector<std::vector<int>> rings,
+                                 int local_size, std::vector<std::vector<int>> local_rings,
+                                 std::vector<std::vector<int>> node_rings, bool accum_fp32) {
   const int N = (int)bufs.size();
   TORCH_CHECK(N >= 1, "virtual_allreduce: no buffers");
   const int64_t n = bufs[0].numel();
@@ -690,7 +636,7 @@ static void virtual_allreduce(std::vector<at::Tensor> bufs, int algo, bool avera
   }
   TORCH_CHECK(dtype == at::kFloat || dtype == at::kBFloat16, "virtual_allreduce: fp32 / bf16 only");
   TORCH_CHECK(algo >= comm::kBuiltin && algo < comm::kAlgoCount, "virtual_allreduce: unknown algorithm ", algo);
-  if (N == 1 || n == 0) return;
+  if (N == 1 || n == 0) return 0;
   std::vector<Plan> plans;
   Topology t0 = make_topology(0, N, rings, local_size, local_rings, node_rings);
   for (int r = 0; r < N; ++r) {
@@ -703,37 +649,41 @@ static void virtual_allreduce(std::vector<at::Tensor> bufs, int algo, bool avera
     }
   }
   const bool stage = accum_fp32 && dtype == at::kBFloat16;
-  std::vector<at::Tensor> work = bufs;
   if (cuda) {
-    c10::hip::HIPGuard guard((c10::DeviceIndex)bufs[0].device().index());
-    hipStream_t st = c10::hip::getCurrentHIPStream(bufs[0].device().index()).stream();
-    if (stage) {
-      for (int r = 0; r < N; ++r) {
-        work[r] = at::empty({n}, bufs[r].options().dtype(at::kFloat));
-        launch_cast(work[r].data_ptr(), kF32, bufs[r].data_ptr(), kBF16, n, 1.f, st);
-      }
-    }
+    const int dev = bufs[0].device().index();
+    c10::hip::HIPGuard guard((c10::DeviceIndex)dev);
+    hipStream_t st = c10::hip::getCurrentHIPStream(dev).stream();
+    const int dt = dtype == at::kBFloat16 ? kBF16 : kF32;
     DeviceBackend be;
-    be.esz = work[0].element_size();
-    be.dt = work[0].scalar_type() == at::kBFloat16 ? kBF16 : kF32;
-    be.st = be.main = st;
-    be.device = bufs[0].device().index();
     be.opts = at::TensorOptions().dtype(at::kByte).device(bufs[0].device());
     std::vector<at::Tensor> scr;
+    std::vector<comm::StagedLayout> lay;
     for (int r = 0; r < N; ++r) {
-      scr.push_back(at::empty({(int64_t)((size_t)plans[r].scratch_elems * be.esz + 256)}, be.opts));
-      be.data.push_back(static_cast<char*>(work[r].data_ptr()));
-      be.scratch.push_back(static_cast<char*>(scr.back().data_ptr()));
+      scr.push_back(at::empty({(int64_t)comm::staged_scratch_bytes(plans[r].scratch_elems, n, stage, dt)}, be.opts));
+      lay.push_back(comm::staged_layout(bufs[r].data_ptr(), dt, bufs[r].element_size(),
+                                        static_cast<char*>(scr.back().data_ptr()), n, stage));
+      if (stage) launch_cast(lay[r].data, kF32, bufs[r].data_ptr(), kBF16, n, 1.f, st);
+      be.data.push_back(lay[r].data);
+      be.scratch.push_back(lay[r].scratch);
     }
+    be.esz = lay[0].esz;
+    be.dt = lay[0].dt;
+    comm::LocalIssuer iss(be.dt, be.esz);
+    be.iss = &iss;
     comm::VirtualRun<DeviceBackend> run(plans, t0, be);
+    comm::EventPool ev;
+    VirtualTransport tr{run, iss, dev, nullptr};
     try {
-      run.run();
+      run.validate();
+      comm::execute_plan(tr, plans[0], st, ev);
     } catch (const std::exception& e) {
       TORCH_CHECK(false, e.what());
     }
     if (stage)
-      for (int r = 0; r < N; ++r) launch_cast(bufs[r].data_ptr(), kBF16, work[r].data_ptr(), kF32, n, 1.f, st);
-    return;
+      for (int r = 0; r < N; ++r) launch_cast(bufs[r].data_ptr(), kBF16, lay[r].data, kF32, n, 1.f, st);
+    // temporaries of the emulated collectives are freed with `be`: their last use is queued on `st`
+    // (the side stream only runs plan-local ops on rank buffers), which the caching allocator orders
+    return iss.launches();
   }
   comm::HostBackend be;
   std::vector<std::vector<char>> stage_mem, scr;
@@ -765,6 +715,7 @@ static void virtual_allreduce(std::vector<at::Tensor> bufs, int algo, bool avera
       for (int64_t i = 0; i < n; ++i) b[i] = comm::HostBackend::f2b(f[i]);
     }
   }
+  return 0;
 }
 
 static std::string plan_describe(int algo, int rank, int world, int64_t n, std::vector<std::vector<int>> rings,
@@ -827,6 +778,7 @@ void bind_comm(pybind11::module& m) {
   m.attr("ALGO_HIER_RING") = (int)comm::kHierRing;
   m.attr("ALGO_HIER_COLL") = (int)comm::kHierColl;
   m.attr("ALGO_RING_PIPE") = (int)comm::kRingPipe;
+  m.attr("ALGO_HIER_CENTRAL") = (int)comm::kHierCentral;
 }
 
 }  // namespace dla

@@ -288,6 +288,43 @@ void append_central(Plan& p, const std::vector<int>& members, int me, int64_t ba
   p.steps.push_back(std::move(s2));
 }
 
+// Central (parameter-server) all-reduce of several lanes at once: member 0 receives every member's
+// copy of every lane, sums them in member order (allreduce.py:30-32) and sends the result back; two
+// steps whatever the lane count.
+void append_central_lanes(Plan& p, const std::vector<int>& members, int me, const std::vector<Lane>& lanes, float scale) {
+  const int M = (int)members.size();
+  if (M <= 1) return;
+  int64_t mx = 1;
+  for (const auto& l : lanes) mx = std::max(mx, l.len);
+  const int64_t slot = round_up(mx, kAlign);
+  Step s1, s2;
+  if (me == 0) {
+    p.scratch_elems = std::max(p.scratch_elems, slot * (M - 1) * (int64_t)lanes.size());
+    auto at = [&](size_t c, int r) { return scratch(((int64_t)c * (M - 1) + (r - 1)) * slot); };
+    for (size_t c = 0; c < lanes.size(); ++c)
+      if (lanes[c].len > 0)
+        for (int r = 1; r < M; ++r) s1.ops.push_back(p2p(kRecv, members[r], at(c, r), lanes[c].len));
+    for (size_t c = 0; c < lanes.size(); ++c) {
+      if (lanes[c].len <= 0) continue;
+      int r = 1;
+      while (r < M) {
+        std::vector<Ref> srcs;
+        while (r < M && (int)srcs.size() < kPlanMaxSrc) srcs.push_back(at(c, r++));
+        s1.ops.push_back(reduce_op(data(lanes[c].off), srcs, lanes[c].len, true, r >= M ? scale : 1.f));
+      }
+      for (int q = 1; q < M; ++q) s2.ops.push_back(p2p(kSend, members[q], data(lanes[c].off), lanes[c].len));
+    }
+  } else {
+    for (const auto& l : lanes)
+      if (l.len > 0) {
+        s1.ops.push_back(p2p(kSend, members[0], data(l.off), l.len));
+        s2.ops.push_back(p2p(kRecv, members[0], data(l.off), l.len));
+      }
+  }
+  p.steps.push_back(std::move(s1));
+  p.steps.push_back(std::move(s2));
+}
+
 // ReduceScatter / (AllReduce of the shard) / AllGather on RCCL collectives. `L` members in the
 // comm that reduce-scatters (kWorld for the flat algorithm, kIntra for the 2-step one), `lr` my
 // index there. n not divisible by L is staged through zero-padded scratch.
@@ -336,6 +373,7 @@ const char* algo_name(int algo) {
     case kHierRing: return "hier_ring";
     case kHierColl: return "hier_coll";
     case kRingPipe: return "ring_pipe";
+    case kHierCentral: return "hier_central";
     default: return "?";
   }
 }
@@ -405,7 +443,8 @@ Plan build_plan(int algo, const Topology& t, int64_t n, float avg) {
     case kCentral:
       append_central(p, world_members, t.rank, 0, n, avg);
       break;
-    case kHierRing: {
+    case kHierRing:
+    case kHierCentral: {
       const int L = t.L(), K = t.nodes();
       const int node = t.rank / L, lr = t.rank % L;
       std::vector<int> intra(L), inter(K);
@@ -424,7 +463,10 @@ Plan build_plan(int algo, const Topology& t, int64_t n, float avg) {
         } else {
           shards = channel_lanes(0, n, norders);
         }
-        append_ring_allreduce(p, inter, node, shards, average ? 1.f / (float)K : 1.f);
+        if (algo == kHierCentral)
+          append_central_lanes(p, inter, node, shards, average ? 1.f / (float)K : 1.f);
+        else
+          append_ring_allreduce(p, inter, node, shards, average ? 1.f / (float)K : 1.f);
       }
       if (L > 1) append_ring_ag(p, intra, lr, lanes);
       break;

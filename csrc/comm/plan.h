@@ -38,7 +38,10 @@ enum Algo : int {
   kHierColl = 6,  // 2-step on sub-communicators: intra ncclReduceScatter -> inter ncclAllReduce -> intra ncclAllGather
   kRingPipe = 7,  // ring whose reduce-scatter runs in two half-chunk sub-steps: the reduce kernel of
                   // one half overlaps the P2P transfer of the other (double-buffered scratch slots)
-  kAlgoCount = 8,
+  kHierCentral = 8,  // 2-step with a parameter server between nodes: intra RS -> the owned shards summed
+                     // at node 0's rank of the same local index and sent back -> intra AG
+                     // (reference main_central_reduce: NodeAgg(central), /root/reference/src/main.py:198-206)
+  kAlgoCount = 9,
 };
 const char* algo_name(int algo);
 

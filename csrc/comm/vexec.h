@@ -9,10 +9,11 @@
 // lengths, a receive overlapping a buffer the same step sends from, ranks disagreeing on the
 // step structure — throws instead of hanging, which is what a real multi-GPU run would do.
 //
-// The Backend supplies memory and arithmetic: the device backend (engine.cpp) issues
-// hipMemcpyAsync + the reduce kernel of reduce.hip on a main stream (and a side stream for
-// overlapped local ops, kConcurrent); the host backend (below) runs the same arithmetic on CPU
-// memory, so the schedules are checked in the CPU test suite too.
+// The Backend supplies memory and arithmetic: the device backend (engine.cpp) issues through the
+// engine's LocalIssuer (multi-lane reduce / copy launches, plan_exec.h), and the step / side-stream
+// sequencing is the engine's own execute_plan driving this class's per-step calls; the host
+// backend (below) runs the same arithmetic serially on CPU memory, so the schedules are checked in
+// the CPU test suite too.
 #pragma once
 
 #include <algorithm>
@@ -33,24 +34,15 @@ class VirtualRun {
  public:
   VirtualRun(const std::vector<Plan>& plans, const Topology& topo, Backend& be) : plans_(plans), t_(topo), be_(be) {}
 
-  void run() {
+  // Structure checks shared by both executors: one plan per rank, same step count, collective and
+  // overlap flags identical across ranks, and every overlapped step disjoint from its predecessor's
+  // local ops.
+  void validate() {
     const int N = (int)plans_.size();
     if (N != t_.world) fail("need one plan per virtual rank");
-    size_t S = plans_[0].steps.size();
+    const size_t S = plans_[0].steps.size();
     for (const auto& p : plans_)
       if (p.steps.size() != S) fail("ranks disagree on the number of steps");
-    // Step::overlap_prev: the previous step's local ops are deferred until after this step's
-    // transfers (the order a concurrent executor may produce), after checking that the two touch
-    // disjoint memory on every rank.
-    if constexpr (Backend::kConcurrent) {
-      run_concurrent(S);
-      return;
-    }
-    long pending = -1;
-    auto flush = [&]() {
-      if (pending >= 0) run_locals((size_t)pending);
-      pending = -1;
-    };
     for (size_t s = 0; s < S; ++s) {
       const bool coll = plans_[0].steps[s].is_coll();
       const bool ovl = plans_[0].steps[s].overlap_prev;
@@ -58,27 +50,56 @@ class VirtualRun {
         if (plans_[r].steps[s].is_coll() != coll) fail("step " + std::to_string(s) + ": collective on some ranks only");
         if (plans_[r].steps[s].overlap_prev != ovl) fail("step " + std::to_string(s) + ": ranks disagree on overlap");
       }
-      if (coll) {
-        if (ovl) fail("step " + std::to_string(s) + ": a collective step cannot overlap local ops");
-        flush();
-        run_coll(s);
-        continue;
-      }
       if (ovl) {
+        if (coll) fail("step " + std::to_string(s) + ": a collective step cannot overlap local ops");
         if (s == 0 || plans_[0].steps[s - 1].is_coll()) fail("step " + std::to_string(s) + ": nothing to overlap");
         check_disjoint(s - 1, s);
-      } else {
-        flush();
       }
-      run_transfers(s);
+    }
+  }
+
+  // Serial executor (host backend): Step::overlap_prev defers the previous step's local ops until
+  // after this step's transfers, the order a concurrent executor may produce. The device backend
+  // instead runs the engine's own issuing code (plan_exec.h execute_plan) through the per-step
+  // calls below.
+  void run() {
+    validate();
+    const size_t S = plans_[0].steps.size();
+    long pending = -1;
+    auto flush = [&]() {
+      if (pending >= 0) locals((size_t)pending);
+      pending = -1;
+    };
+    for (size_t s = 0; s < S; ++s) {
+      if (plans_[0].steps[s].is_coll()) {
+        flush();
+        coll(s);
+        continue;
+      }
+      if (!plans_[0].steps[s].overlap_prev) flush();
+      transfers(s);
       flush();  // the deferred local ops of step s-1 run after step s's transfers
       if (s + 1 < S && plans_[0].steps[s + 1].overlap_prev)
         pending = (long)s;
       else
-        run_locals(s);
+        locals(s);
     }
     flush();
   }
+
+  // ---- per-step issue (the transport interface of plan_exec.h) ----------------------------------
+  bool has_local(size_t s) const {
+    for (const auto& p : plans_)
+      for (const Op& o : p.steps[s].ops)
+        if (o.kind == kReduce || o.kind == kCopy || o.kind == kZero) return true;
+    return false;
+  }
+  void locals(size_t s) {
+    for (int r = 0; r < (int)plans_.size(); ++r)
+      for (const Op& o : plans_[r].steps[s].ops) local(r, o);
+  }
+  void coll(size_t s) { run_coll(s); }
+  void transfers(size_t s) { run_transfers(s); }
 
  private:
   [[noreturn]] void fail(const std::string& m) { throw std::runtime_error("virtual ranks: " + m); }
@@ -90,52 +111,6 @@ class VirtualRun {
   };
   static bool overlap(const Span& a, const Span& b) {
     return a.rank == b.rank && a.buf == b.buf && a.lo < b.hi && b.lo < a.hi;
-  }
-
-  // A backend with a second queue (the device backend) runs the local ops of a step whose successor
-  // overlaps it on that queue, concurrently with the successor's transfers — the RCCL engine's
-  // order (engine.cpp run_plan): side_begin / side_end(tag) bracket them, main_wait(tag) joins.
-  void run_concurrent(size_t S) {
-    const int N = (int)plans_.size();
-    long side_last = -1, joined = -1;
-    auto join_upto = [&](long k) {
-      const long j = std::min(k, side_last);
-      if (j > joined) {
-        be_.main_wait((size_t)j);
-        joined = j;
-      }
-    };
-    for (size_t s = 0; s < S; ++s) {
-      const bool coll = plans_[0].steps[s].is_coll();
-      const bool ovl = plans_[0].steps[s].overlap_prev;
-      for (int r = 1; r < N; ++r) {
-        if (plans_[r].steps[s].is_coll() != coll) fail("step " + std::to_string(s) + ": collective on some ranks only");
-        if (plans_[r].steps[s].overlap_prev != ovl) fail("step " + std::to_string(s) + ": ranks disagree on overlap");
-      }
-      if (coll) {
-        if (ovl) fail("step " + std::to_string(s) + ": a collective step cannot overlap local ops");
-        join_upto((long)s);
-        run_coll(s);
-        continue;
-      }
-      if (ovl) {
-        if (s == 0 || plans_[0].steps[s - 1].is_coll()) fail("step " + std::to_string(s) + ": nothing to overlap");
-        check_disjoint(s - 1, s);
-        join_upto((long)s - 2);
-      } else {
-        join_upto((long)s - 1);
-      }
-      run_transfers(s);
-      if (s + 1 < S && plans_[0].steps[s + 1].overlap_prev) {
-        be_.side_begin();
-        run_locals(s);
-        be_.side_end(s);
-        side_last = (long)s;
-      } else {
-        run_locals(s);
-      }
-    }
-    join_upto((long)S);
   }
 
   // Local ops of step a vs P2P ops of step b, per rank: no write of one may meet a read or write of
@@ -164,11 +139,6 @@ class VirtualRun {
         fail("step " + std::to_string(b) + " overlaps the local ops of step " + std::to_string(a) + " on rank " +
              std::to_string(r) + " but touches their memory");
     }
-  }
-
-  void run_locals(size_t s) {
-    for (int r = 0; r < (int)plans_.size(); ++r)
-      for (const Op& o : plans_[r].steps[s].ops) local(r, o);
   }
 
   void run_transfers(size_t s) {
@@ -320,7 +290,6 @@ class VirtualRun {
 // Host backend: CPU buffers, fp32 or bf16 (round-to-nearest-even, as v_cvt_pk_bf16_f32). Serial:
 // overlapped steps run in the deferred order (VirtualRun::run).
 struct HostBackend {
-  static constexpr bool kConcurrent = false;
   std::vector<char*> data, scratch;
   size_t esz = 4;
   bool bf16 = false;

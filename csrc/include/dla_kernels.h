@@ -71,6 +71,23 @@ struct ReduceSrcs {
 void launch_reduce_sum(void* dst, bool accumulate_dst, const ReduceSrcs& srcs, int64_t n, int dtype,
                        float scale, hipStream_t stream);
 void launch_scale(void* data, int64_t n, int dtype, float scale, hipStream_t stream);
+// Many independent single-source reductions in ONE launch (one ring step of C channels x N virtual
+// ranks): lane i computes dst_i = scale_i * ([dst_i] + src_i) over n_i elements (src_i may be null:
+// pure scale). Passed by value (no table upload), so a step costs one launch whatever C is.
+constexpr int kMaxReduceLanes = 64;
+struct ReduceLane {
+  void* dst;
+  const void* src;
+  int64_t n;
+  float scale;
+  int accumulate;
+};
+struct ReduceLanes {
+  ReduceLane lane[kMaxReduceLanes];
+  int blk0[kMaxReduceLanes + 1];  // first block of each lane (prefix over lanes), filled by the launcher
+  int count;
+};
+void launch_reduce_lanes(ReduceLanes& lanes, int dtype, hipStream_t stream);
 // dst = scale * src with dtype conversion (fp32 / bf16 either way)
 void launch_cast(void* dst, int dst_dtype, const void* src, int src_dtype, int64_t n, float scale, hipStream_t stream);
 

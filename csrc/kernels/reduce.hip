@@ -112,6 +112,80 @@ void launch_reduce_sum(void* dst, bool accumulate_dst, const ReduceSrcs& srcs, i
   }
 }
 
+// ---- multi-lane reduce: one launch for all single-source reductions of a ring step -----------
+// Blocks are dealt to lanes in proportion to their 16-byte vector counts (blk0 prefix, <= 8 compares
+// to find the lane); inside a lane a grid-stride loop over that lane's blocks. A lane whose pointers
+// are not 16-byte aligned takes the scalar loop (never the case for plan slices: 64-element aligned).
+template <typename T>
+__global__ __launch_bounds__(kRBlock) void reduce_lanes_kernel(ReduceLanes L) {
+  constexpr int V = 16 / sizeof(T);
+  const int b = blockIdx.x;
+  int li = 0;
+  while (li + 1 < L.count && b >= L.blk0[li + 1]) ++li;
+  const ReduceLane ln = L.lane[li];
+  const int lb = b - L.blk0[li], nb = L.blk0[li + 1] - L.blk0[li];
+  T* __restrict__ dst = static_cast<T*>(ln.dst);
+  const T* __restrict__ src = static_cast<const T*>(ln.src);
+  const uintptr_t al = reinterpret_cast<uintptr_t>(ln.dst) | reinterpret_cast<uintptr_t>(ln.src);
+  const int64_t stride = (int64_t)nb * kRBlock;
+  int64_t done = 0;
+  if (ln.accumulate == 2) {  // bit copy (a virtual-rank link / plan copy): no arithmetic, -0 and NaN kept
+    if ((al & 15) == 0) {
+      const int64_t nvec = ln.n / V;
+      for (int64_t v = (int64_t)lb * kRBlock + threadIdx.x; v < nvec; v += stride)
+        reinterpret_cast<float4_t*>(dst)[v] = reinterpret_cast<const float4_t*>(src)[v];
+      done = nvec * V;
+    }
+    for (int64_t i = done + (int64_t)lb * kRBlock + threadIdx.x; i < ln.n; i += stride) dst[i] = src[i];
+    return;
+  }
+  if ((al & 15) == 0) {
+    const int64_t nvec = ln.n / V;
+    for (int64_t v = (int64_t)lb * kRBlock + threadIdx.x; v < nvec; v += stride) {
+      if constexpr (V == 4) {
+        float4_t x = ln.accumulate ? reinterpret_cast<const float4_t*>(dst)[v] : float4_t{0.f, 0.f, 0.f, 0.f};
+        if (src) x += reinterpret_cast<const float4_t*>(src)[v];
+        reinterpret_cast<float4_t*>(dst)[v] = x * ln.scale;
+      } else {
+        ushort8_t x = ln.accumulate ? reinterpret_cast<const ushort8_t*>(dst)[v] : ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        ushort8_t y = src ? reinterpret_cast<const ushort8_t*>(src)[v] : ushort8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        ushort8_t o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16((bf16_to_f32(x[j]) + bf16_to_f32(y[j])) * ln.scale);
+        reinterpret_cast<ushort8_t*>(dst)[v] = o;
+      }
+    }
+    done = nvec * V;
+  }
+  for (int64_t i = done + (int64_t)lb * kRBlock + threadIdx.x; i < ln.n; i += stride) {
+    float a = ln.accumulate ? Cvt<T>::to_f32(dst[i]) : 0.f;
+    if (src) a += Cvt<T>::to_f32(src[i]);
+    dst[i] = Cvt<T>::from_f32(a * ln.scale);
+  }
+}
+
+void launch_reduce_lanes(ReduceLanes& L, int dtype, hipStream_t stream) {
+  if (L.count <= 0) return;
+  const int V = dtype == kF32 ? 4 : 8;
+  int64_t total = 0;
+  for (int i = 0; i < L.count; ++i) total += L.lane[i].n / V + 1;
+  // ~2048 blocks over the whole step (8 per CU), at least one per lane
+  const double per = total > 0 ? 2048.0 / (double)total : 0.0;
+  int acc = 0;
+  for (int i = 0; i < L.count; ++i) {
+    L.blk0[i] = acc;
+    const int64_t need = (L.lane[i].n / V + kRBlock) / kRBlock;  // blocks to cover the lane once
+    int64_t nb = (int64_t)((double)(L.lane[i].n / V + 1) * per + 0.5);
+    nb = nb < 1 ? 1 : (nb > need ? need : nb);
+    acc += (int)nb;
+  }
+  L.blk0[L.count] = acc;
+  if (dtype == kF32)
+    hipLaunchKernelGGL(reduce_lanes_kernel<float>, dim3(acc), dim3(kRBlock), 0, stream, L);
+  else
+    hipLaunchKernelGGL(reduce_lanes_kernel<bf16_t>, dim3(acc), dim3(kRBlock), 0, stream, L);
+}
+
 // dst = scale * src with a dtype conversion (fp32 <-> bf16): staging of bf16 buckets in fp32 for
 // full-precision accumulation across ranks (CommEngine accum_fp32).
 template <typename D, typename S>

@@ -57,14 +57,25 @@ def build_parser() -> argparse.ArgumentParser:
     # MI355X options
     p.add_argument("--model", default=None, help="model override (same names as model_type)")
     p.add_argument("--dtype", default=None, choices=["fp32", "bf16"],
-                   help="compute dtype (bf16 autocast on GPU by default, fp32 on CPU)")
+                   help="compute dtype (bf16 on GPU by default, fp32 on CPU); fp32 = the reference's precision")
+    p.add_argument("--precision", default=None, choices=["bf16", "autocast", "fp32"],
+                   help="bf16: bf16 weights + fp32 master weights in the fused SGD, native kernels (GPU default; "
+                        "the bench.py path); autocast: fp32 params under bf16 autocast; fp32: no reduced precision "
+                        "(MIOpen / torch kernels, the reference's numerics)")
+    p.add_argument("--conv", default="native", choices=["native", "miopen"],
+                   help="convolutions / FC heads on the native MFMA kernels (bf16) or MIOpen")
     p.add_argument("--algorithm", default="ring", help="all-reduce algorithm: ring|builtin|central|direct|rsag")
     p.add_argument("--channels", type=int, default=0, help="ring channels (0 = one per xGMI peer)")
     p.add_argument("--native", type=int, default=None, help="1 = C++ RCCL engine (GPU default), 0 = torch.distributed")
     p.add_argument("--kernels", default=None, choices=["native", "torch"], help="model hot-path kernel backend")
     p.add_argument("--comm_dtype", default=None, choices=["fp32", "bf16"], help="gradient wire dtype")
     p.add_argument("--local_size", type=int, default=None, help="devices per (virtual) node for 2-step reducers")
-    p.add_argument("--sync_timers", type=int, default=0, help="1 = synchronise the device at every timer")
+    p.add_argument("--sync_timers", type=int, default=None,
+                   help="0 = host timers only; 1 = synchronise the device at every timer; 2 = synchronise once at "
+                        "the end of each batch, as the reference's per-batch loss print (.item()) did (GPU default)")
+    p.add_argument("--hier_algorithm", default=None,
+                   help="native engine algorithm of the 2-step runners (default hier_ring; hier_central for the "
+                        "central runner; hier_coll = RCCL collectives on ncclCommSplit sub-communicators)")
     p.add_argument("--find_unused", type=int, default=None, help="graph walk for unused params each forward")
     p.add_argument("--results_root", default="results")
     p.add_argument("--checkpoint", default=None, help="path to save a checkpoint at the end of a run")
@@ -98,7 +109,13 @@ def finalize(config):
     config.model_name = model
     config.epoch_count = int(config.epoch_count)
     if config.dtype is None:
-        config.dtype = "bf16" if config.use_gpu else "fp32"
+        config.dtype = "fp32" if (not config.use_gpu or config.precision == "fp32") else "bf16"
+    if config.precision is None:
+        config.precision = "bf16" if config.dtype == "bf16" else "fp32"
+    if not config.use_gpu:
+        config.precision = "fp32"
+    if config.sync_timers is None:
+        config.sync_timers = 2 if config.use_gpu else 0
     if config.native is None:
         config.native = 1 if config.use_gpu else 0
     if config.kernels is None:

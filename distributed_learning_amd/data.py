@@ -57,11 +57,50 @@ class DataPartitioner:
         return Partition(self.data, self.partitions[partition])
 
 
+class EpochSampler(torch.utils.data.Sampler):
+    """Shuffled order drawn from (seed, epoch) alone, with a start offset.
+
+    The reference shuffles with ``DataLoader(shuffle=True)`` (data.py:67), whose order depends on the
+    global RNG state at the moment each epoch starts, so a run cannot be resumed mid-epoch on the same
+    sequence. Here epoch e's permutation is a pure function of (seed, e): a resumed run at global
+    batch k sets epoch k // batches_per_epoch and starts k % batches_per_epoch batches into it,
+    without loading or decoding the skipped samples."""
+
+    def __init__(self, n: int, seed: int = 1234):
+        self.n, self.seed = n, seed
+        self.epoch, self.start = 0, 0
+
+    def set_epoch(self, epoch: int, start: int = 0) -> None:
+        self.epoch, self.start = int(epoch), int(start)
+
+    def order(self, epoch: int) -> List[int]:
+        g = torch.Generator().manual_seed(self.seed * 1_000_003 + epoch)
+        return torch.randperm(self.n, generator=g).tolist()
+
+    def __iter__(self):
+        return iter(self.order(self.epoch)[self.start:])
+
+    def __len__(self):
+        return self.n - self.start
+
+
+def resume_position(start_step: int, batches_per_epoch: int) -> Tuple[int, int]:
+    """(epoch, batches to skip inside it) of global batch ``start_step``."""
+    if batches_per_epoch <= 0:
+        return 0, 0
+    return start_step // batches_per_epoch, start_step % batches_per_epoch
+
+
 def get_partition_loader(dataset, node_id: int, worker_id: int, node_dev: int, total_dev: int,
                          batch_size: int = PER_WORKER_BATCH_SIZE, num_workers: int = 2, seed: int = 1234):
     part = DataPartitioner(dataset, total_dev, batch_size, seed).use(node_id * node_dev + worker_id)
-    return torch.utils.data.DataLoader(part, batch_size=batch_size, shuffle=True, num_workers=num_workers,
-                                       drop_last=True)
+    sampler = EpochSampler(len(part), seed + node_id * node_dev + worker_id)
+    # own generator: the loader's per-iterator worker seed must not be drawn from the global RNG, or every
+    # epoch start (and a resume's first iterator) would shift the model's dropout stream
+    loader = torch.utils.data.DataLoader(part, batch_size=batch_size, sampler=sampler, num_workers=num_workers,
+                                         drop_last=True, generator=torch.Generator().manual_seed(seed))
+    loader.epoch_sampler = sampler
+    return loader
 
 
 # ------------------------------------------------------------------------------------------------

@@ -3,11 +3,15 @@
 Each ``main_*`` composes wrapper x reducer x all-reduce exactly as the reference's matrix
  and runs :func:`train.worker_process` in *this* process (one process per
 device). Differences:
-* the 2-step ("node reducer") runners use :class:`HierarchicalReducer` — intra-node reduce-scatter
-  over xGMI, inter-node all-reduce of shards, intra-node all-gather — instead of a per-node parent
-  process pumping CPU buffers through ``mp.Queue`` (reducers.py:38-69);
-* on GPU the 1-step ring/central runners go through the C++ RCCL engine (``--native 1``) so the
-  collective runs on a dedicated HIP stream; ``--native 0`` uses the torch.distributed algorithms;
+* the 2-step ("node reducer") runners are a device-side hierarchy — intra-node reduce-scatter
+  over xGMI, inter-node all-reduce of the owned shards, intra-node all-gather — instead of a
+  per-node parent process pumping CPU buffers through ``mp.Queue`` (reducers.py:38-69). On GPU they
+  run on the C++ RCCL engine's native 2-step plans (``hier_ring`` for the ring runners,
+  ``hier_central`` for ``main_central_reduce``, ``--hier_algorithm hier_coll`` for RCCL collectives
+  on ncclCommSplit sub-communicators) with ``local_size`` = ``--local_size`` / ``node_dev`` /
+  ``LOCAL_WORLD_SIZE``; on CPU (and with ``--native 0``) on :class:`HierarchicalReducer`;
+* on GPU the 1-step runners go through the C++ RCCL engine (``--native 1``) so the collective
+  runs on a dedicated HIP stream; ``--native 0`` uses the torch.distributed algorithms;
 * ``main_seq`` sets ``experiment_name = "seq"`` (the reference forgot to, main.py:149-156).
 New runners: ``main_onestep_builtin``/``_direct``/``_rsag`` (other engine algorithms),
 ``experiment_algorithms`` (all of them back to back), ``fusion_experiment_onestep``.
@@ -30,11 +34,23 @@ class _NoReducer:
         pass
 
 
+def _local_size(config) -> int:
+    if config.local_size:
+        return int(config.local_size)
+    if config.node_dev and config.node_dev > 1:
+        return int(config.node_dev)
+    return int(os.environ.get("LOCAL_WORLD_SIZE", dist.get_world_size() if dist.is_initialized() else 1))
+
+
 def _reducer(config, kind: str, algorithm: str):
-    native = bool(config.native) and config.use_gpu and kind == "immediate"
+    native = bool(config.native) and bool(config.use_gpu)
     ch = config.channels or (max(1, dist.get_world_size() - 1) if dist.is_initialized() else 1)
     if kind == "hierarchical":
-        return make_reducer("hierarchical", algorithm, channels=1, local_size=config.local_size or config.node_dev)
+        if native:
+            algo = config.hier_algorithm or ("hier_central" if algorithm == "central" else "hier_ring")
+            return make_reducer("hierarchical", algo, native=True, local_size=_local_size(config),
+                                channels=config.channels)
+        return make_reducer("hierarchical", algorithm, channels=1, local_size=_local_size(config))
     return make_reducer("immediate", algorithm, channels=ch if algorithm.startswith("ring") else 1, native=native)
 
 

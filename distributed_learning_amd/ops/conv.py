@@ -30,6 +30,12 @@ from .bn_act import bn_link_of as _bn_link_of
 # DLA_BN_EPILOGUE=1 turns it on for A/B runs.
 BN_EPILOGUE = os.environ.get("DLA_BN_EPILOGUE", "0") == "1"
 
+# Native conv dispatches by kind ("1x1", "1x1_fork", "3x3", "stem"): lets a test assert that a step
+# (e.g. the reference-compatible CLI's) ran the framework's kernels rather than MIOpen.
+import collections as _collections  # noqa: E402
+
+CALLS = _collections.Counter()
+
 
 def bn_link_of(x):
     return _bn_link_of(x) if BN_EPILOGUE else None
@@ -254,6 +260,7 @@ RESIDUAL_HANDOFF = True
 def conv1x1_fork(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False, sub: bool = False):
     """Returns (y, stats-or-None, x_alias, x_sub-or-None); use ``x_alias`` as the residual identity
     and ``x_sub`` (= x[:, :, ::2, ::2], with sub) as a stride-2 downsample conv's input."""
+    CALLS["1x1_fork"] += 1
     rlink = ResidualLink() if RESIDUAL_HANDOFF and x.requires_grad else None
     y, stats, xa, xs = _Conv1x1Fork.apply(x, conv.weight, want_stats, rlink, sub)
     if rlink is not None:
@@ -264,6 +271,7 @@ def conv1x1_fork(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False, sub
 def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False, stride: int | None = None):
     """Returns (y, stats-or-None); stats are [row_blocks, Cout, 2] partial (sum, sumsq).
     ``stride`` overrides the module's (1 for an input that is already subsampled)."""
+    CALLS["1x1"] += 1
     s = conv.stride[0] if stride is None else stride
     if x.shape[2] % s or x.shape[3] % s:
         # odd spatial size with stride 2 (output ceil) — keep F.conv2d semantics exactly
@@ -359,6 +367,7 @@ class _Conv3x3(torch.autograd.Function):
 def conv3x3(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
     """Returns (y, stats-or-None); stats are [row_blocks, Cout, 2] partial (sum, sumsq) when the
     native forward ran."""
+    CALLS["3x3"] += 1
     return _Conv3x3.apply(x, conv.weight, conv.stride[0], want_stats)
 
 
@@ -427,4 +436,5 @@ class _StemConv(torch.autograd.Function):
 def stem_conv(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
     """The ResNet stem conv on the native kernels. Returns (y, stats-or-None); stats are the
     [row_blocks, Cout, 2] (sum, sumsq) partials of y for the fused BatchNorm."""
+    CALLS["stem"] += 1
     return _StemConv.apply(x, conv.weight, want_stats)

@@ -31,6 +31,7 @@ class DistContext:
     backend: str
     device: torch.device
     _engine: object = None
+    _engines: dict = None
 
     @property
     def rank(self) -> int:
@@ -48,13 +49,23 @@ class DistContext:
     def local_world_size(self) -> int:
         return self.env.local_world_size
 
-    def engine(self):
-        """The native RCCL engine for the WORLD group (created lazily, GPU + nccl only)."""
-        if self._engine is None:
-            from .engine import NativeEngine
+    def engine(self, local_size: Optional[int] = None, channels: int = 0):
+        """The native RCCL engine for the WORLD group (created lazily, GPU + nccl only).
 
-            self._engine = NativeEngine.create(dist.group.WORLD, self.device)
-        return self._engine
+        ``local_size`` (ranks per node of the 2-step algorithms) and ``channels`` (ring channels)
+        are part of the engine's topology; one engine is kept per distinct (local_size, channels)."""
+        from .engine import NativeEngine, topology
+
+        topo = topology(self.world_size, channels, local_size)
+        key = (topo["local_size"], len(topo["rings"]))
+        if self._engines is None:
+            self._engines = {}
+        if key not in self._engines:
+            self._engines[key] = NativeEngine.create(dist.group.WORLD, self.device, channels=channels,
+                                                     local_size=topo["local_size"])
+            if self._engine is None:
+                self._engine = self._engines[key]
+        return self._engines[key]
 
 
 def init(backend: Optional[str] = None, rank: Optional[int] = None, world_size: Optional[int] = None,
@@ -120,8 +131,9 @@ def is_initialized() -> bool:
 
 def shutdown() -> None:
     global _CTX
-    if _CTX is not None and _CTX._engine is not None:
-        _CTX._engine.close()
+    if _CTX is not None:
+        for e in (_CTX._engines or {}).values():
+            e.close()
     if dist.is_initialized():
         try:
             dist.barrier()

@@ -12,7 +12,8 @@ node reducer on P2P rings (intra-node RS -> inter-node ring all-reduce of the ow
 intra-node AG), ``hier_coll`` the same hierarchy on RCCL collectives over ``ncclCommSplit``
 sub-communicators (reference /root/reference/src/reducers.py:38-69, main.py:129-137),
 ``ring_pipe`` the ring with its reduce-scatter in half-chunk sub-steps whose reduce kernels run on
-a side stream, overlapped with the next sub-step's transfer.
+a side stream, overlapped with the next sub-step's transfer, ``hier_central`` the 2-step reducer with
+a parameter server between nodes (reference ``main_central_reduce``, main.py:198-206).
 
 Every schedule is a cached Plan (csrc/comm/plan.h); :mod:`.virtual` runs the identical plans for
 N virtual ranks inside one process (one GPU or the CPU), which is how the N>1 paths are tested
@@ -38,6 +39,7 @@ ALGO_CODES: Dict[str, str] = {
     "hier_ring": "ALGO_HIER_RING",
     "hier_coll": "ALGO_HIER_COLL",
     "ring_pipe": "ALGO_RING_PIPE",
+    "hier_central": "ALGO_HIER_CENTRAL",
 }
 
 

@@ -135,7 +135,7 @@ def make_reducer(kind: str = "immediate", algorithm: str = "ring", *, channels: 
         if engine is None:
             from .context import get_context
 
-            engine = get_context().engine()
+            engine = get_context().engine(local_size=local_size, channels=channels if channels > 1 else 0)
         return NativeReducer(engine, algorithm)
     if kind in ("immediate", "1step", "onestep"):
         return ImmediateReducer(algorithm, group, channels)

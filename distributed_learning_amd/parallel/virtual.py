@@ -27,12 +27,15 @@ from .executor import Executor
 
 
 def virtual_allreduce(bufs: Sequence[torch.Tensor], algorithm: str = "ring", average: bool = True,
-                      channels: int = 0, local_size: Optional[int] = None, accum_fp32: bool = False) -> None:
-    """All-reduce ``bufs`` (one tensor per virtual rank) in place with the engine's schedules."""
+                      channels: int = 0, local_size: Optional[int] = None, accum_fp32: bool = False) -> int:
+    """All-reduce ``bufs`` (one tensor per virtual rank) in place with the engine's schedules.
+
+    GPU buffers run through the engine's own issuing code (csrc/comm/plan_exec.h); returns the
+    number of kernel launches the links and local ops took (0 for host buffers)."""
     C = _ext.require()
     n = len(bufs)
     topo = topology(n, channels, local_size if local_size is not None else n)
-    C.virtual_allreduce(list(bufs), algo_code(algorithm), bool(average), topo["rings"], topo["local_size"],
+    return C.virtual_allreduce(list(bufs), algo_code(algorithm), bool(average), topo["rings"], topo["local_size"],
                         topo["local_rings"], topo["node_rings"], bool(accum_fp32))
 
 

@@ -13,7 +13,13 @@ Differences by design:
   reference's f-string forced ``.item()`` every batch) unless ``--sync_timers 1``;
 * a device-accurate ``*_device_times.csv`` (HIP events) is written beside the parity CSV;
 * only one process writes ``{exp}_config.txt`` (the reference raced all workers on it);
-* optional checkpoint save/resume (the reference had none).
+* optional checkpoint save/resume (the reference had none; SURVEY.md §5.4);
+* on GPU the step is the framework's measured headline path (the one ``bench.py`` times): native
+  MFMA convolutions / FC heads and fused BN kernels, bf16 weights with fp32 master weights in the
+  fused SGD (``--precision bf16``, default), on-device synthetic batches, and every gradient
+  collective on the C++ RCCL engine's comm stream. ``--precision fp32`` runs the reference's
+  numerics (fp32 weights and activations on MIOpen / torch kernels); ``--precision autocast`` keeps
+  fp32 parameters under bf16 autocast.
 """
 from __future__ import annotations
 
@@ -44,12 +50,30 @@ def _model_for(config, device):
     return spec, model
 
 
-def _data_for(config, spec, device, rank: int, node_id: int, worker_id: int):
+def _precision(config, device) -> str:
+    return getattr(config, "precision", "fp32") if device.type == "cuda" else "fp32"
+
+
+def setup_compute_path(config, device) -> str:
+    """Select the kernels of the step; returns the precision in effect (bf16 | autocast | fp32)."""
+    prec = _precision(config, device)
+    if device.type != "cuda":
+        dnn.set_backend("torch")
+        dnn.set_native_conv(False)
+        return prec
+    torch.backends.cudnn.benchmark = True
+    native = config.kernels == "native" and prec != "fp32"  # the native kernels are bf16 kernels
+    dnn.set_backend("native" if native else "torch")
+    dnn.set_native_conv(native and getattr(config, "conv", "native") == "native")
+    return prec
+
+
+def _data_for(config, spec, device, rank: int, node_id: int, worker_id: int, dtype=torch.float32):
     if config.random_input or not config.dataset_root or not os.path.isdir(config.dataset_root):
         if not config.random_input:
             print_d(f"dataset root {config.dataset_root!r} not found: using synthetic data", Level.WARNING)
         return D.SyntheticBatches(config.batch_size, spec.input_shape, spec.num_classes, device,
-                                  dtype=torch.float32, seed=config.seed, rank=rank,
+                                  dtype=dtype, seed=config.seed, rank=rank,
                                   channels_last=device.type == "cuda")
     ds = D.load_dataset(spec.dataset, config.dataset_root)
     return D.get_partition_loader(ds, node_id, worker_id, config.node_dev, config.total_dev, config.batch_size)
@@ -93,12 +117,15 @@ def worker_process(config, distribute_model: Callable, reducer, experiment_name:
     worker_id = rank % max(1, config.node_dev) if worker_id is None else worker_id
     device = torch.device(f"cuda:{torch.cuda.current_device()}") if config.use_gpu else torch.device("cpu")
     print_d(f"Starting experiment {experiment_name} ({config.experiment}), {datetime.datetime.now()}", Level.INFO)
-    dnn.set_backend(config.kernels if device.type == "cuda" else "torch")
+    prec = setup_compute_path(config, device)
 
     spec, model = _model_for(config, device)
+    if prec == "bf16":
+        dnn.bf16_weights(model)  # bf16 weights, fp32 masters in the optimizer (bench.py's path)
     model = distribute_model(model, reducer, config.grouping_size, device)
     params = list(getattr(model, "module", model).parameters())
-    optimizer = FusedSGD(params, lr=config.lr, momentum=config.momentum, weight_decay=config.weight_decay)
+    optimizer = FusedSGD(params, lr=config.lr, momentum=config.momentum, weight_decay=config.weight_decay,
+                         master_weights=prec == "bf16")
     start_step = 0
     if getattr(config, "resume", None):
         start_step = load_checkpoint(config.resume, model, optimizer, map_location=device)
@@ -109,10 +136,13 @@ def worker_process(config, distribute_model: Callable, reducer, experiment_name:
         with open(f"{config.folder}/{experiment_name}_config.txt", "w") as f:
             f.write(str(config))
     stem = f"{config.folder}/{experiment_name}_{node_id}_{worker_id}"
-    timers = Timers(sync=bool(config.sync_timers))
+    sync_mode = int(config.sync_timers or 0)
+    timers = Timers(sync=sync_mode == 1)
+    batch_sync = sync_mode == 2 and device.type == "cuda"
     ev = EventTimers() if device.type == "cuda" else None
-    train_set = _data_for(config, spec, device, rank, node_id, worker_id)
-    autocast = torch.autocast("cuda", dtype=torch.bfloat16) if (device.type == "cuda" and config.dtype == "bf16") \
+    train_set = _data_for(config, spec, device, rank, node_id, worker_id,
+                          dtype=torch.bfloat16 if prec == "bf16" else torch.float32)
+    autocast = torch.autocast("cuda", dtype=torch.bfloat16) if prec == "autocast" \
         else torch.autocast("cpu", enabled=False)
     model.train()
 
@@ -120,18 +150,20 @@ def worker_process(config, distribute_model: Callable, reducer, experiment_name:
     # a resumed run continues the original sequence: batch numbering, and the data stream position
     batch_count = start_step
     end_batch = start_step + config.limit_batches
-    skip = 0
+    epoch0, skip = 0, 0
+    sampler = getattr(train_set, "epoch_sampler", None)
     if isinstance(train_set, D.SyntheticBatches):
         train_set.seek(start_step)
-    else:
-        skip = start_step
+    elif sampler is not None:
+        # resume inside the same per-epoch order without loading the skipped batches
+        epoch0, skip = D.resume_position(start_step, len(train_set))
     t_start = time.time()
-    for epoch in range(config.epoch_count):
+    for epoch in range(epoch0, config.epoch_count):
         if batch_count >= end_batch:
             break
+        if sampler is not None:
+            sampler.set_epoch(epoch, skip * config.batch_size if epoch == epoch0 else 0)
         gen = iter(train_set)
-        while skip > 0 and next(gen, None) is not None:
-            skip -= 1
         while batch_count < end_batch:
             timers.start("batch")
             ev and ev.start("batch")
@@ -145,6 +177,8 @@ def worker_process(config, distribute_model: Callable, reducer, experiment_name:
             timers.start("data2dev")
             x = x.to(device, non_blocking=True)
             y = y.to(device, non_blocking=True)
+            if prec == "bf16" and x.is_floating_point() and x.dtype != torch.bfloat16:
+                x = x.to(torch.bfloat16)
             if device.type == "cuda" and x.dim() == 4:
                 x = x.contiguous(memory_format=torch.channels_last)
             timers.end("data2dev")
@@ -180,8 +214,10 @@ def worker_process(config, distribute_model: Callable, reducer, experiment_name:
             timers.end("optimizer_step")
 
             losses.append(loss.detach().float())
-            if config.sync_timers:
+            if sync_mode == 1:
                 print_d(f"Worker {node_id}:{worker_id} loss for batch {batch_count}: {losses[-1].item()}", Level.DEBUG)
+            elif batch_sync:
+                torch.cuda.synchronize()  # the reference's per-batch loss print synchronised here (main.py:94-96)
             timers.end("batch")
             ev and ev.end("batch")
             extra = {"batch_count": batch_count, "data_len": x.size(0)}
@@ -201,6 +237,12 @@ def worker_process(config, distribute_model: Callable, reducer, experiment_name:
     timers.writeout(f"{stem}_times.csv")
     if ev:
         ev.writeout(f"{stem}_device_times.csv")
+    if device.type == "cuda":
+        from .ops import conv as nconv
+
+        print_d(f"native conv dispatches ({experiment_name}): {dict(sorted(nconv.CALLS.items()))} "
+                f"[precision {prec}, ops backend {dnn.get_backend()}, native conv {dnn.native_conv()}]", Level.INFO)
+        nconv.CALLS.clear()
     if getattr(config, "checkpoint", None):
         save_checkpoint(config.checkpoint, model, optimizer, batch_count)
     model.cleanup()

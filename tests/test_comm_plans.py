@@ -18,7 +18,7 @@ from distributed_learning_amd.parallel.virtual import plan_text, virtual_allredu
 pytestmark = pytest.mark.skipif(not _ext.available(), reason="native extension not built")
 
 FLAT = ["builtin", "ring", "direct", "central", "rsag", "ring_pipe"]
-HIER = ["hier_ring", "hier_coll"]
+HIER = ["hier_ring", "hier_coll", "hier_central"]
 
 
 def _inputs(N, n, dtype, seed=0):

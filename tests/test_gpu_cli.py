@@ -23,7 +23,18 @@ def _run(tmp_path, model, experiment, *extra, batch=16, batches=3):
            "--job_id", "g", *extra]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    _run.stdout = r.stdout
     return tmp_path / f"{experiment}_1_g"
+
+
+def _dispatches(stdout, exp):
+    """The native conv dispatch counts train.py logs at the end of run ``exp``."""
+    import ast
+    import re
+
+    m = re.search(r"native conv dispatches \(" + exp + r"\): (\{[^}]*\}) \[precision (\w+)", stdout)
+    assert m, stdout[-2000:]
+    return ast.literal_eval(m.group(1)), m.group(2)
 
 
 def _check(folder, exp, batches=3, first=0):
@@ -42,6 +53,23 @@ def test_cli_experiment2_resnet50(cuda, tmp_path):
     folder = _run(tmp_path, "resnet50", "experiment2")
     for exp in ["warmup", "ddp", "onestep_reduce", "onestep_central"]:
         _check(folder, exp)
+
+
+def test_cli_step_runs_native_kernels(cuda, tmp_path):
+    """The reference-compatible CLI runs the headline path: bf16 weights + native MFMA convs (1x1, 3x3,
+    stem) in every step, the same kernels bench.py times (VERDICT r2 missing item 1)."""
+    folder = _run(tmp_path, "resnet50", "experiment_single", batch=32, batches=2)
+    _check(folder, "single", batches=2)
+    calls, prec = _dispatches(_run.stdout, "single")
+    assert prec == "bf16"
+    assert calls.get("stem", 0) >= 2 and calls.get("3x3", 0) >= 2 * 16, calls
+    assert calls.get("1x1", 0) + calls.get("1x1_fork", 0) >= 2 * 30, calls
+    # --precision fp32: the reference's numerics on MIOpen / torch, no native conv dispatch
+    sub = tmp_path / "fp32"
+    sub.mkdir()
+    _run(sub, "resnet18", "experiment_single", "--precision", "fp32", batch=8, batches=2)
+    calls, prec = _dispatches(_run.stdout, "single")
+    assert prec == "fp32" and not calls, calls
 
 
 def test_cli_experiment1_googlenet(cuda, tmp_path):

@@ -19,7 +19,7 @@ from distributed_learning_amd.parallel.virtual import VirtualGroup, virtual_allr
 pytestmark = pytest.mark.gpu
 
 DEV = torch.device("cuda", 0)
-ALGOS = ["builtin", "ring", "direct", "central", "rsag", "hier_ring", "hier_coll", "ring_pipe"]
+ALGOS = ["builtin", "ring", "direct", "central", "rsag", "hier_ring", "hier_coll", "ring_pipe", "hier_central"]
 
 
 def _inputs(N, n, dtype, seed=0):
@@ -159,3 +159,15 @@ def test_gradsync_virtual_ranks_native_resnet_bf16():
     finally:
         dnn.set_backend("torch")
         dnn.set_native_conv(False)
+
+
+def test_ring_step_launches_do_not_scale_with_channels():
+    """One ring step = one launch for all links and one for all reduces, whatever the channel count
+    (7 channels issued 7 reduce launches per step). The count comes from the engine's own
+    issuing code (plan_exec.h LocalIssuer), which the virtual harness shares with CommEngine."""
+    N, n = 8, 4 * 1024 * 1024
+    bufs = [torch.randn(n, device=DEV) for _ in range(N)]
+    counts = {ch: virtual_allreduce(bufs, "ring", channels=ch, average=False) for ch in (1, 3, 7)}
+    assert counts[1] == counts[3] == counts[7] == 3 * (N - 1), counts
+    # the pipelined ring: two sub-steps per reduce-scatter step, each one link + one reduce launch
+    assert virtual_allreduce(bufs, "ring_pipe", channels=7, average=False) == 2 * 2 * (N - 1) + (N - 1)
