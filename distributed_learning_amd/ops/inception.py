@@ -362,7 +362,7 @@ def inception_forward(block, x: torch.Tensor) -> torch.Tensor:
             bn_act._PENDING_COUNTERS.append(bn.num_batches_tracked)
         acts = _BNReluGroup.apply(rmetas, dslr, *rt)
         for i, a in enumerate(acts):
-            if a.grad_fn.links[i] is not None:
+            if a.grad_fn is not None and a.grad_fn.links[i] is not None:
                 a._dla_bn = a.grad_fn.links[i]
     else:
         acts = [bn_act.fused_bn_act(red.contiguous(memory_format=CL), bn, True, None,

@@ -1,0 +1,142 @@
+"""Teacher-forced, segment-by-segment comparison of the native training step with fp32 PyTorch.
+
+A whole-model bf16-vs-fp32 comparison at random init is chaotic: relative errors compound over 50
+layers, so the early layers' gradients differ by O(1) (the round-2 smoke printed ``conv1.grad rel
+1.34`` for both the native path and torch autocast), and a bound that passes that checks nothing.
+Here the native path runs the whole model once, exactly as in training (autograd connects the
+segments, so every cross-segment fusion — the dgrad-epilogue BN partials handed to the producer's
+BatchNorm, the residual-gradient handoff into the next block's fork — is in the graph), and every
+segment boundary's activation and gradient is captured. Then each segment is re-run alone in fp32
+PyTorch (MIOpen convs, torch BN, the same bf16-valued weights held in fp32) on the native path's
+own input, and back-propagated from the native path's own output gradient. Errors cannot compound:
+each segment is judged on its own inputs. Per segment the check covers the output, the input
+gradient and every parameter gradient (relative L2 error).
+
+Segments: ResNet — stem (conv+BN+ReLU+max-pool), every residual block, head (global average pool +
+FC); GoogLeNet — the two fused stem stages, conv2, every Inception block and max-pool, head.
+The head excludes dropout (random masks) and GoogLeNet's aux heads (outside the loss, reference
+network.py:41).
+"""
+from __future__ import annotations
+
+import copy
+from typing import Callable, Dict, List, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+Segment = Tuple[str, Callable, List[nn.Module]]
+
+
+def _rel(a: torch.Tensor, b: torch.Tensor) -> float:
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def segments(model: nn.Module) -> List[Segment]:
+    from ..models.googlenet import GoogLeNet
+    from ..models.resnet import ResNet
+    from ..ops import nn as dnn
+    from ..ops.pool import global_avg_pool
+
+    segs: List[Segment] = []
+    if isinstance(model, ResNet):
+        segs.append(("stem", lambda m, x: dnn.conv_bn_act_maxpool(x, m.conv1, m.bn1, m.maxpool), ["conv1", "bn1"]))
+        for li in range(1, 5):
+            for bi in range(len(getattr(model, f"layer{li}"))):
+                name = f"layer{li}.{bi}"
+                segs.append((name, (lambda li, bi: lambda m, x: getattr(m, f"layer{li}")[bi](x))(li, bi), [name]))
+        segs.append(("head", lambda m, x: dnn.linear(global_avg_pool(x), m.fc), ["fc"]))
+        return segs
+    if isinstance(model, GoogLeNet):
+        segs.append(("stem1", lambda m, x: dnn.conv_bn_act_maxpool(x, m.conv1.conv, m.conv1.bn, m.maxpool1), ["conv1"]))
+        segs.append(("conv2", lambda m, x: m.conv2(x), ["conv2"]))
+        segs.append(("stem3", lambda m, x: dnn.conv_bn_act_maxpool(x, m.conv3.conv, m.conv3.bn, m.maxpool2), ["conv3"]))
+        for name in ["inception3a", "inception3b", "maxpool3", "inception4a", "inception4b", "inception4c",
+                     "inception4d", "inception4e", "maxpool4", "inception5a", "inception5b"]:
+            segs.append((name, (lambda n: lambda m, x: getattr(m, n)(x))(name), [name]))
+        segs.append(("head", lambda m, x: dnn.linear(global_avg_pool(x), m.fc), ["fc"]))
+        return segs
+    raise TypeError(f"no segment map for {type(model).__name__}")
+
+
+def _params(model: nn.Module, names: List[str]) -> Dict[str, nn.Parameter]:
+    out = {}
+    for n in names:
+        mod = model.get_submodule(n)
+        for pn, p in mod.named_parameters():
+            out[f"{n}.{pn}"] = p
+    return out
+
+
+def teacher_forced(model: nn.Module, x: torch.Tensor, y: torch.Tensor) -> List[Dict[str, float]]:
+    """Run the native step on ``model`` (bf16 weights, channels_last, on the GPU) and compare every
+    segment with fp32 PyTorch. Returns one row per segment: ``out`` (output rel. error), ``dx``
+    (input-gradient rel. error; None for the first segment) and ``dw`` (max over the segment's
+    parameter gradients, with ``dw_worst`` naming it); the head row also has ``dlogits`` (the fused
+    cross-entropy's gradient vs torch's on the same logits)."""
+    from ..ops import nn as dnn
+    from ..ops.loss import cross_entropy
+
+    segs = segments(model)
+    ref = copy.deepcopy(model)
+    for p in ref.parameters():
+        p.data = p.data.float()
+    prev_backend, prev_conv = dnn.get_backend(), dnn.native_conv()
+    rows: List[Dict[str, float]] = []
+    try:
+        # ---- native run: the segments chained under autograd, boundaries retained ------------
+        dnn.set_backend("native")
+        dnn.set_native_conv(True)
+        model.zero_grad(set_to_none=True)
+        acts = [x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)]
+        for _, fn, _ in segs:
+            a = fn(model, acts[-1])
+            a.retain_grad()
+            acts.append(a)
+        logits = acts[-1]
+        loss = cross_entropy(logits, y)
+        loss.backward()
+        torch.cuda.synchronize()
+        # ---- fp32 reference, one segment at a time on the native path's own tensors ----------
+        dnn.set_backend("torch")
+        dnn.set_native_conv(False)
+        for k, (name, fn, mods) in enumerate(segs):
+            ref.zero_grad(set_to_none=True)
+            xin = acts[k].detach().float().contiguous(memory_format=torch.channels_last)
+            xin.requires_grad_(k > 0)
+            out = fn(ref, xin)
+            gout = acts[k + 1].grad
+            row: Dict[str, float] = {"segment": name, "out": _rel(acts[k + 1].detach().float(), out.detach())}
+            out.backward(gout.float())
+            row["dx"] = _rel(acts[k].grad.float(), xin.grad) if k > 0 else None
+            worst, wname = 0.0, ""
+            nat_p, ref_p = _params(model, mods), _params(ref, mods)
+            for pn, rp in ref_p.items():
+                if rp.grad is None:
+                    continue
+                e = _rel(nat_p[pn].grad.float(), rp.grad)
+                if e > worst:
+                    worst, wname = e, pn
+            row["dw"], row["dw_worst"] = worst, wname
+            if name == "head":
+                lg = logits.detach().float()
+                dl = (F.softmax(lg, 1) - F.one_hot(y, lg.shape[1]).float()) / lg.shape[0]
+                row["dlogits"] = _rel(gout.float(), dl)
+            rows.append(row)
+    finally:
+        dnn.set_backend(prev_backend)
+        dnn.set_native_conv(prev_conv)
+    return rows
+
+
+def worst(rows: List[Dict[str, float]]) -> Tuple[float, str]:
+    """Largest error over all segments and checks, and where it occurred."""
+    w, where = 0.0, ""
+    for r in rows:
+        for k in ("out", "dx", "dw", "dlogits"):
+            v = r.get(k)
+            if v is not None and v > w:
+                w, where = v, f"{r['segment']}.{k}" + (f" ({r['dw_worst']})" if k == "dw" else "")
+    return w, where
