@@ -245,6 +245,13 @@ inline int tile_bn(int cfg) {
 }
 // rows of BN-statistics partials ([rows][N][2]) a stats-producing launch writes (one per row tile)
 int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto, int K = 0);
+// Virtual conv output (gemm.hip gemm_vy_kernel): y = A * B^T (stride-1 1x1 conv, B = [N][K] weights)
+// recomputed by each consumer. mode 0 statistics partials, 1 out = relu(BN(y) + res) + ReLU bits,
+// 2 BN-backward reduce partials from dy and the bits, 3 BN-backward apply (dx). part: [gemm_vy_rows][N][2].
+int gemm_vy_rows(int M, int N);
+void launch_gemm_vy(int mode, const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K,
+                    const float* ws, const void* res, const void* dy, void* out, uint8_t* mask, float* part,
+                    hipStream_t stream);
 // BatchNorm-backward reduction fused into a bf16-output GEMM epilogue (the output is the BN's dy):
 // x = the BN input [M, N], ws = its 7N workspace, mask/mode as launch_bn_bwd (0, 1 or 2),
 // part = [stats_rows][N][2] partial (sum dy', sum dy'(x - mean)).

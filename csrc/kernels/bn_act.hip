@@ -921,6 +921,7 @@ void launch_bn_bwd(const void* dy, const void* y, const uint8_t* mask, const voi
   hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, fp, nrb, M, C, gamma, ws,
                      dgamma, dbeta);
   }
+  if (!dx) return;  // finalize only (the virtual-output GEMM applies the coefficients itself)
   int atpr, anrb, anct;
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
 #define DLA_BN_BAPPLY(T, K, D)                                                                                      \

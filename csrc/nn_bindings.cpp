@@ -277,6 +277,76 @@ static void check_mat(const at::Tensor& t, const char* what) {
   TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, what, " must be 16-byte aligned");
 }
 
+// ---- virtual bottleneck output: conv3 (1x1, stride 1) + BN3 + residual + ReLU, y3 never stored ----
+// a: [M, K] rows of the conv input (channels_last view), w2: [N, K] bf16 weights. Forward returns
+// (out [M, N], ws [7N], mask): statistics pass -> BN finalize (running stats updated) -> apply pass
+// that recomputes y3 = a w2^T tile by tile (gemm.hip gemm_vy_kernel).
+std::vector<at::Tensor> conv_bn_res_vy_fwd(at::Tensor a, at::Tensor w2, at::Tensor residual, at::Tensor weight,
+                                           at::Tensor bias, c10::optional<at::Tensor> running_mean,
+                                           c10::optional<at::Tensor> running_var, double momentum, double eps) {
+  check_mat(a, "a");
+  check_mat(w2, "w2");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && w2.scalar_type() == at::kBFloat16, "conv_bn_res_vy: bf16 operands");
+  const int M = (int)a.size(0), K = (int)a.size(1), N = (int)w2.size(0);
+  TORCH_CHECK(w2.size(1) == K && N % 8 == 0 && K % 8 == 0, "conv_bn_res_vy: w2 must be [N, K], N % 8 == 0");
+  TORCH_CHECK(residual.is_cuda() && residual.scalar_type() == at::kBFloat16 && residual.numel() == (int64_t)M * N &&
+                  (residual.dim() == 2 ? residual.is_contiguous() : residual.is_contiguous(at::MemoryFormat::ChannelsLast)),
+              "conv_bn_res_vy: residual must be the [M, N] bf16 rows (channels_last)");
+  TORCH_CHECK(weight.scalar_type() == at::kFloat && bias.scalar_type() == at::kFloat && weight.numel() == N &&
+                  bias.numel() == N,
+              "conv_bn_res_vy: fp32 BN affine parameters of N channels");
+  auto f32 = a.options().dtype(at::kFloat);
+  const int rows = gemm_vy_rows(M, N);
+  at::Tensor stats = at::empty({rows, N, 2}, f32);
+  hipStream_t st = current_stream(a);
+  launch_gemm_vy(0, a.data_ptr(), a.stride(0), w2.data_ptr(), w2.stride(0), M, N, K, nullptr, nullptr, nullptr,
+                 nullptr, nullptr, stats.data_ptr<float>(), st);
+  at::Tensor ws = at::empty({7 * (int64_t)N}, f32);
+  at::Tensor part = at::empty({std::max<int64_t>(1, (int64_t)bn_fold_groups(rows) * N * 2)}, f32);
+  auto fptr = [](const c10::optional<at::Tensor>& t) -> float* {
+    return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+  };
+  launch_bn_fwd(nullptr, nullptr, nullptr, M, N, kBF16, weight.data_ptr<float>(), bias.data_ptr<float>(), (float)eps,
+                (float)momentum, fptr(running_mean), fptr(running_var), ws.data_ptr<float>(), part.data_ptr<float>(),
+                true, true, st, stats.data_ptr<float>(), rows);
+  at::Tensor out = at::empty({M, N}, a.options());
+  at::Tensor mask = at::empty({((int64_t)M * N + 7) / 8}, a.options().dtype(at::kByte));
+  launch_gemm_vy(1, a.data_ptr(), a.stride(0), w2.data_ptr(), w2.stride(0), M, N, K, ws.data_ptr<float>(),
+                 residual.data_ptr(), nullptr, out.data_ptr(), mask.data_ptr<uint8_t>(), nullptr, st);
+  return {out, ws, mask};
+}
+
+// Backward of conv_bn_res_vy_fwd up to the BN input: returns (dy3 [M, N], dgamma, dbeta). dy: [M, N]
+// gradient of the block output (channels_last rows); mask: the forward's ReLU bits. The residual's
+// gradient (dy masked) and the conv's own dgrad / wgrad are the caller's.
+std::vector<at::Tensor> conv_bn_res_vy_bwd(at::Tensor a, at::Tensor w2, at::Tensor dy, at::Tensor mask, at::Tensor ws,
+                                           at::Tensor weight) {
+  check_mat(a, "a");
+  check_mat(w2, "w2");
+  const int M = (int)a.size(0), K = (int)a.size(1), N = (int)w2.size(0);
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.numel() == (int64_t)M * N &&
+                  (dy.dim() == 2 ? dy.is_contiguous() : dy.is_contiguous(at::MemoryFormat::ChannelsLast)),
+              "conv_bn_res_vy_bwd: dy must be [M, N] bf16 rows (channels_last)");
+  TORCH_CHECK(mask.scalar_type() == at::kByte && mask.numel() * 8 >= (int64_t)M * N, "conv_bn_res_vy_bwd: bit mask");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() == 7 * (int64_t)N, "conv_bn_res_vy_bwd: 7N workspace");
+  auto f32 = a.options().dtype(at::kFloat);
+  const int rows = gemm_vy_rows(M, N);
+  at::Tensor part = at::empty({rows, N, 2}, f32);
+  hipStream_t st = current_stream(a);
+  launch_gemm_vy(2, a.data_ptr(), a.stride(0), w2.data_ptr(), w2.stride(0), M, N, K, ws.data_ptr<float>(), nullptr,
+                 dy.data_ptr(), nullptr, mask.data_ptr<uint8_t>(), part.data_ptr<float>(), st);
+  at::Tensor dg = at::empty({N}, f32), db = at::empty({N}, f32);
+  at::Tensor scratch = at::empty({1}, f32);
+  launch_bn_bwd(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, N, kBF16, weight.data_ptr<float>(),
+                ws.data_ptr<float>(), scratch.data_ptr<float>(), dg.data_ptr<float>(), db.data_ptr<float>(), 2, st,
+                part.data_ptr<float>(), rows);
+  at::Tensor dx = at::empty({M, N}, a.options());
+  launch_gemm_vy(3, a.data_ptr(), a.stride(0), w2.data_ptr(), w2.stride(0), M, N, K, ws.data_ptr<float>(), nullptr,
+                 dy.data_ptr(), dx.data_ptr(), mask.data_ptr<uint8_t>(), nullptr, st);
+  return {dx, dg, db};
+}
+
+
 // C = A @ B^T (A [M,K], B [N,K]; or C = A @ B with B [K,N] when b_kmajor) in bf16 with fp32 accumulation. Optionally returns per-row-block
 // column statistics partials [ceil(M/128), N, 2] (sum, sum of squares of the bf16 outputs).
 static const uint8_t* addend_mask_ptr(const c10::optional<at::Tensor>& m, int64_t M, int64_t N, bool add) {
@@ -936,6 +1006,9 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("ceil_mode") = false,
         pybind11::arg("need_pos") = true);
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pooling backward (gather form)");
+  m.def("conv_bn_res_vy_fwd", &conv_bn_res_vy_fwd,
+        "bottleneck conv3 + BN + residual + ReLU with the conv output recomputed per pass (never stored)");
+  m.def("conv_bn_res_vy_bwd", &conv_bn_res_vy_bwd, "backward of conv_bn_res_vy_fwd to the conv output (dy3, dgamma, dbeta)");
   m.def("bn_dual_fwd", &bn_dual_fwd, "training act(BN(x) + BN_d(xd)) in one apply pass (downsample residual)");
   m.def("bn_dual_bwd", &bn_dual_bwd, "backward of bn_dual_fwd (one dy read for both BatchNorms)");
   m.def("gap_fwd", &gap_fwd, "NHWC global average pooling -> [N, C]");

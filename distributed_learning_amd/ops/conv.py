@@ -438,3 +438,76 @@ def stem_conv(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
     [row_blocks, Cout, 2] (sum, sumsq) partials of y for the fused BatchNorm."""
     CALLS["stem"] += 1
     return _StemConv.apply(x, conv.weight, want_stats)
+
+
+# ---- bottleneck conv3 + BN3 + residual + ReLU with a virtual conv output --------------------------
+# The expanding 1x1 conv of a ResNet bottleneck (P -> 4P, stride 1) feeds only its BatchNorm, whose
+# output is added to the residual and ReLU'd. Its output y3 is 4x the bytes of its input a2, and the
+# stored-y path writes it once and reads it three times (BN apply; BN-backward reduce and apply). Here
+# every pass recomputes y3 = a2 W3^T tile by tile from a2 (K = P MFMA GEMM, csrc/kernels/gemm.hip
+# gemm_vy_kernel) and y3 never touches HBM: per block that trades 4 passes over y3 for 3 extra reads
+# of a2 (1/4 of y3 each) plus MFMA work. Bit-identical recomputation, so statistics, ReLU bits and
+# gradients are those of the stored-y path. Used where the trade pays: K = P <= VIRTUAL_Y_MAX_K (the
+# large-M stages; at K = 512 the recompute GEMM is MFMA-bound and costs more than the bytes it saves).
+VIRTUAL_Y = os.environ.get("DLA_VIRTUAL_Y", "1") == "1"
+VIRTUAL_Y_MAX_K = int(os.environ.get("DLA_VIRTUAL_Y_MAX_K", "256"))
+
+
+def virtual_y_supported(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual) -> bool:
+    return (VIRTUAL_Y and residual is not None and bn.training and bn.momentum is not None
+            and bn.weight is not None and bn.weight.dtype == torch.float32 and supported(x, conv)
+            and conv.stride in ((1, 1), 1) and conv.in_channels <= VIRTUAL_Y_MAX_K
+            and residual.dtype == torch.bfloat16 and residual.shape == (x.shape[0], conv.out_channels) + x.shape[2:]
+            and residual.is_contiguous(memory_format=torch.channels_last) and residual.data_ptr() % 16 == 0)
+
+
+class _Conv1x1BNResVirtual(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, residual, running_mean, running_var, momentum, eps, rlink):
+        C = _ext.require()
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        w2 = weight.reshape(cout, cin).to(torch.bfloat16).contiguous()
+        out2, ws, mask = C.conv_bn_res_vy_fwd(_rows(x), w2, _rows(residual), gamma, beta, running_mean, running_var,
+                                              momentum, eps)
+        ctx.save_for_backward(x, w2, ws, gamma, mask)
+        ctx.rlink = rlink
+        ctx.wdtype, ctx.wshape, ctx.wstride = weight.dtype, weight.shape, weight.stride()
+        return out2.view(n, h, w, cout).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.require()
+        x, w2, ws, gamma, mask = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        if dy.dtype != torch.bfloat16:
+            dy = dy.to(torch.bfloat16)
+        dy2 = _rows(dy)
+        dy3, dg, db = C.conv_bn_res_vy_bwd(_rows(x), w2, dy2, mask, ws, gamma)
+        need = ctx.needs_input_grad
+        dw = dx = dres = None
+        if need[1]:
+            odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
+            dw = _as_param_layout(C.gemm_tn(dy3, _rows(x), odt, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
+        if need[0]:
+            n, cin, h, w = x.shape
+            dx2, _ = C.gemm_nt(dy3, w2, False, None, True)
+            dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+        rl = ctx.rlink
+        if rl is not None:  # the forking conv adds dy (masked by the ReLU bits) in its dgrad epilogue
+            rl.dy, rl.mask = dy, mask
+        elif need[4]:
+            dres = dy * _unpack_bits(mask, dy)
+        return (dx, dw, dg if need[2] else None, db if need[3] else None, dres, None, None, None, None, None)
+
+
+def conv1x1_bn_res_virtual(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual: torch.Tensor):
+    """``relu(bn(conv(x)) + residual)`` (training mode) with the conv output never stored."""
+    from .bn_act import _PENDING_COUNTERS, fork_link_of
+
+    CALLS["1x1_vy"] += 1
+    rm, rv = (bn.running_mean, bn.running_var) if bn.track_running_stats else (None, None)
+    if bn.track_running_stats:
+        _PENDING_COUNTERS.append(bn.num_batches_tracked)
+    return _Conv1x1BNResVirtual.apply(x, conv.weight, bn.weight, bn.bias, residual, rm, rv, float(bn.momentum),
+                                      float(bn.eps), fork_link_of(residual))

@@ -104,6 +104,8 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
         from . import conv as nconv
         from .bn_act import fused_bn_act, supported as bn_supported
 
+        if relu and not presubsampled and nconv.virtual_y_supported(x, conv, bn, residual):
+            return nconv.conv1x1_bn_res_virtual(x, conv, bn, residual)
         if nconv.supported(x, conv):
             stride = 1 if presubsampled else None
             y, stats = nconv.conv1x1(x, conv, want_stats=bn.training, stride=stride)

@@ -1,0 +1,87 @@
+"""Bottleneck conv3 + BN3 + residual + ReLU with a virtual (recomputed, never stored) conv output
+(ops/conv.py _Conv1x1BNResVirtual, csrc/kernels/gemm.hip gemm_vy_kernel).
+
+The recomputation is bit-identical to the stored output, so the forward (activation + ReLU bits +
+running statistics) must equal the stored-y path exactly; the backward differs from it only by the
+summation order of the BatchNorm-backward partials. Both are also checked against fp32 PyTorch.
+"""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(8, 64, 56, 56, 256), (4, 128, 28, 28, 512), (3, 256, 14, 14, 1024), (5, 64, 9, 7, 64), (2, 128, 7, 9, 256)]
+
+
+def _setup(n, k, h, w, cout, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, k, h, w, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = torch.randn(n, cout, h, w, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    conv = nn.Conv2d(k, cout, 1, bias=False).to(dev)
+    conv.weight.data = (torch.randn(cout, k, 1, 1, generator=g) * k ** -0.5).to(dev, torch.bfloat16)
+    bn = nn.BatchNorm2d(cout).to(dev)
+    bn.weight.data = torch.rand(cout, generator=g).to(dev) + 0.5
+    bn.bias.data = torch.randn(cout, generator=g).to(dev) * 0.1
+    dy = torch.randn(n, cout, h, w, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    return x, res, conv, bn, dy
+
+
+def _run(x, res, conv, bn, dy, virtual):
+    from distributed_learning_amd.ops import conv as nconv
+    from distributed_learning_amd.ops import nn as dnn
+
+    old = nconv.VIRTUAL_Y
+    nconv.VIRTUAL_Y = virtual
+    dnn.set_backend("native")
+    dnn.set_native_conv(True)
+    try:
+        xi = x.clone().requires_grad_(True)
+        ri = res.clone().requires_grad_(True)
+        before = dict(nconv.CALLS)
+        out = dnn.conv_bn_act(xi, conv, bn, relu=True, residual=ri)
+        used = nconv.CALLS.get("1x1_vy", 0) - before.get("1x1_vy", 0)
+        out.backward(dy)
+        torch.cuda.synchronize()
+        return out.detach(), xi.grad, ri.grad, conv.weight.grad.clone(), bn.weight.grad.clone(), bn.bias.grad.clone(), used
+    finally:
+        nconv.VIRTUAL_Y = old
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_virtual_matches_stored_path(cuda, shape):
+    x, res, conv, bn, dy = _setup(*shape, cuda)
+    conv_v, bn_v = copy.deepcopy(conv), copy.deepcopy(bn)
+    o_s, dx_s, dr_s, dw_s, dg_s, db_s, used_s = _run(x, res, conv, bn, dy, False)
+    o_v, dx_v, dr_v, dw_v, dg_v, db_v, used_v = _run(x, res, conv_v, bn_v, dy, True)
+    assert used_s == 0 and used_v == 1
+    assert torch.equal(o_v, o_s)  # recomputed y3 is bit-identical: same activation, same ReLU decisions
+    torch.testing.assert_close(bn_v.running_mean, bn.running_mean, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(bn_v.running_var, bn.running_var, rtol=1e-6, atol=1e-7)
+    assert torch.equal(dr_v, dr_s)  # residual gradient = dy masked by the same bits
+    for a, b, what in ((dx_v, dx_s, "dx"), (dw_v, dw_s, "dw"), (dg_v, dg_s, "dgamma"), (db_v, db_s, "dbeta")):
+        assert _rel(a, b) < 5e-3, (what, _rel(a, b))
+
+
+@pytest.mark.parametrize("shape", SHAPES[:3])
+def test_virtual_vs_fp32_torch(cuda, shape):
+    x, res, conv, bn, dy = _setup(*shape, cuda, seed=1)
+    ref_conv, ref_bn = copy.deepcopy(conv).float(), copy.deepcopy(bn)
+    o_v, dx_v, dr_v, dw_v, dg_v, db_v, used = _run(x, res, conv, bn, dy, True)
+    assert used == 1
+    xr = x.float().requires_grad_(True)
+    rr = res.float().requires_grad_(True)
+    out = F.relu(ref_bn(ref_conv(xr)) + rr)
+    out.backward(dy.float())
+    checks = {"out": _rel(o_v, out.detach()), "dx": _rel(dx_v, xr.grad), "dres": _rel(dr_v, rr.grad),
+              "dw": _rel(dw_v, ref_conv.weight.grad), "dgamma": _rel(dg_v, ref_bn.weight.grad),
+              "dbeta": _rel(db_v, ref_bn.bias.grad)}
+    assert max(checks.values()) < 2e-2, checks
