@@ -236,9 +236,34 @@ struct VyArgs {
   float* part;         // statistics / backward-reduce partials [row tiles][N][2]
 };
 
+// The streamed operand (residual or dy) and the ReLU-mask bytes of this thread's epilogue rows,
+// loaded before the main loop: their HBM round trip overlaps the A-tile loads and the MFMAs instead of
+// following them (one round trip per tile instead of two).
+template <int BM, int BN, int MODE, int NT>
+struct VyPrefetch {
+  static constexpr int CPR = BN / 8;
+  static constexpr int NIT = BM * CPR / NT;
+  ushort8_t ld[NIT];
+  uint32_t mb[NIT];
+  __device__ __forceinline__ void load(int64_t M, int N, int64_t row0, int col0, const VyArgs& va) {
+    const int tid = threadIdx.x, my_cc = (tid % CPR) * 8;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int r = (tid + it * NT) / CPR;
+      const int64_t gm = row0 + r;
+      const int gn = col0 + my_cc;
+      const bool ok = gm < M && gn < N;
+      const int64_t off = ok ? gm * N + gn : 0;
+      ld[it] = ok ? *reinterpret_cast<const ushort8_t*>((MODE == kVyApply ? va.res : va.dy) + off) : zero8();
+      mb[it] = (MODE != kVyApply && ok) ? (uint32_t)va.mask[off >> 3] : 0u;
+    }
+  }
+};
+
 template <int BM, int BN, int MODE, int NT>
 __device__ __forceinline__ void epilogue_vy(const Acc<BM, BN, NT>& acc, int64_t M, int N, int64_t row0, int col0,
-                                            int bm, const VyArgs& va, char* smem) {
+                                            int bm, const VyArgs& va, char* smem,
+                                            const VyPrefetch<BM, BN, MODE, NT>& pf) {
   using AC = Acc<BM, BN, NT>;
   constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
   constexpr int LDS_C = BN + 8;
@@ -273,20 +298,8 @@ __device__ __forceinline__ void epilogue_vy(const Acc<BM, BN, NT>& acc, int64_t 
       }
     }
   }
-  // the streamed operand (residual or dy) and mask bytes of all this thread's rows are loaded up front
-  // so their global loads overlap each other and the first stores
-  ushort8_t ld[NIT];
-  uint32_t mb[NIT];
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int r = (tid + it * NT) / CPR;
-    const int64_t gm = row0 + r;
-    const int gn = col0 + my_cc;
-    const bool ok = gm < M && gn < N;
-    const int64_t off = ok ? gm * N + gn : 0;
-    ld[it] = ok ? *reinterpret_cast<const ushort8_t*>((MODE == kVyApply ? va.res : va.dy) + off) : zero8();
-    mb[it] = (MODE != kVyApply && ok) ? (uint32_t)va.mask[off >> 3] : 0u;
-  }
+  const ushort8_t* ld = pf.ld;
+  const uint32_t* mb = pf.mb;
   float bs[8], bq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bs[j] = bq[j] = 0.f;
@@ -362,6 +375,8 @@ __global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void gemm_vy_kernel(
   acc.zero();
   const RowLoader<BM, NT> la{A, lda, row0, M, K};
   const RowLoader<BN, NT> lb{B, ldb, (int64_t)col0, N, K};
+  VyPrefetch<BM, BN, MODE, NT> pf;
+  if constexpr (MODE != kVyStats) pf.load(M, N, row0, col0, va);
   run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
   if constexpr (MODE == kVyStats) {
     // gemm_nt's statistics epilogue without the store: (sum, sumsq) of the bf16-rounded outputs,
@@ -383,7 +398,7 @@ __global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void gemm_vy_kernel(
         }
     stats_flush<BM, BN, NT>(st, va.part + (int64_t)bm * N * 2, N, col0, smem_raw);
   } else {
-    epilogue_vy<BM, BN, MODE, NT>(acc, M, N, row0, col0, bm, va, smem_raw);
+    epilogue_vy<BM, BN, MODE, NT>(acc, M, N, row0, col0, bm, va, smem_raw, pf);
   }
 }
 

@@ -12,6 +12,16 @@ own input, and back-propagated from the native path's own output gradient. Error
 each segment is judged on its own inputs. Per segment the check covers the output, the input
 gradient and every parameter gradient (relative L2 error).
 
+Storage precision is the framework's policy, not a kernel property: the native path keeps every
+activation (conv outputs, ReLU outputs) in bf16. An fp32 reference that keeps them in fp32 makes a
+different ReLU decision for every pre-activation within bf16 rounding of zero, and each such flip
+moves one full gradient element — with ~0.3 % of elements near zero that alone is a ~5 % relative
+L2 difference in every input gradient, whatever the kernels do. So the reference rounds what the
+native path stores (conv inputs and outputs, linear inputs and outputs) to bf16 in its forward
+(straight-through in its backward) and computes everything else — convolutions, BatchNorm
+statistics and normalisation, ReLU, pooling, the whole backward — in fp32. What remains is the
+kernels' arithmetic error: fp32 accumulation order and the bf16 rounding of gradient tensors.
+
 Segments: ResNet — stem (conv+BN+ReLU+max-pool), every residual block, head (global average pool +
 FC); GoogLeNet — the two fused stem stages, conv2, every Inception block and max-pool, head.
 The head excludes dropout (random masks) and GoogLeNet's aux heads (outside the loss, reference
@@ -61,6 +71,23 @@ def segments(model: nn.Module) -> List[Segment]:
     raise TypeError(f"no segment map for {type(model).__name__}")
 
 
+def _bf16_ste(t: torch.Tensor) -> torch.Tensor:
+    """Round to bf16 in the forward, identity in the backward."""
+    return t + (t.to(torch.bfloat16).to(t.dtype) - t).detach()
+
+
+def bf16_storage_hooks(model: nn.Module) -> list:
+    """Round the inputs and outputs of every Conv2d / Linear of ``model`` to bf16 (straight-through),
+    i.e. the activation storage precision of the native path. Returns the hook handles."""
+    handles = []
+    for m in model.modules():
+        if isinstance(m, (nn.Conv2d, nn.Linear)):
+            handles.append(m.register_forward_pre_hook(lambda mod, args: tuple(
+                _bf16_ste(a) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)))
+            handles.append(m.register_forward_hook(lambda mod, args, out: _bf16_ste(out)))
+    return handles
+
+
 def _params(model: nn.Module, names: List[str]) -> Dict[str, nn.Parameter]:
     out = {}
     for n in names:
@@ -70,12 +97,15 @@ def _params(model: nn.Module, names: List[str]) -> Dict[str, nn.Parameter]:
     return out
 
 
-def teacher_forced(model: nn.Module, x: torch.Tensor, y: torch.Tensor) -> List[Dict[str, float]]:
+def teacher_forced(model: nn.Module, x: torch.Tensor, y: torch.Tensor,
+                   bf16_storage: bool = True) -> List[Dict[str, float]]:
     """Run the native step on ``model`` (bf16 weights, channels_last, on the GPU) and compare every
     segment with fp32 PyTorch. Returns one row per segment: ``out`` (output rel. error), ``dx``
     (input-gradient rel. error; None for the first segment) and ``dw`` (max over the segment's
     parameter gradients, with ``dw_worst`` naming it); the head row also has ``dlogits`` (the fused
-    cross-entropy's gradient vs torch's on the same logits)."""
+    cross-entropy's gradient vs torch's on the same logits). ``bf16_storage``: the reference rounds
+    stored activations to bf16 like the native path (module docstring); False compares against pure
+    fp32 activations (then ReLU-decision flips dominate the gradient errors)."""
     from ..ops import nn as dnn
     from ..ops.loss import cross_entropy
 
@@ -102,6 +132,7 @@ def teacher_forced(model: nn.Module, x: torch.Tensor, y: torch.Tensor) -> List[D
         # ---- fp32 reference, one segment at a time on the native path's own tensors ----------
         dnn.set_backend("torch")
         dnn.set_native_conv(False)
+        hooks = bf16_storage_hooks(ref) if bf16_storage else []
         for k, (name, fn, mods) in enumerate(segs):
             ref.zero_grad(set_to_none=True)
             xin = acts[k].detach().float().contiguous(memory_format=torch.channels_last)
@@ -125,6 +156,8 @@ def teacher_forced(model: nn.Module, x: torch.Tensor, y: torch.Tensor) -> List[D
                 dl = (F.softmax(lg, 1) - F.one_hot(y, lg.shape[1]).float()) / lg.shape[0]
                 row["dlogits"] = _rel(gout.float(), dl)
             rows.append(row)
+        for h in hooks:
+            h.remove()
     finally:
         dnn.set_backend(prev_backend)
         dnn.set_native_conv(prev_conv)
