@@ -249,6 +249,14 @@ int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto, int K = 0);
 // recomputed by each consumer. mode 0 statistics partials, 1 out = relu(BN(y) + res) + ReLU bits,
 // 2 BN-backward reduce partials from dy and the bits, 3 BN-backward apply (dx). part: [gemm_vy_rows][N][2].
 int gemm_vy_rows(int M, int N);
+// Streaming form of the same passes (vy_stream.hip: weights resident in VGPRs, transposed MFMA,
+// persistent pixel streams) for K in {64, 128, 256}; partials of mode 0 / 2 are
+// [vy_stream_rows(mode, K, M, N)][N][2].
+bool vy_stream_supported(int K, int N);
+int vy_stream_streams(int64_t M, int N, int target_blocks);
+int vy_stream_rows(int mode, int K, int64_t M, int N);
+void launch_vy_stream(int mode, const void* A, int64_t lda, const void* W, int64_t M, int N, int K, const float* ws,
+                      const void* src, void* out, uint8_t* mask, float* part, hipStream_t stream);
 void launch_gemm_vy(int mode, const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K,
                     const float* ws, const void* res, const void* dy, void* out, uint8_t* mask, float* part,
                     hipStream_t stream);

@@ -278,6 +278,27 @@ static void check_mat(const at::Tensor& t, const char* what) {
 }
 
 // ---- virtual bottleneck output: conv3 (1x1, stride 1) + BN3 + residual + ReLU, y3 never stored ----
+// The passes run on the streaming kernels (vy_stream.hip) where they apply, else on the tiled
+// gemm_vy_kernel (DLA_VY_STREAM=0 forces the tiled form, for A/B runs).
+static bool vy_use_stream(int K, int N) {
+  static const bool on = [] {
+    const char* e = std::getenv("DLA_VY_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  return on && vy_stream_supported(K, N);
+}
+static int vy_rows(int mode, int M, int N, int K) {
+  return vy_use_stream(K, N) ? vy_stream_rows(mode, K, M, N) : gemm_vy_rows(M, N);
+}
+static void vy_pass(int mode, const at::Tensor& a, const at::Tensor& w2, int M, int N, int K, const float* ws,
+                    const void* res, const void* dy, void* out, uint8_t* mask, float* part, hipStream_t st) {
+  if (vy_use_stream(K, N))
+    launch_vy_stream(mode, a.data_ptr(), a.stride(0), w2.data_ptr(), M, N, K, ws, mode == 1 ? res : dy, out, mask,
+                     part, st);
+  else
+    launch_gemm_vy(mode, a.data_ptr(), a.stride(0), w2.data_ptr(), w2.stride(0), M, N, K, ws, res, dy, out, mask,
+                   part, st);
+}
 // a: [M, K] rows of the conv input (channels_last view), w2: [N, K] bf16 weights. Forward returns
 // (out [M, N], ws [7N], mask): statistics pass -> BN finalize (running stats updated) -> apply pass
 // that recomputes y3 = a w2^T tile by tile (gemm.hip gemm_vy_kernel).
@@ -296,11 +317,10 @@ std::vector<at::Tensor> conv_bn_res_vy_fwd(at::Tensor a, at::Tensor w2, at::Tens
                   bias.numel() == N,
               "conv_bn_res_vy: fp32 BN affine parameters of N channels");
   auto f32 = a.options().dtype(at::kFloat);
-  const int rows = gemm_vy_rows(M, N);
+  const int rows = vy_rows(0, M, N, K);
   at::Tensor stats = at::empty({rows, N, 2}, f32);
   hipStream_t st = current_stream(a);
-  launch_gemm_vy(0, a.data_ptr(), a.stride(0), w2.data_ptr(), w2.stride(0), M, N, K, nullptr, nullptr, nullptr,
-                 nullptr, nullptr, stats.data_ptr<float>(), st);
+  vy_pass(0, a, w2, M, N, K, nullptr, nullptr, nullptr, nullptr, nullptr, stats.data_ptr<float>(), st);
   at::Tensor ws = at::empty({7 * (int64_t)N}, f32);
   at::Tensor part = at::empty({std::max<int64_t>(1, (int64_t)bn_fold_groups(rows) * N * 2)}, f32);
   auto fptr = [](const c10::optional<at::Tensor>& t) -> float* {
@@ -311,8 +331,8 @@ std::vector<at::Tensor> conv_bn_res_vy_fwd(at::Tensor a, at::Tensor w2, at::Tens
                 true, true, st, stats.data_ptr<float>(), rows);
   at::Tensor out = at::empty({M, N}, a.options());
   at::Tensor mask = at::empty({((int64_t)M * N + 7) / 8}, a.options().dtype(at::kByte));
-  launch_gemm_vy(1, a.data_ptr(), a.stride(0), w2.data_ptr(), w2.stride(0), M, N, K, ws.data_ptr<float>(),
-                 residual.data_ptr(), nullptr, out.data_ptr(), mask.data_ptr<uint8_t>(), nullptr, st);
+  vy_pass(1, a, w2, M, N, K, ws.data_ptr<float>(), residual.data_ptr(), nullptr, out.data_ptr(),
+          mask.data_ptr<uint8_t>(), nullptr, st);
   return {out, ws, mask};
 }
 
@@ -330,19 +350,19 @@ std::vector<at::Tensor> conv_bn_res_vy_bwd(at::Tensor a, at::Tensor w2, at::Tens
   TORCH_CHECK(mask.scalar_type() == at::kByte && mask.numel() * 8 >= (int64_t)M * N, "conv_bn_res_vy_bwd: bit mask");
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() == 7 * (int64_t)N, "conv_bn_res_vy_bwd: 7N workspace");
   auto f32 = a.options().dtype(at::kFloat);
-  const int rows = gemm_vy_rows(M, N);
+  const int rows = vy_rows(2, M, N, K);
   at::Tensor part = at::empty({rows, N, 2}, f32);
   hipStream_t st = current_stream(a);
-  launch_gemm_vy(2, a.data_ptr(), a.stride(0), w2.data_ptr(), w2.stride(0), M, N, K, ws.data_ptr<float>(), nullptr,
-                 dy.data_ptr(), nullptr, mask.data_ptr<uint8_t>(), part.data_ptr<float>(), st);
+  vy_pass(2, a, w2, M, N, K, ws.data_ptr<float>(), nullptr, dy.data_ptr(), nullptr, mask.data_ptr<uint8_t>(),
+          part.data_ptr<float>(), st);
   at::Tensor dg = at::empty({N}, f32), db = at::empty({N}, f32);
   at::Tensor scratch = at::empty({1}, f32);
   launch_bn_bwd(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, N, kBF16, weight.data_ptr<float>(),
                 ws.data_ptr<float>(), scratch.data_ptr<float>(), dg.data_ptr<float>(), db.data_ptr<float>(), 2, st,
                 part.data_ptr<float>(), rows);
   at::Tensor dx = at::empty({M, N}, a.options());
-  launch_gemm_vy(3, a.data_ptr(), a.stride(0), w2.data_ptr(), w2.stride(0), M, N, K, ws.data_ptr<float>(), nullptr,
-                 dy.data_ptr(), dx.data_ptr(), mask.data_ptr<uint8_t>(), nullptr, st);
+  vy_pass(3, a, w2, M, N, K, ws.data_ptr<float>(), nullptr, dy.data_ptr(), dx.data_ptr(), mask.data_ptr<uint8_t>(),
+          nullptr, st);
   return {dx, dg, db};
 }
 

@@ -17,7 +17,7 @@ activation (conv outputs, ReLU outputs) in bf16. An fp32 reference that keeps th
 different ReLU decision for every pre-activation within bf16 rounding of zero, and each such flip
 moves one full gradient element — with ~0.3 % of elements near zero that alone is a ~5 % relative
 L2 difference in every input gradient, whatever the kernels do. So the reference rounds what the
-native path stores (conv inputs and outputs, linear inputs and outputs) to bf16 in its forward
+native path stores (conv inputs and outputs, linear inputs and outputs, max-pool inputs) to bf16 in its forward
 (straight-through in its backward) and computes everything else — convolutions, BatchNorm
 statistics and normalisation, ReLU, pooling, the whole backward — in fp32. What remains is the
 kernels' arithmetic error: fp32 accumulation order and the bf16 rounding of gradient tensors.
@@ -81,6 +81,9 @@ def bf16_storage_hooks(model: nn.Module) -> list:
     i.e. the activation storage precision of the native path. Returns the hook handles."""
     handles = []
     for m in model.modules():
+        if isinstance(m, nn.MaxPool2d):  # the native pools take the max of the stored (bf16) activations
+            handles.append(m.register_forward_pre_hook(lambda mod, args: tuple(
+                _bf16_ste(a) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)))
         if isinstance(m, (nn.Conv2d, nn.Linear)):
             handles.append(m.register_forward_pre_hook(lambda mod, args: tuple(
                 _bf16_ste(a) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)))

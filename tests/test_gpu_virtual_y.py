@@ -1,9 +1,10 @@
 """Bottleneck conv3 + BN3 + residual + ReLU with a virtual (recomputed, never stored) conv output
 (ops/conv.py _Conv1x1BNResVirtual, csrc/kernels/gemm.hip gemm_vy_kernel).
 
-The recomputation is bit-identical to the stored output, so the forward (activation + ReLU bits +
-running statistics) must equal the stored-y path exactly; the backward differs from it only by the
-summation order of the BatchNorm-backward partials. Both are also checked against fp32 PyTorch.
+Every pass recomputes the same y3 bits, so the virtual path differs from the stored-y path only by the
+summation order of the BatchNorm statistics / backward partials (fp32 rounding of mean, variance and
+the backward coefficients): activations agree to one bf16 ulp with identical ReLU decisions except at
+exact ties, gradients to fp32-rounding level. Both paths are also checked against fp32 PyTorch.
 """
 import copy
 
@@ -63,10 +64,14 @@ def test_virtual_matches_stored_path(cuda, shape):
     o_s, dx_s, dr_s, dw_s, dg_s, db_s, used_s = _run(x, res, conv, bn, dy, False)
     o_v, dx_v, dr_v, dw_v, dg_v, db_v, used_v = _run(x, res, conv_v, bn_v, dy, True)
     assert used_s == 0 and used_v == 1
-    assert torch.equal(o_v, o_s)  # recomputed y3 is bit-identical: same activation, same ReLU decisions
-    torch.testing.assert_close(bn_v.running_mean, bn.running_mean, rtol=1e-6, atol=1e-7)
-    torch.testing.assert_close(bn_v.running_var, bn.running_var, rtol=1e-6, atol=1e-7)
-    assert torch.equal(dr_v, dr_s)  # residual gradient = dy masked by the same bits
+    diff = (o_v.float() - o_s.float()).abs()
+    ulp = o_s.float().abs().clamp_min(1e-30) * 2.0 ** -7
+    assert bool((diff <= ulp).all()), float((diff / ulp).max())  # at most one bf16 ulp apart
+    assert float((diff > 0).float().mean()) < 1e-3
+    torch.testing.assert_close(bn_v.running_mean, bn.running_mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(bn_v.running_var, bn.running_var, rtol=1e-5, atol=1e-6)
+    # residual gradient = dy masked by the ReLU bits: the same decisions but at exact ties
+    assert float((dr_v != dr_s).float().mean()) < 1e-4
     for a, b, what in ((dx_v, dx_s, "dx"), (dw_v, dw_s, "dw"), (dg_v, dg_s, "dgamma"), (db_v, db_s, "dbeta")):
         assert _rel(a, b) < 5e-3, (what, _rel(a, b))
 
