@@ -12,8 +12,10 @@
 //     channels of ONE pixel: the residual / dy / output / dx accesses are 8-byte row segments in
 //     the tensors' own channels_last layout, and the ReLU bits a nibble of the mask byte;
 //   * every block is persistent over a strided set of 16-pixel groups with the next group's a2, dy /
-//     residual and mask loads issued before the current group's MFMAs and stores (double-buffered
-//     registers), so each wave keeps a group's worth of loads in flight at all times;
+//     residual and mask loads issued before the current group's MFMAs and stores (two ping-pong
+//     register buffers), so each wave keeps a group's worth of loads in flight at all times; all
+//     memory ops are buffer ops whose out-of-range offsets the hardware zero-fills / drops, so there
+//     is no branch around a load and the vmcnt waits stay exact;
 //   * the 4 waves of a block cover 128 channels of the same pixels (a2 rows shared through L1/L2),
 //     and the N/128 channel panels of one pixel stream are placed on the same XCD (shared L2).
 // Statistics / backward-reduction partials are reduced in registers and across the 16 pixel lanes,
@@ -108,22 +110,34 @@ __global__ __launch_bounds__(256) void vy_stream_kernel(const VsArgs v) {
     for (int r = 0; r < 4; ++r) s[f][r] = q[f][r] = 0.f;
 
   const int64_t ngrp = (M + 16 * PF - 1) / (16 * PF);
+  // Buffer resources: an out-of-range pixel's offset is past num_records, so its loads return zeros
+  // and its stores are dropped by the hardware — no branches around memory ops, so the compiler's
+  // vmcnt bookkeeping stays exact and the next group's loads stay in flight during this group.
+  const __amdgpu_buffer_rsrc_t ra = make_srd(v.a, (uint32_t)(M * v.lda * 2));
+  const __amdgpu_buffer_rsrc_t rs = make_srd(v.src, (uint32_t)(M * N * 2));
+  const __amdgpu_buffer_rsrc_t ro = make_srd(v.out, (uint32_t)(M * N * 2));
+  const __amdgpu_buffer_rsrc_t rm = make_srd(v.mask, (uint32_t)((M * N + 7) / 8));
   auto load = [&](int64_t grp, VsBuf<KF, PF>& b) {
 #pragma unroll
     for (int pf = 0; pf < PF; ++pf) {
       const int64_t px = grp * (16 * PF) + pf * 16 + lr;
       const bool ok = px < M;
+      const uint32_t ao = ok ? (uint32_t)((px * v.lda + 8 * g) * 2) : kOOB;
 #pragma unroll
-      for (int kf = 0; kf < KF; ++kf)
-        b.a[pf][kf] = ok ? *reinterpret_cast<const bf16x8_t*>(v.a + px * v.lda + kf * 32 + 8 * g) : bf16x8_t{};
+      for (int kf = 0; kf < KF; ++kf) {
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(ra, ao, kf * 64, 0);
+        b.a[pf][kf] = __builtin_bit_cast(bf16x8_t, r);
+      }
       if constexpr (MODE != kVsStats) {
 #pragma unroll
         for (int f = 0; f < kCF; ++f) {
           const int c = ch0 + f * 16 + 4 * g;
           const bool okc = ok && c < N;
-          const int64_t off = okc ? px * N + c : 0;
-          b.d[pf][f] = okc ? *reinterpret_cast<const u32x2_t*>(v.src + off) : u32x2_t{0u, 0u};
-          if constexpr (MODE != kVsApply) b.m[pf][f] = okc ? ((uint32_t)v.mask[off >> 3] >> (c & 4)) & 0xfu : 0u;
+          const uint32_t e = okc ? (uint32_t)(px * N + c) : 0u;
+          const auto d = __builtin_amdgcn_raw_buffer_load_b64(rs, okc ? e * 2 : kOOB, 0, 0);
+          b.d[pf][f] = __builtin_bit_cast(u32x2_t, d);
+          if constexpr (MODE != kVsApply)
+            b.m[pf][f] = ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rm, okc ? (e >> 3) : kOOB, 0, 0) >> (c & 4)) & 0xfu;
         }
       }
     }
@@ -133,29 +147,33 @@ __global__ __launch_bounds__(256) void vy_stream_kernel(const VsArgs v) {
     for (int pf = 0; pf < PF; ++pf) {
       const int64_t px = grp * (16 * PF) + pf * 16 + lr;
       const bool ok = px < M;
+      // the kCF accumulator chains interleaved (independent MFMAs back to back)
+      f32x4_t acc[kCF];
+#pragma unroll
+      for (int f = 0; f < kCF; ++f) acc[f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kf = 0; kf < KF; ++kf)
+#pragma unroll
+        for (int f = 0; f < kCF; ++f) acc[f] = mfma16(wf[f][kf], b.a[pf][kf], acc[f]);
 #pragma unroll
       for (int f = 0; f < kCF; ++f) {
-        f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kf = 0; kf < KF; ++kf) acc = mfma16(wf[f][kf], b.a[pf][kf], acc);
         const int c = ch0 + f * 16 + 4 * g;
         const bool okc = ok && c < N;
-        const int64_t off = okc ? px * N + c : 0;
+        const uint32_t e = okc ? (uint32_t)(px * N + c) : 0u;
         float yv[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) yv[r] = bf16_to_f32(f32_to_bf16(acc[r]));
+        for (int r = 0; r < 4; ++r) yv[r] = bf16_to_f32(f32_to_bf16(acc[f][r]));
         if constexpr (MODE == kVsStats) {
-          if (ok) {
+          const float z = ok ? 1.f : 0.f;  // out-of-range pixels computed zeros; keep them out anyway
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              s[f][r] += yv[r];
-              q[f][r] = fmaf(yv[r], yv[r], q[f][r]);
-            }
+          for (int r = 0; r < 4; ++r) {
+            s[f][r] += yv[r] * z;
+            q[f][r] = fmaf(yv[r] * z, yv[r], q[f][r]);
           }
         } else {
           const float dv[4] = {bf_lo(b.d[pf][f].x), bf_hi(b.d[pf][f].x), bf_lo(b.d[pf][f].y), bf_hi(b.d[pf][f].y)};
           if constexpr (MODE == kVsApply) {
-            uint32_t nib = 0, o[2];
+            uint32_t nib = 0;
             float ov[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -164,44 +182,54 @@ __global__ __launch_bounds__(256) void vy_stream_kernel(const VsArgs v) {
               nib |= (a > 0.f ? 1u : 0u) << r;
               ov[r] = fmaxf(a, 0.f);
             }
-            o[0] = (uint32_t)f32_to_bf16(ov[0]) | ((uint32_t)f32_to_bf16(ov[1]) << 16);
-            o[1] = (uint32_t)f32_to_bf16(ov[2]) | ((uint32_t)f32_to_bf16(ov[3]) << 16);
-            if (okc) *reinterpret_cast<u32x2_t*>(v.out + off) = u32x2_t{o[0], o[1]};
+            const u32x2_t o{(uint32_t)f32_to_bf16(ov[0]) | ((uint32_t)f32_to_bf16(ov[1]) << 16),
+                            (uint32_t)f32_to_bf16(ov[2]) | ((uint32_t)f32_to_bf16(ov[3]) << 16)};
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0)), o),
+                                                  ro, okc ? e * 2 : kOOB, 0, 0);
             // channels 4g..4g+3 and those of lane g^1 form one mask byte (bit = channel % 8)
             const uint32_t other = (uint32_t)__shfl_xor((int)nib, 16, 64);
-            if (okc && (g & 1) == 0) v.mask[off >> 3] = (uint8_t)(nib | (other << 4));
+            __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(nib | (other << 4)), rm,
+                                                 (okc && (g & 1) == 0) ? (e >> 3) : kOOB, 0, 0);
           } else {
             float gv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) gv[r] = ((b.m[pf][f] >> r) & 1u) ? dv[r] : 0.f;
             if constexpr (MODE == kVsBwdReduce) {
-              if (ok) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                  s[f][r] += gv[r];
-                  q[f][r] = fmaf(gv[r], yv[r] - c0[f][r], q[f][r]);
-                }
+              for (int r = 0; r < 4; ++r) {  // out-of-range pixels read dy = 0, mask 0: g = 0
+                s[f][r] += gv[r];
+                q[f][r] = fmaf(gv[r], yv[r] - c0[f][r], q[f][r]);
               }
             } else {
               float ov[4];
 #pragma unroll
               for (int r = 0; r < 4; ++r) ov[r] = c1[f][r] * (gv[r] - c2[f][r] - (yv[r] - c0[f][r]) * c3[f][r]);
-              const uint32_t o0 = (uint32_t)f32_to_bf16(ov[0]) | ((uint32_t)f32_to_bf16(ov[1]) << 16);
-              const uint32_t o1 = (uint32_t)f32_to_bf16(ov[2]) | ((uint32_t)f32_to_bf16(ov[3]) << 16);
-              if (okc) *reinterpret_cast<u32x2_t*>(v.out + off) = u32x2_t{o0, o1};
+              const u32x2_t o{(uint32_t)f32_to_bf16(ov[0]) | ((uint32_t)f32_to_bf16(ov[1]) << 16),
+                              (uint32_t)f32_to_bf16(ov[2]) | ((uint32_t)f32_to_bf16(ov[3]) << 16)};
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0)), o),
+                                                    ro, okc ? e * 2 : kOOB, 0, 0);
             }
           }
         }
       }
     }
   };
+  // ping-pong over two named register buffers (no buffer copies, so the compiler's vmcnt for one
+  // buffer's loads leaves the other buffer's loads outstanding): group i+1 loads during group i
+  VsBuf<KF, PF> b0, b1;
+  // loads are issued unconditionally (a group past the end reads zeros through the buffer bounds and
+  // touches no memory), so every path reaches a compute with the same outstanding-op count and the
+  // waits stay exact
   int64_t grp = y;
-  VsBuf<KF, PF> cur, nxt;
-  if (grp < ngrp) load(grp, cur);
-  for (; grp < ngrp; grp += v.gy) {
-    if (grp + v.gy < ngrp) load(grp + v.gy, nxt);  // next group's loads in flight during this one
-    compute(grp, cur);
-    cur = nxt;
+  load(grp, b0);
+  for (;;) {
+    load(grp + v.gy, b1);
+    if (grp >= ngrp) break;
+    compute(grp, b0);
+    load(grp + 2 * v.gy, b0);
+    if (grp + v.gy >= ngrp) break;
+    compute(grp + v.gy, b1);
+    grp += 2 * v.gy;
   }
   if constexpr (MODE == kVsStats || MODE == kVsBwdReduce) {
     // sum over the 16 pixel lanes of each channel group (lanes 16 g .. 16 g + 15), fixed order
