@@ -278,14 +278,16 @@ static void check_mat(const at::Tensor& t, const char* what) {
 }
 
 // ---- virtual bottleneck output: conv3 (1x1, stride 1) + BN3 + residual + ReLU, y3 never stored ----
-// The passes run on the streaming kernels (vy_stream.hip) where they apply, else on the tiled
-// gemm_vy_kernel (DLA_VY_STREAM=0 forces the tiled form, for A/B runs).
+// The passes run on the tiled gemm_vy_kernel; DLA_VY_STREAM=1 selects the streaming kernels
+// (vy_stream.hip) where they apply (measured slower: profiles/r3/virtual_y_ab.md).
+static int g_vy_stream = -1;  // -1: DLA_VY_STREAM (default off)
+static void set_vy_stream(bool on) { g_vy_stream = on ? 1 : 0; }
 static bool vy_use_stream(int K, int N) {
-  static const bool on = [] {
+  if (g_vy_stream < 0) {
     const char* e = std::getenv("DLA_VY_STREAM");
-    return !(e && e[0] == '0');
-  }();
-  return on && vy_stream_supported(K, N);
+    g_vy_stream = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_vy_stream == 1 && vy_stream_supported(K, N);
 }
 static int vy_rows(int mode, int M, int N, int K) {
   return vy_use_stream(K, N) ? vy_stream_rows(mode, K, M, N) : gemm_vy_rows(M, N);
@@ -1028,6 +1030,7 @@ void bind_nn(pybind11::module& m) {
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pooling backward (gather form)");
   m.def("conv_bn_res_vy_fwd", &conv_bn_res_vy_fwd,
         "bottleneck conv3 + BN + residual + ReLU with the conv output recomputed per pass (never stored)");
+  m.def("set_vy_stream", &set_vy_stream, "virtual-output passes on the streaming kernels (vy_stream.hip) or tiled");
   m.def("conv_bn_res_vy_bwd", &conv_bn_res_vy_bwd, "backward of conv_bn_res_vy_fwd to the conv output (dy3, dgamma, dbeta)");
   m.def("bn_dual_fwd", &bn_dual_fwd, "training act(BN(x) + BN_d(xd)) in one apply pass (downsample residual)");
   m.def("bn_dual_bwd", &bn_dual_bwd, "backward of bn_dual_fwd (one dy read for both BatchNorms)");

@@ -447,9 +447,12 @@ def stem_conv(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
 # every pass recomputes y3 = a2 W3^T tile by tile from a2 (K = P MFMA GEMM, csrc/kernels/gemm.hip
 # gemm_vy_kernel) and y3 never touches HBM: per block that trades 4 passes over y3 for 3 extra reads
 # of a2 (1/4 of y3 each) plus MFMA work. Bit-identical recomputation, so statistics, ReLU bits and
-# gradients are those of the stored-y path. Used where the trade pays: K = P <= VIRTUAL_Y_MAX_K (the
-# large-M stages; at K = 512 the recompute GEMM is MFMA-bound and costs more than the bytes it saves).
-VIRTUAL_Y = os.environ.get("DLA_VIRTUAL_Y", "1") == "1"
+# gradients are those of the stored-y path up to the BN sums' order. Eligible: K = P <= VIRTUAL_Y_MAX_K.
+# OFF by default — measured slower end to end (profiles/r3/virtual_y_ab.md): the byte accounting holds
+# (BatchNorm passes 29.9 -> 18.3 ms/step), but the recompute passes are latency-bound GEMM kernels at
+# ~2.5-3 TB/s (tiled, gemm.hip) or less (streaming, vy_stream.hip) while the plain BN passes they
+# replace stream at ~5.2 TB/s: 77.2 / 87.2 ms vs 75.2 ms per step at bs1024. DLA_VIRTUAL_Y=1 for A/B.
+VIRTUAL_Y = os.environ.get("DLA_VIRTUAL_Y", "0") == "1"
 VIRTUAL_Y_MAX_K = int(os.environ.get("DLA_VIRTUAL_Y_MAX_K", "256"))
 
 

@@ -32,6 +32,7 @@ def _setup(n, k, h, w, cout, dev, seed=0):
 
 
 def _run(x, res, conv, bn, dy, virtual):
+    # the virtual path is off by default (slower end to end, profiles/r3/virtual_y_ab.md); forced here
     from distributed_learning_amd.ops import conv as nconv
     from distributed_learning_amd.ops import nn as dnn
 
@@ -57,8 +58,18 @@ def _rel(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
+@pytest.fixture(params=["tiled", "stream"])
+def vy_form(request):
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    C.set_vy_stream(request.param == "stream")
+    yield request.param
+    C.set_vy_stream(False)
+
+
 @pytest.mark.parametrize("shape", SHAPES)
-def test_virtual_matches_stored_path(cuda, shape):
+def test_virtual_matches_stored_path(cuda, shape, vy_form):
     x, res, conv, bn, dy = _setup(*shape, cuda)
     conv_v, bn_v = copy.deepcopy(conv), copy.deepcopy(bn)
     o_s, dx_s, dr_s, dw_s, dg_s, db_s, used_s = _run(x, res, conv, bn, dy, False)
@@ -79,7 +90,7 @@ def test_virtual_matches_stored_path(cuda, shape):
 
 
 @pytest.mark.parametrize("shape", SHAPES[:3])
-def test_virtual_vs_fp32_torch(cuda, shape):
+def test_virtual_vs_fp32_torch(cuda, shape, vy_form):
     x, res, conv, bn, dy = _setup(*shape, cuda, seed=1)
     ref_conv, ref_bn = copy.deepcopy(conv).float(), copy.deepcopy(bn)
     o_v, dx_v, dr_v, dw_v, dg_v, db_v, used = _run(x, res, conv, bn, dy, True)
