@@ -251,6 +251,9 @@ def main():
     torch.cuda.synchronize()
     engine.consume_comm_ms()
     engine.set_timing(not graphed)
+    gsync = getattr(model, "sync", None)
+    if gsync is not None:
+        gsync.hook_s, gsync.hook_calls = 0.0, 0
     tele["before_timed"] = telemetry.sample(dev.index or 0)
     tev = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
     dist.barrier()
@@ -321,6 +324,9 @@ def main():
             "warmup_step_ms": [round(x, 2) for x in warm_ms],
             "telemetry": tele,
         }
+        if gsync is not None and gsync.hook_calls:
+            rec["hook_host_ms_per_step"] = round(gsync.hook_s * 1000.0 / a.steps, 3)
+            rec["hook_calls_per_step"] = gsync.hook_calls / a.steps
         print(json.dumps(rec), flush=True)
     prof_out = os.environ.get("DLA_TORCH_PROF")
     if prof_out and rank == 0:  # diagnostics only, after the timed region: op -> kernel attribution

@@ -59,6 +59,7 @@ class Bucket:
     launched: bool = False
     pack_table: object = None    # native PackTable (pack mode on GPU)
     views: List[torch.Tensor] = field(default_factory=list)
+    is_ready: List[bool] = field(default_factory=list)  # per parameter, this step
 
     @property
     def nbytes(self) -> int:
@@ -67,6 +68,7 @@ class Bucket:
     def reset(self) -> None:
         self.ready = 0
         self.launched = False
+        self.is_ready = [False] * len(self.params)
 
 
 def dtype_fusion_groups(params: Sequence[torch.Tensor], grouping_size: int) -> List[List[torch.Tensor]]:

@@ -144,9 +144,15 @@ class GradSync:
         self.passes_per_step = int(passes_per_step)
         self._pass_count = {}
         self._hooks = []
+        # DLA_HOOK_TIMING=1: host seconds spent inside the gradient-ready hooks (the Python work the
+        # autograd thread does per parameter, incl. the engine's enqueue of complete buckets)
+        self.hook_s, self.hook_calls = 0.0, 0
         if overlap:
+            import os
+
+            hook = self._on_grad_ready_timed if os.environ.get("DLA_HOOK_TIMING") == "1" else self._on_grad_ready
             for p in self.params:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
+                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
         self.step_count = 0
         if hasattr(self.executor, "reserve"):
             self.executor.reserve(self.buckets)
@@ -225,6 +231,14 @@ class GradSync:
                 p.grad = torch.zeros_like(p)
             self._ready(p)
 
+    def _on_grad_ready_timed(self, p: torch.Tensor) -> None:
+        import time
+
+        t0 = time.perf_counter()
+        self._on_grad_ready(p)
+        self.hook_s += time.perf_counter() - t0
+        self.hook_calls += 1
+
     def _on_grad_ready(self, p: torch.Tensor) -> None:
         if not self._enabled:
             return
@@ -242,15 +256,18 @@ class GradSync:
 
     def _ready(self, p: torch.Tensor) -> None:
         b, j = self._owner[id(p)]
+        if len(b.is_ready) != len(b.params):
+            b.is_ready = [False] * len(b.params)
+        if b.is_ready[j]:
+            raise RuntimeError(f"bucket {b.index}: parameter reported ready twice in one step "
+                               "(backward called twice without prepare()/no_sync?)")
+        b.is_ready[j] = True
         if self.grad_mode == "steal" and p.grad is not None:
             g = p.grad
             if g.dtype != b.flat.dtype or not same_layout(g, p):
                 g = g.to(b.flat.dtype) if same_layout(g, p) else torch.empty_like(p, dtype=b.flat.dtype).copy_(g)
             b.stolen.append((g, b.offsets[j]))
         b.ready += 1
-        if b.ready > len(b.params):
-            raise RuntimeError(f"bucket {b.index}: parameter reported ready twice in one step "
-                               "(backward called twice without prepare()/no_sync?)")
         self._launch_in_order()
 
     def _launch_in_order(self) -> None:
@@ -269,9 +286,10 @@ class GradSync:
         for b in self.buckets[self._next:]:
             if b.ready < len(b.params):
                 if self.grad_mode == "steal":
-                    recorded = {off for _, off in b.stolen}
-                    for p, off in zip(b.params, b.offsets):
-                        if off not in recorded:
+                    if len(b.is_ready) != len(b.params):
+                        b.is_ready = [False] * len(b.params)
+                    for j, p in enumerate(b.params):
+                        if not b.is_ready[j]:  # (marked-unused parameters are ready already)
                             if p.grad is None and not self.passthrough:
                                 p.grad = torch.zeros_like(p)
                             self._ready(p)  # records the gradient (no launch: bucket incomplete until the end)

@@ -322,3 +322,37 @@ def test_resume_with_real_loader_continues_the_batch_sequence(tmp_path):
     assert lines[0].startswith("Worker 0:0 loss for batch 6: ")
     assert first == full[:6]
     assert second == pytest.approx(full[6:], rel=1e-5, abs=1e-6)
+
+
+def test_gradsync_steal_mode_unused_params_without_overlap():
+    """Steal mode (the native engine's) + no overlap hooks (SeqMergeDist) + parameters marked unused
+    (GoogLeNet aux heads) at one rank: flush must not report the unused ones ready a second time
+    (round-3 GPU CLI failure in experiment1's seq_merge)."""
+    from distributed_learning_amd.parallel.executor import Executor
+    from distributed_learning_amd.parallel.grad_sync import GradSync
+
+    class StealExec(Executor):
+        supports_steal = True
+        passthrough = True
+
+        def __init__(self):
+            self.submitted = []
+
+        def submit(self, b):
+            self.submitted.append(b.index)
+
+        def finish(self):
+            pass
+
+    net = torch.nn.Sequential(torch.nn.Linear(4, 4), torch.nn.Linear(4, 4), torch.nn.Linear(4, 2))
+    ex = StealExec()
+    gs = GradSync(net.parameters(), bucket_cap_bytes=64, executor=ex, overlap=False)
+    assert gs.grad_mode == "steal"
+    for _ in range(2):
+        gs.prepare()
+        unused = list(net[1].parameters())
+        gs.mark_ready(unused)
+        net[2](net[0](torch.randn(3, 4))).sum().backward()
+        gs.synchronize()
+        assert sorted(ex.submitted) == list(range(len(gs.buckets)))
+        ex.submitted.clear()
