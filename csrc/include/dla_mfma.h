@@ -38,6 +38,12 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
 constexpr int kThreads = 256;
 constexpr int kBK = 64;
 
+// GEMM epilogues load their addends for all of a thread's rows before the store loop (1), or per row
+// inside it (0; build-time A/B: python -m distributed_learning_amd._build -D DLA_EPI_PRELOAD=0 --out ...)
+#ifndef DLA_EPI_PRELOAD
+#define DLA_EPI_PRELOAD 1
+#endif
+
 // resident blocks per CU a kernel is compiled for: 2 for the 4-wave 128x128-or-smaller tiles
 // (64 KB of 2-stage LDS each), 1 for the 8-wave tiles and the 4-wave 256x128 / 128x256 tiles
 // (3-stage LDS-DMA at 144 KB)
@@ -852,6 +858,39 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
       mr[it] = (ok && bnb->mode == 2) ? (uint32_t)bnb->mask[off >> 3] : 0xffu;
     }
   }
+  // The addends (D, its mask bits, the stride-2 d2) of all this thread's rows are loaded up front too:
+  // loaded inside the store loop, each row waited a full round trip for its addend before its store
+  // (the ISA showed vmcnt(0) twice per row), so a dgrad epilogue cost ~2 NIT serial HBM latencies.
+  ushort8_t dr[NIT], er[NIT];
+  uint32_t dbr[NIT];
+  bool eok[NIT];
+  constexpr bool kPre = DLA_EPI_PRELOAD != 0;  // build-time A/B switch (-DDLA_EPI_PRELOAD=0: per-row loads)
+  if (kPre && D) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int r = (tid + it * NT) / CPR;
+      const int64_t gm = row0 + r;
+      const int gn = col0 + my_cc;
+      const bool ok = gm < M && gn < N;
+      dr[it] = ok ? *reinterpret_cast<const ushort8_t*>(D + gm * ldd + gn) : zero8();
+      dbr[it] = (ok && dmask) ? (uint32_t)dmask[(gm * ldd + gn) >> 3] : 0xffu;
+    }
+  }
+  if (kPre && d2) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int r = (tid + it * NT) / CPR;
+      const int64_t gm = row0 + r;
+      const int gn = col0 + my_cc;
+      const uint32_t q = fdiv((uint32_t)gm, epi->fW);
+      const int w = (int)gm - (int)q * epi->W;
+      const uint32_t n = fdiv(q, epi->fH);
+      const int h = (int)q - (int)n * epi->H;
+      eok[it] = gm < M && gn < N && ((h | w) & 1) == 0;
+      const int64_t r2 = ((int64_t)n * (epi->H >> 1) + (h >> 1)) * (epi->W >> 1) + (w >> 1);
+      er[it] = eok[it] ? *reinterpret_cast<const ushort8_t*>(d2 + r2 * ldc + gn) : zero8();
+    }
+  }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int c = tid + it * NT;
@@ -861,20 +900,29 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
     if (gm < M && gn < N) {
       ushort8_t v = *reinterpret_cast<ushort8_t*>(Cs + r * LDS_C + cc);
       if (D) {
-        const ushort8_t d = *reinterpret_cast<const ushort8_t*>(D + gm * ldd + gn);
-        const uint32_t db = dmask ? (uint32_t)dmask[(gm * ldd + gn) >> 3] : 0xffu;
+        const ushort8_t d = kPre ? dr[it] : *reinterpret_cast<const ushort8_t*>(D + gm * ldd + gn);
+        const uint32_t db = kPre ? dbr[it] : (dmask ? (uint32_t)dmask[(gm * ldd + gn) >> 3] : 0xffu);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           v[j] = f32_to_bf16(bf16_to_f32(v[j]) + (((db >> j) & 1u) ? bf16_to_f32(d[j]) : 0.f));
       }
       if (d2) {
-        const uint32_t q = fdiv((uint32_t)gm, epi->fW);
-        const int w = (int)gm - (int)q * epi->W;
-        const uint32_t n = fdiv(q, epi->fH);
-        const int h = (int)q - (int)n * epi->H;
-        if (((h | w) & 1) == 0) {
-          const int64_t r2 = ((int64_t)n * (epi->H >> 1) + (h >> 1)) * (epi->W >> 1) + (w >> 1);
-          const ushort8_t e = *reinterpret_cast<const ushort8_t*>(d2 + r2 * ldc + gn);
+        bool ok2;
+        ushort8_t e;
+        if constexpr (kPre) {
+          ok2 = eok[it];
+          e = er[it];
+        } else {
+          const uint32_t q = fdiv((uint32_t)gm, epi->fW);
+          const int w = (int)gm - (int)q * epi->W;
+          const uint32_t n = fdiv(q, epi->fH);
+          const int h = (int)q - (int)n * epi->H;
+          ok2 = ((h | w) & 1) == 0;
+          e = ok2 ? *reinterpret_cast<const ushort8_t*>(
+                        d2 + (((int64_t)n * (epi->H >> 1) + (h >> 1)) * (epi->W >> 1) + (w >> 1)) * ldc + gn)
+                  : zero8();
+        }
+        if (ok2) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(e[j]));
         }
