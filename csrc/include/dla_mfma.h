@@ -864,7 +864,9 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
   ushort8_t dr[NIT], er[NIT];
   uint32_t dbr[NIT];
   bool eok[NIT];
-  constexpr bool kPre = DLA_EPI_PRELOAD != 0;  // build-time A/B switch (-DDLA_EPI_PRELOAD=0: per-row loads)
+  // build-time A/B switch (-DDLA_EPI_PRELOAD=0: per-row loads); dgrad instantiations (kEpi) only: the
+  // preload arrays cost VGPRs that lowered the forward GEMMs' occupancy (+0.6 ms/step, g09)
+  constexpr bool kPre = DLA_EPI_PRELOAD != 0 && kEpi;
   if (kPre && D) {
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
