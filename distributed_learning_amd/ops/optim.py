@@ -39,6 +39,22 @@ class FusedSGD(torch.optim.Optimizer):
         self.master_weights = master_weights
         self._tables = {}
 
+    def load_state_dict(self, state_dict):
+        """torch.optim.Optimizer.load_state_dict casts floating-point state to each parameter's dtype
+        (through a policy it calls by class name); the fp32 master copies and momentum buffers of
+        bf16 parameters must stay fp32 for a bit-exact resume, so they are re-installed afterwards."""
+        keep = {}
+        for idx, st in state_dict.get("state", {}).items():
+            for k in ("master", "momentum_buffer"):
+                if k in st and torch.is_tensor(st[k]) and st[k].dtype == torch.float32:
+                    keep[(idx, k)] = st[k]
+        super().load_state_dict(state_dict)
+        params = [p for g in self.param_groups for p in g["params"]]
+        for (idx, k), v in keep.items():
+            p = params[idx]
+            self.state[p][k] = v.to(device=p.device, copy=True)
+        self._tables = {}
+
     def _master(self, p):
         if p.dtype == torch.float32 or not self.master_weights:
             return None

@@ -356,3 +356,21 @@ def test_gradsync_steal_mode_unused_params_without_overlap():
         gs.synchronize()
         assert sorted(ex.submitted) == list(range(len(gs.buckets)))
         ex.submitted.clear()
+
+
+def test_fused_sgd_master_state_survives_checkpoint(tmp_path):
+    """bf16 parameters + fp32 masters: a checkpoint round trip keeps the masters and momentum fp32 and
+    bit-exact (torch's load_state_dict would cast them to the parameter dtype)."""
+    from distributed_learning_amd.ops.optim import FusedSGD
+
+    p = torch.nn.Parameter(torch.randn(33).to(torch.bfloat16))
+    opt = FusedSGD([p], lr=0.1, momentum=0.5, master_weights=True)
+    p.grad = torch.randn(33).to(torch.bfloat16)
+    opt.step()
+    torch.save(opt.state_dict(), tmp_path / "o.pt")
+    q = torch.nn.Parameter(p.detach().clone())
+    opt2 = FusedSGD([q], lr=0.1, momentum=0.5, master_weights=True)
+    opt2.load_state_dict(torch.load(tmp_path / "o.pt", weights_only=True))
+    for k in ("master", "momentum_buffer"):
+        assert opt2.state[q][k].dtype == torch.float32
+        assert torch.equal(opt2.state[q][k], opt.state[p][k])
