@@ -45,13 +45,20 @@ def _model_for(config, device):
     spec = get_spec(config.model_name)
     torch.manual_seed(config.seed)  # identical init on all ranks (reference main.py:31) ...
     model = spec.build().to(device)
-    if device.type == "cuda":
+    if _channels_last(config, device):
         model = model.to(memory_format=torch.channels_last)
     return spec, model
 
 
 def _precision(config, device) -> str:
     return getattr(config, "precision", "fp32") if device.type == "cuda" else "fp32"
+
+
+def _channels_last(config, device) -> bool:
+    """NHWC on the GPU for the native (bf16) kernels; the fp32 reference-precision path keeps the
+    reference's NCHW layout, where MIOpen has its tuned fp32 kernels (fp32 NHWC fell back to kernels
+    that needed minutes per GoogLeNet step)."""
+    return device.type == "cuda" and _precision(config, device) != "fp32"
 
 
 def setup_compute_path(config, device) -> str:
@@ -61,7 +68,9 @@ def setup_compute_path(config, device) -> str:
         dnn.set_backend("torch")
         dnn.set_native_conv(False)
         return prec
-    torch.backends.cudnn.benchmark = True
+    # MIOpen's exhaustive find for the fp32 reference-precision path costs minutes of tuning per new
+    # shape; its default (immediate-mode) choice is what the reference's own runs used
+    torch.backends.cudnn.benchmark = prec != "fp32"
     native = config.kernels == "native" and prec != "fp32"  # the native kernels are bf16 kernels
     dnn.set_backend("native" if native else "torch")
     dnn.set_native_conv(native and getattr(config, "conv", "native") == "native")
@@ -74,7 +83,7 @@ def _data_for(config, spec, device, rank: int, node_id: int, worker_id: int, dty
             print_d(f"dataset root {config.dataset_root!r} not found: using synthetic data", Level.WARNING)
         return D.SyntheticBatches(config.batch_size, spec.input_shape, spec.num_classes, device,
                                   dtype=dtype, seed=config.seed, rank=rank,
-                                  channels_last=device.type == "cuda")
+                                  channels_last=_channels_last(config, device))
     ds = D.load_dataset(spec.dataset, config.dataset_root)
     return D.get_partition_loader(ds, node_id, worker_id, config.node_dev, config.total_dev, config.batch_size)
 
@@ -139,6 +148,7 @@ def worker_process(config, distribute_model: Callable, reducer, experiment_name:
     sync_mode = int(config.sync_timers or 0)
     timers = Timers(sync=sync_mode == 1)
     batch_sync = sync_mode == 2 and device.type == "cuda"
+    cl = _channels_last(config, device)
     ev = EventTimers() if device.type == "cuda" else None
     train_set = _data_for(config, spec, device, rank, node_id, worker_id,
                           dtype=torch.bfloat16 if prec == "bf16" else torch.float32)
@@ -179,7 +189,7 @@ def worker_process(config, distribute_model: Callable, reducer, experiment_name:
             y = y.to(device, non_blocking=True)
             if prec == "bf16" and x.is_floating_point() and x.dtype != torch.bfloat16:
                 x = x.to(torch.bfloat16)
-            if device.type == "cuda" and x.dim() == 4:
+            if x.dim() == 4 and cl:
                 x = x.contiguous(memory_format=torch.channels_last)
             timers.end("data2dev")
 

@@ -1,41 +1,63 @@
 """Join the FETCH_SIZE / WRITE_SIZE passes of scripts/gpu_pmc_bench.sh with the kernel durations:
-per kernel name, calls per step, ms per step, HBM-side MB per step and achieved TB/s.
-(The last `steps` dispatches of every kernel name are taken as the steady state.)"""
+HBM-side MB and achieved TB/s per kernel, per step.
+
+    python scripts/pmc_bytes.py [DIR=gpurun_out] [--by-grid]
+
+Steady state: the dispatches after the last-but-``steps`` ``xent_mean_kernel`` (one per training step),
+i.e. the last ``steps`` whole steps of the profiled run. ``--by-grid`` keys the rows by (kernel, grid
+size), which separates the layers one GEMM / conv template serves. Durations are those of the counter
+run (dispatches serialised by the profiler): within a few % of the kernel-trace run for kernels of
+more than ~50 us.
+"""
+import argparse
 import collections
 import csv
-import sys
-
-d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 
 
-def load(c):
-    rows = list(csv.DictReader(open(f"{d}/pmcb_{c}/p_counter_collection.csv")))
+def load(d, c):
     out = {}
-    for r in rows:
+    for r in csv.DictReader(open(f"{d}/pmcb_{c}/p_counter_collection.csv")):
         key = int(r["Dispatch_Id"])
-        e = out.setdefault(key, {"name": r["Kernel_Name"], "v": 0.0, "t": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
+        e = out.setdefault(key, {"name": r["Kernel_Name"], "grid": r.get("Grid_Size", ""), "v": 0.0,
+                                 "t": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
         e["v"] += float(r["Counter_Value"])
     return out
 
 
-f, w = load("FETCH_SIZE"), load("WRITE_SIZE")
-# steady state: the last third of dispatches (bench: 3 warmup + 3 timed + profiling tail)
-ids = sorted(f)
-tail = ids[len(ids) // 2:]
-agg = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0])
-for i in tail:
-    n = f[i]["name"]
-    short = n.split("(")[0][:90]
-    a = agg[short]
-    a[0] += 1
-    a[1] += f[i]["t"] / 1e6
-    a[2] += f[i]["v"] / 1024  # FETCH_SIZE is in KB
-    a[3] += (w[i]["v"] / 1024) if i in w else 0.0
-nst = max(1, round(len(tail) / max(1, len(ids)) * 6))
-tot = sum(a[1] for a in agg.values())
-print(f"| kernel | calls | ms | fetch MB | write MB | TB/s |\n|---|---:|---:|---:|---:|---:|")
-for k, a in sorted(agg.items(), key=lambda kv: -kv[1][1])[:45]:
-    tb = (a[2] + a[3]) / 1e6 / (a[1] / 1e3) if a[1] else 0
-    print(f"| `{k}` | {a[0]} | {a[1]:.3f} | {a[2]:.0f} | {a[3]:.0f} | {tb:.2f} |")
-print(f"\ntotal kernel ms in window: {tot:.2f}")
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir", nargs="?", default="gpurun_out")
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--by-grid", action="store_true")
+    ap.add_argument("--top", type=int, default=60)
+    a = ap.parse_args()
+    f, w = load(a.dir, "FETCH_SIZE"), load(a.dir, "WRITE_SIZE")
+    ids = sorted(f)
+    marks = [i for i in ids if "xent_mean" in f[i]["name"]]
+    steps = min(a.steps, max(1, len(marks) - 1))
+    start = marks[-steps - 1] if len(marks) > steps else ids[len(ids) // 2]
+    tail = [i for i in ids if i > start]
+    agg = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0])
+    for i in tail:
+        short = f[i]["name"].split("(")[0][:90]
+        key = (short, f[i]["grid"]) if a.by_grid else (short, "")
+        e = agg[key]
+        e[0] += 1
+        e[1] += f[i]["t"] / 1e6
+        e[2] += f[i]["v"] / 1024  # FETCH_SIZE / WRITE_SIZE are in KB
+        e[3] += (w[i]["v"] / 1024) if i in w else 0.0
+    tot_ms = sum(e[1] for e in agg.values()) / steps
+    tot_mb = sum(e[2] + e[3] for e in agg.values()) / steps
+    grid_col = " grid |" if a.by_grid else ""
+    print(f"steady-state steps: {steps}; per step: {tot_ms:.2f} ms of kernels (counter run), "
+          f"{tot_mb / 1e3:.1f} GB HBM-side, {tot_mb / 1e6 / (tot_ms / 1e3):.2f} TB/s average\n")
+    print(f"| kernel |{grid_col} calls/step | ms/step | fetch MB/step | write MB/step | TB/s |")
+    print("|---|" + ("---:|" if a.by_grid else "") + "---:|---:|---:|---:|---:|")
+    for (k, g), e in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
+        tb = (e[2] + e[3]) / 1e6 / (e[1] / 1e3) if e[1] else 0.0
+        gc = f" {g} |" if a.by_grid else ""
+        print(f"| `{k}` |{gc} {e[0] / steps:g} | {e[1] / steps:.3f} | {e[2] / steps:.0f} | {e[3] / steps:.0f} | {tb:.2f} |")
+
+
+if __name__ == "__main__":
+    main()
