@@ -23,6 +23,7 @@ numel % N != 0 work with no dummy traffic.
 """
 from __future__ import annotations
 
+import functools
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -49,6 +50,18 @@ def split_ranges(n: int, parts: int, align: int = ALIGN) -> List[Tuple[int, int]
 
 
 def edge_disjoint_rings(n: int, want: int) -> List[List[int]]:
+    """Up to ``want`` edge-disjoint directed rings of K_n (cached: the search is deterministic and
+    costs milliseconds at n = 8, which a per-call caller such as the virtual-rank harness would
+    otherwise pay on every all-reduce)."""
+    return [list(r) for r in _edge_disjoint_rings(n, want)]
+
+
+@functools.lru_cache(maxsize=None)
+def _edge_disjoint_rings(n: int, want: int) -> Tuple[Tuple[int, ...], ...]:
+    return tuple(tuple(r) for r in _search_rings(n, want))
+
+
+def _search_rings(n: int, want: int) -> List[List[int]]:
     """Up to ``want`` directed Hamiltonian cycles of K_n with pairwise-disjoint directed edges.
 
     For an 8-GPU MI355X node (7 xGMI links per GPU) ``want = 7`` yields 7 rings whose union uses
