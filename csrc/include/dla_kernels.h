@@ -245,6 +245,13 @@ inline int tile_bn(int cfg) {
 }
 // rows of BN-statistics partials ([rows][N][2]) a stats-producing launch writes (one per row tile)
 int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto, int K = 0);
+// Persistent streaming 1x1 GEMM (gemm_stream.hip) for K in {64, 128, 256}, N % 64 == 0, long M: the
+// number of BN-statistics partial rows it writes (0 = shape not served: use launch_gemm_nt), and the
+// launcher (false = not served). set_gemm_stream: -1 environment (DLA_GEMM_STREAM, default on), 0 / 1.
+int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc);
+bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
+                        int M, int N, int K, float* stats, hipStream_t stream);
+void set_gemm_stream(int mode);
 // Virtual conv output (gemm.hip gemm_vy_kernel): y = A * B^T (stride-1 1x1 conv, B = [N][K] weights)
 // recomputed by each consumer. mode 0 statistics partials, 1 out = relu(BN(y) + res) + ReLU bits,
 // 2 BN-backward reduce partials from dy and the bits, 3 BN-backward apply (dx). part: [gemm_vy_rows][N][2].

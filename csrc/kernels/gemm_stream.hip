@@ -1,0 +1,338 @@
+// Persistent streaming GEMM for the memory-bound 1x1 convolutions (short K, long M):
+//   C[M, N] = A[M, K] * B^T,  B = W [N][K] (forward) or W [K][N] (data gradient, k-major),
+//   K in {64, 128, 256}, bf16 in / out, fp32 accumulate, optional BatchNorm column statistics.
+//
+// Why a second 1x1 kernel. The tile-per-block gemm_nt (gemm.hip) runs each tile as
+// load -> MFMA -> epilogue -> store, one latency after the other; at K <= 256 its blocks hold less than
+// one tile of loads in flight per CU on average, and the per-kernel bytes table
+// (profiles/r3/resnet50_bs1024_bytes_per_kernel.md) shows those kernels at 3.6-3.8 TB/s against 5.6 TB/s
+// for the BatchNorm streams next to them. Here
+//   * one block per CU stays resident over a strided set of 128-row tiles (grid = CUs), the weight
+//     panel [BN][K] is staged into LDS ONCE per block;
+//   * A moves HBM -> LDS by buffer LDS-DMA (no VGPRs) through a ring of kS 64-deep K-chunk slots, kP chunks
+//     ahead of the MFMAs and ACROSS tile boundaries, so the next tile's rows are in flight while this
+//     tile multiplies and stores: ~64 KB in flight per CU at all times;
+//   * the product is computed transposed (weights as the MFMA A operand), with the weight rows
+//     permuted in LDS so that each lane's 16 accumulators of one output row are 16 consecutive
+//     channels: the tile leaves straight from registers as two 16-byte buffer stores per row and lane
+//     (no LDS round trip, no barrier);
+//   * every memory op is a buffer op whose out-of-range offset the hardware zero-fills / drops, so each
+//     loop iteration issues the same number of them and the vmcnt waits are compile-time counts;
+//   * BatchNorm statistics of the stored (bf16-rounded) outputs accumulate in registers over all of a
+//     block's tiles and are reduced once at the end: one [N][2] partial row per row group, fixed order.
+// Blocks of one row group (its N / BN column panels) sit on one XCD and read the same A rows from
+// that XCD's L2.
+#include <cstdlib>
+
+#include "dla_common.h"
+#include "dla_kernels.h"
+#include "dla_mfma.h"
+
+namespace dla {
+
+using namespace mm;
+
+namespace {
+
+constexpr int kSBM = 128;  // rows per tile
+constexpr int kSP = 4;     // K-chunks in flight ahead of the MFMAs
+constexpr int kSS = kSP + 1;  // ring slots (one being read, kSP in flight)
+constexpr int kChunkElems = kSBM * kBK;  // one ring slot [128][64]
+
+struct StreamArgs {
+  const bf16_t* a;
+  int64_t lda;
+  const bf16_t* b;
+  int64_t ldb;
+  bf16_t* c;
+  int64_t ldc;
+  int M, N;
+  int mg;       // row groups (blocks per column panel)
+  int per_xcd;  // row groups per XCD
+  float* stats;  // [mg][N][2] or null
+};
+
+// image row of panel-local weight row p (0..63 within a wave's 64 columns): the MFMA A-operand row
+// 16 i + 4 g + r holds output column 16 g + 4 i + r, so lane group g accumulates columns 16 g .. 16 g + 15
+__device__ __forceinline__ int perm64(int p) { return 16 * ((p >> 2) & 3) + 4 * (p >> 4) + (p & 3); }
+
+// element offset of (row, logical 8-element chunk lc) in a [rows][64] LDS image (rm_glds_frag's swizzle)
+__device__ __forceinline__ int img_off(int row, int lc) { return row * kBK + ((lc ^ ((row >> 1) & 7)) << 3); }
+
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+template <int BN, int KC, bool kBT, bool kStats>
+__global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s) {
+  constexpr int WN = 64;                    // columns per wave
+  constexpr int WGN = BN / WN;              // waves along N (2 or 1)
+  constexpr int WGM = 4 / WGN;              // waves along M
+  constexpr int WM = kSBM / WGM;            // rows per wave (64 or 32)
+  constexpr int TJ = WM / 16;               // 16-row fragments per wave
+  constexpr int Q = kSP / KC;               // tile ends inside kSP consecutive chunks
+  static_assert(kSP % KC == 0, "the in-flight window must hold whole tiles");
+  constexpr int D = kChunkElems / 8 / 256;  // LDS-DMA instructions per wave per chunk (4)
+  constexpr int E = 2 * TJ;                 // buffer stores per wave per tile
+  constexpr int kPanelElems = BN * kBK;     // one weight sub-image [BN][64]
+
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16_t* Bs = reinterpret_cast<bf16_t*>(smem_raw);  // KC sub-images [BN][64]
+  bf16_t* ring = Bs + KC * kPanelElems;              // kSS slots [128][64]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave % WGN, wm = wave / WGN;
+  const int lr = lane & 15, g = lane >> 4;
+  // XCD-aware block -> (column panel, row group)
+  const int nbn = s.N / BN;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int bn = slot % nbn;
+  const int grp = xcd * s.per_xcd + slot / nbn;
+  const int col0 = bn * BN;
+  const int M = s.M;
+  const int mt = (M + kSBM - 1) / kSBM;
+  const int ntile = grp < mt ? (mt - grp + s.mg - 1) / s.mg : 0;
+  const int nchunk = ntile * KC;
+
+  // ---- weight panel -> LDS (once): rows permuted per 64-column wave panel --------------------------
+  // all of a thread's chunk loads are issued before any LDS write (one latency, not one per chunk)
+  {
+    constexpr int kPer = BN * KC * kBK / 8 / 256;  // 16-byte chunks per thread (2 .. 16)
+    static_assert(BN * KC * kBK / 8 % 256 == 0, "whole chunks per thread");
+    ushort8_t v[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int c = tid + u * 256;
+      if constexpr (!kBT) {
+        const int n = c / (KC * 8), kc = c % (KC * 8);  // 8-element chunk kc of weight row n
+        v[u] = *reinterpret_cast<const ushort8_t*>(s.b + (int64_t)(col0 + n) * s.ldb + kc * 8);
+      } else {
+        const int k = c / (BN / 8), nc = (c % (BN / 8)) * 8;  // 8 columns nc.. of k-row k
+        v[u] = *reinterpret_cast<const ushort8_t*>(s.b + (int64_t)k * s.ldb + col0 + nc);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int c = tid + u * 256;
+      if constexpr (!kBT) {
+        const int n = c / (KC * 8), kc = c % (KC * 8);
+        const int row = (n & ~63) + perm64(n & 63);
+        *reinterpret_cast<ushort8_t*>(Bs + (kc >> 3) * kPanelElems + img_off(row, kc & 7)) = v[u];
+      } else {
+        const int k = c / (BN / 8), nc = (c % (BN / 8)) * 8;
+        bf16_t* sub = Bs + (k >> 6) * kPanelElems;
+        const int kk = k & 63;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int n = nc + e, row = (n & ~63) + perm64(n & 63);
+          sub[img_off(row, kk >> 3) + (kk & 7)] = v[u][e];
+        }
+      }
+    }
+  }
+
+  // ---- A ring: chunk q = (tile q / KC, k-chunk q % KC) -> slot q % kSS ------------------------------
+  const __amdgpu_buffer_rsrc_t ra = make_srd(s.a, (uint32_t)((int64_t)M * s.lda * 2));
+  uint32_t vo[D];
+  int vr[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    const int c = tid + i * 256, r = c >> 3;
+    vr[i] = r;
+    vo[i] = (uint32_t)(((int64_t)r * s.lda + rm_glds_kc(c)) * 2);
+  }
+  const uint32_t ring0 = lds_addr(ring) + (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
+  auto issue = [&](int q) {
+    const int t = q / KC, kc = q % KC;
+    const int64_t row0 = (int64_t)(grp + t * s.mg) * kSBM;  // past the end for q >= nchunk: all OOB
+    uint32_t o[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) o[i] = row0 + vr[i] < M ? vo[i] : kOOB;
+    const uint32_t soff = row0 < M ? (uint32_t)((row0 * s.lda + kc * kBK) * 2) : 0u;
+    bglds<D, 256 * 16>(o, ra, (uint32_t)__builtin_amdgcn_readfirstlane(soff),
+                       ring0 + (uint32_t)((q % kSS) * kChunkElems * 2));
+  };
+
+  // the weight panel's plain loads and LDS writes must be complete before the ring starts counting
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kSP; ++q) issue(q);
+
+  const __amdgpu_buffer_rsrc_t rc = make_srd(s.c, (uint32_t)((int64_t)M * s.ldc * 2));
+  float st_s[4][4], st_q[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st_s[i][r] = st_q[i][r] = 0.f;
+  accv_t acc[4][TJ];
+
+  for (int q = 0; q < nchunk; ++q) {
+    // this wave's DMAs for chunk q are done once at most the younger ones are outstanding: the chunks
+    // q+1 .. q+kSP-1 (D each) and the stores of the Q tiles that ended after chunk q was issued
+    if (q < kSP) vm_wait<(kSP - 1) * D>();
+    else vm_wait<(kSP - 1) * D + Q * E>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: slot (q-1) % kSS is refilled below
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(q + kSP);  // past this block's last chunk: OOB rows, zeros into a free slot (uniform counts)
+    const int kc = q % KC;
+    if (kc == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = accv_t{};
+    }
+    const bf16_t* As = ring + (q % kSS) * kChunkElems;
+    const bf16_t* Ws = Bs + kc * kPanelElems;
+#pragma unroll
+    for (int kk = 0; kk < kBK / 32; ++kk) {
+      bf16x8_t wf[4], xf[TJ];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) wf[i] = rm_glds_frag(Ws, wn * WN + 16 * i, kk);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) xf[j] = rm_glds_frag(As, wm * WM + 16 * j, kk);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = mfma(wf[i], xf[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    if (kc == KC - 1) {
+      // ---- tile epilogue: lane (lr, g) holds rows wm*WM + 16 j + lr, columns wn*64 + 16 g .. + 15 ----
+      const int64_t row0 = (int64_t)(grp + (q / KC) * s.mg) * kSBM;
+      const int gc = col0 + wn * WN + 16 * g;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int64_t gm = row0 + wm * WM + 16 * j + lr;
+        const bool ok = gm < M;
+        uint32_t w[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          bf16_t h[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            h[r] = f32_to_bf16(acc[i][j][r]);
+            if constexpr (kStats) {
+              const float v = bf16_to_f32(h[r]);  // statistics of the stored values; OOB rows are 0
+              st_s[i][r] += v;
+              st_q[i][r] = fmaf(v, v, st_q[i][r]);
+            }
+          }
+          w[2 * i] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+          w[2 * i + 1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+        }
+        const uint32_t off = ok ? (uint32_t)((gm * s.ldc + gc) * 2) : kOOB;
+        const i32x4_t lo{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+        const i32x4_t hi{(int)w[4], (int)w[5], (int)w[6], (int)w[7]};
+        __builtin_amdgcn_raw_buffer_store_b128(lo, rc, ok ? off : kOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(hi, rc, ok ? off + 16 : kOOB, 0, 0);
+      }
+    }
+  }
+  vm_wait<0>();  // no LDS-DMA may land after the block's LDS is released
+  if constexpr (kStats) {
+    // columns of this lane: wn*64 + 16 g + 4 i + r; sum the 16 row lanes (lr), then the WGM waves
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int x = 1; x < 16; x <<= 1) {
+          st_s[i][r] += __shfl_xor(st_s[i][r], x, 64);
+          st_q[i][r] += __shfl_xor(st_q[i][r], x, 64);
+        }
+    __syncthreads();  // every wave is past its last ring read: reuse the LDS
+    float* red = reinterpret_cast<float*>(smem_raw);  // [WGM][BN][2]
+    if (lr == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = wn * WN + 16 * g + 4 * i + r;
+          red[(wm * BN + n) * 2 + 0] = st_s[i][r];
+          red[(wm * BN + n) * 2 + 1] = st_q[i][r];
+        }
+    }
+    __syncthreads();
+    if (tid < BN * 2 && grp < s.mg) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < WGM; ++w) v += red[w * BN * 2 + tid];
+      s.stats[((int64_t)grp * s.N + col0) * 2 + tid] = v;
+    }
+  }
+}
+
+template <int BN, int KC>
+constexpr size_t stream_lds_bytes() {
+  return (size_t)(KC * BN * kBK + kSS * kChunkElems) * sizeof(bf16_t);
+}
+
+int g_stream_mode = -1;  // -1: environment (DLA_GEMM_STREAM, default on), 0 off, 1 on
+
+bool stream_enabled() {
+  if (g_stream_mode >= 0) return g_stream_mode == 1;
+  static const bool v = [] {
+    const char* e = std::getenv("DLA_GEMM_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+struct StreamPlan {
+  int bn = 0, mg = 0, per_xcd = 0, grid = 0;
+};
+
+StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc) {
+  StreamPlan p;
+  if (!stream_enabled() || M <= 0) return p;
+  if (K != 64 && K != 128 && K != 256) return p;
+  if (N % 64 != 0 || lda % 8 != 0 || ldc % 8 != 0) return p;
+  if (M * lda * 2 >= (int64_t)kOOB || M * ldc * 2 >= (int64_t)kOOB) return p;
+  p.bn = N % 128 == 0 ? 128 : 64;
+  const int nbn = N / p.bn;
+  const int mt = (int)((M + kSBM - 1) / kSBM);
+  // one block per CU: 256 blocks = 8 XCDs x per_xcd row groups x nbn panels; at least two tiles per
+  // row group, or the ring has nothing to overlap (the tile kernel serves small M)
+  int per_xcd = std::max(1, 32 / nbn);
+  while (per_xcd > 1 && mt < 2 * 8 * per_xcd) per_xcd >>= 1;
+  if (mt < 2 * 8 * per_xcd) return StreamPlan{};
+  p.per_xcd = per_xcd;
+  p.mg = 8 * per_xcd;
+  p.grid = p.mg * nbn;
+  return p;
+}
+
+}  // namespace
+
+void set_gemm_stream(int mode) { g_stream_mode = mode < 0 ? -1 : (mode ? 1 : 0); }
+
+int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc) { return stream_plan(M, N, K, lda, ldc).mg; }
+
+bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
+                        int M, int N, int K, float* stats, hipStream_t stream) {
+  const StreamPlan p = stream_plan(M, N, K, lda, ldc);
+  if (!p.mg) return false;
+  StreamArgs a{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, p.mg, p.per_xcd, stats};
+#define DLA_ST(BN_, KC_)                                                                                         \
+  {                                                                                                              \
+    const size_t lds = stream_lds_bytes<BN_, KC_>();                                                             \
+    if (b_kmajor) {                                                                                              \
+      if (stats) hipLaunchKernelGGL((gemm_stream_kernel<BN_, KC_, true, true>), dim3(p.grid), dim3(256), lds, stream, a); \
+      else hipLaunchKernelGGL((gemm_stream_kernel<BN_, KC_, true, false>), dim3(p.grid), dim3(256), lds, stream, a);      \
+    } else {                                                                                                     \
+      if (stats) hipLaunchKernelGGL((gemm_stream_kernel<BN_, KC_, false, true>), dim3(p.grid), dim3(256), lds, stream, a); \
+      else hipLaunchKernelGGL((gemm_stream_kernel<BN_, KC_, false, false>), dim3(p.grid), dim3(256), lds, stream, a);     \
+    }                                                                                                            \
+  }
+  const int kc = K / kBK;
+  if (p.bn == 128) {
+    if (kc == 1) DLA_ST(128, 1) else if (kc == 2) DLA_ST(128, 2) else DLA_ST(128, 4)
+  } else {
+    if (kc == 1) DLA_ST(64, 1) else if (kc == 2) DLA_ST(64, 2) else DLA_ST(64, 4)
+  }
+#undef DLA_ST
+  return true;
+}
+
+}  // namespace dla

@@ -1,0 +1,76 @@
+"""Persistent streaming 1x1 GEMM (csrc/kernels/gemm_stream.hip) vs fp32 PyTorch, and vs the tile kernel.
+
+Shapes cover every instantiation (K = 64 / 128 / 256 -> 1 / 2 / 4 ring chunks per tile, 128- and 64-wide
+column panels, weights [N][K] and k-major [K][N]), ragged M (last tile partly out of range: zero-filled
+loads, dropped stores), several column panels per row group, row-strided A (a channel slice) and the
+BatchNorm-statistics epilogue, whose partial rows must sum to the column sums of the stored bf16 output.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # (M, K, N)
+    (9000, 64, 64), (9000, 64, 256), (20000, 128, 512), (5001, 256, 128), (70000, 256, 64), (33333, 128, 128),
+    (131072, 64, 256),
+]
+
+
+@pytest.fixture
+def C():
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    yield C
+    C.set_gemm_stream(-1)
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("kmajor", [False, True])
+@pytest.mark.parametrize("shape", SHAPES)
+def test_stream_matches_fp32_and_tile_kernel(cuda, C, shape, kmajor):
+    M, K, N = shape
+    g = torch.Generator().manual_seed(M + K + N)
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(cuda, torch.bfloat16)
+    B = W.t().contiguous() if kmajor else W  # dgrad form: [K][N]
+    assert C.gemm_stream_rows(M, N, K, K, N) > 0, "shape not served by the streaming kernel"
+    C.set_gemm_stream(1)
+    out, st = C.gemm_nt(A, B, True, None, kmajor)
+    C.set_gemm_stream(0)
+    ref_tile, _ = C.gemm_nt(A, B, False, None, kmajor)
+    torch.cuda.synchronize()
+    ref = A.float() @ W.float().t()
+    assert _rel(out, ref) < 5e-3
+    # same fp32 accumulation of the same bf16 products: the two kernels agree to bf16 rounding
+    assert float((out.float() - ref_tile.float()).abs().max()) <= float(ref.abs().max()) * 2 ** -7
+    assert st.shape[0] == C.gemm_stream_rows(M, N, K, K, N) and st.shape[1:] == (N, 2)
+    tot = st.double().sum(0)
+    of = out.double()
+    torch.testing.assert_close(tot[:, 0], of.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(tot[:, 1], (of * of).sum(0), rtol=1e-4, atol=1e-3)
+
+
+def test_stream_row_strided_input(cuda, C):
+    """A is a channel slice of a wider tensor (lda > K), as for a branch of a concatenated block input."""
+    M, K, N = 12345, 64, 128
+    g = torch.Generator().manual_seed(7)
+    wide = torch.randn(M, 3 * K, generator=g).to(cuda, torch.bfloat16)
+    A = wide[:, K:2 * K]
+    W = (torch.randn(N, K, generator=g) * 0.1).to(cuda, torch.bfloat16)
+    C.set_gemm_stream(1)
+    if C.gemm_stream_rows(M, N, K, A.stride(0), N) == 0:
+        pytest.skip("strided input not served")
+    out, _ = C.gemm_nt(A, W, False)
+    torch.cuda.synchronize()
+    assert _rel(out, A.float() @ W.float().t()) < 5e-3
+
+
+def test_small_m_stays_on_tile_kernel(cuda, C):
+    # fewer than 2 tiles per row group: the tile kernel serves it (nothing for the ring to overlap)
+    assert C.gemm_stream_rows(1000, 256, 64, 64, 256) == 0
+    assert C.gemm_stream_rows(100000, 256, 512, 512, 256) == 0  # K = 512: not served
