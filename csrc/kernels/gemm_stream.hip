@@ -268,7 +268,7 @@ constexpr size_t stream_lds_bytes() {
   return (size_t)(KC * BN * kBK + kSS * kChunkElems) * sizeof(bf16_t);
 }
 
-int g_stream_mode = -1;  // -1: environment (DLA_GEMM_STREAM, default on), 0 off, 1 on
+int g_stream_mode = -1;  // -1: environment (DLA_GEMM_STREAM, default on), 0 off, 1 on (every K <= 256)
 
 bool stream_enabled() {
   if (g_stream_mode >= 0) return g_stream_mode == 1;
@@ -283,10 +283,14 @@ struct StreamPlan {
   int bn = 0, mg = 0, per_xcd = 0, grid = 0;
 };
 
-StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc) {
+// Served shapes, from the per-layer A/B at ResNet-50 bs1024 (profiles/r3/gemm_stream_ab.md): K = 64 / 128
+// win or tie everywhere (fwd K 64 x N 256 -11 %, dgrad K 128 x N 256 -45 %); at K = 256 only the data
+// gradient (k-major weights) wins (-11 % at N 512); the forward K = 256 shapes lose 1-12 % (N >= 512 at
+// M <= 802k: the tile kernel's 2-4 co-resident blocks beat one 4-wave block per CU there).
+StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor) {
   StreamPlan p;
   if (!stream_enabled() || M <= 0) return p;
-  if (K != 64 && K != 128 && K != 256) return p;
+  if (K != 64 && K != 128 && !(K == 256 && (b_kmajor || g_stream_mode == 1))) return p;
   if (N % 64 != 0 || lda % 8 != 0 || ldc % 8 != 0) return p;
   if (M * lda * 2 >= (int64_t)kOOB || M * ldc * 2 >= (int64_t)kOOB) return p;
   p.bn = N % 128 == 0 ? 128 : 64;
@@ -307,11 +311,13 @@ StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc) {
 
 void set_gemm_stream(int mode) { g_stream_mode = mode < 0 ? -1 : (mode ? 1 : 0); }
 
-int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc) { return stream_plan(M, N, K, lda, ldc).mg; }
+int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor) {
+  return stream_plan(M, N, K, lda, ldc, b_kmajor).mg;
+}
 
 bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
                         int M, int N, int K, float* stats, hipStream_t stream) {
-  const StreamPlan p = stream_plan(M, N, K, lda, ldc);
+  const StreamPlan p = stream_plan(M, N, K, lda, ldc, b_kmajor);
   if (!p.mg) return false;
   StreamArgs a{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, p.mg, p.per_xcd, stats};
 #define DLA_ST(BN_, KC_)                                                                                         \

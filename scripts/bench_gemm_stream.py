@@ -53,7 +53,8 @@ def main():
                 B, km, st = (torch.randn(N, K, device=dev) * 0.05).to(torch.bfloat16), False, True
             else:
                 B, km, st = (torch.randn(K, N, device=dev) * 0.05).to(torch.bfloat16), True, False
-            served = C.gemm_stream_rows(M, N, K, K, N) > 0
+            C.set_gemm_stream(1)
+            served = C.gemm_stream_rows(M, N, K, K, N, km) > 0
             r = {"layer": name, "pass": kind, "M": M, "K": K, "N": N, "stream_served": served}
             byts = (M * K + M * N + K * N) * 2
             for mode in ((1, 0) if served else (0,)):

@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--by-grid", action="store_true")
     ap.add_argument("--top", type=int, default=60)
     ap.add_argument("--stats", default="")
+    # gfx950: FETCH_SIZE reports half the bytes of streaming reads (a pass reading and writing the same
+    # tensor shape, bn_apply_kernel<bf16, false, true, false>, shows fetch = write / 2); scale 2 corrects it
+    ap.add_argument("--fetch-scale", type=float, default=1.0)
     a = ap.parse_args()
     f, w = load(a.dir, "FETCH_SIZE"), load(a.dir, "WRITE_SIZE")
     ids = sorted(f)
@@ -52,7 +55,7 @@ def main():
         e = agg[key]
         e[0] += 1
         e[1] += (mean_ns.get(short, f[i]["t"]) if a.stats else f[i]["t"]) / 1e6
-        e[2] += f[i]["v"] / 1024  # FETCH_SIZE / WRITE_SIZE are in KB
+        e[2] += f[i]["v"] / 1024 * a.fetch_scale  # FETCH_SIZE / WRITE_SIZE are in KB
         e[3] += (w[i]["v"] / 1024) if i in w else 0.0
     tot_ms = sum(e[1] for e in agg.values()) / steps
     tot_mb = sum(e[2] + e[3] for e in agg.values()) / steps

@@ -38,8 +38,9 @@ def test_stream_matches_fp32_and_tile_kernel(cuda, C, shape, kmajor):
     A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
     W = (torch.randn(N, K, generator=g) * K ** -0.5).to(cuda, torch.bfloat16)
     B = W.t().contiguous() if kmajor else W  # dgrad form: [K][N]
-    assert C.gemm_stream_rows(M, N, K, K, N) > 0, "shape not served by the streaming kernel"
     C.set_gemm_stream(1)
+    rows = C.gemm_stream_rows(M, N, K, K, N, kmajor)
+    assert rows > 0, "shape not served by the streaming kernel"
     out, st = C.gemm_nt(A, B, True, None, kmajor)
     C.set_gemm_stream(0)
     ref_tile, _ = C.gemm_nt(A, B, False, None, kmajor)
@@ -48,7 +49,7 @@ def test_stream_matches_fp32_and_tile_kernel(cuda, C, shape, kmajor):
     assert _rel(out, ref) < 5e-3
     # same fp32 accumulation of the same bf16 products: the two kernels agree to bf16 rounding
     assert float((out.float() - ref_tile.float()).abs().max()) <= float(ref.abs().max()) * 2 ** -7
-    assert st.shape[0] == C.gemm_stream_rows(M, N, K, K, N) and st.shape[1:] == (N, 2)
+    assert st.shape[0] == rows and st.shape[1:] == (N, 2)
     tot = st.double().sum(0)
     of = out.double()
     torch.testing.assert_close(tot[:, 0], of.sum(0), rtol=1e-4, atol=1e-3)
@@ -71,6 +72,11 @@ def test_stream_row_strided_input(cuda, C):
 
 
 def test_small_m_stays_on_tile_kernel(cuda, C):
+    C.set_gemm_stream(1)
     # fewer than 2 tiles per row group: the tile kernel serves it (nothing for the ring to overlap)
     assert C.gemm_stream_rows(1000, 256, 64, 64, 256) == 0
     assert C.gemm_stream_rows(100000, 256, 512, 512, 256) == 0  # K = 512: not served
+    # default policy (environment mode): forward K = 256 stays on the tile kernel, dgrad K = 256 streams
+    C.set_gemm_stream(-1)
+    assert C.gemm_stream_rows(802816, 512, 256, 256, 512, False) == 0
+    assert C.gemm_stream_rows(802816, 512, 256, 256, 512, True) > 0
