@@ -7,7 +7,8 @@ MI355X the trade-off has different constants, so the size is derived instead of 
 * **Collective time** of one S-byte bucket, ``T(S) = alpha + beta * S``:
 
   - ``ring`` with C channels over edge-disjoint directed rings (csrc/comm/plan.cpp): 2(N-1) P2P
-    steps, each one RCCL group launch plus one reduce kernel -> ``alpha = 2 (N-1) alpha_step``;
+    steps, each one RCCL group launch plus one multi-lane local-op launch -> ``alpha = 2 (N-1) alpha_step``
+    (alpha_step measured on the virtual-rank harness + an RCCL group input: ``measured_step_alpha_us``);
     every channel moves 2 (N-1)/N * S/C bytes through ONE xGMI link (≈153 GB/s each, 7 per GPU)
     -> ``beta = 2 (N-1) / N / (C * link_bw)``;
   - ``builtin`` (ncclAllReduce): RCCL drives all links itself; ``alpha`` = one launch,
@@ -55,13 +56,38 @@ class CollectiveModel:
         return self.alpha_s + self.beta_s_per_byte * nbytes
 
 
+# Per-step issue cost of the engine's ring schedules, measured on the virtual-rank harness
+# (scripts/vrank_ring_timing.py: the production execute_plan / LocalIssuer code with device copies as
+# links, 8 ranks on one MI355X; fitted by scripts/fit_ring_alpha.py over 64 KiB .. 64 MiB buckets,
+# profiles/r3/g12/vrank_eager.jsonl and profiles/r3/g08b/vrank_graph.jsonl): intercept / 2(N-1) steps.
+# Eager = host issue + the step's multi-lane local-op launches; graph = device-side cost alone.
+VRANK_STEP_ALPHA_US = {("ring", 1, "eager"): 5.3, ("ring", 7, "eager"): 16.1,
+                       ("ring", 1, "graph"): 3.4, ("ring", 7, "graph"): 8.0}
+# What the harness cannot see: one RCCL group (C sends + C receives) per step on a real node. An input,
+# not a measurement (no multi-GPU node is available to the builder); replace it with a fitted value
+# from the engine's comm-stream timers (allreduce_ms_per_step at two bucket sizes) when one is.
+RCCL_GROUP_US = 8.0
+
+
+def measured_step_alpha_us(channels: int, graph: bool = False) -> float:
+    """Issue cost per ring step for C channels: linear between the measured 1- and 7-channel points,
+    plus the RCCL group launch."""
+    mode = "graph" if graph else "eager"
+    a1, a7 = VRANK_STEP_ALPHA_US[("ring", 1, mode)], VRANK_STEP_ALPHA_US[("ring", 7, mode)]
+    c = max(1, min(int(channels), 7))
+    return a1 + (a7 - a1) * (c - 1) / 6.0 + RCCL_GROUP_US
+
+
 def ring_model(world: int, channels: int = 7, link_gbps: float = XGMI_LINK_GBPS,
-               step_alpha_us: float = 12.0) -> CollectiveModel:
-    """Multi-channel P2P ring (the engine's ``ring``): 2(N-1) steps, S/C bytes per channel link."""
+               step_alpha_us: Optional[float] = None, graph: bool = False) -> CollectiveModel:
+    """Multi-channel P2P ring (the engine's ``ring``): 2(N-1) steps, S/C bytes per channel link.
+    ``step_alpha_us`` defaults to :func:`measured_step_alpha_us` for the channel count."""
     n = max(1, world)
     if n == 1:
         return CollectiveModel("ring", 0.0, 0.0)
     c = max(1, min(channels, n - 1))
+    if step_alpha_us is None:
+        step_alpha_us = measured_step_alpha_us(c, graph)
     return CollectiveModel(f"ring{c}", 2 * (n - 1) * step_alpha_us * 1e-6,
                            2.0 * (n - 1) / n / (c * link_gbps * 1e9))
 

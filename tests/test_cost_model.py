@@ -56,3 +56,12 @@ def test_resnet_caps_at_8_gpus(name, bwd_s):
         by = {r["cap_mib"]: r for r in rows}
         assert by[cap]["cost_ms"] <= by[25]["cost_ms"] + 1e-9  # never worse than the reference's 25 MiB
         assert 2 <= cap <= 64
+
+
+def test_ring_alpha_defaults_to_the_measured_issue_cost():
+    a1, a7 = cm.measured_step_alpha_us(1), cm.measured_step_alpha_us(7)
+    assert a1 == cm.VRANK_STEP_ALPHA_US[("ring", 1, "eager")] + cm.RCCL_GROUP_US
+    assert a7 == cm.VRANK_STEP_ALPHA_US[("ring", 7, "eager")] + cm.RCCL_GROUP_US
+    assert a1 < cm.measured_step_alpha_us(4) < a7
+    assert cm.ring_model(8, 7).alpha_s == 14 * a7 * 1e-6
+    assert cm.ring_model(8, 7, graph=True).alpha_s < cm.ring_model(8, 7).alpha_s
