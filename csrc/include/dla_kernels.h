@@ -332,6 +332,13 @@ void launch_stem_fwd(const void* xs, const void* wpk, void* y, int N, int H, int
 int stem_wgrad_splits(int N, int H, int W, int Cout);
 void launch_stem_wgrad(const void* dy, const void* xs, float* partial, int splits, void* dwpk, int out_dtype, int N,
                        int H, int W, int Cout, hipStream_t stream);
+// Halo-tiled 64 -> 64 channel 3x3 / stride-1 weight gradient (conv_halo_wgrad.hip): persistent blocks over
+// a padded pixel space, x rows through an LDS ring; splits = partial slabs of [64][9][64] fp32.
+bool halo_wgrad_eligible(int Cin, int Cout, int W, int stride);
+void set_halo_wgrad(int mode);  // -1 environment (DLA_HALO_WGRAD, default on), 0 off, 1 on
+int halo_wgrad_splits(int N, int H, int W);
+void launch_conv3x3_halo_wgrad(const void* dy, const void* x, float* partial, int splits, void* dw, int out_dtype,
+                               int N, int H, int W, hipStream_t stream);
 int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int stride);
 void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int splits, void* dw, int out_dtype, int N,
                           int H, int W, int Cin, int Cout, int stride, hipStream_t stream);

@@ -1000,9 +1000,16 @@ at::Tensor conv3x3_wgrad(at::Tensor dy, at::Tensor x, int64_t stride, c10::Scala
   TORCH_CHECK(x.numel() / x.size(1) < (1 << 24), "conv3x3_wgrad: too many pixels");
   const int N = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Cout = (int)dy.size(1);
   TORCH_CHECK(dy.size(2) == (H - 1) / stride + 1 && dy.size(3) == (W - 1) / stride + 1, "conv3x3_wgrad: dy shape");
+  at::Tensor dw = at::empty({Cout, Cin, 3, 3}, x.options().dtype(out_dtype).memory_format(at::MemoryFormat::ChannelsLast));
+  if (halo_wgrad_eligible(Cin, Cout, W, (int)stride) && (int64_t)N * (H + 2) * (W + 2) < (1 << 30)) {
+    const int hs = halo_wgrad_splits(N, H, W);
+    at::Tensor hpart = at::empty({(int64_t)hs * Cout * 9 * Cin}, x.options().dtype(at::kFloat));
+    launch_conv3x3_halo_wgrad(dy.data_ptr(), x.data_ptr(), hpart.data_ptr<float>(), hs, dw.data_ptr(),
+                              out_dtype == at::kFloat ? kF32 : kBF16, N, H, W, current_stream(x));
+    return dw;
+  }
   const int splits = conv3x3_wgrad_splits(N, H, W, Cin, Cout, (int)stride);
   at::Tensor part = at::empty({(int64_t)splits * Cout * 9 * Cin}, x.options().dtype(at::kFloat));
-  at::Tensor dw = at::empty({Cout, Cin, 3, 3}, x.options().dtype(out_dtype).memory_format(at::MemoryFormat::ChannelsLast));
   launch_conv3x3_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), splits, dw.data_ptr(),
                        out_dtype == at::kFloat ? kF32 : kBF16, N, H, W, Cin, Cout, (int)stride, current_stream(x));
   return dw;
@@ -1064,6 +1071,9 @@ void bind_nn(pybind11::module& m) {
         "tile config the auto policy picks for an M x N GEMM with reduction K (TileCfg: 1 = 128x128, 2 = 128x64, 8 = 256x256)");
   m.def("gemm_tn_splits", [](int64_t Mo, int64_t No, int64_t K) { return gemm_tn_splits((int)Mo, (int)No, (int)K); },
         "split-K count of a weight-gradient gemm_tn launch");
+  m.def("set_halo_wgrad", &set_halo_wgrad, "halo 64-channel 3x3 weight gradient: -1 environment (default on), 0 off, 1 on");
+  m.def("halo_wgrad_eligible", [](int64_t Cin, int64_t Cout, int64_t W, int64_t stride) {
+        return halo_wgrad_eligible((int)Cin, (int)Cout, (int)W, (int)stride); });
   m.def("halo_conv_eligible", [](int64_t Cin, int64_t Cout, int64_t W, int64_t stride, bool fwd) {
         return halo_conv_eligible((int)Cin, (int)Cout, (int)W, (int)stride, fwd); },
         "whether a 3x3 conv pass runs on the halo-tiled kernel (conv_halo.hip) under the current DLA_HALO mode");
