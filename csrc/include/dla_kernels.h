@@ -249,8 +249,11 @@ int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto, int K = 0);
 // number of BN-statistics partial rows it writes (0 = shape not served: use launch_gemm_nt), and the
 // launcher (false = not served). set_gemm_stream: -1 environment (DLA_GEMM_STREAM, default on), 0 / 1.
 int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor);
+// addend (data gradients): C = bf16(bf16(A B^T) + (mask bit ? addend : 0)), addend [M][N] row stride ldd,
+// k-major B and no statistics only (false = not served).
 bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
-                        int M, int N, int K, float* stats, hipStream_t stream);
+                        int M, int N, int K, float* stats, hipStream_t stream, const void* addend = nullptr,
+                        int64_t ldd = 0, const uint8_t* addend_mask = nullptr);
 void set_gemm_stream(int mode);
 // Virtual conv output (gemm.hip gemm_vy_kernel): y = A * B^T (stride-1 1x1 conv, B = [N][K] weights)
 // recomputed by each consumer. mode 0 statistics partials, 1 out = relu(BN(y) + res) + ReLU bits,

@@ -35,9 +35,12 @@ using namespace mm;
 namespace {
 
 constexpr int kSBM = 128;  // rows per tile
-constexpr int kSP = 4;     // K-chunks in flight ahead of the MFMAs
-constexpr int kSS = kSP + 1;  // ring slots (one being read, kSP in flight)
 constexpr int kChunkElems = kSBM * kBK;  // one ring slot [128][64]
+// K-chunks in flight ahead of the MFMAs (ring slots = that + 1). With the fused addend epilogue each tile
+// also issues its addend / mask loads, and 4 chunks of lookahead would need a vmcnt above its 6-bit
+// limit at K = 64, so those variants keep max(2, KC) chunks in flight (the addend of the next tile is
+// itself a tile ahead).
+__host__ __device__ constexpr int stream_lookahead(int KC, bool add) { return add ? (KC > 2 ? KC : 2) : 4; }
 
 struct StreamArgs {
   const bf16_t* a;
@@ -50,6 +53,11 @@ struct StreamArgs {
   int mg;       // row groups (blocks per column panel)
   int per_xcd;  // row groups per XCD
   float* stats;  // [mg][N][2] or null
+  // fused addend (data-gradient epilogue): C = bf16(bf16(acc) + (mask bit ? D : 0)), D [M][N] with row
+  // stride ldd; mask: 1 bit per D element (null = all set), bit e of byte e >> 3 for element e = m * ldd + n
+  const bf16_t* d;
+  int64_t ldd;
+  const uint8_t* dmask;
 };
 
 // image row of panel-local weight row p (0..63 within a wave's 64 columns): the MFMA A-operand row
@@ -61,8 +69,26 @@ __device__ __forceinline__ int img_off(int row, int lc) { return row * kBK + ((l
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
-template <int BN, int KC, bool kBT, bool kStats>
+// Epilogue-operand loads in inline asm: hipcc's own vmcnt bookkeeping cannot see the LDS-DMA ring (asm),
+// so for a visible load it would wait vmcnt(0) at the first use and drain the ring; hidden loads are
+// waited for by the kernel's counted vm_wait, and `pin` orders every use after that wait.
+__device__ __forceinline__ i32x4_t asm_load_b128(__amdgpu_buffer_rsrc_t srd, uint32_t voff) {
+  i32x4_t r;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(r) : "v"(voff), "s"(srd) : "memory");
+  return r;
+}
+__device__ __forceinline__ uint32_t asm_load_u16(__amdgpu_buffer_rsrc_t srd, uint32_t voff) {
+  uint32_t r;
+  asm volatile("buffer_load_ushort %0, %1, %2, 0 offen" : "=v"(r) : "v"(voff), "s"(srd) : "memory");
+  return r;
+}
+template <class T>
+__device__ __forceinline__ void pin(T& v) { asm volatile("" : "+v"(v)); }
+
+template <int BN, int KC, bool kBT, bool kStats, bool kAdd = false>
 __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s) {
+  constexpr int kSP = stream_lookahead(KC, kAdd);
+  constexpr int kSS = kSP + 1;
   constexpr int WN = 64;                    // columns per wave
   constexpr int WGN = BN / WN;              // waves along N (2 or 1)
   constexpr int WGM = 4 / WGN;              // waves along M
@@ -72,6 +98,8 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s)
   static_assert(kSP % KC == 0, "the in-flight window must hold whole tiles");
   constexpr int D = kChunkElems / 8 / 256;  // LDS-DMA instructions per wave per chunk (4)
   constexpr int E = 2 * TJ;                 // buffer stores per wave per tile
+  constexpr int F = kAdd ? 3 * TJ : 0;      // addend (2 x 16 B) + mask (2 B) loads per wave per tile
+  static_assert((kSP - 1) * 4 + Q * (E + F) <= 63, "vmcnt is a 6-bit count");
   constexpr int kPanelElems = BN * kBK;     // one weight sub-image [BN][64]
 
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -154,6 +182,30 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s)
   // the weight panel's plain loads and LDS writes must be complete before the ring starts counting
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
+
+  // addend operands of one tile, one tile ahead of their use (registers): lane (lr, g) needs rows
+  // wm*WM + 16 j + lr, columns wn*64 + 16 g .. + 15 (the positions it stores)
+  const __amdgpu_buffer_rsrc_t rd = make_srd(kAdd ? (const void*)s.d : (const void*)s.c, kAdd ? (uint32_t)((int64_t)M * s.ldd * 2) : 0u);
+  const __amdgpu_buffer_rsrc_t rmk =
+      make_srd(kAdd && s.dmask ? (const void*)s.dmask : (const void*)s.c, kAdd && s.dmask ? (uint32_t)(((int64_t)M * s.ldd + 7) / 8) : 0u);
+  i32x4_t dv[kAdd ? TJ : 1][2];
+  uint32_t mb[kAdd ? TJ : 1];
+  auto load_operands = [&](int t) {
+    if constexpr (kAdd) {
+      const int64_t row0 = (int64_t)(grp + t * s.mg) * kSBM;
+      const int gc = col0 + wn * WN + 16 * g;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int64_t gm = row0 + wm * WM + 16 * j + lr;
+        const bool ok = gm < M;
+        const uint32_t off = ok ? (uint32_t)((gm * s.ldd + gc) * 2) : kOOB;
+        dv[j][0] = asm_load_b128(rd, off);
+        dv[j][1] = asm_load_b128(rd, ok ? off + 16 : kOOB);
+        mb[j] = asm_load_u16(rmk, ok ? (uint32_t)((gm * s.ldd + gc) >> 3) : kOOB);
+      }
+    }
+  };
+  load_operands(0);
 #pragma unroll
   for (int q = 0; q < kSP; ++q) issue(q);
 
@@ -167,9 +219,10 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s)
 
   for (int q = 0; q < nchunk; ++q) {
     // this wave's DMAs for chunk q are done once at most the younger ones are outstanding: the chunks
-    // q+1 .. q+kSP-1 (D each) and the stores of the Q tiles that ended after chunk q was issued
+    // q+1 .. q+kSP-1 (D each) and the stores (+ next-tile operand loads) of the Q tiles that ended
+    // after chunk q was issued
     if (q < kSP) vm_wait<(kSP - 1) * D>();
-    else vm_wait<(kSP - 1) * D + Q * E>();
+    else vm_wait<(kSP - 1) * D + Q * (E + F)>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: slot (q-1) % kSS is refilled below
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -201,6 +254,17 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s)
       // ---- tile epilogue: lane (lr, g) holds rows wm*WM + 16 j + lr, columns wn*64 + 16 g .. + 15 ----
       const int64_t row0 = (int64_t)(grp + (q / KC) * s.mg) * kSBM;
       const int gc = col0 + wn * WN + 16 * g;
+      // this tile's operands were loaded after the previous tile's stores: only this tile's KC chunk
+      // DMAs are younger
+      if constexpr (kAdd) {
+        vm_wait<KC * D>();
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          pin(dv[j][0]);
+          pin(dv[j][1]);
+          pin(mb[j]);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int64_t gm = row0 + wm * WM + 16 * j + lr;
@@ -212,6 +276,13 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             h[r] = f32_to_bf16(acc[i][j][r]);
+            if constexpr (kAdd) {  // column 4 i + r of the lane's 16: the unfused bf16 add, masked
+              const int e = 4 * i + r;
+              const uint32_t dw = (uint32_t)dv[j][e >> 3][(e >> 1) & 3];
+              const float d = bf16_to_f32((bf16_t)((e & 1) ? (dw >> 16) : (dw & 0xffffu)));
+              const uint32_t bits = s.dmask ? mb[j] : 0xffffu;
+              h[r] = f32_to_bf16(bf16_to_f32(h[r]) + (((bits >> e) & 1u) ? d : 0.f));
+            }
             if constexpr (kStats) {
               const float v = bf16_to_f32(h[r]);  // statistics of the stored values; OOB rows are 0
               st_s[i][r] += v;
@@ -227,6 +298,7 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s)
         __builtin_amdgcn_raw_buffer_store_b128(lo, rc, ok ? off : kOOB, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(hi, rc, ok ? off + 16 : kOOB, 0, 0);
       }
+      load_operands(q / KC + 1);  // past this block's last tile: OOB rows, zeros (uniform counts)
     }
   }
   vm_wait<0>();  // no LDS-DMA may land after the block's LDS is released
@@ -263,9 +335,9 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s)
   }
 }
 
-template <int BN, int KC>
+template <int BN, int KC, bool kAdd>
 constexpr size_t stream_lds_bytes() {
-  return (size_t)(KC * BN * kBK + kSS * kChunkElems) * sizeof(bf16_t);
+  return (size_t)(KC * BN * kBK + (stream_lookahead(KC, kAdd) + 1) * kChunkElems) * sizeof(bf16_t);
 }
 
 int g_stream_mode = -1;  // -1: environment (DLA_GEMM_STREAM, default on), 0 off, 1 on (every K <= 256)
@@ -316,14 +388,20 @@ int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_k
 }
 
 bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
-                        int M, int N, int K, float* stats, hipStream_t stream) {
+                        int M, int N, int K, float* stats, hipStream_t stream, const void* addend, int64_t ldd,
+                        const uint8_t* addend_mask) {
   const StreamPlan p = stream_plan(M, N, K, lda, ldc, b_kmajor);
   if (!p.mg) return false;
-  StreamArgs a{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, p.mg, p.per_xcd, stats};
+  if (addend && (stats || !b_kmajor || ldd % 8 != 0 || (int64_t)M * ldd * 2 >= (int64_t)kOOB)) return false;
+  StreamArgs a{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, p.mg, p.per_xcd, stats,
+               (const bf16_t*)addend, ldd, addend_mask};
 #define DLA_ST(BN_, KC_)                                                                                         \
   {                                                                                                              \
-    const size_t lds = stream_lds_bytes<BN_, KC_>();                                                             \
-    if (b_kmajor) {                                                                                              \
+    const size_t lds = stream_lds_bytes<BN_, KC_, false>();                                                      \
+    if (addend) {                                                                                                \
+      hipLaunchKernelGGL((gemm_stream_kernel<BN_, KC_, true, false, true>), dim3(p.grid), dim3(256),             \
+                         (stream_lds_bytes<BN_, KC_, true>()), stream, a);                                        \
+    } else if (b_kmajor) {                                                                                       \
       if (stats) hipLaunchKernelGGL((gemm_stream_kernel<BN_, KC_, true, true>), dim3(p.grid), dim3(256), lds, stream, a); \
       else hipLaunchKernelGGL((gemm_stream_kernel<BN_, KC_, true, false>), dim3(p.grid), dim3(256), lds, stream, a);      \
     } else {                                                                                                     \

@@ -630,14 +630,20 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
   }
   at::Tensor C = at::empty({M, N}, A.options());
   at::Tensor S;
-  // memory-bound short-K shapes without epilogue operands: the persistent streaming kernel
-  const bool bare = tile == kTileAuto && !add && !(addend_mask.has_value() && addend_mask->defined()) &&
-                    !(addend2.has_value() && addend2->defined());
-  const int srows = bare ? gemm_stream_rows(M, N, K, A.stride(0), C.stride(0), b_kmajor) : 0;
+  // memory-bound short-K shapes: the persistent streaming kernel (forward with statistics, data gradient
+  // with the fused identity-gradient addend + ReLU-bit mask; not the stride-2 second addend)
+  const bool add2 = addend2.has_value() && addend2->defined();
+  const bool mask = addend_mask.has_value() && addend_mask->defined();
+  const bool stream_ok = tile == kTileAuto && !add2 && (!mask || add) &&
+                         (!add || (b_kmajor && !stats && addend->stride(0) > 0 && addend->stride(0) % 8 == 0 &&
+                                   (int64_t)M * addend->stride(0) * 2 < (int64_t(1) << 31)));
+  const int srows = stream_ok ? gemm_stream_rows(M, N, K, A.stride(0), C.stride(0), b_kmajor) : 0;
   if (srows > 0) {
     if (stats) S = at::empty({srows, N, 2}, A.options().dtype(at::kFloat));
     TORCH_CHECK(launch_gemm_stream(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), b_kmajor, C.data_ptr(),
-                                   C.stride(0), M, N, K, stats ? S.data_ptr<float>() : nullptr, current_stream(A)),
+                                   C.stride(0), M, N, K, stats ? S.data_ptr<float>() : nullptr, current_stream(A),
+                                   add ? addend->data_ptr() : nullptr, add ? addend->stride(0) : 0,
+                                   addend_mask_ptr(addend_mask, M, N, add)),
                 "gemm_nt: streaming kernel refused a shape it planned");
     return {C, S};
   }

@@ -47,26 +47,29 @@ def main():
     rows = []
     for name, px, cin, cout in convs:
         M = b * px
-        for kind, K, N in (("fwd", cin, cout), ("dgrad", cout, cin)):
+        for kind, K, N in (("fwd", cin, cout), ("dgrad", cout, cin), ("dgrad_fork", cout, cin)):
             A = torch.randn(M, K, device=dev).to(torch.bfloat16)
             if kind == "fwd":
                 B, km, st = (torch.randn(N, K, device=dev) * 0.05).to(torch.bfloat16), False, True
             else:
                 B, km, st = (torch.randn(K, N, device=dev) * 0.05).to(torch.bfloat16), True, False
+            # the fork's data gradient: + the identity gradient, masked by the ReLU bits
+            D = torch.randn(M, N, device=dev).to(torch.bfloat16) if kind == "dgrad_fork" else None
+            mk = torch.randint(0, 256, ((M * N + 7) // 8,), device=dev, dtype=torch.uint8) if D is not None else None
             C.set_gemm_stream(1)
             served = C.gemm_stream_rows(M, N, K, K, N, km) > 0
             r = {"layer": name, "pass": kind, "M": M, "K": K, "N": N, "stream_served": served}
-            byts = (M * K + M * N + K * N) * 2
+            byts = (M * K + M * N + K * N) * 2 + ((M * N * 2 + M * N // 8) if D is not None else 0)
             for mode in ((1, 0) if served else (0,)):
                 C.set_gemm_stream(mode)
-                ms = timeit(lambda: C.gemm_nt(A, B, st, None, km))
+                ms = timeit(lambda: C.gemm_nt(A, B, st, D, km, 0, mk))
                 key = "stream" if mode else "tile"
                 r[f"{key}_ms"] = round(ms, 4)
                 r[f"{key}_TBps"] = round(byts / ms / 1e9, 3)
             C.set_gemm_stream(-1)
             rows.append(r)
             print(json.dumps(r), flush=True)
-            del A, B
+            del A, B, D, mk
     if a.out:
         with open(a.out, "w") as f:
             for r in rows:

@@ -10,6 +10,8 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_gemm_stream.py tests/test_g
 tail -1 $O/test.log
 timeout -k 10 120 python -u scripts/bench_halo_wgrad.py > $O/halo_wgrad.log 2>&1 || { tail -20 $O/halo_wgrad.log; exit 1; }
 cat $O/halo_wgrad.log
+timeout -k 10 400 python -u scripts/bench_gemm_stream.py --out $O/layers.jsonl > $O/layers.log 2>&1 || { tail -30 $O/layers.log; exit 1; }
+grep fork $O/layers.jsonl
 CLI="python -u -m distributed_learning_amd.main 1 0 1 1 127.0.0.1 lo"
 timeout -k 10 240 $CLI imagenet /none 1 --experiment experiment_single --batch_size 128 --random_input 1 --limit_batches 3 --precision fp32 --results_root $O/res_fp32_cold --job_id cold > $O/cli_g_fp32_cold.log 2>&1 || { tail -30 $O/cli_g_fp32_cold.log; exit 1; }
 timeout -k 10 240 $CLI imagenet /none 1 --experiment experiment_single --batch_size 128 --random_input 1 --limit_batches 30 --precision fp32 --results_root $O/res_fp32 --job_id gfp32 > $O/cli_g_fp32.log 2>&1 || { tail -30 $O/cli_g_fp32.log; exit 1; }
@@ -17,9 +19,10 @@ timeout -k 10 240 $CLI imagenet /none 1 --experiment experiment_single --batch_s
 python scripts/cli_vs_bench.py --cli $O/res_fp32_cold/experiment_single_1_cold --cli $O/res_fp32/experiment_single_1_gfp32 --cli $O/res_bf16/experiment_single_1_gbf16 > $O/googlenet_cli.json
 grep -h '"img_s"' $O/googlenet_cli.json
 for i in 1 2; do
-  for hw in 0 1; do
-    DLA_HALO_WGRAD=$hw timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > $O/bench_hw${hw}_$i.log 2>&1 || { tail -30 $O/bench_hw${hw}_$i.log; exit 1; }
-    echo "halo_wgrad=$hw $(grep -o '"ms_per_step": [0-9.]*' $O/bench_hw${hw}_$i.log)" | tee -a $O/ab.txt
+  for cfg in "DLA_HALO_WGRAD=1 DLA_GEMM_STREAM=1" "DLA_HALO_WGRAD=0 DLA_GEMM_STREAM=1" "DLA_HALO_WGRAD=1 DLA_GEMM_STREAM=0"; do
+    tag=$(echo $cfg | tr ' =' '__')
+    env $cfg timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > $O/bench_${tag}_$i.log 2>&1 || { tail -30 $O/bench_${tag}_$i.log; exit 1; }
+    echo "$cfg $(grep -o '"ms_per_step": [0-9.]*' $O/bench_${tag}_$i.log)" | tee -a $O/ab.txt
   done
 done
 cd /tmp && export TMPDIR=/tmp

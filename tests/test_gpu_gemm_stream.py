@@ -80,3 +80,28 @@ def test_small_m_stays_on_tile_kernel(cuda, C):
     C.set_gemm_stream(-1)
     assert C.gemm_stream_rows(802816, 512, 256, 256, 512, False) == 0
     assert C.gemm_stream_rows(802816, 512, 256, 256, 512, True) > 0
+
+
+@pytest.mark.parametrize("masked", [False, True])
+@pytest.mark.parametrize("shape", [(9000, 64, 256), (20000, 128, 512), (5001, 256, 128), (70000, 64, 64)])
+def test_stream_dgrad_addend_matches_tile_kernel(cuda, C, shape, masked):
+    """The fused identity-gradient epilogue: C = bf16(bf16(dY W) + (bit ? D : 0)); same bf16 products in
+    the same k order as the tile kernel, so the two agree bit for bit."""
+    M, K, N = shape
+    g = torch.Generator().manual_seed(M + 3 * K + N)
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    B = (torch.randn(K, N, generator=g) * K ** -0.5).to(cuda, torch.bfloat16)
+    D = torch.randn(M, N, generator=g).to(cuda, torch.bfloat16)
+    mask = torch.randint(0, 256, ((M * N + 7) // 8,), generator=g, dtype=torch.uint8).to(cuda) if masked else None
+    C.set_gemm_stream(1)
+    assert C.gemm_stream_rows(M, N, K, K, N, True) > 0
+    out, _ = C.gemm_nt(A, B, False, D, True, 0, mask)
+    C.set_gemm_stream(0)
+    ref, _ = C.gemm_nt(A, B, False, D, True, 0, mask)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    # and against the definition
+    bits = torch.ones(M * N, device=cuda) if mask is None else \
+        torch.stack([(mask >> j) & 1 for j in range(8)], 1).reshape(-1)[: M * N].float()
+    exp = ((A.float() @ B.float()).to(torch.bfloat16).float() + D.float() * bits.view(M, N)).to(torch.bfloat16)
+    assert float((out.float() - exp.float()).abs().max()) <= float(exp.float().abs().max()) * 2 ** -6
