@@ -248,7 +248,7 @@ int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto, int K = 0);
 // Persistent streaming 1x1 GEMM (gemm_stream.hip) for K in {64, 128, 256}, N % 64 == 0, long M: the
 // number of BN-statistics partial rows it writes (0 = shape not served: use launch_gemm_nt), and the
 // launcher (false = not served). set_gemm_stream: -1 environment (DLA_GEMM_STREAM, default on), 0 / 1.
-int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor);
+int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor, bool add = false);
 // addend (data gradients): C = bf16(bf16(A B^T) + (mask bit ? addend : 0)), addend [M][N] row stride ldd,
 // k-major B and no statistics only (false = not served).
 bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,

@@ -36,11 +36,12 @@ namespace {
 
 constexpr int kSBM = 128;  // rows per tile
 constexpr int kChunkElems = kSBM * kBK;  // one ring slot [128][64]
-// K-chunks in flight ahead of the MFMAs (ring slots = that + 1). With the fused addend epilogue each tile
-// also issues its addend / mask loads, and 4 chunks of lookahead would need a vmcnt above its 6-bit
-// limit at K = 64, so those variants keep max(2, KC) chunks in flight (the addend of the next tile is
-// itself a tile ahead).
-__host__ __device__ constexpr int stream_lookahead(int KC, bool add) { return add ? (KC > 2 ? KC : 2) : 4; }
+// K-chunks in flight ahead of the MFMAs (ring slots = that + 1). The fused-addend variants run two blocks
+// per CU (80 KB of LDS each) with 2 chunks in flight: their epilogue loads its addend just in time and
+// waits for it, and the co-resident block's ring keeps HBM busy meanwhile. (Loading the addend a tile
+// ahead into registers with hidden asm loads broke at K = 128: loop-carried registers get copied by the
+// register allocator before the data lands, which no waitcnt covers.)
+__host__ __device__ constexpr int stream_lookahead(int KC, bool add) { return add ? 2 : 4; }
 
 struct StreamArgs {
   const bf16_t* a;
@@ -69,24 +70,9 @@ __device__ __forceinline__ int img_off(int row, int lc) { return row * kBK + ((l
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
-// Epilogue-operand loads in inline asm: hipcc's own vmcnt bookkeeping cannot see the LDS-DMA ring (asm),
-// so for a visible load it would wait vmcnt(0) at the first use and drain the ring; hidden loads are
-// waited for by the kernel's counted vm_wait, and `pin` orders every use after that wait.
-__device__ __forceinline__ i32x4_t asm_load_b128(__amdgpu_buffer_rsrc_t srd, uint32_t voff) {
-  i32x4_t r;
-  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(r) : "v"(voff), "s"(srd) : "memory");
-  return r;
-}
-__device__ __forceinline__ uint32_t asm_load_u16(__amdgpu_buffer_rsrc_t srd, uint32_t voff) {
-  uint32_t r;
-  asm volatile("buffer_load_ushort %0, %1, %2, 0 offen" : "=v"(r) : "v"(voff), "s"(srd) : "memory");
-  return r;
-}
-template <class T>
-__device__ __forceinline__ void pin(T& v) { asm volatile("" : "+v"(v)); }
 
 template <int BN, int KC, bool kBT, bool kStats, bool kAdd = false>
-__global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s) {
+__global__ __launch_bounds__(256, kAdd ? 2 : 1) void gemm_stream_kernel(const StreamArgs s) {
   constexpr int kSP = stream_lookahead(KC, kAdd);
   constexpr int kSS = kSP + 1;
   constexpr int WN = 64;                    // columns per wave
@@ -183,8 +169,9 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s)
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // addend operands of one tile, one tile ahead of their use (registers): lane (lr, g) needs rows
-  // wm*WM + 16 j + lr, columns wn*64 + 16 g .. + 15 (the positions it stores)
+  // addend operands of a tile, loaded at its epilogue (all rows before the first use; the compiler's
+  // wait drains this block's ring, the other block on the CU streams meanwhile): lane (lr, g) needs
+  // rows wm*WM + 16 j + lr, columns wn*64 + 16 g .. + 15 (the positions it stores)
   const __amdgpu_buffer_rsrc_t rd = make_srd(kAdd ? (const void*)s.d : (const void*)s.c, kAdd ? (uint32_t)((int64_t)M * s.ldd * 2) : 0u);
   const __amdgpu_buffer_rsrc_t rmk =
       make_srd(kAdd && s.dmask ? (const void*)s.dmask : (const void*)s.c, kAdd && s.dmask ? (uint32_t)(((int64_t)M * s.ldd + 7) / 8) : 0u);
@@ -199,13 +186,12 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s)
         const int64_t gm = row0 + wm * WM + 16 * j + lr;
         const bool ok = gm < M;
         const uint32_t off = ok ? (uint32_t)((gm * s.ldd + gc) * 2) : kOOB;
-        dv[j][0] = asm_load_b128(rd, off);
-        dv[j][1] = asm_load_b128(rd, ok ? off + 16 : kOOB);
-        mb[j] = asm_load_u16(rmk, ok ? (uint32_t)((gm * s.ldd + gc) >> 3) : kOOB);
+        dv[j][0] = __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0);
+        dv[j][1] = __builtin_amdgcn_raw_buffer_load_b128(rd, ok ? off + 16 : kOOB, 0, 0);
+        mb[j] = __builtin_amdgcn_raw_buffer_load_b16(rmk, ok ? (uint32_t)((gm * s.ldd + gc) >> 3) : kOOB, 0, 0);
       }
     }
   };
-  load_operands(0);
 #pragma unroll
   for (int q = 0; q < kSP; ++q) issue(q);
 
@@ -254,17 +240,7 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s)
       // ---- tile epilogue: lane (lr, g) holds rows wm*WM + 16 j + lr, columns wn*64 + 16 g .. + 15 ----
       const int64_t row0 = (int64_t)(grp + (q / KC) * s.mg) * kSBM;
       const int gc = col0 + wn * WN + 16 * g;
-      // this tile's operands were loaded after the previous tile's stores: only this tile's KC chunk
-      // DMAs are younger
-      if constexpr (kAdd) {
-        vm_wait<KC * D>();
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) {
-          pin(dv[j][0]);
-          pin(dv[j][1]);
-          pin(mb[j]);
-        }
-      }
+      load_operands(q / KC);
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int64_t gm = row0 + wm * WM + 16 * j + lr;
@@ -298,7 +274,6 @@ __global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const StreamArgs s)
         __builtin_amdgcn_raw_buffer_store_b128(lo, rc, ok ? off : kOOB, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(hi, rc, ok ? off + 16 : kOOB, 0, 0);
       }
-      load_operands(q / KC + 1);  // past this block's last tile: OOB rows, zeros (uniform counts)
     }
   }
   vm_wait<0>();  // no LDS-DMA may land after the block's LDS is released
@@ -359,8 +334,9 @@ struct StreamPlan {
 // win or tie everywhere (fwd K 64 x N 256 -11 %, dgrad K 128 x N 256 -45 %); at K = 256 only the data
 // gradient (k-major weights) wins (-11 % at N 512); the forward K = 256 shapes lose 1-12 % (N >= 512 at
 // M <= 802k: the tile kernel's 2-4 co-resident blocks beat one 4-wave block per CU there).
-StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor) {
+StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor, bool add = false) {
   StreamPlan p;
+  if (add && K > 128) return p;  // 2 blocks per CU: the K = 256 weight panel does not fit 80 KB
   if (!stream_enabled() || M <= 0) return p;
   if (K != 64 && K != 128 && !(K == 256 && (b_kmajor || g_stream_mode == 1))) return p;
   if (N % 64 != 0 || lda % 8 != 0 || ldc % 8 != 0) return p;
@@ -370,7 +346,7 @@ StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b
   const int mt = (int)((M + kSBM - 1) / kSBM);
   // one block per CU: 256 blocks = 8 XCDs x per_xcd row groups x nbn panels; at least two tiles per
   // row group, or the ring has nothing to overlap (the tile kernel serves small M)
-  int per_xcd = std::max(1, 32 / nbn);
+  int per_xcd = std::max(1, (add ? 64 : 32) / nbn);
   while (per_xcd > 1 && mt < 2 * 8 * per_xcd) per_xcd >>= 1;
   if (mt < 2 * 8 * per_xcd) return StreamPlan{};
   p.per_xcd = per_xcd;
@@ -379,43 +355,52 @@ StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b
   return p;
 }
 
+template <int BN, int KC>
+void launch_stream_kc(const StreamArgs& a, int grid, bool kmajor, bool stats, bool add, hipStream_t stream) {
+  const dim3 g(grid), b(256);
+  if constexpr (KC <= 2) {
+    if (add) {  // data gradient with the fused addend (k-major weights, no statistics)
+      hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, true, false, true>), g, b, (stream_lds_bytes<BN, KC, true>()),
+                         stream, a);
+      return;
+    }
+  }
+  constexpr size_t lds = stream_lds_bytes<BN, KC, false>();
+  if (kmajor) {
+    if (stats) hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, true, true>), g, b, lds, stream, a);
+    else hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, true, false>), g, b, lds, stream, a);
+  } else {
+    if (stats) hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, false, true>), g, b, lds, stream, a);
+    else hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, false, false>), g, b, lds, stream, a);
+  }
+}
+
 }  // namespace
 
 void set_gemm_stream(int mode) { g_stream_mode = mode < 0 ? -1 : (mode ? 1 : 0); }
 
-int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor) {
-  return stream_plan(M, N, K, lda, ldc, b_kmajor).mg;
+int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor, bool add) {
+  return stream_plan(M, N, K, lda, ldc, b_kmajor, add).mg;
 }
 
 bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
                         int M, int N, int K, float* stats, hipStream_t stream, const void* addend, int64_t ldd,
                         const uint8_t* addend_mask) {
-  const StreamPlan p = stream_plan(M, N, K, lda, ldc, b_kmajor);
+  const StreamPlan p = stream_plan(M, N, K, lda, ldc, b_kmajor, addend != nullptr);
   if (!p.mg) return false;
   if (addend && (stats || !b_kmajor || ldd % 8 != 0 || (int64_t)M * ldd * 2 >= (int64_t)kOOB)) return false;
   StreamArgs a{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, p.mg, p.per_xcd, stats,
                (const bf16_t*)addend, ldd, addend_mask};
-#define DLA_ST(BN_, KC_)                                                                                         \
-  {                                                                                                              \
-    const size_t lds = stream_lds_bytes<BN_, KC_, false>();                                                      \
-    if (addend) {                                                                                                \
-      hipLaunchKernelGGL((gemm_stream_kernel<BN_, KC_, true, false, true>), dim3(p.grid), dim3(256),             \
-                         (stream_lds_bytes<BN_, KC_, true>()), stream, a);                                        \
-    } else if (b_kmajor) {                                                                                       \
-      if (stats) hipLaunchKernelGGL((gemm_stream_kernel<BN_, KC_, true, true>), dim3(p.grid), dim3(256), lds, stream, a); \
-      else hipLaunchKernelGGL((gemm_stream_kernel<BN_, KC_, true, false>), dim3(p.grid), dim3(256), lds, stream, a);      \
-    } else {                                                                                                     \
-      if (stats) hipLaunchKernelGGL((gemm_stream_kernel<BN_, KC_, false, true>), dim3(p.grid), dim3(256), lds, stream, a); \
-      else hipLaunchKernelGGL((gemm_stream_kernel<BN_, KC_, false, false>), dim3(p.grid), dim3(256), lds, stream, a);     \
-    }                                                                                                            \
-  }
   const int kc = K / kBK;
   if (p.bn == 128) {
-    if (kc == 1) DLA_ST(128, 1) else if (kc == 2) DLA_ST(128, 2) else DLA_ST(128, 4)
+    if (kc == 1) launch_stream_kc<128, 1>(a, p.grid, b_kmajor, stats != nullptr, addend != nullptr, stream);
+    else if (kc == 2) launch_stream_kc<128, 2>(a, p.grid, b_kmajor, stats != nullptr, addend != nullptr, stream);
+    else launch_stream_kc<128, 4>(a, p.grid, b_kmajor, stats != nullptr, addend != nullptr, stream);
   } else {
-    if (kc == 1) DLA_ST(64, 1) else if (kc == 2) DLA_ST(64, 2) else DLA_ST(64, 4)
+    if (kc == 1) launch_stream_kc<64, 1>(a, p.grid, b_kmajor, stats != nullptr, addend != nullptr, stream);
+    else if (kc == 2) launch_stream_kc<64, 2>(a, p.grid, b_kmajor, stats != nullptr, addend != nullptr, stream);
+    else launch_stream_kc<64, 4>(a, p.grid, b_kmajor, stats != nullptr, addend != nullptr, stream);
   }
-#undef DLA_ST
   return true;
 }
 

@@ -637,7 +637,7 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
   const bool stream_ok = tile == kTileAuto && !add2 && (!mask || add) &&
                          (!add || (b_kmajor && !stats && addend->stride(0) > 0 && addend->stride(0) % 8 == 0 &&
                                    (int64_t)M * addend->stride(0) * 2 < (int64_t(1) << 31)));
-  const int srows = stream_ok ? gemm_stream_rows(M, N, K, A.stride(0), C.stride(0), b_kmajor) : 0;
+  const int srows = stream_ok ? gemm_stream_rows(M, N, K, A.stride(0), C.stride(0), b_kmajor, add) : 0;
   if (srows > 0) {
     if (stats) S = at::empty({srows, N, 2}, A.options().dtype(at::kFloat));
     TORCH_CHECK(launch_gemm_stream(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), b_kmajor, C.data_ptr(),
@@ -1033,7 +1033,8 @@ void bind_nn(pybind11::module& m) {
   m.def("set_mfma_pipeline", &set_mfma_pipeline, "MFMA main loop: 0 register staging, 2/3 LDS-DMA stages, -1 per-shape auto");
   m.def("set_gemm_stream", &set_gemm_stream, "persistent streaming 1x1 GEMM: -1 environment (default on), 0 off, 1 on");
   m.def("gemm_stream_rows", &gemm_stream_rows, "BN-statistics partial rows of the streaming GEMM (0: shape not served)",
-        pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("lda"), pybind11::arg("ldc"), pybind11::arg("b_kmajor") = false);
+        pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("lda"), pybind11::arg("ldc"), pybind11::arg("b_kmajor") = false,
+        pybind11::arg("add") = false);
   m.def("mfma_pipeline", &mfma_pipeline);
   m.def("set_bn_red_blocks", &set_bn_red_blocks, "BN reduction-pass block target (0 = default / DLA_BN_RED_BLOCKS)");
   m.def("bn_red_blocks", &bn_red_blocks);

@@ -57,7 +57,7 @@ def main():
             D = torch.randn(M, N, device=dev).to(torch.bfloat16) if kind == "dgrad_fork" else None
             mk = torch.randint(0, 256, ((M * N + 7) // 8,), device=dev, dtype=torch.uint8) if D is not None else None
             C.set_gemm_stream(1)
-            served = C.gemm_stream_rows(M, N, K, K, N, km) > 0
+            served = C.gemm_stream_rows(M, N, K, K, N, km, D is not None) > 0
             r = {"layer": name, "pass": kind, "M": M, "K": K, "N": N, "stream_served": served}
             byts = (M * K + M * N + K * N) * 2 + ((M * N * 2 + M * N // 8) if D is not None else 0)
             for mode in ((1, 0) if served else (0,)):

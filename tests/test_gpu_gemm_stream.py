@@ -78,12 +78,13 @@ def test_small_m_stays_on_tile_kernel(cuda, C):
     assert C.gemm_stream_rows(100000, 256, 512, 512, 256) == 0  # K = 512: not served
     # default policy (environment mode): forward K = 256 stays on the tile kernel, dgrad K = 256 streams
     C.set_gemm_stream(-1)
+    assert C.gemm_stream_rows(802816, 512, 256, 256, 512, True, True) == 0  # addend form: K <= 128
     assert C.gemm_stream_rows(802816, 512, 256, 256, 512, False) == 0
     assert C.gemm_stream_rows(802816, 512, 256, 256, 512, True) > 0
 
 
 @pytest.mark.parametrize("masked", [False, True])
-@pytest.mark.parametrize("shape", [(9000, 64, 256), (20000, 128, 512), (5001, 256, 128), (70000, 64, 64)])
+@pytest.mark.parametrize("shape", [(9000, 64, 256), (20000, 128, 512), (5001, 128, 128), (70000, 64, 64)])
 def test_stream_dgrad_addend_matches_tile_kernel(cuda, C, shape, masked):
     """The fused identity-gradient epilogue: C = bf16(bf16(dY W) + (bit ? D : 0)); same bf16 products in
     the same k order as the tile kernel, so the two agree bit for bit."""
@@ -94,7 +95,7 @@ def test_stream_dgrad_addend_matches_tile_kernel(cuda, C, shape, masked):
     D = torch.randn(M, N, generator=g).to(cuda, torch.bfloat16)
     mask = torch.randint(0, 256, ((M * N + 7) // 8,), generator=g, dtype=torch.uint8).to(cuda) if masked else None
     C.set_gemm_stream(1)
-    assert C.gemm_stream_rows(M, N, K, K, N, True) > 0
+    assert C.gemm_stream_rows(M, N, K, K, N, True, True) > 0
     out, _ = C.gemm_nt(A, B, False, D, True, 0, mask)
     C.set_gemm_stream(0)
     ref, _ = C.gemm_nt(A, B, False, D, True, 0, mask)
