@@ -113,8 +113,9 @@ __device__ __forceinline__ int tr_off(int row, int col) {  // element offset of 
 __device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* lo_ptr, const bf16_t* hi_ptr) {
   const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(lo_ptr));
   const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(hi_ptr));
-  const short v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return *reinterpret_cast<const bf16x8_t*>(v);
+  // a vector concatenation, not an element-wise copy: the element form made hipcc emit a v_bfi_b32 on
+  // each freshly loaded register, i.e. an lgkmcnt wait right behind every read
+  return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 template <int W, int NT = kThreads>

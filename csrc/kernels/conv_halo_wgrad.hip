@@ -136,25 +136,44 @@ __global__ __launch_bounds__(256, 1) void conv3x3_halo_wgrad_kernel(const HaloWg
     const bf16_t* dyb = dys + (s % kWDySlots) * (kWDyBytes / 2);
     const int g = lane >> 4, qq = (lane & 15) >> 2, p = lane & 3;
     const int cn = wave * 16 + 4 * p;  // this wave's 16 input channels
+    // ring row of this lane's first transposing read at k-step 0, tap (0, 0): later k-steps and taps
+    // add compile-time row offsets (32 kk + shift), wrapped into the ring
+    const int rbase = (int)((q0 + 8 * g + qq + ring_off - (Wp + 1)) & (kWRing - 1));
+    // The 36 (k-step, tap) steps of the strip run as one unrolled sequence: step u's 4 MFMAs issue while
+    // the x fragment of step u + 2 (and, in the last 4 taps of a k-step, one dy fragment of the next
+    // k-step) is read. One wave per SIMD, so nothing else hides the LDS latency; and lgkmcnt is a 4-bit
+    // count, so a deeper run of reads would make hipcc's waits drain to 0.
+    bf16x8_t af[2][4], bx[3];
+    auto load_a = [&](int kk, int b, int i) {
+      const int kr = kk * 32 + 8 * g + qq;
+      af[b][i] = tr_frag(dyb + tr_off<kWC>(kr, 16 * i + 4 * p), dyb + tr_off<kWC>(kr + 4, 16 * i + 4 * p));
+    };
+    auto load_x = [&](int u) {
+      const int kk = u / 9, t = u % 9;
+      const int o = kk * 32 + (t / 3) * Wp + (t % 3);  // shift + (Wp + 1) >= 0
+      const int r0 = (rbase + o) & (kWRing - 1), r1 = (rbase + o + 4) & (kWRing - 1);
+      bx[u % 3] = tr_frag(ring + tr_off<kWC>(r0, cn), ring + tr_off<kWC>(r1, cn));
+    };
+    constexpr int kSteps = kWS / 32 * 9;
 #pragma unroll
-    for (int kk = 0; kk < kWS / 32; ++kk) {
-      bf16x8_t af[4];
-      const int kr = kk * 32 + 8 * g + qq;  // k-row (strip position) of this lane's transposing read
+    for (int i = 0; i < 4; ++i) load_a(0, 0, i);
+    load_x(0);
+    load_x(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[i] = tr_frag(dyb + tr_off<kWC>(kr, 16 * i + 4 * p), dyb + tr_off<kWC>(kr + 4, 16 * i + 4 * p));
+    for (int u = 0; u < kSteps; ++u) {
+      const int kk = u / 9, t = u % 9;
+      if (u + 2 < kSteps) load_x(u + 2);
+      const bool la = t >= 5 && kk + 1 < kWS / 32;
+      if (la) load_a(kk + 1, (kk + 1) & 1, t - 5);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int shift = (t / 3 - 1) * Wp + (t % 3 - 1);
-        const int64_t qa = q0 + kr + shift;
-        const int r0 = (int)((qa + ring_off) & (kWRing - 1));
-        const int r1 = (int)((qa + 4 + ring_off) & (kWRing - 1));
-        const bf16x8_t bx = tr_frag(ring + tr_off<kWC>(r0, cn), ring + tr_off<kWC>(r1, cn));
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[t][i] = mfma(af[i], bx, acc[t][i]);
-        __builtin_amdgcn_s_setprio(0);
+      for (int i = 0; i < 4; ++i) acc[t][i] = mfma(af[kk & 1][i], bx[u % 3], acc[t][i]);
+      __builtin_amdgcn_s_setprio(0);
+      if (u + 2 < kSteps) {
+        if (la) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        else __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     }
   }
   vm_wait<0>();  // no LDS-DMA may land after the block's LDS is released
