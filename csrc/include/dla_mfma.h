@@ -43,6 +43,10 @@ constexpr int kBK = 64;
 #ifndef DLA_EPI_PRELOAD
 #define DLA_EPI_PRELOAD 1
 #endif
+// transposing operand reads combined by vector concatenation (1) or element-wise (0; build-time A/B)
+#ifndef DLA_TR_CONCAT
+#define DLA_TR_CONCAT 1
+#endif
 
 // resident blocks per CU a kernel is compiled for: 2 for the 4-wave 128x128-or-smaller tiles
 // (64 KB of 2-stage LDS each), 1 for the 8-wave tiles and the 4-wave 256x128 / 128x256 tiles
@@ -113,9 +117,14 @@ __device__ __forceinline__ int tr_off(int row, int col) {  // element offset of 
 __device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* lo_ptr, const bf16_t* hi_ptr) {
   const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(lo_ptr));
   const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(hi_ptr));
+#if DLA_TR_CONCAT
   // a vector concatenation, not an element-wise copy: the element form made hipcc emit a v_bfi_b32 on
   // each freshly loaded register, i.e. an lgkmcnt wait right behind every read
   return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#else
+  const short v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return *reinterpret_cast<const bf16x8_t*>(v);
+#endif
 }
 
 template <int W, int NT = kThreads>
