@@ -98,6 +98,85 @@ class _SideWork:
         return self.out
 
 
+# Late-joined weight gradients (DLA_WGRAD_DEFER = "3x3" | "auto" | "all" | "0"): a conv's weight gradient is issued
+# on the side stream right AFTER its data gradient, so it runs alongside the memory-bound BatchNorm-backward
+# passes and the next data gradients of the compute stream instead of between them. The compute stream
+# joins the side stream at the end of the backward pass (autograd queue_callback; DLA_WGRAD_JOIN=end) or
+# already at the next conv backward (=conv). Collective executors make their stream wait for it (join_into) before
+# they read a gradient. Only for parameters without an existing .grad: AccumulateGrad would add into one
+# on the compute stream before the join. Default "3x3": ResNet-50 bs1024 on one MI355X, same box,
+# interleaved (profiles/r3/g18_g19_wgrad_defer.md): 72.58-72.77 ms/step vs 73.67-73.80 inline; deferring
+# the 1x1 weight gradients too ("all") gains nothing (they stream like the BN passes they would overlap).
+WGRAD_DEFER = os.environ.get("DLA_WGRAD_DEFER", "3x3")
+WGRAD_JOIN = os.environ.get("DLA_WGRAD_JOIN", "end")
+_DEFER_PENDING: dict = {}  # device -> the side stream holds work the compute stream has not joined yet
+_DEFER_CB: dict = {}  # device -> an end-of-backward join is queued
+
+
+def _side_stream(device: torch.device) -> torch.cuda.Stream:
+    side = _SIDE_STREAMS.get(device)
+    if side is None:
+        side = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
+    return side
+
+
+def side_pending(device: torch.device) -> bool:
+    return bool(_DEFER_PENDING.get(device))
+
+
+def join_into(stream, device: torch.device) -> None:
+    """Make ``stream`` wait for the deferred weight gradients issued so far on ``device``."""
+    if _DEFER_PENDING.get(device):
+        stream.wait_stream(_SIDE_STREAMS[device])
+
+
+def join_compute(device: torch.device) -> None:
+    if _DEFER_PENDING.get(device):
+        torch.cuda.current_stream(device).wait_stream(_SIDE_STREAMS[device])
+        _DEFER_PENDING[device] = False
+
+
+def _end_of_backward_join(device: torch.device) -> None:
+    _DEFER_CB[device] = False
+    join_compute(device)
+
+
+# "auto": the 3x3 weight gradients plus the 1x1 ones whose arithmetic intensity Cin*Cout/(Cin+Cout)
+# (FLOP per byte of the two streamed operands) is at least WGRAD_DEFER_MIN_AI: those are the MFMA-bound
+# ones that complement the memory-bound passes they overlap; the short-channel 1x1 ones stream operands
+# like the BatchNorm passes and only contend with them.
+WGRAD_DEFER_MIN_AI = float(os.environ.get("DLA_WGRAD_DEFER_MIN_AI", "200"))
+
+
+def _wants_defer(kind: str, ctx, cin: int = 0, cout: int = 0) -> bool:
+    if not ctx.needs_input_grad[1]:
+        return False
+    if WGRAD_DEFER == "auto":
+        return kind == "3x3" or cin * cout >= WGRAD_DEFER_MIN_AI * (cin + cout)
+    return WGRAD_DEFER in ("all", kind)
+
+
+def _wgrad_after_dgrad(fn, ctx, keep, device: torch.device):
+    """The weight gradient issued after the data gradient: on the side stream (after everything the
+    compute stream has issued so far) when the parameter has no .grad yet, else inline."""
+    weight = getattr(ctx, "weight_leaf", None)
+    if weight is None or weight.grad is not None:
+        return fn()
+    cur = torch.cuda.current_stream(device)
+    side = _side_stream(device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        out = fn()
+    for t in keep:  # inputs the compute stream may free before the side stream has read them
+        t.record_stream(side)
+    out.record_stream(cur)
+    _DEFER_PENDING[device] = True
+    if not _DEFER_CB.get(device):  # the end-of-backward join (also after the last conv in "conv" mode)
+        _DEFER_CB[device] = True
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _end_of_backward_join(device))
+    return out
+
+
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride: int, want_stats: bool):
@@ -117,6 +196,7 @@ class _Conv1x1(torch.autograd.Function):
         ctx.in_hw = None
         ctx.wdtype = weight.dtype
         ctx.wshape = weight.shape
+        ctx.weight_leaf = weight if weight.is_leaf else None
         if stats is not None:
             ctx.mark_non_differentiable(stats)
         return y, stats
@@ -133,10 +213,16 @@ class _Conv1x1(torch.autograd.Function):
         dy2 = _rows(dy)
         dx = dw = None
         wg = None
-        if ctx.needs_input_grad[1]:
-            odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
-            wg = _SideWork(lambda: _as_param_layout(C.gemm_tn(dy2, _rows(x), odt, 1.0).to(ctx.wdtype), ctx.wshape,
-                                                    ctx.wstride), dy2.shape[0], dy.device)
+        if WGRAD_JOIN == "conv":
+            join_compute(dy.device)
+        odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
+
+        def wgrad():
+            return _as_param_layout(C.gemm_tn(dy2, _rows(x), odt, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
+
+        defer = _wants_defer("1x1", ctx, x.shape[1], dy.shape[1])
+        if ctx.needs_input_grad[1] and not defer:
+            wg = _SideWork(wgrad, dy2.shape[0], dy.device)
         if ctx.needs_input_grad[0]:
             link = ctx.link
             if link is not None:
@@ -153,6 +239,8 @@ class _Conv1x1(torch.autograd.Function):
                 dx[:, :, ::ctx.stride, ::ctx.stride] = dxs
             else:
                 dx = dxs
+        if defer:
+            dw = _wgrad_after_dgrad(wgrad, ctx, (dy, x), dy.device)
         if wg is not None:
             dw = wg.result()
         return dx, dw, None, None
@@ -183,6 +271,7 @@ class _Conv1x1Fork(torch.autograd.Function):
         ctx.save_for_backward(x, w2)
         ctx.wdtype = weight.dtype
         ctx.wshape = weight.shape
+        ctx.weight_leaf = weight if weight.is_leaf else None
         ctx.wstride = weight.stride()
         ctx.link = bn_link_of(x)
         if stats is not None:
@@ -221,10 +310,16 @@ class _Conv1x1Fork(torch.autograd.Function):
         dy2 = _rows(dy)
         dx = dw = None
         wg = None
-        if ctx.needs_input_grad[1]:
-            odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
-            wg = _SideWork(lambda: _as_param_layout(C.gemm_tn(dy2, _rows(x), odt, 1.0).to(ctx.wdtype), ctx.wshape,
-                                                    ctx.wstride), dy2.shape[0], dy.device)
+        if WGRAD_JOIN == "conv":
+            join_compute(dy.device)
+        odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
+
+        def wgrad():
+            return _as_param_layout(C.gemm_tn(dy2, _rows(x), odt, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
+
+        defer = _wants_defer("1x1", ctx, x.shape[1], dy.shape[1])
+        if ctx.needs_input_grad[1] and not defer:
+            wg = _SideWork(wgrad, dy2.shape[0], dy.device)
         if ctx.needs_input_grad[0]:
             add = None if dident is None else _rows(dident)
             link = ctx.link
@@ -236,6 +331,8 @@ class _Conv1x1Fork(torch.autograd.Function):
             dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
             if link is not None:
                 link.publish(dx, part)
+        if defer:
+            dw = _wgrad_after_dgrad(wgrad, ctx, (dy, x), dy.device)
         if wg is not None:
             dw = wg.result()
         return dx, dw, None, None, None
@@ -321,6 +418,7 @@ class _Conv3x3(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.stride = stride
         ctx.wdtype = weight.dtype
+        ctx.weight_leaf = weight if weight.is_leaf else None
         if stats is not None:
             ctx.mark_non_differentiable(stats)
         return y, stats
@@ -334,6 +432,9 @@ class _Conv3x3(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
         dx = dw = None
         wg = None
+        if WGRAD_JOIN == "conv":
+            join_compute(dy.device)
+        defer = _wants_defer("3x3", ctx)
         if ctx.needs_input_grad[1]:
             odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
 
@@ -345,7 +446,8 @@ class _Conv3x3(torch.autograd.Function):
                                                             [0, 0], 1, [False, True, False])[1]
                 return g.to(ctx.wdtype)
 
-            wg = _SideWork(wgrad, dy.shape[0] * dy.shape[2] * dy.shape[3], dy.device)
+            if not defer:
+                wg = _SideWork(wgrad, dy.shape[0] * dy.shape[2] * dy.shape[3], dy.device)
         if ctx.needs_input_grad[0]:
             if ctx.stride == 1 and x.shape[1] <= CONV3_POLICY["dgrad_native_max_cin"]:
                 link = ctx.link
@@ -359,6 +461,8 @@ class _Conv3x3(torch.autograd.Function):
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, [ctx.stride] * 2, [1, 1], [1, 1], False,
                                                          [0, 0], 1, [True, False, False])[0]
+        if defer:
+            dw = _wgrad_after_dgrad(wgrad, ctx, (dy, x), dy.device)
         if wg is not None:
             dw = wg.result()
         return dx, dw, None, None

@@ -26,6 +26,19 @@ import torch
 from .bucketing import Bucket
 
 
+def _side_pending(device) -> bool:
+    from ..ops import conv
+
+    return device.type == "cuda" and conv.side_pending(device)
+
+
+def _late_wgrads_into(stream, device) -> None:
+    from ..ops import conv
+
+    if device.type == "cuda":
+        conv.join_into(stream, device)
+
+
 class BucketIO:
     """Host-side pack/unpack of a bucket for the non-native paths."""
 
@@ -148,6 +161,7 @@ class TorchStreamExecutor(Executor):
     def submit(self, b: Bucket) -> None:
         cur = torch.cuda.current_stream(b.flat.device)
         self.stream.wait_stream(cur)
+        _late_wgrads_into(self.stream, b.flat.device)
         with torch.cuda.stream(self.stream):
             BucketIO.pack(b)
             self.reduce_fn(b.flat)
@@ -168,10 +182,26 @@ class NativeStreamExecutor(Executor):
         # one rank: nothing to reduce, gradients stay where autograd put them (tests can force the
         # full gather/reduce/re-point path with passthrough=False)
         self.passthrough = (engine.impl.world() == 1) if passthrough is None else passthrough
+        self._join: dict = {}
 
     def submit(self, b: Bucket) -> None:
         if self.passthrough:
             return
+        dev = b.flat.device
+        if _side_pending(dev):
+            # weight gradients still running on the conv side stream (ops/conv.py WGRAD_DEFER): the engine
+            # waits on the current stream, so issue from a stream that has joined both
+            j = self._join.get(dev)
+            if j is None:
+                j = self._join[dev] = torch.cuda.Stream(device=dev)
+            j.wait_stream(torch.cuda.current_stream(dev))
+            _late_wgrads_into(j, dev)
+            with torch.cuda.stream(j):
+                self._submit(b)
+            return
+        self._submit(b)
+
+    def _submit(self, b: Bucket) -> None:
         stolen = getattr(b, "stolen", None)
         if stolen is not None:
             self.engine.bucket_allreduce_list(b.flat, self.algorithm, [g for g, _ in stolen], [o for _, o in stolen])

@@ -250,6 +250,10 @@ class GradSync:
         b, j = self._owner[id(p)]
         if self.grad_as_bucket_view and p.grad.data_ptr() != b.views[j].data_ptr():
             # the user replaced .grad (e.g. set_to_none between prepare and backward): fold it back
+            if p.grad.is_cuda:  # a late weight gradient (ops/conv.py WGRAD_DEFER) may still be running
+                from ..ops import conv as _conv
+
+                _conv.join_into(torch.cuda.current_stream(p.grad.device), p.grad.device)
             b.views[j].copy_(p.grad)
             p.grad = b.views[j]
         self._ready(p)
@@ -265,6 +269,10 @@ class GradSync:
         if self.grad_mode == "steal" and p.grad is not None:
             g = p.grad
             if g.dtype != b.flat.dtype or not same_layout(g, p):
+                if g.is_cuda:  # the conversion reads g on the compute stream: wait for a late weight gradient
+                    from ..ops import conv as _conv
+
+                    _conv.join_into(torch.cuda.current_stream(g.device), g.device)
                 g = g.to(b.flat.dtype) if same_layout(g, p) else torch.empty_like(p, dtype=b.flat.dtype).copy_(g)
             b.stolen.append((g, b.offsets[j]))
         b.ready += 1
