@@ -189,7 +189,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const void* base, uin
 
 // CH slots, LDS destination of slot i = lds + i * STRIDE (wave-uniform), one statement: M0 saved
 // once, written per slot (s_nop 0 before each DMA), restored; s_nop 4 lets a freshly computed
-// scalar soffset settle before the first buffer op reads it.
+// scalar soffset settle before the first buffer op reads it. The M0 advance (s_add_u32) writes SCC,
+// which the statement must declare: hipcc otherwise keeps a branch condition in SCC across it (seen
+// in gemm_stream_kernel<64, 2, ...>: the q % KC == KC - 1 test read the add's carry, so every tile
+// after the peeled prologue skipped its stores).
 template <int CH, int STRIDE>
 __device__ __forceinline__ void bglds(const uint32_t (&vo)[CH], __amdgpu_buffer_rsrc_t srd, uint32_t soff,
                                       uint32_t lds) {
@@ -205,7 +208,7 @@ __device__ __forceinline__ void bglds(const uint32_t (&vo)[CH], __amdgpu_buffer_
         "buffer_load_dwordx4 %1, %3, %5 offen lds\n\t"
         "s_add_u32 m0, m0, %6\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %5 offen lds\n\t"
         "s_mov_b32 m0, %0"
-        : "=&s"(keep) : "v"(vo[0]), "v"(vo[1]), "s"(srd), "s"(lds), "s"(soff), "i"(STRIDE) : "memory");
+        : "=&s"(keep) : "v"(vo[0]), "v"(vo[1]), "s"(srd), "s"(lds), "s"(soff), "i"(STRIDE) : "memory", "scc");
   } else if constexpr (CH == 4) {
     asm volatile(
         "s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\t"
@@ -216,7 +219,7 @@ __device__ __forceinline__ void bglds(const uint32_t (&vo)[CH], __amdgpu_buffer_
         "s_mov_b32 m0, %0"
         : "=&s"(keep)
         : "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "s"(srd), "s"(lds), "s"(soff), "i"(STRIDE)
-        : "memory");
+        : "memory", "scc");
   } else {
     static_assert(CH == 8, "1, 2, 4 or 8 slots");
     asm volatile(
@@ -233,7 +236,7 @@ __device__ __forceinline__ void bglds(const uint32_t (&vo)[CH], __amdgpu_buffer_
         : "=&s"(keep)
         : "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "v"(vo[5]), "v"(vo[6]), "v"(vo[7]),
           "s"(srd), "s"(lds), "s"(soff), "i"(STRIDE)
-        : "memory");
+        : "memory", "scc");
   }
 }
 

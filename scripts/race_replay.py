@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--bucket_mb", type=float, default=1.0)
     ap.add_argument("--nodp", action="store_true", help="plain model, no DP wrapper / comm stream (diagnosis)")
     a = ap.parse_args()
+    a.nodp = a.nodp or os.environ.get("RACE_NODP") == "1"
     os.environ.setdefault("RANK", "0")
     os.environ.setdefault("WORLD_SIZE", "1")
     os.environ.setdefault("LOCAL_RANK", "0")
@@ -67,6 +68,13 @@ def main():
         opt.zero_grad(set_to_none=True)
         loss = cross_entropy(w(x), y)
         loss.backward()
+        if os.environ.get("RACE_JOIN") == "1":  # diagnosis: explicit join of the conv side stream
+            from distributed_learning_amd.ops import conv as _conv
+
+            for st in _conv._SIDE_STREAMS.values():
+                torch.cuda.current_stream().wait_stream(st)
+        if os.environ.get("RACE_SYNC") == "1":  # diagnosis: drain the device after backward
+            torch.cuda.synchronize()
         w.sync_gradients()
         opt.step()
         losses.append(loss.detach())

@@ -106,3 +106,26 @@ def test_stream_dgrad_addend_matches_tile_kernel(cuda, C, shape, masked):
         torch.stack([(mask >> j) & 1 for j in range(8)], 1).reshape(-1)[: M * N].float()
     exp = ((A.float() @ B.float()).to(torch.bfloat16).float() + D.float() * bits.view(M, N)).to(torch.bfloat16)
     assert float((out.float() - exp.float()).abs().max()) <= float(exp.float().abs().max()) * 2 ** -6
+
+
+@pytest.mark.parametrize("kmajor", [False, True])
+@pytest.mark.parametrize("shape", SHAPES + [(12544, 128, 64)])
+def test_stream_without_statistics_writes_every_row(cuda, C, shape, kmajor):
+    """The statistics-free instantiations (data gradients, plain forwards). The output block is poisoned
+    with NaN first, so a tile whose stores were skipped cannot pass on stale correct values left in a
+    recycled allocation (the K = 128 instantiation skipped every tile after the peeled prologue while an
+    inline-asm M0 advance clobbered the SCC branch condition; dla_mfma.h bglds)."""
+    M, K, N = shape
+    g = torch.Generator().manual_seed(M * 3 + K + N)
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(cuda, torch.bfloat16)
+    B = W.t().contiguous() if kmajor else W
+    C.set_gemm_stream(1)
+    assert C.gemm_stream_rows(M, N, K, K, N, kmajor) > 0
+    poison = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+    del poison  # the caching allocator hands this block to the next [M, N] bf16 output
+    out, st = C.gemm_nt(A, B, False, None, kmajor)
+    torch.cuda.synchronize()
+    assert st is None or st.numel() == 0
+    assert torch.isfinite(out).all(), f"{int((~torch.isfinite(out)).any(1).sum())} rows never written"
+    assert _rel(out, A.float() @ W.float().t()) < 5e-3
