@@ -145,7 +145,9 @@ DUAL_RESIDUAL = True
 # to the shortcut conv, which then runs concurrently with the conv1 -> conv2 -> conv3 chain of the compute
 # stream; the final dual apply joins it. Autograd replays each backward node on the stream its forward ran
 # on, so the shortcut conv's data and weight gradients also run on the branch stream, synchronised with
-# their producer and consumer by autograd.
+# their producer and consumer by autograd. Off by default: ResNet-50 bs1024, same box, interleaved
+# (profiles/r3/g21_branch_stream_ab.txt) 73.42-73.62 ms/step with it vs 72.46-72.53 without; the shortcut
+# GEMMs stream their operands and contend with the compute stream's passes rather than filling gaps.
 BRANCH_STREAM = os.environ.get("DLA_BRANCH_STREAM", "0") == "1"
 _BRANCH_STREAMS: dict = {}
 

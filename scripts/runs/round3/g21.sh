@@ -3,7 +3,7 @@
 # interleaved end-to-end A/B, 3 rounds.
 set -o pipefail
 O=gpurun_out/g21; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_branch_stream.py tests/test_gpu_wgrad_defer.py -x -q --timeout 200 --timeout-method thread > $O/test.log 2>&1 || { tail -40 $O/test.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_branch_stream.py tests/test_gpu_wgrad_defer.py tests/test_gpu_uninit.py tests/test_gpu_gemm_stream.py -x -q --timeout 200 --timeout-method thread > $O/test.log 2>&1 || { tail -40 $O/test.log; exit 1; }
 tail -1 $O/test.log
 for i in 1 2 3; do
   for v in 0 1; do
