@@ -545,7 +545,10 @@ bool splitk_xcd_remap() {
 
 // Workgroups a split-K weight-gradient launch aims for (tiles x splits): 512 = 2 per CU;
 // DLA_SPLITK_BLOCKS overrides it for A/B runs
+static int g_splitk_blocks = 0;  // set_splitk_blocks(): > 0 overrides the environment / default
+void set_splitk_blocks(int blocks) { g_splitk_blocks = blocks > 0 ? blocks : 0; }
 int splitk_target_blocks() {
+  if (g_splitk_blocks > 0) return g_splitk_blocks;
   static const int v = [] {
     const char* e = std::getenv("DLA_SPLITK_BLOCKS");
     const int b = e ? std::atoi(e) : 0;
