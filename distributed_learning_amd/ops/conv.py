@@ -148,11 +148,6 @@ def _end_of_backward_join(device: torch.device) -> None:
 WGRAD_DEFER_MIN_AI = float(os.environ.get("DLA_WGRAD_DEFER_MIN_AI", "200"))
 
 
-# Split-K block target of the late weight gradients (0 = the global default, 512): more, shorter blocks
-# retire sooner, so a compute-stream kernel launched while they cover the chip waits less for CUs.
-WGRAD_DEFER_SPLITK_BLOCKS = int(os.environ.get("DLA_WGRAD_DEFER_SPLITK_BLOCKS", "0"))
-
-
 def _wants_defer(kind: str, ctx, cin: int = 0, cout: int = 0) -> bool:
     if not ctx.needs_input_grad[1]:
         return False
@@ -170,15 +165,8 @@ def _wgrad_after_dgrad(fn, ctx, keep, device: torch.device):
     cur = torch.cuda.current_stream(device)
     side = _side_stream(device)
     side.wait_stream(cur)
-    C = _ext.require()
-    if WGRAD_DEFER_SPLITK_BLOCKS:
-        C.set_splitk_blocks(WGRAD_DEFER_SPLITK_BLOCKS)
-    try:
-        with torch.cuda.stream(side):
-            out = fn()
-    finally:
-        if WGRAD_DEFER_SPLITK_BLOCKS:
-            C.set_splitk_blocks(0)
+    with torch.cuda.stream(side):
+        out = fn()
     for t in keep:  # inputs the compute stream may free before the side stream has read them
         t.record_stream(side)
     out.record_stream(cur)
