@@ -101,23 +101,26 @@ __global__ __launch_bounds__(kBNThreads) void bn_stats_kernel(const T* __restric
 // latency-bound (~1 us per dependent round trip): WPC = 1 for the <= 1024 partial rows of the
 // reduction passes, WPC = 4 for the per-128-row-tile partials of the GEMM epilogues.
 // Fixed order -> bitwise reproducible.
-template <int WPC>
+// NF loads in flight per lane: 8, or 4 for the lean finalize kernels (kFinalizeVgprs), which must fit
+// beside a 256x256 weight-gradient block (2 x 240 of a SIMD's 512 VGPRs): the late weight gradients
+// (ops/conv.py WGRAD_DEFER) then no longer hold a finalize back until their blocks retire.
+template <int WPC, int NF = 8>
 __device__ __forceinline__ bool reduce_partials(int bx, const float* __restrict__ part, int nrb, int C, float& S,
                                                 float& Q, int& c, int ldp = 0) {
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   c = bx * (4 / WPC) + wave / WPC;
-  float s[8], q[8];
+  float s[NF], q[NF];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) s[u] = q[u] = 0.f;
+  for (int u = 0; u < NF; ++u) s[u] = q[u] = 0.f;
   if (c < C) {
     const float2* p2 = reinterpret_cast<const float2*>(part);
     const int64_t ld = ldp ? ldp : C;
     constexpr int kStride = 64 * WPC;
     int b = lane + 64 * (wave % WPC);
-    for (; b + 7 * kStride < nrb; b += 8 * kStride) {
+    for (; b + (NF - 1) * kStride < nrb; b += NF * kStride) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < NF; ++u) {
         const float2 v = p2[(int64_t)(b + kStride * u) * ld + c];
         s[u] += v.x;
         q[u] += v.y;
@@ -129,8 +132,15 @@ __device__ __forceinline__ bool reduce_partials(int bx, const float* __restrict_
       q[0] += v.y;
     }
   }
-  float ss = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-  float qq = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+  float ss, qq;
+  if constexpr (NF == 8) {
+    ss = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    qq = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+  } else {
+    static_assert(NF == 4, "4 or 8 loads in flight");
+    ss = (s[0] + s[1]) + (s[2] + s[3]);
+    qq = (q[0] + q[1]) + (q[2] + q[3]);
+  }
   ss = wave_sum(ss);
   qq = wave_sum(qq);
   if constexpr (WPC > 1) {
@@ -542,14 +552,14 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_reduce_kernel(DY dy, const 
   bn_bwd_reduce_body<T, kMask, DY>(blockIdx.x, dy, y, mask, x, ws, M, C, nrb, tpr, part);
 }
 
-template <int WPC>
+template <int WPC, int NF = 8>
 __device__ __forceinline__ void bn_bwd_finalize_body(int bx, const float* __restrict__ part, int nrb, int64_t M,
                                                               int C, const float* __restrict__ gamma,
                                                               float* __restrict__ ws, float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta, int ldp = 0) {
   float S, Q;
   int c;
-  if (!reduce_partials<WPC>(bx, part, nrb, C, S, Q, c, ldp)) return;
+  if (!reduce_partials<WPC, NF>(bx, part, nrb, C, S, Q, c, ldp)) return;
   const float invstd = ws[C + c];
   const float g = gamma ? gamma[c] : 1.f;
   if (dgamma) dgamma[c] = Q * invstd;
@@ -562,11 +572,23 @@ __device__ __forceinline__ void bn_bwd_finalize_body(int bx, const float* __rest
   ws[6 * C + c] = invstd * invstd * Q * inv_m;
 }
 
+// build-time A/B: -D DLA_LEAN_FINALIZE=0 restores the 8-in-flight, uncapped finalize
+#ifndef DLA_LEAN_FINALIZE
+#define DLA_LEAN_FINALIZE 1
+#endif
+#if DLA_LEAN_FINALIZE
+constexpr int kFinalizeVgprs = 32, kFinalizeNF = 4;
+#define DLA_FINALIZE_ATTR __attribute__((amdgpu_num_vgpr(kFinalizeVgprs)))
+#else
+constexpr int kFinalizeNF = 8;
+#define DLA_FINALIZE_ATTR
+#endif
+
 template <int WPC>
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int64_t M, int C,
-                                                              const float* __restrict__ gamma, float* __restrict__ ws,
-                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  bn_bwd_finalize_body<WPC>(blockIdx.x, part, nrb, M, C, gamma, ws, dgamma, dbeta);
+__global__ __launch_bounds__(256) DLA_FINALIZE_ATTR void bn_bwd_finalize_kernel(
+    const float* __restrict__ part, int nrb, int64_t M, int C, const float* __restrict__ gamma, float* __restrict__ ws,
+    float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  bn_bwd_finalize_body<WPC, kFinalizeNF>(blockIdx.x, part, nrb, M, C, gamma, ws, dgamma, dbeta);
 }
 
 template <typename T, int kMask, bool kDres, class DY = DirectDy<T>>

@@ -561,12 +561,14 @@ int splitk_target_blocks() {
 // multiples of 256 (the stage-3/4 1x1 convs: compute-bound, like the fwd/dgrad shapes pick_tile
 // sends to kTile256x256); DLA_TILE256=0 turns them off with the other 256x256 tiles
 // (DLA_TN256=0 turns off only these and the 3x3 ones, for A/B)
+static int g_tn256 = -1;  // set_tn256(): -1 environment (DLA_TN256, default on), 0 off, 1 on
+void set_tn256(int mode) { g_tn256 = mode < 0 ? -1 : (mode ? 1 : 0); }
 bool tn256_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("DLA_TN256");
     return !(e && e[0] == '0');
   }();
-  return on && tile256_enabled();
+  return (g_tn256 < 0 ? on : g_tn256 == 1) && tile256_enabled();
 }
 static bool tn_wide(int Mo, int No) { return tn256_enabled() && Mo % 256 == 0 && No % 256 == 0; }
 
