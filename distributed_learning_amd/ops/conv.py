@@ -148,12 +148,6 @@ def _end_of_backward_join(device: torch.device) -> None:
 WGRAD_DEFER_MIN_AI = float(os.environ.get("DLA_WGRAD_DEFER_MIN_AI", "200"))
 
 
-# Tile config of the late 3x3 weight gradients (DLA_WGRAD_DEFER_TILE): "wide" keeps the 256x256 8-wave
-# tiles (2 x 240 VGPRs per SIMD: nothing of the compute stream fits beside a block), "narrow" uses the
-# 128x128 4-wave tiles (2 blocks x 160 VGPRs: the BN passes' blocks fit beside them).
-WGRAD_DEFER_TILE = os.environ.get("DLA_WGRAD_DEFER_TILE", "wide")
-
-
 def _wants_defer(kind: str, ctx, cin: int = 0, cout: int = 0) -> bool:
     if not ctx.needs_input_grad[1]:
         return False
@@ -171,15 +165,8 @@ def _wgrad_after_dgrad(fn, ctx, keep, device: torch.device):
     cur = torch.cuda.current_stream(device)
     side = _side_stream(device)
     side.wait_stream(cur)
-    narrow = WGRAD_DEFER_TILE == "narrow"
-    if narrow:
-        _ext.require().set_tn256(0)
-    try:
-        with torch.cuda.stream(side):
-            out = fn()
-    finally:
-        if narrow:
-            _ext.require().set_tn256(-1)
+    with torch.cuda.stream(side):
+        out = fn()
     for t in keep:  # inputs the compute stream may free before the side stream has read them
         t.record_stream(side)
     out.record_stream(cur)
