@@ -289,6 +289,7 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
 // out[Mo,No] (= scale * A^T B [+ out]) with A [K, lda>=Mo], B [K, ldb>=No]; partial: splits*Mo*No f32.
 int gemm_tn_splits(int Mo, int No, int K);
 bool splitk_xcd_remap();
+void set_stem_halo(int mode);  // stem forward: -1 DLA_STEM_HALO / default implicit GEMM, 0 implicit GEMM, 1 halo
 void set_tn256(int mode);  // 256x256 weight-gradient tiles: -1 DLA_TN256 / default on, 0 off, 1 on
 void set_splitk_blocks(int blocks);  // 0: DLA_SPLITK_BLOCKS / default (512)
 int splitk_target_blocks();  // split-K grids: tiles of one split co-scheduled on one XCD (DLA_SPLITK_XCD=0: off)

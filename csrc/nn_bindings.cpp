@@ -1036,6 +1036,7 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("lda"), pybind11::arg("ldc"), pybind11::arg("b_kmajor") = false,
         pybind11::arg("add") = false);
   m.def("mfma_pipeline", &mfma_pipeline);
+  m.def("set_stem_halo", &set_stem_halo, "stem forward: -1 environment (DLA_STEM_HALO, default off), 0 implicit GEMM, 1 halo-tiled");
   m.def("set_tn256", &set_tn256, "256x256 weight-gradient tiles: -1 environment (DLA_TN256, default on), 0 off, 1 on");
   m.def("set_splitk_blocks", &set_splitk_blocks, "split-K weight-gradient block target (0 = default / DLA_SPLITK_BLOCKS)");
   m.def("splitk_target_blocks", &splitk_target_blocks);
