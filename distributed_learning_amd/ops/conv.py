@@ -160,7 +160,9 @@ def _wgrad_after_dgrad(fn, ctx, keep, device: torch.device):
     """The weight gradient issued after the data gradient: on the side stream (after everything the
     compute stream has issued so far) when the parameter has no .grad yet, else inline."""
     weight = getattr(ctx, "weight_leaf", None)
-    if weight is None or weight.grad is not None:
+    # inside HIP-graph capture (GoogLeNet bs128 --graph on: 19.8k vs 20.7k img/s with the fork / join
+    # nodes, profiles/r3/g38_other_models_ab.txt) the weight gradient stays on the captured stream
+    if weight is None or weight.grad is not None or torch.cuda.is_current_stream_capturing():
         return fn()
     cur = torch.cuda.current_stream(device)
     side = _side_stream(device)
