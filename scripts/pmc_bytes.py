@@ -47,10 +47,10 @@ def main():
     mean_ns = {}
     if a.stats:
         for r in csv.DictReader(open(a.stats)):
-            mean_ns[r["Name"].split("(")[0][:90]] = float(r["AverageNs"])
+            mean_ns[r["Name"].replace("(anonymous namespace)::", "").split("(")[0][:90]] = float(r["AverageNs"])
     agg = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0])
     for i in tail:
-        short = f[i]["name"].split("(")[0][:90]
+        short = f[i]["name"].replace("(anonymous namespace)::", "").split("(")[0][:90]
         key = (short, f[i]["grid"]) if a.by_grid else (short, "")
         e = agg[key]
         e[0] += 1

@@ -25,7 +25,7 @@ SIMDS = 256 * 4
 
 
 def short(name: str) -> str:
-    n = re.sub(r"\(.*", "", name)
+    n = re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", ""))
     n = n.replace("void ", "").replace("dla::", "")
     return n[:80]
 
