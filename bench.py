@@ -60,11 +60,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    # 1024 per GPU, sized for the 288 GB of HBM3E (60 GB peak): the stage-3/4 layers (M = batch x 14^2 or
-    # 7^2 rows) fill the 256 CUs better and per-step fixed costs are amortised, +4.3 % images/s over 512
-    # on one MI355X (profiles/r5f/, same box: 512 -> 12,794-12,819, 768 -> 12,994-13,022, 1024 -> 13,347-
-    # 13,367). 1024 is also the largest batch inside the 24-bit pixel-index limits of the stem kernels.
-    ap.add_argument("--batch", type=int, default=1024, help="per-GPU batch size")
+    # 1280 per GPU, sized for the 288 GB of HBM3E (74.5 GB peak): the stage-3/4 layers (M = batch x 14^2 or
+    # 7^2 rows) fill the 256 CUs better and per-step fixed costs are amortised: +4.3 % images/s from 512 to
+    # 1024 (profiles/r5f/: 512 -> 12,794-12,819, 768 -> 12,994-13,022, 1024 -> 13,347-13,367) and +2.5 % from
+    # 1024 to 1280 with the round-3 kernels (profiles/r3/g45_batch_ab.txt: 14,088-14,102 -> 14,444-14,471,
+    # same box). The 24-bit pixel-index limit of the stem / fused stem-pool kernels (N * 112^2 < 2^24, checked
+    # on the host) caps the batch at 1337; the largest stage-1 activation (2.06 GB) stays under the 2 GiB
+    # buffer-descriptor range.
+    ap.add_argument("--batch", type=int, default=1280, help="per-GPU batch size")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--algorithm", default="builtin", help="native engine all-reduce: builtin|ring|ring_pipe|direct|rsag|central|hier_ring|hier_coll")
     # 8 MiB of bf16 gradients = 16 MiB of fp32 on the wire (fp32 accumulation at N > 1): the cap the
