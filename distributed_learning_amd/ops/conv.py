@@ -106,7 +106,10 @@ class _SideWork:
 # they read a gradient. Only for parameters without an existing .grad: AccumulateGrad would add into one
 # on the compute stream before the join. Default "3x3": ResNet-50 bs1024 on one MI355X, same box,
 # interleaved (profiles/r3/g18_g19_wgrad_defer.md): 72.58-72.77 ms/step vs 73.67-73.80 inline; deferring
-# the 1x1 weight gradients too ("all") gains nothing (they stream like the BN passes they would overlap).
+# the 1x1 weight gradients too ("all") gains nothing (they stream like the BN passes they would overlap),
+# and at bs1280 it stalls: p50 89.7 ms but single steps of 1.4-6.9 s (profiles/r3/g47_defer_batch_ab.md),
+# from the caching allocator's cross-stream frees (record_stream) forcing synchronising retries near the
+# memory ceiling. Keep "all" for tests and small batches.
 WGRAD_DEFER = os.environ.get("DLA_WGRAD_DEFER", "3x3")
 WGRAD_JOIN = os.environ.get("DLA_WGRAD_JOIN", "end")
 _DEFER_PENDING: dict = {}  # device -> the side stream holds work the compute stream has not joined yet
