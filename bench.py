@@ -69,12 +69,25 @@ def parse():
     # buffer-descriptor range.
     ap.add_argument("--batch", type=int, default=1280, help="per-GPU batch size")
     ap.add_argument("--model", default="resnet50")
-    ap.add_argument("--algorithm", default="builtin", help="native engine all-reduce: builtin|ring|ring_pipe|direct|rsag|central|hier_ring|hier_coll")
-    # 8 MiB of bf16 gradients = 16 MiB of fp32 on the wire (fp32 accumulation at N > 1): the cap the
-    # cost model (parallel/cost_model.py) derives for ResNet-50 on an 8-GPU node with the builtin
-    # collective (the reference's 25 MiB costs ~30 % more exposed + contended comm there); "auto"
-    # re-derives it for --model / --gpus
-    ap.add_argument("--bucket_mb", default="8")
+    ap.add_argument("--algorithm", default="auto",
+                    help="native engine all-reduce: auto (N > 1 or --force_comm: every candidate verified and timed "
+                         "before warmup, each bucket gets the fastest, parallel/autotune.py; else builtin) or "
+                         "[ipc_]builtin|ring|ring_pipe|direct|rsag|central|hier_ring|hier_coll[:channels]")
+    # auto: N > 1 derives the cap from the fitted model of the measured best algorithm (autotune);
+    # N = 1 uses 8 MiB of bf16 gradients (= 16 MiB of fp32 on the wire): the cost model's cap for
+    # ResNet-50 on an 8-GPU node with an assumed builtin bandwidth (parallel/cost_model.py)
+    ap.add_argument("--bucket_mb", default="auto")
+    ap.add_argument("--transport", default=None, choices=["rccl", "ipc"],
+                    help="gradient transport (default rccl; ipc with --same_device): ipc = peer-mapped windows "
+                         "with flag barriers (csrc/comm/ipc.h)")
+    ap.add_argument("--same_device", type=int, default=0,
+                    help="1 = every rank on cuda:0 (N processes sharing one GPU; gloo process group + IPC "
+                         "transport, since RCCL refuses that): the real multi-process data path on a one-GPU box")
+    ap.add_argument("--check_dir", default=None,
+                    help="each rank saves its final parameters / gradients / master weights to DIR/rank<r>.pt")
+    ap.add_argument("--fail_rank", type=int, default=-1,
+                    help="fault injection: this rank exits (status 17) after the forward of step --fail_step")
+    ap.add_argument("--fail_step", type=int, default=1)
     ap.add_argument("--kernels", default=os.environ.get("DLA_KERNELS", "native"), choices=["torch", "native"])
     ap.add_argument("--precision", default=os.environ.get("DLA_PRECISION", "bf16"), choices=["autocast", "bf16"],
                     help="autocast: fp32 params + bf16 autocast; bf16: bf16 weights + fp32 master weights in the "
@@ -113,7 +126,7 @@ def launch_ranks(a) -> int:
     Runs before anything initialises the GPU in this process (``torch.cuda.device_count()`` does not, on
     this image). The child inherits stdout, so rank 0's JSON line is relayed as is; the return value is the
     launcher's exit status (non-zero if any rank failed), 124 on timeout."""
-    if not a.dry_run:
+    if not a.dry_run and not a.same_device:
         ndev = torch.cuda.device_count()
         if a.gpus > ndev:
             print(f"error: --gpus {a.gpus} requested but this node has {ndev} GPU(s); refusing to measure fewer",
@@ -124,6 +137,8 @@ def launch_ranks(a) -> int:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "4")
+    if a.same_device:
+        env["DLA_SAME_DEVICE"] = "1"
     p = subprocess.Popen(cmd, env=env, start_new_session=True)
     try:
         rc = p.wait(timeout=a.launch_timeout)
@@ -169,10 +184,11 @@ def main():
     if a.gpus != int(os.environ["WORLD_SIZE"]):
         print(f"error: --gpus {a.gpus} but WORLD_SIZE {os.environ['WORLD_SIZE']}", file=sys.stderr, flush=True)
         sys.exit(2)
-    if a.gpus > torch.cuda.device_count():
+    same = bool(a.same_device) or os.environ.get("DLA_SAME_DEVICE") == "1"
+    if a.gpus > torch.cuda.device_count() and not same:
         print(f"error: --gpus {a.gpus} but this node has {torch.cuda.device_count()} GPU(s)", file=sys.stderr, flush=True)
         sys.exit(2)
-    c = ctxmod.init(backend="nccl")
+    c = ctxmod.init(backend="gloo" if same else "nccl", same_device=same, transport=a.transport)
     world, rank = c.world_size, c.rank
     dev = c.device
     torch.backends.cudnn.benchmark = True
@@ -189,25 +205,39 @@ def main():
     bf16 = a.precision == "bf16"
     if bf16:
         dnn.bf16_weights(model)
-    reducer = make_reducer("immediate", a.algorithm, native=True)
-    if a.bucket_mb == "auto":
-        from distributed_learning_amd.parallel import cost_model as cm
+    tune = None
+    comm_active = world > 1 or bool(a.force_comm)
+    base_algo = "builtin" if a.algorithm == "auto" else a.algorithm
+    reducer = make_reducer("immediate", base_algo, native=True)
+    if a.force_comm and world == 1:
+        reducer.engine.impl.set_force(True)  # the N>1 data path incl. fp32 staging, as a 1-rank collective
+        reducer.engine.set_accum_fp32(True)
+    if a.algorithm == "auto" and comm_active:
+        from distributed_learning_amd.parallel import autotune as at
 
-        cpu_model = spec.build()
-        ready = cm.ready_times_from_flops(cpu_model, spec.input_shape, 0.028)
-        cmodel = cm.builtin_model(world) if a.algorithm == "builtin" else cm.ring_model(world, 7)
-        cap, _ = cm.choose_bucket_cap(list(cpu_model.parameters()), ready, 0.028, cmodel, wire_bytes_per_elem=4)
-        a.bucket_mb = cap / 2 if bf16 else cap  # the model's cap is in fp32 (wire) bytes
-        del cpu_model
+        tune = at.Autotune(reducer.engine, torch.bfloat16 if bf16 else torch.float32,
+                           at.candidates(world, reducer.engine.transport))
+        tune.run_grid()
+        base_algo = tune.best_model()[0]
+        reducer.algorithm = base_algo
+    if a.bucket_mb == "auto":
+        if tune is not None:
+            cpu_model = spec.build()
+            a.bucket_mb = tune.choose_cap(cpu_model, spec.input_shape, 0.028)
+            del cpu_model
+        else:
+            a.bucket_mb = 8.0
     a.bucket_mb = float(a.bucket_mb)
     model = PipelinedFusedDP(model, reducer, int(a.bucket_mb * 1024 * 1024), dev)
     if a.force_comm and world == 1:
         from distributed_learning_amd.parallel.executor import NativeStreamExecutor
 
-        model.sync.executor = NativeStreamExecutor(reducer.engine, a.algorithm, passthrough=False)
+        model.sync.executor = NativeStreamExecutor(reducer.engine, base_algo, passthrough=False)
         model.sync.passthrough = False
-        reducer.engine.impl.set_force(True)  # the N>1 data path incl. fp32 staging, as a 1-rank collective
-        reducer.engine.set_accum_fp32(True)
+    if tune is not None:
+        per_size = tune.run_buckets([b.flat.numel() for b in model.sync.buckets])
+        model.sync.executor.per_bucket = {b.index: per_size[b.flat.numel()] for b in model.sync.buckets}
+    if comm_active:
         model.sync.executor.reserve(model.sync.buckets)
     opt = FusedSGD(model.module.parameters(), lr=a.lr, momentum=a.momentum, master_weights=bf16)
     data = SyntheticBatches(a.batch, spec.input_shape, spec.num_classes, dev,
@@ -215,12 +245,18 @@ def main():
                             seed=1234, rank=rank, channels_last=True, device_step=a.graph == "on")
     engine = reducer.engine
 
+    nstep = [0]
+
     def step():
         x, y = data.next()
         opt.zero_grad(set_to_none=True)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=not bf16):
             out = model(x)
             loss = cross_entropy(out, y)
+        nstep[0] += 1
+        if rank == a.fail_rank and nstep[0] == a.fail_step:
+            print(f"rank {rank}: injected failure after the forward of step {nstep[0]}", file=sys.stderr, flush=True)
+            os._exit(17)
         loss.backward()
         model.sync_gradients()
         opt.step()
@@ -276,7 +312,7 @@ def main():
     step_seq = [round(tev[i].elapsed_time(tev[i + 1]), 2) for i in range(a.steps)]
     comm_ms = engine.consume_comm_ms() / max(1, a.steps) if not graphed else comm_ms_eager
     engine.set_timing(False)
-    t = torch.tensor([elapsed, comm_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, comm_ms], dtype=torch.float64, device=dev if c.backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, comm_ms = float(t[0]), float(t[1])
     final_loss = float(loss.detach().float())
@@ -297,7 +333,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(img_s / ref, 3) if ref else None,
-            "dtype": "bf16",
+            "dtype": "bf16" if (bf16 or a.precision == "autocast") else "fp32",
             "data": "synthetic (on-device Philox uniform images, random labels; random-init weights)",
             "config": {
                 "model": a.model,
@@ -306,13 +342,15 @@ def main():
                 "seq_len": None,
                 "image_size": list(spec.input_shape),
                 "parallelism": f"dp{world}",
-                "allreduce": a.algorithm,
-                "bucket_mb": a.bucket_mb,
+                "allreduce": a.algorithm if tune is None else "auto:" + base_algo,
+                "bucket_mb": round(a.bucket_mb, 4),
+                "transport": reducer.engine.transport,
+                "same_device": same,
                 "kernels": a.kernels,
                 "precision": a.precision,
                 "conv1x1": a.conv,
                 "hip_graph": graphed,
-                "optimizer": f"fused SGD momentum={a.momentum} (fp32 master weights)",
+                "optimizer": f"fused SGD momentum={a.momentum}" + (" (fp32 master weights)" if bf16 else " (fp32 weights)"),
                 "force_comm": bool(a.force_comm),
             },
             "allreduce_ms_per_step": round(comm_ms, 3),
@@ -327,6 +365,10 @@ def main():
             "warmup_step_ms": [round(x, 2) for x in warm_ms],
             "telemetry": tele,
         }
+        if tune is not None:
+            rec["allreduce_table"] = tune.report()
+            ex = model.sync.executor
+            rec["allreduce_per_bucket"] = [ex.algorithm_for(b) for b in model.sync.buckets]
         if gsync is not None and gsync.hook_calls:
             rec["hook_host_ms_per_step"] = round(gsync.hook_s * 1000.0 / a.steps, 3)
             rec["hook_calls_per_step"] = gsync.hook_calls / a.steps
@@ -344,6 +386,20 @@ def main():
             f.write("\n\n")
             f.write(prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=40,
                                                                 max_name_column_width=60, max_src_column_width=400))
+    if a.check_dir:
+        os.makedirs(a.check_dir, exist_ok=True)
+        names = dict((id(p), n) for n, p in model.module.named_parameters())
+        st = {"params": {}, "grads": {}, "masters": {}}
+        for p in model.module.parameters():
+            n = names[id(p)]
+            st["params"][n] = p.detach().cpu()
+            if p.grad is not None:
+                st["grads"][n] = p.grad.detach().cpu()
+            m = opt.state.get(p, {}).get("master")
+            if m is not None:
+                st["masters"][n] = m.detach().cpu()
+        torch.cuda.synchronize()
+        torch.save(st, os.path.join(a.check_dir, f"rank{rank}.pt"))
     model.cleanup()
     ctxmod.shutdown()
 

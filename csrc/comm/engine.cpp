@@ -21,6 +21,12 @@
 // with hipMemcpyAsync as the links (vexec.h), so every algorithm's multi-rank path executes and
 // is checked on a one-GPU box.
 //
+// Transports: RCCL (ncclSend/Recv groups and collectives), or IPC (ipc.h): each rank exports one
+// window (hipIpcGetMemHandle) and the others map it; P2P steps become pulls out of the sender's
+// window and collectives are emulated with the reduce kernels, ordered by per-rank flag barriers
+// (ipc_sync.hip). IPC runs where RCCL cannot (several ranks on one GPU) and is a candidate
+// transport on an xGMI node, where a rank's pulls load from all 7 peers at once.
+//
 // Failure hygiene: synchronize() polls the stream and ncclCommGetAsyncError
 // with a deadline (DLA_COMM_TIMEOUT_S, default 600 s) and aborts the communicators
 // (ncclCommAbort) on error or timeout instead of blocking forever; the destructor never waits
@@ -46,6 +52,7 @@
 #include "dla_bindings.h"
 #include "dla_kernels.h"
 #include "dla_tables.h"
+#include "ipc.h"
 #include "plan.h"
 #include "plan_exec.h"
 #include "vexec.h"
@@ -104,10 +111,32 @@ static Topology make_topology(int rank, int world, std::vector<std::vector<int>>
   return t;
 }
 
-// Plans are float-agnostic; these algorithms need the reduce kernel (fp32 / bf16 only).
-static bool needs_reduce_kernel(int algo) {
-  return algo == comm::kRing || algo == comm::kDirect || algo == comm::kCentral || algo == comm::kHierRing ||
-         algo == comm::kRingPipe || algo == comm::kHierCentral;
+// Algorithm codes from Python (parallel/engine.py algo_code): bits 0-3 the schedule (comm::Algo),
+// bits 4-7 the ring channel count (0 = every ring of the engine's topology; a prefix of an
+// edge-disjoint set is edge-disjoint), bit 8 the IPC transport (peer-mapped windows, ipc.h)
+// instead of RCCL.
+struct AlgoSel {
+  int algo;
+  int channels;
+  bool ipc;
+};
+static AlgoSel decode_algo(int code) { return AlgoSel{code & 15, (code >> 4) & 15, ((code >> 8) & 1) != 0}; }
+
+// Rings of `t` cut to an algorithm code's channel count (decode_algo).
+static void cut_channels(Topology& t, int code) {
+  const int c = decode_algo(code).channels;
+  if (c > 0)
+    for (auto* v : {&t.rings, &t.local_rings, &t.node_rings})
+      if ((int)v->size() > c) v->resize(c);
+}
+
+// Plans are float-agnostic; these algorithms need the reduce kernel (fp32 / bf16 only). Every
+// algorithm does on the IPC transport (its collectives are emulated with the reduce kernels).
+static bool needs_reduce_kernel(int code) {
+  const AlgoSel s = decode_algo(code);
+  const int algo = s.algo;
+  return s.ipc || algo == comm::kRing || algo == comm::kDirect || algo == comm::kCentral ||
+         algo == comm::kHierRing || algo == comm::kRingPipe || algo == comm::kHierCentral;
 }
 
 static double comm_timeout_s() {
@@ -125,12 +154,18 @@ class CommEngine {
       : device_(device),
         topo_(make_topology(rank, world, std::move(rings), local_size, std::move(local_rings), std::move(node_rings))) {
     std::string id = unique_id;
-    TORCH_CHECK(id.size() == sizeof(ncclUniqueId), "CommEngine: bad unique id size");
-    std::memcpy(&uid_, id.data(), sizeof(ncclUniqueId));
+    // An empty id builds an IPC-only engine (no RCCL communicator): the ranks of a same-device
+    // multi-process run, which RCCL refuses, exchange through peer-mapped windows only.
+    TORCH_CHECK(id.empty() || id.size() == sizeof(ncclUniqueId), "CommEngine: bad unique id size");
+    if (!id.empty()) std::memcpy(&uid_, id.data(), sizeof(ncclUniqueId));
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
     // High-priority stream from torch's pool so the caching allocator knows it.
     stream_ = std::make_unique<c10::hip::HIPStream>(c10::hip::getStreamFromPool(/*isHighPriority=*/true, device_));
-    {
+    int clk_khz = 100000;
+    if (hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeWallClockRate, device_) != hipSuccess || clk_khz <= 0)
+      clk_khz = 100000;
+    wall_khz_ = clk_khz;
+    if (!id.empty()) {
       pybind11::gil_scoped_release nogil;
       DLA_NCCL_CHECK(ncclCommInitRank(&comm_, world, uid_, rank));
       const int L = topo_.L(), K = topo_.nodes();
@@ -158,6 +193,7 @@ class CommEngine {
       if (intra_) ncclCommDestroy(intra_);
       if (comm_) ncclCommDestroy(comm_);
     }
+    ipc_release();
     for (auto& e : timing_events_) hipEventDestroy(e);
     for (auto& e : ready_pool_) hipEventDestroy(e);
     if (last_done_) hipEventDestroy(last_done_);
@@ -179,6 +215,7 @@ class CommEngine {
   void set_force(bool on) {
     force_ = on;
     plans_.clear();
+    ipc_entries_.clear();
   }
   bool accum_fp32() const { return accum_fp32_; }
 
@@ -223,11 +260,72 @@ class CommEngine {
 
   // Build (and cache) the plans of every bucket size up front and size the scratch buffer for the
   // largest, so no allocation ever happens mid-backward or inside a HIP-graph capture.
+  // IPC codes instead record the window size they need (ipc_need); the Python front-end then
+  // grows every rank's window collectively (ipc_alloc / ipc_open), since peers map it.
   void reserve(int algo, std::vector<int64_t> sizes, int dtype) {
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
+    if (uses_ipc(algo)) {
+      for (int64_t n : sizes) {
+        if ((topo_.world == 1 && !force_) || n == 0) continue;
+        const size_t esz = staged(algo, dtype) ? 4 : (dtype == kBF16 ? 2 : 4);
+        ipc_need_ = std::max(ipc_need_, comm::kIpcHeaderBytes + (size_t)ipc_entry(algo, n).sched.total * esz + 256);
+      }
+      return;
+    }
     size_t need = 0;
     for (int64_t n : sizes) need = std::max(need, scratch_bytes(plan_for(algo, n), n, dtype));
     ensure_scratch(need);
+  }
+
+  // ---------------------------------------------------------------------------------------
+  // IPC windows (ipc.h). Collective over the group, driven from Python: every rank calls
+  // ipc_alloc(bytes) with the same size, the handles are all-gathered, every rank calls ipc_open.
+  // ---------------------------------------------------------------------------------------
+  bool uses_ipc(int code) const { return !comm_ || decode_algo(code).ipc; }
+  int64_t ipc_need() const { return (int64_t)ipc_need_; }
+  int64_t ipc_capacity() const { return (int64_t)ipc_bytes_; }
+  bool has_rccl() const { return comm_ != nullptr; }
+
+  pybind11::bytes ipc_alloc(int64_t bytes) {
+    TORCH_CHECK(bytes > (int64_t)comm::kIpcHeaderBytes, "ipc_alloc: window too small");
+    c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
+    ipc_release();
+    DLA_HIP_THROW(hipMalloc(&ipc_base_, (size_t)bytes));
+    DLA_HIP_THROW(hipMemset(ipc_base_, 0, (size_t)bytes));
+    DLA_HIP_THROW(hipDeviceSynchronize());
+    ipc_bytes_ = (size_t)bytes;
+    hipIpcMemHandle_t h;
+    DLA_HIP_THROW(hipIpcGetMemHandle(&h, ipc_base_));
+    return pybind11::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  }
+
+  void ipc_open(std::vector<pybind11::bytes> handles) {
+    TORCH_CHECK((int)handles.size() == topo_.world, "ipc_open: need one handle per rank");
+    TORCH_CHECK(ipc_base_, "ipc_open: call ipc_alloc first");
+    c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
+    ipc_close_peers();
+    ipc_peer_.assign(topo_.world, nullptr);
+    for (int r = 0; r < topo_.world; ++r) {
+      if (r == topo_.rank) {
+        ipc_peer_[r] = static_cast<char*>(ipc_base_);
+        continue;
+      }
+      std::string s = handles[r];
+      TORCH_CHECK(s.size() == sizeof(hipIpcMemHandle_t), "ipc_open: bad handle size");
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, s.data(), sizeof(h));
+      void* p = nullptr;
+      DLA_HIP_THROW(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+      ipc_peer_[r] = static_cast<char*>(p);
+    }
+  }
+
+  // 1 when a barrier timed out (a peer never arrived); valid after the comm stream drained
+  int ipc_error() {
+    if (!ipc_base_) return 0;
+    int v = 0;
+    DLA_HIP_THROW(hipMemcpy(&v, static_cast<char*>(ipc_base_) + comm::kIpcErrOffset, sizeof(int), hipMemcpyDeviceToHost));
+    return v;
   }
 
   // ---------------------------------------------------------------------------------------
@@ -270,6 +368,7 @@ class CommEngine {
 
   void broadcast(at::Tensor t, int root) {
     check(t);
+    TORCH_CHECK(comm_, "CommEngine.broadcast needs the RCCL communicator (IPC-only engine)");
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
     join_current();
     pybind11::gil_scoped_release nogil;
@@ -281,6 +380,7 @@ class CommEngine {
     check(out);
     check(in);
     TORCH_CHECK(out.numel() == in.numel() * topo_.world, "allgather: out must hold world * in elements");
+    TORCH_CHECK(comm_, "CommEngine.allgather needs the RCCL communicator (IPC-only engine)");
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
     join_current();
     pybind11::gil_scoped_release nogil;
@@ -323,7 +423,16 @@ class CommEngine {
     int spins = 0;
     while (true) {
       hipError_t q = hipStreamQuery(stream_->stream());
-      if (q == hipSuccess) return true;
+      if (q == hipSuccess) {
+        if (ipc_base_ && ipc_error()) {
+          abort_comms();
+          if (throw_on_fail)
+            throw std::runtime_error("CommEngine: an IPC peer did not reach a barrier within the timeout "
+                                     "(DLA_COMM_TIMEOUT_S; peer failure?); engine aborted");
+          return false;
+        }
+        return true;
+      }
       if (q != hipErrorNotReady) {
         abort_comms();
         if (throw_on_fail) throw std::runtime_error(std::string("CommEngine: comm stream failed: ") + hipGetErrorString(q));
@@ -345,6 +454,25 @@ class CommEngine {
       }
       if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(spins > 4096 ? 1000 : 20));
     }
+  }
+
+  void ipc_close_peers() {
+    for (int r = 0; r < (int)ipc_peer_.size(); ++r)
+      if (r != topo_.rank && ipc_peer_[r]) hipIpcCloseMemHandle(ipc_peer_[r]);
+    ipc_peer_.clear();
+  }
+
+  // bounded drain of the comm stream, then unmap the peers and free the window
+  void ipc_release() {
+    if (!ipc_base_ && ipc_peer_.empty()) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (hipStreamQuery(stream_->stream()) == hipErrorNotReady &&
+           std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < 60.0)
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    ipc_close_peers();
+    if (ipc_base_) hipFree(ipc_base_);
+    ipc_base_ = nullptr;
+    ipc_bytes_ = 0;
   }
 
   void abort_comms() {
@@ -385,15 +513,47 @@ class CommEngine {
     used_timing_ += 2;
   }
 
-  const Plan& plan_for(int algo, int64_t n) {
-    auto key = std::make_pair(algo, n);
+  // the engine's topology seen from `rank`, its rings cut to the code's channel count
+  Topology topo_for(int code, int rank) const {
+    Topology t = topo_;
+    t.rank = rank;
+    cut_channels(t, code);
+    return t;
+  }
+
+  const Plan& plan_for(int code, int64_t n) {
+    auto key = std::make_pair(code, n);
     auto it = plans_.find(key);
     if (it != plans_.end()) return it->second;
+    return plans_.emplace(key, make_plan(code, topo_.rank, n)).first->second;
+  }
+
+  struct IpcEntry {
+    std::vector<Plan> plans;  // every rank's (the receiver matches its pulls against the senders')
+    comm::IpcSchedule sched;
+  };
+
+  const IpcEntry& ipc_entry(int code, int64_t n) {
+    auto key = std::make_pair(code, n);
+    auto it = ipc_entries_.find(key);
+    if (it != ipc_entries_.end()) return it->second;
+    IpcEntry e;
+    for (int r = 0; r < topo_.world; ++r) e.plans.push_back(make_plan(code, r, n));
+    try {
+      e.sched = comm::build_ipc_schedule(e.plans, topo_for(code, topo_.rank), topo_.rank, n);
+    } catch (const std::exception& ex) {
+      TORCH_CHECK(false, ex.what());
+    }
+    return ipc_entries_.emplace(key, std::move(e)).first->second;
+  }
+
+  Plan make_plan(int code, int rank, int64_t n) const {
+    const int algo = decode_algo(code).algo;
     TORCH_CHECK(algo >= comm::kBuiltin && algo < comm::kAlgoCount, "CommEngine: unknown algorithm ", algo);
     Plan p;
     try {
       // plans are built for summation; the average is folded into the last reduce of each phase
-      p = comm::build_plan(algo, topo_, n, 1.f / (float)topo_.world);
+      p = comm::build_plan(algo, topo_for(code, rank), n, 1.f / (float)topo_.world);
     } catch (const std::exception& e) {
       TORCH_CHECK(false, e.what());
     }
@@ -410,7 +570,7 @@ class CommEngine {
       st.ops.push_back(o);
       p.steps.push_back(st);
     }
-    return plans_.emplace(key, std::move(p)).first->second;
+    return p;
   }
 
   bool staged(int algo, int dtype) const { return accum_fp32_ && dtype == kBF16 && (topo_.world > 1 || force_); }
@@ -459,6 +619,10 @@ class CommEngine {
       if (grads) pack_tensors_on(*grads, *offsets, flat, 1.f, st);
       return;
     }
+    if (uses_ipc(algo)) {
+      allreduce_ipc(flat, algo, average, grads, offsets);
+      return;
+    }
     const Plan& plan = plan_for(algo, n);
     const bool stg = staged(algo, dt) && (flat.scalar_type() == at::kBFloat16);
     ensure_scratch(scratch_bytes(plan, n, dt));
@@ -478,6 +642,100 @@ class CommEngine {
     comm::execute_plan(tr, plan, st, plan_events_);
     if (stg) launch_cast(flat.data_ptr(), kBF16, lay.data, kF32, n, 1.f, st);
   }
+
+  // The same Plan over peer-mapped windows (ipc.h): the bucket is staged into this rank's window
+  // (fp32 for accum_fp32 bf16 buckets, else its own dtype), the plan runs there with pulls from the
+  // peers' windows and flag barriers, and the result is cast / copied back into `flat`.
+  void allreduce_ipc(const at::Tensor& flat, int code, bool average, const std::vector<at::Tensor>* grads,
+                     const std::vector<int64_t>* offsets) {
+    const int64_t n = flat.numel();
+    hipStream_t st = stream_->stream();
+    const int dt = flat.scalar_type() == at::kBFloat16 ? kBF16 : kF32;
+    const bool stg = staged(code, dt);
+    const int wdt = stg ? kF32 : dt;
+    const size_t esz = wdt == kF32 ? 4 : 2;
+    const IpcEntry& e = ipc_entry(code, n);
+    const size_t need = comm::kIpcHeaderBytes + (size_t)e.sched.total * esz;
+    TORCH_CHECK(ipc_base_ && !ipc_peer_.empty() && need <= ipc_bytes_,
+                "CommEngine: the IPC window (", ipc_bytes_, " B) does not hold this all-reduce (", need,
+                " B); call reserve() with the bucket sizes first (NativeEngine.reserve maps the windows)");
+    char* data = static_cast<char*>(ipc_base_) + comm::kIpcHeaderBytes;
+    if (grads) {
+      at::Tensor dst = at::from_blob(data, {n}, at::TensorOptions()
+                                                    .dtype(wdt == kF32 ? at::kFloat : at::kBFloat16)
+                                                    .device(at::kCUDA, device_));
+      pack_tensors_on(*grads, *offsets, dst, 1.f, st);
+    } else {
+      launch_cast(data, wdt, flat.data_ptr(), dt, n, 1.f, st);
+    }
+    comm::LocalIssuer iss(wdt, esz);
+    iss.set_stream(st);
+    IpcDeviceBackend be{*this, e.sched, esz, iss};
+    comm::IpcRunner<IpcDeviceBackend> run{be, e.sched, e.plans[topo_.rank], topo_.rank, average, ipc_tok_};
+    IpcTransport tr{run, be, iss, e.plans[topo_.rank], average, *this};
+    comm::execute_plan(tr, e.plans[topo_.rank], st, plan_events_);
+    iss.set_stream(st);
+    iss.flush();
+    launch_cast(flat.data_ptr(), dt, data, wdt, n, 1.f, st);
+  }
+
+  struct IpcDeviceBackend {
+    CommEngine& e;
+    const comm::IpcSchedule& s;
+    size_t esz;
+    comm::LocalIssuer& iss;
+    char* win(int r) const { return e.ipc_peer_[r] + comm::kIpcHeaderBytes; }
+    void* ptr(int r, const comm::Ref& ref) const {
+      return win(r) + (size_t)((ref.buf == comm::kData ? 0 : s.scratch_off) + ref.off) * esz;
+    }
+    void* tmp(int r, int64_t off) const { return win(r) + (size_t)(s.temp_off + off) * esz; }
+    void barrier(uint64_t set, const std::vector<int>& wait_ranks, uint64_t wait) {
+      iss.flush();
+      IpcBarrier b{};
+      b.mine = reinterpret_cast<uint64_t*>(e.ipc_peer_[e.topo_.rank]);
+      b.set = set;
+      TORCH_CHECK((int)wait_ranks.size() <= kMaxIpcPeers, "IPC barrier: too many peers");
+      b.npeers = (int)wait_ranks.size();
+      for (int i = 0; i < b.npeers; ++i) b.peer[i] = reinterpret_cast<const uint64_t*>(e.ipc_peer_[wait_ranks[i]]);
+      b.wait = wait;
+      b.err = reinterpret_cast<int*>(e.ipc_peer_[e.topo_.rank] + comm::kIpcErrOffset);
+      b.timeout_ticks = (uint64_t)(comm_timeout_s() * (double)e.wall_khz_ * 1000.0);
+      launch_ipc_barrier(b, iss.stream());
+    }
+    void copy(void* dst, const void* src, int64_t n) { iss.copy(dst, src, n); }
+    void reduce(void* dst, bool acc, const void* const* srcs, int nsrc, int64_t n, float scale) {
+      iss.reduce(dst, acc, srcs, nsrc, n, scale);
+    }
+  };
+
+  // plan_exec.h transport over the IPC runner: P2P steps and collectives are pulls + barriers on
+  // the comm stream, local ops go through the multi-lane issuer on the given stream.
+  struct IpcTransport {
+    comm::IpcRunner<IpcDeviceBackend>& run;
+    IpcDeviceBackend& be;
+    comm::LocalIssuer& iss;
+    const Plan& p;
+    bool average;
+    CommEngine& e;
+    void coll(size_t k, hipStream_t st) {
+      iss.set_stream(st);
+      run.coll(k);
+      iss.flush();
+    }
+    void transfers(size_t k, hipStream_t st) {
+      iss.set_stream(st);
+      run.transfers(k);
+      iss.flush();
+    }
+    bool has_local(size_t k) const { return std::any_of(p.steps[k].ops.begin(), p.steps[k].ops.end(), comm::is_local); }
+    void locals(size_t k, hipStream_t ls) {
+      iss.set_stream(ls);
+      const int me = e.topo_.rank;
+      comm::issue_locals(p.steps[k], [&](const comm::Ref& r) { return be.ptr(me, r); }, iss, average);
+      iss.flush();
+    }
+    hipStream_t side_stream() { return e.side_stream(); }
+  };
 
   // The RCCL transport of plan_exec.h: collectives and P2P groups on this rank's communicators,
   // local ops through the multi-lane issuer.
@@ -547,6 +805,12 @@ class CommEngine {
   bool force_ = false;
   std::unique_ptr<c10::hip::HIPStream> stream_;
   std::map<std::pair<int, int64_t>, Plan> plans_;
+  std::map<std::pair<int, int64_t>, IpcEntry> ipc_entries_;
+  void* ipc_base_ = nullptr;       // this rank's window (hipMalloc, exported)
+  size_t ipc_bytes_ = 0, ipc_need_ = 0;
+  std::vector<char*> ipc_peer_;    // every rank's window base as mapped here (mine = ipc_base_)
+  uint64_t ipc_tok_ = 0;           // barrier token counter, identical sequence on every rank
+  int wall_khz_ = 100000;          // constant-clock rate for the barrier timeout
   at::Tensor scratch_;
   std::vector<hipEvent_t> ready_pool_;
   comm::EventPool plan_events_;
@@ -635,10 +899,12 @@ static int64_t virtual_allreduce(std::vector<at::Tensor> bufs, int algo, bool av
                 "virtual_allreduce: buffers must share numel, dtype, device and be contiguous");
   }
   TORCH_CHECK(dtype == at::kFloat || dtype == at::kBFloat16, "virtual_allreduce: fp32 / bf16 only");
+  Topology t0 = make_topology(0, N, rings, local_size, local_rings, node_rings);
+  cut_channels(t0, algo);
+  algo = decode_algo(algo).algo;
   TORCH_CHECK(algo >= comm::kBuiltin && algo < comm::kAlgoCount, "virtual_allreduce: unknown algorithm ", algo);
   if (N == 1 || n == 0) return 0;
   std::vector<Plan> plans;
-  Topology t0 = make_topology(0, N, rings, local_size, local_rings, node_rings);
   for (int r = 0; r < N; ++r) {
     Topology t = t0;
     t.rank = r;
@@ -718,10 +984,96 @@ static int64_t virtual_allreduce(std::vector<at::Tensor> bufs, int algo, bool av
   return 0;
 }
 
+// All-reduce host buffers (one CPU tensor per rank) through the IPC protocol of ipc.h with one
+// thread per rank and atomic flags: the schedule matching and barrier protocol the GPU transport
+// runs, checked under real concurrency in the CPU test suite.
+static void ipc_host_allreduce(std::vector<at::Tensor> bufs, int code, bool average, std::vector<std::vector<int>> rings,
+                               int local_size, std::vector<std::vector<int>> local_rings,
+                               std::vector<std::vector<int>> node_rings, bool accum_fp32, double timeout_s) {
+  const int N = (int)bufs.size();
+  TORCH_CHECK(N >= 1, "ipc_host_allreduce: no buffers");
+  const int64_t n = bufs[0].numel();
+  const auto dtype = bufs[0].scalar_type();
+  for (auto& b : bufs)
+    TORCH_CHECK(!b.is_cuda() && b.numel() == n && b.scalar_type() == dtype && b.is_contiguous(),
+                "ipc_host_allreduce: contiguous CPU buffers of one numel / dtype");
+  TORCH_CHECK(dtype == at::kFloat || dtype == at::kBFloat16, "ipc_host_allreduce: fp32 / bf16 only");
+  if (N == 1 || n == 0) return;
+  Topology t0 = make_topology(0, N, rings, local_size, local_rings, node_rings);
+  cut_channels(t0, code);
+  const int algo = decode_algo(code).algo;
+  std::vector<Plan> plans;
+  for (int r = 0; r < N; ++r) {
+    Topology t = t0;
+    t.rank = r;
+    try {
+      plans.push_back(comm::build_plan(algo, t, n, 1.f / (float)N));
+    } catch (const std::exception& e) {
+      TORCH_CHECK(false, e.what());
+    }
+  }
+  std::vector<comm::IpcSchedule> sch;
+  for (int r = 0; r < N; ++r) {
+    Topology t = t0;
+    t.rank = r;
+    try {
+      sch.push_back(comm::build_ipc_schedule(plans, t, r, n));
+    } catch (const std::exception& e) {
+      TORCH_CHECK(false, e.what());
+    }
+  }
+  const bool stage = accum_fp32 && dtype == at::kBFloat16;
+  comm::IpcHostShared sh(N);
+  sh.bf16 = dtype == at::kBFloat16 && !stage;
+  sh.esz = sh.bf16 ? 2 : 4;
+  sh.scratch_off = sch[0].scratch_off;
+  sh.temp_off = sch[0].temp_off;
+  sh.timeout_s = timeout_s;
+  for (int r = 0; r < N; ++r) {
+    sh.windows[r].assign((size_t)sch[r].total * sh.esz + 64, 0);
+    char* w = sh.windows[r].data();
+    if (stage) {
+      const uint16_t* b = static_cast<const uint16_t*>(bufs[r].data_ptr());
+      for (int64_t i = 0; i < n; ++i) reinterpret_cast<float*>(w)[i] = comm::HostBackend::b2f(b[i]);
+    } else {
+      std::memcpy(w, bufs[r].data_ptr(), (size_t)n * sh.esz);
+    }
+  }
+  std::vector<std::string> errs(N);
+  {
+    pybind11::gil_scoped_release nogil;
+    std::vector<std::thread> th;
+    for (int r = 0; r < N; ++r)
+      th.emplace_back([&, r] {
+        try {
+          comm::IpcHostBackend be{sh, r};
+          uint64_t tok = 0;
+          comm::ipc_host_run(be, sch[r], plans[r], average, tok);
+        } catch (const std::exception& e) {
+          errs[r] = e.what();
+          sh.timeout_s = 0.0;  // let the other ranks fail fast instead of waiting out the timeout
+        }
+      });
+    for (auto& x : th) x.join();
+  }
+  for (int r = 0; r < N; ++r) TORCH_CHECK(errs[r].empty(), "ipc_host_allreduce rank ", r, ": ", errs[r]);
+  for (int r = 0; r < N; ++r) {
+    const char* w = sh.windows[r].data();
+    if (stage) {
+      uint16_t* b = static_cast<uint16_t*>(bufs[r].data_ptr());
+      for (int64_t i = 0; i < n; ++i) b[i] = comm::HostBackend::f2b(reinterpret_cast<const float*>(w)[i]);
+    } else {
+      std::memcpy(bufs[r].data_ptr(), w, (size_t)n * sh.esz);
+    }
+  }
+}
+
 static std::string plan_describe(int algo, int rank, int world, int64_t n, std::vector<std::vector<int>> rings,
                                  int local_size, std::vector<std::vector<int>> local_rings,
                                  std::vector<std::vector<int>> node_rings, bool average) {
   Topology t = make_topology(rank, world, std::move(rings), local_size, std::move(local_rings), std::move(node_rings));
+  cut_channels(t, algo);
+  algo = decode_algo(algo).algo;
   try {
     return comm::describe(comm::build_plan(algo, t, n, average ? 1.f / (float)world : 1.f));
   } catch (const std::exception& e) {
@@ -762,7 +1114,20 @@ void bind_comm(pybind11::module& m) {
       .def("broadcast", &CommEngine::broadcast)
       .def("allgather", &CommEngine::allgather)
       .def("set_timing", &CommEngine::set_timing)
-      .def("consume_comm_ms", &CommEngine::consume_comm_ms);
+      .def("consume_comm_ms", &CommEngine::consume_comm_ms)
+      .def("has_rccl", &CommEngine::has_rccl)
+      .def("ipc_need", &CommEngine::ipc_need)
+      .def("ipc_capacity", &CommEngine::ipc_capacity)
+      .def("ipc_alloc", &CommEngine::ipc_alloc)
+      .def("ipc_open", &CommEngine::ipc_open)
+      .def("ipc_error", &CommEngine::ipc_error);
+  m.def("ipc_host_allreduce", &ipc_host_allreduce,
+        "all-reduce CPU buffers with the IPC transport's pull/barrier protocol, one thread per rank",
+        pybind11::arg("bufs"), pybind11::arg("algo"), pybind11::arg("average") = true, pybind11::arg("rings") = VV{},
+        pybind11::arg("local_size") = 0, pybind11::arg("local_rings") = VV{}, pybind11::arg("node_rings") = VV{},
+        pybind11::arg("accum_fp32") = false, pybind11::arg("timeout_s") = 30.0);
+  m.attr("ALGO_IPC_FLAG") = 256;
+  m.attr("ALGO_CHANNEL_SHIFT") = 4;
   m.def("virtual_allreduce", &virtual_allreduce, "all-reduce N virtual ranks' buffers with the engine's schedules",
         pybind11::arg("bufs"), pybind11::arg("algo"), pybind11::arg("average") = true, pybind11::arg("rings") = VV{},
         pybind11::arg("local_size") = 0, pybind11::arg("local_rings") = VV{}, pybind11::arg("node_rings") = VV{},

@@ -91,6 +91,24 @@ void launch_reduce_lanes(ReduceLanes& lanes, int dtype, hipStream_t stream);
 // dst = scale * src with dtype conversion (fp32 / bf16 either way)
 void launch_cast(void* dst, int dst_dtype, const void* src, int src_dtype, int64_t n, float scale, hipStream_t stream);
 
+// ---- cross-process barrier over peer-mapped memory (ipc_sync.hip) ---------------------------
+// One wave: publish `set` into this rank's flag (system-scope release, so everything the stream
+// wrote before is visible to peers that observe it), then wait until every listed peer flag is
+// >= `wait` (system-scope acquire). A peer that never arrives ends the wait after `timeout_ticks`
+// of the constant 100 MHz clock with err[0] = 1 instead of spinning forever, so the grid always
+// drains; the host reads err after the stream completes.
+constexpr int kMaxIpcPeers = 16;
+struct IpcBarrier {
+  uint64_t* mine;  // null: do not publish
+  uint64_t set;
+  const uint64_t* peer[kMaxIpcPeers];
+  int npeers;
+  uint64_t wait;
+  int* err;
+  uint64_t timeout_ticks;
+};
+void launch_ipc_barrier(const IpcBarrier& b, hipStream_t stream);
+
 // ---- synthetic data (synthetic.hip) ---------------------------------------------------------
 // Philox stream position = offset [+ (*step) * per_step when `step` (device int64 counter) is set].
 void launch_uniform_fill(void* out, int64_t n, int dtype, uint64_t seed, uint64_t offset, float lo, float hi,

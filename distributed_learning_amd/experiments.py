@@ -51,7 +51,9 @@ def _reducer(config, kind: str, algorithm: str):
             return make_reducer("hierarchical", algo, native=True, local_size=_local_size(config),
                                 channels=config.channels)
         return make_reducer("hierarchical", algorithm, channels=1, local_size=_local_size(config))
-    return make_reducer("immediate", algorithm, channels=ch if algorithm.startswith("ring") else 1, native=native)
+    if native:  # the engine's default is one ring per outgoing link; an explicit --channels passes through
+        return make_reducer("immediate", algorithm, channels=config.channels or None, native=True)
+    return make_reducer("immediate", algorithm, channels=ch if algorithm.startswith("ring") else 1)
 
 
 def _wrap(cls, config, **kw):

@@ -110,10 +110,24 @@ class _SideWork:
 # and at bs1280 it stalls: p50 89.7 ms but single steps of 1.4-6.9 s (profiles/r3/g47_defer_batch_ab.md),
 # from the caching allocator's cross-stream frees (record_stream) forcing synchronising retries near the
 # memory ceiling. Keep "all" for tests and small batches.
+#
+# Who may see a deferred gradient before the join: AccumulateGrad stores it (no read), the end-of-backward
+# callback joins before backward() returns, GradSync's executors join it into their stream before they read,
+# FusedSGD.step joins as a safety net. Consumers that read gradients INSIDE backward without joining
+# (torch DDP's reducer hooks) must call block_deferral() for their lifetime: TorchDDP does.
 WGRAD_DEFER = os.environ.get("DLA_WGRAD_DEFER", "3x3")
 WGRAD_JOIN = os.environ.get("DLA_WGRAD_JOIN", "end")
 _DEFER_PENDING: dict = {}  # device -> the side stream holds work the compute stream has not joined yet
-_DEFER_CB: dict = {}  # device -> an end-of-backward join is queued
+_DEFERRED_W: dict = {}  # device -> ids of the weights deferred in the running backward (each at most once)
+_DEFER_BLOCKS = [0]  # > 0: some live consumer reads gradients inside backward without joining
+
+
+def block_deferral() -> None:
+    _DEFER_BLOCKS[0] += 1
+
+
+def unblock_deferral() -> None:
+    _DEFER_BLOCKS[0] = max(0, _DEFER_BLOCKS[0] - 1)
 
 
 def _side_stream(device: torch.device) -> torch.cuda.Stream:
@@ -137,11 +151,15 @@ def join_compute(device: torch.device) -> None:
     if _DEFER_PENDING.get(device):
         torch.cuda.current_stream(device).wait_stream(_SIDE_STREAMS[device])
         _DEFER_PENDING[device] = False
+    _DEFERRED_W.pop(device, None)
 
 
-def _end_of_backward_join(device: torch.device) -> None:
-    _DEFER_CB[device] = False
-    join_compute(device)
+def join_all_devices() -> None:
+    """Safety net for optimizers: join every device's pending late weight gradients (a backward that
+    raised drops its end-of-backward callback)."""
+    for dev, pending in list(_DEFER_PENDING.items()):
+        if pending:
+            join_compute(dev)
 
 
 # "auto": the 3x3 weight gradients plus the 1x1 ones whose arithmetic intensity Cin*Cout/(Cin+Cout)
@@ -165,8 +183,16 @@ def _wgrad_after_dgrad(fn, ctx, keep, device: torch.device):
     weight = getattr(ctx, "weight_leaf", None)
     # inside HIP-graph capture (GoogLeNet bs128 --graph on: 19.8k vs 20.7k img/s with the fork / join
     # nodes, profiles/r3/g38_other_models_ab.txt) the weight gradient stays on the captured stream
-    if weight is None or weight.grad is not None or torch.cuda.is_current_stream_capturing():
+    if (weight is None or weight.grad is not None or _DEFER_BLOCKS[0] or
+            torch.cuda.is_current_stream_capturing()):
         return fn()
+    seen = _DEFERRED_W.setdefault(device, set())
+    if id(weight) in seen:
+        # a weight used twice in one graph: autograd sums its two gradients on the compute stream before any
+        # join, so the first (deferred) one must be complete first and this one runs inline
+        join_compute(device)
+        return fn()
+    seen.add(id(weight))
     cur = torch.cuda.current_stream(device)
     side = _side_stream(device)
     side.wait_stream(cur)
@@ -176,9 +202,10 @@ def _wgrad_after_dgrad(fn, ctx, keep, device: torch.device):
         t.record_stream(side)
     out.record_stream(cur)
     _DEFER_PENDING[device] = True
-    if not _DEFER_CB.get(device):  # the end-of-backward join (also after the last conv in "conv" mode)
-        _DEFER_CB[device] = True
-        torch.autograd.Variable._execution_engine.queue_callback(lambda: _end_of_backward_join(device))
+    # the end-of-backward join (also after the last conv in "conv" mode), queued on THIS graph task by every
+    # deferral: a backward that raises drops its callbacks with it instead of leaving a sticky "queued" flag
+    # that would skip the join of every later backward; the extra callbacks find nothing pending
+    torch.autograd.Variable._execution_engine.queue_callback(lambda: join_compute(device))
     return out
 
 
@@ -467,7 +494,7 @@ class _Conv3x3(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, [ctx.stride] * 2, [1, 1], [1, 1], False,
                                                          [0, 0], 1, [True, False, False])[0]
         if defer:
-            dw = _wgrad_after_dgrad(wgrad, ctx, (dy, x), dy.device)
+            dw = _wgrad_after_dgrad(wgrad, ctx, (dy, x, w), dy.device)  # w: the aten fallback reads it
         if wg is not None:
             dw = wg.result()
         return dx, dw, None, None

@@ -69,6 +69,9 @@ class FusedSGD(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        from . import conv as _conv
+
+        _conv.join_all_devices()  # late weight gradients of a backward that raised before its own join
         for gi, group in enumerate(self.param_groups):
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:

@@ -49,20 +49,26 @@ class DistContext:
     def local_world_size(self) -> int:
         return self.env.local_world_size
 
-    def engine(self, local_size: Optional[int] = None, channels: int = 0):
-        """The native RCCL engine for the WORLD group (created lazily, GPU + nccl only).
+    transport: str = "rccl"
+    same_device: bool = False
+
+    def engine(self, local_size: Optional[int] = None, channels: int = 0, transport: Optional[str] = None):
+        """The native engine for the WORLD group (created lazily, GPU only).
 
         ``local_size`` (ranks per node of the 2-step algorithms) and ``channels`` (ring channels)
-        are part of the engine's topology; one engine is kept per distinct (local_size, channels)."""
+        are part of the engine's topology; ``transport`` (default: the context's, ``rccl`` unless
+        the ranks share one GPU) picks RCCL or the IPC windows; one engine is kept per distinct
+        (local_size, channels, transport)."""
         from .engine import NativeEngine, topology
 
+        transport = transport or self.transport
         topo = topology(self.world_size, channels, local_size)
-        key = (topo["local_size"], len(topo["rings"]))
+        key = (topo["local_size"], len(topo["rings"]), transport)
         if self._engines is None:
             self._engines = {}
         if key not in self._engines:
             self._engines[key] = NativeEngine.create(dist.group.WORLD, self.device, channels=channels,
-                                                     local_size=topo["local_size"])
+                                                     local_size=topo["local_size"], transport=transport)
             if self._engine is None:
                 self._engine = self._engines[key]
         return self._engines[key]
@@ -70,8 +76,17 @@ class DistContext:
 
 def init(backend: Optional[str] = None, rank: Optional[int] = None, world_size: Optional[int] = None,
          master_addr: Optional[str] = None, master_port: Optional[int] = None, device: Optional[str] = None,
-         timeout_s: float = 600.0, ifname: Optional[str] = None) -> DistContext:
-    """Initialise (or return) the process-wide distributed context."""
+         timeout_s: float = 600.0, ifname: Optional[str] = None, same_device: Optional[bool] = None,
+         transport: Optional[str] = None) -> DistContext:
+    """Initialise (or return) the process-wide distributed context.
+
+    ``same_device`` (default: ``DLA_SAME_DEVICE=1``): every rank uses ``cuda:0`` -- N processes
+    sharing one GPU, the way the multi-process data path is exercised on a one-GPU box. RCCL
+    refuses that, so the process group is Gloo and the gradient engine uses the IPC transport.
+    ``transport`` (default ``DLA_TRANSPORT`` or ``rccl``; ``ipc`` when ``same_device``)."""
+    if same_device is None:
+        same_device = os.environ.get("DLA_SAME_DEVICE", "0") == "1"
+    transport = transport or os.environ.get("DLA_TRANSPORT") or ("ipc" if same_device else "rccl")
     global _CTX
     if _CTX is not None:
         return _CTX
@@ -92,10 +107,12 @@ def init(backend: Optional[str] = None, rank: Optional[int] = None, world_size: 
         os.environ.setdefault("GLOO_SOCKET_IFNAME", ifname)
     use_gpu = torch.cuda.is_available() if device is None else str(device).startswith("cuda")
     if backend is None:
-        backend = "nccl" if use_gpu else "gloo"
+        backend = "nccl" if use_gpu and not same_device else "gloo"
+    if same_device and backend == "nccl" and env.world_size > 1:
+        raise ValueError("same_device: RCCL cannot run several ranks on one GPU; use the gloo backend")
     if use_gpu:
         ndev = torch.cuda.device_count()
-        dev = torch.device("cuda", env.local_rank % max(1, ndev))
+        dev = torch.device("cuda", 0 if same_device else env.local_rank % max(1, ndev))
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
@@ -108,6 +125,8 @@ def init(backend: Optional[str] = None, rank: Optional[int] = None, world_size: 
             kw["device_id"] = dev
         dist.init_process_group(init_method=f"tcp://{env.master_addr}:{env.master_port}", **kw)
     _CTX = DistContext(env, backend, dev)
+    _CTX.transport = transport
+    _CTX.same_device = bool(same_device)
     return _CTX
 
 

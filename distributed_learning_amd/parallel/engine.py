@@ -15,12 +15,17 @@ sub-communicators (reference /root/reference/src/reducers.py:38-69, main.py:129-
 a side stream, overlapped with the next sub-step's transfer, ``hier_central`` the 2-step reducer with
 a parameter server between nodes (reference ``main_central_reduce``, main.py:198-206).
 
+Transports: every schedule runs on RCCL, or -- ``ipc_`` prefix, or an engine created with
+``transport="ipc"`` -- on peer-mapped IPC windows with flag barriers (csrc/comm/ipc.h): pulls
+from the peers' HBM (same GPU, or over xGMI). ``:C`` suffix = C ring channels.
+
 Every schedule is a cached Plan (csrc/comm/plan.h); :mod:`.virtual` runs the identical plans for
 N virtual ranks inside one process (one GPU or the CPU), which is how the N>1 paths are tested
 on a one-GPU box.
 """
 from __future__ import annotations
 
+import functools
 from typing import Dict, List, Optional
 
 import torch
@@ -43,12 +48,28 @@ ALGO_CODES: Dict[str, str] = {
 }
 
 
+def parse_algo(name: str):
+    """``[ipc_]<schedule>[:<channels>]`` -> (schedule, channels, ipc). ``ipc_`` runs the schedule on the
+    IPC transport (peer-mapped windows, csrc/comm/ipc.h) instead of RCCL; ``:C`` uses the first C
+    edge-disjoint rings of the engine's topology (ring schedules; 0 / absent = all)."""
+    base, _, ch = name.partition(":")
+    ipc = base.startswith("ipc_")
+    if ipc:
+        base = base[4:]
+    if base not in ALGO_CODES:
+        raise ValueError(f"unknown native all-reduce algorithm {name!r}; choose from {sorted(ALGO_CODES)} "
+                         "(optionally 'ipc_' prefixed and ':<channels>' suffixed)")
+    c = int(ch) if ch else 0
+    if not 0 <= c <= 15:
+        raise ValueError(f"channel count must be 0..15, got {c}")
+    return base, c, ipc
+
+
+@functools.lru_cache(maxsize=None)
 def algo_code(name: str) -> int:
     C = _ext.require()
-    try:
-        return int(getattr(C, ALGO_CODES[name]))
-    except KeyError:
-        raise ValueError(f"unknown native all-reduce algorithm {name!r}; choose from {sorted(ALGO_CODES)}") from None
+    base, c, ipc = parse_algo(name)
+    return int(getattr(C, ALGO_CODES[base])) | (c << 4) | (256 if ipc else 0)
 
 
 def topology(world: int, channels: int = 0, local_size: Optional[int] = None) -> Dict[str, object]:
@@ -77,18 +98,26 @@ def topology(world: int, channels: int = 0, local_size: Optional[int] = None) ->
 class NativeEngine:
     """Wraps ``_C.CommEngine`` for one process group."""
 
-    def __init__(self, impl, group, device: torch.device, channels: int):
+    def __init__(self, impl, group, device: torch.device, channels: int, transport: str = "rccl"):
         self.impl = impl
         self.group = group
         self.device = device
         self.channels = channels
+        self.transport = transport
 
     @classmethod
     def create(cls, group=None, device: Optional[torch.device] = None, channels: int = 0,
-               local_size: Optional[int] = None, accum_fp32: Optional[bool] = None) -> "NativeEngine":
+               local_size: Optional[int] = None, accum_fp32: Optional[bool] = None,
+               transport: str = "rccl") -> "NativeEngine":
         """``local_size``: ranks per node for the 2-step algorithms (default ``LOCAL_WORLD_SIZE`` or
-        the group size); ``accum_fp32``: reduce bf16 buckets in fp32 (default: on when n > 1)."""
+        the group size); ``accum_fp32``: reduce bf16 buckets in fp32 (default: on when n > 1).
+
+        ``transport``: ``rccl`` builds the RCCL communicator (``ipc_*`` algorithm names still run
+        over peer-mapped windows, mapped on first use); ``ipc`` builds no communicator and runs every
+        algorithm over the windows -- several ranks on ONE GPU, which RCCL refuses."""
         C = _ext.require()
+        if transport not in ("rccl", "ipc"):
+            raise ValueError(f"transport must be 'rccl' or 'ipc', got {transport!r}")
         group = group if group is not None else dist.group.WORLD
         ranks = dist.get_process_group_ranks(group) if group is not dist.group.WORLD else list(
             range(dist.get_world_size()))
@@ -96,17 +125,49 @@ class NativeEngine:
         me = ranks.index(dist.get_rank())
         device = device or torch.device("cuda", torch.cuda.current_device())
         topo = topology(n, channels, local_size)
-        obj: List[object] = [C.CommEngine.get_unique_id() if me == 0 else None]
-        dist.broadcast_object_list(obj, src=ranks[0], group=group)
-        impl = C.CommEngine(me, n, obj[0], device.index, topo["rings"], topo["local_size"], topo["local_rings"],
+        if transport == "rccl":
+            obj: List[object] = [C.CommEngine.get_unique_id() if me == 0 else None]
+            dist.broadcast_object_list(obj, src=ranks[0], group=group)
+            uid = obj[0]
+        else:
+            uid = b""
+        impl = C.CommEngine(me, n, uid, device.index, topo["rings"], topo["local_size"], topo["local_rings"],
                             topo["node_rings"])
         impl.set_accum_fp32(n > 1 if accum_fp32 is None else bool(accum_fp32))
-        return cls(impl, group, device, len(topo["rings"]))
+        return cls(impl, group, device, len(topo["rings"]), transport)
 
     # -- setup -------------------------------------------------------------------------------
+    def uses_ipc(self, algo: str) -> bool:
+        return self.transport == "ipc" or parse_algo(algo)[2]
+
     def reserve(self, algo: str, sizes, dtype: torch.dtype) -> None:
-        """Pre-build the plans of these bucket sizes and size the scratch buffer once."""
+        """Pre-build the plans of these bucket sizes and size the scratch buffer once (IPC
+        algorithms: grow and map every rank's window, a collective call)."""
         self.impl.reserve(algo_code(algo), [int(s) for s in sizes], 1 if dtype == torch.bfloat16 else 0)
+        if self.uses_ipc(algo):
+            self._map_windows()
+
+    def _map_windows(self) -> None:
+        """Collective: every rank calls it at the same point (the need is deterministic, so all
+        ranks agree on whether to grow; it is all-gathered anyway)."""
+        need = int(self.impl.ipc_need())
+        world = self.impl.world()
+        needs: List[object] = [None] * world
+        dist.all_gather_object(needs, need, group=self.group)
+        need = max(int(x) for x in needs)
+        if need <= int(self.impl.ipc_capacity()):
+            return
+        self.impl.synchronize()  # nothing of mine in flight reads a peer window
+        dist.barrier(group=self.group)  # ... nor of any peer's that reads mine
+        handle = self.impl.ipc_alloc(int(need * 1.25) + (1 << 20))
+        handles: List[object] = [None] * world
+        dist.all_gather_object(handles, handle, group=self.group)
+        self.impl.ipc_open(handles)
+        dist.barrier(group=self.group)
+
+    def _lazy_reserve(self, algo: str, flat: torch.Tensor) -> None:
+        if self.uses_ipc(algo) and self.impl.world() > 1:
+            self.reserve(algo, [flat.numel()], flat.dtype)
 
     def set_accum_fp32(self, on: bool) -> None:
         self.impl.set_accum_fp32(bool(on))
@@ -122,10 +183,12 @@ class NativeEngine:
 
     # -- collectives -------------------------------------------------------------------------
     def allreduce(self, flat: torch.Tensor, algo: str = "builtin", average: bool = True) -> None:
+        self._lazy_reserve(algo, flat)
         self.impl.allreduce(flat, algo_code(algo), average)
 
     def bucket_allreduce(self, flat: torch.Tensor, algo: str, average: bool = True, table=None,
                          pack_scale: float = 1.0, unpack_scale: float = 1.0) -> None:
+        self._lazy_reserve(algo, flat)
         self.impl.bucket_allreduce(flat, algo_code(algo), average, table, pack_scale, unpack_scale)
 
     def bucket_allreduce_list(self, flat: torch.Tensor, algo: str, grads, offsets, average: bool = True) -> None:

@@ -183,6 +183,12 @@ class NativeStreamExecutor(Executor):
         # full gather/reduce/re-point path with passthrough=False)
         self.passthrough = (engine.impl.world() == 1) if passthrough is None else passthrough
         self._join: dict = {}
+        # bucket index -> algorithm (parallel/autotune.py: the fastest verified one for that bucket's
+        # size); identical on every rank, so the collective sequences still match
+        self.per_bucket: dict = {}
+
+    def algorithm_for(self, b: Bucket) -> str:
+        return self.per_bucket.get(b.index, self.algorithm)
 
     def submit(self, b: Bucket) -> None:
         if self.passthrough:
@@ -202,24 +208,26 @@ class NativeStreamExecutor(Executor):
         self._submit(b)
 
     def _submit(self, b: Bucket) -> None:
+        algo = self.algorithm_for(b)
         stolen = getattr(b, "stolen", None)
         if stolen is not None:
-            self.engine.bucket_allreduce_list(b.flat, self.algorithm, [g for g, _ in stolen], [o for _, o in stolen])
+            self.engine.bucket_allreduce_list(b.flat, algo, [g for g, _ in stolen], [o for _, o in stolen])
             return
         table = None if b.views else b.pack_table
         if not b.views and table is None:
             raise RuntimeError("native executor needs grad-as-bucket-view or a native PackTable")
-        self.engine.bucket_allreduce(b.flat, self.algorithm, True, table)
+        self.engine.bucket_allreduce(b.flat, algo, True, table)
 
     def reserve(self, buckets) -> None:
-        """Build the engine's plans and size its scratch for these buckets once, at setup."""
+        """Build the engine's plans and size its scratch / IPC windows for these buckets once, at
+        setup (collective for IPC algorithms: every rank calls it in the same order)."""
         if self.passthrough:
             return
-        by_dtype = {}
+        groups = {}
         for b in buckets:
-            by_dtype.setdefault(b.flat.dtype, []).append(b.flat.numel())
-        for dt, sizes in by_dtype.items():
-            self.engine.reserve(self.algorithm, sizes, dt)
+            groups.setdefault((self.algorithm_for(b), b.flat.dtype), []).append(b.flat.numel())
+        for (algo, dt), sizes in sorted(groups.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
+            self.engine.reserve(algo, sizes, dt)
 
     def finish(self) -> None:
         self.engine.wait_on_current()

@@ -128,17 +128,21 @@ class NativeReducer(Reducer):
         self.engine.wait_on_current()
 
 
-def make_reducer(kind: str = "immediate", algorithm: str = "ring", *, channels: int = 1, native: bool = False,
-                 engine=None, local_size: Optional[int] = None, group=None) -> Reducer:
-    """Factory used by the experiment runners and the public API."""
+def make_reducer(kind: str = "immediate", algorithm: str = "ring", *, channels: Optional[int] = None,
+                 native: bool = False, engine=None, local_size: Optional[int] = None, group=None) -> Reducer:
+    """Factory used by the experiment runners and the public API.
+
+    ``channels``: ring channels. ``None`` = the default (native engine: one ring per outgoing xGMI
+    link, i.e. n - 1; Python rings: 1); an explicit count, including 1, is passed through."""
     if native:
         if engine is None:
             from .context import get_context
 
-            engine = get_context().engine(local_size=local_size, channels=channels if channels > 1 else 0)
+            engine = get_context().engine(local_size=local_size, channels=channels or 0)
         return NativeReducer(engine, algorithm)
+    ch = 1 if channels is None else int(channels)
     if kind in ("immediate", "1step", "onestep"):
-        return ImmediateReducer(algorithm, group, channels)
+        return ImmediateReducer(algorithm, group, ch)
     if kind in ("hierarchical", "node", "2step", "twostep"):
-        return HierarchicalReducer(local_size, algorithm, channels)
+        return HierarchicalReducer(local_size, algorithm, ch)
     raise ValueError(f"unknown reducer kind {kind!r}")

@@ -39,6 +39,20 @@ def virtual_allreduce(bufs: Sequence[torch.Tensor], algorithm: str = "ring", ave
                         topo["local_rings"], topo["node_rings"], bool(accum_fp32))
 
 
+def ipc_host_allreduce(bufs: Sequence[torch.Tensor], algorithm: str = "ring", average: bool = True,
+                       channels: int = 0, local_size: Optional[int] = None, accum_fp32: bool = False,
+                       timeout_s: float = 30.0) -> None:
+    """All-reduce host ``bufs`` with the IPC transport's protocol (csrc/comm/ipc.h): one thread per
+    rank, each pulling from the peers' windows between flag barriers, exactly the schedule matching
+    and barrier sequence the GPU transport issues -- checked here under real concurrency. A
+    protocol bug surfaces as a wrong result or a barrier timeout, never a hang."""
+    C = _ext.require()
+    n = len(bufs)
+    topo = topology(n, channels, local_size if local_size is not None else n)
+    C.ipc_host_allreduce(list(bufs), algo_code(algorithm), bool(average), topo["rings"], topo["local_size"],
+                         topo["local_rings"], topo["node_rings"], bool(accum_fp32), float(timeout_s))
+
+
 def plan_text(algorithm: str, rank: int, world: int, n: int, channels: int = 0,
               local_size: Optional[int] = None, average: bool = True) -> str:
     """The schedule rank ``rank`` of ``world`` runs for an ``n``-element all-reduce (debugging)."""

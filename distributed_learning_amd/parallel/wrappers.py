@@ -44,9 +44,15 @@ def broadcast_module(module: nn.Module, root: int = 0, group=None) -> None:
     by_key = {}
     for t in tensors:
         by_key.setdefault((t.dtype, t.device), []).append(t)
+    host_staged = dist.get_backend(group) == "gloo"  # Gloo ranks sharing one GPU: move through the host
     for _, ts in by_key.items():
         flat = torch.cat([t.detach().reshape(-1) for t in ts])
-        dist.broadcast(flat, src=root, group=group)
+        if host_staged and flat.is_cuda:
+            buf = flat.cpu()
+            dist.broadcast(buf, src=root, group=group)
+            flat.copy_(buf)
+        else:
+            dist.broadcast(flat, src=root, group=group)
         off = 0
         with torch.no_grad():
             for t in ts:
@@ -188,6 +194,13 @@ class TorchDDP(_DPBase):
                  find_unused_parameters: bool = True, gradient_as_bucket_view: bool = True):
         super().__init__(model, broadcast=False)
         dev = next(model.parameters()).device
+        # DDP's reducer hooks copy gradients into its buckets inside backward, on the compute stream,
+        # without joining the late weight-gradient side stream (ops/conv.py WGRAD_DEFER): no deferral
+        # while a DDP wrapper lives
+        from ..ops import conv as _conv
+
+        _conv.block_deferral()
+        self._blocks_deferral = True
         self.ddp = nn.parallel.DistributedDataParallel(
             model, device_ids=[dev.index] if dev.type == "cuda" else None,
             bucket_cap_mb=max(grouping_size, 1) / 1024 / 1024, find_unused_parameters=find_unused_parameters,
@@ -195,6 +208,13 @@ class TorchDDP(_DPBase):
 
     def forward(self, *args, **kw):
         return self.ddp(*args, **kw)
+
+    def cleanup(self) -> None:
+        if getattr(self, "_blocks_deferral", False):
+            from ..ops import conv as _conv
+
+            _conv.unblock_deferral()
+            self._blocks_deferral = False
 
 
 # Reference class names

@@ -1,0 +1,109 @@
+"""In-run all-reduce selection (parallel/autotune.py) on Gloo CPU ranks with a stand-in engine.
+
+The stand-in has the NativeEngine surface the autotuner uses (reserve / allreduce / synchronize /
+comm-stream timers) over ``dist.all_reduce``; its algorithms differ in a simulated per-call cost
+that is rank-dependent (the table must take the MAX over ranks), one of them returns wrong numbers
+(verification must exclude it) and one cannot be set up on one rank (setup failures must be agreed
+on before anything is timed). Checked: identical decisions on every rank, the per-size choice, the
+alpha/beta fit and the cap derivation. The GPU twin is tests/test_gpu_multiproc.py.
+"""
+import torch
+import torch.distributed as dist
+
+from distributed_learning_amd.parallel import autotune as at
+import dist_util
+
+COST_US = {"fast_small": (5.0, 0.004), "fast_large": (60.0, 0.0005), "broken": (1.0, 0.0001),
+           "unmappable": (1.0, 0.0001)}  # (alpha us, us per KiB)
+
+
+class _Impl:
+    def __init__(self, rank, world):
+        self._r, self._w = rank, world
+
+    def world(self):
+        return self._w
+
+    def rank(self):
+        return self._r
+
+    def accum_fp32(self):
+        return True
+
+
+class FakeEngine:
+    def __init__(self, rank, world):
+        self.impl = _Impl(rank, world)
+        self.group = dist.group.WORLD
+        self.device = torch.device("cpu")
+        self.transport = "rccl"
+        self._t = 0.0
+        self._timing = False
+
+    def reserve(self, algo, sizes, dtype):
+        if algo == "unmappable" and self.impl.rank() == 1:
+            raise RuntimeError("cannot map peer memory")
+
+    def allreduce(self, buf, algo, average=True):
+        dist.all_reduce(buf)
+        if average:
+            buf /= self.impl.world()
+        if algo == "broken":
+            buf += 1
+        a, b = COST_US[algo]
+        ms = (a + b * buf.numel() * buf.element_size() / 1024) * 1e-3 * (1 + 0.5 * self.impl.rank())
+        if self._timing:
+            self._t += ms
+
+    def synchronize(self):
+        pass
+
+    def set_timing(self, on):
+        self._timing = on
+
+    def consume_comm_ms(self):
+        t, self._t = self._t, 0.0
+        return t
+
+
+def _tune(rank, world):
+    eng = FakeEngine(rank, world)
+    t = at.Autotune(eng, torch.float32, list(COST_US), reps=2, warmup=1)
+    at.GRID_MIB = (0.25, 1.0, 4.0)
+    t.run_grid()
+    small, large = 1024, 4 << 20
+    per = t.run_buckets([small, large, small])
+    return {"ok": t.ok, "per": per, "best": t.best_model()[0], "report": t.report(),
+            "grid": t.grid_table}
+
+
+def test_autotune_consistent_verified_and_fastest():
+    res = dist_util.run(_tune, 2)
+    a, b = res
+    assert a["per"] == b["per"] and a["best"] == b["best"] and a["ok"] == b["ok"]
+    assert a["ok"]["broken"] is False and a["ok"]["unmappable"] is False
+    assert a["ok"]["fast_small"] and a["ok"]["fast_large"]
+    assert a["per"][1024] == "fast_small"
+    assert a["per"][4 << 20] == "fast_large"
+    # the table is the max over ranks: rank 1's simulated costs are 1.5x rank 0's
+    row = a["grid"]["fast_small"]
+    n = min(row)
+    alpha, beta = COST_US["fast_small"]
+    want = (alpha + beta * n * 4 / 1024) * 1e-3 * 1.5
+    assert abs(row[n] - want) / want < 1e-6
+    fit = a["report"]["fit"]["fast_large"]
+    assert abs(fit["alpha_us"] - 60.0 * 1.5) < 1.0
+
+
+def test_fit_recovers_alpha_beta():
+    row = {n: (10.0 + 2e-6 * n * 4) for n in (1000, 10_000, 100_000)}  # ms
+    m = at.fit(row, 4)
+    assert abs(m.alpha_s - 10e-3) < 1e-9
+    assert abs(m.beta_s_per_byte - 2e-9) < 1e-15
+
+
+def test_candidates():
+    c8 = at.candidates(8, "rccl")
+    assert "builtin" in c8 and "ring:7" in c8 and "ipc_direct" in c8
+    assert "ring:7" not in at.candidates(4, "rccl")
+    assert all(not x.startswith("ipc_") for x in at.candidates(2, "ipc"))

@@ -112,3 +112,76 @@ def test_deferred_wgrad_through_dp_hooks(native):
     ctxmod.shutdown()
     for i, (a, b) in enumerate(zip(results[1], results[0])):
         assert torch.equal(a, b), f"parameter {i}: gradient after the collective differs"
+
+
+def test_torch_ddp_blocks_deferral(native):
+    """torch DDP copies gradients into its buckets inside backward without joining the side stream
+    (ADVICE r3): while a TorchDDP wrapper lives no weight gradient is deferred, so its all-reduced
+    gradients equal the inline ones bit for bit."""
+    from distributed_learning_amd.ops import conv
+    from distributed_learning_amd.ops.loss import cross_entropy
+    from distributed_learning_amd.parallel import context as ctxmod
+    from distributed_learning_amd.parallel.wrappers import TorchDDP
+
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    os.environ.setdefault("LOCAL_RANK", "0")
+    ctxmod.init(backend="nccl")
+    ref = _grads(_model(), "0", "end")
+    old = conv.WGRAD_DEFER
+    conv.WGRAD_DEFER = "all"
+    base = _model()
+    ddp = TorchDDP(base, grouping_size=8 << 20, find_unused_parameters=False)
+    try:
+        assert conv._DEFER_BLOCKS[0] > 0
+        g = torch.Generator().manual_seed(5)
+        x = torch.rand(16, 3, 224, 224, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (16,), generator=g).to(DEV)
+        cross_entropy(ddp(x), y).backward()
+        torch.cuda.synchronize()
+        got = [p.grad.detach().clone() for p in base.parameters()]
+    finally:
+        conv.WGRAD_DEFER = old
+        ddp.cleanup()
+        ctxmod.shutdown()
+    assert conv._DEFER_BLOCKS[0] == 0
+    for i, (a, b) in enumerate(zip(got, ref)):
+        assert torch.equal(a, b), f"parameter {i}: DDP gradient differs from the inline one"
+
+
+def test_shared_weight_deferred_once(native):
+    """A conv weight used twice in one graph is deferred at most once: the second use
+    joins the first and runs inline, so autograd's sum of the two is taken over finished tensors."""
+    import torch.nn as nn
+
+    from distributed_learning_amd.ops import conv
+    from distributed_learning_amd.ops import nn as dnn
+
+    torch.manual_seed(3)
+
+    class Twice(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.c = nn.Conv2d(64, 64, 3, padding=1, bias=False)
+
+        def forward(self, x):
+            y, _ = conv.conv3x3(x, self.c)
+            y, _ = conv.conv3x3(torch.relu(y), self.c)
+            return y
+
+    def run(defer):
+        torch.manual_seed(3)
+        m = Twice().to(DEV).to(memory_format=torch.channels_last)
+        dnn.bf16_weights(m)
+        x = torch.randn(8, 64, 56, 56, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        old = conv.WGRAD_DEFER
+        conv.WGRAD_DEFER = defer
+        try:
+            m(x).float().square().mean().backward()
+            assert not conv.side_pending(DEV)
+            torch.cuda.synchronize()
+            return m.c.weight.grad.detach().clone()
+        finally:
+            conv.WGRAD_DEFER = old
+
+    assert torch.equal(run("all"), run("0"))
