@@ -39,6 +39,7 @@ import torch.distributed as dist  # noqa: E402
 sys.path.insert(0, _ROOT)
 
 import distributed_learning_amd as dla  # noqa: E402
+from distributed_learning_amd import knobs  # noqa: E402
 from distributed_learning_amd.data import SyntheticBatches  # noqa: E402
 from distributed_learning_amd.models import get_spec  # noqa: E402
 from distributed_learning_amd.ops import nn as dnn  # noqa: E402
@@ -88,13 +89,21 @@ def parse():
     ap.add_argument("--fail_rank", type=int, default=-1,
                     help="fault injection: this rank exits (status 17) after the forward of step --fail_step")
     ap.add_argument("--fail_step", type=int, default=1)
-    ap.add_argument("--kernels", default=os.environ.get("DLA_KERNELS", "native"), choices=["torch", "native"])
-    ap.add_argument("--precision", default=os.environ.get("DLA_PRECISION", "bf16"), choices=["autocast", "bf16"],
-                    help="autocast: fp32 params + bf16 autocast; bf16: bf16 weights + fp32 master weights in the "
-                         "fused optimizer (no per-step weight casts, bf16 gradients on the wire)")
-    ap.add_argument("--conv", default=os.environ.get("DLA_CONV", "native"), choices=["miopen", "native"],
+    ap.add_argument("--bucket_mb_sweep", default=None,
+                    help="comma list of bucket caps (MiB, 0 = per tensor): time K steps at each and report one line "
+                         "with the sub-table (the reference's fusion_experiment sweep)")
+    ap.add_argument("--phases", type=int, default=0,
+                    help="N > 0: after the timed region, N more steps with per-phase device timers; the record gets "
+                         "the reference's latency-breakdown columns (get_data ... optimizer_step, batch)")
+    ap.add_argument("--phases_csv", default=None, help="also write those rows as a reference-schema times.csv")
+    ap.add_argument("--kernels", default=knobs.get("KERNELS"), choices=["torch", "native"])
+    ap.add_argument("--precision", default=knobs.get("PRECISION"), choices=["autocast", "bf16", "fp32"],
+                    help="bf16: bf16 weights + fp32 master weights in the fused optimizer (no per-step weight casts, "
+                         "bf16 gradients on the wire); autocast: fp32 params + bf16 autocast; fp32: the reference's "
+                         "precision (fp32 weights and activations, NCHW, MIOpen / torch kernels)")
+    ap.add_argument("--conv", default=knobs.get("CONV"), choices=["miopen", "native"],
                     help="1x1 convolutions on the native MFMA GEMMs (with fused BN statistics) or MIOpen")
-    ap.add_argument("--graph", default=os.environ.get("DLA_GRAPH", "off"), choices=["on", "off"],
+    ap.add_argument("--graph", default=knobs.get("GRAPH"), choices=["on", "off"],
                     help="capture the whole training step (data, fwd, bwd, collectives, optimizer) in a HIP graph")
     ap.add_argument("--force_comm", type=int, default=0,
                     help="1 = run the multi-rank gradient path (gather -> RCCL all-reduce -> re-point) even at "
@@ -171,6 +180,107 @@ def dry_run(a) -> None:
     dist.destroy_process_group()
 
 
+PHASES = ("get_data", "data2dev", "zero_grad", "forward", "backprop", "sync", "optimizer_step")
+
+
+def build_dp(model, reducer, cap_mb: float, dev, a, tune, world):
+    """Wrap ``model`` for data parallelism at bucket cap ``cap_mb`` (0 = one bucket per tensor, the
+    reference's fusion-off mode); per-bucket algorithms from the autotuner; plans / windows reserved."""
+    dp = PipelinedFusedDP(model, reducer, int(cap_mb * 1024 * 1024), dev)
+    if a.force_comm and world == 1:
+        from distributed_learning_amd.parallel.executor import NativeStreamExecutor
+
+        dp.sync.executor = NativeStreamExecutor(reducer.engine, reducer.algorithm, passthrough=False)
+        dp.sync.passthrough = False
+    if tune is not None:
+        per_size = tune.run_buckets([b.flat.numel() for b in dp.sync.buckets])
+        dp.sync.executor.per_bucket = {b.index: per_size[b.flat.numel()] for b in dp.sync.buckets}
+    if world > 1 or a.force_comm:
+        dp.sync.executor.reserve(dp.sync.buckets)
+    return dp
+
+
+def time_steps(step, a, dev, engine, graphed, backend):
+    """W warmup steps, then exactly K timed steps between barrier + synchronize on both sides; the
+    elapsed time is the MAX over ranks."""
+    tele = {"before_warmup": telemetry.sample(dev.index or 0)}
+    # one event per step boundary (warmup and timed): the per-step GPU-stream time distribution goes into
+    # the record, so a slow first-steps ramp and a uniformly slow box can be told apart
+    wev = [torch.cuda.Event(enable_timing=True) for _ in range(a.warmup + 1)]
+    wev[0].record()
+    for i in range(a.warmup):
+        step()
+        wev[i + 1].record()
+    torch.cuda.synchronize()
+    engine.consume_comm_ms()
+    engine.set_timing(not graphed)
+    tele["before_timed"] = telemetry.sample(dev.index or 0)
+    tev = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tev[0].record()
+    loss = None
+    for i in range(a.steps):
+        loss = step()
+        tev[i + 1].record()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    tele["after_timed"] = telemetry.sample(dev.index or 0)
+    comm_ms = engine.consume_comm_ms() / max(1, a.steps)
+    engine.set_timing(False)
+    t = torch.tensor([elapsed, comm_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    step_ms = [tev[i].elapsed_time(tev[i + 1]) for i in range(a.steps)]
+    srt = sorted(step_ms)
+    return {"elapsed": float(t[0]), "comm_ms": float(t[1]), "loss": loss, "tele": tele,
+            "warm_ms": [round(wev[i].elapsed_time(wev[i + 1]), 2) for i in range(a.warmup)],
+            "step_ms": {"p50": round(srt[len(srt) // 2], 3), "min": round(srt[0], 3), "max": round(srt[-1], 3),
+                        "seq": [round(x, 2) for x in step_ms] if a.steps <= 200 else None}}
+
+
+def phase_breakdown(parts, n: int, csv_path=None, name="bench"):
+    """Per-phase device time (HIP events, no host sync inside the step) over ``n`` steps, in the
+    reference's times.csv columns (/root/reference/src/timing.py:28-40, main.py:54-97)."""
+    from distributed_learning_amd.timing import EventTimers
+
+    et = EventTimers()
+    data, opt, model, fwd_loss = parts
+    for i in range(n):
+        et.start("batch")
+        et.start("get_data")
+        x, y = data.next()
+        et.end("get_data")
+        et.start("data2dev")  # synthetic batches are generated on the device: nothing to copy
+        et.end("data2dev")
+        et.start("zero_grad")
+        opt.zero_grad(set_to_none=True)
+        et.end("zero_grad")
+        et.start("forward")
+        loss = fwd_loss(x, y)
+        et.end("forward")
+        et.start("backprop")
+        loss.backward()
+        et.end("backprop")
+        et.start("sync")
+        model.sync_gradients()
+        et.end("sync")
+        et.start("optimizer_step")
+        opt.step()
+        et.end("optimizer_step")
+        et.end("batch")
+        et.end_experiment(name, {"batch_count": i, "data_len": x.shape[0]})
+    torch.cuda.synchronize()
+    et._resolve()
+    rows = [r for _, r in et.collected]
+    mean = {k: round(sum(r[k] for r in rows) / len(rows), 3) for k in PHASES + ("batch",)}
+    if csv_path:
+        et.writeout(csv_path)
+    return mean
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ:
@@ -184,16 +294,19 @@ def main():
     if a.gpus != int(os.environ["WORLD_SIZE"]):
         print(f"error: --gpus {a.gpus} but WORLD_SIZE {os.environ['WORLD_SIZE']}", file=sys.stderr, flush=True)
         sys.exit(2)
-    same = bool(a.same_device) or os.environ.get("DLA_SAME_DEVICE") == "1"
+    same = bool(a.same_device) or os.environ.get(knobs.env_name("SAME_DEVICE")) == "1"
     if a.gpus > torch.cuda.device_count() and not same:
         print(f"error: --gpus {a.gpus} but this node has {torch.cuda.device_count()} GPU(s)", file=sys.stderr, flush=True)
         sys.exit(2)
     c = ctxmod.init(backend="gloo" if same else "nccl", same_device=same, transport=a.transport)
     world, rank = c.world_size, c.rank
     dev = c.device
-    torch.backends.cudnn.benchmark = True
-    dnn.set_backend(a.kernels)
-    dnn.set_native_conv(a.conv == "native")
+    fp32 = a.precision == "fp32"
+    bf16 = a.precision == "bf16"
+    # the native kernels are bf16 kernels; the fp32 reference-precision path keeps NCHW on MIOpen / torch
+    torch.backends.cudnn.benchmark = not fp32
+    dnn.set_backend("torch" if fp32 else a.kernels)
+    dnn.set_native_conv(a.conv == "native" and not fp32)
     if a.wgrad_overlap_rows is not None:
         from distributed_learning_amd.ops import conv as nconv
 
@@ -201,22 +314,24 @@ def main():
 
     spec = get_spec(a.model)
     torch.manual_seed(1234)
-    model = spec.build().to(dev).to(memory_format=torch.channels_last)
-    bf16 = a.precision == "bf16"
+    base = spec.build().to(dev)
+    if not fp32:
+        base = base.to(memory_format=torch.channels_last)
     if bf16:
-        dnn.bf16_weights(model)
+        dnn.bf16_weights(base)
     tune = None
     comm_active = world > 1 or bool(a.force_comm)
     base_algo = "builtin" if a.algorithm == "auto" else a.algorithm
     reducer = make_reducer("immediate", base_algo, native=True)
+    engine = reducer.engine
     if a.force_comm and world == 1:
-        reducer.engine.impl.set_force(True)  # the N>1 data path incl. fp32 staging, as a 1-rank collective
-        reducer.engine.set_accum_fp32(True)
+        engine.impl.set_force(True)  # the N>1 data path incl. fp32 staging, as a 1-rank collective
+        engine.set_accum_fp32(True)
+    grad_dtype = torch.bfloat16 if bf16 else torch.float32
     if a.algorithm == "auto" and comm_active:
         from distributed_learning_amd.parallel import autotune as at
 
-        tune = at.Autotune(reducer.engine, torch.bfloat16 if bf16 else torch.float32,
-                           at.candidates(world, reducer.engine.transport))
+        tune = at.Autotune(engine, grad_dtype, at.candidates(world, engine.transport))
         tune.run_grid()
         base_algo = tune.best_model()[0]
         reducer.algorithm = base_algo
@@ -228,35 +343,28 @@ def main():
         else:
             a.bucket_mb = 8.0
     a.bucket_mb = float(a.bucket_mb)
-    model = PipelinedFusedDP(model, reducer, int(a.bucket_mb * 1024 * 1024), dev)
-    if a.force_comm and world == 1:
-        from distributed_learning_amd.parallel.executor import NativeStreamExecutor
-
-        model.sync.executor = NativeStreamExecutor(reducer.engine, base_algo, passthrough=False)
-        model.sync.passthrough = False
-    if tune is not None:
-        per_size = tune.run_buckets([b.flat.numel() for b in model.sync.buckets])
-        model.sync.executor.per_bucket = {b.index: per_size[b.flat.numel()] for b in model.sync.buckets}
-    if comm_active:
-        model.sync.executor.reserve(model.sync.buckets)
-    opt = FusedSGD(model.module.parameters(), lr=a.lr, momentum=a.momentum, master_weights=bf16)
+    sweep = [float(v) for v in a.bucket_mb_sweep.split(",")] if a.bucket_mb_sweep else None
+    model = build_dp(base, reducer, sweep[0] if sweep else a.bucket_mb, dev, a, tune, world)
+    opt = FusedSGD(base.parameters(), lr=a.lr, momentum=a.momentum, master_weights=bf16)
     data = SyntheticBatches(a.batch, spec.input_shape, spec.num_classes, dev,
                             dtype=torch.bfloat16 if bf16 else torch.float32,
-                            seed=1234, rank=rank, channels_last=True, device_step=a.graph == "on")
-    engine = reducer.engine
-
+                            seed=1234, rank=rank, channels_last=not fp32, device_step=a.graph == "on")
     nstep = [0]
 
-    def step():
-        x, y = data.next()
-        opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=not bf16):
+    def fwd_loss(x, y):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.precision == "autocast"):
             out = model(x)
             loss = cross_entropy(out, y)
         nstep[0] += 1
         if rank == a.fail_rank and nstep[0] == a.fail_step:
             print(f"rank {rank}: injected failure after the forward of step {nstep[0]}", file=sys.stderr, flush=True)
             os._exit(17)
+        return loss
+
+    def step():
+        x, y = data.next()
+        opt.zero_grad(set_to_none=True)
+        loss = fwd_loss(x, y)
         loss.backward()
         model.sync_gradients()
         opt.step()
@@ -264,6 +372,7 @@ def main():
 
     graphed = a.graph == "on"
     comm_ms_eager = None
+    run_step = step
     if graphed:
         from distributed_learning_amd.parallel.graphs import GraphedStep
 
@@ -278,49 +387,44 @@ def main():
         torch.cuda.synchronize()
         engine.set_timing(False)
         comm_ms_eager = engine.consume_comm_ms()
-        step = GraphedStep(step, warmup=2, device=dev)
-    tele = {"before_warmup": telemetry.sample(dev.index or 0)}
-    # one event per step boundary (warmup and timed): the per-step GPU-stream time distribution goes into
-    # the record, so a slow first-steps ramp and a uniformly slow box can be told apart
-    wev = [torch.cuda.Event(enable_timing=True) for _ in range(a.warmup + 1)]
-    wev[0].record()
-    for i in range(a.warmup):
-        step()
-        wev[i + 1].record()
-    torch.cuda.synchronize()
-    engine.consume_comm_ms()
-    engine.set_timing(not graphed)
+        run_step = GraphedStep(step, warmup=2, device=dev)
+
+    sweep_rows = []
+    if sweep:
+        for cap in sweep:
+            if cap != sweep[0]:
+                model.cleanup()
+                model = build_dp(base, reducer, cap, dev, a, tune, world)
+            gs = model.sync
+            gs.hook_s, gs.hook_calls = 0.0, 0
+            r = time_steps(step, a, dev, engine, False, c.backend)
+            sweep_rows.append({"bucket_mb": cap, "buckets": len(gs.buckets),
+                               "ms_per_step": round(r["elapsed"] / a.steps * 1000.0, 3),
+                               "img_s": round(a.batch * world * a.steps / r["elapsed"], 2),
+                               "allreduce_ms_per_step": round(r["comm_ms"], 3),
+                               "hook_calls_per_step": gs.hook_calls / a.steps,
+                               "step_ms_p50": r["step_ms"]["p50"]})
+        best = min(sweep_rows, key=lambda x: x["ms_per_step"])
+        res = r  # telemetry / loss of the last cap's run; the line's value is the best cap's
     gsync = getattr(model, "sync", None)
     if gsync is not None:
         gsync.hook_s, gsync.hook_calls = 0.0, 0
-    tele["before_timed"] = telemetry.sample(dev.index or 0)
-    tev = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    tev[0].record()
-    for i in range(a.steps):
-        loss = step()
-        tev[i + 1].record()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    tele["after_timed"] = telemetry.sample(dev.index or 0)
-    warm_ms = [wev[i].elapsed_time(wev[i + 1]) for i in range(a.warmup)]
-    step_ms = sorted(tev[i].elapsed_time(tev[i + 1]) for i in range(a.steps))
-    step_seq = [round(tev[i].elapsed_time(tev[i + 1]), 2) for i in range(a.steps)]
-    comm_ms = engine.consume_comm_ms() / max(1, a.steps) if not graphed else comm_ms_eager
-    engine.set_timing(False)
-    t = torch.tensor([elapsed, comm_ms], dtype=torch.float64, device=dev if c.backend == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, comm_ms = float(t[0]), float(t[1])
-    final_loss = float(loss.detach().float())
+    if not sweep:
+        res = time_steps(run_step, a, dev, engine, graphed, c.backend)
+    elapsed = res["elapsed"]
+    comm_ms = res["comm_ms"] if not graphed else comm_ms_eager
+    final_loss = float(res["loss"].detach().float())
     ms = elapsed / a.steps * 1000.0
     img_s = a.batch * world * a.steps / elapsed
+    if sweep:  # the line's value is the best cap of the sweep
+        ms, img_s = best["ms_per_step"], best["img_s"]
+    phases = None
+    if a.phases > 0:  # after the timed region: per-phase device times in the reference's CSV columns
+        phases = phase_breakdown((data, opt, model, fwd_loss), a.phases,
+                                 a.phases_csv if rank == 0 else None, name=f"bench_{a.model}")
     # the reference publishes fp32 GoogLeNet numbers only: a ratio against a different model or
     # a lower precision measures nothing, so vs_baseline is null unless model and precision match
-    ref = REFERENCE_IMG_S.get(world) if (a.model.startswith("googlenet") and a.precision == "fp32") else None
+    ref = REFERENCE_IMG_S.get(world) if (a.model.startswith("googlenet") and fp32) else None
     if rank == 0:
         rec = {
             "metric": f"images/sec (whole node) {MODEL_NAMES.get(a.model, a.model)} synthetic ImageNet",
@@ -333,7 +437,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(img_s / ref, 3) if ref else None,
-            "dtype": "bf16" if (bf16 or a.precision == "autocast") else "fp32",
+            "dtype": "fp32" if fp32 else "bf16",
             "data": "synthetic (on-device Philox uniform images, random labels; random-init weights)",
             "config": {
                 "model": a.model,
@@ -344,15 +448,16 @@ def main():
                 "parallelism": f"dp{world}",
                 "allreduce": a.algorithm if tune is None else "auto:" + base_algo,
                 "bucket_mb": round(a.bucket_mb, 4),
-                "transport": reducer.engine.transport,
+                "transport": engine.transport,
                 "same_device": same,
-                "kernels": a.kernels,
+                "kernels": "torch" if fp32 else a.kernels,
                 "precision": a.precision,
-                "conv1x1": a.conv,
+                "conv1x1": "miopen" if fp32 else a.conv,
                 "hip_graph": graphed,
                 "optimizer": f"fused SGD momentum={a.momentum}" + (" (fp32 master weights)" if bf16 else " (fp32 weights)"),
                 "force_comm": bool(a.force_comm),
             },
+            "knobs": knobs.non_default(),
             "allreduce_ms_per_step": round(comm_ms, 3),
             "comm_world": int(engine.impl.world()),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
@@ -360,11 +465,15 @@ def main():
             "baseline_ref": {"value": REFERENCE_IMG_S.get(world),
                              "what": "reference best published img/s at this N (GoogLeNet fp32, P100, Gloo); "
                                      "not comparable unless model=googlenet and precision=fp32"},
-            "step_ms": {"p50": round(step_ms[len(step_ms) // 2], 3), "min": round(step_ms[0], 3),
-                        "max": round(step_ms[-1], 3), "seq": step_seq if a.steps <= 200 else None},
-            "warmup_step_ms": [round(x, 2) for x in warm_ms],
-            "telemetry": tele,
+            "step_ms": res["step_ms"],
+            "warmup_step_ms": res["warm_ms"],
+            "telemetry": res["tele"],
         }
+        if sweep:
+            rec["config"]["bucket_mb"] = best["bucket_mb"]
+            rec["bucket_sweep"] = sweep_rows
+        if phases is not None:
+            rec["latency_breakdown_ms"] = phases
         if tune is not None:
             rec["allreduce_table"] = tune.report()
             ex = model.sync.executor
@@ -373,7 +482,7 @@ def main():
             rec["hook_host_ms_per_step"] = round(gsync.hook_s * 1000.0 / a.steps, 3)
             rec["hook_calls_per_step"] = gsync.hook_calls / a.steps
         print(json.dumps(rec), flush=True)
-    prof_out = os.environ.get("DLA_TORCH_PROF")
+    prof_out = knobs.get("TORCH_PROF")
     if prof_out and rank == 0:  # diagnostics only, after the timed region: op -> kernel attribution
         from torch.profiler import ProfilerActivity, profile
 
@@ -388,9 +497,9 @@ def main():
                                                                 max_name_column_width=60, max_src_column_width=400))
     if a.check_dir:
         os.makedirs(a.check_dir, exist_ok=True)
-        names = dict((id(p), n) for n, p in model.module.named_parameters())
+        names = dict((id(p), n) for n, p in base.named_parameters())
         st = {"params": {}, "grads": {}, "masters": {}}
-        for p in model.module.parameters():
+        for p in base.parameters():
             n = names[id(p)]
             st["params"][n] = p.detach().cpu()
             if p.grad is not None:

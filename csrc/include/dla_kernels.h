@@ -273,21 +273,6 @@ bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, 
                         int M, int N, int K, float* stats, hipStream_t stream, const void* addend = nullptr,
                         int64_t ldd = 0, const uint8_t* addend_mask = nullptr);
 void set_gemm_stream(int mode);
-// Virtual conv output (gemm.hip gemm_vy_kernel): y = A * B^T (stride-1 1x1 conv, B = [N][K] weights)
-// recomputed by each consumer. mode 0 statistics partials, 1 out = relu(BN(y) + res) + ReLU bits,
-// 2 BN-backward reduce partials from dy and the bits, 3 BN-backward apply (dx). part: [gemm_vy_rows][N][2].
-int gemm_vy_rows(int M, int N);
-// Streaming form of the same passes (vy_stream.hip: weights resident in VGPRs, transposed MFMA,
-// persistent pixel streams) for K in {64, 128, 256}; partials of mode 0 / 2 are
-// [vy_stream_rows(mode, K, M, N)][N][2].
-bool vy_stream_supported(int K, int N);
-int vy_stream_streams(int64_t M, int N, int target_blocks);
-int vy_stream_rows(int mode, int K, int64_t M, int N);
-void launch_vy_stream(int mode, const void* A, int64_t lda, const void* W, int64_t M, int N, int K, const float* ws,
-                      const void* src, void* out, uint8_t* mask, float* part, hipStream_t stream);
-void launch_gemm_vy(int mode, const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K,
-                    const float* ws, const void* res, const void* dy, void* out, uint8_t* mask, float* part,
-                    hipStream_t stream);
 // BatchNorm-backward reduction fused into a bf16-output GEMM epilogue (the output is the BN's dy):
 // x = the BN input [M, N], ws = its 7N workspace, mask/mode as launch_bn_bwd (0, 1 or 2),
 // part = [stats_rows][N][2] partial (sum dy', sum dy'(x - mean)).
@@ -307,7 +292,6 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
 // out[Mo,No] (= scale * A^T B [+ out]) with A [K, lda>=Mo], B [K, ldb>=No]; partial: splits*Mo*No f32.
 int gemm_tn_splits(int Mo, int No, int K);
 bool splitk_xcd_remap();
-void set_stem_halo(int mode);  // stem forward: -1 DLA_STEM_HALO / default implicit GEMM, 0 implicit GEMM, 1 halo
 void set_tn256(int mode);  // 256x256 weight-gradient tiles: -1 DLA_TN256 / default on, 0 off, 1 on
 void set_splitk_blocks(int blocks);  // 0: DLA_SPLITK_BLOCKS / default (512)
 int splitk_target_blocks();  // split-K grids: tiles of one split co-scheduled on one XCD (DLA_SPLITK_XCD=0: off)

@@ -213,196 +213,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_sg_kernel(const float* __re
 }
 
 // ---------------------------------------------------------------------------------------------
-// "Virtual" conv output: y = A * B^T of a stride-1 1x1 conv recomputed by every consumer instead of
-// stored. A ResNet bottleneck's last conv expands P -> 4P channels (K = P), so its output y3 is 4x the
-// bytes of its input a2: the four passes that touch y3 (BN statistics, BN + residual + ReLU apply,
-// BN-backward reduce, BN-backward apply) each re-read a2 (1/4 of y3) and redo the K = P MFMA GEMM in
-// the epilogue's place, and y3 is never written or read. The recomputed tile is bit-identical in
-// every pass (same k order, same MFMAs, bf16 rounding of the accumulator), so the statistics, the
-// ReLU bits and the gradients are exactly those of the stored-y path (bn_act.hip arithmetic):
-//   kVyStats     per-column (sum, sumsq) partials of bf16(y) — gemm_nt's statistics epilogue, no store;
-//   kVyApply     out = relu(y * scale + shift + res), the 1-bit ReLU mask (bn_apply_body, kRes/kRelu);
-//   kVyBwdReduce partials (sum g, sum g (y - mean)), g = dy where the mask bit is set (kMaskBits);
-//   kVyBwdApply  dx = k1 (g - m1 - (y - mean) k2) (bn_bwd_apply_body, kMaskBits).
-// ---------------------------------------------------------------------------------------------
-enum : int { kVyStats = 0, kVyApply = 1, kVyBwdReduce = 2, kVyBwdApply = 3 };
-
-struct VyArgs {
-  const float* ws;     // the BatchNorm's 7N workspace (mean | invstd | scale | shift | k1 | m1 | k2)
-  const bf16_t* res;   // apply: residual [M][N]
-  const bf16_t* dy;    // backward: incoming gradient [M][N]
-  bf16_t* out;         // apply: activation out; backward apply: dx out
-  uint8_t* mask;       // apply: ReLU bits out; backward: in (one byte per 8 channels of a row)
-  float* part;         // statistics / backward-reduce partials [row tiles][N][2]
-};
-
-// The streamed operand (residual or dy) and the ReLU-mask bytes of this thread's epilogue rows,
-// loaded before the main loop: their HBM round trip overlaps the A-tile loads and the MFMAs instead of
-// following them (one round trip per tile instead of two).
-template <int BM, int BN, int MODE, int NT>
-struct VyPrefetch {
-  static constexpr int CPR = BN / 8;
-  static constexpr int NIT = BM * CPR / NT;
-  ushort8_t ld[NIT];
-  uint32_t mb[NIT];
-  __device__ __forceinline__ void load(int64_t M, int N, int64_t row0, int col0, const VyArgs& va) {
-    const int tid = threadIdx.x, my_cc = (tid % CPR) * 8;
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int r = (tid + it * NT) / CPR;
-      const int64_t gm = row0 + r;
-      const int gn = col0 + my_cc;
-      const bool ok = gm < M && gn < N;
-      const int64_t off = ok ? gm * N + gn : 0;
-      ld[it] = ok ? *reinterpret_cast<const ushort8_t*>((MODE == kVyApply ? va.res : va.dy) + off) : zero8();
-      mb[it] = (MODE != kVyApply && ok) ? (uint32_t)va.mask[off >> 3] : 0u;
-    }
-  }
-};
-
-template <int BM, int BN, int MODE, int NT>
-__device__ __forceinline__ void epilogue_vy(const Acc<BM, BN, NT>& acc, int64_t M, int N, int64_t row0, int col0,
-                                            int bm, const VyArgs& va, char* smem,
-                                            const VyPrefetch<BM, BN, MODE, NT>& pf) {
-  using AC = Acc<BM, BN, NT>;
-  constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
-  constexpr int LDS_C = BN + 8;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN,
-            fr = acc_col(lane);
-  bf16_t* Cs = reinterpret_cast<bf16_t*>(smem);
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < kAccN; ++r)
-        Cs[(wr * WM + i * kMS + acc_row(lane, r)) * LDS_C + wc * WN + j * kMS + fr] = f32_to_bf16(acc.v[i][j][r]);
-  __syncthreads();
-  constexpr int CPR = BN / 8;
-  constexpr int NIT = BM * CPR / NT;
-  static_assert(NT % CPR == 0 && BM * CPR % NT == 0, "whole store-loop iterations, fixed columns per thread");
-  const int my_cc = (tid % CPR) * 8;
-  float c0v[8], c1v[8], c2v[8], c3v[8];  // per-column coefficients of this thread's 8 columns
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int gc = min(col0 + my_cc + j, N - 1);
-    if constexpr (MODE == kVyApply) {
-      c0v[j] = va.ws[2 * N + gc];  // scale
-      c1v[j] = va.ws[3 * N + gc];  // shift
-    } else {
-      c0v[j] = va.ws[gc];  // mean
-      if constexpr (MODE == kVyBwdApply) {
-        c1v[j] = va.ws[4 * N + gc];  // k1
-        c2v[j] = va.ws[5 * N + gc];  // m1
-        c3v[j] = va.ws[6 * N + gc];  // k2
-      }
-    }
-  }
-  const ushort8_t* ld = pf.ld;
-  const uint32_t* mb = pf.mb;
-  float bs[8], bq[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bs[j] = bq[j] = 0.f;
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int r = (tid + it * NT) / CPR;
-    const int64_t gm = row0 + r;
-    const int gn = col0 + my_cc;
-    if (gm < M && gn < N) {
-      const int64_t off = gm * N + gn;
-      const ushort8_t v = *reinterpret_cast<const ushort8_t*>(Cs + r * LDS_C + my_cc);
-      if constexpr (MODE == kVyApply) {
-        ushort8_t o;
-        uint32_t bits = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float a = fmaf(bf16_to_f32(v[j]), c0v[j], c1v[j]);
-          a += bf16_to_f32(ld[it][j]);
-          bits |= (a > 0.f ? 1u : 0u) << j;
-          o[j] = f32_to_bf16(fmaxf(a, 0.f));
-        }
-        *reinterpret_cast<ushort8_t*>(va.out + off) = o;
-        va.mask[off >> 3] = (uint8_t)bits;
-      } else if constexpr (MODE == kVyBwdReduce) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float g = ((mb[it] >> j) & 1u) ? bf16_to_f32(ld[it][j]) : 0.f;
-          bs[j] += g;
-          bq[j] = fmaf(g, bf16_to_f32(v[j]) - c0v[j], bq[j]);
-        }
-      } else {
-        ushort8_t o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float g = ((mb[it] >> j) & 1u) ? bf16_to_f32(ld[it][j]) : 0.f;
-          o[j] = f32_to_bf16(c1v[j] * (g - c2v[j] - (bf16_to_f32(v[j]) - c0v[j]) * c3v[j]));
-        }
-        *reinterpret_cast<ushort8_t*>(va.out + off) = o;
-      }
-    }
-  }
-  if constexpr (MODE == kVyBwdReduce) {
-    __syncthreads();  // C staging no longer read: reuse it for the row-group combine
-    constexpr int RG = NT / CPR;
-    float* red = reinterpret_cast<float*>(smem);  // [RG][BN][2]
-    const int rg = tid / CPR;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      red[(rg * BN + my_cc + j) * 2 + 0] = bs[j];
-      red[(rg * BN + my_cc + j) * 2 + 1] = bq[j];
-    }
-    __syncthreads();
-    for (int idx = tid; idx < BN * 2; idx += NT) {
-      float a = 0.f;
-      for (int g = 0; g < RG; ++g) a += red[g * BN * 2 + idx];
-      const int col = idx >> 1;
-      if (col0 + col < N) va.part[((int64_t)bm * N + col0 + col) * 2 + (idx & 1)] = a;
-    }
-  }
-}
-
-template <int BM, int BN, int MODE, int PIPE, int NT>
-__global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void gemm_vy_kernel(const bf16_t* __restrict__ A, int64_t lda,
-                                                                               const bf16_t* __restrict__ B, int64_t ldb,
-                                                                               int M, int N, int K, VyArgs va) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  const int nbn = (N + BN - 1) / BN;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int bm = tile / nbn, bn = tile % nbn;
-  const int64_t row0 = (int64_t)bm * BM;
-  const int col0 = bn * BN;
-  Acc<BM, BN, NT> acc;
-  acc.zero();
-  const RowLoader<BM, NT> la{A, lda, row0, M, K};
-  const RowLoader<BN, NT> lb{B, ldb, (int64_t)col0, N, K};
-  VyPrefetch<BM, BN, MODE, NT> pf;
-  if constexpr (MODE != kVyStats) pf.load(M, N, row0, col0, va);
-  run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
-  if constexpr (MODE == kVyStats) {
-    // gemm_nt's statistics epilogue without the store: (sum, sumsq) of the bf16-rounded outputs,
-    // accumulated from the registers in the same order, then one partial row per block
-    using AC = Acc<BM, BN, NT>;
-    ColStats<BM, BN, NT> st;
-    st.zero();
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid / AC::WGN;
-#pragma unroll
-    for (int i = 0; i < AC::TM; ++i)
-#pragma unroll
-      for (int j = 0; j < AC::TN; ++j)
-#pragma unroll
-        for (int r = 0; r < kAccN; ++r) {
-          const int m = wr * AC::WM + i * kMS + acc_row(lane, r);
-          const float v = (row0 + m < M) ? bf16_to_f32(f32_to_bf16(acc.v[i][j][r])) : 0.f;
-          st.s[j] += v;
-          st.q[j] = fmaf(v, v, st.q[j]);
-        }
-    stats_flush<BM, BN, NT>(st, va.part + (int64_t)bm * N * 2, N, col0, smem_raw);
-  } else {
-    epilogue_vy<BM, BN, MODE, NT>(acc, M, N, row0, col0, bm, va, smem_raw, pf);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------------
 // MFMA main-loop pipeline (dla_mfma.h run_mainloop). -1 = per shape, from scripts/bench_gemm.py /
@@ -702,50 +512,5 @@ void launch_gemm_nt_splitk(const void* A, int64_t lda, const void* B, int64_t ld
   launch_splitk_reduce(partial, splits, (int64_t)M * N, C, kBF16, 1.f, false, stream, addend, ld_addend, N);
 }
 
-
-// Virtual-output GEMM passes (gemm_vy_kernel). Same tile / main loop for every mode so the recomputed
-// outputs are identical; rows of the partials = gemm_vy_rows(M, N).
-static int vy_tile_bm() { return 128; }
-int gemm_vy_rows(int M, int N) { return (M + vy_tile_bm() - 1) / vy_tile_bm(); }
-
-template <int BN, int MODE>
-static void launch_vy_t(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N, int K,
-                        const VyArgs& va, hipStream_t stream) {
-  constexpr int BM = 128;
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  const int pipe = mfma_pipeline() >= 0 ? mfma_pipeline() : (K > 512 ? 2 : 0);
-  if (pipe == 0) {
-    const size_t lds = std::max(run_mainloop_lds_bytes<0, BM, BN, RowLoader<BM>, RowLoader<BN>>(),
-                                epilogue_lds_bytes<BM, BN, true>());
-    hipLaunchKernelGGL((gemm_vy_kernel<BM, BN, MODE, 0, kThreads>), dim3(tiles), dim3(kThreads), lds, stream, A, lda,
-                       B, ldb, M, N, K, va);
-  } else {
-    const size_t lds = std::max(run_mainloop_lds_bytes<2, BM, BN, RowLoader<BM>, RowLoader<BN>>(),
-                                epilogue_lds_bytes<BM, BN, true>());
-    hipLaunchKernelGGL((gemm_vy_kernel<BM, BN, MODE, 2, kThreads>), dim3(tiles), dim3(kThreads), lds, stream, A, lda,
-                       B, ldb, M, N, K, va);
-  }
-}
-
-void launch_gemm_vy(int mode, const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K,
-                    const float* ws, const void* res, const void* dy, void* out, uint8_t* mask, float* part,
-                    hipStream_t stream) {
-  VyArgs va{ws, (const bf16_t*)res, (const bf16_t*)dy, (bf16_t*)out, mask, part};
-  const bf16_t* a = (const bf16_t*)A;
-  const bf16_t* b = (const bf16_t*)B;
-#define DLA_VY(BN_)                                                                   \
-  switch (mode) {                                                                     \
-    case kVyStats: launch_vy_t<BN_, kVyStats>(a, lda, b, ldb, M, N, K, va, stream); break;         \
-    case kVyApply: launch_vy_t<BN_, kVyApply>(a, lda, b, ldb, M, N, K, va, stream); break;         \
-    case kVyBwdReduce: launch_vy_t<BN_, kVyBwdReduce>(a, lda, b, ldb, M, N, K, va, stream); break; \
-    default: launch_vy_t<BN_, kVyBwdApply>(a, lda, b, ldb, M, N, K, va, stream); break;            \
-  }
-  if (N <= 64) {
-    DLA_VY(64)
-  } else {
-    DLA_VY(128)
-  }
-#undef DLA_VY
-}
 
 }  // namespace dla

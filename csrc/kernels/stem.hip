@@ -240,174 +240,9 @@ void launch_stem_fold(const void* x, void* xs, int N, int H, int W, hipStream_t 
                        g.BW);
 }
 
-// ---- halo-tiled forward (the conv_halo.hip scheme on the folded image) ----------------------------------
-// The implicit-GEMM forward gathers every folded pixel 16 times (once per tap) from L2 into LDS: 6.6 GB
-// of L2 -> LDS traffic at batch 1024 for a 0.4 GB input, which bounds it (~1.04 ms for 241 GFLOP and a
-// 1.6 GB output). Here a persistent block owns contiguous 128-pixel strips of the flat output (oh, ow
-// order); per strip the flat folded-input range [p0 - 2 BW - 2, p0 + 128 + BW + 1) -- the strip plus two
-// image rows (and two pixels) of halo before it and one after -- is DMA'd into one of two 16 KB patch
-// buffers while the previous strip is multiplied, so each input pixel crosses L2 -> LDS ~(128 + 3 BW)/128
-// times instead of 16. The A fragment of tap (th, tw) for output pixel p is patch pixel
-// p - p0 + th * BW + tw; taps outside the image are zeroed after the read. Weights [64][256] stay in LDS
-// (4 row-major 64-deep images, the rm_glds_frag swizzle); 2 x 2 waves of 64 x 32 outputs, one block per
-// CU; shared bf16 + BN-statistics epilogue (the partial row of strip s is row s, as the 128-row tiles).
-constexpr int kSHBM = 128;                 // output pixels per strip
-constexpr int kSHNT = 256;
-constexpr int kSHPatchBytes = 16384;       // >= (128 + 3 BW + 3) * 32 B for BW <= 123
-constexpr int kSHWBytes = 64 * kStemK * 2;  // 32 KB
-constexpr int kSHStageBytes = kSHBM * (64 + 8) * 2;
-constexpr int kSHLds = kSHWBytes + 2 * kSHPatchBytes + kSHStageBytes;
-// 16-byte chunk h (0 / 1) of patch pixel px is stored at (h ^ ((px >> 3) & 1)): the 16 rows of a fragment
-// read then cover all 64 banks (32-byte pixels would otherwise pair up 2-way)
-__device__ __forceinline__ int shsw(int px) { return (px >> 3) & 1; }
-
-template <bool kStats>
-__global__ __launch_bounds__(kSHNT, 1) void stem_halo_fwd_kernel(const bf16_t* __restrict__ xs,
-                                                                 const bf16_t* __restrict__ w,
-                                                                 bf16_t* __restrict__ y, int BH, int BW, int P,
-                                                                 int nstrips, int per_block,
-                                                                 float* __restrict__ stats) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  using AC = Acc<kSHBM, 64, kSHNT>;
-  static_assert(AC::TM == 4 && AC::TN == 2 && AC::WM == 64 && AC::WN == 32, "2x2 waves of 64 x 32");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave / AC::WGN, wc = wave % AC::WGN;
-  const int s_begin = blockIdx.x * per_block;
-  const int s_end = min(nstrips, s_begin + per_block);
-  if (s_begin >= s_end) return;
-
-  char* wimg = smem_raw;
-  char* patch0 = smem_raw + kSHWBytes;
-  char* stage = patch0 + 2 * kSHPatchBytes;
-  const uint32_t lds_w = lds_addr(wimg), lds_p0 = lds_addr(patch0);
-  const uint32_t wofs = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
-
-  // weights: 4 images [64 co][64 k] (k-step = filter row th), slot c of image t: row c >> 3, logical
-  // k chunk rm_glds_kc(c)
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + i * kSHNT;
-      glds16(w + (int64_t)(c >> 3) * kStemK + t * kBK + rm_glds_kc(c),
-             lds_w + (uint32_t)(t * 64 * kBK * 2 + i * kSHNT * 16) + wofs);
-    }
-
-  const int npx = kSHBM + 3 * BW + 3;  // patch pixels
-  auto issue_patch = [&](int s, int b) {
-    const int64_t q0 = (int64_t)s * kSHBM - 2 * BW - 2;
-#pragma unroll
-    for (int i = 0; i < kSHPatchBytes / (16 * kSHNT); ++i) {
-      const int c = tid + i * kSHNT;
-      const int px = c >> 1;
-      const int64_t q = q0 + px;
-      const int lc = (c & 1) ^ shsw(px);
-      const void* src = (px < npx && q >= 0 && q < P) ? (const void*)(xs + q * kStemC + lc * 8) : zero_src();
-      glds16(src, lds_p0 + (uint32_t)(b * kSHPatchBytes + i * kSHNT * 16) + wofs);
-    }
-  };
-  issue_patch(s_begin, 0);
-
-  const int g4 = lane >> 4;  // k group of the lane inside a 32-deep half: tap 2 kk + (g4 >> 1), channels (g4 & 1) * 8
-  for (int s = s_begin; s < s_end; ++s) {
-    const int b = (s - s_begin) & 1;
-    if (s == s_begin) vm_wait<0>();
-    else vm_wait<4>();  // this patch's DMA is older than the previous strip's 4 tile stores
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (s + 1 < s_end) issue_patch(s + 1, b ^ 1);  // that buffer was last read before this barrier
-
-    const int64_t row0 = (int64_t)s * kSHBM;
-    // per A fragment row: the 16-bit tap validity mask (bit th * 4 + tw) of the lane's output pixel
-    uint32_t vmask[AC::TM];
-#pragma unroll
-    for (int i = 0; i < AC::TM; ++i) {
-      const int64_t p = row0 + wr * AC::WM + i * 16 + (lane & 15);
-      const int pp = (int)(p < P ? p : 0);
-      const int q = pp / BW, ow = pp - q * BW, oh = q % BH;
-      uint32_t m = 0;
-#pragma unroll
-      for (int th = 0; th < 4; ++th)
-#pragma unroll
-        for (int tw = 0; tw < 4; ++tw)
-          if (p < P && (unsigned)(oh + th - 2) < (unsigned)BH && (unsigned)(ow + tw - 2) < (unsigned)BW)
-            m |= 1u << (th * 4 + tw);
-      vmask[i] = m;
-    }
-    const char* pbuf = patch0 + b * kSHPatchBytes;
-    AC acc;
-    acc.zero();
-#pragma unroll
-    for (int th = 0; th < 4; ++th) {
-      const bf16_t* wt = reinterpret_cast<const bf16_t*>(wimg + th * 64 * kBK * 2);
-#pragma unroll
-      for (int kk = 0; kk < kBK / kKS; ++kk) {
-        const int tw = 2 * kk + (g4 >> 1);
-        const int bit = th * 4 + tw;
-        bf16x8_t af[AC::TM], bfr[AC::TN];
-#pragma unroll
-        for (int i = 0; i < AC::TM; ++i) {
-          const int sp = wr * AC::WM + i * 16 + (lane & 15) + th * BW + tw;
-          const bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(pbuf + sp * 32 + (((g4 & 1) ^ shsw(sp)) << 4));
-          af[i] = ((vmask[i] >> bit) & 1u) ? v : bf16x8_t{};
-        }
-#pragma unroll
-        for (int j = 0; j < AC::TN; ++j) bfr[j] = rm_glds_frag(wt, wc * AC::WN + j * 16, kk);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < AC::TM; ++i)
-#pragma unroll
-          for (int j = 0; j < AC::TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
-    ColStats<kSHBM, 64, kSHNT> st;
-    st.zero();
-    epilogue_bf16<kSHBM, 64, kStats, false, kSHNT>(acc, y, 64, P, 64, row0, 0, st, nullptr, 0, stage);
-    if constexpr (kStats) stats_flush<kSHBM, 64, kSHNT>(st, stats + (int64_t)s * 64 * 2, 64, 0, stage);
-  }
-  vm_wait<0>();
-}
-
-// DLA_STEM_HALO=1: the halo-tiled forward for Cout = 64 and BW <= 123; default 0, the implicit GEMM:
-// measured slower at batch 1024 (1.48 vs 1.19 ms incl. the fold; 73.42-73.62 vs 73.18-73.42 ms/step,
-// profiles/r3/g39_stem_halo.md): one 4-wave block per CU leaves the 16-cycle MFMAs latency-bound, as for the
-// v1 3x3 halo kernel, and the implicit GEMM's 16x gather is served by L2 better than assumed.
-static int g_stem_halo = -1;
-void set_stem_halo(int mode) { g_stem_halo = mode < 0 ? -1 : (mode ? 1 : 0); }
-static bool stem_halo_on(int Cout, int BW) {
-  static const bool env = [] {
-    const char* e = std::getenv("DLA_STEM_HALO");
-    return e && e[0] == '1';
-  }();
-  const bool on = g_stem_halo < 0 ? env : g_stem_halo == 1;
-  return on && Cout == 64 && 3 * BW + 3 + kSHBM <= kSHPatchBytes / 32;
-}
-
 void launch_stem_fwd(const void* xs, const void* wpk, void* y, int N, int H, int W, int Cout, float* stats,
                      hipStream_t stream) {
   const StemGeom g = make_stem_geom(N, H, W);
-  if (stem_halo_on(Cout, g.BW)) {
-    const int P = N * g.BH * g.BW;
-    const int nstrips = (P + kSHBM - 1) / kSHBM;
-    if (nstrips == 0) return;
-    static const int cus = [] {
-      int dev = 0, n = 0;
-      hipGetDevice(&dev);
-      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-      return n > 0 ? n : 256;
-    }();
-    const int per_block = (nstrips + cus - 1) / cus;
-    const int grid = (nstrips + per_block - 1) / per_block;
-    const size_t lds = (size_t)std::max<int>(kSHLds, (int)epilogue_lds_bytes<128, 64, true>());
-    if (stats)
-      hipLaunchKernelGGL(stem_halo_fwd_kernel<true>, dim3(grid), dim3(kSHNT), lds, stream, (const bf16_t*)xs,
-                         (const bf16_t*)wpk, (bf16_t*)y, g.BH, g.BW, P, nstrips, per_block, stats);
-    else
-      hipLaunchKernelGGL(stem_halo_fwd_kernel<false>, dim3(grid), dim3(kSHNT), lds, stream, (const bf16_t*)xs,
-                         (const bf16_t*)wpk, (bf16_t*)y, g.BH, g.BW, P, nstrips, per_block, stats);
-    return;
-  }
   const int64_t P = (int64_t)N * g.BH * g.BW;
   const int tiles = (int)((P + 127) / 128) * ((Cout + 63) / 64);
   const int pipe = mfma_pipeline() >= 0 ? mfma_pipeline() : 2;

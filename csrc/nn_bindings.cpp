@@ -9,6 +9,17 @@
 
 namespace dla {
 
+// Bytes one operand spans (its last element's offset + 1): the MFMA main loops and the streaming GEMM
+// address operands through buffer descriptors whose out-of-range slots use offset 0x80000000 (kOOB,
+// dla_mfma.h), so every operand must stay below 2 GiB; beyond it they would read wrapped data.
+static void check_span(const at::Tensor& t, const char* what) {
+  int64_t last = 0;
+  for (int64_t d = 0; d < t.dim(); ++d) last += (t.size(d) - 1) * t.stride(d);
+  const int64_t bytes = t.numel() ? (last + 1) * (int64_t)t.element_size() : 0;
+  TORCH_CHECK(bytes < (int64_t(1) << 31), what, ": ", bytes,
+              " bytes reach the 2 GiB buffer-descriptor range of the native kernels (lower the per-GPU batch)");
+}
+
 static void check_act(const at::Tensor& t, const char* what) {
   TORCH_CHECK(t.is_cuda(), what, " must be a GPU tensor");
   TORCH_CHECK(t.dim() == 4 || t.dim() == 2, what, " must be NCHW-shaped (channels_last) or [M, C]");
@@ -16,6 +27,7 @@ static void check_act(const at::Tensor& t, const char* what) {
   TORCH_CHECK(ok, what, " must be channels_last (4-D) or contiguous (2-D)");
   TORCH_CHECK(t.size(1) % 8 == 0, what, ": channel count must be a multiple of 8");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, what, " must be 16-byte aligned");
+  check_span(t, what);
 }
 
 static int64_t rows_of(const at::Tensor& t) { return t.numel() / t.size(1); }
@@ -275,99 +287,8 @@ static void check_mat(const at::Tensor& t, const char* what) {
   TORCH_CHECK(t.stride(1) == 1, what, " must have unit stride in its last dim");
   TORCH_CHECK(t.size(1) % 8 == 0 && t.stride(0) % 8 == 0, what, ": rows must be multiples of 8 elements");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, what, " must be 16-byte aligned");
+  check_span(t, what);
 }
-
-// ---- virtual bottleneck output: conv3 (1x1, stride 1) + BN3 + residual + ReLU, y3 never stored ----
-// The passes run on the tiled gemm_vy_kernel; DLA_VY_STREAM=1 selects the streaming kernels
-// (vy_stream.hip) where they apply (measured slower: profiles/r3/virtual_y_ab.md).
-static int g_vy_stream = -1;  // -1: DLA_VY_STREAM (default off)
-static void set_vy_stream(bool on) { g_vy_stream = on ? 1 : 0; }
-static bool vy_use_stream(int K, int N) {
-  if (g_vy_stream < 0) {
-    const char* e = std::getenv("DLA_VY_STREAM");
-    g_vy_stream = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_vy_stream == 1 && vy_stream_supported(K, N);
-}
-static int vy_rows(int mode, int M, int N, int K) {
-  return vy_use_stream(K, N) ? vy_stream_rows(mode, K, M, N) : gemm_vy_rows(M, N);
-}
-static void vy_pass(int mode, const at::Tensor& a, const at::Tensor& w2, int M, int N, int K, const float* ws,
-                    const void* res, const void* dy, void* out, uint8_t* mask, float* part, hipStream_t st) {
-  if (vy_use_stream(K, N))
-    launch_vy_stream(mode, a.data_ptr(), a.stride(0), w2.data_ptr(), M, N, K, ws, mode == 1 ? res : dy, out, mask,
-                     part, st);
-  else
-    launch_gemm_vy(mode, a.data_ptr(), a.stride(0), w2.data_ptr(), w2.stride(0), M, N, K, ws, res, dy, out, mask,
-                   part, st);
-}
-// a: [M, K] rows of the conv input (channels_last view), w2: [N, K] bf16 weights. Forward returns
-// (out [M, N], ws [7N], mask): statistics pass -> BN finalize (running stats updated) -> apply pass
-// that recomputes y3 = a w2^T tile by tile (gemm.hip gemm_vy_kernel).
-std::vector<at::Tensor> conv_bn_res_vy_fwd(at::Tensor a, at::Tensor w2, at::Tensor residual, at::Tensor weight,
-                                           at::Tensor bias, c10::optional<at::Tensor> running_mean,
-                                           c10::optional<at::Tensor> running_var, double momentum, double eps) {
-  check_mat(a, "a");
-  check_mat(w2, "w2");
-  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && w2.scalar_type() == at::kBFloat16, "conv_bn_res_vy: bf16 operands");
-  const int M = (int)a.size(0), K = (int)a.size(1), N = (int)w2.size(0);
-  TORCH_CHECK(w2.size(1) == K && N % 8 == 0 && K % 8 == 0, "conv_bn_res_vy: w2 must be [N, K], N % 8 == 0");
-  TORCH_CHECK(residual.is_cuda() && residual.scalar_type() == at::kBFloat16 && residual.numel() == (int64_t)M * N &&
-                  (residual.dim() == 2 ? residual.is_contiguous() : residual.is_contiguous(at::MemoryFormat::ChannelsLast)),
-              "conv_bn_res_vy: residual must be the [M, N] bf16 rows (channels_last)");
-  TORCH_CHECK(weight.scalar_type() == at::kFloat && bias.scalar_type() == at::kFloat && weight.numel() == N &&
-                  bias.numel() == N,
-              "conv_bn_res_vy: fp32 BN affine parameters of N channels");
-  auto f32 = a.options().dtype(at::kFloat);
-  const int rows = vy_rows(0, M, N, K);
-  at::Tensor stats = at::empty({rows, N, 2}, f32);
-  hipStream_t st = current_stream(a);
-  vy_pass(0, a, w2, M, N, K, nullptr, nullptr, nullptr, nullptr, nullptr, stats.data_ptr<float>(), st);
-  at::Tensor ws = at::empty({7 * (int64_t)N}, f32);
-  at::Tensor part = at::empty({std::max<int64_t>(1, (int64_t)bn_fold_groups(rows) * N * 2)}, f32);
-  auto fptr = [](const c10::optional<at::Tensor>& t) -> float* {
-    return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
-  };
-  launch_bn_fwd(nullptr, nullptr, nullptr, M, N, kBF16, weight.data_ptr<float>(), bias.data_ptr<float>(), (float)eps,
-                (float)momentum, fptr(running_mean), fptr(running_var), ws.data_ptr<float>(), part.data_ptr<float>(),
-                true, true, st, stats.data_ptr<float>(), rows);
-  at::Tensor out = at::empty({M, N}, a.options());
-  at::Tensor mask = at::empty({((int64_t)M * N + 7) / 8}, a.options().dtype(at::kByte));
-  vy_pass(1, a, w2, M, N, K, ws.data_ptr<float>(), residual.data_ptr(), nullptr, out.data_ptr(),
-          mask.data_ptr<uint8_t>(), nullptr, st);
-  return {out, ws, mask};
-}
-
-// Backward of conv_bn_res_vy_fwd up to the BN input: returns (dy3 [M, N], dgamma, dbeta). dy: [M, N]
-// gradient of the block output (channels_last rows); mask: the forward's ReLU bits. The residual's
-// gradient (dy masked) and the conv's own dgrad / wgrad are the caller's.
-std::vector<at::Tensor> conv_bn_res_vy_bwd(at::Tensor a, at::Tensor w2, at::Tensor dy, at::Tensor mask, at::Tensor ws,
-                                           at::Tensor weight) {
-  check_mat(a, "a");
-  check_mat(w2, "w2");
-  const int M = (int)a.size(0), K = (int)a.size(1), N = (int)w2.size(0);
-  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.numel() == (int64_t)M * N &&
-                  (dy.dim() == 2 ? dy.is_contiguous() : dy.is_contiguous(at::MemoryFormat::ChannelsLast)),
-              "conv_bn_res_vy_bwd: dy must be [M, N] bf16 rows (channels_last)");
-  TORCH_CHECK(mask.scalar_type() == at::kByte && mask.numel() * 8 >= (int64_t)M * N, "conv_bn_res_vy_bwd: bit mask");
-  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() == 7 * (int64_t)N, "conv_bn_res_vy_bwd: 7N workspace");
-  auto f32 = a.options().dtype(at::kFloat);
-  const int rows = vy_rows(2, M, N, K);
-  at::Tensor part = at::empty({rows, N, 2}, f32);
-  hipStream_t st = current_stream(a);
-  vy_pass(2, a, w2, M, N, K, ws.data_ptr<float>(), nullptr, dy.data_ptr(), nullptr, mask.data_ptr<uint8_t>(),
-          part.data_ptr<float>(), st);
-  at::Tensor dg = at::empty({N}, f32), db = at::empty({N}, f32);
-  at::Tensor scratch = at::empty({1}, f32);
-  launch_bn_bwd(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, N, kBF16, weight.data_ptr<float>(),
-                ws.data_ptr<float>(), scratch.data_ptr<float>(), dg.data_ptr<float>(), db.data_ptr<float>(), 2, st,
-                part.data_ptr<float>(), rows);
-  at::Tensor dx = at::empty({M, N}, a.options());
-  vy_pass(3, a, w2, M, N, K, ws.data_ptr<float>(), nullptr, dy.data_ptr(), dx.data_ptr(), mask.data_ptr<uint8_t>(),
-          nullptr, st);
-  return {dx, dg, db};
-}
-
 
 // C = A @ B^T (A [M,K], B [N,K]; or C = A @ B with B [K,N] when b_kmajor) in bf16 with fp32 accumulation. Optionally returns per-row-block
 // column statistics partials [ceil(M/128), N, 2] (sum, sum of squares of the bf16 outputs).
@@ -629,6 +550,7 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
     TORCH_CHECK(addend->size(0) == M && addend->size(1) == N, "gemm_nt: addend must be [M, N]");
   }
   at::Tensor C = at::empty({M, N}, A.options());
+  check_span(C, "gemm_nt output");
   at::Tensor S;
   // memory-bound short-K shapes: the persistent streaming kernel (forward with statistics, data gradient
   // with the fused identity-gradient addend + ReLU-bit mask; not the stride-2 second addend)
@@ -685,6 +607,7 @@ std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at:
     TORCH_CHECK(addend->size(0) == M && addend->size(1) == N, "gemm_nt_bn: addend must be [M, N]");
   }
   at::Tensor C = at::empty({M, N}, A.options());
+  check_span(C, "gemm_nt_bn output");
   at::Tensor part;
   const BnBwdArgs bnb = make_bn_bwd(x_bn, ws, mask, mode, M, N, gemm_nt_stats_rows(M, N, kTileAuto, K), part);
   launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K, nullptr,
@@ -903,6 +826,9 @@ static void check_conv3(const at::Tensor& x, const at::Tensor& w) {
   TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(w.data_ptr()) & 15) == 0,
               "conv3x3: 16-byte aligned operands required");
   TORCH_CHECK(x.numel() / x.size(1) < (1 << 24), "conv3x3: too many pixels for 24-bit index math");
+  check_span(x, "conv3x3 input");
+  TORCH_CHECK(x.numel() / x.size(1) * w.size(0) * 2 < (int64_t(1) << 31),
+              "conv3x3: the output reaches the 2 GiB buffer-descriptor range (lower the per-GPU batch)");
 }
 
 // 3x3 / pad 1 convolution forward (stride 1 or 2). Returns (y, stats-or-undefined).
@@ -1036,7 +962,6 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("lda"), pybind11::arg("ldc"), pybind11::arg("b_kmajor") = false,
         pybind11::arg("add") = false);
   m.def("mfma_pipeline", &mfma_pipeline);
-  m.def("set_stem_halo", &set_stem_halo, "stem forward: -1 environment (DLA_STEM_HALO, default off), 0 implicit GEMM, 1 halo-tiled");
   m.def("set_tn256", &set_tn256, "256x256 weight-gradient tiles: -1 environment (DLA_TN256, default on), 0 off, 1 on");
   m.def("set_splitk_blocks", &set_splitk_blocks, "split-K weight-gradient block target (0 = default / DLA_SPLITK_BLOCKS)");
   m.def("splitk_target_blocks", &splitk_target_blocks);
@@ -1060,10 +985,6 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("ceil_mode") = false,
         pybind11::arg("need_pos") = true);
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pooling backward (gather form)");
-  m.def("conv_bn_res_vy_fwd", &conv_bn_res_vy_fwd,
-        "bottleneck conv3 + BN + residual + ReLU with the conv output recomputed per pass (never stored)");
-  m.def("set_vy_stream", &set_vy_stream, "virtual-output passes on the streaming kernels (vy_stream.hip) or tiled");
-  m.def("conv_bn_res_vy_bwd", &conv_bn_res_vy_bwd, "backward of conv_bn_res_vy_fwd to the conv output (dy3, dgamma, dbeta)");
   m.def("bn_dual_fwd", &bn_dual_fwd, "training act(BN(x) + BN_d(xd)) in one apply pass (downsample residual)");
   m.def("bn_dual_bwd", &bn_dual_bwd, "backward of bn_dual_fwd (one dy read for both BatchNorms)");
   m.def("gap_fwd", &gap_fwd, "NHWC global average pooling -> [N, C]");

@@ -1,0 +1,111 @@
+"""Every environment switch of the framework, in one table, read in one place.
+
+Each knob is the environment variable ``DLA_<NAME>``. Python reads it only through :func:`get`
+(parsed once, cached); the C++/HIP side reads its own (``std::getenv`` once per process, in the
+file named in the table) and the table documents those too, so :func:`non_default` reports every
+switch a run was started with. ``bench.py`` records ``non_default()`` as ``"knobs"`` in its JSON
+line: ``{}`` means the shipped defaults, the only combination the end-to-end tests and the credited
+numbers use. Defaults are the measured-best settings; the alternatives stay for A/B runs
+(the profile that decided each default is cited).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+
+@dataclass(frozen=True)
+class Knob:
+    default: str
+    where: str
+    what: str
+
+
+PREFIX = "DLA_"
+
+TABLE: Dict[str, Knob] = {
+    # ---- run configuration -------------------------------------------------------------------------
+    "KERNELS": Knob("native", "bench.py", "native | torch: the model's kernels (bench --kernels default)"),
+    "PRECISION": Knob("bf16", "bench.py", "bf16 | autocast | fp32 (bench --precision default)"),
+    "CONV": Knob("native", "bench.py", "native | miopen 1x1 convolutions (bench --conv default)"),
+    "GRAPH": Knob("off", "bench.py", "on | off: HIP-graph capture of the whole step (bench --graph default)"),
+    "SAME_DEVICE": Knob("0", "parallel/context.py", "1: every rank on cuda:0 (gloo + IPC transport)"),
+    "TRANSPORT": Knob("", "parallel/context.py", "rccl | ipc gradient transport (default rccl; ipc with SAME_DEVICE)"),
+    "COMM_TIMEOUT_S": Knob("600", "csrc/comm/engine.cpp", "seconds before a collective / IPC barrier is declared dead"),
+    # ---- scheduling of the backward ----------------------------------------------------------------
+    "WGRAD_DEFER": Knob("3x3", "ops/conv.py", "3x3 | auto | all | 0: weight gradients on the side stream "
+                                              "(profiles/r3/g18_g19_wgrad_defer.md, g47_defer_batch_ab.md)"),
+    "WGRAD_JOIN": Knob("end", "ops/conv.py", "end | conv: where the compute stream joins the side stream"),
+    "WGRAD_DEFER_MIN_AI": Knob("200", "ops/conv.py", "WGRAD_DEFER=auto: 1x1 arithmetic-intensity threshold"),
+    "BN_EPILOGUE": Knob("0", "ops/conv.py", "1: BN-backward partials in the dgrad GEMM epilogue "
+                                            "(profiles/bn_epilogue_ab_bs512.jsonl)"),
+    # ---- GoogLeNet Inception fusions ---------------------------------------------------------------
+    "BN_GROUPED": Knob("1", "ops/inception.py", "0: one BN launch chain per Inception branch (profiles/r3p/)"),
+    "FANIN_CAT": Knob("1", "ops/inception.py", "0: three separate fan-in 1x1 GEMMs (profiles/r3y/)"),
+    # ---- kernel selection (C++) --------------------------------------------------------------------
+    "TILE256": Knob("1", "csrc/kernels/gemm.hip", "0: no 256x256 tiles for fwd / dgrad (profiles/r5a/)"),
+    "TN256": Knob("1", "csrc/kernels/gemm.hip", "0: no 256x256 weight-gradient tiles (profiles/r5c/, r5d/)"),
+    "SPLITK_XCD": Knob("1", "csrc/kernels/gemm.hip", "0: no XCD-aware split-K grids (round-2 README row)"),
+    "SPLITK_BLOCKS": Knob("512", "csrc/kernels/gemm.hip", "split-K grid target in blocks"),
+    "SPLITK_SG": Knob("1", "csrc/kernels/gemm.hip", "0: no split-group split-K reduce (profiles/r3n/)"),
+    "GEMM_SPLITK": Knob("1", "csrc/nn_bindings.cpp", "0: no split-K for the FC heads"),
+    "GEMM_STREAM": Knob("1", "csrc/kernels/gemm_stream.hip", "0: no persistent streaming 1x1 GEMM (profiles/r3/)"),
+    "CONV_PIPE": Knob("-1", "csrc/kernels/conv.hip", "3x3 conv main-loop pipeline for K >= 256 (-1: per shape)"),
+    "HALO": Knob("2", "csrc/kernels/conv_halo.hip", "0 off, 1 dgrad only, 2 fwd + dgrad halo-tiled 64-ch 3x3 (r5l/)"),
+    "HALO_V": Knob("1", "csrc/kernels/conv_halo.hip", "halo kernel version (1 / 2)"),
+    "HALO_WGRAD": Knob("1", "csrc/kernels/conv_halo_wgrad.hip", "0: implicit-GEMM 64-ch 3x3 weight gradient"),
+    "POOL3_SEP": Knob("4", "csrc/kernels/pool.hip", "separable 3x3 stride-1 max-pool variant (4 / 7; other: off; r3w/)"),
+    "BN_RED_BLOCKS": Knob("1024", "csrc/kernels/bn_act.hip", "BN reduction-pass block target"),
+    # ---- diagnostics -------------------------------------------------------------------------------
+    "HOOK_TIMING": Knob("0", "parallel/grad_sync.py", "1: host time inside the gradient hooks"),
+    "TRACE": Knob("0", "utils/trace.py", "1: roctx ranges per phase"),
+    "VERBOSE": Knob("", "utils/log.py", "log level (default INFO)"),
+    "TORCH_PROF": Knob("", "bench.py", "path: torch.profiler table after the timed region"),
+    # ---- build / load ------------------------------------------------------------------------------
+    "AUTOBUILD": Knob("0", "ops/_ext.py", "1: build the extension on first import"),
+    "EXT_SO": Knob("", "ops/_ext.py", "path of a variant _C.so (A/B builds, _build.py --out)"),
+}
+
+_CACHE: Dict[str, str] = {}
+
+
+def get(name: str) -> str:
+    """The knob's value (environment or default), read once per process."""
+    if name not in TABLE:
+        raise KeyError(f"unknown knob {name!r}; every switch must be listed in knobs.TABLE")
+    if name not in _CACHE:
+        _CACHE[name] = os.environ.get(PREFIX + name, TABLE[name].default)
+    return _CACHE[name]
+
+
+def flag(name: str) -> bool:
+    return get(name) not in ("", "0", "off", "false", "False")
+
+
+def env_name(name: str) -> str:
+    return PREFIX + name
+
+
+def non_default(environ: Optional[Dict[str, str]] = None) -> Dict[str, str]:
+    """Every knob set in the environment to something other than its default, plus any unknown
+    ``DLA_*`` variable (reported under its full name, so a typo is visible too)."""
+    env = os.environ if environ is None else environ
+    out: Dict[str, str] = {}
+    for k, v in env.items():
+        if not k.startswith(PREFIX):
+            continue
+        name = k[len(PREFIX):]
+        knob = TABLE.get(name)
+        if knob is None:
+            out[k] = v
+        elif v != knob.default:
+            out[name] = v
+    return out
+
+
+def table_markdown() -> str:
+    rows = ["| knob (env `DLA_<NAME>`) | default | read in | what |", "|---|---|---|---|"]
+    for n, k in TABLE.items():
+        rows.append(f"| `{n}` | `{k.default}` | `{k.where}` | {k.what} |")
+    return "\n".join(rows)

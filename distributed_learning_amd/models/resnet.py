@@ -46,13 +46,9 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        branch = None
-        if self.downsample is not None:  # the shortcut conv alongside conv1 / conv2 (ops/nn.py BRANCH_STREAM)
-            branch = dnn.start_shortcut(x, self.downsample[0], self.downsample[1])
         out = dnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
         if self.downsample is not None:  # one apply pass for relu(bn2(conv2) + bn_d(conv_d))
-            return dnn.conv_bn_add_conv_bn_act(out, self.conv2, self.bn2, x, self.downsample[0], self.downsample[1],
-                                               branch=branch)
+            return dnn.conv_bn_add_conv_bn_act(out, self.conv2, self.bn2, x, self.downsample[0], self.downsample[1])
         return dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=x)
 
 
@@ -81,19 +77,14 @@ class Bottleneck(nn.Module):
         else:
             out, xa = dnn.conv_bn_act_fork(x, self.conv1, self.bn1, relu=True)
             xs = None
-        branch = None
-        if self.downsample is not None:  # the shortcut conv runs alongside conv1..conv3 (ops/nn.py BRANCH_STREAM)
-            branch = dnn.start_shortcut(xs if xs is not None else xa, self.downsample[0], self.downsample[1],
-                                        presubsampled=xs is not None)
         out = dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True)
         if self.downsample is None:
             return dnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=xa)
         # the shortcut BN is applied inside the block's final apply pass (never materialised)
         ds_conv, ds_bn = self.downsample[0], self.downsample[1]
         if xs is not None:
-            return dnn.conv_bn_add_conv_bn_act(out, self.conv3, self.bn3, xs, ds_conv, ds_bn, presubsampled=True,
-                                               branch=branch)
-        return dnn.conv_bn_add_conv_bn_act(out, self.conv3, self.bn3, xa, ds_conv, ds_bn, branch=branch)
+            return dnn.conv_bn_add_conv_bn_act(out, self.conv3, self.bn3, xs, ds_conv, ds_bn, presubsampled=True)
+        return dnn.conv_bn_add_conv_bn_act(out, self.conv3, self.bn3, xa, ds_conv, ds_bn)
 
 
 class Downsample(nn.Sequential):

@@ -8,6 +8,7 @@ The extension is built in-tree by ``python -m distributed_learning_amd._build`` 
 """
 from __future__ import annotations
 
+from .. import knobs
 import os
 
 import torch  # noqa: F401  -- must load torch's HIP runtime/RCCL before _C (same SONAMEs)
@@ -21,7 +22,7 @@ def _load():
     if _C is not None or _ERR is not None:
         return
     try:
-        variant = os.environ.get("DLA_EXT_SO")
+        variant = knobs.get("EXT_SO") or None
         if variant:  # A/B runs of a variant build (python -m distributed_learning_amd._build -D ... --out ...)
             import importlib.util
             import sys
@@ -35,7 +36,7 @@ def _load():
 
         _C = mod
     except Exception as e:  # pragma: no cover - depends on build state
-        if os.environ.get("DLA_AUTOBUILD") == "1":
+        if knobs.get("AUTOBUILD") == "1":
             from .. import _build
 
             _build.build()

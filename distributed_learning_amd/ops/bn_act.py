@@ -12,6 +12,7 @@ import torch
 import torch.nn as nn
 
 from . import _ext
+from . import limits as _limits
 
 
 MASK_NONE, MASK_RECOMPUTE, MASK_BITS, MASK_Y = 0, 1, 2, 3
@@ -242,7 +243,7 @@ def fused_bn_relu_maxpool(x: torch.Tensor, bn: nn.BatchNorm2d, pool: nn.MaxPool2
     ok = (bn.training and bn.momentum is not None and x.dtype == torch.bfloat16 and supported(x, bn, None)
           and None not in (k, s, p) and _pair_same(pool.dilation) == 1
           and not pool.return_indices and 1 <= k <= 15 and 2 * p <= k
-          and x.numel() // x.shape[1] < (1 << 24))
+          and _limits.pixels_ok(x.numel() // x.shape[1], "stem BN+ReLU+max-pool"))
     if not ok:
         return max_pool2d(fused_bn_act(x, bn, True, None, stats), pool.kernel_size, pool.stride, pool.padding,
                           pool.dilation, pool.ceil_mode)

@@ -13,6 +13,7 @@ odd channel counts, grouped/dilated/padded convs) uses ``F.conv2d``.
 """
 from __future__ import annotations
 
+from .. import knobs
 import os
 
 import torch
@@ -20,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _ext
+from . import limits as _limits
 from .bn_act import ResidualLink
 from .bn_act import bn_link_of as _bn_link_of
 
@@ -28,7 +30,7 @@ from .bn_act import bn_link_of as _bn_link_of
 # GEMM epilogue costs about as much as the standalone reduction pass it replaces (the epilogue's
 # loads do not overlap the tile's MFMA work), so the fused step was 0.3 ms slower end to end.
 # DLA_BN_EPILOGUE=1 turns it on for A/B runs.
-BN_EPILOGUE = os.environ.get("DLA_BN_EPILOGUE", "0") == "1"
+BN_EPILOGUE = knobs.get("BN_EPILOGUE") == "1"
 
 # Native conv dispatches by kind ("1x1", "1x1_fork", "3x3", "stem"): lets a test assert that a step
 # (e.g. the reference-compatible CLI's) ran the framework's kernels rather than MIOpen.
@@ -45,7 +47,9 @@ def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and conv.kernel_size == (1, 1)
             and conv.padding in ((0, 0), 0) and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
             and conv.stride in ((1, 1), (2, 2)) and conv.in_channels % 8 == 0 and conv.out_channels % 8 == 0
-            and x.is_contiguous(memory_format=torch.channels_last))
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and _limits.span_ok(max(x.numel(), x.numel() // x.shape[1] // conv.stride[0] ** 2 * conv.out_channels)
+                                * x.element_size(), "conv1x1 operand"))
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:
@@ -115,8 +119,8 @@ class _SideWork:
 # callback joins before backward() returns, GradSync's executors join it into their stream before they read,
 # FusedSGD.step joins as a safety net. Consumers that read gradients INSIDE backward without joining
 # (torch DDP's reducer hooks) must call block_deferral() for their lifetime: TorchDDP does.
-WGRAD_DEFER = os.environ.get("DLA_WGRAD_DEFER", "3x3")
-WGRAD_JOIN = os.environ.get("DLA_WGRAD_JOIN", "end")
+WGRAD_DEFER = knobs.get("WGRAD_DEFER")
+WGRAD_JOIN = knobs.get("WGRAD_JOIN")
 _DEFER_PENDING: dict = {}  # device -> the side stream holds work the compute stream has not joined yet
 _DEFERRED_W: dict = {}  # device -> ids of the weights deferred in the running backward (each at most once)
 _DEFER_BLOCKS = [0]  # > 0: some live consumer reads gradients inside backward without joining
@@ -166,7 +170,7 @@ def join_all_devices() -> None:
 # (FLOP per byte of the two streamed operands) is at least WGRAD_DEFER_MIN_AI: those are the MFMA-bound
 # ones that complement the memory-bound passes they overlap; the short-channel 1x1 ones stream operands
 # like the BatchNorm passes and only contend with them.
-WGRAD_DEFER_MIN_AI = float(os.environ.get("DLA_WGRAD_DEFER_MIN_AI", "200"))
+WGRAD_DEFER_MIN_AI = float(knobs.get("WGRAD_DEFER_MIN_AI"))
 
 
 def _wants_defer(kind: str, ctx, cin: int = 0, cout: int = 0) -> bool:
@@ -423,7 +427,9 @@ def supported3x3(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and conv.kernel_size == (3, 3)
             and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
             and _conv3_channels_ok(conv) and x.is_contiguous(memory_format=torch.channels_last)
-            and x.numel() // x.shape[1] < (1 << 24))
+            and _limits.pixels_ok(x.numel() // x.shape[1], "conv3x3")
+            and _limits.span_ok(max(x.numel(), x.numel() // x.shape[1] // conv.stride[0] ** 2 * conv.out_channels)
+                                * x.element_size(), "conv3x3 operand"))
 
 
 def _conv3_channels_ok(conv: nn.Conv2d) -> bool:
@@ -519,7 +525,7 @@ def supported_stem(x: torch.Tensor, conv: nn.Conv2d) -> bool:
             and conv.kernel_size == (7, 7) and conv.stride == (2, 2) and conv.padding == (3, 3)
             and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None and conv.out_channels % 64 == 0
             and x.is_contiguous(memory_format=torch.channels_last)
-            and x.shape[0] * ((x.shape[2] + 1) // 2) * ((x.shape[3] + 1) // 2) < (1 << 24))  # output pixels
+            and _limits.pixels_ok(x.shape[0] * ((x.shape[2] + 1) // 2) * ((x.shape[3] + 1) // 2), "stem conv"))
 
 
 def stem_pack_weight(w: torch.Tensor) -> torch.Tensor:
@@ -575,78 +581,3 @@ def stem_conv(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
     CALLS["stem"] += 1
     return _StemConv.apply(x, conv.weight, want_stats)
 
-
-# ---- bottleneck conv3 + BN3 + residual + ReLU with a virtual conv output --------------------------
-# The expanding 1x1 conv of a ResNet bottleneck (P -> 4P, stride 1) feeds only its BatchNorm, whose
-# output is added to the residual and ReLU'd. Its output y3 is 4x the bytes of its input a2, and the
-# stored-y path writes it once and reads it three times (BN apply; BN-backward reduce and apply). Here
-# every pass recomputes y3 = a2 W3^T tile by tile from a2 (K = P MFMA GEMM, csrc/kernels/gemm.hip
-# gemm_vy_kernel) and y3 never touches HBM: per block that trades 4 passes over y3 for 3 extra reads
-# of a2 (1/4 of y3 each) plus MFMA work. Bit-identical recomputation, so statistics, ReLU bits and
-# gradients are those of the stored-y path up to the BN sums' order. Eligible: K = P <= VIRTUAL_Y_MAX_K.
-# OFF by default — measured slower end to end (profiles/r3/virtual_y_ab.md): the byte accounting holds
-# (BatchNorm passes 29.9 -> 18.3 ms/step), but the recompute passes are latency-bound GEMM kernels at
-# ~2.5-3 TB/s (tiled, gemm.hip) or less (streaming, vy_stream.hip) while the plain BN passes they
-# replace stream at ~5.2 TB/s: 77.2 / 87.2 ms vs 75.2 ms per step at bs1024. DLA_VIRTUAL_Y=1 for A/B.
-VIRTUAL_Y = os.environ.get("DLA_VIRTUAL_Y", "0") == "1"
-VIRTUAL_Y_MAX_K = int(os.environ.get("DLA_VIRTUAL_Y_MAX_K", "256"))
-
-
-def virtual_y_supported(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual) -> bool:
-    return (VIRTUAL_Y and residual is not None and bn.training and bn.momentum is not None
-            and bn.weight is not None and bn.weight.dtype == torch.float32 and supported(x, conv)
-            and conv.stride in ((1, 1), 1) and conv.in_channels <= VIRTUAL_Y_MAX_K
-            and residual.dtype == torch.bfloat16 and residual.shape == (x.shape[0], conv.out_channels) + x.shape[2:]
-            and residual.is_contiguous(memory_format=torch.channels_last) and residual.data_ptr() % 16 == 0)
-
-
-class _Conv1x1BNResVirtual(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, weight, gamma, beta, residual, running_mean, running_var, momentum, eps, rlink):
-        C = _ext.require()
-        n, cin, h, w = x.shape
-        cout = weight.shape[0]
-        w2 = weight.reshape(cout, cin).to(torch.bfloat16).contiguous()
-        out2, ws, mask = C.conv_bn_res_vy_fwd(_rows(x), w2, _rows(residual), gamma, beta, running_mean, running_var,
-                                              momentum, eps)
-        ctx.save_for_backward(x, w2, ws, gamma, mask)
-        ctx.rlink = rlink
-        ctx.wdtype, ctx.wshape, ctx.wstride = weight.dtype, weight.shape, weight.stride()
-        return out2.view(n, h, w, cout).permute(0, 3, 1, 2)
-
-    @staticmethod
-    def backward(ctx, dy):
-        C = _ext.require()
-        x, w2, ws, gamma, mask = ctx.saved_tensors
-        dy = dy.contiguous(memory_format=torch.channels_last)
-        if dy.dtype != torch.bfloat16:
-            dy = dy.to(torch.bfloat16)
-        dy2 = _rows(dy)
-        dy3, dg, db = C.conv_bn_res_vy_bwd(_rows(x), w2, dy2, mask, ws, gamma)
-        need = ctx.needs_input_grad
-        dw = dx = dres = None
-        if need[1]:
-            odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
-            dw = _as_param_layout(C.gemm_tn(dy3, _rows(x), odt, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
-        if need[0]:
-            n, cin, h, w = x.shape
-            dx2, _ = C.gemm_nt(dy3, w2, False, None, True)
-            dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
-        rl = ctx.rlink
-        if rl is not None:  # the forking conv adds dy (masked by the ReLU bits) in its dgrad epilogue
-            rl.dy, rl.mask = dy, mask
-        elif need[4]:
-            dres = dy * _unpack_bits(mask, dy)
-        return (dx, dw, dg if need[2] else None, db if need[3] else None, dres, None, None, None, None, None)
-
-
-def conv1x1_bn_res_virtual(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual: torch.Tensor):
-    """``relu(bn(conv(x)) + residual)`` (training mode) with the conv output never stored."""
-    from .bn_act import _PENDING_COUNTERS, fork_link_of
-
-    CALLS["1x1_vy"] += 1
-    rm, rv = (bn.running_mean, bn.running_var) if bn.track_running_stats else (None, None)
-    if bn.track_running_stats:
-        _PENDING_COUNTERS.append(bn.num_batches_tracked)
-    return _Conv1x1BNResVirtual.apply(x, conv.weight, bn.weight, bn.bias, residual, rm, rv, float(bn.momentum),
-                                      float(bn.eps), fork_link_of(residual))

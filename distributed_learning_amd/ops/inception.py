@@ -35,6 +35,7 @@ torch.hub (/root/reference/src/network.py:33-54).
 """
 from __future__ import annotations
 
+from .. import knobs
 import os
 
 import torch
@@ -288,9 +289,9 @@ def _dx_out(dsl, ys):
             else torch.empty(y.shape, dtype=y.dtype, device=y.device, memory_format=CL) for d, y in zip(dsl, ys)]
 
 
-# DLA_BN_GROUPED=0 keeps one BN launch chain per branch; DLA_FANIN_CAT=0 keeps three fan-in GEMMs (A/B runs)
-_GROUPED = os.environ.get("DLA_BN_GROUPED", "1") != "0"
-_FANIN_CAT = os.environ.get("DLA_FANIN_CAT", "1") != "0"
+# knobs BN_GROUPED=0 keeps one BN launch chain per branch; FANIN_CAT=0 keeps three fan-in GEMMs (A/B runs)
+_GROUPED = knobs.get("BN_GROUPED") != "0"
+_FANIN_CAT = knobs.get("FANIN_CAT") != "0"
 
 
 def _grouped_ok(ys, gs, bs, metas) -> bool:

@@ -106,8 +106,6 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
         from . import conv as nconv
         from .bn_act import fused_bn_act, supported as bn_supported
 
-        if relu and not presubsampled and nconv.virtual_y_supported(x, conv, bn, residual):
-            return nconv.conv1x1_bn_res_virtual(x, conv, bn, residual)
         if nconv.supported(x, conv):
             stride = 1 if presubsampled else None
             y, stats = nconv.conv1x1(x, conv, want_stats=bn.training, stride=stride)
@@ -141,65 +139,19 @@ def _native_conv_stats(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool, presu
 # act(BN(conv(x)) + BN_d(conv_d(xd))) in one apply pass (bench A/B switch)
 DUAL_RESIDUAL = True
 
-# Downsample shortcut conv on a branch stream (DLA_BRANCH_STREAM=1): the block's first conv hands its input
-# to the shortcut conv, which then runs concurrently with the conv1 -> conv2 -> conv3 chain of the compute
-# stream; the final dual apply joins it. Autograd replays each backward node on the stream its forward ran
-# on, so the shortcut conv's data and weight gradients also run on the branch stream, synchronised with
-# their producer and consumer by autograd. Off by default: ResNet-50 bs1024, same box, interleaved
-# (profiles/r3/g21_branch_stream_ab.txt) 73.42-73.62 ms/step with it vs 72.46-72.53 without; the shortcut
-# GEMMs stream their operands and contend with the compute stream's passes rather than filling gaps.
-BRANCH_STREAM = os.environ.get("DLA_BRANCH_STREAM", "0") == "1"
-_BRANCH_STREAMS: dict = {}
-
-
-class ShortcutBranch:
-    """``_native_conv_stats(xd, conv_d, True, presubsampled)`` issued on the branch stream."""
-
-    def __init__(self, xd: torch.Tensor, conv_d: nn.Conv2d, presubsampled: bool):
-        dev = xd.device
-        self.cur = torch.cuda.current_stream(dev)
-        side = _BRANCH_STREAMS.get(dev)
-        if side is None:
-            side = _BRANCH_STREAMS[dev] = torch.cuda.Stream(device=dev)
-        side.wait_stream(self.cur)
-        with torch.cuda.stream(side):
-            self.r = _native_conv_stats(xd, conv_d, True, presubsampled)
-        xd.record_stream(side)
-        self.side = side
-
-    def result(self):
-        self.cur.wait_stream(self.side)
-        if self.r is not None:
-            for t in self.r:
-                if t is not None:
-                    t.record_stream(self.cur)  # allocated on the branch stream, read by the compute stream
-        return self.r
-
-
-def start_shortcut(xd: torch.Tensor, conv_d: nn.Conv2d, bn_d: nn.BatchNorm2d, presubsampled: bool = False):
-    """A ShortcutBranch when the native dual-residual path applies, else None (the caller then passes
-    nothing and ``conv_bn_add_conv_bn_act`` runs the shortcut inline)."""
-    if not (BRANCH_STREAM and _BACKEND == "native" and _NATIVE_CONV and DUAL_RESIDUAL and xd.is_cuda
-            and bn_d.training):
-        return None
-    return ShortcutBranch(xd, conv_d, presubsampled)
-
-
 def conv_bn_add_conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, xd: torch.Tensor,
                             conv_d: nn.Conv2d, bn_d: nn.BatchNorm2d, relu: bool = True,
-                            presubsampled: bool = False, branch: "ShortcutBranch | None" = None) -> torch.Tensor:
+                            presubsampled: bool = False) -> torch.Tensor:
     """``act(BN(conv(x)) + BN_d(conv_d(xd)))`` — a residual block's last conv plus its downsample
     shortcut. Native path: both convs emit their BN statistics and one apply pass reads both conv
     outputs (the shortcut BN's output is never written). ``presubsampled``: ``xd`` is already the
-    stride-2 subsample the strided ``conv_d`` would take. ``branch``: the shortcut conv already issued
-    on the branch stream (``start_shortcut``)."""
+    stride-2 subsample the strided ``conv_d`` would take. (Issuing the shortcut conv on a second stream
+    measured slower: 73.42-73.62 vs 72.46-72.53 ms/step, profiles/r3/g21_branch_stream_ab.txt.)"""
     if _BACKEND == "native" and _NATIVE_CONV and DUAL_RESIDUAL and x.is_cuda and bn.training and bn_d.training:
         from .bn_act import dual_supported, fused_bn_add_bn_act
 
         a = _native_conv_stats(x, conv, True)
-        b = branch.result() if branch is not None else None
-        if b is None:
-            b = _native_conv_stats(xd, conv_d, True, presubsampled) if a is not None else None
+        b = _native_conv_stats(xd, conv_d, True, presubsampled) if a is not None else None
         if a is not None and b is not None and dual_supported(a[0], bn, b[0], bn_d):
             return fused_bn_add_bn_act(a[0], bn, b[0], bn_d, relu, a[1], b[1])
         if a is not None and b is not None:  # convs done; BN the plain way

@@ -12,6 +12,7 @@ and creates ``size`` two-rank groups for its broadcast-emulated NCCL ring. Here:
 """
 from __future__ import annotations
 
+from .. import knobs
 import datetime
 import os
 from dataclasses import dataclass
@@ -85,8 +86,8 @@ def init(backend: Optional[str] = None, rank: Optional[int] = None, world_size: 
     refuses that, so the process group is Gloo and the gradient engine uses the IPC transport.
     ``transport`` (default ``DLA_TRANSPORT`` or ``rccl``; ``ipc`` when ``same_device``)."""
     if same_device is None:
-        same_device = os.environ.get("DLA_SAME_DEVICE", "0") == "1"
-    transport = transport or os.environ.get("DLA_TRANSPORT") or ("ipc" if same_device else "rccl")
+        same_device = os.environ.get(knobs.env_name("SAME_DEVICE"), "0") == "1"
+    transport = transport or knobs.get("TRANSPORT") or ("ipc" if same_device else "rccl")
     global _CTX
     if _CTX is not None:
         return _CTX

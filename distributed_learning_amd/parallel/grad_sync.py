@@ -30,6 +30,7 @@ Fixes and MI355X design:
 """
 from __future__ import annotations
 
+from .. import knobs
 import contextlib
 from typing import Callable, Iterable, List, Optional, Sequence, Set
 
@@ -150,7 +151,7 @@ class GradSync:
         if overlap:
             import os
 
-            hook = self._on_grad_ready_timed if os.environ.get("DLA_HOOK_TIMING") == "1" else self._on_grad_ready
+            hook = self._on_grad_ready_timed if knobs.get("HOOK_TIMING") == "1" else self._on_grad_ready
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(hook))
         self.step_count = 0

@@ -7,6 +7,7 @@ multi-process logs stay readable.
 """
 from __future__ import annotations
 
+from .. import knobs
 import enum
 import os
 import sys
@@ -18,7 +19,7 @@ class Level(enum.IntEnum):
     DEBUG = 3
 
 
-_VERBOSE = int(os.environ.get("DLA_VERBOSE", int(Level.INFO)))
+_VERBOSE = int(knobs.get("VERBOSE") or int(Level.INFO))
 
 
 def set_verbosity(level: int) -> None:

@@ -101,14 +101,16 @@ def _params(model: nn.Module, names: List[str]) -> Dict[str, nn.Parameter]:
 
 
 def teacher_forced(model: nn.Module, x: torch.Tensor, y: torch.Tensor,
-                   bf16_storage: bool = True) -> List[Dict[str, float]]:
+                   bf16_storage: bool = True, only=None) -> List[Dict[str, float]]:
     """Run the native step on ``model`` (bf16 weights, channels_last, on the GPU) and compare every
     segment with fp32 PyTorch. Returns one row per segment: ``out`` (output rel. error), ``dx``
     (input-gradient rel. error; None for the first segment) and ``dw`` (max over the segment's
     parameter gradients, with ``dw_worst`` naming it); the head row also has ``dlogits`` (the fused
     cross-entropy's gradient vs torch's on the same logits). ``bf16_storage``: the reference rounds
     stored activations to bf16 like the native path (module docstring); False compares against pure
-    fp32 activations (then ReLU-decision flips dominate the gradient errors)."""
+    fp32 activations (then ReLU-decision flips dominate the gradient errors). ``only``: names of the
+    segments to compare (the native step still runs whole; e.g. the early segments at the benchmark
+    batch, where the largest tensors and indices live)."""
     from ..ops import nn as dnn
     from ..ops.loss import cross_entropy
 
@@ -137,6 +139,8 @@ def teacher_forced(model: nn.Module, x: torch.Tensor, y: torch.Tensor,
         dnn.set_native_conv(False)
         hooks = bf16_storage_hooks(ref) if bf16_storage else []
         for k, (name, fn, mods) in enumerate(segs):
+            if only is not None and name not in only:
+                continue
             ref.zero_grad(set_to_none=True)
             xin = acts[k].detach().float().contiguous(memory_format=torch.channels_last)
             xin.requires_grad_(k > 0)

@@ -7,12 +7,13 @@ which kernels belong to which phase/bucket. Off by default: zero cost.
 """
 from __future__ import annotations
 
+from .. import knobs
 import contextlib
 import os
 
 import torch
 
-_ON = os.environ.get("DLA_TRACE", "0") == "1"
+_ON = knobs.get("TRACE") == "1"
 
 
 def enabled() -> bool:

@@ -1,0 +1,155 @@
+"""Correctness at the batch the headline runs at.
+
+bench.py's default per-GPU batch is 1280: stage 1 of ResNet-50 has M = 1280 * 56 * 56 = 4,014,080
+rows, its largest activation (1280 x 256 x 56 x 56 bf16) spans 2.06 GB -- just under the 2 GiB
+buffer-descriptor range of the MFMA main loops -- and the stem has 1280 * 112 * 112 = 16.06 M pixels,
+4 % under the 2^24 limit of its index math. Parity tests elsewhere run at batch 16 / 32, so an
+off-by-one in a 32-bit offset that only bites past some row count would silently corrupt the
+credited number. Here:
+
+* the teacher-forced segment comparison (utils/parity.py) of the whole native step at batch 1280,
+  judged on the stem and layer1.0-2 (where the 2 GB tensors and the 24-bit stem indices live)
+  against fp32 PyTorch, with the 2e-2 bound of the small-batch parity test;
+* the stage-1 kernels at exactly M = 4,014,080: the 1x1 GEMMs (forward with statistics, k-major
+  data gradient with the identity-gradient addend, split-K weight gradient), the halo-tiled 64-ch
+  3x3 conv (forward, data and weight gradient) and the fused BN passes;
+* the host guards: batch 1338 raises before any kernel runs.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+BATCH = 1280
+M1 = BATCH * 56 * 56
+CL = torch.channels_last
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.fixture
+def native(cuda):
+    from distributed_learning_amd.ops import nn as dnn
+
+    dnn.set_backend("native")
+    dnn.set_native_conv(True)
+    yield
+    dnn.set_backend("torch")
+    dnn.set_native_conv(False)
+
+
+def _resnet50(cuda):
+    from distributed_learning_amd import models
+    from distributed_learning_amd.ops import nn as dnn
+
+    torch.manual_seed(1234)
+    m = models.resnet50().to(cuda).to(memory_format=CL)
+    dnn.bf16_weights(m)
+    return m
+
+
+def test_guard_batch_1338_raises(cuda, native):
+    from distributed_learning_amd.ops.limits import NativeLimitError
+
+    m = _resnet50(cuda)
+    x = torch.rand(1338, 3, 224, 224, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    with pytest.raises(NativeLimitError, match="2\\^24"):
+        m(x)
+    torch.cuda.synchronize()
+
+
+def test_teacher_forced_stem_and_stage1_at_bench_batch(cuda, native):
+    from distributed_learning_amd.utils.parity import teacher_forced, worst
+
+    m = _resnet50(cuda)
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(BATCH, 3, 224, 224, generator=g).to(cuda, torch.bfloat16).contiguous(memory_format=CL)
+    y = torch.randint(0, 1000, (BATCH,), generator=g).to(cuda)
+    rows = teacher_forced(m, x, y, only={"stem", "layer1.0", "layer1.1", "layer1.2"})
+    assert [r["segment"] for r in rows] == ["stem", "layer1.0", "layer1.1", "layer1.2"]
+    w, where = worst(rows)
+    print("bench-batch parity", rows)
+    assert w <= 2e-2, (w, where)
+
+
+def test_stage1_gemms_at_bench_rows(cuda):
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    g = torch.Generator().manual_seed(3)
+    A = torch.randn(M1, 64, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(256, 64, generator=g) * 0.125).to(cuda, torch.bfloat16)
+    out, st = C.gemm_nt(A, W, True)  # conv3 forward of a stage-1 block (+ BN statistics)
+    ref = A.float() @ W.float().t()
+    assert _rel(out, ref) < 5e-3
+    of = out.double()
+    torch.testing.assert_close(st.double().sum(0)[:, 0], of.sum(0), rtol=1e-4, atol=1e-2)
+    # the rows at the very end of the range (the last tiles) against a direct fp32 product
+    tail = slice(M1 - 4096, M1)
+    assert _rel(out[tail], A[tail].float() @ W.float().t()) < 5e-3
+    del ref, of
+    dy = torch.randn(M1, 256, generator=g).to(cuda, torch.bfloat16)
+    add = torch.randn(M1, 64, generator=g).to(cuda, torch.bfloat16)
+    dx, _ = C.gemm_nt(dy, W, False, add, True)  # k-major data gradient with the identity-gradient addend
+    ref = (dy.float() @ W.float() + add.float())
+    assert _rel(dx, ref) < 5e-3
+    assert _rel(dx[tail], dy[tail].float() @ W.float() + add[tail].float()) < 5e-3
+    del ref
+    dw = C.gemm_tn(A, dy, torch.float32, 1.0)  # weight gradient [64, 256] = A^T dy over 4 M rows
+    ref = A.float().t() @ dy.float()
+    assert _rel(dw, ref) < 1e-3
+
+
+def test_stage1_halo_conv_at_bench_rows(cuda):
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(BATCH, 64, 56, 56, generator=g).to(cuda, torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(64, 64, 3, 3, generator=g) * (2.0 / 576) ** 0.5).to(cuda, torch.bfloat16).contiguous(
+        memory_format=CL)
+    y, st = C.conv3x3_fwd(x, w, 1, True)
+    ref = F.conv2d(x.float(), w.float(), None, 1, 1)
+    assert _rel(y, ref) < 1e-2
+    torch.testing.assert_close(st.double().sum(0)[:, 0], y.double().sum((0, 2, 3)), rtol=1e-4, atol=1.0)
+    assert _rel(y[-2:], ref[-2:]) < 1e-2  # the last images (the highest pixel indices)
+    del ref
+    dy = torch.randn(BATCH, 64, 56, 56, generator=g).to(cuda, torch.bfloat16).contiguous(memory_format=CL)
+    dx = C.conv3x3_dgrad(dy, w)
+    refx = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), 1, 1)
+    assert _rel(dx, refx) < 1e-2 and _rel(dx[-2:], refx[-2:]) < 1e-2
+    del refx
+    dw = C.conv3x3_wgrad(dy, x, 1, torch.float32)
+    refw = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), 1, 1)
+    assert _rel(dw, refw) < 1e-3
+
+
+def test_stage1_bn_at_bench_rows(cuda, native):
+    import torch.nn as nn
+
+    from distributed_learning_amd.ops.bn_act import fused_bn_act
+
+    torch.manual_seed(0)
+    bn = nn.BatchNorm2d(256).to(cuda)
+    bn_ref = nn.BatchNorm2d(256).to(cuda)
+    bn_ref.load_state_dict(bn.state_dict())
+    x = (torch.randn(BATCH, 256, 56, 56, device=cuda) * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=CL)
+    res = torch.randn_like(x)
+    x1 = x.clone().requires_grad_(True)
+    r1 = res.clone().requires_grad_(True)
+    yv = fused_bn_act(x1, bn, True, r1)
+    x2 = x.float().requires_grad_(True)
+    pre = F.batch_norm(x2, None, None, bn_ref.weight, bn_ref.bias, True, 0.0, bn_ref.eps) + res.float()
+    assert _rel(yv, torch.relu(pre)) < 1e-2
+    assert _rel(yv[-2:], torch.relu(pre[-2:])) < 1e-2
+    gy = torch.randn_like(x)
+    yv.backward(gy)
+    mask = (yv.detach() > 0).float()
+    (pre * mask * gy.float()).sum().backward()
+    assert _rel(x1.grad, x2.grad) < 2e-2
+    assert _rel(bn.weight.grad, bn_ref.weight.grad) < 1e-2
+    assert _rel(bn.bias.grad, bn_ref.bias.grad) < 1e-2
