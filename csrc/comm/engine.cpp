@@ -424,11 +424,13 @@ class CommEngine {
     while (true) {
       hipError_t q = hipStreamQuery(stream_->stream());
       if (q == hipSuccess) {
-        if (ipc_base_ && ipc_error()) {
-          abort_comms();
+        if (ipc_base_ && !ipc_broken_ && ipc_error()) {
+          // the IPC windows are out of step from here on (a barrier gave up), the RCCL communicator is not:
+          // refuse further IPC collectives instead of aborting RCCL
+          ipc_broken_ = true;
           if (throw_on_fail)
             throw std::runtime_error("CommEngine: an IPC peer did not reach a barrier within the timeout "
-                                     "(DLA_COMM_TIMEOUT_S; peer failure?); engine aborted");
+                                     "(DLA_COMM_TIMEOUT_S; peer failure?); IPC transport disabled");
           return false;
         }
         return true;
@@ -656,6 +658,7 @@ class CommEngine {
     const size_t esz = wdt == kF32 ? 4 : 2;
     const IpcEntry& e = ipc_entry(code, n);
     const size_t need = comm::kIpcHeaderBytes + (size_t)e.sched.total * esz;
+    TORCH_CHECK(!ipc_broken_, "CommEngine: the IPC transport was disabled after a barrier timeout");
     TORCH_CHECK(ipc_base_ && !ipc_peer_.empty() && need <= ipc_bytes_,
                 "CommEngine: the IPC window (", ipc_bytes_, " B) does not hold this all-reduce (", need,
                 " B); call reserve() with the bucket sizes first (NativeEngine.reserve maps the windows)");
@@ -810,6 +813,7 @@ class CommEngine {
   size_t ipc_bytes_ = 0, ipc_need_ = 0;
   std::vector<char*> ipc_peer_;    // every rank's window base as mapped here (mine = ipc_base_)
   uint64_t ipc_tok_ = 0;           // barrier token counter, identical sequence on every rank
+  bool ipc_broken_ = false;        // a barrier timed out: tokens are out of step, no more IPC collectives
   int wall_khz_ = 100000;          // constant-clock rate for the barrier timeout
   at::Tensor scratch_;
   std::vector<hipEvent_t> ready_pool_;

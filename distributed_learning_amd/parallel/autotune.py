@@ -103,6 +103,8 @@ def measure(engine, algos: Sequence[str], sizes: Sequence[int], dtype: torch.dty
     Algorithms whose setup fails (e.g. peer memory that cannot be mapped) are reported as not ok;
     setup failures are agreed on across ranks before anything is timed, so no rank is left waiting
     in a collective the others skipped."""
+    import os
+
     group = group if group is not None else engine.group
     table: Dict[str, Dict[int, float]] = {}
     ok: Dict[str, bool] = {}
@@ -119,11 +121,26 @@ def measure(engine, algos: Sequence[str], sizes: Sequence[int], dtype: torch.dty
             continue
         row = {}
         good = True
-        for n in sizes:
-            ms, v = _time_algo(engine, a, int(n), dtype, reps, warmup, verify)
-            row[int(n)] = ms
-            good = good and v
-        table[a] = row
+        # an IPC barrier that never completes gives up after DLA_COMM_TIMEOUT_S: short while probing, so a
+        # transport that cannot synchronise on this node costs seconds and is excluded (the engine then
+        # refuses IPC; RCCL is untouched)
+        old_to = os.environ.get("DLA_COMM_TIMEOUT_S")
+        if engine.uses_ipc(a) if hasattr(engine, "uses_ipc") else False:
+            os.environ["DLA_COMM_TIMEOUT_S"] = "30"
+        try:
+            for n in sizes:
+                ms, v = _time_algo(engine, a, int(n), dtype, reps, warmup, verify)
+                row[int(n)] = ms
+                good = good and v
+        except Exception:  # noqa: BLE001
+            good = False
+        finally:
+            if old_to is None:
+                os.environ.pop("DLA_COMM_TIMEOUT_S", None)
+            else:
+                os.environ["DLA_COMM_TIMEOUT_S"] = old_to
+        if good:
+            table[a] = row
         ok[a] = good
     return _gather_max(table, ok, group)
 

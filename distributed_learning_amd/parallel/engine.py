@@ -159,15 +159,37 @@ class NativeEngine:
             return
         self.impl.synchronize()  # nothing of mine in flight reads a peer window
         dist.barrier(group=self.group)  # ... nor of any peer's that reads mine
-        handle = self.impl.ipc_alloc(int(need * 1.25) + (1 << 20))
+        # every step below is agreed on across ranks before the next, so a rank whose allocation or
+        # mapping fails (e.g. peer memory this node cannot map) raises on EVERY rank at the same point
+        # instead of leaving the others waiting in a collective
+        handle, err = None, ""
+        try:
+            handle = self.impl.ipc_alloc(int(need * 1.25) + (1 << 20))
+        except Exception as e:  # noqa: BLE001
+            err = f"ipc_alloc: {e}"
         handles: List[object] = [None] * world
-        dist.all_gather_object(handles, handle, group=self.group)
-        self.impl.ipc_open(handles)
-        dist.barrier(group=self.group)
+        dist.all_gather_object(handles, (handle, err), group=self.group)
+        errs = [e for _, e in handles if e]
+        if errs:
+            raise RuntimeError("IPC window allocation failed: " + "; ".join(errs))
+        try:
+            self.impl.ipc_open([h for h, _ in handles])
+        except Exception as e:  # noqa: BLE001
+            err = f"ipc_open: {e}"
+        flags: List[object] = [None] * world
+        dist.all_gather_object(flags, err, group=self.group)
+        errs = [e for e in flags if e]
+        if errs:
+            raise RuntimeError("IPC window mapping failed: " + "; ".join(errs))
 
     def _lazy_reserve(self, algo: str, flat: torch.Tensor) -> None:
+        """First use of a size the windows do not hold yet: grow them (collective -- the need is a
+        deterministic function of the call sequence, so every rank takes this branch together). The
+        steady state issues no host collective."""
         if self.uses_ipc(algo) and self.impl.world() > 1:
-            self.reserve(algo, [flat.numel()], flat.dtype)
+            self.impl.reserve(algo_code(algo), [flat.numel()], 1 if flat.dtype == torch.bfloat16 else 0)
+            if int(self.impl.ipc_need()) > int(self.impl.ipc_capacity()):
+                self._map_windows()
 
     def set_accum_fp32(self, on: bool) -> None:
         self.impl.set_accum_fp32(bool(on))

@@ -7,7 +7,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(graphed: bool, steps: int, world1, arch: str = "resnet18"):
+def _run(graphed: bool, steps: int, world1, arch: str = "resnet18", force: bool = False):
     from distributed_learning_amd.data import SyntheticBatches
     from distributed_learning_amd.models import googlenet, resnet18
     from distributed_learning_amd.ops import nn as dnn
@@ -26,7 +26,16 @@ def _run(graphed: bool, steps: int, world1, arch: str = "resnet18"):
         m = resnet18(10).to(dev).to(memory_format=torch.channels_last)
         shape = (3, 32, 32)
     dnn.bf16_weights(m)
-    w = PipelinedFusedDP(m, make_reducer("immediate", "builtin", native=True), 1 << 20, dev, broadcast=False)
+    red = make_reducer("immediate", "builtin", native=True)
+    w = PipelinedFusedDP(m, red, 1 << 20, dev, broadcast=False)
+    if force:  # the multi-rank data path (gather -> fp32 staging -> ncclAllReduce -> cast) as graph nodes
+        from distributed_learning_amd.parallel.executor import NativeStreamExecutor
+
+        red.engine.impl.set_force(True)
+        red.engine.set_accum_fp32(True)
+        w.sync.executor = NativeStreamExecutor(red.engine, "builtin", passthrough=False)
+        w.sync.passthrough = False
+        w.sync.executor.reserve(w.sync.buckets)
     opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, master_weights=True)
     data = SyntheticBatches(16, shape, 10, dev, dtype=torch.bfloat16, channels_last=True, device_step=True)
 
@@ -47,6 +56,9 @@ def _run(graphed: bool, steps: int, world1, arch: str = "resnet18"):
     if graphed:
         assert runner.captured
     w.cleanup()
+    if force:
+        red.engine.impl.set_force(False)
+        red.engine.set_accum_fp32(False)
     return losses, [p.detach().float().clone() for p in m.parameters()]
 
 
@@ -78,6 +90,26 @@ def test_graphed_step_matches_eager(world1, arch):
         dnn.set_backend("torch")
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
     # eager: 7 steps; graphed: 2 eager warmups + 5 replays -> replays are steps 3..7
+    assert lg == pytest.approx(le[2:], rel=1e-5, abs=1e-5)
+    for a, b in zip(pe, pg):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_graphed_step_with_collectives_matches_eager(world1):
+    """the captured step must contain real collective nodes. With --force_comm's
+    data path every bucket is gathered into the fp32 staging buffer and all-reduced by a 1-rank
+    ncclAllReduce on the comm stream; the graph (collectives, the engine's reserved scratch, the
+    cross-stream joins) must replay to the eager result."""
+    from distributed_learning_amd.ops import nn as dnn
+
+    dnn.set_backend("native")
+    dnn.set_native_conv(True)
+    try:
+        le, pe = _run(False, 5, world1, "resnet18", force=True)
+        lg, pg = _run(True, 5, world1, "resnet18", force=True)
+    finally:
+        dnn.set_native_conv(False)
+        dnn.set_backend("torch")
     assert lg == pytest.approx(le[2:], rel=1e-5, abs=1e-5)
     for a, b in zip(pe, pg):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
