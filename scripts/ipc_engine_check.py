@@ -2,7 +2,7 @@
 """Multi-process check of the native engine's IPC transport: N real processes, one GPU each or all
 on one GPU (``--same_device 1``, the way a one-GPU box runs it; RCCL refuses that).
 
-Launched with torch.distributed.run (``python scripts/ipc_engine_check.py --nproc 2`` starts the
+Launched with torch.distributed.run (``python scripts/ipc_engine_check.py --ranks 2`` starts the
 ranks itself). Every rank all-reduces a rank-dependent, exactly representable pattern with every
 schedule on the IPC transport (csrc/comm/ipc.h: pulls out of the peers' windows between flag
 barriers), at odd sizes, fp32 and bf16 (fp32-staged), averaging and summing, checks the result
@@ -33,7 +33,7 @@ def _free_port() -> int:
 
 
 def launch(a) -> int:
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.nproc}",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.ranks}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -91,7 +91,7 @@ def worker(a) -> None:
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__)
-    ap.add_argument("--nproc", type=int, default=2)
+    ap.add_argument("--ranks", type=int, default=2)
     ap.add_argument("--same_device", type=int, default=1)
     ap.add_argument("--algos", default=",".join(ALGOS))
     ap.add_argument("--timeout", type=float, default=600.0)

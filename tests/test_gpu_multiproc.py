@@ -41,7 +41,7 @@ def _env():
 
 
 def test_ipc_engine_two_processes(cuda):
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "ipc_engine_check.py"), "--nproc", "2",
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "ipc_engine_check.py"), "--ranks", "2",
                         "--same_device", "1", "--timeout", "200"],
                        capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
