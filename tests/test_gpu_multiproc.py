@@ -132,9 +132,10 @@ def test_matches_one_process_microbatch_oracle(two_rank_run, cuda):
     for n, p in model.named_parameters():
         g_ref = p.grad.detach().float().cpu()
         worst_g = max(worst_g, _rel(got["grads"][n].float(), g_ref))
-        m_ref = opt.state[p]["master"].detach().cpu()
+        # fp32 masters for the bf16 weights; BatchNorm affine parameters are fp32 themselves
+        m_ref = opt.state[p].get("master", p).detach().float().cpu()
         upd_ref = m_ref - init[n].cpu()
-        upd = got["masters"][n] - init[n].cpu()
+        upd = got["masters"].get(n, got["params"][n]).float() - init[n].cpu()
         if float(upd_ref.norm()) > 0:
             worst_u = max(worst_u, _rel(upd, upd_ref))
     assert worst_g <= 2e-2, worst_g
