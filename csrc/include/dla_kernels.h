@@ -266,12 +266,16 @@ int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto, int K = 0);
 // Persistent streaming 1x1 GEMM (gemm_stream.hip) for K in {64, 128, 256}, N % 64 == 0, long M: the
 // number of BN-statistics partial rows it writes (0 = shape not served: use launch_gemm_nt), and the
 // launcher (false = not served). set_gemm_stream: -1 environment (DLA_GEMM_STREAM, default on), 0 / 1.
-int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor, bool add = false);
+int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor, bool add = false,
+                     bool bnb = false);
 // addend (data gradients): C = bf16(bf16(A B^T) + (mask bit ? addend : 0)), addend [M][N] row stride ldd,
 // k-major B and no statistics only (false = not served).
+struct BnBwdArgs;
+// bn_bwd (k-major data gradients): the output is the dy of a fused BN; its backward-reduction partials
+// [gemm_stream_rows][N][2] are written to bn_bwd->part instead of statistics.
 bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
                         int M, int N, int K, float* stats, hipStream_t stream, const void* addend = nullptr,
-                        int64_t ldd = 0, const uint8_t* addend_mask = nullptr);
+                        int64_t ldd = 0, const uint8_t* addend_mask = nullptr, const BnBwdArgs* bn_bwd = nullptr);
 void set_gemm_stream(int mode);
 // BatchNorm-backward reduction fused into a bf16-output GEMM epilogue (the output is the BN's dy):
 // x = the BN input [M, N], ws = its 7N workspace, mask/mode as launch_bn_bwd (0, 1 or 2),

@@ -59,6 +59,16 @@ struct StreamArgs {
   const bf16_t* d;
   int64_t ldd;
   const uint8_t* dmask;
+  // BatchNorm-backward partials (kBnb, data gradients): the output IS the dy of a fused BN(+ReLU) whose
+  // input x [M][N] (row stride ldbx) and 7N workspace are given; per column the sums of dy' and
+  // dy' (x - mean), dy' = dy masked by the BN's ReLU (mode 1: recomputed from x with the forward's
+  // scale / shift, 2: its 1-bit mask laid out like the output, 0: none), accumulated over the block's
+  // tiles and written like the statistics ([mg][N][2] into `stats`)
+  const bf16_t* bx;
+  int64_t ldbx;
+  const float* bws;
+  const uint8_t* bmask;
+  int bmode;
 };
 
 // image row of panel-local weight row p (0..63 within a wave's 64 columns): the MFMA A-operand row
@@ -71,9 +81,18 @@ __device__ __forceinline__ int img_off(int row, int lc) { return row * kBK + ((l
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
 
-template <int BN, int KC, bool kBT, bool kStats, bool kAdd = false>
-__global__ __launch_bounds__(256, kAdd ? 2 : 1) void gemm_stream_kernel(const StreamArgs s) {
-  constexpr int kSP = stream_lookahead(KC, kAdd);
+// kBM: BN-backward partials of the output's consuming BN, -1 none, else its ReLU mode (0 none, 1 recomputed
+// from x, 2 bit mask): compile-time so each variant holds only the registers its mode needs
+// Two blocks per CU (80 KB of LDS each, 2 chunks in flight) for the plain fused-addend variant; with the BN
+// partials on top its operand registers no longer fit two blocks, so it runs one block per CU with the
+// 4-chunk ring of the other variants.
+__host__ __device__ constexpr bool stream_two_blocks(bool add, bool bnb) { return add && !bnb; }
+
+template <int BN, int KC, bool kBT, bool kStats, bool kAdd = false, int kBM = -1>
+__global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) void gemm_stream_kernel(const StreamArgs s) {
+  constexpr bool kBnb = kBM >= 0;
+  static_assert(!(kStats && kBnb), "the partials buffer holds either the statistics or the BN-backward sums");
+  constexpr int kSP = stream_lookahead(KC, stream_two_blocks(kAdd, kBnb));
   constexpr int kSS = kSP + 1;
   constexpr int WN = 64;                    // columns per wave
   constexpr int WGN = BN / WN;              // waves along N (2 or 1)
@@ -84,8 +103,12 @@ __global__ __launch_bounds__(256, kAdd ? 2 : 1) void gemm_stream_kernel(const St
   static_assert(kSP % KC == 0, "the in-flight window must hold whole tiles");
   constexpr int D = kChunkElems / 8 / 256;  // LDS-DMA instructions per wave per chunk (4)
   constexpr int E = 2 * TJ;                 // buffer stores per wave per tile
-  constexpr int F = kAdd ? 3 * TJ : 0;      // addend (2 x 16 B) + mask (2 B) loads per wave per tile
-  static_assert((kSP - 1) * 4 + Q * (E + F) <= 63, "vmcnt is a 6-bit count");
+  constexpr int F = (kAdd ? 3 * TJ : 0) + (kBnb ? (kBM == 2 ? 3 : 2) * TJ : 0);  // addend / BN x (2 x 16 B) + mask (2 B)
+  // ops issued after chunk q before its wait. The epilogue's operand loads are waited for by their use
+  // (which drains everything older, chunk q included), so a count clamped to the 6-bit field is only
+  // stricter than necessary, never too weak
+  constexpr int kVmAfter = ((kSP - 1) * 4 + Q * (E + F)) < 63 ? ((kSP - 1) * 4 + Q * (E + F)) : 63;
+  static_assert(kBnb || (kSP - 1) * 4 + Q * (E + F) <= 63, "vmcnt is a 6-bit count");
   constexpr int kPanelElems = BN * kBK;     // one weight sub-image [BN][64]
 
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -177,10 +200,30 @@ __global__ __launch_bounds__(256, kAdd ? 2 : 1) void gemm_stream_kernel(const St
       make_srd(kAdd && s.dmask ? (const void*)s.dmask : (const void*)s.c, kAdd && s.dmask ? (uint32_t)(((int64_t)M * s.ldd + 7) / 8) : 0u);
   i32x4_t dv[kAdd ? TJ : 1][2];
   uint32_t mb[kAdd ? TJ : 1];
+  // BN-backward operands: x rows of the lane's 16 columns and the BN's mask bits; per-column constants
+  // of the block's fixed column panel held in registers
+  const __amdgpu_buffer_rsrc_t rbx = make_srd(kBnb ? (const void*)s.bx : (const void*)s.c,
+                                              kBnb ? (uint32_t)((int64_t)M * s.ldbx * 2) : 0u);
+  const __amdgpu_buffer_rsrc_t rbm = make_srd(kBM == 2 ? (const void*)s.bmask : (const void*)s.c,
+                                              kBM == 2 ? (uint32_t)(((int64_t)M * s.ldc + 7) / 8) : 0u);
+  i32x4_t xv[kBnb ? TJ : 1][2];
+  uint32_t xb[kBM == 2 ? TJ : 1];
+  float bmean[kBnb ? 16 : 1], bsc[kBM == 1 ? 16 : 1], bsh[kBM == 1 ? 16 : 1];
+  if constexpr (kBnb) {
+    const int gc = col0 + wn * WN + 16 * g;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      bmean[e] = s.bws[gc + e];
+      if constexpr (kBM == 1) {
+        bsc[e] = s.bws[2 * s.N + gc + e];
+        bsh[e] = s.bws[3 * s.N + gc + e];
+      }
+    }
+  }
   auto load_operands = [&](int t) {
+    const int64_t row0 = (int64_t)(grp + t * s.mg) * kSBM;
+    const int gc = col0 + wn * WN + 16 * g;
     if constexpr (kAdd) {
-      const int64_t row0 = (int64_t)(grp + t * s.mg) * kSBM;
-      const int gc = col0 + wn * WN + 16 * g;
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int64_t gm = row0 + wm * WM + 16 * j + lr;
@@ -189,6 +232,18 @@ __global__ __launch_bounds__(256, kAdd ? 2 : 1) void gemm_stream_kernel(const St
         dv[j][0] = __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, 0);
         dv[j][1] = __builtin_amdgcn_raw_buffer_load_b128(rd, ok ? off + 16 : kOOB, 0, 0);
         mb[j] = __builtin_amdgcn_raw_buffer_load_b16(rmk, ok ? (uint32_t)((gm * s.ldd + gc) >> 3) : kOOB, 0, 0);
+      }
+    }
+    if constexpr (kBnb) {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int64_t gm = row0 + wm * WM + 16 * j + lr;
+        const bool ok = gm < M;
+        const uint32_t off = ok ? (uint32_t)((gm * s.ldbx + gc) * 2) : kOOB;
+        xv[j][0] = __builtin_amdgcn_raw_buffer_load_b128(rbx, off, 0, 0);
+        xv[j][1] = __builtin_amdgcn_raw_buffer_load_b128(rbx, ok ? off + 16 : kOOB, 0, 0);
+        if constexpr (kBM == 2)
+          xb[j] = __builtin_amdgcn_raw_buffer_load_b16(rbm, ok ? (uint32_t)((gm * s.ldc + gc) >> 3) : kOOB, 0, 0);
       }
     }
   };
@@ -208,7 +263,7 @@ __global__ __launch_bounds__(256, kAdd ? 2 : 1) void gemm_stream_kernel(const St
     // q+1 .. q+kSP-1 (D each) and the stores (+ next-tile operand loads) of the Q tiles that ended
     // after chunk q was issued
     if (q < kSP) vm_wait<(kSP - 1) * D>();
-    else vm_wait<(kSP - 1) * D + Q * (E + F)>();
+    else vm_wait<kVmAfter>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: slot (q-1) % kSS is refilled below
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -264,6 +319,16 @@ __global__ __launch_bounds__(256, kAdd ? 2 : 1) void gemm_stream_kernel(const St
               st_s[i][r] += v;
               st_q[i][r] = fmaf(v, v, st_q[i][r]);
             }
+            if constexpr (kBnb) {  // the BN backward's reduction of the stored dy (OOB rows: dy = x = 0)
+              const int e = 4 * i + r;
+              const uint32_t xw = (uint32_t)xv[j][e >> 3][(e >> 1) & 3];
+              const float xf = bf16_to_f32((bf16_t)((e & 1) ? (xw >> 16) : (xw & 0xffffu)));
+              float gv = bf16_to_f32(h[r]);
+              if constexpr (kBM == 1) gv = fmaf(xf, bsc[e], bsh[e]) > 0.f ? gv : 0.f;  // same fmaf as the forward
+              if constexpr (kBM == 2) gv = ((xb[j] >> e) & 1u) ? gv : 0.f;
+              st_s[i][r] += gv;
+              st_q[i][r] = fmaf(gv, xf - bmean[e], st_q[i][r]);
+            }
           }
           w[2 * i] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
           w[2 * i + 1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
@@ -277,7 +342,7 @@ __global__ __launch_bounds__(256, kAdd ? 2 : 1) void gemm_stream_kernel(const St
     }
   }
   vm_wait<0>();  // no LDS-DMA may land after the block's LDS is released
-  if constexpr (kStats) {
+  if constexpr (kStats || kBnb) {
     // columns of this lane: wn*64 + 16 g + 4 i + r; sum the 16 row lanes (lr), then the WGM waves
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -310,9 +375,9 @@ __global__ __launch_bounds__(256, kAdd ? 2 : 1) void gemm_stream_kernel(const St
   }
 }
 
-template <int BN, int KC, bool kAdd>
+template <int BN, int KC, bool kTwo>
 constexpr size_t stream_lds_bytes() {
-  return (size_t)(KC * BN * kBK + (stream_lookahead(KC, kAdd) + 1) * kChunkElems) * sizeof(bf16_t);
+  return (size_t)(KC * BN * kBK + (stream_lookahead(KC, kTwo) + 1) * kChunkElems) * sizeof(bf16_t);
 }
 
 int g_stream_mode = -1;  // -1: environment (DLA_GEMM_STREAM, default on), 0 off, 1 on (every K <= 256)
@@ -334,7 +399,8 @@ struct StreamPlan {
 // win or tie everywhere (fwd K 64 x N 256 -11 %, dgrad K 128 x N 256 -45 %); at K = 256 only the data
 // gradient (k-major weights) wins (-11 % at N 512); the forward K = 256 shapes lose 1-12 % (N >= 512 at
 // M <= 802k: the tile kernel's 2-4 co-resident blocks beat one 4-wave block per CU there).
-StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor, bool add = false) {
+StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor, bool add = false,
+                       bool bnb = false) {
   StreamPlan p;
   if (add && K > 128) return p;  // 2 blocks per CU: the K = 256 weight panel does not fit 80 KB
   if (!stream_enabled() || M <= 0) return p;
@@ -346,7 +412,7 @@ StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b
   const int mt = (int)((M + kSBM - 1) / kSBM);
   // one block per CU: 256 blocks = 8 XCDs x per_xcd row groups x nbn panels; at least two tiles per
   // row group, or the ring has nothing to overlap (the tile kernel serves small M)
-  int per_xcd = std::max(1, (add ? 64 : 32) / nbn);
+  int per_xcd = std::max(1, (stream_two_blocks(add, bnb) ? 64 : 32) / nbn);
   while (per_xcd > 1 && mt < 2 * 8 * per_xcd) per_xcd >>= 1;
   if (mt < 2 * 8 * per_xcd) return StreamPlan{};
   p.per_xcd = per_xcd;
@@ -358,13 +424,30 @@ StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b
 template <int BN, int KC>
 void launch_stream_kc(const StreamArgs& a, int grid, bool kmajor, bool stats, bool add, hipStream_t stream) {
   const dim3 g(grid), b(256);
+  const int bm = a.bx != nullptr ? a.bmode : -1;
+#define DLA_SBN(ADD_, M_)                                                                                         \
+  hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, true, false, ADD_, M_>), g, b,                                  \
+                     (stream_lds_bytes<BN, KC, stream_two_blocks(ADD_, (M_) >= 0)>()), stream, a)
   if constexpr (KC <= 2) {
     if (add) {  // data gradient with the fused addend (k-major weights, no statistics)
-      hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, true, false, true>), g, b, (stream_lds_bytes<BN, KC, true>()),
-                         stream, a);
+      switch (bm) {
+        case 0: DLA_SBN(true, 0); break;
+        case 1: DLA_SBN(true, 1); break;
+        case 2: DLA_SBN(true, 2); break;
+        default: DLA_SBN(true, -1); break;
+      }
       return;
     }
   }
+  if (bm >= 0) {  // data gradient carrying the consuming BN's backward reduction (k-major, no statistics)
+    switch (bm) {
+      case 0: DLA_SBN(false, 0); break;
+      case 1: DLA_SBN(false, 1); break;
+      default: DLA_SBN(false, 2); break;
+    }
+    return;
+  }
+#undef DLA_SBN
   constexpr size_t lds = stream_lds_bytes<BN, KC, false>();
   if (kmajor) {
     if (stats) hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, true, true>), g, b, lds, stream, a);
@@ -379,18 +462,24 @@ void launch_stream_kc(const StreamArgs& a, int grid, bool kmajor, bool stats, bo
 
 void set_gemm_stream(int mode) { g_stream_mode = mode < 0 ? -1 : (mode ? 1 : 0); }
 
-int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor, bool add) {
-  return stream_plan(M, N, K, lda, ldc, b_kmajor, add).mg;
+int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor, bool add, bool bnb) {
+  return stream_plan(M, N, K, lda, ldc, b_kmajor, add, bnb).mg;
 }
 
 bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
                         int M, int N, int K, float* stats, hipStream_t stream, const void* addend, int64_t ldd,
-                        const uint8_t* addend_mask) {
-  const StreamPlan p = stream_plan(M, N, K, lda, ldc, b_kmajor, addend != nullptr);
+                        const uint8_t* addend_mask, const BnBwdArgs* bn_bwd) {
+  const StreamPlan p = stream_plan(M, N, K, lda, ldc, b_kmajor, addend != nullptr, bn_bwd != nullptr);
   if (!p.mg) return false;
   if (addend && (stats || !b_kmajor || ldd % 8 != 0 || (int64_t)M * ldd * 2 >= (int64_t)kOOB)) return false;
-  StreamArgs a{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, p.mg, p.per_xcd, stats,
-               (const bf16_t*)addend, ldd, addend_mask};
+  if (bn_bwd) {  // partials go where the statistics would: [mg][N][2]
+    const int64_t ldbx = bn_bwd->ldx ? bn_bwd->ldx : ldc;
+    if (stats || !b_kmajor || ldbx % 8 != 0 || (int64_t)M * ldbx * 2 >= (int64_t)kOOB) return false;
+  }
+  StreamArgs a{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, p.mg, p.per_xcd,
+               bn_bwd ? bn_bwd->part : stats, (const bf16_t*)addend, ldd, addend_mask,
+               bn_bwd ? (const bf16_t*)bn_bwd->x : nullptr, bn_bwd ? (bn_bwd->ldx ? bn_bwd->ldx : ldc) : 0,
+               bn_bwd ? bn_bwd->ws : nullptr, bn_bwd ? bn_bwd->mask : nullptr, bn_bwd ? bn_bwd->mode : 0};
   const int kc = K / kBK;
   if (p.bn == 128) {
     if (kc == 1) launch_stream_kc<128, 1>(a, p.grid, b_kmajor, stats != nullptr, addend != nullptr, stream);

@@ -609,6 +609,21 @@ std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at:
   at::Tensor C = at::empty({M, N}, A.options());
   check_span(C, "gemm_nt_bn output");
   at::Tensor part;
+  // short-K data gradients: the persistent streaming kernel, whose epilogue loads x while the next tile's
+  // rows are already in flight (the tile kernel's epilogue loads stall its block)
+  const bool add2 = addend2.has_value() && addend2->defined();
+  const bool amask = addend_mask.has_value() && addend_mask->defined();
+  const bool stream_ok = b_kmajor && !add2 && (!amask || add) &&
+                         (!add || (addend->stride(0) > 0 && addend->stride(0) % 8 == 0 &&
+                                   (int64_t)M * addend->stride(0) * 2 < (int64_t(1) << 31)));
+  const int srows = stream_ok ? gemm_stream_rows(M, N, K, A.stride(0), C.stride(0), b_kmajor, add, true) : 0;
+  if (srows > 0) {
+    const BnBwdArgs sb = make_bn_bwd(x_bn, ws, mask, mode, M, N, srows, part);
+    if (launch_gemm_stream(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), b_kmajor, C.data_ptr(), C.stride(0), M,
+                           N, K, nullptr, current_stream(A), add ? addend->data_ptr() : nullptr,
+                           add ? addend->stride(0) : 0, addend_mask_ptr(addend_mask, M, N, add), &sb))
+      return {C, part};
+  }
   const BnBwdArgs bnb = make_bn_bwd(x_bn, ws, mask, mode, M, N, gemm_nt_stats_rows(M, N, kTileAuto, K), part);
   launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K, nullptr,
                  current_stream(A), add ? addend->data_ptr() : nullptr, add ? addend->stride(0) : 0, b_kmajor,
@@ -960,7 +975,7 @@ void bind_nn(pybind11::module& m) {
   m.def("set_gemm_stream", &set_gemm_stream, "persistent streaming 1x1 GEMM: -1 environment (default on), 0 off, 1 on");
   m.def("gemm_stream_rows", &gemm_stream_rows, "BN-statistics partial rows of the streaming GEMM (0: shape not served)",
         pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("lda"), pybind11::arg("ldc"), pybind11::arg("b_kmajor") = false,
-        pybind11::arg("add") = false);
+        pybind11::arg("add") = false, pybind11::arg("bnb") = false);
   m.def("mfma_pipeline", &mfma_pipeline);
   m.def("set_tn256", &set_tn256, "256x256 weight-gradient tiles: -1 environment (DLA_TN256, default on), 0 off, 1 on");
   m.def("set_splitk_blocks", &set_splitk_blocks, "split-K weight-gradient block target (0 = default / DLA_SPLITK_BLOCKS)");

@@ -76,18 +76,34 @@ def _bf16_ste(t: torch.Tensor) -> torch.Tensor:
     return t + (t.to(torch.bfloat16).to(t.dtype) - t).detach()
 
 
-def bf16_storage_hooks(model: nn.Module) -> list:
+class _Bf16Both(torch.autograd.Function):
+    """Round to bf16 in the forward AND round the gradient to bf16 in the backward: the storage
+    precision of the native path's gradient tensors (conv data gradients, BN-backward outputs)."""
+
+    @staticmethod
+    def forward(ctx, t):
+        return t.to(torch.bfloat16).to(t.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def bf16_storage_hooks(model: nn.Module, grads: bool = False) -> list:
     """Round the inputs and outputs of every Conv2d / Linear of ``model`` to bf16 (straight-through),
-    i.e. the activation storage precision of the native path. Returns the hook handles."""
+    i.e. the activation storage precision of the native path. ``grads``: round the gradients that
+    cross those points too (the native path stores every activation gradient in bf16). Returns the
+    hook handles."""
+    rnd = _Bf16Both.apply if grads else _bf16_ste
     handles = []
     for m in model.modules():
         if isinstance(m, nn.MaxPool2d):  # the native pools take the max of the stored (bf16) activations
             handles.append(m.register_forward_pre_hook(lambda mod, args: tuple(
-                _bf16_ste(a) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)))
+                rnd(a) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)))
         if isinstance(m, (nn.Conv2d, nn.Linear)):
             handles.append(m.register_forward_pre_hook(lambda mod, args: tuple(
-                _bf16_ste(a) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)))
-            handles.append(m.register_forward_hook(lambda mod, args, out: _bf16_ste(out)))
+                rnd(a) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)))
+            handles.append(m.register_forward_hook(lambda mod, args, out: rnd(out)))
     return handles
 
 
@@ -101,7 +117,7 @@ def _params(model: nn.Module, names: List[str]) -> Dict[str, nn.Parameter]:
 
 
 def teacher_forced(model: nn.Module, x: torch.Tensor, y: torch.Tensor,
-                   bf16_storage: bool = True, only=None) -> List[Dict[str, float]]:
+                   bf16_storage: bool = True, only=None, bf16_grads: bool = False) -> List[Dict[str, float]]:
     """Run the native step on ``model`` (bf16 weights, channels_last, on the GPU) and compare every
     segment with fp32 PyTorch. Returns one row per segment: ``out`` (output rel. error), ``dx``
     (input-gradient rel. error; None for the first segment) and ``dw`` (max over the segment's
@@ -110,7 +126,11 @@ def teacher_forced(model: nn.Module, x: torch.Tensor, y: torch.Tensor,
     stored activations to bf16 like the native path (module docstring); False compares against pure
     fp32 activations (then ReLU-decision flips dominate the gradient errors). ``only``: names of the
     segments to compare (the native step still runs whole; e.g. the early segments at the benchmark
-    batch, where the largest tensors and indices live)."""
+    batch, where the largest tensors and indices live). ``bf16_grads``: the reference also rounds the
+    activation gradients to bf16 where the native path stores them. Needed at large batch: a weight
+    gradient or BN-bias gradient whose true value nearly cancels over N*H*W rows (BN-backward outputs
+    sum to zero per channel) picks up the per-element bf16 rounding of the stored gradients as
+    ~2^-9 sqrt(N*H*W) relative noise, which is storage policy, not kernel error."""
     from ..ops import nn as dnn
     from ..ops.loss import cross_entropy
 
@@ -137,7 +157,7 @@ def teacher_forced(model: nn.Module, x: torch.Tensor, y: torch.Tensor,
         # ---- fp32 reference, one segment at a time on the native path's own tensors ----------
         dnn.set_backend("torch")
         dnn.set_native_conv(False)
-        hooks = bf16_storage_hooks(ref) if bf16_storage else []
+        hooks = bf16_storage_hooks(ref, grads=bf16_grads) if bf16_storage else []
         for k, (name, fn, mods) in enumerate(segs):
             if only is not None and name not in only:
                 continue

@@ -69,7 +69,9 @@ def test_teacher_forced_stem_and_stage1_at_bench_batch(cuda, native):
     g = torch.Generator().manual_seed(11)
     x = torch.rand(BATCH, 3, 224, 224, generator=g).to(cuda, torch.bfloat16).contiguous(memory_format=CL)
     y = torch.randint(0, 1000, (BATCH,), generator=g).to(cuda)
-    rows = teacher_forced(m, x, y, only={"stem", "layer1.0", "layer1.1", "layer1.2"})
+    # activation gradients rounded to bf16 in the reference too (utils/parity.py bf16_grads): at 4 M rows the
+    # near-cancelling weight / BN-bias gradient sums otherwise measure the storage rounding (~2^-9 sqrt(rows))
+    rows = teacher_forced(m, x, y, only={"stem", "layer1.0", "layer1.1", "layer1.2"}, bf16_grads=True)
     assert [r["segment"] for r in rows] == ["stem", "layer1.0", "layer1.1", "layer1.2"]
     w, where = worst(rows)
     print("bench-batch parity", rows)

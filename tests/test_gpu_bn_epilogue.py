@@ -157,3 +157,39 @@ def test_fork_subsample_is_exact(cuda):
     assert torch.equal(o1, o0)
     for n in g0:
         assert torch.equal(g1[n], g0[n]), n
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("shape,add", [((40000, 64, 256), True), ((40000, 128, 512), True), ((40000, 256, 64), False),
+                                       ((40001, 128, 128), False), ((70000, 64, 128), True)])
+def test_gemm_nt_bn_streaming_kernel(cuda, mode, shape, add):
+    """Short-K data gradients take the persistent streaming kernel (gemm_stream.hip, kBM variants): its
+    output must equal the plain streaming dgrad bitwise (with the fused masked addend of the identity
+    gradient where present) and its per-row-group partials must sum to the BN backward's reduction."""
+    C = _C()
+    M, K, N = shape
+    assert C.gemm_stream_rows(M, N, K, K, N, True, add, True) > 0, "shape not served by the streaming kernel"
+    g = torch.Generator().manual_seed(M + K + N + mode)
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(K, N, generator=g) * K ** -0.5).to(cuda, torch.bfloat16)
+    x = torch.randn(M, N, generator=g).to(cuda, torch.bfloat16)
+    ws = torch.randn(7 * N, generator=g).to(cuda)
+    mask = torch.randint(0, 256, ((M * N + 7) // 8,), generator=g, dtype=torch.uint8).to(cuda)
+    D = torch.randn(M, N, generator=g).to(cuda, torch.bfloat16) if add else None
+    dmask = torch.randint(0, 256, ((M * N + 7) // 8,), generator=g, dtype=torch.uint8).to(cuda) if add else None
+    dy, part = C.gemm_nt_bn(A, W, D, True, x, ws, mask, mode, dmask)
+    ref, _ = C.gemm_nt(A, W, False, D, True, 0, dmask)
+    torch.cuda.synchronize()
+    assert torch.equal(dy, ref)
+    assert part.shape[0] == C.gemm_stream_rows(M, N, K, K, N, True, add, True)
+    gf = dy.float()
+    xf = x.float()
+    if mode == 1:
+        gf = torch.where(torch.addcmul(ws[3 * N:4 * N], xf, ws[2 * N:3 * N]) > 0, gf, torch.zeros_like(gf))
+    elif mode == 2:
+        bits = torch.stack([(mask >> j) & 1 for j in range(8)], 1).reshape(-1)[: M * N].view(M, N)
+        gf = gf * bits
+    s = gf.double().sum(0)
+    q = (gf.double() * (xf.double() - ws[:N].double())).sum(0)
+    torch.testing.assert_close(part.double().sum(0)[:, 0], s, rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part.double().sum(0)[:, 1], q, rtol=1e-4, atol=1e-2)
