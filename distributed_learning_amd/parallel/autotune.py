@@ -28,6 +28,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from .. import knobs
 from . import cost_model as cm
 
 MiB = 1024 * 1024
@@ -124,9 +125,10 @@ def measure(engine, algos: Sequence[str], sizes: Sequence[int], dtype: torch.dty
         # an IPC barrier that never completes gives up after DLA_COMM_TIMEOUT_S: short while probing, so a
         # transport that cannot synchronise on this node costs seconds and is excluded (the engine then
         # refuses IPC; RCCL is untouched)
-        old_to = os.environ.get("DLA_COMM_TIMEOUT_S")
+        key = knobs.env_name("COMM_TIMEOUT_S")  # read by the engine at every barrier launch
+        old_to = os.environ.get(key)
         if engine.uses_ipc(a) if hasattr(engine, "uses_ipc") else False:
-            os.environ["DLA_COMM_TIMEOUT_S"] = "30"
+            os.environ[key] = "30"
         try:
             for n in sizes:
                 ms, v = _time_algo(engine, a, int(n), dtype, reps, warmup, verify)
@@ -136,9 +138,9 @@ def measure(engine, algos: Sequence[str], sizes: Sequence[int], dtype: torch.dty
             good = False
         finally:
             if old_to is None:
-                os.environ.pop("DLA_COMM_TIMEOUT_S", None)
+                os.environ.pop(key, None)
             else:
-                os.environ["DLA_COMM_TIMEOUT_S"] = old_to
+                os.environ[key] = old_to
         if good:
             table[a] = row
         ok[a] = good
