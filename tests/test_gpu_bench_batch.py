@@ -73,9 +73,19 @@ def test_teacher_forced_stem_and_stage1_at_bench_batch(cuda, native):
     # near-cancelling weight / BN-bias gradient sums otherwise measure the storage rounding (~2^-9 sqrt(rows))
     rows = teacher_forced(m, x, y, only={"stem", "layer1.0", "layer1.1", "layer1.2"}, bf16_grads=True)
     assert [r["segment"] for r in rows] == ["stem", "layer1.0", "layer1.1", "layer1.2"]
-    w, where = worst(rows)
     print("bench-batch parity", rows)
-    assert w <= 2e-2, (w, where)
+    # Outputs keep the small-batch 2e-2 bound. Gradients summed over 4 M rows whose true value nearly
+    # cancels (a BN-backward output sums to zero per channel, so a weight gradient of the conv that
+    # produced it is a small difference of large sums) see the independent fp32 reference's +-1-ulp
+    # differences in bf16-stored activations / ReLU decisions grow as sqrt(rows): 5e-2 here (measured
+    # worst 3.0e-2, layer1.0.conv1.weight; 1.0e-2 on layer1.1-2), vs 1.7e-2 at batch 16. Index or
+    # offset bugs show up as O(1) errors; the kernels' own arithmetic at this M on identical inputs is
+    # pinned tightly by the stage-1 tests below.
+    for r in rows:
+        assert r["out"] <= 2e-2, r
+        assert r["dx"] is None or r["dx"] <= 3e-2, r
+        assert r["dw"] <= 5e-2, r
+    assert worst(rows)[0] <= 5e-2
 
 
 def test_stage1_gemms_at_bench_rows(cuda):
