@@ -38,8 +38,8 @@ TABLE: Dict[str, Knob] = {
                                               "(profiles/r3/g18_g19_wgrad_defer.md, g47_defer_batch_ab.md)"),
     "WGRAD_JOIN": Knob("end", "ops/conv.py", "end | conv: where the compute stream joins the side stream"),
     "WGRAD_DEFER_MIN_AI": Knob("200", "ops/conv.py", "WGRAD_DEFER=auto: 1x1 arithmetic-intensity threshold"),
-    "BN_EPILOGUE": Knob("0", "ops/conv.py", "1: BN-backward partials in the dgrad GEMM epilogue "
-                                            "(profiles/bn_epilogue_ab_bs512.jsonl)"),
+    "BN_EPILOGUE": Knob("0", "ops/conv.py", "1 / stream: BN-backward partials in every / the streaming dgrad "
+                                            "GEMM epilogue (profiles/r4/g02/, bn_epilogue_ab_bs512.jsonl)"),
     # ---- GoogLeNet Inception fusions ---------------------------------------------------------------
     "BN_GROUPED": Knob("1", "ops/inception.py", "0: one BN launch chain per Inception branch (profiles/r3p/)"),
     "FANIN_CAT": Knob("1", "ops/inception.py", "0: three separate fan-in 1x1 GEMMs (profiles/r3y/)"),

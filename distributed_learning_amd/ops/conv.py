@@ -26,11 +26,21 @@ from .bn_act import ResidualLink
 from .bn_act import bn_link_of as _bn_link_of
 
 # Fuse the backward reduction of a producing BatchNorm into this conv's dgrad epilogue (BNLink).
-# Off by default: measured on MI355X (scripts/bench_gemm.py dgrad_bn*), reading the BN input in the
-# GEMM epilogue costs about as much as the standalone reduction pass it replaces (the epilogue's
-# loads do not overlap the tile's MFMA work), so the fused step was 0.3 ms slower end to end.
-# DLA_BN_EPILOGUE=1 turns it on for A/B runs.
-BN_EPILOGUE = knobs.get("BN_EPILOGUE") == "1"
+# "0" (default) off, "1" every dgrad, "stream" only the short-K 1x1 data gradients the persistent
+# streaming kernel serves (gemm_stream.hip kBM variants: the epilogue's x loads overlap the next tile's
+# rows in flight). Measured on MI355X: round 2, reading the BN input in the tile kernels' epilogue cost
+# about what the standalone reduction pass saves (+0.3 ms/step at bs512); round 4 at bs1280 "1" is
+# 3.8 % slower (92.0 vs 88.5 ms/step, profiles/r4/g02/).
+BN_EPILOGUE = knobs.get("BN_EPILOGUE")
+
+
+def _epi_ok(M: int, N: int, K: int, add: bool) -> bool:
+    """Use the BN-epilogue data gradient for this k-major 1x1 dgrad (output [M, N], K = its input channels)."""
+    if BN_EPILOGUE == "1":
+        return True
+    if BN_EPILOGUE != "stream":
+        return False
+    return _ext.require().gemm_stream_rows(M, N, K, K, N, True, add, True) > 0
 
 # Native conv dispatches by kind ("1x1", "1x1_fork", "3x3", "stem"): lets a test assert that a step
 # (e.g. the reference-compatible CLI's) ran the framework's kernels rather than MIOpen.
@@ -40,7 +50,7 @@ CALLS = _collections.Counter()
 
 
 def bn_link_of(x):
-    return _bn_link_of(x) if BN_EPILOGUE else None
+    return _bn_link_of(x) if BN_EPILOGUE != "0" else None
 
 
 def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -261,6 +271,8 @@ class _Conv1x1(torch.autograd.Function):
             wg = _SideWork(wgrad, dy2.shape[0], dy.device)
         if ctx.needs_input_grad[0]:
             link = ctx.link
+            if link is not None and not _epi_ok(dy2.shape[0], w2.shape[1], dy2.shape[1], False):
+                link = None
             if link is not None:
                 dx2, part = C.gemm_nt_bn(dy2, w2, None, True, _rows(link.x), link.ws, link.mask, link.mode)
                 link.publish(dx2, part)
@@ -359,6 +371,9 @@ class _Conv1x1Fork(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             add = None if dident is None else _rows(dident)
             link = ctx.link
+            if link is not None and (dsub is not None or not _epi_ok(dy2.shape[0], w2.shape[1], dy2.shape[1],
+                                                                     add is not None)) and BN_EPILOGUE != "1":
+                link = None
             if link is not None:
                 dx2, part = C.gemm_nt_bn(dy2, w2, add, True, _rows(link.x), link.ws, link.mask, link.mode, amask,
                                          dsub, h, w)
@@ -488,7 +503,7 @@ class _Conv3x3(torch.autograd.Function):
                 wg = _SideWork(wgrad, dy.shape[0] * dy.shape[2] * dy.shape[3], dy.device)
         if ctx.needs_input_grad[0]:
             if ctx.stride == 1 and x.shape[1] <= CONV3_POLICY["dgrad_native_max_cin"]:
-                link = ctx.link
+                link = ctx.link if BN_EPILOGUE == "1" else None
                 if link is not None:
                     dx, part = C.conv3x3_dgrad_bn(dy, w, None, link.x, link.ws, link.mask, link.mode)
                     link.publish(dx, part)

@@ -21,5 +21,7 @@ run 300 python -u bench.py --force_comm 1 --bucket_mb 0 --steps 10 --warmup 3 --
   --phases_csv $O/fusion_off_times.csv > $O/fusion_off.jsonl 2> $O/fusion_off.err || exit 1
 run 300 python -u bench.py --force_comm 1 --steps 10 --warmup 3 --phases 5 \
   --phases_csv $O/fusion_on_times.csv > $O/fusion_on.jsonl 2> $O/fusion_on.err || exit 1
+run 400 python -u bench.py --gpus 2 --same_device 1 --batch 256 --steps 10 --warmup 3 \
+  > $O/two_ranks_one_gpu.jsonl 2> $O/two_ranks_one_gpu.err || exit 1
 run 600 python -u bench.py --model resnet152 --batch 256 --force_comm 1 --bucket_mb_sweep 0,1,4,8,16,25,64 \
   --steps 10 --warmup 3 > $O/r152_sweep.jsonl 2> $O/r152_sweep.err || exit 1

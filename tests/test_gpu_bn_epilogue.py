@@ -55,7 +55,8 @@ def test_conv3x3_dgrad_bn_partials(cuda):
     torch.testing.assert_close(part.sum(0)[:, 1], (g * (xf - ws[:64])).sum(0), rtol=1e-4, atol=1e-2)
 
 
-def test_resnet_blocks_with_and_without_bn_epilogue(cuda):
+@pytest.mark.parametrize("mode", ["1", "stream"])
+def test_resnet_blocks_with_and_without_bn_epilogue(cuda, mode):
     """Whole ResNet-50 layer stack: the fused path must reproduce the unfused gradients (up to the
     summation order of the per-channel reductions)."""
     from distributed_learning_amd.models import resnet50
@@ -66,7 +67,8 @@ def test_resnet_blocks_with_and_without_bn_epilogue(cuda):
         torch.manual_seed(0)
         m = resnet50(10).to(cuda).to(memory_format=CL)
         dnn.bf16_weights(m)
-        x = torch.randn(4, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+        # 64 x 112 x 112 pixels: the stage-1 data gradients are long enough for the streaming kernel
+        x = torch.randn(64, 3, 224, 224, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
         old = nconv.BN_EPILOGUE
         nconv.BN_EPILOGUE = fused
         try:
@@ -79,7 +81,7 @@ def test_resnet_blocks_with_and_without_bn_epilogue(cuda):
     dnn.set_backend("native")
     dnn.set_native_conv(True)
     try:
-        g1, g0 = run(True), run(False)
+        g1, g0 = run(mode), run("0")
     finally:
         dnn.set_native_conv(False)
         dnn.set_backend("torch")
@@ -115,7 +117,7 @@ def test_residual_handoff_is_exact(cuda):
     dnn.set_backend("native")
     dnn.set_native_conv(True)
     try:
-        g1, g0 = run(True), run(False)
+        g1, g0 = run(mode), run("0")
     finally:
         dnn.set_native_conv(False)
         dnn.set_backend("torch")
