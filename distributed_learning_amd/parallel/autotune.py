@@ -164,14 +164,23 @@ def fit(row: Dict[int, float], esz: int) -> cm.CollectiveModel:
     return cm.CollectiveModel("fit", alpha, beta)
 
 
+# a bucket leaves the model-wide default only for an algorithm faster by more than this fraction: at world 1
+# (and between near-identical schedules) the per-size timings differ by noise, and a noise winner per bucket
+# buys nothing but extra plans (profiles/r4/g03: four 1-rank candidates within 3 % of each other)
+SWITCH_MARGIN = 0.05
+
+
 def choose_per_size(table: Dict[str, Dict[int, float]], ok: Dict[str, bool], sizes: Sequence[int],
-                    default: str) -> Dict[int, str]:
+                    default: str, margin: float = SWITCH_MARGIN) -> Dict[int, str]:
     out = {}
     for n in sizes:
         best, bt = default, math.inf
         for a, row in table.items():
             if ok.get(a) and int(n) in row and row[int(n)] < bt:
                 best, bt = a, row[int(n)]
+        dt = table.get(default, {}).get(int(n))
+        if ok.get(default) and dt is not None and bt >= dt * (1.0 - margin):
+            best = default
         out[int(n)] = best
     return out
 

@@ -1,19 +1,23 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 ``--kernel-trace`` CSV over the steady-state training steps only.
+"""Summarise a rocprofv3 ``--kernel-trace`` (CSV or rocpd .db) over the steady-state training steps only.
 
 The trace of a bench run also contains start-up work (MIOpen find-mode tuning, warm-up steps)
 that dwarfs a training step, so the stock ``kernel_stats.csv`` is useless for step anatomy. Steps
 are delimited by the framework's on-device synthetic-data kernel (one Philox ``uniform_kernel``
 launch per step); the last ``--steps`` steps are aggregated per kernel and per category.
 
-usage: kernel_summary.py TRACE.csv --steps 8 [--out profiles/NAME]
+usage: kernel_summary.py TRACE.csv|TRACE_results.db --steps 8 [--out profiles/NAME]
 """
 from __future__ import annotations
 
 import argparse
-import csv
+import os
 import re
+import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from trace_rows import load_rows  # noqa: E402
 
 CATS = [
     ("conv_wgrad", re.compile(r"wrw|bwd_weight|BwdWeight|conv_bwd_w|conv3x3_wgrad|stem_wgrad", re.I)),
@@ -46,8 +50,8 @@ def main():
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     rows = []
-    with open(a.trace) as f:
-        for r in csv.DictReader(f):
+    if True:
+        for r in load_rows(a.trace):
             grid = "x".join(r.get(k, "?") for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"))
             wg = r.get("Workgroup_Size_X", "?")
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], grid, wg,

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-stream anatomy of the steady-state training steps from a rocprofv3 ``--kernel-trace`` CSV.
+"""Per-stream anatomy of the steady-state training steps from a rocprofv3 ``--kernel-trace`` CSV or rocpd .db.
 
 For each HIP stream (rocprofv3 ``Stream_Id``) over the last ``--steps`` steps (delimited by the
 on-device data kernel, as scripts/kernel_summary.py): busy time (union of its kernels' intervals),
@@ -9,21 +9,17 @@ the late-weight-gradient side stream (ops/conv.py WGRAD_DEFER) and the engine's 
 (gather / staging casts / collectives, csrc/comm/engine.cpp). The question it answers: does the
 gradient path overlap the compute stream, and what does the comm stream cost while it does.
 
-usage: stream_timeline.py TRACE.csv[.gz] --steps 5 [--out FILE.md]
+usage: stream_timeline.py TRACE.csv[.gz]|TRACE_results.db --steps 5 [--out FILE.md]
 """
 from __future__ import annotations
 
 import argparse
-import csv
-import gzip
-import io
+import os
+import sys
 from collections import defaultdict
 
-
-def _open(path):
-    if path.endswith(".gz"):
-        return io.TextIOWrapper(gzip.open(path, "rb"))
-    return open(path)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from trace_rows import load_rows  # noqa: E402
 
 
 def union(iv):
@@ -63,8 +59,8 @@ def main():
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     rows = []
-    with _open(a.trace) as f:
-        for r in csv.DictReader(f):
+    if True:
+        for r in load_rows(a.trace):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r.get("Stream_Id", "?"),
                          r.get("Queue_Id", "?")))
     rows.sort()

@@ -71,7 +71,7 @@ def _tune(rank, world):
     t = at.Autotune(eng, torch.float32, list(COST_US), reps=2, warmup=1)
     at.GRID_MIB = (0.25, 1.0, 4.0)
     t.run_grid()
-    small, large = 1024, 4 << 20
+    small, large = 1024, 16 << 20
     per = t.run_buckets([small, large, small])
     return {"ok": t.ok, "per": per, "best": t.best_model()[0], "report": t.report(),
             "grid": t.grid_table}
@@ -84,7 +84,7 @@ def test_autotune_consistent_verified_and_fastest():
     assert a["ok"]["broken"] is False and a["ok"]["unmappable"] is False
     assert a["ok"]["fast_small"] and a["ok"]["fast_large"]
     assert a["per"][1024] == "fast_small"
-    assert a["per"][4 << 20] == "fast_large"
+    assert a["per"][16 << 20] == "fast_large"
     # the table is the max over ranks: rank 1's simulated costs are 1.5x rank 0's
     row = a["grid"]["fast_small"]
     n = min(row)
@@ -107,3 +107,13 @@ def test_candidates():
     assert "builtin" in c8 and "ring:7" in c8 and "ipc_direct" in c8
     assert "ring:7" not in at.candidates(4, "rccl")
     assert all(not x.startswith("ipc_") for x in at.candidates(2, "ipc"))
+
+
+def test_per_size_choice_keeps_default_within_margin():
+    ok = {"builtin": True, "ring": True, "direct": True, "bad": False}
+    table = {"builtin": {1: 1.00, 2: 1.00, 3: 1.00}, "ring": {1: 0.97, 2: 0.90, 3: 1.02},
+             "direct": {1: 0.99, 2: 0.94}, "bad": {1: 0.10, 2: 0.10, 3: 0.10}}
+    per = at.choose_per_size(table, ok, [1, 2, 3], "builtin")
+    # 3 % faster is noise at the default margin; 10 % faster switches; unverified never wins
+    assert per == {1: "builtin", 2: "ring", 3: "builtin"}
+    assert at.choose_per_size(table, ok, [1], "builtin", margin=0.0) == {1: "ring"}
