@@ -263,6 +263,7 @@ inline int tile_bn(int cfg) {
 }
 // rows of BN-statistics partials ([rows][N][2]) a stats-producing launch writes (one per row tile)
 int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto, int K = 0);
+void set_tile256_min_k(int k);  // smallest K of the auto 256x256 tiles (A/B runs; <= 0 restores the default)
 // Persistent streaming 1x1 GEMM (gemm_stream.hip) for K in {64, 128, 256}, N % 64 == 0, long M: the
 // number of BN-statistics partial rows it writes (0 = shape not served: use launch_gemm_nt), and the
 // launcher (false = not served). set_gemm_stream: -1 environment (DLA_GEMM_STREAM, default on), 0 / 1.

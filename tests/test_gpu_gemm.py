@@ -74,8 +74,9 @@ def test_gemm_nt_kmajor_b_and_addend(cuda, M, N, K):
     assert torch.equal(out_d, out + D)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 8])
-@pytest.mark.parametrize("M,N,K", [(1000, 64, 256), (777, 136, 72), (4096, 512, 128), (1300, 520, 640)])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 8])
+@pytest.mark.parametrize("M,N,K", [(1000, 64, 256), (777, 136, 72), (4096, 512, 128), (1300, 520, 640),
+                                   (70000, 512, 256)])
 def test_gemm_nt_tile_configs(cuda, tile, M, N, K):
     C = _C()
     torch.manual_seed(0)
@@ -87,6 +88,17 @@ def test_gemm_nt_tile_configs(cuda, tile, M, N, K):
     torch.testing.assert_close(stats.sum(0)[:, 0], out.float().sum(0), rtol=1e-4, atol=1e-2 * M ** 0.5)
     outk, _ = C.gemm_nt(A, B.t().contiguous(), False, None, True, tile)
     assert torch.equal(outk, ref)
+
+
+def test_auto_tile_policy():
+    """256x256 tiles from K = 256 (N % 256 == 0, enough tiles to fill the chip), 128-row tiles otherwise."""
+    C = _C()
+    assert C.pick_tile(1003520, 512, 256, True) == 8
+    assert C.pick_tile(250880, 1024, 512, True) == 8
+    assert C.pick_tile(1003520, 128, 512, True) == 1
+    assert C.pick_tile(4014080, 64, 256, True) == 2
+    assert C.pick_tile(1000, 512, 256, True) == 1  # 8 tiles: too few for 256 CUs
+    assert C.pick_tile(1003520, 512, 256, False) == 1
 
 
 @pytest.mark.parametrize("pipe", [0, 2, 3, 4, 5, 6])
