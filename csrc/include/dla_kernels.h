@@ -339,6 +339,7 @@ void launch_conv3x3s2_dgrad(const void* dy, const void* w, void* dx, int N, int 
 // wpk = packed weight [Cout][256] (k = (th * 4 + tw) * 16 + (ph * 2 + pw) * 3 + c, see stem.hip);
 // y [N,OH,OW,Cout] with optional BN-statistics partials stats[stem_stats_rows(P)][Cout][2].
 int stem_stats_rows(int64_t P);
+
 void launch_stem_fold(const void* x, void* xs, int N, int H, int W, hipStream_t stream);
 void launch_stem_fwd(const void* xs, const void* wpk, void* y, int N, int H, int W, int Cout, float* stats,
                      hipStream_t stream);

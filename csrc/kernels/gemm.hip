@@ -277,13 +277,12 @@ bool tile256_enabled() {
   return v;
 }
 
-static int g_tile256_min_k = 256;  // A/B setter (set_tile256_min_k); round 3 used 1024
-void set_tile256_min_k(int k) { g_tile256_min_k = k > 0 ? k : 256; }
+// K >= 256 wins per shape in isolation (profiles/r4/g04) but not in the step (g05: +0.1 ms): 1024 stays
+static int g_tile256_min_k = 1024;  // A/B setter (set_tile256_min_k)
+void set_tile256_min_k(int k) { g_tile256_min_k = k > 0 ? k : 1024; }
 
 int pick_tile(int64_t M, int N, int tile, int K, bool wide_ok) {
   if (tile != kTileAuto) return tile;
-  // 256x256 from K = 256 up: at bs1280 it beats the 128x128 tile on every ResNet-50 1x1 shape with N % 256 == 0
-  // that the streaming kernel does not serve (-4 ... -17 %, profiles/r4/g04/gemm_bs1280.md)
   if (wide_ok && tile256_enabled() && K >= g_tile256_min_k && N % 256 == 0 && ((M + 255) / 256) * (N / 256) >= 192)
     return kTile256x256;
   // the 128-row tiles win at every other ResNet shape, including the small-M layers, so the narrow

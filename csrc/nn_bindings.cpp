@@ -977,7 +977,7 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("lda"), pybind11::arg("ldc"), pybind11::arg("b_kmajor") = false,
         pybind11::arg("add") = false, pybind11::arg("bnb") = false);
   m.def("mfma_pipeline", &mfma_pipeline);
-  m.def("set_tile256_min_k", &set_tile256_min_k, "smallest K of the auto 256x256 gemm_nt / conv tiles (A/B; <= 0 default 256)");
+  m.def("set_tile256_min_k", &set_tile256_min_k, "smallest K of the auto 256x256 gemm_nt / conv tiles (A/B; <= 0 default 1024)");
   m.def("set_tn256", &set_tn256, "256x256 weight-gradient tiles: -1 environment (DLA_TN256, default on), 0 off, 1 on");
   m.def("set_splitk_blocks", &set_splitk_blocks, "split-K weight-gradient block target (0 = default / DLA_SPLITK_BLOCKS)");
   m.def("splitk_target_blocks", &splitk_target_blocks);
