@@ -647,6 +647,32 @@ at::Tensor gemm_tn(at::Tensor A, at::Tensor B, c10::ScalarType out_dtype, double
   return out;
 }
 
+// Data and weight gradient of a stride-1 1x1 conv in one pass over dy (gemm_dual.hip): dy [M, Cout], x [M, Cin]
+// rows, w [Cout, Cin]. Returns (dx [M, Cin] bf16, dw [Cout, Cin] out_dtype), or an empty list when the shape
+// is not served (the caller then runs gemm_nt + gemm_tn).
+std::vector<at::Tensor> conv1x1_dual(at::Tensor dy, at::Tensor x, at::Tensor w, c10::ScalarType out_dtype) {
+  check_mat(dy, "dy");
+  check_mat(x, "x");
+  TORCH_CHECK(w.is_cuda() && w.dim() == 2 && w.scalar_type() == at::kBFloat16 && w.is_contiguous(),
+              "conv1x1_dual: w must be a contiguous bf16 [Cout, Cin] matrix");
+  TORCH_CHECK(dy.size(0) == x.size(0) && w.size(0) == dy.size(1) && w.size(1) == x.size(1), "conv1x1_dual: shapes");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "conv1x1_dual: fp32/bf16 weight gradient");
+  const int64_t M = dy.size(0);
+  const int Cout = (int)dy.size(1), Cin = (int)x.size(1);
+  const int blocks = conv1x1_dual_blocks(M, Cin, Cout);
+  if (!blocks || dy.stride(0) != Cout || x.stride(0) != Cin) return {};
+  at::Tensor dx = at::empty({M, Cin}, dy.options());
+  at::Tensor part = at::empty({(int64_t)blocks * Cout * Cin}, dy.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({Cout, Cin}, dy.options().dtype(out_dtype));
+  hipStream_t st = current_stream(dy);
+  TORCH_CHECK(launch_conv1x1_dual(dy.data_ptr(), x.data_ptr(), w.data_ptr(), dx.data_ptr(), part.data_ptr<float>(), M,
+                                  Cin, Cout, st),
+              "conv1x1_dual: kernel refused a shape it planned");
+  launch_splitk_reduce(part.data_ptr<float>(), blocks, (int64_t)Cout * Cin, dw.data_ptr(),
+                       out_dtype == at::kFloat ? kF32 : kBF16, 1.f, false, st);
+  return {dx, dw};
+}
+
 static int pool_out(int in, int k, int s, int p, bool ceil_mode);
 
 // Stem BatchNorm (training) + ReLU + max-pool: returns (y_pool, ws, pos). x is the BN input
@@ -1025,6 +1051,10 @@ void bind_nn(pybind11::module& m) {
   m.def("halo_conv_eligible", [](int64_t Cin, int64_t Cout, int64_t W, int64_t stride, bool fwd) {
         return halo_conv_eligible((int)Cin, (int)Cout, (int)W, (int)stride, fwd); },
         "whether a 3x3 conv pass runs on the halo-tiled kernel (conv_halo.hip) under the current DLA_HALO mode");
+  m.def("conv1x1_dual_blocks", [](int64_t M, int64_t Cin, int64_t Cout) { return conv1x1_dual_blocks(M, (int)Cin, (int)Cout); },
+        "blocks of the one-pass dgrad + wgrad 1x1 kernel for this shape (0: not served)");
+  m.def("conv1x1_dual", &conv1x1_dual, "stride-1 1x1 conv data + weight gradient in one pass over dy",
+        pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("out_dtype") = at::kFloat);
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),
         pybind11::arg("out_dtype") = at::kFloat, pybind11::arg("scale") = 1.0);
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC", pybind11::arg("x"),

@@ -223,6 +223,11 @@ def _wgrad_after_dgrad(fn, ctx, keep, device: torch.device):
     return out
 
 
+# Both gradients of the stride-1 1x1 convs whose shape gemm_dual.hip serves (stage 1: 64 -> 256 channels) in
+# one pass over dy instead of a data-gradient GEMM and a weight-gradient GEMM that each stream it from HBM.
+DUAL_1X1 = True
+
+
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride: int, want_stats: bool):
@@ -267,6 +272,14 @@ class _Conv1x1(torch.autograd.Function):
             return _as_param_layout(C.gemm_tn(dy2, _rows(x), odt, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
 
         defer = _wants_defer("1x1", ctx, x.shape[1], dy.shape[1])
+        if (DUAL_1X1 and ctx.stride == 1 and ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and not defer
+                and ctx.link is None and x.dtype == torch.bfloat16
+                and C.conv1x1_dual_blocks(dy2.shape[0], x.shape[1], dy.shape[1]) > 0):
+            out = C.conv1x1_dual(dy2, _rows(x), w2, odt)
+            if out:  # one pass over dy for both gradients (gemm_dual.hip)
+                n, cin, h, w = x.shape
+                dx = out[0].view(n, h, w, cin).permute(0, 3, 1, 2)
+                return dx, _as_param_layout(out[1].to(ctx.wdtype), ctx.wshape, ctx.wstride), None, None
         if ctx.needs_input_grad[1] and not defer:
             wg = _SideWork(wgrad, dy2.shape[0], dy.device)
         if ctx.needs_input_grad[0]:

@@ -1,0 +1,77 @@
+"""One-pass data + weight gradient of a stride-1 1x1 conv (csrc/kernels/gemm_dual.hip) vs the separate
+kernels and fp32 PyTorch (gpu).
+
+Shapes: the ResNet-50 stage-1 shape it serves (Cin 64, Cout 256), ragged row counts (last tile partly
+past the end: zero-filled loads, dropped stores), row groups with one tile fewer than others; then the
+conv autograd path with the kernel on and off."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def C():
+    from distributed_learning_amd.ops import _ext
+
+    return _ext.require()
+
+
+@pytest.mark.parametrize("M", [65536, 70001, 200003, 1 << 20])
+@pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
+def test_dual_matches_separate_kernels_and_fp32(cuda, C, M, odt):
+    g = torch.Generator().manual_seed(M)
+    dy = torch.randn(M, 256, generator=g).to(cuda, torch.bfloat16)
+    x = torch.randn(M, 64, generator=g).to(cuda, torch.bfloat16)
+    w = (torch.randn(256, 64, generator=g) * 0.0625).to(cuda, torch.bfloat16)
+    assert C.conv1x1_dual_blocks(M, 64, 256) == 256
+    dx, dw = C.conv1x1_dual(dy, x, w, odt)
+    dx_ref, _ = C.gemm_nt(dy, w, False, None, True)  # the data gradient as the step runs it otherwise
+    torch.cuda.synchronize()
+    ref = dy.float() @ w.float()
+    scale = float(ref.abs().max())
+    assert float((dx.float() - dx_ref.float()).abs().max()) <= scale * 2 ** -7
+    assert float((dx.float() - ref).norm() / ref.norm()) < 5e-3
+    dw_ref = dy.double().t() @ x.double()
+    assert dw.dtype == odt and dw.shape == (256, 64)
+    rel = float((dw.double() - dw_ref).norm() / dw_ref.norm())
+    assert rel < (1e-5 if odt == torch.float32 else 5e-3), rel
+    dw_tn = C.gemm_tn(dy, x, odt, 1.0)
+    assert float((dw.double() - dw_tn.double()).norm() / dw_ref.norm()) < (1e-5 if odt == torch.float32 else 8e-3)
+
+
+def test_dual_not_served_shapes(C):
+    assert C.conv1x1_dual_blocks(1000, 64, 256) == 0  # too few tiles
+    assert C.conv1x1_dual_blocks(1 << 20, 128, 512) == 0
+    assert C.conv1x1_dual_blocks(1 << 20, 256, 64) == 0
+
+
+def test_conv_autograd_uses_dual_and_matches(cuda):
+    """_Conv1x1.backward with the one-pass kernel vs the separate kernels: same data gradient (same
+    MFMA order), weight gradient to fp32 summation-order noise."""
+    import torch.nn as nn
+
+    from distributed_learning_amd.ops import conv as nconv
+
+    torch.manual_seed(0)
+    m = nn.Conv2d(64, 256, 1, bias=False).to(cuda).to(memory_format=torch.channels_last)
+    m.weight.data = m.weight.data.to(torch.bfloat16)
+    x0 = torch.randn(24, 64, 56, 56, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(24, 256, 56, 56, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    def run(flag):
+        old = nconv.DUAL_1X1
+        nconv.DUAL_1X1 = flag
+        try:
+            m.weight.grad = None
+            x = x0.clone().requires_grad_(True)
+            y, _ = nconv.conv1x1(x, m)
+            y.backward(gy)
+            return x.grad.float(), m.weight.grad.float()
+        finally:
+            nconv.DUAL_1X1 = old
+
+    dx1, dw1 = run(True)
+    dx0, dw0 = run(False)
+    assert float((dx1 - dx0).abs().max()) <= float(dx0.abs().max()) * 2 ** -7
+    assert float((dw1 - dw0).norm() / dw0.norm()) < 1e-2
