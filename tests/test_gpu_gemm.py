@@ -97,7 +97,18 @@ def test_auto_tile_policy():
     """256x256 tiles from K = 1024 (N % 256 == 0, enough tiles to fill the chip), 128-row tiles otherwise;
     the threshold setter moves it (A/B runs)."""
     C = _C()
-    assert C.pick_tile(250880, 1024, 512, True) == 8
+    # pick_tile(M, N, K, wide_ok)
+    assert C.pick_tile(250880, 512, 1024, True) == 8
+    assert C.pick_tile(1003520, 256, 512, True) == 1
+    assert C.pick_tile(1003520, 512, 128, True) == 1
+    assert C.pick_tile(4014080, 64, 256, True) == 2
+    assert C.pick_tile(2000, 512, 1024, True) == 1  # 16 tiles: too few for 256 CUs
+    assert C.pick_tile(250880, 512, 1024, False) == 1
+    try:
+        C.set_tile256_min_k(256)
+        assert C.pick_tile(1003520, 512, 256, True) == 8
+    finally:
+        C.set_tile256_min_k(0)
     assert C.pick_tile(1003520, 512, 256, True) == 1
     assert C.pick_tile(1003520, 128, 512, True) == 1
     assert C.pick_tile(4014080, 64, 256, True) == 2
