@@ -304,9 +304,10 @@ void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, floa
                     int K, void* out, int out_dtype, float scale, bool accumulate, hipStream_t stream);
 // out[n] (= scale * sum_s partial[s][n] [+ addend] [+ out]), fp32 or bf16 out; addend: bf16 rows of
 // ncol with row stride ld_addend (0 = one broadcast row).
-// Both gradients of a stride-1 1x1 conv in one pass over dY (gemm_dual.hip; Cin 64, Cout 256): dx [M][64]
-// bf16 and the per-block fp32 dW partials part [blocks][256][64]; 0 blocks = shape not served
+// Both gradients of a stride-1 1x1 conv in one pass over dY (gemm_dual.hip; (Cout, Cin) = (256, 64),
+// (512, 128 / 256)): dx [M][Cin] bf16 and fp32 dW partials part [groups][Cout][Cin]; 0 blocks = not served
 int conv1x1_dual_blocks(int64_t M, int Cin, int Cout);
+int conv1x1_dual_groups(int64_t M, int Cin, int Cout);
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
                          int Cout, hipStream_t stream);
 void launch_splitk_reduce(const float* partial, int splits, int64_t n, void* out, int out_dtype, float scale,

@@ -13,8 +13,8 @@
 //   * weight gradient: the same dY sub-images read transposed (ds_read_b64_tr_b16, K = rows) against the
 //     transposed X image, accumulated in registers over all of the block's tiles; one fp32 [Cout][Cin]
 //     partial per block at the end, summed by splitk_reduce in fixed order (deterministic).
-// LDS: W panel 4 x 8 KB + 3 x 40 KB ring = 152 KB. Wave w: dX rows 16 w .. 16 w + 15 (all 64 ci), dW
-// rows co 64 w .. 64 w + 63 (all 64 ci).
+// Wider Cin is split into 64-channel slices, one block each (the slices of a row group share an XCD's L2
+// for the dY tiles they all read); see DualCfg for the tile / ring shapes.
 #include "dla_common.h"
 #include "dla_kernels.h"
 #include "dla_mfma.h"
@@ -25,29 +25,37 @@ using namespace mm;
 
 namespace {
 
-constexpr int kUR = 64;                      // rows per tile
-constexpr int kUCo = 256;                    // Cout: K of the data gradient
-constexpr int kUCi = 64;                     // Cin
-constexpr int kUKC = kUCo / kBK;             // dY sub-images per tile (4)
-constexpr int kUSub = kUR * kBK;             // elements of one [64][64] sub-image (8 KB)
-constexpr int kUStage = (kUKC + 1) * kUSub;  // dY sub-images + X sub-image
-constexpr int kUNS = 3;                      // ring stages: tiles t+1, t+2 in flight while t is multiplied
-constexpr int kUPanel = kUCi * kBK;          // one W^T sub-image [64 ci][64 co]
-constexpr int kUSlots = kUSub / 8 / 256;     // LDS-DMA slots per thread per sub-image (2)
-constexpr int kULoads = (kUKC + 1) * kUSlots;  // DMA ops per wave per tile (10)
-constexpr int kUStores = 2;                  // dX stores per lane per tile (16 channels = 2 x 16 B)
-constexpr size_t kULds = (size_t)(kUKC * kUPanel + kUNS * kUStage) * sizeof(bf16_t);
-static_assert(kULds <= 160 * 1024, "dual 1x1 LDS budget");
-static_assert(kMS == 16, "fragment maps assume v_mfma_f32_16x16x32_bf16");
+// Shape configurations (CO = Cout, the data gradient's K; the block owns a 64-channel slice of Cin):
+//   CO 256, 64-row tiles, 3-stage ring (Cin 64: stage 1 conv3 / downsample)
+//   CO 512, 32-row tiles, 2-stage ring (Cin 128 / 256: stage 2 conv3 / downsample; the 2 or 4 slice
+//   blocks of a row group sit on one XCD and read the same dY tiles, the later ones from its L2)
+// LDS = CO x 64 weight panel + NS x (CO / 64 + 1) sub-images of R x 64.
+constexpr int kUCi = 64;  // input channels per block (slice)
+template <int CO, int R, int NS>
+struct DualCfg {
+  static constexpr int KC = CO / kBK;                 // dY sub-images per tile
+  static constexpr int Sub = R * kBK;                 // elements of one [R][64] sub-image
+  static constexpr int Stage = (KC + 1) * Sub;        // dY sub-images + the X slice
+  static constexpr int Panel = kUCi * kBK;            // one W^T sub-image [64 ci][64 co]
+  static constexpr int Slots = Sub / 8 / 256;         // LDS-DMA slots per thread per sub-image
+  static constexpr int Loads = (KC + 1) * Slots;      // DMA ops per wave per tile
+  static constexpr int RF = R / 16;                   // 16-row fragments of a tile
+  static constexpr int NCF = RF;                      // data gradient: 16-channel fragments per wave (4 waves)
+  static constexpr int Stores = NCF / 2;              // dX stores per lane per tile (4 NCF channels)
+  static constexpr int TMW = CO / 64;                 // weight gradient: 16-row co fragments per wave
+  static constexpr size_t Lds = (size_t)(KC * Panel + NS * Stage) * sizeof(bf16_t);
+  static_assert(Lds <= 160 * 1024, "dual 1x1 LDS budget");
+  static_assert(Slots >= 1 && (RF == 2 || RF == 4) && (NS == 2 || NS == 3), "tile configuration");
+};
 
 struct DualArgs {
-  const bf16_t* dy;  // [M][256]
-  const bf16_t* x;   // [M][64]
-  const bf16_t* w;   // [256][64]  (W[co][ci], the k-major form of the data gradient)
-  bf16_t* dx;        // [M][64]
-  float* part;       // [grid][256][64]
-  int M;
-  int mg, per_xcd;   // row groups (= blocks), per XCD
+  const bf16_t* dy;  // [M][CO]
+  const bf16_t* x;   // [M][CI]
+  const bf16_t* w;   // [CO][CI]  (W[co][ci], the k-major form of the data gradient)
+  bf16_t* dx;        // [M][CI]
+  float* part;       // [mg][CO][CI]
+  int M, CI;
+  int mg, per_xcd, nsl;  // row groups, row groups per XCD, Cin slices
 };
 
 // image row of panel-local weight row p (gemm_stream.hip): MFMA A-operand row 16 i + 4 g + r holds output
@@ -70,172 +78,195 @@ __device__ __forceinline__ bf16x8_t urm_tr_frag(const bf16_t* s, int c0, int kk)
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
+template <int CO, int R, int NS>
 __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) {
+  using G = DualCfg<CO, R, NS>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  bf16_t* Ws = reinterpret_cast<bf16_t*>(smem_raw);  // kUKC sub-images [64 ci (permuted)][64 co]
-  bf16_t* ring = Ws + kUKC * kUPanel;                 // kUNS stages of kUStage
+  bf16_t* Ws = reinterpret_cast<bf16_t*>(smem_raw);  // KC sub-images [64 ci (permuted)][64 co]
+  bf16_t* ring = Ws + G::KC * G::Panel;               // NS stages
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, g = lane >> 4;
+  // XCD-aware: the nsl slice blocks of one row group are adjacent slots of one XCD
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-  const int grp = xcd * s.per_xcd + slot;
-  const int M = s.M;
-  const int mt = (M + kUR - 1) / kUR;
+  const int sl = slot % s.nsl;
+  const int grp = xcd * s.per_xcd + slot / s.nsl;
+  const int ci0 = sl * kUCi;
+  const int M = s.M, CI = s.CI;
+  const int mt = (M + R - 1) / R;
   const int ntile = grp < mt ? (mt - grp + s.mg - 1) / s.mg : 0;
 
-  // ---- weight panel -> LDS once: W[co][ci] k-major, written transposed and row-permuted ---------------
+  // ---- weight panel -> LDS once: W[co][ci0 .. ci0 + 63] k-major, written transposed and row-permuted ---
   {
-    constexpr int kPer = kUCo * kUCi / 8 / 256;  // 16-byte chunks per thread (8)
+    constexpr int kPer = CO * kUCi / 8 / 256;  // 16-byte chunks per thread
     ushort8_t v[kPer];
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int c = tid + u * 256;
       const int k = c / (kUCi / 8), nc = (c % (kUCi / 8)) * 8;  // columns nc .. nc + 7 of co-row k
-      v[u] = *reinterpret_cast<const ushort8_t*>(s.w + (int64_t)k * kUCi + nc);
+      v[u] = *reinterpret_cast<const ushort8_t*>(s.w + (int64_t)k * CI + ci0 + nc);
     }
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int c = tid + u * 256;
       const int k = c / (kUCi / 8), nc = (c % (kUCi / 8)) * 8;
-      bf16_t* sub = Ws + (k >> 6) * kUPanel;
+      bf16_t* sub = Ws + (k >> 6) * G::Panel;
       const int kk = k & 63;
 #pragma unroll
       for (int e = 0; e < 8; ++e) sub[uimg(uperm64(nc + e), kk >> 3) + (kk & 7)] = v[u][e];
     }
   }
 
-  // ---- ring: tile t -> stage t % kUNS; slot i of a sub-image covers rows 32 i .. 32 i + 31 --------------
-  const __amdgpu_buffer_rsrc_t rdy = make_srd(s.dy, (uint32_t)((int64_t)M * kUCo * 2));
-  const __amdgpu_buffer_rsrc_t rx = make_srd(s.x, (uint32_t)((int64_t)M * kUCi * 2));
-  uint32_t vdy[kUSlots], vx[kUSlots];
-  int vr[kUSlots];
+  // ---- ring: tile t -> stage t % NS; slot i of a sub-image covers rows 32 i .. 32 i + 31 ----------------
+  const __amdgpu_buffer_rsrc_t rdy = make_srd(s.dy, (uint32_t)((int64_t)M * CO * 2));
+  const __amdgpu_buffer_rsrc_t rx = make_srd(s.x, (uint32_t)((int64_t)M * CI * 2));
+  uint32_t vdy[G::Slots], vx[G::Slots];
+  int vr[G::Slots];
 #pragma unroll
-  for (int i = 0; i < kUSlots; ++i) {
+  for (int i = 0; i < G::Slots; ++i) {
     const int c = tid + i * 256, r = c >> 3;
     vr[i] = r;
-    vdy[i] = (uint32_t)((r * kUCo + rm_glds_kc(c)) * 2);
-    vx[i] = (uint32_t)((r * kUCi + rm_glds_kc(c)) * 2);
+    vdy[i] = (uint32_t)((r * CO + rm_glds_kc(c)) * 2);
+    vx[i] = (uint32_t)((r * CI + ci0 + rm_glds_kc(c)) * 2);
   }
   const uint32_t ring0 = lds_addr(ring) + (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
   auto issue = [&](int t) {
-    const int64_t row0 = (int64_t)(grp + t * s.mg) * kUR;  // past the end: every slot OOB (zero-filled)
-    const uint32_t st = ring0 + (uint32_t)((t % kUNS) * kUStage * 2);
-    uint32_t o[kUSlots];
+    const int64_t row0 = (int64_t)(grp + t * s.mg) * R;  // past the end: every slot OOB (zero-filled)
+    const uint32_t st = ring0 + (uint32_t)((t % NS) * G::Stage * 2);
+    uint32_t o[G::Slots];
 #pragma unroll
-    for (int kc = 0; kc < kUKC; ++kc) {
+    for (int kc = 0; kc < G::KC; ++kc) {
 #pragma unroll
-      for (int i = 0; i < kUSlots; ++i) o[i] = row0 + vr[i] < M ? vdy[i] : kOOB;
-      const uint32_t soff = row0 < M ? (uint32_t)((row0 * kUCo + kc * kBK) * 2) : 0u;
-      bglds<kUSlots, 256 * 16>(o, rdy, (uint32_t)__builtin_amdgcn_readfirstlane(soff), st + (uint32_t)(kc * kUSub * 2));
+      for (int i = 0; i < G::Slots; ++i) o[i] = row0 + vr[i] < M ? vdy[i] : kOOB;
+      const uint32_t soff = row0 < M ? (uint32_t)((row0 * CO + kc * kBK) * 2) : 0u;
+      bglds<G::Slots, 256 * 16>(o, rdy, (uint32_t)__builtin_amdgcn_readfirstlane(soff), st + (uint32_t)(kc * G::Sub * 2));
     }
 #pragma unroll
-    for (int i = 0; i < kUSlots; ++i) o[i] = row0 + vr[i] < M ? vx[i] : kOOB;
-    const uint32_t soff = row0 < M ? (uint32_t)(row0 * kUCi * 2) : 0u;
-    bglds<kUSlots, 256 * 16>(o, rx, (uint32_t)__builtin_amdgcn_readfirstlane(soff), st + (uint32_t)(kUKC * kUSub * 2));
+    for (int i = 0; i < G::Slots; ++i) o[i] = row0 + vr[i] < M ? vx[i] : kOOB;
+    const uint32_t soff = row0 < M ? (uint32_t)(row0 * CI * 2) : 0u;
+    bglds<G::Slots, 256 * 16>(o, rx, (uint32_t)__builtin_amdgcn_readfirstlane(soff), st + (uint32_t)(G::KC * G::Sub * 2));
   };
 
   // the panel's plain loads and LDS writes complete before the ring starts counting
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  issue(0);
-  issue(1);
-
-  const __amdgpu_buffer_rsrc_t rc = make_srd(s.dx, (uint32_t)((int64_t)M * kUCi * 2));
-  accv_t aw[4][4];  // dW rows co = 64 wave + 16 i + 4 g + r, columns ci = 16 j + lr
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int t = 0; t < NS - 1; ++t) issue(t);
+
+  const __amdgpu_buffer_rsrc_t rc = make_srd(s.dx, (uint32_t)((int64_t)M * CI * 2));
+  // data gradient of this wave: row fragment rf, channel fragments cf0 .. cf0 + NCF - 1 of the slice
+  const int rf = wave % G::RF, cf0 = (wave / G::RF) * G::NCF;
+  accv_t aw[G::TMW][4];  // dW rows co = (CO / 4) wave + 16 i + 4 g + r, slice columns 16 j + lr
+#pragma unroll
+  for (int i = 0; i < G::TMW; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) aw[i][j] = accv_t{};
 
   for (int t = 0; t < ntile; ++t) {
-    // tile t's DMAs (issued two iterations back) are done once only the younger ones are outstanding, in
-    // issue order L0 L1 | L2 S0 | L3 S1 | ...: the stores of tiles t-2 and t-1 and the loads of tile t+1
-    if (t == 0) vm_wait<kULoads>();
-    else if (t == 1) vm_wait<kULoads + kUStores>();
-    else vm_wait<kULoads + 2 * kUStores>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: stage (t-1) % kUNS is refilled below
+    // tile t's DMAs (issued NS - 1 iterations back) are done once only the younger ones are outstanding;
+    // issue order (NS = 3) L0 L1 | L2 S0 | L3 S1 | ..., (NS = 2) L0 | L1 S0 | L2 S1 | ...
+    if (t >= NS - 1) vm_wait<(NS - 2) * G::Loads + (NS - 1) * G::Stores>();
+    else if (t == 0) vm_wait<(NS - 2) * G::Loads>();
+    else vm_wait<(NS - 2) * G::Loads + G::Stores>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: stage (t-1) % NS is refilled below
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    issue(t + 2);
-    const bf16_t* Ds = ring + (t % kUNS) * kUStage;  // dY sub-images
-    const bf16_t* Xs = Ds + kUKC * kUSub;            // X sub-image
+    issue(t + NS - 1);
+    const bf16_t* Ds = ring + (t % NS) * G::Stage;  // dY sub-images
+    const bf16_t* Xs = Ds + G::KC * G::Sub;         // X slice
 
-    // ---- data gradient: rows 16 wave + lr, all 64 input channels --------------------------------------
-    accv_t ad[4];
+    // ---- data gradient: rows 16 rf + lr, channels of fragments cf0 .. ------------------------------------
+    accv_t ad[G::NCF];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ad[i] = accv_t{};
+    for (int i = 0; i < G::NCF; ++i) ad[i] = accv_t{};
 #pragma unroll
-    for (int kc = 0; kc < kUKC; ++kc) {
+    for (int kc = 0; kc < G::KC; ++kc) {
 #pragma unroll
       for (int kk = 0; kk < kBK / 32; ++kk) {
-        bf16x8_t wf[4];
+        bf16x8_t wf[G::NCF];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) wf[i] = rm_glds_frag(Ws + kc * kUPanel, 16 * i, kk);
-        const bf16x8_t yf = rm_glds_frag(Ds + kc * kUSub, 16 * wave, kk);
+        for (int i = 0; i < G::NCF; ++i) wf[i] = rm_glds_frag(Ws + kc * G::Panel, 16 * (cf0 + i), kk);
+        const bf16x8_t yf = rm_glds_frag(Ds + kc * G::Sub, 16 * rf, kk);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ad[i] = mfma(wf[i], yf, ad[i]);
+        for (int i = 0; i < G::NCF; ++i) ad[i] = mfma(wf[i], yf, ad[i]);
         __builtin_amdgcn_s_setprio(0);
       }
     }
-    // ---- weight gradient: co rows of this wave's dY sub-image, all 64 ci; K = the tile's 64 rows --------
+    // ---- weight gradient: this wave's CO / 4 rows of co, the slice's 64 ci; K = the tile's R rows --------
 #pragma unroll
-    for (int kk = 0; kk < kUR / 32; ++kk) {
-      bf16x8_t af[4], bf[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = urm_tr_frag(Ds + wave * kUSub, 16 * i, kk);
+    for (int kk = 0; kk < R / 32; ++kk) {
+      bf16x8_t bf[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) bf[j] = urm_tr_frag(Xs, 16 * j, kk);
-      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < G::TMW; ++i) {
+        const int co = (CO / 4) * wave + 16 * i;
+        const bf16x8_t af = urm_tr_frag(Ds + (co >> 6) * G::Sub, co & 63, kk);
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) aw[i][j] = mfma(af[i], bf[j], aw[i][j]);
-      __builtin_amdgcn_s_setprio(0);
+        for (int j = 0; j < 4; ++j) aw[i][j] = mfma(af, bf[j], aw[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
     }
-    // ---- dX store: lane (lr, g) holds row 16 wave + lr, channels 16 g .. 16 g + 15 ------------------------
+    // ---- dX store: lane (lr, g) holds row 16 rf + lr, channels 16 g + 4 cf0 .. + 4 NCF - 1 ---------------
     {
-      const int64_t gm = (int64_t)(grp + t * s.mg) * kUR + 16 * wave + lr;
+      const int64_t gm = (int64_t)(grp + t * s.mg) * R + 16 * rf + lr;
       const bool ok = gm < M;
-      uint32_t wv[8];
+      uint32_t wv[2 * G::NCF];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < G::NCF; ++i) {
         wv[2 * i] = (uint32_t)f32_to_bf16(ad[i][0]) | ((uint32_t)f32_to_bf16(ad[i][1]) << 16);
         wv[2 * i + 1] = (uint32_t)f32_to_bf16(ad[i][2]) | ((uint32_t)f32_to_bf16(ad[i][3]) << 16);
       }
-      const uint32_t off = ok ? (uint32_t)((gm * kUCi + 16 * g) * 2) : kOOB;
-      const i32x4_t lo{(int)wv[0], (int)wv[1], (int)wv[2], (int)wv[3]};
-      const i32x4_t hi{(int)wv[4], (int)wv[5], (int)wv[6], (int)wv[7]};
-      __builtin_amdgcn_raw_buffer_store_b128(lo, rc, off, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(hi, rc, ok ? off + 16 : kOOB, 0, 0);
+      const uint32_t off = ok ? (uint32_t)((gm * CI + ci0 + 16 * g + 4 * cf0) * 2) : kOOB;
+#pragma unroll
+      for (int h = 0; h < G::Stores; ++h) {
+        const i32x4_t v{(int)wv[4 * h], (int)wv[4 * h + 1], (int)wv[4 * h + 2], (int)wv[4 * h + 3]};
+        __builtin_amdgcn_raw_buffer_store_b128(v, rc, ok ? off + 16 * h : kOOB, 0, 0);
+      }
     }
   }
   vm_wait<0>();  // no LDS-DMA may land after the block's LDS is released
-  // ---- this block's dW partial: [co][ci] fp32 (blocks without tiles write zeros) --------------------------
-  float* P = s.part + (int64_t)blockIdx.x * kUCo * kUCi;
+  // ---- this row group's dW partial, slice columns: [co][ci0 + ..] fp32 (no tiles: zeros) -----------------
+  float* P = s.part + (int64_t)grp * CO * CI + ci0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < G::TMW; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) P[(64 * wave + 16 * i + 4 * g + r) * kUCi + 16 * j + lr] = aw[i][j][r];
+      for (int r = 0; r < 4; ++r) P[(int64_t)((CO / 4) * wave + 16 * i + 4 * g + r) * CI + 16 * j + lr] = aw[i][j][r];
 }
 
 }  // namespace
 
+// Served shapes (Cout, Cin): (256, 64) and (512, 128 / 256); at least 4 tiles per block.
 int conv1x1_dual_blocks(int64_t M, int Cin, int Cout) {
-  if (Cin != kUCi || Cout != kUCo || M <= 0) return 0;
-  if (M * kUCo * 2 >= (int64_t)kOOB) return 0;
-  const int64_t mt = (M + kUR - 1) / kUR;
-  if (mt < 256 * 4) return 0;  // a few tiles per block at least, or the ring has nothing to overlap
+  if (M <= 0 || Cin % kUCi) return 0;
+  const int nsl = Cin / kUCi;
+  int R;
+  if (Cout == 256 && nsl == 1) R = 64;
+  else if (Cout == 512 && (nsl == 2 || nsl == 4)) R = 32;
+  else return 0;
+  if (M * Cout * 2 >= (int64_t)kOOB || M * Cin * 2 >= (int64_t)kOOB) return 0;
+  const int mg = 256 / nsl;
+  if ((M + R - 1) / R < (int64_t)mg * 4) return 0;  // a few tiles per block, or the ring has nothing to overlap
   return 256;
+}
+
+int conv1x1_dual_groups(int64_t M, int Cin, int Cout) {
+  return conv1x1_dual_blocks(M, Cin, Cout) ? 256 / (Cin / kUCi) : 0;
 }
 
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
                          int Cout, hipStream_t stream) {
   const int grid = conv1x1_dual_blocks(M, Cin, Cout);
   if (!grid) return false;
-  DualArgs a{(const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)dx, part, (int)M, grid, grid / 8};
-  hipLaunchKernelGGL(conv1x1_dual_kernel, dim3(grid), dim3(256), kULds, stream, a);
+  const int nsl = Cin / kUCi, mg = grid / nsl;
+  DualArgs a{(const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)dx, part, (int)M, Cin, mg, mg / 8, nsl};
+  if (Cout == 256)
+    hipLaunchKernelGGL((conv1x1_dual_kernel<256, 64, 3>), dim3(grid), dim3(256), (DualCfg<256, 64, 3>::Lds), stream, a);
+  else
+    hipLaunchKernelGGL((conv1x1_dual_kernel<512, 32, 2>), dim3(grid), dim3(256), (DualCfg<512, 32, 2>::Lds), stream, a);
   return true;
 }
 

@@ -659,16 +659,16 @@ std::vector<at::Tensor> conv1x1_dual(at::Tensor dy, at::Tensor x, at::Tensor w, 
   TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "conv1x1_dual: fp32/bf16 weight gradient");
   const int64_t M = dy.size(0);
   const int Cout = (int)dy.size(1), Cin = (int)x.size(1);
-  const int blocks = conv1x1_dual_blocks(M, Cin, Cout);
-  if (!blocks || dy.stride(0) != Cout || x.stride(0) != Cin) return {};
+  const int groups = conv1x1_dual_groups(M, Cin, Cout);
+  if (!groups || dy.stride(0) != Cout || x.stride(0) != Cin) return {};
   at::Tensor dx = at::empty({M, Cin}, dy.options());
-  at::Tensor part = at::empty({(int64_t)blocks * Cout * Cin}, dy.options().dtype(at::kFloat));
+  at::Tensor part = at::empty({(int64_t)groups * Cout * Cin}, dy.options().dtype(at::kFloat));
   at::Tensor dw = at::empty({Cout, Cin}, dy.options().dtype(out_dtype));
   hipStream_t st = current_stream(dy);
   TORCH_CHECK(launch_conv1x1_dual(dy.data_ptr(), x.data_ptr(), w.data_ptr(), dx.data_ptr(), part.data_ptr<float>(), M,
                                   Cin, Cout, st),
               "conv1x1_dual: kernel refused a shape it planned");
-  launch_splitk_reduce(part.data_ptr<float>(), blocks, (int64_t)Cout * Cin, dw.data_ptr(),
+  launch_splitk_reduce(part.data_ptr<float>(), groups, (int64_t)Cout * Cin, dw.data_ptr(),
                        out_dtype == at::kFloat ? kF32 : kBF16, 1.f, false, st);
   return {dx, dw};
 }

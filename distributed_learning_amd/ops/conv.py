@@ -226,6 +226,7 @@ def _wgrad_after_dgrad(fn, ctx, keep, device: torch.device):
 # Both gradients of the stride-1 1x1 convs whose shape gemm_dual.hip serves (stage 1: 64 -> 256 channels) in
 # one pass over dy instead of a data-gradient GEMM and a weight-gradient GEMM that each stream it from HBM.
 DUAL_1X1 = True
+DUAL_1X1_MAX_COUT = 512  # A/B: 256 keeps it to stage 1
 
 
 class _Conv1x1(torch.autograd.Function):
@@ -272,7 +273,8 @@ class _Conv1x1(torch.autograd.Function):
             return _as_param_layout(C.gemm_tn(dy2, _rows(x), odt, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
 
         defer = _wants_defer("1x1", ctx, x.shape[1], dy.shape[1])
-        if (DUAL_1X1 and ctx.stride == 1 and ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and not defer
+        if (DUAL_1X1 and dy.shape[1] <= DUAL_1X1_MAX_COUT and ctx.stride == 1 and ctx.needs_input_grad[0]
+                and ctx.needs_input_grad[1] and not defer
                 and ctx.link is None and x.dtype == torch.bfloat16
                 and C.conv1x1_dual_blocks(dy2.shape[0], x.shape[1], dy.shape[1]) > 0):
             out = C.conv1x1_dual(dy2, _rows(x), w2, odt)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4, call g06: one-pass 1x1 data + weight gradient (gemm_dual.hip) -- tests, then interleaved A/B x2
-# (default = on; off through scripts/ab_call.py) and a kernel trace of the default
+# (default = stages 1+2; stage 1 only; off -- through scripts/ab_call.py) and a kernel trace of the default
 set -o pipefail
 O=gpurun_out/g06
 mkdir -p $O
@@ -9,6 +9,8 @@ run 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/te
   > $O/pytest.log 2>&1 || exit 1
 for i in 1 2; do
   run 200 python -u bench.py --steps 15 --warmup 5 >> $O/ab_dual.jsonl 2>> $O/ab.err || exit 1
+  run 200 python -u scripts/ab_call.py "from distributed_learning_amd.ops import conv; conv.DUAL_1X1_MAX_COUT = 256" bench.py \
+    --steps 15 --warmup 5 >> $O/ab_dual_s1.jsonl 2>> $O/ab.err || exit 1
   run 200 python -u scripts/ab_call.py "from distributed_learning_amd.ops import conv; conv.DUAL_1X1 = False" bench.py \
     --steps 15 --warmup 5 >> $O/ab_sep.jsonl 2>> $O/ab.err || exit 1
 done

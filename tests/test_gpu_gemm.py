@@ -110,16 +110,6 @@ def test_auto_tile_policy():
     finally:
         C.set_tile256_min_k(0)
     assert C.pick_tile(1003520, 512, 256, True) == 1
-    assert C.pick_tile(1003520, 128, 512, True) == 1
-    assert C.pick_tile(4014080, 64, 256, True) == 2
-    assert C.pick_tile(2000, 512, 1024, True) == 1  # 16 tiles: too few for 256 CUs
-    assert C.pick_tile(250880, 1024, 512, False) == 1
-    try:
-        C.set_tile256_min_k(256)
-        assert C.pick_tile(1003520, 512, 256, True) == 8
-    finally:
-        C.set_tile256_min_k(0)
-    assert C.pick_tile(1003520, 512, 256, True) == 1
 
 
 @pytest.mark.parametrize("pipe", [0, 2, 3, 4, 5, 6])

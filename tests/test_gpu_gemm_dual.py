@@ -1,7 +1,8 @@
 """One-pass data + weight gradient of a stride-1 1x1 conv (csrc/kernels/gemm_dual.hip) vs the separate
 kernels and fp32 PyTorch (gpu).
 
-Shapes: the ResNet-50 stage-1 shape it serves (Cin 64, Cout 256), ragged row counts (last tile partly
+Shapes: the ResNet-50 stage-1 / stage-2 shapes it serves ((Cin, Cout) = (64, 256), (128 / 256, 512), the
+latter as 64-channel slices sharing the dY tiles), ragged row counts (last tile partly
 past the end: zero-filled loads, dropped stores), row groups with one tile fewer than others; then the
 conv autograd path with the kernel on and off."""
 import pytest
@@ -17,14 +18,15 @@ def C():
     return _ext.require()
 
 
-@pytest.mark.parametrize("M", [65536, 70001, 200003, 1 << 20])
+@pytest.mark.parametrize("M,ci,co", [(65536, 64, 256), (70001, 64, 256), (200003, 64, 256), (1 << 20, 64, 256),
+                                     (16384, 128, 512), (50001, 128, 512), (40003, 256, 512), (131072, 256, 512)])
 @pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
-def test_dual_matches_separate_kernels_and_fp32(cuda, C, M, odt):
-    g = torch.Generator().manual_seed(M)
-    dy = torch.randn(M, 256, generator=g).to(cuda, torch.bfloat16)
-    x = torch.randn(M, 64, generator=g).to(cuda, torch.bfloat16)
-    w = (torch.randn(256, 64, generator=g) * 0.0625).to(cuda, torch.bfloat16)
-    assert C.conv1x1_dual_blocks(M, 64, 256) == 256
+def test_dual_matches_separate_kernels_and_fp32(cuda, C, M, ci, co, odt):
+    g = torch.Generator().manual_seed(M + ci)
+    dy = torch.randn(M, co, generator=g).to(cuda, torch.bfloat16)
+    x = torch.randn(M, ci, generator=g).to(cuda, torch.bfloat16)
+    w = (torch.randn(co, ci, generator=g) * co ** -0.5).to(cuda, torch.bfloat16)
+    assert C.conv1x1_dual_blocks(M, ci, co) == 256
     dx, dw = C.conv1x1_dual(dy, x, w, odt)
     dx_ref, _ = C.gemm_nt(dy, w, False, None, True)  # the data gradient as the step runs it otherwise
     torch.cuda.synchronize()
@@ -33,7 +35,7 @@ def test_dual_matches_separate_kernels_and_fp32(cuda, C, M, odt):
     assert float((dx.float() - dx_ref.float()).abs().max()) <= scale * 2 ** -7
     assert float((dx.float() - ref).norm() / ref.norm()) < 5e-3
     dw_ref = dy.double().t() @ x.double()
-    assert dw.dtype == odt and dw.shape == (256, 64)
+    assert dw.dtype == odt and dw.shape == (co, ci)
     rel = float((dw.double() - dw_ref).norm() / dw_ref.norm())
     assert rel < (1e-5 if odt == torch.float32 else 5e-3), rel
     dw_tn = C.gemm_tn(dy, x, odt, 1.0)
@@ -42,8 +44,9 @@ def test_dual_matches_separate_kernels_and_fp32(cuda, C, M, odt):
 
 def test_dual_not_served_shapes(C):
     assert C.conv1x1_dual_blocks(1000, 64, 256) == 0  # too few tiles
-    assert C.conv1x1_dual_blocks(1 << 20, 128, 512) == 0
+    assert C.conv1x1_dual_blocks(1 << 20, 256, 1024) == 0  # weight panel too large for LDS
     assert C.conv1x1_dual_blocks(1 << 20, 256, 64) == 0
+    assert C.conv1x1_dual_blocks(1 << 20, 512, 512) == 0
 
 
 def test_conv_autograd_uses_dual_and_matches(cuda):
