@@ -308,8 +308,12 @@ void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, floa
 // (512, 128 / 256)): dx [M][Cin] bf16 and fp32 dW partials part [groups][Cout][Cin]; 0 blocks = not served
 int conv1x1_dual_blocks(int64_t M, int Cin, int Cout);
 int conv1x1_dual_groups(int64_t M, int Cin, int Cout);
+// ybn / mask / ws: dy is the incoming gradient of the BN(+residual)+ReLU that consumed the conv's output
+// (bit-mask ReLU, finalized workspace); its backward apply runs inside the kernel (Cout 256 only)
+bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout);
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
-                         int Cout, hipStream_t stream);
+                         int Cout, hipStream_t stream, const void* ybn = nullptr, const uint8_t* mask = nullptr,
+                         const float* ws = nullptr);
 void launch_splitk_reduce(const float* partial, int splits, int64_t n, void* out, int out_dtype, float scale,
                           bool accumulate, hipStream_t stream, const void* addend = nullptr, int64_t ld_addend = 0,
                           int ncol = 1);

@@ -31,14 +31,21 @@ namespace {
 //   blocks of a row group sit on one XCD and read the same dY tiles, the later ones from its L2)
 // LDS = CO x 64 weight panel + NS x (CO / 64 + 1) sub-images of R x 64.
 constexpr int kUCi = 64;  // input channels per block (slice)
-template <int CO, int R, int NS>
+// kBN: dY is the backward of the BatchNorm(+residual)+ReLU that consumed the conv's output, applied on the
+// fly: the tile brings the BN's incoming gradient (into the dY slots), its input y and its 1-bit ReLU mask,
+// and a pass over LDS writes dY = k1 (g - m1 - (y - mean) k2), g = masked gradient, over the gradient in
+// place (bn_bwd_apply's arithmetic and rounding) -- dY is never written to HBM.
+constexpr int kUMaskWave = 1024;  // bytes of mask area per wave and stage (the first R / 4 rows x CO / 8 used)
+template <int CO, int R, int NS, bool kBN = false>
 struct DualCfg {
   static constexpr int KC = CO / kBK;                 // dY sub-images per tile
   static constexpr int Sub = R * kBK;                 // elements of one [R][64] sub-image
-  static constexpr int Stage = (KC + 1) * Sub;        // dY sub-images + the X slice
+  static constexpr int MaskElems = kBN ? 4 * kUMaskWave / 2 : 0;
+  static constexpr int Stage = ((kBN ? 2 : 1) * KC + 1) * Sub + MaskElems;  // dY (+ y) sub-images, X slice, mask
   static constexpr int Panel = kUCi * kBK;            // one W^T sub-image [64 ci][64 co]
   static constexpr int Slots = Sub / 8 / 256;         // LDS-DMA slots per thread per sub-image
-  static constexpr int Loads = (KC + 1) * Slots;      // DMA ops per wave per tile
+  static constexpr int Loads = ((kBN ? 2 : 1) * KC + 1) * Slots + (kBN ? 1 : 0);  // DMA ops per wave per tile
+  static_assert(!kBN || (CO * R / 8 / 4 <= 16 * 16 && CO == 256), "BN mask: one 16-lane DMA per wave");
   static constexpr int RF = R / 16;                   // 16-row fragments of a tile
   static constexpr int NCF = RF;                      // data gradient: 16-channel fragments per wave (4 waves)
   static constexpr int Stores = NCF / 2;              // dX stores per lane per tile (4 NCF channels)
@@ -49,13 +56,16 @@ struct DualCfg {
 };
 
 struct DualArgs {
-  const bf16_t* dy;  // [M][CO]
+  const bf16_t* dy;  // [M][CO] (kBN: the BN's incoming gradient)
   const bf16_t* x;   // [M][CI]
   const bf16_t* w;   // [CO][CI]  (W[co][ci], the k-major form of the data gradient)
   bf16_t* dx;        // [M][CI]
   float* part;       // [mg][CO][CI]
   int M, CI;
   int mg, per_xcd, nsl;  // row groups, row groups per XCD, Cin slices
+  const bf16_t* ybn;     // kBN: the BN input [M][CO]
+  const uint8_t* mask;   // kBN: its ReLU bit mask (bit e of byte e >> 3, e = m * CO + c)
+  const float* ws;       // kBN: the finalized 7 CO workspace (mean, ..., k1, m1, k2)
 };
 
 // image row of panel-local weight row p (gemm_stream.hip): MFMA A-operand row 16 i + 4 g + r holds output
@@ -78,9 +88,9 @@ __device__ __forceinline__ bf16x8_t urm_tr_frag(const bf16_t* s, int c0, int kk)
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
-template <int CO, int R, int NS>
+template <int CO, int R, int NS, bool kBN = false>
 __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) {
-  using G = DualCfg<CO, R, NS>;
+  using G = DualCfg<CO, R, NS, kBN>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16_t* Ws = reinterpret_cast<bf16_t*>(smem_raw);  // KC sub-images [64 ci (permuted)][64 co]
   bf16_t* ring = Ws + G::KC * G::Panel;               // NS stages
@@ -119,6 +129,8 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
   // ---- ring: tile t -> stage t % NS; slot i of a sub-image covers rows 32 i .. 32 i + 31 ----------------
   const __amdgpu_buffer_rsrc_t rdy = make_srd(s.dy, (uint32_t)((int64_t)M * CO * 2));
   const __amdgpu_buffer_rsrc_t rx = make_srd(s.x, (uint32_t)((int64_t)M * CI * 2));
+  const __amdgpu_buffer_rsrc_t rybn = make_srd(kBN ? (const void*)s.ybn : (const void*)s.dy, (uint32_t)((int64_t)M * CO * 2));
+  const __amdgpu_buffer_rsrc_t rmsk = make_srd(kBN ? (const void*)s.mask : (const void*)s.dy, (uint32_t)(((int64_t)M * CO + 7) / 8));
   uint32_t vdy[G::Slots], vx[G::Slots];
   int vr[G::Slots];
 #pragma unroll
@@ -140,10 +152,31 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
       const uint32_t soff = row0 < M ? (uint32_t)((row0 * CO + kc * kBK) * 2) : 0u;
       bglds<G::Slots, 256 * 16>(o, rdy, (uint32_t)__builtin_amdgcn_readfirstlane(soff), st + (uint32_t)(kc * G::Sub * 2));
     }
+    if constexpr (kBN) {
+#pragma unroll
+      for (int kc = 0; kc < G::KC; ++kc) {
+#pragma unroll
+        for (int i = 0; i < G::Slots; ++i) o[i] = row0 + vr[i] < M ? vdy[i] : kOOB;
+        const uint32_t soff = row0 < M ? (uint32_t)((row0 * CO + kc * kBK) * 2) : 0u;
+        bglds<G::Slots, 256 * 16>(o, rybn, (uint32_t)__builtin_amdgcn_readfirstlane(soff),
+                                  st + (uint32_t)((G::KC + kc) * G::Sub * 2));
+      }
+    }
+    constexpr int kXs = (kBN ? 2 : 1) * G::KC;  // X slice sub-image index in the stage
 #pragma unroll
     for (int i = 0; i < G::Slots; ++i) o[i] = row0 + vr[i] < M ? vx[i] : kOOB;
     const uint32_t soff = row0 < M ? (uint32_t)(row0 * CI * 2) : 0u;
-    bglds<G::Slots, 256 * 16>(o, rx, (uint32_t)__builtin_amdgcn_readfirstlane(soff), st + (uint32_t)(G::KC * G::Sub * 2));
+    bglds<G::Slots, 256 * 16>(o, rx, (uint32_t)__builtin_amdgcn_readfirstlane(soff), st + (uint32_t)(kXs * G::Sub * 2));
+    if constexpr (kBN) {
+      // mask bytes of the tile: wave w fetches rows R/4 w .. (R / 4 bytes x CO / 8 per row, 16 B per lane)
+      // into its own 1 KB area; the other lanes are out of range and write zeros behind them
+      constexpr int kWaveBytes = R / 4 * CO / 8;
+      const int64_t mrow = row0 + (R / 4) * wave + lane * 16 / (CO / 8);  // the row this lane's 16 bytes belong to
+      uint32_t om[1] = {lane * 16 < kWaveBytes && mrow < M ? (uint32_t)(lane * 16) : kOOB};
+      const uint32_t msoff = row0 < M ? (uint32_t)(row0 * CO / 8 + wave * kWaveBytes) : 0u;
+      bglds<1, 0>(om, rmsk, (uint32_t)__builtin_amdgcn_readfirstlane(msoff),
+                  st - (uint32_t)(wave * 64 * 16) + (uint32_t)((kXs + 1) * G::Sub * 2) + (uint32_t)(wave * kUMaskWave));
+    }
   };
 
   // the panel's plain loads and LDS writes complete before the ring starts counting
@@ -153,6 +186,19 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
   for (int t = 0; t < NS - 1; ++t) issue(t);
 
   const __amdgpu_buffer_rsrc_t rc = make_srd(s.dx, (uint32_t)((int64_t)M * CI * 2));
+  // kBN: this thread's 8 channels (chunk column tid % (CO / 8)) in every row it converts
+  constexpr int kCpr = CO / 8;  // 8-channel chunks per row
+  float bmean[kBN ? 8 : 1], bk1[kBN ? 8 : 1], bm1[kBN ? 8 : 1], bk2[kBN ? 8 : 1];
+  if constexpr (kBN) {
+    const int c0 = (tid % kCpr) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bmean[j] = s.ws[c0 + j];
+      bk1[j] = s.ws[4 * CO + c0 + j];
+      bm1[j] = s.ws[5 * CO + c0 + j];
+      bk2[j] = s.ws[6 * CO + c0 + j];
+    }
+  }
   // data gradient of this wave: row fragment rf, channel fragments cf0 .. cf0 + NCF - 1 of the slice
   const int rf = wave % G::RF, cf0 = (wave / G::RF) * G::NCF;
   accv_t aw[G::TMW][4];  // dW rows co = (CO / 4) wave + 16 i + 4 g + r, slice columns 16 j + lr
@@ -171,8 +217,34 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     issue(t + NS - 1);
-    const bf16_t* Ds = ring + (t % NS) * G::Stage;  // dY sub-images
-    const bf16_t* Xs = Ds + G::KC * G::Sub;         // X slice
+    bf16_t* Ds = ring + (t % NS) * G::Stage;                 // dY sub-images
+    const bf16_t* Xs = Ds + (kBN ? 2 : 1) * G::KC * G::Sub;  // X slice
+    if constexpr (kBN) {
+      // dY = k1 (g - m1 - (y - mean) k2) over the gradient in place; g = the gradient where the mask bit is set
+      const bf16_t* Ys = Ds + G::KC * G::Sub;
+      const uint8_t* Ms = reinterpret_cast<const uint8_t*>(Xs + G::Sub);
+      constexpr int kPer = R * kCpr / 256;  // chunks per thread
+      const int cg = tid % kCpr, sub = cg >> 3, lc = cg & 7;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const int r = tid / kCpr + k * (256 / kCpr);
+        const int o = sub * G::Sub + uimg(r, lc);
+        const ushort8_t gv = *reinterpret_cast<const ushort8_t*>(Ds + o);
+        const ushort8_t yv = *reinterpret_cast<const ushort8_t*>(Ys + o);
+        const uint32_t bits = Ms[(r / (R / 4)) * kUMaskWave + (r % (R / 4)) * kCpr + cg];
+        ushort8_t out;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float g = ((bits >> j) & 1u) ? bf16_to_f32((bf16_t)gv[j]) : 0.f;
+          const float y = bf16_to_f32((bf16_t)yv[j]);
+          out[j] = f32_to_bf16(bk1[j] * (g - bm1[j] - (y - bmean[j]) * bk2[j]));
+        }
+        *reinterpret_cast<ushort8_t*>(Ds + o) = out;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
 
     // ---- data gradient: rows 16 rf + lr, channels of fragments cf0 .. ------------------------------------
     accv_t ad[G::NCF];
@@ -257,12 +329,21 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout) {
   return conv1x1_dual_blocks(M, Cin, Cout) ? 256 / (Cin / kUCi) : 0;
 }
 
+bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout) { return Cout == 256 && conv1x1_dual_blocks(M, Cin, Cout) > 0; }
+
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
-                         int Cout, hipStream_t stream) {
+                         int Cout, hipStream_t stream, const void* ybn, const uint8_t* mask, const float* ws) {
   const int grid = conv1x1_dual_blocks(M, Cin, Cout);
   if (!grid) return false;
   const int nsl = Cin / kUCi, mg = grid / nsl;
-  DualArgs a{(const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)dx, part, (int)M, Cin, mg, mg / 8, nsl};
+  DualArgs a{(const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)dx, part, (int)M, Cin, mg, mg / 8, nsl,
+             (const bf16_t*)ybn, mask, ws};
+  if (ybn) {
+    if (!conv1x1_dual_bn_ok(M, Cin, Cout) || !mask || !ws) return false;
+    hipLaunchKernelGGL((conv1x1_dual_kernel<256, 32, 3, true>), dim3(grid), dim3(256), (DualCfg<256, 32, 3, true>::Lds),
+                       stream, a);
+    return true;
+  }
   if (Cout == 256)
     hipLaunchKernelGGL((conv1x1_dual_kernel<256, 64, 3>), dim3(grid), dim3(256), (DualCfg<256, 64, 3>::Lds), stream, a);
   else

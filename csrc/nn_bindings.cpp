@@ -209,7 +209,8 @@ std::vector<at::Tensor> bn_dual_bwd(at::Tensor dy, c10::optional<at::Tensor> mas
 // 1 recompute the ReLU branch from x, 2 use `mask` from bn_act_fwd, 3 use the saved output `y`.
 std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, c10::optional<at::Tensor> mask,
                                    at::Tensor x, at::Tensor ws, c10::optional<at::Tensor> weight, int64_t mask_mode,
-                                   bool need_dres, c10::optional<at::Tensor> ext_part) {
+                                   bool need_dres, c10::optional<at::Tensor> ext_part, bool want_dx) {
+  TORCH_CHECK(want_dx || !need_dres, "bn_act_bwd: the residual gradient comes from the apply pass");
   check_act(x, "x");
   const int C = (int)x.size(1);
   const int64_t M = rows_of(x);
@@ -247,11 +248,12 @@ std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, c
                     ext_part->size(1) == C && ext_part->size(2) == 2,
                 "ext_part must be fp32 [rows, C, 2] (sum dy', sum dy'(x-mean)) partials");
   at::Tensor part = at::empty({ext ? 1 : partial_floats(M, C)}, f32);
-  at::Tensor dx = at::empty_like(x);
+  // want_dx = false: reduction + finalize only (ws then holds the apply coefficients for a fused consumer)
+  at::Tensor dx = want_dx ? at::empty_like(x) : at::Tensor();
   at::Tensor dres = need_dres ? at::empty_like(x) : at::Tensor();
   at::Tensor dg = at::empty({C}, f32), db = at::empty({C}, f32);
   const float* g = (weight.has_value() && weight->defined()) ? weight->data_ptr<float>() : nullptr;
-  launch_bn_bwd(dy.data_ptr(), yp, mp, x.data_ptr(), dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr, M, C,
+  launch_bn_bwd(dy.data_ptr(), yp, mp, x.data_ptr(), want_dx ? dx.data_ptr() : nullptr, need_dres ? dres.data_ptr() : nullptr, M, C,
                 dtype_code(x), g, ws.data_ptr<float>(), part.data_ptr<float>(), dg.data_ptr<float>(),
                 db.data_ptr<float>(), (int)mask_mode, current_stream(x), ext ? ext_part->data_ptr<float>() : nullptr,
                 ext ? (int)ext_part->size(0) : 0, ld_dy);
@@ -650,7 +652,11 @@ at::Tensor gemm_tn(at::Tensor A, at::Tensor B, c10::ScalarType out_dtype, double
 // Data and weight gradient of a stride-1 1x1 conv in one pass over dy (gemm_dual.hip): dy [M, Cout], x [M, Cin]
 // rows, w [Cout, Cin]. Returns (dx [M, Cin] bf16, dw [Cout, Cin] out_dtype), or an empty list when the shape
 // is not served (the caller then runs gemm_nt + gemm_tn).
-std::vector<at::Tensor> conv1x1_dual(at::Tensor dy, at::Tensor x, at::Tensor w, c10::ScalarType out_dtype) {
+// With y_bn (+ ws, mask): dy is the incoming gradient of the BN(+residual)+ReLU whose input y_bn is this conv's
+// output; its backward apply (bit-mask ReLU, finalized ws) runs inside the kernel.
+std::vector<at::Tensor> conv1x1_dual(at::Tensor dy, at::Tensor x, at::Tensor w, c10::ScalarType out_dtype,
+                                     c10::optional<at::Tensor> y_bn, c10::optional<at::Tensor> ws,
+                                     c10::optional<at::Tensor> mask) {
   check_mat(dy, "dy");
   check_mat(x, "x");
   TORCH_CHECK(w.is_cuda() && w.dim() == 2 && w.scalar_type() == at::kBFloat16 && w.is_contiguous(),
@@ -661,12 +667,24 @@ std::vector<at::Tensor> conv1x1_dual(at::Tensor dy, at::Tensor x, at::Tensor w, 
   const int Cout = (int)dy.size(1), Cin = (int)x.size(1);
   const int groups = conv1x1_dual_groups(M, Cin, Cout);
   if (!groups || dy.stride(0) != Cout || x.stride(0) != Cin) return {};
+  const bool bn = y_bn.has_value() && y_bn->defined();
+  if (bn) {
+    if (!conv1x1_dual_bn_ok(M, Cin, Cout)) return {};
+    check_mat(*y_bn, "y_bn");
+    TORCH_CHECK(y_bn->sizes() == dy.sizes() && y_bn->stride(0) == Cout, "conv1x1_dual: y_bn must be laid out like dy");
+    TORCH_CHECK(ws.has_value() && ws->scalar_type() == at::kFloat && ws->is_contiguous() && ws->numel() == 7 * Cout,
+                "conv1x1_dual: ws must be the BN's finalized 7C workspace");
+    TORCH_CHECK(mask.has_value() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                    mask->numel() * 8 >= M * Cout,
+                "conv1x1_dual: the BN's 1-bit ReLU mask");
+  }
   at::Tensor dx = at::empty({M, Cin}, dy.options());
   at::Tensor part = at::empty({(int64_t)groups * Cout * Cin}, dy.options().dtype(at::kFloat));
   at::Tensor dw = at::empty({Cout, Cin}, dy.options().dtype(out_dtype));
   hipStream_t st = current_stream(dy);
   TORCH_CHECK(launch_conv1x1_dual(dy.data_ptr(), x.data_ptr(), w.data_ptr(), dx.data_ptr(), part.data_ptr<float>(), M,
-                                  Cin, Cout, st),
+                                  Cin, Cout, st, bn ? y_bn->data_ptr() : nullptr,
+                                  bn ? mask->data_ptr<uint8_t>() : nullptr, bn ? ws->data_ptr<float>() : nullptr),
               "conv1x1_dual: kernel refused a shape it planned");
   launch_splitk_reduce(part.data_ptr<float>(), groups, (int64_t)Cout * Cin, dw.data_ptr(),
                        out_dtype == at::kFloat ? kF32 : kBF16, 1.f, false, st);
@@ -1054,7 +1072,11 @@ void bind_nn(pybind11::module& m) {
   m.def("conv1x1_dual_blocks", [](int64_t M, int64_t Cin, int64_t Cout) { return conv1x1_dual_blocks(M, (int)Cin, (int)Cout); },
         "blocks of the one-pass dgrad + wgrad 1x1 kernel for this shape (0: not served)");
   m.def("conv1x1_dual", &conv1x1_dual, "stride-1 1x1 conv data + weight gradient in one pass over dy",
-        pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("out_dtype") = at::kFloat);
+        pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("out_dtype") = at::kFloat,
+        pybind11::arg("y_bn") = pybind11::none(), pybind11::arg("ws") = pybind11::none(),
+        pybind11::arg("mask") = pybind11::none());
+  m.def("conv1x1_dual_bn_ok", [](int64_t M, int64_t Cin, int64_t Cout) { return conv1x1_dual_bn_ok(M, (int)Cin, (int)Cout); },
+        "the one-pass 1x1 gradient kernel can also apply the consuming BN's backward for this shape");
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),
         pybind11::arg("out_dtype") = at::kFloat, pybind11::arg("scale") = 1.0);
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC", pybind11::arg("x"),
@@ -1072,7 +1094,8 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("exts") = std::vector<at::Tensor>{}, pybind11::arg("dx_out") = std::vector<at::Tensor>{});
   m.def("bn_act_bwd", &bn_act_bwd, "fused BatchNorm(+residual)(+ReLU) backward, NHWC", pybind11::arg("dy"),
         pybind11::arg("y"), pybind11::arg("mask"), pybind11::arg("x"), pybind11::arg("ws"), pybind11::arg("weight"),
-        pybind11::arg("mask_mode"), pybind11::arg("need_dres"), pybind11::arg("ext_part") = pybind11::none());
+        pybind11::arg("mask_mode"), pybind11::arg("need_dres"), pybind11::arg("ext_part") = pybind11::none(),
+        pybind11::arg("want_dx") = true);
 }
 
 }  // namespace dla

@@ -70,7 +70,7 @@ def bn_link_of(t: torch.Tensor):
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu, stats,
-                rlink=None):
+                rlink=None, dlink=None):
         C = _ext.require()
         y, ws, mask = C.bn_act_fwd(x, residual, weight, bias, running_mean, running_var, training, momentum, eps,
                                    relu, stats)
@@ -83,6 +83,10 @@ class _BNAct(torch.autograd.Function):
         m = mask if mask is not None and mask.numel() else None
         ctx.save_for_backward(x, ws, weight, m)
         ctx.link = BNLink(x, ws, m, ctx.mask_mode) if training and x.dtype == torch.bfloat16 else None
+        # the producing 1x1 conv applies this BN's backward itself (ops/conv.py DualBNLink): bit-mask ReLU
+        # after the residual add, residual gradient handed to the fork, bf16
+        ctx.dlink = dlink if (dlink is not None and ctx.rlink is not None and ctx.mask_mode == MASK_BITS
+                              and m is not None and x.dtype == torch.bfloat16) else None
         return y
 
     @staticmethod
@@ -93,6 +97,15 @@ class _BNAct(torch.autograd.Function):
         C = _ext.require()
         ext = ctx.link.take(dy) if ctx.link is not None else None
         rl = ctx.rlink
+        if ctx.dlink is not None and rl is not None:
+            # reduction + finalize only; the conv backward applies (dy, x, mask, ws) in its own kernel
+            dy = dy.contiguous(memory_format=torch.channels_last)
+            _, _, dg, db = C.bn_act_bwd(dy, None, mask, x, ws, weight, ctx.mask_mode, False, ext, False)
+            dx = ctx.dlink.park(dy, x, ws, mask, weight)
+            rl.dy, rl.mask = dy, mask
+            need = ctx.needs_input_grad
+            return (dx, dg if need[1] else None, db if need[2] else None, None,
+                    None, None, None, None, None, None, None, None, None)
         dx, dres, dg, db = C.bn_act_bwd(dy, None, mask, x, ws, weight, ctx.mask_mode, ctx.has_res and rl is None, ext)
         if rl is not None:  # the forking conv adds dy (masked) in its dgrad epilogue
             rl.dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
@@ -100,7 +113,7 @@ class _BNAct(torch.autograd.Function):
             dres = None
         need = ctx.needs_input_grad
         return (dx, dg if need[1] else None, db if need[2] else None, dres if ctx.has_res else None,
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None)
 
 
 class _BNDualAct(torch.autograd.Function):
@@ -201,8 +214,9 @@ def fused_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residua
     rlink = fork_link_of(residual)
     if rlink is not None and residual.dtype != torch.bfloat16:  # the epilogue addend is bf16
         rlink = None
+    dlink = getattr(x, "_dla_dual", None) if (training and rlink is not None) else None
     y = _BNAct.apply(x, bn.weight, bn.bias, residual, rm, rv, training, float(bn.momentum or 0.0),
-                     float(bn.eps), relu, stats if training else None, rlink)
+                     float(bn.eps), relu, stats if training else None, rlink, dlink)
     if y.grad_fn is not None:
         link = getattr(y.grad_fn, "link", None)
         if link is not None:

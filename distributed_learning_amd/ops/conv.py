@@ -227,6 +227,34 @@ def _wgrad_after_dgrad(fn, ctx, keep, device: torch.device):
 # one pass over dy instead of a data-gradient GEMM and a weight-gradient GEMM that each stream it from HBM.
 DUAL_1X1 = True
 DUAL_1X1_MAX_COUT = 512  # A/B: 256 keeps it to stage 1
+# ... and, where its output feeds a BN(+residual)+ReLU with a bit mask (the block's last BN), that BN's
+# backward apply inside the same kernel: the BN backward stops after its reduction and hands (dy, y, mask,
+# coefficients) over; dY never reaches HBM (gemm_dual.hip kBN).
+DUAL_BN = True
+
+
+class DualBNLink:
+    """Hand-off from the BN(+residual)+ReLU consuming a 1x1 conv's output to that conv's backward.
+
+    The BN backward returns a zero-stride placeholder as its input gradient and parks its incoming gradient,
+    input, mask and finalized coefficients here; the conv backward recognises the placeholder and runs the
+    one-pass kernel with the BN apply fused. If autograd summed the placeholder with other gradients of the
+    conv output (more consumers), the conv backward materialises the BN's gradient and adds it."""
+
+    __slots__ = ("ph", "dout", "ybn", "ws", "mask", "weight")
+
+    def __init__(self):
+        self.ph = self.dout = self.ybn = self.ws = self.mask = self.weight = None
+
+    def park(self, dout, ybn, ws, mask, weight):
+        self.dout, self.ybn, self.ws, self.mask, self.weight = dout, ybn, ws, mask, weight
+        self.ph = torch.zeros((), dtype=ybn.dtype, device=ybn.device).expand(ybn.shape)
+        return self.ph
+
+    def take(self):
+        out = (self.ph, self.dout, self.ybn, self.ws, self.mask, self.weight)
+        self.ph = self.dout = self.ybn = self.ws = self.mask = self.weight = None
+        return out
 
 
 class _Conv1x1(torch.autograd.Function):
@@ -244,6 +272,8 @@ class _Conv1x1(torch.autograd.Function):
         y2, stats = C.gemm_nt(_rows(x), w2, want_stats)
         y = y2.view(n, h, w, cout).permute(0, 3, 1, 2)
         ctx.save_for_backward(x, w2)
+        ctx.dlink = DualBNLink() if (DUAL_1X1 and DUAL_BN and stride == 1 and x.dtype == torch.bfloat16
+                                     and C.conv1x1_dual_bn_ok(n * h * w, cin, cout)) else None
         ctx.stride = stride
         ctx.in_hw = None
         ctx.wdtype = weight.dtype
@@ -255,10 +285,26 @@ class _Conv1x1(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dstats):
-        if dy is None:
-            return None, None, None, None
         C = _ext.require()
         x, w2 = ctx.saved_tensors
+        odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
+        dl = ctx.dlink
+        if dl is not None and dl.ph is not None:
+            ph, dout, ybn, ws, mask, weight = dl.take()
+            if (dy is not None and dy.data_ptr() == ph.data_ptr() and dy.stride() == ph.stride()
+                    and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
+                    and not _wants_defer("1x1", ctx, x.shape[1], ybn.shape[1])):
+                out = C.conv1x1_dual(_rows(dout), _rows(x), w2, odt, _rows(ybn), ws, mask)
+                if out:  # BN apply + data gradient + weight gradient, one pass over the BN's gradient
+                    CALLS["1x1_dual_bn"] += 1
+                    n, cin, h, w = x.shape
+                    dx = out[0].view(n, h, w, cin).permute(0, 3, 1, 2)
+                    return dx, _as_param_layout(out[1].to(ctx.wdtype), ctx.wshape, ctx.wstride), None, None
+            # materialise the BN's input gradient (its reduction is re-run: ws is recomputed identically)
+            dbn = C.bn_act_bwd(dout, None, mask, ybn, ws, weight, 2, False, None)[0]
+            dy = dbn if (dy is None or (dy.data_ptr() == ph.data_ptr() and dy.stride() == ph.stride())) else dy + dbn
+        if dy is None:
+            return None, None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
         if dy.dtype != torch.bfloat16:
             dy = dy.to(torch.bfloat16)
@@ -267,7 +313,6 @@ class _Conv1x1(torch.autograd.Function):
         wg = None
         if WGRAD_JOIN == "conv":
             join_compute(dy.device)
-        odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
 
         def wgrad():
             return _as_param_layout(C.gemm_tn(dy2, _rows(x), odt, 1.0).to(ctx.wdtype), ctx.wshape, ctx.wstride)
@@ -279,6 +324,7 @@ class _Conv1x1(torch.autograd.Function):
                 and C.conv1x1_dual_blocks(dy2.shape[0], x.shape[1], dy.shape[1]) > 0):
             out = C.conv1x1_dual(dy2, _rows(x), w2, odt)
             if out:  # one pass over dy for both gradients (gemm_dual.hip)
+                CALLS["1x1_dual"] += 1
                 n, cin, h, w = x.shape
                 dx = out[0].view(n, h, w, cin).permute(0, 3, 1, 2)
                 return dx, _as_param_layout(out[1].to(ctx.wdtype), ctx.wshape, ctx.wstride), None, None
@@ -439,7 +485,11 @@ def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False, stride: 
     if x.shape[2] % s or x.shape[3] % s:
         # odd spatial size with stride 2 (output ceil) — keep F.conv2d semantics exactly
         return F.conv2d(x, conv.weight.to(x.dtype), None, s), None
-    return _Conv1x1.apply(x, conv.weight, s, want_stats)
+    y, stats = _Conv1x1.apply(x, conv.weight, s, want_stats)
+    dl = getattr(y.grad_fn, "dlink", None) if y.grad_fn is not None else None
+    if dl is not None:
+        y._dla_dual = dl
+    return y, stats
 
 
 # ---------------------------------------------------------------------------------------------

@@ -78,3 +78,69 @@ def test_conv_autograd_uses_dual_and_matches(cuda):
     dx0, dw0 = run(False)
     assert float((dx1 - dx0).abs().max()) <= float(dx0.abs().max()) * 2 ** -7
     assert float((dw1 - dw0).norm() / dw0.norm()) < 1e-2
+
+
+@pytest.mark.parametrize("M", [65536, 100003])
+def test_dual_with_bn_apply_matches_separate(cuda, C, M):
+    """kBN: the consuming BN(+residual)+ReLU's backward apply inside the kernel (gradient, BN input, bit mask,
+    finalized coefficients) == bn_act_bwd's apply pass followed by the plain one-pass kernel."""
+    g = torch.Generator().manual_seed(M)
+    dout = torch.randn(M, 256, generator=g).to(cuda, torch.bfloat16)
+    ybn = (torch.randn(M, 256, generator=g) * 2 + 0.5).to(cuda, torch.bfloat16)
+    x = torch.randn(M, 64, generator=g).to(cuda, torch.bfloat16)
+    w = (torch.randn(256, 64, generator=g) * 0.0625).to(cuda, torch.bfloat16)
+    mask = torch.randint(0, 256, ((M * 256 + 7) // 8,), generator=g, dtype=torch.uint8).to(cuda)
+    gamma = (torch.rand(256, generator=g) + 0.5).to(cuda)
+    yf = ybn.float()
+    ws = torch.zeros(7 * 256, device=cuda)
+    ws[:256] = yf.mean(0)
+    ws[256:512] = (yf.var(0, unbiased=False) + 1e-5).rsqrt()
+    ws_a, ws_b = ws.clone(), ws.clone()
+    assert C.conv1x1_dual_bn_ok(M, 64, 256)
+    dY, _, dg, db = C.bn_act_bwd(dout, None, mask, ybn, ws_a, gamma, 2, False, None)
+    dx_ref, dw_ref = C.conv1x1_dual(dY, x, w, torch.float32)
+    _, _, dg2, db2 = C.bn_act_bwd(dout, None, mask, ybn, ws_b, gamma, 2, False, None, False)
+    dx, dw = C.conv1x1_dual(dout, x, w, torch.float32, ybn, ws_b, mask)
+    torch.cuda.synchronize()
+    assert torch.equal(ws_a, ws_b) and torch.equal(dg, dg2) and torch.equal(db, db2)
+    scale = float(dx_ref.float().abs().max())
+    assert float((dx.float() - dx_ref.float()).abs().max()) <= scale * 2 ** -7
+    ref = dY.float() @ w.float()
+    assert float((dx.float() - ref).norm() / ref.norm()) < 5e-3
+    assert float((dw - dw_ref).norm() / dw_ref.norm()) < 1e-5
+
+
+def test_resnet_layer1_with_and_without_fused_bn_apply(cuda):
+    """Whole ResNet-50 step: the BN-apply hand-off (BN backward stops after its reduction, the conv3 backward
+    applies it inside the one-pass kernel) reproduces the unfused gradients up to fp32 summation order."""
+    from distributed_learning_amd.models import resnet50
+    from distributed_learning_amd.ops import conv as nconv
+    from distributed_learning_amd.ops import nn as dnn
+
+    CL = torch.channels_last
+
+    def run(flag):
+        torch.manual_seed(0)
+        m = resnet50(10).to(cuda).to(memory_format=CL)
+        dnn.bf16_weights(m)
+        x = torch.randn(24, 3, 224, 224, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+        old = nconv.DUAL_BN
+        nconv.DUAL_BN = flag
+        before = nconv.CALLS["1x1_dual_bn"]
+        try:
+            m(x).float().square().mean().backward()
+        finally:
+            nconv.DUAL_BN = old
+        # stage-1 blocks 1 and 2 (block 0's last BN is the dual BN with the downsample)
+        assert (nconv.CALLS["1x1_dual_bn"] - before == 2) == flag
+        return {n: p.grad.float().clone() for n, p in m.named_parameters()}
+
+    dnn.set_backend("native")
+    dnn.set_native_conv(True)
+    try:
+        g1, g0 = run(True), run(False)
+    finally:
+        dnn.set_native_conv(False)
+        dnn.set_backend("torch")
+    rels = sorted(float((g1[n] - g0[n]).norm() / g0[n].norm().clamp_min(1e-20)) for n in g0)
+    assert rels[len(rels) // 2] < 2e-2 and rels[-1] < 0.2, rels[-5:]
