@@ -117,7 +117,7 @@ def test_residual_handoff_is_exact(cuda):
     dnn.set_backend("native")
     dnn.set_native_conv(True)
     try:
-        g1, g0 = run(mode), run("0")
+        g1, g0 = run(True), run(False)
     finally:
         dnn.set_native_conv(False)
         dnn.set_backend("torch")
