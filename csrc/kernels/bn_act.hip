@@ -1309,6 +1309,7 @@ void launch_bn_dual_bwd(const void* dy, const uint8_t* mask, const void* x, cons
                      dgamma, dbeta);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, fpd, frd, M, C, gamma_d,
                      wsd, dgamma_d, dbeta_d);
+  if (!dx) return;  // finalize only: both consumers apply the coefficients themselves (gemm_dual.hip kBN)
   int atpr, anrb, anct;
   bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
 #define DLA_DUAL_APPLY(T, K)                                                                                      \

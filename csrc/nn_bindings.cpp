@@ -175,7 +175,7 @@ std::vector<at::Tensor> bn_dual_fwd(at::Tensor x, at::Tensor xd, c10::optional<a
 // Backward of bn_dual_fwd: returns (dx, dgamma, dbeta, dxd, dgamma_d, dbeta_d).
 std::vector<at::Tensor> bn_dual_bwd(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x, at::Tensor ws,
                                     c10::optional<at::Tensor> weight, at::Tensor xd, at::Tensor wsd,
-                                    c10::optional<at::Tensor> weight_d) {
+                                    c10::optional<at::Tensor> weight_d, bool want_dx) {
   dy = dy.dim() == 4 ? dy.contiguous(at::MemoryFormat::ChannelsLast) : dy.contiguous();
   check_act(dy, "dy");
   check_act(x, "x");
@@ -193,12 +193,14 @@ std::vector<at::Tensor> bn_dual_bwd(at::Tensor dy, c10::optional<at::Tensor> mas
   }
   auto f32 = x.options().dtype(at::kFloat);
   at::Tensor part = at::empty({partial_floats(M, C)}, f32), partd = at::empty({partial_floats(M, C)}, f32);
-  at::Tensor dx = at::empty_like(x), dxd = at::empty_like(xd);
+  // want_dx = false: reductions + finalizes only (ws / wsd then hold the apply coefficients)
+  at::Tensor dx = want_dx ? at::empty_like(x) : at::Tensor(), dxd = want_dx ? at::empty_like(xd) : at::Tensor();
   at::Tensor dg = at::empty({C}, f32), db = at::empty({C}, f32), dgd = at::empty({C}, f32), dbd = at::empty({C}, f32);
   auto gp = [](const c10::optional<at::Tensor>& w) -> const float* {
     return (w.has_value() && w->defined()) ? w->data_ptr<float>() : nullptr;
   };
-  launch_bn_dual_bwd(dy.data_ptr(), mp, x.data_ptr(), xd.data_ptr(), dx.data_ptr(), dxd.data_ptr(), M, C,
+  launch_bn_dual_bwd(dy.data_ptr(), mp, x.data_ptr(), xd.data_ptr(), want_dx ? dx.data_ptr() : nullptr,
+                     want_dx ? dxd.data_ptr() : nullptr, M, C,
                      dtype_code(x), gp(weight), gp(weight_d), ws.data_ptr<float>(), wsd.data_ptr<float>(),
                      part.data_ptr<float>(), partd.data_ptr<float>(), dg.data_ptr<float>(), db.data_ptr<float>(),
                      dgd.data_ptr<float>(), dbd.data_ptr<float>(), current_stream(x));
@@ -1046,7 +1048,9 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("need_pos") = true);
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pooling backward (gather form)");
   m.def("bn_dual_fwd", &bn_dual_fwd, "training act(BN(x) + BN_d(xd)) in one apply pass (downsample residual)");
-  m.def("bn_dual_bwd", &bn_dual_bwd, "backward of bn_dual_fwd (one dy read for both BatchNorms)");
+  m.def("bn_dual_bwd", &bn_dual_bwd, "backward of bn_dual_fwd (one dy read for both BatchNorms)", pybind11::arg("dy"),
+        pybind11::arg("mask"), pybind11::arg("x"), pybind11::arg("ws"), pybind11::arg("weight"), pybind11::arg("xd"),
+        pybind11::arg("wsd"), pybind11::arg("weight_d"), pybind11::arg("want_dx") = true);
   m.def("gap_fwd", &gap_fwd, "NHWC global average pooling -> [N, C]");
   m.def("subsample2", &subsample2, "x[:, :, ::2, ::2] of a channels_last bf16 tensor, compact channels_last");
   m.def("stem_fwd", &stem_fwd, "7x7/s2/p3 stem conv, 3 input channels (space-to-depth + MFMA implicit GEMM, BN-statistics epilogue)");

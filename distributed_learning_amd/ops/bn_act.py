@@ -124,21 +124,30 @@ class _BNDualAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, xd, weight_d, bias_d, rm, rv, rmd, rvd, momentum, momentum_d, eps, eps_d,
-                relu, stats, stats_d):
+                relu, stats, stats_d, dlink=None, dlink_d=None):
         C = _ext.require()
         y, ws, wsd, mask = C.bn_dual_fwd(x, xd, weight, bias, rm, rv, weight_d, bias_d, rmd, rvd, momentum,
                                          momentum_d, eps, eps_d, relu, stats, stats_d)
         ctx.relu = relu
         ctx.save_for_backward(x, ws, weight, xd, wsd, weight_d, mask if relu else None)
+        # both inputs come from 1x1 convs that can apply their BN's backward themselves (ops/conv.py DualBNLink)
+        ctx.dlinks = (dlink, dlink_d) if (dlink is not None and dlink_d is not None and relu and mask is not None
+                                           and mask.numel() and x.dtype == torch.bfloat16) else None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, ws, weight, xd, wsd, weight_d, mask = ctx.saved_tensors
-        dx, dg, db, dxd, dgd, dbd = _ext.require().bn_dual_bwd(dy, mask, x, ws, weight, xd, wsd, weight_d)
         need = ctx.needs_input_grad
+        if ctx.dlinks is not None:
+            dy = dy.contiguous(memory_format=torch.channels_last)
+            _, dg, db, _, dgd, dbd = _ext.require().bn_dual_bwd(dy, mask, x, ws, weight, xd, wsd, weight_d, False)
+            dx = ctx.dlinks[0].park(dy, x, ws, mask, weight)
+            dxd = ctx.dlinks[1].park(dy, xd, wsd, mask, weight_d)
+        else:
+            dx, dg, db, dxd, dgd, dbd = _ext.require().bn_dual_bwd(dy, mask, x, ws, weight, xd, wsd, weight_d)
         return (dx, dg if need[1] else None, db if need[2] else None, dxd, dgd if need[4] else None,
-                dbd if need[5] else None) + (None,) * 11
+                dbd if need[5] else None) + (None,) * 13
 
 
 def dual_supported(x: torch.Tensor, bn: nn.BatchNorm2d, xd: torch.Tensor, bnd: nn.BatchNorm2d) -> bool:
@@ -160,7 +169,8 @@ def fused_bn_add_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, xd: torch.Tensor, b
     if len(_PENDING_COUNTERS) >= 1024:
         flush_bn_counters()
     return _BNDualAct.apply(x, bn.weight, bn.bias, xd, bnd.weight, bnd.bias, *running, float(bn.momentum),
-                            float(bnd.momentum), float(bn.eps), float(bnd.eps), relu, stats, stats_d)
+                            float(bnd.momentum), float(bn.eps), float(bnd.eps), relu, stats, stats_d,
+                            getattr(x, "_dla_dual", None), getattr(xd, "_dla_dual", None))
 
 
 # num_batches_tracked increments are batched into one multi-tensor launch per forward instead of

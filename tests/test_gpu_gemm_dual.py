@@ -131,8 +131,8 @@ def test_resnet_layer1_with_and_without_fused_bn_apply(cuda):
             m(x).float().square().mean().backward()
         finally:
             nconv.DUAL_BN = old
-        # stage-1 blocks 1 and 2 (block 0's last BN is the dual BN with the downsample)
-        assert (nconv.CALLS["1x1_dual_bn"] - before == 2) == flag
+        # stage 1: the conv3 of blocks 1 and 2, and block 0's conv3 + downsample conv (its dual BN hands both over)
+        assert (nconv.CALLS["1x1_dual_bn"] - before == 4) == flag
         return {n: p.grad.float().clone() for n, p in m.named_parameters()}
 
     dnn.set_backend("native")

@@ -13,11 +13,18 @@ DEV = torch.device("cuda", 0)
 
 @pytest.fixture
 def native(cuda):
+    from distributed_learning_amd.ops import conv
     from distributed_learning_amd.ops import nn as dnn
 
     dnn.set_backend("native")
     dnn.set_native_conv(True)
+    # the one-pass 1x1 kernel (DUAL_1X1) computes a weight gradient only when it is not deferred, so with it
+    # an inline schedule and an "all" schedule run different weight-gradient kernels: these tests compare the
+    # deferral itself, on the separate kernels
+    old = conv.DUAL_1X1
+    conv.DUAL_1X1 = False
     yield
+    conv.DUAL_1X1 = old
     dnn.set_backend("torch")
     dnn.set_native_conv(False)
 
