@@ -36,7 +36,9 @@ constexpr int kUCi = 64;  // input channels per block (slice)
 // and a pass over LDS writes dY = k1 (g - m1 - (y - mean) k2), g = masked gradient, over the gradient in
 // place (bn_bwd_apply's arithmetic and rounding) -- dY is never written to HBM.
 constexpr int kUMaskWave = 1024;  // bytes of mask area per wave and stage (the first R / 4 rows x CO / 8 used)
-template <int CO, int R, int NS, bool kBN = false>
+// kWReg: each wave holds its W^T fragments in registers instead of a block-wide LDS panel (Cout 512: the
+// 64 KB panel would leave no room for a deeper ring or the kBN tiles).
+template <int CO, int R, int NS, bool kBN = false, bool kWReg = false>
 struct DualCfg {
   static constexpr int KC = CO / kBK;                 // dY sub-images per tile
   static constexpr int Sub = R * kBK;                 // elements of one [R][64] sub-image
@@ -45,12 +47,12 @@ struct DualCfg {
   static constexpr int Panel = kUCi * kBK;            // one W^T sub-image [64 ci][64 co]
   static constexpr int Slots = Sub / 8 / 256;         // LDS-DMA slots per thread per sub-image
   static constexpr int Loads = ((kBN ? 2 : 1) * KC + 1) * Slots + (kBN ? 1 : 0);  // DMA ops per wave per tile
-  static_assert(!kBN || (CO * R / 8 / 4 <= 16 * 16 && CO == 256), "BN mask: one 16-lane DMA per wave");
+  static_assert(!kBN || CO * R / 8 / 4 <= kUMaskWave, "BN mask: one DMA per wave (64 lanes x 16 B)");
   static constexpr int RF = R / 16;                   // 16-row fragments of a tile
   static constexpr int NCF = RF;                      // data gradient: 16-channel fragments per wave (4 waves)
   static constexpr int Stores = NCF / 2;              // dX stores per lane per tile (4 NCF channels)
   static constexpr int TMW = CO / 64;                 // weight gradient: 16-row co fragments per wave
-  static constexpr size_t Lds = (size_t)(KC * Panel + NS * Stage) * sizeof(bf16_t);
+  static constexpr size_t Lds = (size_t)((kWReg ? 0 : KC * Panel) + NS * Stage) * sizeof(bf16_t);
   static_assert(Lds <= 160 * 1024, "dual 1x1 LDS budget");
   static_assert(Slots >= 1 && (RF == 2 || RF == 4) && (NS == 2 || NS == 3), "tile configuration");
 };
@@ -88,12 +90,12 @@ __device__ __forceinline__ bf16x8_t urm_tr_frag(const bf16_t* s, int c0, int kk)
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
-template <int CO, int R, int NS, bool kBN = false>
+template <int CO, int R, int NS, bool kBN = false, bool kWReg = false>
 __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) {
-  using G = DualCfg<CO, R, NS, kBN>;
+  using G = DualCfg<CO, R, NS, kBN, kWReg>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16_t* Ws = reinterpret_cast<bf16_t*>(smem_raw);  // KC sub-images [64 ci (permuted)][64 co]
-  bf16_t* ring = Ws + G::KC * G::Panel;               // NS stages
+  bf16_t* ring = Ws + (kWReg ? 0 : G::KC * G::Panel);  // NS stages
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, g = lane >> 4;
   // XCD-aware: the nsl slice blocks of one row group are adjacent slots of one XCD
@@ -105,8 +107,26 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
   const int mt = (M + R - 1) / R;
   const int ntile = grp < mt ? (mt - grp + s.mg - 1) / s.mg : 0;
 
+  // data gradient of this wave: row fragment rf, channel fragments cf0 .. cf0 + NCF - 1 of the slice
+  const int rf = wave % G::RF, cf0 = (wave / G::RF) * G::NCF;
+  // kWReg: this wave's W^T fragments (what rm_glds_frag would read from the panel below), loaded once
+  bf16x8_t wreg[kWReg ? G::NCF : 1][kWReg ? 2 * G::KC : 1];
+  if constexpr (kWReg) {
+#pragma unroll
+    for (int i = 0; i < G::NCF; ++i) {
+      const int ci = ci0 + uperm64(16 * (cf0 + i) + lr);  // the permuted panel row's input channel
+#pragma unroll
+      for (int q = 0; q < 2 * G::KC; ++q) {
+        const int co0 = (q >> 1) * kBK + ((q & 1) * 4 + g) * 8;
+        ushort8_t v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = reinterpret_cast<const uint16_t*>(s.w)[(int64_t)(co0 + e) * CI + ci];
+        wreg[i][q] = __builtin_bit_cast(bf16x8_t, v);
+      }
+    }
+  }
   // ---- weight panel -> LDS once: W[co][ci0 .. ci0 + 63] k-major, written transposed and row-permuted ---
-  {
+  if constexpr (!kWReg) {
     constexpr int kPer = CO * kUCi / 8 / 256;  // 16-byte chunks per thread
     ushort8_t v[kPer];
 #pragma unroll
@@ -199,8 +219,6 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
       bk2[j] = s.ws[6 * CO + c0 + j];
     }
   }
-  // data gradient of this wave: row fragment rf, channel fragments cf0 .. cf0 + NCF - 1 of the slice
-  const int rf = wave % G::RF, cf0 = (wave / G::RF) * G::NCF;
   accv_t aw[G::TMW][4];  // dW rows co = (CO / 4) wave + 16 i + 4 g + r, slice columns 16 j + lr
 #pragma unroll
   for (int i = 0; i < G::TMW; ++i)
@@ -256,7 +274,10 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
       for (int kk = 0; kk < kBK / 32; ++kk) {
         bf16x8_t wf[G::NCF];
 #pragma unroll
-        for (int i = 0; i < G::NCF; ++i) wf[i] = rm_glds_frag(Ws + kc * G::Panel, 16 * (cf0 + i), kk);
+        for (int i = 0; i < G::NCF; ++i) {
+          if constexpr (kWReg) wf[i] = wreg[i][2 * kc + kk];
+          else wf[i] = rm_glds_frag(Ws + kc * G::Panel, 16 * (cf0 + i), kk);
+        }
         const bf16x8_t yf = rm_glds_frag(Ds + kc * G::Sub, 16 * rf, kk);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -329,7 +350,7 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout) {
   return conv1x1_dual_blocks(M, Cin, Cout) ? 256 / (Cin / kUCi) : 0;
 }
 
-bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout) { return Cout == 256 && conv1x1_dual_blocks(M, Cin, Cout) > 0; }
+bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout) { return conv1x1_dual_blocks(M, Cin, Cout) > 0; }
 
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
                          int Cout, hipStream_t stream, const void* ybn, const uint8_t* mask, const float* ws) {
@@ -338,16 +359,18 @@ bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx,
   const int nsl = Cin / kUCi, mg = grid / nsl;
   DualArgs a{(const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)dx, part, (int)M, Cin, mg, mg / 8, nsl,
              (const bf16_t*)ybn, mask, ws};
+#define DLA_DUAL(CO_, R_, NS_, BN_, WR_)                                                                      \
+  hipLaunchKernelGGL((conv1x1_dual_kernel<CO_, R_, NS_, BN_, WR_>), dim3(grid), dim3(256),                     \
+                     (DualCfg<CO_, R_, NS_, BN_, WR_>::Lds), stream, a)
   if (ybn) {
     if (!conv1x1_dual_bn_ok(M, Cin, Cout) || !mask || !ws) return false;
-    hipLaunchKernelGGL((conv1x1_dual_kernel<256, 32, 3, true>), dim3(grid), dim3(256), (DualCfg<256, 32, 3, true>::Lds),
-                       stream, a);
+    if (Cout == 256) DLA_DUAL(256, 32, 3, true, false);
+    else DLA_DUAL(512, 32, 2, true, true);
     return true;
   }
-  if (Cout == 256)
-    hipLaunchKernelGGL((conv1x1_dual_kernel<256, 64, 3>), dim3(grid), dim3(256), (DualCfg<256, 64, 3>::Lds), stream, a);
-  else
-    hipLaunchKernelGGL((conv1x1_dual_kernel<512, 32, 2>), dim3(grid), dim3(256), (DualCfg<512, 32, 2>::Lds), stream, a);
+  if (Cout == 256) DLA_DUAL(256, 64, 3, false, false);
+  else DLA_DUAL(512, 32, 3, false, true);
+#undef DLA_DUAL
   return true;
 }
 

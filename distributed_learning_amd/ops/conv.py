@@ -273,6 +273,7 @@ class _Conv1x1(torch.autograd.Function):
         y = y2.view(n, h, w, cout).permute(0, 3, 1, 2)
         ctx.save_for_backward(x, w2)
         ctx.dlink = DualBNLink() if (DUAL_1X1 and DUAL_BN and stride == 1 and x.dtype == torch.bfloat16
+                                     and cout <= DUAL_1X1_MAX_COUT
                                      and C.conv1x1_dual_bn_ok(n * h * w, cin, cout)) else None
         ctx.stride = stride
         ctx.in_hw = None

@@ -80,23 +80,24 @@ def test_conv_autograd_uses_dual_and_matches(cuda):
     assert float((dw1 - dw0).norm() / dw0.norm()) < 1e-2
 
 
-@pytest.mark.parametrize("M", [65536, 100003])
-def test_dual_with_bn_apply_matches_separate(cuda, C, M):
+@pytest.mark.parametrize("M,ci,co", [(65536, 64, 256), (100003, 64, 256), (50001, 128, 512), (40003, 256, 512)])
+def test_dual_with_bn_apply_matches_separate(cuda, C, M, ci, co):
     """kBN: the consuming BN(+residual)+ReLU's backward apply inside the kernel (gradient, BN input, bit mask,
-    finalized coefficients) == bn_act_bwd's apply pass followed by the plain one-pass kernel."""
-    g = torch.Generator().manual_seed(M)
-    dout = torch.randn(M, 256, generator=g).to(cuda, torch.bfloat16)
-    ybn = (torch.randn(M, 256, generator=g) * 2 + 0.5).to(cuda, torch.bfloat16)
-    x = torch.randn(M, 64, generator=g).to(cuda, torch.bfloat16)
-    w = (torch.randn(256, 64, generator=g) * 0.0625).to(cuda, torch.bfloat16)
-    mask = torch.randint(0, 256, ((M * 256 + 7) // 8,), generator=g, dtype=torch.uint8).to(cuda)
-    gamma = (torch.rand(256, generator=g) + 0.5).to(cuda)
+    finalized coefficients) == bn_act_bwd's apply pass followed by the plain one-pass kernel (Cout 512: the
+    weight fragments held in registers)."""
+    g = torch.Generator().manual_seed(M + ci)
+    dout = torch.randn(M, co, generator=g).to(cuda, torch.bfloat16)
+    ybn = (torch.randn(M, co, generator=g) * 2 + 0.5).to(cuda, torch.bfloat16)
+    x = torch.randn(M, ci, generator=g).to(cuda, torch.bfloat16)
+    w = (torch.randn(co, ci, generator=g) * co ** -0.5).to(cuda, torch.bfloat16)
+    mask = torch.randint(0, 256, ((M * co + 7) // 8,), generator=g, dtype=torch.uint8).to(cuda)
+    gamma = (torch.rand(co, generator=g) + 0.5).to(cuda)
     yf = ybn.float()
-    ws = torch.zeros(7 * 256, device=cuda)
-    ws[:256] = yf.mean(0)
-    ws[256:512] = (yf.var(0, unbiased=False) + 1e-5).rsqrt()
+    ws = torch.zeros(7 * co, device=cuda)
+    ws[:co] = yf.mean(0)
+    ws[co:2 * co] = (yf.var(0, unbiased=False) + 1e-5).rsqrt()
     ws_a, ws_b = ws.clone(), ws.clone()
-    assert C.conv1x1_dual_bn_ok(M, 64, 256)
+    assert C.conv1x1_dual_bn_ok(M, ci, co)
     dY, _, dg, db = C.bn_act_bwd(dout, None, mask, ybn, ws_a, gamma, 2, False, None)
     dx_ref, dw_ref = C.conv1x1_dual(dY, x, w, torch.float32)
     _, _, dg2, db2 = C.bn_act_bwd(dout, None, mask, ybn, ws_b, gamma, 2, False, None, False)
@@ -110,7 +111,7 @@ def test_dual_with_bn_apply_matches_separate(cuda, C, M):
     assert float((dw - dw_ref).norm() / dw_ref.norm()) < 1e-5
 
 
-def test_resnet_layer1_with_and_without_fused_bn_apply(cuda):
+def test_resnet_with_and_without_fused_bn_apply(cuda):
     """Whole ResNet-50 step: the BN-apply hand-off (BN backward stops after its reduction, the conv3 backward
     applies it inside the one-pass kernel) reproduces the unfused gradients up to fp32 summation order."""
     from distributed_learning_amd.models import resnet50
@@ -131,8 +132,9 @@ def test_resnet_layer1_with_and_without_fused_bn_apply(cuda):
             m(x).float().square().mean().backward()
         finally:
             nconv.DUAL_BN = old
-        # stage 1: the conv3 of blocks 1 and 2, and block 0's conv3 + downsample conv (its dual BN hands both over)
-        assert (nconv.CALLS["1x1_dual_bn"] - before == 4) == flag
+        # the conv3 of blocks 1.. and block 0's conv3 + downsample conv (its dual BN hands both over):
+        # stage 1 (2 + 2) and stage 2 (3 + 2)
+        assert (nconv.CALLS["1x1_dual_bn"] - before == 9) == flag
         return {n: p.grad.float().clone() for n, p in m.named_parameters()}
 
     dnn.set_backend("native")
