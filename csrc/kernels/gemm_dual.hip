@@ -350,7 +350,13 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout) {
   return conv1x1_dual_blocks(M, Cin, Cout) ? 256 / (Cin / kUCi) : 0;
 }
 
-bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout) { return conv1x1_dual_blocks(M, Cin, Cout) > 0; }
+// The fused BN apply only for Cout 256: at Cout 512 (W fragments in registers, 2-stage ring, 2-4 slice blocks
+// each streaming the BN's gradient AND input) it measured 1.32 ms per call against 0.50 ms for the plain kernel
+// plus 0.33 ms for the separate apply pass (profiles/r4/g08).
+bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout) { return Cout == 256 && conv1x1_dual_blocks(M, Cin, Cout) > 0; }
+
+static int g_dual_wreg = 1;  // Cout 512 plain kernel: 1 = weight fragments in registers + 3-stage ring, 0 = LDS panel + 2 stages
+void set_dual_wreg(int on) { g_dual_wreg = on ? 1 : 0; }
 
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
                          int Cout, hipStream_t stream, const void* ybn, const uint8_t* mask, const float* ws) {
@@ -364,12 +370,12 @@ bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx,
                      (DualCfg<CO_, R_, NS_, BN_, WR_>::Lds), stream, a)
   if (ybn) {
     if (!conv1x1_dual_bn_ok(M, Cin, Cout) || !mask || !ws) return false;
-    if (Cout == 256) DLA_DUAL(256, 32, 3, true, false);
-    else DLA_DUAL(512, 32, 2, true, true);
+    DLA_DUAL(256, 32, 3, true, false);
     return true;
   }
   if (Cout == 256) DLA_DUAL(256, 64, 3, false, false);
-  else DLA_DUAL(512, 32, 3, false, true);
+  else if (g_dual_wreg) DLA_DUAL(512, 32, 3, false, true);
+  else DLA_DUAL(512, 32, 2, false, false);
 #undef DLA_DUAL
   return true;
 }

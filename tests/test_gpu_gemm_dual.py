@@ -47,6 +47,27 @@ def test_dual_not_served_shapes(C):
     assert C.conv1x1_dual_blocks(1 << 20, 256, 1024) == 0  # weight panel too large for LDS
     assert C.conv1x1_dual_blocks(1 << 20, 256, 64) == 0
     assert C.conv1x1_dual_blocks(1 << 20, 512, 512) == 0
+    assert C.conv1x1_dual_bn_ok(1 << 20, 64, 256) and not C.conv1x1_dual_bn_ok(1 << 20, 128, 512)
+
+
+@pytest.mark.parametrize("wreg", [0, 1])
+def test_dual_cout512_weight_forms_agree(cuda, C, wreg):
+    """The Cout-512 kernel with register-held weight fragments (3-stage ring) and with the LDS panel
+    (2-stage): the same products in the same order."""
+    M = 60001
+    g = torch.Generator().manual_seed(7)
+    dy = torch.randn(M, 512, generator=g).to(cuda, torch.bfloat16)
+    x = torch.randn(M, 128, generator=g).to(cuda, torch.bfloat16)
+    w = (torch.randn(512, 128, generator=g) * 0.05).to(cuda, torch.bfloat16)
+    try:
+        C.set_dual_wreg(wreg)
+        dx, dw = C.conv1x1_dual(dy, x, w, torch.float32)
+    finally:
+        C.set_dual_wreg(1)
+    ref = dy.float() @ w.float()
+    assert float((dx.float() - ref).norm() / ref.norm()) < 5e-3
+    dw_ref = dy.double().t() @ x.double()
+    assert float((dw.double() - dw_ref).norm() / dw_ref.norm()) < 1e-5
 
 
 def test_conv_autograd_uses_dual_and_matches(cuda):
@@ -80,7 +101,7 @@ def test_conv_autograd_uses_dual_and_matches(cuda):
     assert float((dw1 - dw0).norm() / dw0.norm()) < 1e-2
 
 
-@pytest.mark.parametrize("M,ci,co", [(65536, 64, 256), (100003, 64, 256), (50001, 128, 512), (40003, 256, 512)])
+@pytest.mark.parametrize("M,ci,co", [(65536, 64, 256), (100003, 64, 256)])
 def test_dual_with_bn_apply_matches_separate(cuda, C, M, ci, co):
     """kBN: the consuming BN(+residual)+ReLU's backward apply inside the kernel (gradient, BN input, bit mask,
     finalized coefficients) == bn_act_bwd's apply pass followed by the plain one-pass kernel (Cout 512: the
@@ -132,9 +153,8 @@ def test_resnet_with_and_without_fused_bn_apply(cuda):
             m(x).float().square().mean().backward()
         finally:
             nconv.DUAL_BN = old
-        # the conv3 of blocks 1.. and block 0's conv3 + downsample conv (its dual BN hands both over):
-        # stage 1 (2 + 2) and stage 2 (3 + 2)
-        assert (nconv.CALLS["1x1_dual_bn"] - before == 9) == flag
+        # stage 1: the conv3 of blocks 1 and 2, and block 0's conv3 + downsample conv (its dual BN hands both over)
+        assert (nconv.CALLS["1x1_dual_bn"] - before == 4) == flag
         return {n: p.grad.float().clone() for n, p in m.named_parameters()}
 
     dnn.set_backend("native")
