@@ -108,6 +108,21 @@ def test_matches_one_process_microbatch_oracle(two_rank_run, cuda):
 
     dnn.set_backend("native")
     dnn.set_native_conv(True)
+    try:
+        _oracle_steps(got_dir=d, cuda=cuda)
+    finally:
+        dnn.set_native_conv(False)
+        dnn.set_backend("torch")
+
+
+def _oracle_steps(got_dir, cuda):
+    from distributed_learning_amd.data import SyntheticBatches
+    from distributed_learning_amd.models import get_spec
+    from distributed_learning_amd.ops import nn as dnn
+    from distributed_learning_amd.ops.loss import cross_entropy
+    from distributed_learning_amd.ops.optim import FusedSGD
+
+    d = got_dir
     spec = get_spec("resnet50")
     torch.manual_seed(1234)
     model = spec.build().to(cuda).to(memory_format=torch.channels_last)
