@@ -312,9 +312,13 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout);
 // (bit-mask ReLU, finalized workspace); its backward apply runs inside the kernel (Cout 256 only)
 bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout);
 void set_dual_wreg(int on);  // A/B: Cout-512 kernel with register-held weights (1, default) or the LDS panel (0)
+// add / amask: the fork form (data gradient + masked identity-gradient addend, BN mode 1 = ReLU recomputed from
+// ybn); its partial groups come from conv1x1_dual_fork_groups
+int conv1x1_dual_fork_groups(int64_t M, int Cin, int Cout);
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
                          int Cout, hipStream_t stream, const void* ybn = nullptr, const uint8_t* mask = nullptr,
-                         const float* ws = nullptr);
+                         const float* ws = nullptr, int bn_mode = 2, const void* add = nullptr,
+                         const uint8_t* amask = nullptr);
 void launch_splitk_reduce(const float* partial, int splits, int64_t n, void* out, int out_dtype, float scale,
                           bool accumulate, hipStream_t stream, const void* addend = nullptr, int64_t ld_addend = 0,
                           int ncol = 1);

@@ -83,10 +83,13 @@ class _BNAct(torch.autograd.Function):
         m = mask if mask is not None and mask.numel() else None
         ctx.save_for_backward(x, ws, weight, m)
         ctx.link = BNLink(x, ws, m, ctx.mask_mode) if training and x.dtype == torch.bfloat16 else None
-        # the producing 1x1 conv applies this BN's backward itself (ops/conv.py DualBNLink): bit-mask ReLU
-        # after the residual add, residual gradient handed to the fork, bf16
-        ctx.dlink = dlink if (dlink is not None and ctx.rlink is not None and ctx.mask_mode == MASK_BITS
-                              and m is not None and x.dtype == torch.bfloat16) else None
+        # the producing 1x1 conv applies this BN's backward itself (ops/conv.py DualBNLink): a bit-mask ReLU after
+        # the residual add with the residual gradient handed to the fork (conv3), or a ReLU recomputed from x with
+        # no residual (the fork conv1); bf16
+        ok = dlink is not None and x.dtype == torch.bfloat16 and ctx.mask_mode in dlink.modes and (
+            (ctx.mask_mode == MASK_BITS and ctx.rlink is not None and m is not None) or
+            (ctx.mask_mode == MASK_RECOMPUTE and not ctx.has_res))
+        ctx.dlink = dlink if ok else None
         return y
 
     @staticmethod
@@ -97,12 +100,13 @@ class _BNAct(torch.autograd.Function):
         C = _ext.require()
         ext = ctx.link.take(dy) if ctx.link is not None else None
         rl = ctx.rlink
-        if ctx.dlink is not None and rl is not None:
+        if ctx.dlink is not None:
             # reduction + finalize only; the conv backward applies (dy, x, mask, ws) in its own kernel
             dy = dy.contiguous(memory_format=torch.channels_last)
             _, _, dg, db = C.bn_act_bwd(dy, None, mask, x, ws, weight, ctx.mask_mode, False, ext, False)
-            dx = ctx.dlink.park(dy, x, ws, mask, weight)
-            rl.dy, rl.mask = dy, mask
+            dx = ctx.dlink.park(dy, x, ws, mask, weight, ctx.mask_mode)
+            if rl is not None:
+                rl.dy, rl.mask = dy, mask
             need = ctx.needs_input_grad
             return (dx, dg if need[1] else None, db if need[2] else None, None,
                     None, None, None, None, None, None, None, None, None)
@@ -132,7 +136,8 @@ class _BNDualAct(torch.autograd.Function):
         ctx.save_for_backward(x, ws, weight, xd, wsd, weight_d, mask if relu else None)
         # both inputs come from 1x1 convs that can apply their BN's backward themselves (ops/conv.py DualBNLink)
         ctx.dlinks = (dlink, dlink_d) if (dlink is not None and dlink_d is not None and relu and mask is not None
-                                           and mask.numel() and x.dtype == torch.bfloat16) else None
+                                           and mask.numel() and x.dtype == torch.bfloat16
+                                           and MASK_BITS in dlink.modes and MASK_BITS in dlink_d.modes) else None
         return y
 
     @staticmethod
@@ -142,8 +147,8 @@ class _BNDualAct(torch.autograd.Function):
         if ctx.dlinks is not None:
             dy = dy.contiguous(memory_format=torch.channels_last)
             _, dg, db, _, dgd, dbd = _ext.require().bn_dual_bwd(dy, mask, x, ws, weight, xd, wsd, weight_d, False)
-            dx = ctx.dlinks[0].park(dy, x, ws, mask, weight)
-            dxd = ctx.dlinks[1].park(dy, xd, wsd, mask, weight_d)
+            dx = ctx.dlinks[0].park(dy, x, ws, mask, weight, MASK_BITS)
+            dxd = ctx.dlinks[1].park(dy, xd, wsd, mask, weight_d, MASK_BITS)
         else:
             dx, dg, db, dxd, dgd, dbd = _ext.require().bn_dual_bwd(dy, mask, x, ws, weight, xd, wsd, weight_d)
         return (dx, dg if need[1] else None, db if need[2] else None, dxd, dgd if need[4] else None,
@@ -224,7 +229,7 @@ def fused_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residua
     rlink = fork_link_of(residual)
     if rlink is not None and residual.dtype != torch.bfloat16:  # the epilogue addend is bf16
         rlink = None
-    dlink = getattr(x, "_dla_dual", None) if (training and rlink is not None) else None
+    dlink = getattr(x, "_dla_dual", None) if training else None
     y = _BNAct.apply(x, bn.weight, bn.bias, residual, rm, rv, training, float(bn.momentum or 0.0),
                      float(bn.eps), relu, stats if training else None, rlink, dlink)
     if y.grad_fn is not None:
