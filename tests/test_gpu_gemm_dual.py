@@ -48,7 +48,7 @@ def test_dual_not_served_shapes(C):
     assert C.conv1x1_dual_blocks(1 << 20, 256, 64) == 0
     assert C.conv1x1_dual_blocks(1 << 20, 512, 512) == 0
     assert C.conv1x1_dual_bn_ok(1 << 20, 64, 256) and not C.conv1x1_dual_bn_ok(1 << 20, 128, 512)
-    assert C.conv1x1_dual_fork_groups(1 << 22, 256, 64) == 64 and C.conv1x1_dual_fork_groups(1 << 20, 512, 128) == 32
+    assert C.conv1x1_dual_fork_groups(4014080, 256, 64) == 64 and C.conv1x1_dual_fork_groups(1 << 20, 512, 128) == 32
     assert C.conv1x1_dual_fork_groups(1 << 20, 1024, 256) == 0 and C.conv1x1_dual_fork_groups(1000, 256, 64) == 0
 
 
