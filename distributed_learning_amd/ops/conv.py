@@ -231,7 +231,10 @@ DUAL_1X1_MAX_COUT = 512  # A/B: 256 keeps it to stage 1
 # backward apply inside the same kernel: the BN backward stops after its reduction and hands (dy, y, mask,
 # coefficients) over; dY never reaches HBM (gemm_dual.hip kBN).
 DUAL_BN = True
-DUAL_FORK = True  # ... and the block's first BN(+ReLU) inside its conv1 (fork) backward
+# ... and the block's first BN(+ReLU) inside its conv1 (fork) backward: off -- with 32-row tiles of 64-128 channels
+# the per-tile cost dominates (3.0 / 1.6 ms per call at stages 1 / 2 vs ~1.5 / 0.8 ms for apply + dgrad + wgrad;
+# 88.1 vs 84.2 ms/step, profiles/r4/g11); kept selectable and tested (tests/test_gpu_gemm_dual.py)
+DUAL_FORK = False
 
 
 class DualBNLink:

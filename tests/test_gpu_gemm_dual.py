@@ -148,13 +148,13 @@ def test_resnet_with_and_without_fused_bn_apply(cuda):
         m = resnet50(10).to(cuda).to(memory_format=CL)
         dnn.bf16_weights(m)
         x = torch.randn(24, 3, 224, 224, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
-        old = nconv.DUAL_BN
-        nconv.DUAL_BN = flag
+        old = nconv.DUAL_BN, nconv.DUAL_FORK
+        nconv.DUAL_BN = nconv.DUAL_FORK = flag
         before, before_f = nconv.CALLS["1x1_dual_bn"], nconv.CALLS["1x1_dual_fork"]
         try:
             m(x).float().square().mean().backward()
         finally:
-            nconv.DUAL_BN = old
+            nconv.DUAL_BN, nconv.DUAL_FORK = old
         # stage 1: the conv3 of blocks 1 and 2, and block 0's conv3 + downsample conv (its dual BN hands both over)
         assert (nconv.CALLS["1x1_dual_bn"] - before == 4) == flag
         # fork form: conv1 of stage-1 blocks 1-2 and stage-2 blocks 1-3 (block 0 forks hand on a subsample)
