@@ -281,6 +281,12 @@ def phase_breakdown(parts, n: int, csv_path=None, name="bench"):
     return mean
 
 
+def _dual_calls():
+    from distributed_learning_amd.ops import conv as nconv
+
+    return {k: nconv.CALLS[k] for k in ("1x1_dual", "1x1_dual_bn", "1x1_dual_fork")}
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ:
@@ -453,6 +459,9 @@ def main():
                 "kernels": "torch" if fp32 else a.kernels,
                 "precision": a.precision,
                 "conv1x1": "miopen" if fp32 else a.conv,
+                # 1x1 backward: both gradients in one pass over dY (gemm_dual.hip), the consuming BN's apply
+                # fused where served (ops/conv.py DUAL_*); what actually ran this process
+                "conv1x1_bwd": None if fp32 else {k: int(v) for k, v in _dual_calls().items()},
                 "hip_graph": graphed,
                 "optimizer": f"fused SGD momentum={a.momentum}" + (" (fp32 master weights)" if bf16 else " (fp32 weights)"),
                 "force_comm": bool(a.force_comm),

@@ -23,7 +23,7 @@ CATS = [
     ("conv_wgrad", re.compile(r"wrw|bwd_weight|BwdWeight|conv_bwd_w|conv3x3_wgrad|stem_wgrad", re.I)),
     ("conv_dgrad", re.compile(r"igemm_bwd|bwd_data|conv_bwd_d|BwdData|naive_conv.*_bwd|conv3x3(s2)?_dgrad", re.I)),
     ("conv_fwd", re.compile(r"igemm_fwd|conv_fwd|ConvFwd|naive_conv.*_fwd|grouped_conv_fwd|conv3x3_fwd|conv3x3_halo|stem_f", re.I)),
-    ("gemm", re.compile(r"gemm|Cijk|dla_gemm|splitk_reduce", re.I)),
+    ("gemm", re.compile(r"gemm|Cijk|dla_gemm|splitk_reduce|conv1x1_dual", re.I)),
     ("batchnorm", re.compile(r"BatchNorm|bn_", re.I)),
     ("dla_bn_act", re.compile(r"bn_act|bnact", re.I)),
     ("optimizer", re.compile(r"sgd_kernel|multi_tensor|foreach", re.I)),
