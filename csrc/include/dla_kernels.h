@@ -315,6 +315,7 @@ void set_dual_wreg(int on);  // A/B: Cout-512 kernel with register-held weights 
 // add / amask: the fork form (data gradient + masked identity-gradient addend, BN mode 1 = ReLU recomputed from
 // ybn); its partial groups come from conv1x1_dual_fork_groups
 int conv1x1_dual_fork_groups(int64_t M, int Cin, int Cout);
+void set_dual_fork_rows(int rows);  // A/B: 32- or 64-row tiles (default 64) of the fork form
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
                          int Cout, hipStream_t stream, const void* ybn = nullptr, const uint8_t* mask = nullptr,
                          const float* ws = nullptr, int bn_mode = 2, const void* add = nullptr,

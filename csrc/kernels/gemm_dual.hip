@@ -417,11 +417,14 @@ void set_dual_wreg(int on) { g_dual_wreg = on ? 1 : 0; }
 // The fork form (a block's first 1x1 conv, whose input also feeds the identity branch): the BN(+ReLU, recomputed)
 // consuming its output applied on the fly, the identity gradient added in the data gradient's epilogue;
 // (Cout, Cin) = (64, 256 / 512 / 1024) or (128, 512 / 1024), 32-row tiles, 3-stage ring.
+static int g_fork_rows = 64;  // A/B: 32 or 64-row tiles of the fork form
+void set_dual_fork_rows(int rows) { g_fork_rows = rows == 32 ? 32 : 64; }
+
 int conv1x1_dual_fork_groups(int64_t M, int Cin, int Cout) {
   if (M <= 0 || Cin % 128 || (Cout != 64 && Cout != 128) || Cin > 1024 || Cin < 4 * Cout) return 0;
   if (M * Cout * 2 >= (int64_t)kOOB || M * Cin * 2 >= (int64_t)kOOB) return 0;
   const int mg = 256 / (Cin / kUCi);
-  if ((M + 31) / 32 < (int64_t)mg * 4) return 0;
+  if ((M + g_fork_rows - 1) / g_fork_rows < (int64_t)mg * 4) return 0;
   return mg;
 }
 
@@ -439,8 +442,14 @@ bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx,
                      (DualCfg<CO_, R_, NS_, BN_, WR_, AD_>::Lds), stream, a)
   if (fork) {
     if (!ybn || !ws || bn_mode != 1) return false;
-    if (Cout == 64) DLA_DUAL(64, 32, 3, 1, false, true);
-    else DLA_DUAL(128, 32, 3, 1, false, true);
+    // 64-row tiles (Cout 128: 2 stages to fit LDS): the 32-row form spends its time in per-tile overhead (g11)
+    if (g_fork_rows == 64) {
+      if (Cout == 64) DLA_DUAL(64, 64, 3, 1, false, true);
+      else DLA_DUAL(128, 64, 2, 1, false, true);
+    } else {
+      if (Cout == 64) DLA_DUAL(64, 32, 3, 1, false, true);
+      else DLA_DUAL(128, 32, 3, 1, false, true);
+    }
     return true;
   }
   if (ybn) {

@@ -1100,6 +1100,7 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("y_bn") = pybind11::none(), pybind11::arg("ws") = pybind11::none(),
         pybind11::arg("mask") = pybind11::none(), pybind11::arg("bn_mode") = 2,
         pybind11::arg("addend") = pybind11::none(), pybind11::arg("addend_mask") = pybind11::none());
+  m.def("set_dual_fork_rows", &set_dual_fork_rows, "A/B: 32- or 64-row tiles of the fork form (default 64)");
   m.def("conv1x1_dual_fork_groups", [](int64_t M, int64_t Cin, int64_t Cout) { return conv1x1_dual_fork_groups(M, (int)Cin, (int)Cout); },
         "row groups of the fork form of the one-pass 1x1 gradient kernel (0: shape not served)");
   m.def("set_dual_wreg", &set_dual_wreg, "A/B: Cout-512 one-pass kernel with register-held weights (1) or the LDS panel (0)");

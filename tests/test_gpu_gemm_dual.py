@@ -172,8 +172,9 @@ def test_resnet_with_and_without_fused_bn_apply(cuda):
     assert rels[len(rels) // 2] < 2e-2 and rels[-1] < 0.2, rels[-5:]
 
 
+@pytest.mark.parametrize("rows", [32, 64])
 @pytest.mark.parametrize("M,ci,co,masked", [(80001, 256, 64, True), (80001, 256, 64, False), (30011, 512, 128, True)])
-def test_dual_fork_form_matches_separate(cuda, C, M, ci, co, masked):
+def test_dual_fork_form_matches_separate(cuda, C, M, ci, co, masked, rows):
     """Fork form: the block's first BN(+ReLU recomputed from its input) applied on the fly, data gradient with the
     identity gradient added under its 1-bit mask (gemm_stream's kAdd arithmetic), weight gradient -- against
     bn_act_bwd's apply pass, the k-major gemm_nt with the masked addend and gemm_tn."""
@@ -197,7 +198,11 @@ def test_dual_fork_form_matches_separate(cuda, C, M, ci, co, masked):
     dx_ref, _ = C.gemm_nt(dY, w, False, add, True, 0, amask)
     dw_ref = C.gemm_tn(dY, x, torch.float32, 1.0)
     C.bn_act_bwd(dout, None, None, ybn, ws_b, gamma, 1, False, None, False)
-    dx, dw = C.conv1x1_dual(dout, x, w, torch.float32, ybn, ws_b, None, 1, add, amask)
+    try:
+        C.set_dual_fork_rows(rows)
+        dx, dw = C.conv1x1_dual(dout, x, w, torch.float32, ybn, ws_b, None, 1, add, amask)
+    finally:
+        C.set_dual_fork_rows(64)
     torch.cuda.synchronize()
     assert torch.equal(ws_a, ws_b)
     scale = float(dx_ref.float().abs().max())
