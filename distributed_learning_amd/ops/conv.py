@@ -233,7 +233,8 @@ DUAL_1X1_MAX_COUT = 512  # A/B: 256 keeps it to stage 1
 DUAL_BN = True
 # ... and the block's first BN(+ReLU) inside its conv1 (fork) backward: off -- with 32-row tiles of 64-128 channels
 # the per-tile cost dominates (3.0 / 1.6 ms per call at stages 1 / 2 vs ~1.5 / 0.8 ms for apply + dgrad + wgrad;
-# 88.1 vs 84.2 ms/step, profiles/r4/g11); kept selectable and tested (tests/test_gpu_gemm_dual.py)
+# 88.1 vs 84.2 ms/step, profiles/r4/g11), and 64-row tiles are still slower (87.2 vs 84.5, g12); kept selectable
+# and tested (tests/test_gpu_gemm_dual.py)
 DUAL_FORK = False
 
 
