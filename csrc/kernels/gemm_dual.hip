@@ -1,20 +1,21 @@
-// Both gradients of a stride-1 1x1 convolution in ONE pass over dY (ResNet-50 stage 1: conv3 and the
-// downsample shortcut, Cin = 64 -> Cout = 256, 4M rows at bs1280):
+// Both gradients of a stride-1 1x1 convolution in ONE pass over dY (ResNet-50 stages 1-2):
 //   dX[M][Cin]      = dY[M][Cout] W[Cout][Cin]       data gradient, bf16
-//   dW[Cout][Cin]   = dY[M][Cout]^T X[M][Cin]        weight gradient, fp32 partial per block + split reduce
-// The separate kernels (gemm_stream / gemm_nt for dX, gemm_tn for dW) each stream dY from HBM: 2 GB per
-// call twice. Here every dY tile crosses HBM -> LDS once and feeds both products:
-//   * persistent blocks (one per CU, XCD-aware row groups as gemm_stream.hip) walk 64-row tiles; per tile
-//     4 dY sub-images [64 rows][64 co] and one X sub-image [64 rows][64 ci] arrive by buffer LDS-DMA
-//     into a 3-stage ring (2 tiles in flight ahead of the MFMAs, 40 KB per stage);
-//   * data gradient: the transposed product of gemm_stream.hip (W^T [ci][co] as the MFMA A operand from
-//     a once-staged, row-permuted panel; dY rows as B), each lane stores 16 consecutive channels of one
-//     row straight from registers;
+//   dW[Cout][Cin]   = dY[M][Cout]^T X[M][Cin]        weight gradient, fp32 partial per row group + split reduce
+// The separate kernels (gemm_stream / gemm_nt for dX, gemm_tn for dW) each stream dY from HBM (2 GB per stage-1
+// call, twice). Here every dY tile crosses HBM -> LDS once and feeds both products:
+//   * persistent blocks (one per CU, XCD-aware row groups as gemm_stream.hip) walk R-row tiles; per tile the dY
+//     sub-images [R rows][64 co] and the block's X slice [R rows][64 ci] arrive by buffer LDS-DMA into an
+//     NS-stage ring (NS - 1 tiles in flight ahead of the MFMAs);
+//   * data gradient: the transposed product of gemm_stream.hip (W^T [ci][co] as the MFMA A operand, from a
+//     once-staged row-permuted LDS panel or, kWReg, per-wave registers; dY rows as B); each lane stores 4 NCF
+//     consecutive channels of one row straight from registers;
 //   * weight gradient: the same dY sub-images read transposed (ds_read_b64_tr_b16, K = rows) against the
-//     transposed X image, accumulated in registers over all of the block's tiles; one fp32 [Cout][Cin]
-//     partial per block at the end, summed by splitk_reduce in fixed order (deterministic).
-// Wider Cin is split into 64-channel slices, one block each (the slices of a row group share an XCD's L2
-// for the dY tiles they all read); see DualCfg for the tile / ring shapes.
+//     transposed X image, accumulated in registers over all of the block's tiles; one fp32 [Cout][64] partial per
+//     block at the end, summed by splitk_reduce in fixed order (deterministic).
+// Wider Cin is split into 64-channel slices, one block each; the slice blocks of a row group sit on one XCD.
+// Served (launch_conv1x1_dual): (Cout, Cin) = (256, 64) with 64-row tiles; (512, 128 / 256) with 32-row tiles and
+// register-held weights; (256, 64) with the consuming BN's backward apply fused (kBNM 2, the block-final BN);
+// and a fork form (kBNM 1 + kAdd, the block's first conv) that is implemented but measured slower (ops/conv.py).
 #include "dla_common.h"
 #include "dla_kernels.h"
 #include "dla_mfma.h"
@@ -25,11 +26,7 @@ using namespace mm;
 
 namespace {
 
-// Shape configurations (CO = Cout, the data gradient's K; the block owns a 64-channel slice of Cin):
-//   CO 256, 64-row tiles, 3-stage ring (Cin 64: stage 1 conv3 / downsample)
-//   CO 512, 32-row tiles, 2-stage ring (Cin 128 / 256: stage 2 conv3 / downsample; the 2 or 4 slice
-//   blocks of a row group sit on one XCD and read the same dY tiles, the later ones from its L2)
-// LDS = CO x 64 weight panel + NS x (CO / 64 + 1) sub-images of R x 64.
+// Configurations: see the served list above; LDS = weight panel (unless kWReg) + NS stages of the tile images.
 constexpr int kUCi = 64;  // input channels per block (slice)
 // kBN: dY is the backward of the BatchNorm(+residual)+ReLU that consumed the conv's output, applied on the
 // fly: the tile brings the BN's incoming gradient (into the dY slots), its input y and its 1-bit ReLU mask,
