@@ -212,3 +212,57 @@ def test_dual_fork_form_matches_separate(cuda, C, M, ci, co, masked, rows):
     ref = dY.float() @ w.float() + add.float() * bits.view(M, ci)
     assert float((dx.float() - ref).norm() / ref.norm()) < 5e-3
     assert float((dw - dw_ref).norm() / dw_ref.norm()) < 1e-5
+
+
+def test_bn_handoff_falls_back_when_output_has_other_consumers(cuda):
+    """The conv output feeding the block-final BN is ALSO used elsewhere: autograd sums the BN's placeholder
+    gradient with the other one, the conv backward sees a different tensor, materialises the BN's gradient and
+    adds it -- the same gradients as without the hand-off."""
+    import torch.nn as nn
+
+    from distributed_learning_amd.ops import bn_act
+    from distributed_learning_amd.ops import conv as nconv
+    from distributed_learning_amd.ops import nn as dnn
+
+    CL = torch.channels_last
+    torch.manual_seed(0)
+    c1 = nn.Conv2d(256, 64, 1, bias=False).to(cuda).to(memory_format=CL)
+    c3 = nn.Conv2d(64, 256, 1, bias=False).to(cuda).to(memory_format=CL)
+    for c in (c1, c3):
+        c.weight.data = c.weight.data.to(torch.bfloat16)
+    bn = nn.BatchNorm2d(256).to(cuda)
+    x0 = torch.randn(24, 256, 56, 56, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    h0 = torch.randn(24, 64, 56, 56, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    wgt = torch.randn(24, 256, 56, 56, device=cuda).contiguous(memory_format=CL)
+
+    def run(flag, extra):
+        old = nconv.DUAL_BN
+        nconv.DUAL_BN = flag
+        try:
+            for p in (c1.weight, c3.weight, bn.weight, bn.bias):
+                p.grad = None
+            x = x0.clone().requires_grad_(True)
+            h = h0.clone().requires_grad_(True)
+            _, _, ident, _ = nconv.conv1x1_fork(x, c1)          # the identity alias with its residual hand-off
+            y3, st = nconv.conv1x1(h, c3, want_stats=True)      # carries the BN hand-off link when flag
+            out = bn_act.fused_bn_act(y3, bn, True, ident, st)
+            loss = (out.float() * wgt).sum()
+            if extra:
+                loss = loss + (y3.float() * wgt).square().mean()  # a second consumer of the conv output
+            before = nconv.CALLS["1x1_dual_bn"]
+            loss.backward()
+            fused = nconv.CALLS["1x1_dual_bn"] - before
+            return fused, [t.float().clone() for t in (x.grad, h.grad, c1.weight.grad, c3.weight.grad, bn.weight.grad)]
+        finally:
+            nconv.DUAL_BN = old
+
+    dnn.set_backend("native")
+    n_alone, g_alone = run(True, False)
+    n_extra, g_extra = run(True, True)
+    _, g_ref_alone = run(False, False)
+    _, g_ref_extra = run(False, True)
+    assert n_alone == 1 and n_extra == 0  # fused when the BN is the only consumer; materialised otherwise
+    for a, b in zip(g_extra, g_ref_extra):
+        assert float((a - b).norm() / b.norm().clamp_min(1e-20)) < 1e-2
+    for a, b in zip(g_alone, g_ref_alone):
+        assert float((a - b).norm() / b.norm().clamp_min(1e-20)) < 1e-2

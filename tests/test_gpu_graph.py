@@ -18,10 +18,16 @@ def _run(graphed: bool, steps: int, world1, arch: str = "resnet18", force: bool 
 
     torch.manual_seed(0)
     dev = torch.device("cuda:0")
+    batch = 16
     if arch == "googlenet":  # aux heads computed but unused (zero-filled grads), ceil-mode pools, torch.cat
         m = googlenet(10).to(dev).to(memory_format=torch.channels_last)
         m.dropout.p = 0.0  # the main-path dropout would make eager and replayed RNG streams matter
         shape = (3, 64, 64)
+    elif arch == "resnet50":  # batch 24 at 224: the stage-1 one-pass 1x1 kernels and the BN hand-off engage
+        from distributed_learning_amd.models import resnet50
+
+        m = resnet50(10).to(dev).to(memory_format=torch.channels_last)
+        shape, batch = (3, 224, 224), 24
     else:
         m = resnet18(10).to(dev).to(memory_format=torch.channels_last)
         shape = (3, 32, 32)
@@ -37,7 +43,7 @@ def _run(graphed: bool, steps: int, world1, arch: str = "resnet18", force: bool 
         w.sync.passthrough = False
         w.sync.executor.reserve(w.sync.buckets)
     opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, master_weights=True)
-    data = SyntheticBatches(16, shape, 10, dev, dtype=torch.bfloat16, channels_last=True, device_step=True)
+    data = SyntheticBatches(batch, shape, 10, dev, dtype=torch.bfloat16, channels_last=True, device_step=True)
 
     def step():
         x, y = data.next()
@@ -74,7 +80,7 @@ def world1(cuda):
     ctx.shutdown()
 
 
-@pytest.mark.parametrize("arch", ["resnet18", "googlenet"])
+@pytest.mark.parametrize("arch", ["resnet18", "googlenet", "resnet50"])
 def test_graphed_step_matches_eager(world1, arch):
     from distributed_learning_amd.ops import nn as dnn
 
