@@ -252,7 +252,8 @@ def test_bn_handoff_falls_back_when_output_has_other_consumers(cuda):
             before = nconv.CALLS["1x1_dual_bn"]
             loss.backward()
             fused = nconv.CALLS["1x1_dual_bn"] - before
-            return fused, [t.float().clone() for t in (x.grad, h.grad, c1.weight.grad, c3.weight.grad, bn.weight.grad)]
+            # (conv1's own output is unused here: only its identity alias carries a gradient)
+            return fused, [t.float().clone() for t in (x.grad, h.grad, c3.weight.grad, bn.weight.grad, bn.bias.grad)]
         finally:
             nconv.DUAL_BN = old
 
