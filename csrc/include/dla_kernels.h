@@ -302,8 +302,6 @@ void set_splitk_blocks(int blocks);  // 0: DLA_SPLITK_BLOCKS / default (512)
 int splitk_target_blocks();  // split-K grids: tiles of one split co-scheduled on one XCD (DLA_SPLITK_XCD=0: off)
 void launch_gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, float* partial, int splits, int Mo, int No,
                     int K, void* out, int out_dtype, float scale, bool accumulate, hipStream_t stream);
-// out[n] (= scale * sum_s partial[s][n] [+ addend] [+ out]), fp32 or bf16 out; addend: bf16 rows of
-// ncol with row stride ld_addend (0 = one broadcast row).
 // Both gradients of a stride-1 1x1 conv in one pass over dY (gemm_dual.hip; (Cout, Cin) = (256, 64),
 // (512, 128 / 256)): dx [M][Cin] bf16 and fp32 dW partials part [groups][Cout][Cin]; 0 blocks = not served
 int conv1x1_dual_blocks(int64_t M, int Cin, int Cout);
@@ -311,15 +309,11 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout);
 // ybn / mask / ws: dy is the incoming gradient of the BN(+residual)+ReLU that consumed the conv's output
 // (bit-mask ReLU, finalized workspace); its backward apply runs inside the kernel (Cout 256 only)
 bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout);
-void set_dual_wreg(int on);  // A/B: Cout-512 kernel with register-held weights (1, default) or the LDS panel (0)
-// add / amask: the fork form (data gradient + masked identity-gradient addend, BN mode 1 = ReLU recomputed from
-// ybn); its partial groups come from conv1x1_dual_fork_groups
-int conv1x1_dual_fork_groups(int64_t M, int Cin, int Cout);
-void set_dual_fork_rows(int rows);  // A/B: 32- or 64-row tiles (default 64) of the fork form
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
                          int Cout, hipStream_t stream, const void* ybn = nullptr, const uint8_t* mask = nullptr,
-                         const float* ws = nullptr, int bn_mode = 2, const void* add = nullptr,
-                         const uint8_t* amask = nullptr);
+                         const float* ws = nullptr);
+// out[n] (= scale * sum_s partial[s][n] [+ addend] [+ out]), fp32 or bf16 out; addend: bf16 rows of
+// ncol with row stride ld_addend (0 = one broadcast row).
 void launch_splitk_reduce(const float* partial, int splits, int64_t n, void* out, int out_dtype, float scale,
                           bool accumulate, hipStream_t stream, const void* addend = nullptr, int64_t ld_addend = 0,
                           int ncol = 1);

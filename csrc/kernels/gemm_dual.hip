@@ -14,8 +14,9 @@
 //     block at the end, summed by splitk_reduce in fixed order (deterministic).
 // Wider Cin is split into 64-channel slices, one block each; the slice blocks of a row group sit on one XCD.
 // Served (launch_conv1x1_dual): (Cout, Cin) = (256, 64) with 64-row tiles; (512, 128 / 256) with 32-row tiles and
-// register-held weights; (256, 64) with the consuming BN's backward apply fused (kBNM 2, the block-final BN);
-// and a fork form (kBNM 1 + kAdd, the block's first conv) that is implemented but measured slower (ops/conv.py).
+// register-held weights; (256, 64) with the consuming BN's backward apply fused (kBN, the block-final BN).
+// A fork form for the block's first conv (BN apply with the ReLU recomputed + the identity gradient added in the
+// epilogue) measured slower (87.2-88.1 vs 84.2-84.5 ms per step, profiles/r4/g11-g12) and was removed.
 #include "dla_common.h"
 #include "dla_kernels.h"
 #include "dla_mfma.h"
@@ -35,24 +36,18 @@ constexpr int kUCi = 64;  // input channels per block (slice)
 constexpr int kUMaskWave = 1024;  // bytes of mask area per wave and stage (the first R / 4 rows x CO / 8 used)
 // kWReg: each wave holds its W^T fragments in registers instead of a block-wide LDS panel (Cout 512: the
 // 64 KB panel would leave no room for a deeper ring or the kBN tiles).
-// kBNM: -1 dY given; 1 / 2 the BN apply with its ReLU recomputed from y (fmaf(y, sc, sh) > 0) / from the 1-bit mask.
-// kAdd: the data gradient's epilogue adds a masked addend (the fork's identity gradient, gemm_stream.hip's kAdd
-// arithmetic): its [R][64-channel slice] tile and 16 mask bytes per row window come through the ring as well.
-template <int CO, int R, int NS, int kBNM = -1, bool kWReg = false, bool kAdd = false>
+template <int CO, int R, int NS, bool kBN = false, bool kWReg = false>
 struct DualCfg {
-  static constexpr bool kBN = kBNM >= 0;
   static constexpr int KC = CO / kBK;                 // dY sub-images per tile
   static constexpr int Sub = R * kBK;                 // elements of one [R][64] sub-image
   static constexpr int Area = 4 * kUMaskWave / 2;     // elements of a per-wave mask area set
-  static constexpr int Xs = (kBN ? 2 : 1) * KC;       // sub-image index of the X slice (then the addend)
-  static constexpr int MaskAt = (Xs + 1 + (kAdd ? 1 : 0)) * Sub;  // BN mask area (kBNM 2), then the addend's
-  static constexpr int AMaskAt = MaskAt + (kBNM == 2 ? Area : 0);
-  static constexpr int Stage = AMaskAt + (kAdd ? Area : 0);
+  static constexpr int Xs = (kBN ? 2 : 1) * KC;       // sub-image index of the X slice
+  static constexpr int MaskAt = (Xs + 1) * Sub;       // kBN: the mask areas
+  static constexpr int Stage = MaskAt + (kBN ? Area : 0);
   static constexpr int Panel = kUCi * kBK;            // one W^T sub-image [64 ci][64 co]
   static constexpr int Slots = Sub / 8 / 256;         // LDS-DMA slots per thread per sub-image
-  static constexpr int Loads = (Xs + 1 + (kAdd ? 1 : 0)) * Slots + (kBNM == 2 ? 1 : 0) + (kAdd ? 1 : 0);
-  static_assert(kBNM != 2 || CO * R / 8 / 4 <= kUMaskWave, "BN mask: one DMA per wave (64 lanes x 16 B)");
-  static_assert(!kAdd || R / 4 <= 64, "addend mask: one row window per lane");
+  static constexpr int Loads = (Xs + 1) * Slots + (kBN ? 1 : 0);
+  static_assert(!kBN || CO * R / 8 / 4 <= kUMaskWave, "BN mask: one DMA per wave (64 lanes x 16 B)");
   static constexpr int RF = R / 16;                   // 16-row fragments of a tile
   static constexpr int NCF = RF;                      // data gradient: 16-channel fragments per wave (4 waves)
   static constexpr int Stores = NCF / 2;              // dX stores per lane per tile (4 NCF channels)
@@ -73,8 +68,6 @@ struct DualArgs {
   const bf16_t* ybn;     // kBN: the BN input [M][CO]
   const uint8_t* mask;   // kBN: its ReLU bit mask (bit e of byte e >> 3, e = m * CO + c)
   const float* ws;       // kBN: the finalized 7 CO workspace (mean, ..., k1, m1, k2)
-  const bf16_t* add;     // kAdd: [M][CI] addend of the data gradient
-  const uint8_t* amask;  // kAdd: its 1-bit mask over [M][CI] (null: add everywhere)
 };
 
 // image row of panel-local weight row p (gemm_stream.hip): MFMA A-operand row 16 i + 4 g + r holds output
@@ -97,10 +90,9 @@ __device__ __forceinline__ bf16x8_t urm_tr_frag(const bf16_t* s, int c0, int kk)
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
-template <int CO, int R, int NS, int kBNM = -1, bool kWReg = false, bool kAdd = false>
+template <int CO, int R, int NS, bool kBN = false, bool kWReg = false>
 __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) {
-  using G = DualCfg<CO, R, NS, kBNM, kWReg, kAdd>;
-  constexpr bool kBN = G::kBN;
+  using G = DualCfg<CO, R, NS, kBN, kWReg>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16_t* Ws = reinterpret_cast<bf16_t*>(smem_raw);  // KC sub-images [64 ci (permuted)][64 co]
   bf16_t* ring = Ws + (kWReg ? 0 : G::KC * G::Panel);  // NS stages
@@ -158,10 +150,7 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
   const __amdgpu_buffer_rsrc_t rdy = make_srd(s.dy, (uint32_t)((int64_t)M * CO * 2));
   const __amdgpu_buffer_rsrc_t rx = make_srd(s.x, (uint32_t)((int64_t)M * CI * 2));
   const __amdgpu_buffer_rsrc_t rybn = make_srd(kBN ? (const void*)s.ybn : (const void*)s.dy, (uint32_t)((int64_t)M * CO * 2));
-  const __amdgpu_buffer_rsrc_t rmsk = make_srd(kBNM == 2 ? (const void*)s.mask : (const void*)s.dy, (uint32_t)(((int64_t)M * CO + 7) / 8));
-  const __amdgpu_buffer_rsrc_t radd = make_srd(kAdd ? (const void*)s.add : (const void*)s.dy, (uint32_t)((int64_t)M * CI * 2));
-  const __amdgpu_buffer_rsrc_t ramk = make_srd(kAdd && s.amask ? (const void*)s.amask : (const void*)s.dy,
-                                               kAdd && s.amask ? (uint32_t)((int64_t)M * CI / 8) : 0u);
+  const __amdgpu_buffer_rsrc_t rmsk = make_srd(kBN ? (const void*)s.mask : (const void*)s.dy, (uint32_t)(((int64_t)M * CO + 7) / 8));
   uint32_t vdy[G::Slots], vx[G::Slots];
   int vr[G::Slots];
 #pragma unroll
@@ -198,21 +187,10 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
     for (int i = 0; i < G::Slots; ++i) o[i] = row0 + vr[i] < M ? vx[i] : kOOB;
     const uint32_t soff = row0 < M ? (uint32_t)(row0 * CI * 2) : 0u;
     bglds<G::Slots, 256 * 16>(o, rx, (uint32_t)__builtin_amdgcn_readfirstlane(soff), st + (uint32_t)(kXs * G::Sub * 2));
-    const uint32_t st0 = st - (uint32_t)(wave * 64 * 16);  // the stage base (st carries this wave's 1 KB offset)
-    if constexpr (kAdd) {
-      // the addend's slice tile, laid out like X; then its mask: lane l < R / 4 fetches the 16-byte window of row
-      // R / 4 wave + l that holds the slice's 8 mask bytes (byte offset 16 (sl / 2) within the row's CI / 8)
-      bglds<G::Slots, 256 * 16>(o, radd, (uint32_t)__builtin_amdgcn_readfirstlane(soff),
-                                st + (uint32_t)((kXs + 1) * G::Sub * 2));
-      const int64_t arow = row0 + (R / 4) * wave + lane;
-      uint32_t oa[1] = {lane < R / 4 && arow < M && s.amask ? (uint32_t)(((R / 4) * wave + lane) * (CI / 8)) : kOOB};
-      const uint32_t asoff = row0 < M ? (uint32_t)(row0 * (CI / 8) + 16 * (sl >> 1)) : 0u;
-      bglds<1, 0>(oa, ramk, (uint32_t)__builtin_amdgcn_readfirstlane(asoff),
-                  st0 + (uint32_t)(G::AMaskAt * 2) + (uint32_t)(wave * kUMaskWave));
-    }
-    if constexpr (kBNM == 2) {
+    if constexpr (kBN) {
       // mask bytes of the tile: wave w fetches rows R/4 w .. (R / 4 bytes x CO / 8 per row, 16 B per lane)
       // into its own 1 KB area; the other lanes are out of range and write zeros behind them
+      const uint32_t st0 = st - (uint32_t)(wave * 64 * 16);  // the stage base (st carries this wave's 1 KB offset)
       constexpr int kWaveBytes = R / 4 * CO / 8;
       const int64_t mrow = row0 + (R / 4) * wave + lane * 16 / (CO / 8);  // the row this lane's 16 bytes belong to
       uint32_t om[1] = {lane * 16 < kWaveBytes && mrow < M ? (uint32_t)(lane * 16) : kOOB};
@@ -232,15 +210,10 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
   // kBN: this thread's 8 channels (chunk column tid % (CO / 8)) in every row it converts
   constexpr int kCpr = CO / 8;  // 8-channel chunks per row
   float bmean[kBN ? 8 : 1], bk1[kBN ? 8 : 1], bm1[kBN ? 8 : 1], bk2[kBN ? 8 : 1];
-  float bsc[kBNM == 1 ? 8 : 1], bsh[kBNM == 1 ? 8 : 1];
   if constexpr (kBN) {
     const int c0 = (tid % kCpr) * 8;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if constexpr (kBNM == 1) {
-        bsc[j] = s.ws[2 * CO + c0 + j];
-        bsh[j] = s.ws[3 * CO + c0 + j];
-      }
       bmean[j] = s.ws[c0 + j];
       bk1[j] = s.ws[4 * CO + c0 + j];
       bm1[j] = s.ws[5 * CO + c0 + j];
@@ -277,15 +250,12 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
         const int o = sub * G::Sub + uimg(r, lc);
         const ushort8_t gv = *reinterpret_cast<const ushort8_t*>(Ds + o);
         const ushort8_t yv = *reinterpret_cast<const ushort8_t*>(Ys + o);
-        const uint32_t bits = kBNM == 2 ? (uint32_t)Ms[(r / (R / 4)) * kUMaskWave + (r % (R / 4)) * kCpr + cg] : 0u;
+        const uint32_t bits = (uint32_t)Ms[(r / (R / 4)) * kUMaskWave + (r % (R / 4)) * kCpr + cg];
         ushort8_t out;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float y = bf16_to_f32((bf16_t)yv[j]);
-          bool keep;
-          if constexpr (kBNM == 1) keep = fmaf(y, bsc[j], bsh[j]) > 0.f;  // bn_bwd_apply's recompute
-          else keep = (bits >> j) & 1u;
-          const float g = keep ? bf16_to_f32((bf16_t)gv[j]) : 0.f;
+          const float g = (bits >> j) & 1u ? bf16_to_f32((bf16_t)gv[j]) : 0.f;
           out[j] = f32_to_bf16(bk1[j] * (g - bm1[j] - (y - bmean[j]) * bk2[j]));
         }
         *reinterpret_cast<ushort8_t*>(Ds + o) = out;
@@ -337,33 +307,11 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
       const int64_t gm = (int64_t)(grp + t * s.mg) * R + 16 * rf + lr;
       const bool ok = gm < M;
       uint32_t wv[2 * G::NCF];
-      if constexpr (kAdd) {
-        // the unfused bf16 add of gemm_stream.hip's kAdd: bf16(bf16(acc) + (mask bit ? addend : 0))
-        const int rl = 16 * rf + lr, cl = 16 * g + 4 * cf0;  // tile row, first slice channel of this lane
-        const bf16_t* As = Ds + (G::Xs + 1) * G::Sub;
-        const uint8_t* Am = reinterpret_cast<const uint8_t*>(Ds + G::AMaskAt) + (rl / (R / 4)) * kUMaskWave +
-                            (rl % (R / 4)) * 16 + (sl & 1) * 8;
-#pragma unroll
-        for (int hc = 0; hc < G::NCF / 2; ++hc) {  // 8-channel chunks of the lane's 4 NCF channels
-          const ushort8_t dv = *reinterpret_cast<const ushort8_t*>(As + uimg(rl, (cl >> 3) + hc));
-          const uint32_t bits = s.amask ? (uint32_t)Am[(cl >> 3) + hc] : 0xffu;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int i = (8 * hc + e) >> 2, r = e & 3;
-            const bf16_t h = f32_to_bf16(ad[i][r]);
-            const float d = ((bits >> e) & 1u) ? bf16_to_f32((bf16_t)dv[e]) : 0.f;
-            const uint32_t hv = (uint32_t)f32_to_bf16(bf16_to_f32(h) + d);
-            if (e & 1) wv[(8 * hc + e) >> 1] |= hv << 16;
-            else wv[(8 * hc + e) >> 1] = hv;
-          }
-        }
-      } else {
 #pragma unroll
         for (int i = 0; i < G::NCF; ++i) {
           wv[2 * i] = (uint32_t)f32_to_bf16(ad[i][0]) | ((uint32_t)f32_to_bf16(ad[i][1]) << 16);
           wv[2 * i + 1] = (uint32_t)f32_to_bf16(ad[i][2]) | ((uint32_t)f32_to_bf16(ad[i][3]) << 16);
         }
-      }
       const uint32_t off = ok ? (uint32_t)((gm * CI + ci0 + 16 * g + 4 * cf0) * 2) : kOOB;
 #pragma unroll
       for (int h = 0; h < G::Stores; ++h) {
@@ -408,55 +356,24 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout) {
 // plus 0.33 ms for the separate apply pass (profiles/r4/g08).
 bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout) { return Cout == 256 && conv1x1_dual_blocks(M, Cin, Cout) > 0; }
 
-static int g_dual_wreg = 1;  // Cout 512 plain kernel: 1 = weight fragments in registers + 3-stage ring, 0 = LDS panel + 2 stages
-void set_dual_wreg(int on) { g_dual_wreg = on ? 1 : 0; }
-
-// The fork form (a block's first 1x1 conv, whose input also feeds the identity branch): the BN(+ReLU, recomputed)
-// consuming its output applied on the fly, the identity gradient added in the data gradient's epilogue;
-// (Cout, Cin) = (64, 256 / 512 / 1024) or (128, 512 / 1024), 32-row tiles, 3-stage ring.
-static int g_fork_rows = 64;  // A/B: 32 or 64-row tiles of the fork form
-void set_dual_fork_rows(int rows) { g_fork_rows = rows == 32 ? 32 : 64; }
-
-int conv1x1_dual_fork_groups(int64_t M, int Cin, int Cout) {
-  if (M <= 0 || Cin % 128 || (Cout != 64 && Cout != 128) || Cin > 1024 || Cin < 4 * Cout) return 0;
-  if (M * Cout * 2 >= (int64_t)kOOB || M * Cin * 2 >= (int64_t)kOOB) return 0;
-  const int mg = 256 / (Cin / kUCi);
-  if ((M + g_fork_rows - 1) / g_fork_rows < (int64_t)mg * 4) return 0;
-  return mg;
-}
-
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
-                         int Cout, hipStream_t stream, const void* ybn, const uint8_t* mask, const float* ws, int bn_mode,
-                         const void* add, const uint8_t* amask) {
-  const bool fork = add != nullptr;
-  const int mg = fork ? conv1x1_dual_fork_groups(M, Cin, Cout) : conv1x1_dual_groups(M, Cin, Cout);
+                         int Cout, hipStream_t stream, const void* ybn, const uint8_t* mask, const float* ws) {
+  const int mg = conv1x1_dual_groups(M, Cin, Cout);
   if (!mg) return false;
   const int nsl = Cin / kUCi, grid = mg * nsl;
   DualArgs a{(const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)dx, part, (int)M, Cin, mg, mg / 8, nsl,
-             (const bf16_t*)ybn, mask, ws, (const bf16_t*)add, amask};
-#define DLA_DUAL(CO_, R_, NS_, BN_, WR_, AD_)                                                                  \
-  hipLaunchKernelGGL((conv1x1_dual_kernel<CO_, R_, NS_, BN_, WR_, AD_>), dim3(grid), dim3(256),                 \
-                     (DualCfg<CO_, R_, NS_, BN_, WR_, AD_>::Lds), stream, a)
-  if (fork) {
-    if (!ybn || !ws || bn_mode != 1) return false;
-    // 64-row tiles (Cout 128: 2 stages to fit LDS): the 32-row form spends its time in per-tile overhead (g11)
-    if (g_fork_rows == 64) {
-      if (Cout == 64) DLA_DUAL(64, 64, 3, 1, false, true);
-      else DLA_DUAL(128, 64, 2, 1, false, true);
-    } else {
-      if (Cout == 64) DLA_DUAL(64, 32, 3, 1, false, true);
-      else DLA_DUAL(128, 32, 3, 1, false, true);
-    }
-    return true;
-  }
+             (const bf16_t*)ybn, mask, ws};
+#define DLA_DUAL(CO_, R_, NS_, BN_, WR_)                                                                       \
+  hipLaunchKernelGGL((conv1x1_dual_kernel<CO_, R_, NS_, BN_, WR_>), dim3(grid), dim3(256),                      \
+                     (DualCfg<CO_, R_, NS_, BN_, WR_>::Lds), stream, a)
   if (ybn) {
-    if (!conv1x1_dual_bn_ok(M, Cin, Cout) || !mask || !ws || bn_mode != 2) return false;
-    DLA_DUAL(256, 32, 3, 2, false, false);
+    if (!conv1x1_dual_bn_ok(M, Cin, Cout) || !mask || !ws) return false;
+    DLA_DUAL(256, 32, 3, true, false);
     return true;
   }
-  if (Cout == 256) DLA_DUAL(256, 64, 3, -1, false, false);
-  else if (g_dual_wreg) DLA_DUAL(512, 32, 3, -1, true, false);
-  else DLA_DUAL(512, 32, 2, -1, false, false);
+  // Cout 512: weight fragments in registers + a 3-stage ring (the LDS-panel form fits only 2 stages: slower)
+  if (Cout == 256) DLA_DUAL(256, 64, 3, false, false);
+  else DLA_DUAL(512, 32, 3, false, true);
 #undef DLA_DUAL
   return true;
 }

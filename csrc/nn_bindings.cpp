@@ -656,12 +656,9 @@ at::Tensor gemm_tn(at::Tensor A, at::Tensor B, c10::ScalarType out_dtype, double
 // is not served (the caller then runs gemm_nt + gemm_tn).
 // With y_bn (+ ws, mask): dy is the incoming gradient of the BN(+residual)+ReLU whose input y_bn is this conv's
 // output; its backward apply (bit-mask ReLU, finalized ws) runs inside the kernel.
-// With addend (+ addend_mask): the fork form -- dx = dy W + (mask bit ? addend : 0), and y_bn / ws with bn_mode 1
-// (the consuming BN's ReLU recomputed from y_bn).
 std::vector<at::Tensor> conv1x1_dual(at::Tensor dy, at::Tensor x, at::Tensor w, c10::ScalarType out_dtype,
                                      c10::optional<at::Tensor> y_bn, c10::optional<at::Tensor> ws,
-                                     c10::optional<at::Tensor> mask, int64_t bn_mode,
-                                     c10::optional<at::Tensor> addend, c10::optional<at::Tensor> addend_mask) {
+                                     c10::optional<at::Tensor> mask) {
   check_mat(dy, "dy");
   check_mat(x, "x");
   TORCH_CHECK(w.is_cuda() && w.dim() == 2 && w.scalar_type() == at::kBFloat16 && w.is_contiguous(),
@@ -670,33 +667,18 @@ std::vector<at::Tensor> conv1x1_dual(at::Tensor dy, at::Tensor x, at::Tensor w, 
   TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "conv1x1_dual: fp32/bf16 weight gradient");
   const int64_t M = dy.size(0);
   const int Cout = (int)dy.size(1), Cin = (int)x.size(1);
-  const bool fork = addend.has_value() && addend->defined();
-  const int groups = fork ? conv1x1_dual_fork_groups(M, Cin, Cout) : conv1x1_dual_groups(M, Cin, Cout);
+  const int groups = conv1x1_dual_groups(M, Cin, Cout);
   if (!groups || dy.stride(0) != Cout || x.stride(0) != Cin) return {};
   const bool bn = y_bn.has_value() && y_bn->defined();
-  const uint8_t* amp = nullptr;
-  if (fork) {
-    TORCH_CHECK(bn && bn_mode == 1, "conv1x1_dual: the fork form applies a BN with a recomputed ReLU (bn_mode 1)");
-    check_mat(*addend, "addend");
-    TORCH_CHECK(addend->sizes() == x.sizes() && addend->stride(0) == Cin, "conv1x1_dual: addend must be laid out like x");
-    if (addend_mask.has_value() && addend_mask->defined()) {
-      TORCH_CHECK(addend_mask->scalar_type() == at::kByte && addend_mask->is_contiguous() &&
-                      addend_mask->numel() * 8 >= M * Cin,
-                  "conv1x1_dual: the addend's 1-bit mask");
-      amp = addend_mask->data_ptr<uint8_t>();
-    }
-  }
   if (bn) {
-    TORCH_CHECK(bn_mode == 1 || bn_mode == 2, "conv1x1_dual: bn_mode 1 (recompute) or 2 (bit mask)");
-    if (!fork && !conv1x1_dual_bn_ok(M, Cin, Cout)) return {};
+    if (!conv1x1_dual_bn_ok(M, Cin, Cout)) return {};
     check_mat(*y_bn, "y_bn");
     TORCH_CHECK(y_bn->sizes() == dy.sizes() && y_bn->stride(0) == Cout, "conv1x1_dual: y_bn must be laid out like dy");
     TORCH_CHECK(ws.has_value() && ws->scalar_type() == at::kFloat && ws->is_contiguous() && ws->numel() == 7 * Cout,
                 "conv1x1_dual: ws must be the BN's finalized 7C workspace");
-    if (bn_mode == 2)
-      TORCH_CHECK(mask.has_value() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
-                      mask->numel() * 8 >= M * Cout,
-                  "conv1x1_dual: the BN's 1-bit ReLU mask");
+    TORCH_CHECK(mask.has_value() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                    mask->numel() * 8 >= M * Cout,
+                "conv1x1_dual: the BN's 1-bit ReLU mask");
   }
   at::Tensor dx = at::empty({M, Cin}, dy.options());
   at::Tensor part = at::empty({(int64_t)groups * Cout * Cin}, dy.options().dtype(at::kFloat));
@@ -704,9 +686,7 @@ std::vector<at::Tensor> conv1x1_dual(at::Tensor dy, at::Tensor x, at::Tensor w, 
   hipStream_t st = current_stream(dy);
   TORCH_CHECK(launch_conv1x1_dual(dy.data_ptr(), x.data_ptr(), w.data_ptr(), dx.data_ptr(), part.data_ptr<float>(), M,
                                   Cin, Cout, st, bn ? y_bn->data_ptr() : nullptr,
-                                  bn && bn_mode == 2 ? mask->data_ptr<uint8_t>() : nullptr,
-                                  bn ? ws->data_ptr<float>() : nullptr, (int)bn_mode,
-                                  fork ? addend->data_ptr() : nullptr, amp),
+                                  bn ? mask->data_ptr<uint8_t>() : nullptr, bn ? ws->data_ptr<float>() : nullptr),
               "conv1x1_dual: kernel refused a shape it planned");
   launch_splitk_reduce(part.data_ptr<float>(), groups, (int64_t)Cout * Cin, dw.data_ptr(),
                        out_dtype == at::kFloat ? kF32 : kBF16, 1.f, false, st);
@@ -1098,12 +1078,7 @@ void bind_nn(pybind11::module& m) {
   m.def("conv1x1_dual", &conv1x1_dual, "stride-1 1x1 conv data + weight gradient in one pass over dy",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("out_dtype") = at::kFloat,
         pybind11::arg("y_bn") = pybind11::none(), pybind11::arg("ws") = pybind11::none(),
-        pybind11::arg("mask") = pybind11::none(), pybind11::arg("bn_mode") = 2,
-        pybind11::arg("addend") = pybind11::none(), pybind11::arg("addend_mask") = pybind11::none());
-  m.def("set_dual_fork_rows", &set_dual_fork_rows, "A/B: 32- or 64-row tiles of the fork form (default 64)");
-  m.def("conv1x1_dual_fork_groups", [](int64_t M, int64_t Cin, int64_t Cout) { return conv1x1_dual_fork_groups(M, (int)Cin, (int)Cout); },
-        "row groups of the fork form of the one-pass 1x1 gradient kernel (0: shape not served)");
-  m.def("set_dual_wreg", &set_dual_wreg, "A/B: Cout-512 one-pass kernel with register-held weights (1) or the LDS panel (0)");
+        pybind11::arg("mask") = pybind11::none());
   m.def("conv1x1_dual_bn_ok", [](int64_t M, int64_t Cin, int64_t Cout) { return conv1x1_dual_bn_ok(M, (int)Cin, (int)Cout); },
         "the one-pass 1x1 gradient kernel can also apply the consuming BN's backward for this shape");
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),

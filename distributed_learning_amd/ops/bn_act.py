@@ -83,12 +83,10 @@ class _BNAct(torch.autograd.Function):
         m = mask if mask is not None and mask.numel() else None
         ctx.save_for_backward(x, ws, weight, m)
         ctx.link = BNLink(x, ws, m, ctx.mask_mode) if training and x.dtype == torch.bfloat16 else None
-        # the producing 1x1 conv applies this BN's backward itself (ops/conv.py DualBNLink): a bit-mask ReLU after
-        # the residual add with the residual gradient handed to the fork (conv3), or a ReLU recomputed from x with
-        # no residual (the fork conv1); bf16
-        ok = dlink is not None and x.dtype == torch.bfloat16 and ctx.mask_mode in dlink.modes and (
-            (ctx.mask_mode == MASK_BITS and ctx.rlink is not None and m is not None) or
-            (ctx.mask_mode == MASK_RECOMPUTE and not ctx.has_res))
+        # the producing 1x1 conv (the block's conv3) applies this BN's backward itself (ops/conv.py DualBNLink):
+        # a bit-mask ReLU after the residual add, the residual gradient handed to the fork; bf16
+        ok = (dlink is not None and x.dtype == torch.bfloat16 and ctx.mask_mode == MASK_BITS
+              and ctx.rlink is not None and m is not None)
         ctx.dlink = dlink if ok else None
         return y
 
@@ -136,8 +134,7 @@ class _BNDualAct(torch.autograd.Function):
         ctx.save_for_backward(x, ws, weight, xd, wsd, weight_d, mask if relu else None)
         # both inputs come from 1x1 convs that can apply their BN's backward themselves (ops/conv.py DualBNLink)
         ctx.dlinks = (dlink, dlink_d) if (dlink is not None and dlink_d is not None and relu and mask is not None
-                                           and mask.numel() and x.dtype == torch.bfloat16
-                                           and MASK_BITS in dlink.modes and MASK_BITS in dlink_d.modes) else None
+                                           and mask.numel() and x.dtype == torch.bfloat16) else None
         return y
 
     @staticmethod

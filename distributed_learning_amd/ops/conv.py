@@ -231,11 +231,8 @@ DUAL_1X1_MAX_COUT = 512  # A/B: 256 keeps it to stage 1
 # backward apply inside the same kernel: the BN backward stops after its reduction and hands (dy, y, mask,
 # coefficients) over; dY never reaches HBM (gemm_dual.hip kBN).
 DUAL_BN = True
-# ... and the block's first BN(+ReLU) inside its conv1 (fork) backward: off -- with 32-row tiles of 64-128 channels
-# the per-tile cost dominates (3.0 / 1.6 ms per call at stages 1 / 2 vs ~1.5 / 0.8 ms for apply + dgrad + wgrad;
-# 88.1 vs 84.2 ms/step, profiles/r4/g11), and 64-row tiles are still slower (87.2 vs 84.5, g12); kept selectable
-# and tested (tests/test_gpu_gemm_dual.py)
-DUAL_FORK = False
+# (The block's first BN(+ReLU) inside its conv1 (fork) backward was built and measured slower -- 32-row tiles of
+# 64-128 channels: 88.1 vs 84.2 ms/step, profiles/r4/g11; 64-row tiles: 87.2 vs 84.5, g12 -- and removed.)
 
 
 class DualBNLink:
@@ -246,10 +243,9 @@ class DualBNLink:
     one-pass kernel with the BN apply fused. If autograd summed the placeholder with other gradients of the
     conv output (more consumers), the conv backward materialises the BN's gradient and adds it."""
 
-    __slots__ = ("modes", "ph", "dout", "ybn", "ws", "mask", "weight", "mode")
+    __slots__ = ("ph", "dout", "ybn", "ws", "mask", "weight", "mode")
 
-    def __init__(self, modes=(2,)):
-        self.modes = modes  # BN ReLU modes the conv's kernel applies: 2 bit mask (conv3), 1 recomputed (fork)
+    def __init__(self):
         self.ph = self.dout = self.ybn = self.ws = self.mask = self.weight = self.mode = None
 
     def park(self, dout, ybn, ws, mask, weight, mode=2):
@@ -392,9 +388,6 @@ class _Conv1x1Fork(torch.autograd.Function):
         y2, stats = C.gemm_nt(_rows(x), w2, want_stats)
         y = y2.view(n, h, w, cout).permute(0, 3, 1, 2)
         ctx.save_for_backward(x, w2)
-        # the block's first BN(+ReLU) applied inside the one-pass kernel of this conv's backward (fork form)
-        ctx.dlink = DualBNLink((1,)) if (DUAL_1X1 and DUAL_BN and DUAL_FORK and not sub and x.dtype == torch.bfloat16
-                                         and C.conv1x1_dual_fork_groups(n * h * w, cin, cout) > 0) else None
         ctx.wdtype = weight.dtype
         ctx.wshape = weight.shape
         ctx.weight_leaf = weight if weight.is_leaf else None
@@ -433,21 +426,6 @@ class _Conv1x1Fork(torch.autograd.Function):
                 dident = full
             return dident, None, None, None, None
         odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
-        dl = ctx.dlink
-        if dl is not None and dl.ph is not None:
-            parked = dl.take()
-            ph, dout, ybn, ws, _, _, _ = parked
-            if (dy is not None and dy.data_ptr() == ph.data_ptr() and dy.stride() == ph.stride() and dsub is None
-                    and dident is not None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
-                    and not _wants_defer("1x1", ctx, x.shape[1], ybn.shape[1])):
-                out = C.conv1x1_dual(_rows(dout), _rows(x), w2, odt, _rows(ybn), ws, None, 1, _rows(dident), amask)
-                if out:  # BN apply + data gradient (+ identity gradient) + weight gradient in one pass
-                    CALLS["1x1_dual_fork"] += 1
-                    return (out[0].view(n, h, w, cin).permute(0, 3, 1, 2),
-                            _as_param_layout(out[1].to(ctx.wdtype), ctx.wshape, ctx.wstride), None, None, None)
-            dy = dl.materialise(C, dy, parked)
-        if dy is None:  # (only reachable through the link: the no-dy case returned above)
-            return dident, None, None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
         dy2 = _rows(dy)
         dx = dw = None
@@ -506,9 +484,6 @@ def conv1x1_fork(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False, sub
     y, stats, xa, xs = _Conv1x1Fork.apply(x, conv.weight, want_stats, rlink, sub)
     if rlink is not None:
         xa._dla_fork = rlink
-    dl = getattr(y.grad_fn, "dlink", None) if y.grad_fn is not None else None
-    if dl is not None:
-        y._dla_dual = dl
     return y, stats, xa, xs
 
 

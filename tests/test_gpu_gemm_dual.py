@@ -48,28 +48,6 @@ def test_dual_not_served_shapes(C):
     assert C.conv1x1_dual_blocks(1 << 20, 256, 64) == 0
     assert C.conv1x1_dual_blocks(1 << 20, 512, 512) == 0
     assert C.conv1x1_dual_bn_ok(1 << 20, 64, 256) and not C.conv1x1_dual_bn_ok(1 << 20, 128, 512)
-    assert C.conv1x1_dual_fork_groups(4014080, 256, 64) == 64 and C.conv1x1_dual_fork_groups(1 << 20, 512, 128) == 32
-    assert C.conv1x1_dual_fork_groups(1 << 20, 1024, 256) == 0 and C.conv1x1_dual_fork_groups(1000, 256, 64) == 0
-
-
-@pytest.mark.parametrize("wreg", [0, 1])
-def test_dual_cout512_weight_forms_agree(cuda, C, wreg):
-    """The Cout-512 kernel with register-held weight fragments (3-stage ring) and with the LDS panel
-    (2-stage): the same products in the same order."""
-    M = 60001
-    g = torch.Generator().manual_seed(7)
-    dy = torch.randn(M, 512, generator=g).to(cuda, torch.bfloat16)
-    x = torch.randn(M, 128, generator=g).to(cuda, torch.bfloat16)
-    w = (torch.randn(512, 128, generator=g) * 0.05).to(cuda, torch.bfloat16)
-    try:
-        C.set_dual_wreg(wreg)
-        dx, dw = C.conv1x1_dual(dy, x, w, torch.float32)
-    finally:
-        C.set_dual_wreg(1)
-    ref = dy.float() @ w.float()
-    assert float((dx.float() - ref).norm() / ref.norm()) < 5e-3
-    dw_ref = dy.double().t() @ x.double()
-    assert float((dw.double() - dw_ref).norm() / dw_ref.norm()) < 1e-5
 
 
 def test_conv_autograd_uses_dual_and_matches(cuda):
@@ -106,8 +84,7 @@ def test_conv_autograd_uses_dual_and_matches(cuda):
 @pytest.mark.parametrize("M,ci,co", [(65536, 64, 256), (100003, 64, 256)])
 def test_dual_with_bn_apply_matches_separate(cuda, C, M, ci, co):
     """kBN: the consuming BN(+residual)+ReLU's backward apply inside the kernel (gradient, BN input, bit mask,
-    finalized coefficients) == bn_act_bwd's apply pass followed by the plain one-pass kernel (Cout 512: the
-    weight fragments held in registers)."""
+    finalized coefficients) == bn_act_bwd's apply pass followed by the plain one-pass kernel."""
     g = torch.Generator().manual_seed(M + ci)
     dout = torch.randn(M, co, generator=g).to(cuda, torch.bfloat16)
     ybn = (torch.randn(M, co, generator=g) * 2 + 0.5).to(cuda, torch.bfloat16)
@@ -148,17 +125,15 @@ def test_resnet_with_and_without_fused_bn_apply(cuda):
         m = resnet50(10).to(cuda).to(memory_format=CL)
         dnn.bf16_weights(m)
         x = torch.randn(24, 3, 224, 224, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
-        old = nconv.DUAL_BN, nconv.DUAL_FORK
-        nconv.DUAL_BN = nconv.DUAL_FORK = flag
-        before, before_f = nconv.CALLS["1x1_dual_bn"], nconv.CALLS["1x1_dual_fork"]
+        old = nconv.DUAL_BN
+        nconv.DUAL_BN = flag
+        before = nconv.CALLS["1x1_dual_bn"]
         try:
             m(x).float().square().mean().backward()
         finally:
-            nconv.DUAL_BN, nconv.DUAL_FORK = old
+            nconv.DUAL_BN = old
         # stage 1: the conv3 of blocks 1 and 2, and block 0's conv3 + downsample conv (its dual BN hands both over)
         assert (nconv.CALLS["1x1_dual_bn"] - before == 4) == flag
-        # fork form: conv1 of stage-1 blocks 1-2 and stage-2 blocks 1-3 (block 0 forks hand on a subsample)
-        assert (nconv.CALLS["1x1_dual_fork"] - before_f == 5) == flag
         return {n: p.grad.float().clone() for n, p in m.named_parameters()}
 
     dnn.set_backend("native")
@@ -170,48 +145,6 @@ def test_resnet_with_and_without_fused_bn_apply(cuda):
         dnn.set_backend("torch")
     rels = sorted(float((g1[n] - g0[n]).norm() / g0[n].norm().clamp_min(1e-20)) for n in g0)
     assert rels[len(rels) // 2] < 2e-2 and rels[-1] < 0.2, rels[-5:]
-
-
-@pytest.mark.parametrize("rows", [32, 64])
-@pytest.mark.parametrize("M,ci,co,masked", [(80001, 256, 64, True), (80001, 256, 64, False), (30011, 512, 128, True)])
-def test_dual_fork_form_matches_separate(cuda, C, M, ci, co, masked, rows):
-    """Fork form: the block's first BN(+ReLU recomputed from its input) applied on the fly, data gradient with the
-    identity gradient added under its 1-bit mask (gemm_stream's kAdd arithmetic), weight gradient -- against
-    bn_act_bwd's apply pass, the k-major gemm_nt with the masked addend and gemm_tn."""
-    g = torch.Generator().manual_seed(M + ci + masked)
-    dout = torch.randn(M, co, generator=g).to(cuda, torch.bfloat16)
-    ybn = (torch.randn(M, co, generator=g) * 2 + 0.3).to(cuda, torch.bfloat16)
-    x = torch.randn(M, ci, generator=g).to(cuda, torch.bfloat16)
-    w = (torch.randn(co, ci, generator=g) * co ** -0.5).to(cuda, torch.bfloat16)
-    add = torch.randn(M, ci, generator=g).to(cuda, torch.bfloat16)
-    amask = torch.randint(0, 256, ((M * ci + 7) // 8,), generator=g, dtype=torch.uint8).to(cuda) if masked else None
-    gamma = (torch.rand(co, generator=g) + 0.5).to(cuda)
-    yf = ybn.float()
-    ws = torch.zeros(7 * co, device=cuda)
-    ws[:co] = yf.mean(0)
-    ws[co:2 * co] = (yf.var(0, unbiased=False) + 1e-5).rsqrt()
-    ws[2 * co:3 * co] = gamma * ws[co:2 * co]          # forward scale / shift: the ReLU recompute reads them
-    ws[3 * co:4 * co] = -ws[:co] * ws[2 * co:3 * co] + 0.1
-    ws_a, ws_b = ws.clone(), ws.clone()
-    assert C.conv1x1_dual_fork_groups(M, ci, co) > 0
-    dY = C.bn_act_bwd(dout, None, None, ybn, ws_a, gamma, 1, False, None)[0]
-    dx_ref, _ = C.gemm_nt(dY, w, False, add, True, 0, amask)
-    dw_ref = C.gemm_tn(dY, x, torch.float32, 1.0)
-    C.bn_act_bwd(dout, None, None, ybn, ws_b, gamma, 1, False, None, False)
-    try:
-        C.set_dual_fork_rows(rows)
-        dx, dw = C.conv1x1_dual(dout, x, w, torch.float32, ybn, ws_b, None, 1, add, amask)
-    finally:
-        C.set_dual_fork_rows(64)
-    torch.cuda.synchronize()
-    assert torch.equal(ws_a, ws_b)
-    scale = float(dx_ref.float().abs().max())
-    assert float((dx.float() - dx_ref.float()).abs().max()) <= scale * 2 ** -7
-    bits = torch.ones(M * ci, device=cuda) if amask is None else \
-        torch.stack([(amask >> j) & 1 for j in range(8)], 1).reshape(-1)[: M * ci].float()
-    ref = dY.float() @ w.float() + add.float() * bits.view(M, ci)
-    assert float((dx.float() - ref).norm() / ref.norm()) < 5e-3
-    assert float((dw - dw_ref).norm() / dw_ref.norm()) < 1e-5
 
 
 def test_bn_handoff_falls_back_when_output_has_other_consumers(cuda):
