@@ -36,7 +36,10 @@ constexpr int kUCi = 64;  // input channels per block (slice)
 constexpr int kUMaskWave = 1024;  // bytes of mask area per wave and stage (the first R / 4 rows x CO / 8 used)
 // kWReg: each wave holds its W^T fragments in registers instead of a block-wide LDS panel (Cout 512: the
 // 64 KB panel would leave no room for a deeper ring or the kBN tiles).
-template <int CO, int R, int NS, bool kBN = false, bool kWReg = false>
+// kXN: X is the INPUT of a BatchNorm+ReLU (its finalized 7 CI workspace xws): the landed X slice is normalised in
+// LDS (bn_apply's fmaf(x, scale, shift), max 0, bf16) before the weight gradient reads it; the slice's 64 scale /
+// shift pairs sit in a 512-byte LDS table behind the ring.
+template <int CO, int R, int NS, bool kBN = false, bool kWReg = false, bool kXN = false>
 struct DualCfg {
   static constexpr int KC = CO / kBK;                 // dY sub-images per tile
   static constexpr int Sub = R * kBK;                 // elements of one [R][64] sub-image
@@ -52,7 +55,8 @@ struct DualCfg {
   static constexpr int NCF = RF;                      // data gradient: 16-channel fragments per wave (4 waves)
   static constexpr int Stores = NCF / 2;              // dX stores per lane per tile (4 NCF channels)
   static constexpr int TMW = CO / 64;                 // weight gradient: 16-row co fragments per wave
-  static constexpr size_t Lds = (size_t)((kWReg ? 0 : KC * Panel) + NS * Stage) * sizeof(bf16_t);
+  static constexpr size_t Ring = (size_t)((kWReg ? 0 : KC * Panel) + NS * Stage) * sizeof(bf16_t);
+  static constexpr size_t Lds = Ring + (kXN ? 2 * kUCi * sizeof(float) : 0);
   static_assert(Lds <= 160 * 1024, "dual 1x1 LDS budget");
   static_assert(Slots >= 1 && (RF == 2 || RF == 4) && (NS == 2 || NS == 3), "tile configuration");
 };
@@ -68,6 +72,7 @@ struct DualArgs {
   const bf16_t* ybn;     // kBN: the BN input [M][CO]
   const uint8_t* mask;   // kBN: its ReLU bit mask (bit e of byte e >> 3, e = m * CO + c)
   const float* ws;       // kBN: the finalized 7 CO workspace (mean, ..., k1, m1, k2)
+  const float* xws;      // kXN: the X BatchNorm's finalized 7 CI workspace (scale at 2 CI, shift at 3 CI)
 };
 
 // image row of panel-local weight row p (gemm_stream.hip): MFMA A-operand row 16 i + 4 g + r holds output
@@ -90,9 +95,9 @@ __device__ __forceinline__ bf16x8_t urm_tr_frag(const bf16_t* s, int c0, int kk)
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
-template <int CO, int R, int NS, bool kBN = false, bool kWReg = false>
+template <int CO, int R, int NS, bool kBN = false, bool kWReg = false, bool kXN = false>
 __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) {
-  using G = DualCfg<CO, R, NS, kBN, kWReg>;
+  using G = DualCfg<CO, R, NS, kBN, kWReg, kXN>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16_t* Ws = reinterpret_cast<bf16_t*>(smem_raw);  // KC sub-images [64 ci (permuted)][64 co]
   bf16_t* ring = Ws + (kWReg ? 0 : G::KC * G::Panel);  // NS stages
@@ -200,6 +205,10 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
     }
   };
 
+  float* Nt = reinterpret_cast<float*>(smem_raw + G::Ring);  // kXN: [64] scale, [64] shift of the slice
+  if constexpr (kXN) {
+    if (tid < 2 * kUCi) Nt[tid] = s.xws[(2 + tid / kUCi) * CI + ci0 + tid % kUCi];
+  }
   // the panel's plain loads and LDS writes complete before the ring starts counting
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
@@ -238,6 +247,28 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
     issue(t + NS - 1);
     bf16_t* Ds = ring + (t % NS) * G::Stage;  // dY sub-images
     const bf16_t* Xs = Ds + G::Xs * G::Sub;   // X slice
+    if constexpr (kXN) {
+      // BN + ReLU over this thread's landed X chunks (chunk c = tid + 256 i at element 8 c: row c / 8, logical
+      // 8-channel chunk (c ^ (c >> 4)) & 7); rows past M stay zero
+      bf16_t* Xn = Ds + G::Xs * G::Sub;
+      const int64_t row0 = (int64_t)(grp + t * s.mg) * R;
+      const int lc = (tid ^ (tid >> 4)) & 7;
+#pragma unroll
+      for (int i = 0; i < G::Slots; ++i) {
+        if (row0 + vr[i] < M) {
+          ushort8_t v = *reinterpret_cast<const ushort8_t*>(Xn + (tid + 256 * i) * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            v[e] = f32_to_bf16(fmaxf(fmaf(bf16_to_f32((bf16_t)v[e]), Nt[lc * 8 + e], Nt[kUCi + lc * 8 + e]), 0.f));
+          *reinterpret_cast<ushort8_t*>(Xn + (tid + 256 * i) * 8) = v;
+        }
+      }
+      if constexpr (!kBN) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+    }
     if constexpr (kBN) {
       // dY = k1 (g - m1 - (y - mean) k2) over the gradient in place; g = the gradient where the ReLU passed
       const bf16_t* Ys = Ds + G::KC * G::Sub;
@@ -357,23 +388,30 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout) {
 bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout) { return Cout == 256 && conv1x1_dual_blocks(M, Cin, Cout) > 0; }
 
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
-                         int Cout, hipStream_t stream, const void* ybn, const uint8_t* mask, const float* ws) {
+                         int Cout, hipStream_t stream, const void* ybn, const uint8_t* mask, const float* ws,
+                         const float* xws) {
   const int mg = conv1x1_dual_groups(M, Cin, Cout);
   if (!mg) return false;
   const int nsl = Cin / kUCi, grid = mg * nsl;
   DualArgs a{(const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)dx, part, (int)M, Cin, mg, mg / 8, nsl,
-             (const bf16_t*)ybn, mask, ws};
-#define DLA_DUAL(CO_, R_, NS_, BN_, WR_)                                                                       \
-  hipLaunchKernelGGL((conv1x1_dual_kernel<CO_, R_, NS_, BN_, WR_>), dim3(grid), dim3(256),                      \
-                     (DualCfg<CO_, R_, NS_, BN_, WR_>::Lds), stream, a)
+             (const bf16_t*)ybn, mask, ws, xws};
+#define DLA_DUAL(CO_, R_, NS_, BN_, WR_, XN_)                                                                  \
+  hipLaunchKernelGGL((conv1x1_dual_kernel<CO_, R_, NS_, BN_, WR_, XN_>), dim3(grid), dim3(256),                 \
+                     (DualCfg<CO_, R_, NS_, BN_, WR_, XN_>::Lds), stream, a)
   if (ybn) {
     if (!conv1x1_dual_bn_ok(M, Cin, Cout) || !mask || !ws) return false;
-    DLA_DUAL(256, 32, 3, true, false);
+    if (xws) DLA_DUAL(256, 32, 3, true, false, true);
+    else DLA_DUAL(256, 32, 3, true, false, false);
     return true;
   }
   // Cout 512: weight fragments in registers + a 3-stage ring (the LDS-panel form fits only 2 stages: slower)
-  if (Cout == 256) DLA_DUAL(256, 64, 3, false, false);
-  else DLA_DUAL(512, 32, 3, false, true);
+  if (Cout == 256) {
+    if (xws) DLA_DUAL(256, 64, 3, false, false, true);
+    else DLA_DUAL(256, 64, 3, false, false, false);
+  } else {
+    if (xws) DLA_DUAL(512, 32, 3, false, true, true);
+    else DLA_DUAL(512, 32, 3, false, true, false);
+  }
 #undef DLA_DUAL
   return true;
 }

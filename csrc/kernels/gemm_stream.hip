@@ -69,6 +69,10 @@ struct StreamArgs {
   const float* bws;
   const uint8_t* bmask;
   int bmode;
+  // kNrm (forward): A is the INPUT of a BatchNorm+ReLU whose finalized 7K workspace this is; each landed
+  // A chunk is normalised in LDS (bn_apply's fmaf(x, scale, shift), max 0, bf16) before the MFMAs read it,
+  // so the activation is never written to HBM
+  const float* nws;
 };
 
 // image row of panel-local weight row p (0..63 within a wave's 64 columns): the MFMA A-operand row
@@ -88,10 +92,11 @@ typedef int i32x4_t __attribute__((ext_vector_type(4)));
 // 4-chunk ring of the other variants.
 __host__ __device__ constexpr bool stream_two_blocks(bool add, bool bnb) { return add && !bnb; }
 
-template <int BN, int KC, bool kBT, bool kStats, bool kAdd = false, int kBM = -1>
+template <int BN, int KC, bool kBT, bool kStats, bool kAdd = false, int kBM = -1, bool kNrm = false>
 __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) void gemm_stream_kernel(const StreamArgs s) {
   constexpr bool kBnb = kBM >= 0;
   static_assert(!(kStats && kBnb), "the partials buffer holds either the statistics or the BN-backward sums");
+  static_assert(!kNrm || (!kBT && !kAdd && !kBnb && KC <= 2), "normalise-on-load: forward, K <= 128");
   constexpr int kSP = stream_lookahead(KC, stream_two_blocks(kAdd, kBnb));
   constexpr int kSS = kSP + 1;
   constexpr int WN = 64;                    // columns per wave
@@ -177,6 +182,13 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
     vo[i] = (uint32_t)(((int64_t)r * s.lda + rm_glds_kc(c)) * 2);
   }
   const uint32_t ring0 = lds_addr(ring) + (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
+  // kNrm: the thread's DMA chunks c = tid + 256 i land at element 8 c of a slot and hold row c / 8, logical
+  // 8-channel chunk (c ^ (c >> 4)) & 7 of the K-chunk: the same 8 channels for every i. The K scale / shift
+  // pairs sit in an LDS table behind the ring (written before the barrier below).
+  float* Nt = reinterpret_cast<float*>(ring + kSS * kChunkElems);  // [K] scale, [K] shift
+  if constexpr (kNrm) {
+    if (tid < 2 * KC * kBK) Nt[tid] = s.nws[(2 + tid / (KC * kBK)) * KC * kBK + tid % (KC * kBK)];
+  }
   auto issue = [&](int q) {
     const int t = q / KC, kc = q % KC;
     const int64_t row0 = (int64_t)(grp + t * s.mg) * kSBM;  // past the end for q >= nchunk: all OOB
@@ -269,6 +281,26 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
     asm volatile("" ::: "memory");
     issue(q + kSP);  // past this block's last chunk: OOB rows, zeros into a free slot (uniform counts)
     const int kc = q % KC;
+    if constexpr (kNrm) {
+      // BN + ReLU over this thread's landed chunks of slot q; rows past M stay zero (the statistics and the
+      // stored rows then match the materialised activation's exactly)
+      bf16_t* An = ring + (q % kSS) * kChunkElems;
+      const int64_t row0 = (int64_t)(grp + (q / KC) * s.mg) * kSBM;
+      const float* nt = Nt + kc * kBK + ((tid ^ (tid >> 4)) & 7) * 8;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        if (row0 + vr[i] < M) {
+          ushort8_t v = *reinterpret_cast<const ushort8_t*>(An + (tid + 256 * i) * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            v[e] = f32_to_bf16(fmaxf(fmaf(bf16_to_f32((bf16_t)v[e]), nt[e], nt[KC * kBK + e]), 0.f));
+          *reinterpret_cast<ushort8_t*>(An + (tid + 256 * i) * 8) = v;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
     if (kc == 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -375,9 +407,10 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
   }
 }
 
-template <int BN, int KC, bool kTwo>
+template <int BN, int KC, bool kTwo, bool kNrm = false>
 constexpr size_t stream_lds_bytes() {
-  return (size_t)(KC * BN * kBK + (stream_lookahead(KC, kTwo) + 1) * kChunkElems) * sizeof(bf16_t);
+  return (size_t)(KC * BN * kBK + (stream_lookahead(KC, kTwo) + 1) * kChunkElems) * sizeof(bf16_t) +
+         (kNrm ? 2 * KC * kBK * sizeof(float) : 0);
 }
 
 int g_stream_mode = -1;  // -1: environment (DLA_GEMM_STREAM, default on), 0 off, 1 on (every K <= 256)
@@ -449,6 +482,14 @@ void launch_stream_kc(const StreamArgs& a, int grid, bool kmajor, bool stats, bo
   }
 #undef DLA_SBN
   constexpr size_t lds = stream_lds_bytes<BN, KC, false>();
+  if constexpr (KC <= 2) {
+    if (a.nws) {  // normalise-on-load forward (A = a BN+ReLU input)
+      constexpr size_t nlds = stream_lds_bytes<BN, KC, false, true>();
+      if (stats) hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, false, true, false, -1, true>), g, b, nlds, stream, a);
+      else hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, false, false, false, -1, true>), g, b, nlds, stream, a);
+      return;
+    }
+  }
   if (kmajor) {
     if (stats) hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, true, true>), g, b, lds, stream, a);
     else hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, true, false>), g, b, lds, stream, a);
@@ -468,9 +509,10 @@ int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_k
 
 bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
                         int M, int N, int K, float* stats, hipStream_t stream, const void* addend, int64_t ldd,
-                        const uint8_t* addend_mask, const BnBwdArgs* bn_bwd) {
+                        const uint8_t* addend_mask, const BnBwdArgs* bn_bwd, const float* a_ws) {
   const StreamPlan p = stream_plan(M, N, K, lda, ldc, b_kmajor, addend != nullptr, bn_bwd != nullptr);
   if (!p.mg) return false;
+  if (a_ws && (b_kmajor || addend || bn_bwd || K > 128)) return false;
   if (addend && (stats || !b_kmajor || ldd % 8 != 0 || (int64_t)M * ldd * 2 >= (int64_t)kOOB)) return false;
   if (bn_bwd) {  // partials go where the statistics would: [mg][N][2]
     const int64_t ldbx = bn_bwd->ldx ? bn_bwd->ldx : ldc;
@@ -479,7 +521,7 @@ bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, 
   StreamArgs a{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, p.mg, p.per_xcd,
                bn_bwd ? bn_bwd->part : stats, (const bf16_t*)addend, ldd, addend_mask,
                bn_bwd ? (const bf16_t*)bn_bwd->x : nullptr, bn_bwd ? (bn_bwd->ldx ? bn_bwd->ldx : ldc) : 0,
-               bn_bwd ? bn_bwd->ws : nullptr, bn_bwd ? bn_bwd->mask : nullptr, bn_bwd ? bn_bwd->mode : 0};
+               bn_bwd ? bn_bwd->ws : nullptr, bn_bwd ? bn_bwd->mask : nullptr, bn_bwd ? bn_bwd->mode : 0, a_ws};
   const int kc = K / kBK;
   if (p.bn == 128) {
     if (kc == 1) launch_stream_kc<128, 1>(a, p.grid, b_kmajor, stats != nullptr, addend != nullptr, stream);
