@@ -36,9 +36,9 @@ constexpr int kUCi = 64;  // input channels per block (slice)
 constexpr int kUMaskWave = 1024;  // bytes of mask area per wave and stage (the first R / 4 rows x CO / 8 used)
 // kWReg: each wave holds its W^T fragments in registers instead of a block-wide LDS panel (Cout 512: the
 // 64 KB panel would leave no room for a deeper ring or the kBN tiles).
-// kXN: X is the INPUT of a BatchNorm+ReLU (its finalized 7 CI workspace xws): the landed X slice is normalised in
-// LDS (bn_apply's fmaf(x, scale, shift), max 0, bf16) before the weight gradient reads it; the slice's 64 scale /
-// shift pairs sit in a 512-byte LDS table behind the ring.
+// kXN: X is the INPUT of a BatchNorm+ReLU (its finalized 7 CI workspace xws): the weight gradient's X operand
+// fragments are normalised in registers after their LDS read (bn_apply's fmaf(x, scale, shift), max 0, bf16); a
+// lane's fragment holds one channel, so its scale / shift pairs are 4 registers each.
 template <int CO, int R, int NS, bool kBN = false, bool kWReg = false, bool kXN = false>
 struct DualCfg {
   static constexpr int KC = CO / kBK;                 // dY sub-images per tile
@@ -55,8 +55,7 @@ struct DualCfg {
   static constexpr int NCF = RF;                      // data gradient: 16-channel fragments per wave (4 waves)
   static constexpr int Stores = NCF / 2;              // dX stores per lane per tile (4 NCF channels)
   static constexpr int TMW = CO / 64;                 // weight gradient: 16-row co fragments per wave
-  static constexpr size_t Ring = (size_t)((kWReg ? 0 : KC * Panel) + NS * Stage) * sizeof(bf16_t);
-  static constexpr size_t Lds = Ring + (kXN ? 2 * kUCi * sizeof(float) : 0);
+  static constexpr size_t Lds = (size_t)((kWReg ? 0 : KC * Panel) + NS * Stage) * sizeof(bf16_t);
   static_assert(Lds <= 160 * 1024, "dual 1x1 LDS budget");
   static_assert(Slots >= 1 && (RF == 2 || RF == 4) && (NS == 2 || NS == 3), "tile configuration");
 };
@@ -205,9 +204,14 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
     }
   };
 
-  float* Nt = reinterpret_cast<float*>(smem_raw + G::Ring);  // kXN: [64] scale, [64] shift of the slice
+  // kXN: scale / shift of the lane's weight-gradient channels ci0 + 16 j + lr
+  float xsc[kXN ? 4 : 1], xsh[kXN ? 4 : 1];
   if constexpr (kXN) {
-    if (tid < 2 * kUCi) Nt[tid] = s.xws[(2 + tid / kUCi) * CI + ci0 + tid % kUCi];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      xsc[j] = s.xws[2 * CI + ci0 + 16 * j + lr];
+      xsh[j] = s.xws[3 * CI + ci0 + 16 * j + lr];
+    }
   }
   // the panel's plain loads and LDS writes complete before the ring starts counting
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -247,28 +251,6 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
     issue(t + NS - 1);
     bf16_t* Ds = ring + (t % NS) * G::Stage;  // dY sub-images
     const bf16_t* Xs = Ds + G::Xs * G::Sub;   // X slice
-    if constexpr (kXN) {
-      // BN + ReLU over this thread's landed X chunks (chunk c = tid + 256 i at element 8 c: row c / 8, logical
-      // 8-channel chunk (c ^ (c >> 4)) & 7); rows past M stay zero
-      bf16_t* Xn = Ds + G::Xs * G::Sub;
-      const int64_t row0 = (int64_t)(grp + t * s.mg) * R;
-      const int lc = (tid ^ (tid >> 4)) & 7;
-#pragma unroll
-      for (int i = 0; i < G::Slots; ++i) {
-        if (row0 + vr[i] < M) {
-          ushort8_t v = *reinterpret_cast<const ushort8_t*>(Xn + (tid + 256 * i) * 8);
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            v[e] = f32_to_bf16(fmaxf(fmaf(bf16_to_f32((bf16_t)v[e]), Nt[lc * 8 + e], Nt[kUCi + lc * 8 + e]), 0.f));
-          *reinterpret_cast<ushort8_t*>(Xn + (tid + 256 * i) * 8) = v;
-        }
-      }
-      if constexpr (!kBN) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      }
-    }
     if constexpr (kBN) {
       // dY = k1 (g - m1 - (y - mean) k2) over the gradient in place; g = the gradient where the ReLU passed
       const bf16_t* Ys = Ds + G::KC * G::Sub;
@@ -323,6 +305,18 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
       bf16x8_t bf[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) bf[j] = urm_tr_frag(Xs, 16 * j, kk);
+      if constexpr (kXN) {
+        // lane (lr, g) of fragment j: channel ci0 + 16 j + lr of tile rows kk 32 + 8 g .. + 7; rows past M stay 0
+        const int valid = (int)min((int64_t)R, (int64_t)M - (int64_t)(grp + t * s.mg) * R) - (kk * 32 + 8 * g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ushort8_t v = __builtin_bit_cast(ushort8_t, bf[j]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            v[e] = e < valid ? f32_to_bf16(fmaxf(fmaf(bf16_to_f32((bf16_t)v[e]), xsc[j], xsh[j]), 0.f)) : (uint16_t)0;
+          bf[j] = __builtin_bit_cast(bf16x8_t, v);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < G::TMW; ++i) {
         const int co = (CO / 4) * wave + 16 * i;

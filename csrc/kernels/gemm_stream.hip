@@ -69,8 +69,8 @@ struct StreamArgs {
   const float* bws;
   const uint8_t* bmask;
   int bmode;
-  // kNrm (forward): A is the INPUT of a BatchNorm+ReLU whose finalized 7K workspace this is; each landed
-  // A chunk is normalised in LDS (bn_apply's fmaf(x, scale, shift), max 0, bf16) before the MFMAs read it,
+  // kNrm (forward): A is the INPUT of a BatchNorm+ReLU whose finalized 7K workspace this is; each A operand
+  // fragment is normalised in registers after its LDS read (bn_apply's fmaf(x, scale, shift), max 0, bf16),
   // so the activation is never written to HBM
   const float* nws;
 };
@@ -182,9 +182,7 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
     vo[i] = (uint32_t)(((int64_t)r * s.lda + rm_glds_kc(c)) * 2);
   }
   const uint32_t ring0 = lds_addr(ring) + (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
-  // kNrm: the thread's DMA chunks c = tid + 256 i land at element 8 c of a slot and hold row c / 8, logical
-  // 8-channel chunk (c ^ (c >> 4)) & 7 of the K-chunk: the same 8 channels for every i. The K scale / shift
-  // pairs sit in an LDS table behind the ring (written before the barrier below).
+  // kNrm: the K scale / shift pairs sit in an LDS table behind the ring (written before the barrier below)
   float* Nt = reinterpret_cast<float*>(ring + kSS * kChunkElems);  // [K] scale, [K] shift
   if constexpr (kNrm) {
     if (tid < 2 * KC * kBK) Nt[tid] = s.nws[(2 + tid / (KC * kBK)) * KC * kBK + tid % (KC * kBK)];
@@ -281,26 +279,6 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
     asm volatile("" ::: "memory");
     issue(q + kSP);  // past this block's last chunk: OOB rows, zeros into a free slot (uniform counts)
     const int kc = q % KC;
-    if constexpr (kNrm) {
-      // BN + ReLU over this thread's landed chunks of slot q; rows past M stay zero (the statistics and the
-      // stored rows then match the materialised activation's exactly)
-      bf16_t* An = ring + (q % kSS) * kChunkElems;
-      const int64_t row0 = (int64_t)(grp + (q / KC) * s.mg) * kSBM;
-      const float* nt = Nt + kc * kBK + ((tid ^ (tid >> 4)) & 7) * 8;
-#pragma unroll
-      for (int i = 0; i < D; ++i) {
-        if (row0 + vr[i] < M) {
-          ushort8_t v = *reinterpret_cast<const ushort8_t*>(An + (tid + 256 * i) * 8);
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            v[e] = f32_to_bf16(fmaxf(fmaf(bf16_to_f32((bf16_t)v[e]), nt[e], nt[KC * kBK + e]), 0.f));
-          *reinterpret_cast<ushort8_t*>(An + (tid + 256 * i) * 8) = v;
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
     if (kc == 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -316,6 +294,24 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
       for (int i = 0; i < 4; ++i) wf[i] = rm_glds_frag(Ws, wn * WN + 16 * i, kk);
 #pragma unroll
       for (int j = 0; j < TJ; ++j) xf[j] = rm_glds_frag(As, wm * WM + 16 * j, kk);
+      if constexpr (kNrm) {
+        // the lane's 8 values of fragment j: channels kc 64 + kk 32 + 8 g .. + 7 of row wm WM + 16 j + lr
+        // (rows past M are zero-filled; normalised they are not zero, so the statistics below skip them)
+        const float* nt = Nt + kc * kBK + kk * 32 + 8 * g;
+        float sc[8], sh[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          sc[e] = nt[e];
+          sh[e] = nt[KC * kBK + e];
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          ushort8_t v = __builtin_bit_cast(ushort8_t, xf[j]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = f32_to_bf16(fmaxf(fmaf(bf16_to_f32((bf16_t)v[e]), sc[e], sh[e]), 0.f));
+          xf[j] = __builtin_bit_cast(bf16x8_t, v);
+        }
+      }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -347,7 +343,8 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
               h[r] = f32_to_bf16(bf16_to_f32(h[r]) + (((bits >> e) & 1u) ? d : 0.f));
             }
             if constexpr (kStats) {
-              const float v = bf16_to_f32(h[r]);  // statistics of the stored values; OOB rows are 0
+              // statistics of the stored values; OOB rows are 0 (kNrm: excluded explicitly)
+              const float v = !kNrm || ok ? bf16_to_f32(h[r]) : 0.f;
               st_s[i][r] += v;
               st_q[i][r] = fmaf(v, v, st_q[i][r]);
             }
