@@ -233,7 +233,7 @@ DUAL_1X1_MAX_COUT = 512  # A/B: 256 keeps it to stage 1
 DUAL_BN = True
 # relu(BN2) of a bottleneck never written to HBM: conv3 normalises it on load in both directions
 # (_BNActConv1x1; models/resnet.py hands it over as a LazyBNAct).
-LAZY_BN_ACT = True
+LAZY_BN_ACT = False  # until measured on the register form (g19)
 # (The block's first BN(+ReLU) inside its conv1 (fork) backward was built and measured slower -- 32-row tiles of
 # 64-128 channels: 88.1 vs 84.2 ms/step, profiles/r4/g11; 64-row tiles: 87.2 vs 84.5, g12 -- and removed.)
 
