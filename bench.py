@@ -284,7 +284,7 @@ def phase_breakdown(parts, n: int, csv_path=None, name="bench"):
 def _dual_calls():
     from distributed_learning_amd.ops import conv as nconv
 
-    return {k: nconv.CALLS[k] for k in ("1x1_dual", "1x1_dual_bn", "1x1_norm")}
+    return {k: nconv.CALLS[k] for k in ("1x1_dual", "1x1_dual_bn")}
 
 
 def main():

@@ -144,8 +144,6 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
                    int ext_nrb = 0, uint8_t* relu_mask = nullptr, int64_t ldy = 0);
 // y = act(BN(x) + BN_d(xd)) from the two finalized workspaces (ws, wsd: launch_bn_fwd with y == nullptr);
 // mask as launch_bn_fwd's ReLU-after-residual bit mask.
-void launch_bn_apply(const void* x, void* y, const float* ws, int64_t M, int C, int dtype, bool relu,
-                     hipStream_t stream);  // apply only, from a finalized workspace
 void launch_bn_dual_apply(const void* x, const void* xd, void* y, const float* ws, const float* wsd, int64_t M, int C,
                           int dtype, bool relu, uint8_t* mask, hipStream_t stream);
 // backward of launch_bn_dual_apply: dx, dxd and both (dgamma, dbeta) from one dy (+ the forward's
@@ -278,8 +276,7 @@ struct BnBwdArgs;
 // [gemm_stream_rows][N][2] are written to bn_bwd->part instead of statistics.
 bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
                         int M, int N, int K, float* stats, hipStream_t stream, const void* addend = nullptr,
-                        int64_t ldd = 0, const uint8_t* addend_mask = nullptr, const BnBwdArgs* bn_bwd = nullptr,
-                        const float* a_ws = nullptr);  // a_ws: A is a BN+ReLU input, normalised on load (fwd, K <= 128)
+                        int64_t ldd = 0, const uint8_t* addend_mask = nullptr, const BnBwdArgs* bn_bwd = nullptr);
 void set_gemm_stream(int mode);
 // BatchNorm-backward reduction fused into a bf16-output GEMM epilogue (the output is the BN's dy):
 // x = the BN input [M, N], ws = its 7N workspace, mask/mode as launch_bn_bwd (0, 1 or 2),
@@ -314,7 +311,7 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout);
 bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout);
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
                          int Cout, hipStream_t stream, const void* ybn = nullptr, const uint8_t* mask = nullptr,
-                         const float* ws = nullptr, const float* xws = nullptr);  // xws: X normalised on load
+                         const float* ws = nullptr);
 // out[n] (= scale * sum_s partial[s][n] [+ addend] [+ out]), fp32 or bf16 out; addend: bf16 rows of
 // ncol with row stride ld_addend (0 = one broadcast row).
 void launch_splitk_reduce(const float* partial, int splits, int64_t n, void* out, int out_dtype, float scale,

@@ -895,23 +895,6 @@ void launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, in
 #undef DLA_BN_APPLY
 }
 
-// The apply pass alone, from a finalized workspace (an activation normalised on load elsewhere, materialised for a
-// consumer that cannot): y = act(x * scale + shift), bn_apply's arithmetic.
-void launch_bn_apply(const void* x, void* y, const float* ws, int64_t M, int C, int dtype, bool relu,
-                     hipStream_t stream) {
-  int atpr, anrb, anct;
-  bn_geometry(M, C, &atpr, &anrb, &anct, 4096);
-#define DLA_BN_APPLY(T, A)                                                                                         \
-  hipLaunchKernelGGL((bn_apply_kernel<T, false, A>), dim3(anct, anrb), dim3(kBNThreads), 0, stream, (const T*)x,   \
-                     nullptr, (T*)y, ws, M, C, anrb, atpr, nullptr, nullptr, 0)
-  if (dtype == kBF16) {
-    if (relu) DLA_BN_APPLY(bf16_t, true); else DLA_BN_APPLY(bf16_t, false);
-  } else {
-    if (relu) DLA_BN_APPLY(float, true); else DLA_BN_APPLY(float, false);
-  }
-#undef DLA_BN_APPLY
-}
-
 void launch_bn_dual_apply(const void* x, const void* xd, void* y, const float* ws, const float* wsd, int64_t M, int C,
                           int dtype, bool relu, uint8_t* mask, hipStream_t stream) {
   int atpr, anrb, anct;

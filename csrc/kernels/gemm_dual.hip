@@ -36,10 +36,7 @@ constexpr int kUCi = 64;  // input channels per block (slice)
 constexpr int kUMaskWave = 1024;  // bytes of mask area per wave and stage (the first R / 4 rows x CO / 8 used)
 // kWReg: each wave holds its W^T fragments in registers instead of a block-wide LDS panel (Cout 512: the
 // 64 KB panel would leave no room for a deeper ring or the kBN tiles).
-// kXN: X is the INPUT of a BatchNorm+ReLU (its finalized 7 CI workspace xws): the weight gradient's X operand
-// fragments are normalised in registers after their LDS read (bn_apply's fmaf(x, scale, shift), max 0, bf16); a
-// lane's fragment holds one channel, so its scale / shift pairs are 4 registers each.
-template <int CO, int R, int NS, bool kBN = false, bool kWReg = false, bool kXN = false>
+template <int CO, int R, int NS, bool kBN = false, bool kWReg = false>
 struct DualCfg {
   static constexpr int KC = CO / kBK;                 // dY sub-images per tile
   static constexpr int Sub = R * kBK;                 // elements of one [R][64] sub-image
@@ -71,7 +68,6 @@ struct DualArgs {
   const bf16_t* ybn;     // kBN: the BN input [M][CO]
   const uint8_t* mask;   // kBN: its ReLU bit mask (bit e of byte e >> 3, e = m * CO + c)
   const float* ws;       // kBN: the finalized 7 CO workspace (mean, ..., k1, m1, k2)
-  const float* xws;      // kXN: the X BatchNorm's finalized 7 CI workspace (scale at 2 CI, shift at 3 CI)
 };
 
 // image row of panel-local weight row p (gemm_stream.hip): MFMA A-operand row 16 i + 4 g + r holds output
@@ -94,9 +90,9 @@ __device__ __forceinline__ bf16x8_t urm_tr_frag(const bf16_t* s, int c0, int kk)
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
-template <int CO, int R, int NS, bool kBN = false, bool kWReg = false, bool kXN = false>
+template <int CO, int R, int NS, bool kBN = false, bool kWReg = false>
 __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) {
-  using G = DualCfg<CO, R, NS, kBN, kWReg, kXN>;
+  using G = DualCfg<CO, R, NS, kBN, kWReg>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16_t* Ws = reinterpret_cast<bf16_t*>(smem_raw);  // KC sub-images [64 ci (permuted)][64 co]
   bf16_t* ring = Ws + (kWReg ? 0 : G::KC * G::Panel);  // NS stages
@@ -204,15 +200,6 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
     }
   };
 
-  // kXN: scale / shift of the lane's weight-gradient channels ci0 + 16 j + lr
-  float xsc[kXN ? 4 : 1], xsh[kXN ? 4 : 1];
-  if constexpr (kXN) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      xsc[j] = s.xws[2 * CI + ci0 + 16 * j + lr];
-      xsh[j] = s.xws[3 * CI + ci0 + 16 * j + lr];
-    }
-  }
   // the panel's plain loads and LDS writes complete before the ring starts counting
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
@@ -305,18 +292,6 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
       bf16x8_t bf[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) bf[j] = urm_tr_frag(Xs, 16 * j, kk);
-      if constexpr (kXN) {
-        // lane (lr, g) of fragment j: channel ci0 + 16 j + lr of tile rows kk 32 + 8 g .. + 7; rows past M stay 0
-        const int valid = (int)min((int64_t)R, (int64_t)M - (int64_t)(grp + t * s.mg) * R) - (kk * 32 + 8 * g);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          ushort8_t v = __builtin_bit_cast(ushort8_t, bf[j]);
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            v[e] = e < valid ? f32_to_bf16(fmaxf(fmaf(bf16_to_f32((bf16_t)v[e]), xsc[j], xsh[j]), 0.f)) : (uint16_t)0;
-          bf[j] = __builtin_bit_cast(bf16x8_t, v);
-        }
-      }
 #pragma unroll
       for (int i = 0; i < G::TMW; ++i) {
         const int co = (CO / 4) * wave + 16 * i;
@@ -382,30 +357,23 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout) {
 bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout) { return Cout == 256 && conv1x1_dual_blocks(M, Cin, Cout) > 0; }
 
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
-                         int Cout, hipStream_t stream, const void* ybn, const uint8_t* mask, const float* ws,
-                         const float* xws) {
+                         int Cout, hipStream_t stream, const void* ybn, const uint8_t* mask, const float* ws) {
   const int mg = conv1x1_dual_groups(M, Cin, Cout);
   if (!mg) return false;
   const int nsl = Cin / kUCi, grid = mg * nsl;
   DualArgs a{(const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)w, (bf16_t*)dx, part, (int)M, Cin, mg, mg / 8, nsl,
-             (const bf16_t*)ybn, mask, ws, xws};
-#define DLA_DUAL(CO_, R_, NS_, BN_, WR_, XN_)                                                                  \
-  hipLaunchKernelGGL((conv1x1_dual_kernel<CO_, R_, NS_, BN_, WR_, XN_>), dim3(grid), dim3(256),                 \
-                     (DualCfg<CO_, R_, NS_, BN_, WR_, XN_>::Lds), stream, a)
+             (const bf16_t*)ybn, mask, ws};
+#define DLA_DUAL(CO_, R_, NS_, BN_, WR_)                                                                       \
+  hipLaunchKernelGGL((conv1x1_dual_kernel<CO_, R_, NS_, BN_, WR_>), dim3(grid), dim3(256),                      \
+                     (DualCfg<CO_, R_, NS_, BN_, WR_>::Lds), stream, a)
   if (ybn) {
     if (!conv1x1_dual_bn_ok(M, Cin, Cout) || !mask || !ws) return false;
-    if (xws) DLA_DUAL(256, 32, 3, true, false, true);
-    else DLA_DUAL(256, 32, 3, true, false, false);
+    DLA_DUAL(256, 32, 3, true, false);
     return true;
   }
   // Cout 512: weight fragments in registers + a 3-stage ring (the LDS-panel form fits only 2 stages: slower)
-  if (Cout == 256) {
-    if (xws) DLA_DUAL(256, 64, 3, false, false, true);
-    else DLA_DUAL(256, 64, 3, false, false, false);
-  } else {
-    if (xws) DLA_DUAL(512, 32, 3, false, true, true);
-    else DLA_DUAL(512, 32, 3, false, true, false);
-  }
+  if (Cout == 256) DLA_DUAL(256, 64, 3, false, false);
+  else DLA_DUAL(512, 32, 3, false, true);
 #undef DLA_DUAL
   return true;
 }

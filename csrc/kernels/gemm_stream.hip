@@ -69,10 +69,6 @@ struct StreamArgs {
   const float* bws;
   const uint8_t* bmask;
   int bmode;
-  // kNrm (forward): A is the INPUT of a BatchNorm+ReLU whose finalized 7K workspace this is; each A operand
-  // fragment is normalised in registers after its LDS read (bn_apply's fmaf(x, scale, shift), max 0, bf16),
-  // so the activation is never written to HBM
-  const float* nws;
 };
 
 // image row of panel-local weight row p (0..63 within a wave's 64 columns): the MFMA A-operand row
@@ -92,11 +88,10 @@ typedef int i32x4_t __attribute__((ext_vector_type(4)));
 // 4-chunk ring of the other variants.
 __host__ __device__ constexpr bool stream_two_blocks(bool add, bool bnb) { return add && !bnb; }
 
-template <int BN, int KC, bool kBT, bool kStats, bool kAdd = false, int kBM = -1, bool kNrm = false>
+template <int BN, int KC, bool kBT, bool kStats, bool kAdd = false, int kBM = -1>
 __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) void gemm_stream_kernel(const StreamArgs s) {
   constexpr bool kBnb = kBM >= 0;
   static_assert(!(kStats && kBnb), "the partials buffer holds either the statistics or the BN-backward sums");
-  static_assert(!kNrm || (!kBT && !kAdd && !kBnb && KC <= 2), "normalise-on-load: forward, K <= 128");
   constexpr int kSP = stream_lookahead(KC, stream_two_blocks(kAdd, kBnb));
   constexpr int kSS = kSP + 1;
   constexpr int WN = 64;                    // columns per wave
@@ -182,11 +177,6 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
     vo[i] = (uint32_t)(((int64_t)r * s.lda + rm_glds_kc(c)) * 2);
   }
   const uint32_t ring0 = lds_addr(ring) + (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
-  // kNrm: the K scale / shift pairs sit in an LDS table behind the ring (written before the barrier below)
-  float* Nt = reinterpret_cast<float*>(ring + kSS * kChunkElems);  // [K] scale, [K] shift
-  if constexpr (kNrm) {
-    if (tid < 2 * KC * kBK) Nt[tid] = s.nws[(2 + tid / (KC * kBK)) * KC * kBK + tid % (KC * kBK)];
-  }
   auto issue = [&](int q) {
     const int t = q / KC, kc = q % KC;
     const int64_t row0 = (int64_t)(grp + t * s.mg) * kSBM;  // past the end for q >= nchunk: all OOB
@@ -294,24 +284,6 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
       for (int i = 0; i < 4; ++i) wf[i] = rm_glds_frag(Ws, wn * WN + 16 * i, kk);
 #pragma unroll
       for (int j = 0; j < TJ; ++j) xf[j] = rm_glds_frag(As, wm * WM + 16 * j, kk);
-      if constexpr (kNrm) {
-        // the lane's 8 values of fragment j: channels kc 64 + kk 32 + 8 g .. + 7 of row wm WM + 16 j + lr
-        // (rows past M are zero-filled; normalised they are not zero, so the statistics below skip them)
-        const float* nt = Nt + kc * kBK + kk * 32 + 8 * g;
-        float sc[8], sh[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          sc[e] = nt[e];
-          sh[e] = nt[KC * kBK + e];
-        }
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) {
-          ushort8_t v = __builtin_bit_cast(ushort8_t, xf[j]);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = f32_to_bf16(fmaxf(fmaf(bf16_to_f32((bf16_t)v[e]), sc[e], sh[e]), 0.f));
-          xf[j] = __builtin_bit_cast(bf16x8_t, v);
-        }
-      }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -343,8 +315,7 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
               h[r] = f32_to_bf16(bf16_to_f32(h[r]) + (((bits >> e) & 1u) ? d : 0.f));
             }
             if constexpr (kStats) {
-              // statistics of the stored values; OOB rows are 0 (kNrm: excluded explicitly)
-              const float v = !kNrm || ok ? bf16_to_f32(h[r]) : 0.f;
+              const float v = bf16_to_f32(h[r]);  // statistics of the stored values; OOB rows are 0
               st_s[i][r] += v;
               st_q[i][r] = fmaf(v, v, st_q[i][r]);
             }
@@ -404,10 +375,9 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
   }
 }
 
-template <int BN, int KC, bool kTwo, bool kNrm = false>
+template <int BN, int KC, bool kTwo>
 constexpr size_t stream_lds_bytes() {
-  return (size_t)(KC * BN * kBK + (stream_lookahead(KC, kTwo) + 1) * kChunkElems) * sizeof(bf16_t) +
-         (kNrm ? 2 * KC * kBK * sizeof(float) : 0);
+  return (size_t)(KC * BN * kBK + (stream_lookahead(KC, kTwo) + 1) * kChunkElems) * sizeof(bf16_t);
 }
 
 int g_stream_mode = -1;  // -1: environment (DLA_GEMM_STREAM, default on), 0 off, 1 on (every K <= 256)
@@ -479,14 +449,6 @@ void launch_stream_kc(const StreamArgs& a, int grid, bool kmajor, bool stats, bo
   }
 #undef DLA_SBN
   constexpr size_t lds = stream_lds_bytes<BN, KC, false>();
-  if constexpr (KC <= 2) {
-    if (a.nws) {  // normalise-on-load forward (A = a BN+ReLU input)
-      constexpr size_t nlds = stream_lds_bytes<BN, KC, false, true>();
-      if (stats) hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, false, true, false, -1, true>), g, b, nlds, stream, a);
-      else hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, false, false, false, -1, true>), g, b, nlds, stream, a);
-      return;
-    }
-  }
   if (kmajor) {
     if (stats) hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, true, true>), g, b, lds, stream, a);
     else hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, true, false>), g, b, lds, stream, a);
@@ -506,10 +468,9 @@ int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_k
 
 bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
                         int M, int N, int K, float* stats, hipStream_t stream, const void* addend, int64_t ldd,
-                        const uint8_t* addend_mask, const BnBwdArgs* bn_bwd, const float* a_ws) {
+                        const uint8_t* addend_mask, const BnBwdArgs* bn_bwd) {
   const StreamPlan p = stream_plan(M, N, K, lda, ldc, b_kmajor, addend != nullptr, bn_bwd != nullptr);
   if (!p.mg) return false;
-  if (a_ws && (b_kmajor || addend || bn_bwd || K > 128)) return false;
   if (addend && (stats || !b_kmajor || ldd % 8 != 0 || (int64_t)M * ldd * 2 >= (int64_t)kOOB)) return false;
   if (bn_bwd) {  // partials go where the statistics would: [mg][N][2]
     const int64_t ldbx = bn_bwd->ldx ? bn_bwd->ldx : ldc;
@@ -518,7 +479,7 @@ bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, 
   StreamArgs a{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, p.mg, p.per_xcd,
                bn_bwd ? bn_bwd->part : stats, (const bf16_t*)addend, ldd, addend_mask,
                bn_bwd ? (const bf16_t*)bn_bwd->x : nullptr, bn_bwd ? (bn_bwd->ldx ? bn_bwd->ldx : ldc) : 0,
-               bn_bwd ? bn_bwd->ws : nullptr, bn_bwd ? bn_bwd->mask : nullptr, bn_bwd ? bn_bwd->mode : 0, a_ws};
+               bn_bwd ? bn_bwd->ws : nullptr, bn_bwd ? bn_bwd->mask : nullptr, bn_bwd ? bn_bwd->mode : 0};
   const int kc = K / kBK;
   if (p.bn == 128) {
     if (kc == 1) launch_stream_kc<128, 1>(a, p.grid, b_kmajor, stats != nullptr, addend != nullptr, stream);

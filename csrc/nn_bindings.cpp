@@ -651,69 +651,6 @@ at::Tensor gemm_tn(at::Tensor A, at::Tensor B, c10::ScalarType out_dtype, double
   return out;
 }
 
-// Forward 1x1 conv of relu(BN(x)) without materialising the activation: the streaming GEMM normalises each
-// landed A chunk in LDS with the finalized workspace ws (7K). Returns (C, stats) or [] when the streaming kernel
-// does not serve the shape (the caller materialises the activation).
-std::vector<at::Tensor> gemm_nt_norm(at::Tensor A, at::Tensor B, bool stats, at::Tensor ws) {
-  check_mat(A, "A");
-  check_mat(B, "B");
-  TORCH_CHECK(A.size(1) == B.size(1), "gemm_nt_norm: K mismatch");
-  const int M = (int)A.size(0), N = (int)B.size(0), K = (int)A.size(1);
-  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() == 7 * (int64_t)K,
-              "gemm_nt_norm: ws must be the finalized 7K BN workspace");
-  if (K > 128 || M <= 0) return {};
-  at::Tensor C = at::empty({M, N}, A.options());
-  const int srows = gemm_stream_rows(M, N, K, A.stride(0), C.stride(0), false, false);
-  if (srows <= 0) return {};
-  at::Tensor S;
-  if (stats) S = at::empty({srows, N, 2}, A.options().dtype(at::kFloat));
-  TORCH_CHECK(launch_gemm_stream(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), false, C.data_ptr(), C.stride(0),
-                                 M, N, K, stats ? S.data_ptr<float>() : nullptr, current_stream(A), nullptr, 0, nullptr,
-                                 nullptr, ws.data_ptr<float>()),
-              "gemm_nt_norm: streaming kernel refused a shape it planned");
-  return {C, S};
-}
-
-// Training BN statistics only (finalize from the producing conv's epilogue partials, or a statistics pass;
-// running statistics updated): returns the 7C workspace. The apply runs later, inside the consumer.
-at::Tensor bn_stats_ws(at::Tensor x, c10::optional<at::Tensor> weight, c10::optional<at::Tensor> bias,
-                       c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var, double momentum,
-                       double eps, c10::optional<at::Tensor> stats) {
-  check_act(x, "x");
-  const int C = (int)x.size(1);
-  const int64_t M = rows_of(x);
-  auto f32 = x.options().dtype(at::kFloat);
-  auto fptr = [](const c10::optional<at::Tensor>& t) -> float* {
-    if (!t.has_value() || !t->defined()) return nullptr;
-    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "BN parameters/stats must be fp32 contiguous");
-    return t->data_ptr<float>();
-  };
-  const bool ext = stats.has_value() && stats->defined();
-  if (ext)
-    TORCH_CHECK(stats->scalar_type() == at::kFloat && stats->is_contiguous() && stats->dim() == 3 &&
-                    stats->size(1) == C && stats->size(2) == 2,
-                "stats must be fp32 [row_blocks, C, 2] partials");
-  at::Tensor ws = at::empty({7 * (int64_t)C}, f32);
-  at::Tensor part = at::empty({ext ? ext_part_floats(stats, C) : partial_floats(M, C)}, f32);
-  launch_bn_fwd(x.data_ptr(), nullptr, nullptr, M, C, dtype_code(x), fptr(weight), fptr(bias), (float)eps,
-                (float)momentum, fptr(running_mean), fptr(running_var), ws.data_ptr<float>(), part.data_ptr<float>(),
-                false, true, current_stream(x), ext ? stats->data_ptr<float>() : nullptr, ext ? (int)stats->size(0) : 0,
-                nullptr, 0);
-  return ws;
-}
-
-// act(x * scale + shift) from a finalized workspace (bn_apply's arithmetic): the activation an on-load
-// normalisation skipped, materialised for a consumer that needs it.
-at::Tensor bn_apply_ws(at::Tensor x, at::Tensor ws, bool relu) {
-  check_act(x, "x");
-  const int C = (int)x.size(1);
-  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() == 7 * (int64_t)C, "bn_apply_ws: ws");
-  at::Tensor y = at::empty_like(x);
-  launch_bn_apply(x.data_ptr(), y.data_ptr(), ws.data_ptr<float>(), rows_of(x), C, dtype_code(x), relu,
-                  current_stream(x));
-  return y;
-}
-
 // Data and weight gradient of a stride-1 1x1 conv in one pass over dy (gemm_dual.hip): dy [M, Cout], x [M, Cin]
 // rows, w [Cout, Cin]. Returns (dx [M, Cin] bf16, dw [Cout, Cin] out_dtype), or an empty list when the shape
 // is not served (the caller then runs gemm_nt + gemm_tn).
@@ -721,7 +658,7 @@ at::Tensor bn_apply_ws(at::Tensor x, at::Tensor ws, bool relu) {
 // output; its backward apply (bit-mask ReLU, finalized ws) runs inside the kernel.
 std::vector<at::Tensor> conv1x1_dual(at::Tensor dy, at::Tensor x, at::Tensor w, c10::ScalarType out_dtype,
                                      c10::optional<at::Tensor> y_bn, c10::optional<at::Tensor> ws,
-                                     c10::optional<at::Tensor> mask, c10::optional<at::Tensor> x_ws) {
+                                     c10::optional<at::Tensor> mask) {
   check_mat(dy, "dy");
   check_mat(x, "x");
   TORCH_CHECK(w.is_cuda() && w.dim() == 2 && w.scalar_type() == at::kBFloat16 && w.is_contiguous(),
@@ -743,18 +680,13 @@ std::vector<at::Tensor> conv1x1_dual(at::Tensor dy, at::Tensor x, at::Tensor w, 
                     mask->numel() * 8 >= M * Cout,
                 "conv1x1_dual: the BN's 1-bit ReLU mask");
   }
-  const bool xn = x_ws.has_value() && x_ws->defined();
-  if (xn)
-    TORCH_CHECK(x_ws->scalar_type() == at::kFloat && x_ws->is_contiguous() && x_ws->numel() == 7 * Cin,
-                "conv1x1_dual: x_ws must be the finalized 7 Cin workspace of the BN+ReLU that x feeds");
   at::Tensor dx = at::empty({M, Cin}, dy.options());
   at::Tensor part = at::empty({(int64_t)groups * Cout * Cin}, dy.options().dtype(at::kFloat));
   at::Tensor dw = at::empty({Cout, Cin}, dy.options().dtype(out_dtype));
   hipStream_t st = current_stream(dy);
   TORCH_CHECK(launch_conv1x1_dual(dy.data_ptr(), x.data_ptr(), w.data_ptr(), dx.data_ptr(), part.data_ptr<float>(), M,
                                   Cin, Cout, st, bn ? y_bn->data_ptr() : nullptr,
-                                  bn ? mask->data_ptr<uint8_t>() : nullptr, bn ? ws->data_ptr<float>() : nullptr,
-                                  xn ? x_ws->data_ptr<float>() : nullptr),
+                                  bn ? mask->data_ptr<uint8_t>() : nullptr, bn ? ws->data_ptr<float>() : nullptr),
               "conv1x1_dual: kernel refused a shape it planned");
   launch_splitk_reduce(part.data_ptr<float>(), groups, (int64_t)Cout * Cin, dw.data_ptr(),
                        out_dtype == at::kFloat ? kF32 : kBF16, 1.f, false, st);
@@ -1146,11 +1078,7 @@ void bind_nn(pybind11::module& m) {
   m.def("conv1x1_dual", &conv1x1_dual, "stride-1 1x1 conv data + weight gradient in one pass over dy",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("out_dtype") = at::kFloat,
         pybind11::arg("y_bn") = pybind11::none(), pybind11::arg("ws") = pybind11::none(),
-        pybind11::arg("mask") = pybind11::none(), pybind11::arg("x_ws") = pybind11::none());
-  m.def("gemm_nt_norm", &gemm_nt_norm, "1x1 conv forward of relu(BN(A)) with the BN applied on load (streaming GEMM)",
-        pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("stats"), pybind11::arg("ws"));
-  m.def("bn_stats_ws", &bn_stats_ws, "training BN statistics -> finalized 7C workspace (no apply)");
-  m.def("bn_apply_ws", &bn_apply_ws, "act(x * scale + shift) from a finalized BN workspace");
+        pybind11::arg("mask") = pybind11::none());
   m.def("conv1x1_dual_bn_ok", [](int64_t M, int64_t Cin, int64_t Cout) { return conv1x1_dual_bn_ok(M, (int)Cin, (int)Cout); },
         "the one-pass 1x1 gradient kernel can also apply the consuming BN's backward for this shape");
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),

@@ -77,7 +77,7 @@ class Bottleneck(nn.Module):
         else:
             out, xa = dnn.conv_bn_act_fork(x, self.conv1, self.bn1, relu=True)
             xs = None
-        out = dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, lazy_next=self.conv3)
+        out = dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True)
         if self.downsample is None:
             return dnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=xa)
         # the shortcut BN is applied inside the block's final apply pass (never materialised)

@@ -231,9 +231,6 @@ DUAL_1X1_MAX_COUT = 512  # A/B: 256 keeps it to stage 1
 # backward apply inside the same kernel: the BN backward stops after its reduction and hands (dy, y, mask,
 # coefficients) over; dY never reaches HBM (gemm_dual.hip kBN).
 DUAL_BN = True
-# relu(BN2) of a bottleneck never written to HBM: conv3 normalises it on load in both directions
-# (_BNActConv1x1; models/resnet.py hands it over as a LazyBNAct).
-LAZY_BN_ACT = False  # until measured on the register form (g19)
 # (The block's first BN(+ReLU) inside its conv1 (fork) backward was built and measured slower -- 32-row tiles of
 # 64-128 channels: 88.1 vs 84.2 ms/step, profiles/r4/g11; 64-row tiles: 87.2 vs 84.5, g12 -- and removed.)
 
@@ -368,127 +365,6 @@ class _Conv1x1(torch.autograd.Function):
         return dx, dw, None, None
 
 
-class _BNActConv1x1(torch.autograd.Function):
-    """``conv1x1(relu(BN(y)))`` (training BN, stride 1) without the activation in HBM.
-
-    Forward: the BN statistics are finalized (no apply pass) and the streaming GEMM normalises each landed
-    A chunk in LDS (gemm_stream.hip kNrm). Backward: the one-pass data + weight gradient kernel normalises
-    the saved BN input's X tiles the same way (gemm_dual.hip kXN), also with the consuming BN's apply fused
-    (DualBNLink) where that runs; the data gradient is the BN+ReLU's incoming gradient and the BN backward
-    (ReLU recomputed from y) follows. Either kernel declining a shape: the activation is materialised with
-    bn_apply's arithmetic, so every path computes the same bf16 activation."""
-
-    @staticmethod
-    def forward(ctx, y, gamma, beta, rm, rv, momentum, eps, stats, weight, want_stats: bool):
-        C = _ext.require()
-        ctx.set_materialize_grads(False)
-        ws = C.bn_stats_ws(y, gamma, beta, rm, rv, momentum, eps, stats)
-        n, cin, h, w = y.shape
-        cout = weight.shape[0]
-        w2 = weight.reshape(cout, cin).to(torch.bfloat16).contiguous()
-        out = C.gemm_nt_norm(_rows(y), w2, want_stats, ws)
-        if out:
-            y3, st = out
-            CALLS["1x1_norm"] += 1
-        else:
-            y3, st = C.gemm_nt(_rows(C.bn_apply_ws(y, ws, True)), w2, want_stats)
-        ctx.save_for_backward(y, ws, gamma, w2)
-        ctx.dlink = DualBNLink() if (DUAL_1X1 and DUAL_BN and cout <= DUAL_1X1_MAX_COUT
-                                     and C.conv1x1_dual_bn_ok(n * h * w, cin, cout)) else None
-        ctx.wdtype = weight.dtype
-        ctx.wshape = weight.shape
-        ctx.wstride = weight.stride()
-        if st is not None:
-            ctx.mark_non_differentiable(st)
-        return y3.view(n, h, w, cout).permute(0, 3, 1, 2), st
-
-    @staticmethod
-    def backward(ctx, dy, _dstats):
-        C = _ext.require()
-        y, ws, gamma, w2 = ctx.saved_tensors
-        n, cin, h, w = y.shape
-        cout = w2.shape[0]
-        odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
-        out = None
-        dl = ctx.dlink
-        if dl is not None and dl.ph is not None:
-            parked = dl.take()
-            ph, dout, ybn, ws3, mask3, _, _ = parked
-            if dy is not None and dy.data_ptr() == ph.data_ptr() and dy.stride() == ph.stride():
-                out = C.conv1x1_dual(_rows(dout), _rows(y), w2, odt, _rows(ybn), ws3, mask3, ws) or None
-                if out:
-                    CALLS["1x1_dual_bn"] += 1
-            if out is None:
-                dy = dl.materialise(C, dy, parked)
-        if out is None:
-            if dy is None:
-                return (None,) * 10
-            dy2 = _rows(dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16))
-            if DUAL_1X1 and cout <= DUAL_1X1_MAX_COUT and C.conv1x1_dual_blocks(dy2.shape[0], cin, cout) > 0:
-                out = C.conv1x1_dual(dy2, _rows(y), w2, odt, None, None, None, ws) or None
-                if out:
-                    CALLS["1x1_dual"] += 1
-            if out is None:
-                a = C.bn_apply_ws(y, ws, True)
-                out = (C.gemm_nt(dy2, w2, False, None, True)[0], C.gemm_tn(dy2, _rows(a), odt, 1.0))
-        da, dw = out
-        dx, _, dg, db = C.bn_act_bwd(da.view(n, h, w, cin).permute(0, 3, 1, 2), None, None, y, ws, gamma, 1,
-                                     False, None)
-        need = ctx.needs_input_grad
-        return (dx, dg if need[1] else None, db if need[2] else None, None, None, None, None, None,
-                _as_param_layout(dw.to(ctx.wdtype), ctx.wshape, ctx.wstride) if need[8] else None, None)
-
-
-class LazyBNAct:
-    """``relu(BN(y))`` of a training BN whose apply is left to the consuming 1x1 conv (conv1x1 takes it
-    directly; anything else calls ``materialize()``, the ordinary fused BN+ReLU)."""
-
-    __slots__ = ("y", "bn", "stats")
-
-    def __init__(self, y, bn, stats):
-        self.y, self.bn, self.stats = y, bn, stats
-
-    @property
-    def is_cuda(self) -> bool:
-        return self.y.is_cuda
-
-    def materialize(self) -> torch.Tensor:
-        from .bn_act import fused_bn_act
-
-        return fused_bn_act(self.y, self.bn, True, None, self.stats)
-
-
-def lazy_ok(y: torch.Tensor, bn: nn.BatchNorm2d, stats, conv: nn.Conv2d) -> bool:
-    """Whether relu(bn(y)) may be handed to ``conv`` as a LazyBNAct."""
-    from .bn_act import supported as bn_supported
-
-    if not (LAZY_BN_ACT and DUAL_1X1 and stats is not None and bn.training and bn.affine and bn.track_running_stats
-            and y.dtype == torch.bfloat16 and bn_supported(y, bn, None) and supported(y, conv)
-            and conv.stride in ((1, 1), 1) and conv.out_channels <= DUAL_1X1_MAX_COUT):
-        return False
-    # both directions must normalise on load, or the activation would be materialised anyway (twice)
-    C = _ext.require()
-    n, cin, h, w = y.shape
-    m = n * h * w
-    return (cin <= 128 and C.gemm_stream_rows(m, conv.out_channels, cin, cin, conv.out_channels, False) > 0
-            and C.conv1x1_dual_blocks(m, cin, conv.out_channels) > 0)
-
-
-def _conv1x1_lazy(x: LazyBNAct, conv: nn.Conv2d, want_stats: bool):
-    from .bn_act import _PENDING_COUNTERS, flush_bn_counters
-
-    bn = x.bn
-    _PENDING_COUNTERS.append(bn.num_batches_tracked)
-    if len(_PENDING_COUNTERS) >= 1024:
-        flush_bn_counters()
-    y, stats = _BNActConv1x1.apply(x.y, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                   float(bn.momentum or 0.0), float(bn.eps), x.stats, conv.weight, want_stats)
-    dl = getattr(y.grad_fn, "dlink", None) if y.grad_fn is not None else None
-    if dl is not None:
-        y._dla_dual = dl
-    return y, stats
-
-
 class _Conv1x1Fork(torch.autograd.Function):
     """Stride-1 1x1 conv that also hands its input on as a second output (the block's identity
     branch). Both gradients of ``x`` then arrive in one backward call, and the identity gradient
@@ -615,10 +491,6 @@ def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False, stride: 
     """Returns (y, stats-or-None); stats are [row_blocks, Cout, 2] partial (sum, sumsq).
     ``stride`` overrides the module's (1 for an input that is already subsampled)."""
     CALLS["1x1"] += 1
-    if isinstance(x, LazyBNAct):
-        if (stride or conv.stride[0]) == 1:
-            return _conv1x1_lazy(x, conv, want_stats)
-        x = x.materialize()
     s = conv.stride[0] if stride is None else stride
     if x.shape[2] % s or x.shape[3] % s:
         # odd spatial size with stride 2 (output ceil) — keep F.conv2d semantics exactly

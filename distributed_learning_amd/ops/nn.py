@@ -96,34 +96,16 @@ def linear(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
     return fc(x)
 
 
-def _lazy_input(x, conv: nn.Conv2d, presubsampled: bool = False):
-    """A LazyBNAct input stays lazy only for a native stride-1 1x1 conv (which applies it on load)."""
-    from . import conv as nconv
-
-    if isinstance(x, nconv.LazyBNAct) and not (_BACKEND == "native" and _NATIVE_CONV and not presubsampled
-                                               and nconv.supported(x.y, conv) and conv.stride in ((1, 1), 1)):
-        return x.materialize()
-    return x
-
-
 def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool = True,
-                residual: torch.Tensor | None = None, presubsampled: bool = False, lazy_next: nn.Conv2d | None = None):
+                residual: torch.Tensor | None = None, presubsampled: bool = False):
     """``act(BN(conv(x)) [+ residual])``. With the native backend and native convs, a 1x1 conv runs as
     an MFMA GEMM whose epilogue also produces BN's batch statistics (one pass over the conv output
     saved). ``presubsampled``: ``x`` is already the stride-2 subsample a strided 1x1 ``conv`` would
-    take (conv_bn_act_fork(..., subsample=True)), so the conv runs with stride 1. ``lazy_next``: the 1x1
-    conv that consumes the result; where it can normalise on load, a ``LazyBNAct`` is returned instead of
-    the activation (ops/conv.py _BNActConv1x1). ``x`` may itself be a LazyBNAct."""
-    x = _lazy_input(x, conv, presubsampled)
-    if _BACKEND == "native" and _NATIVE_CONV and (x.y if not isinstance(x, torch.Tensor) else x).is_cuda:
+    take (conv_bn_act_fork(..., subsample=True)), so the conv runs with stride 1."""
+    if _BACKEND == "native" and _NATIVE_CONV and x.is_cuda:
         from . import conv as nconv
         from .bn_act import fused_bn_act, supported as bn_supported
 
-        if not isinstance(x, torch.Tensor):  # a LazyBNAct the 1x1 conv applies on load
-            y, stats = nconv.conv1x1(x, conv, want_stats=bn.training)
-            if stats is not None and not bn_supported(y, bn, residual):
-                stats = None
-            return fused_bn_act(y, bn, relu, residual, stats)
         if nconv.supported(x, conv):
             stride = 1 if presubsampled else None
             y, stats = nconv.conv1x1(x, conv, want_stats=bn.training, stride=stride)
@@ -135,8 +117,6 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
             y, stats = nconv.conv3x3(x, conv, want_stats=want)
             if stats is not None and not bn_supported(y, bn, residual):
                 stats = None
-            if lazy_next is not None and relu and residual is None and nconv.lazy_ok(y, bn, stats, lazy_next):
-                return nconv.LazyBNAct(y, bn, stats)
             return fused_bn_act(y, bn, relu, residual, stats)
     if presubsampled:
         y = F.conv2d(x, conv.weight, conv.bias, 1, conv.padding, conv.dilation, conv.groups)
@@ -148,8 +128,6 @@ def _native_conv_stats(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool, presu
     """(y, stats-or-None) from a native 1x1 / 3x3 conv, or None when neither applies."""
     from . import conv as nconv
 
-    if isinstance(x, nconv.LazyBNAct):  # (_lazy_input kept it lazy: a native stride-1 1x1 conv)
-        return nconv.conv1x1(x, conv, want_stats=want_stats)
     if nconv.supported(x, conv):
         return nconv.conv1x1(x, conv, want_stats=want_stats, stride=1 if presubsampled else None)
     if not presubsampled and nconv.supported3x3(x, conv):
@@ -168,11 +146,7 @@ def conv_bn_add_conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d
     shortcut. Native path: both convs emit their BN statistics and one apply pass reads both conv
     outputs (the shortcut BN's output is never written). ``presubsampled``: ``xd`` is already the
     stride-2 subsample the strided ``conv_d`` would take. (Issuing the shortcut conv on a second stream
-    measured slower: 73.42-73.62 vs 72.46-72.53 ms/step, profiles/r3/g21_branch_stream_ab.txt.)
-    ``x`` may be a LazyBNAct (conv_bn_act's ``lazy_next``)."""
-    x = _lazy_input(x, conv)
-    if not isinstance(x, torch.Tensor) and not (DUAL_RESIDUAL and bn.training and bn_d.training):
-        x = x.materialize()
+    measured slower: 73.42-73.62 vs 72.46-72.53 ms/step, profiles/r3/g21_branch_stream_ab.txt.)"""
     if _BACKEND == "native" and _NATIVE_CONV and DUAL_RESIDUAL and x.is_cuda and bn.training and bn_d.training:
         from .bn_act import dual_supported, fused_bn_add_bn_act
 
@@ -185,11 +159,6 @@ def conv_bn_add_conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d
 
             ident = fused_bn_act(b[0], bn_d, False, None, b[1])
             return fused_bn_act(a[0], bn, relu, ident, a[1])
-        if a is not None:  # main conv done (a LazyBNAct input is consumed): the shortcut the ordinary way
-            from .bn_act import fused_bn_act, supported as bn_supported
-
-            ident = conv_bn_act(xd, conv_d, bn_d, relu=False, presubsampled=presubsampled)
-            return fused_bn_act(a[0], bn, relu, ident, a[1] if bn_supported(a[0], bn, ident) else None)
     ident = conv_bn_act(xd, conv_d, bn_d, relu=False, presubsampled=presubsampled)
     return conv_bn_act(x, conv, bn, relu=relu, residual=ident)
 

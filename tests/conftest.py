@@ -26,7 +26,7 @@ def cuda():
 
 
 _STATE = (("distributed_learning_amd.ops.nn", ("_BACKEND", "_NATIVE_CONV", "DUAL_RESIDUAL", "FORK_SUBSAMPLE")),
-          ("distributed_learning_amd.ops.conv", ("DUAL_1X1", "DUAL_BN", "DUAL_1X1_MAX_COUT", "LAZY_BN_ACT", "WGRAD_DEFER",
+          ("distributed_learning_amd.ops.conv", ("DUAL_1X1", "DUAL_BN", "DUAL_1X1_MAX_COUT", "WGRAD_DEFER",
                                                  "WGRAD_JOIN", "BN_EPILOGUE", "RESIDUAL_HANDOFF")))
 
 
