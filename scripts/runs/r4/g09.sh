@@ -1,4 +1,5 @@
 #!/bin/bash
+# Record of a past call: the switch it A/Bs was removed from the sources after measuring slower (profiles/r4/README.md).
 # Round 4, call g09: stage-2 one-pass 1x1 kernel (plain, no BN) with register-held weights + 3-stage ring vs
 # the LDS panel + 2 stages vs no stage-2 one-pass kernel; interleaved A/B x2
 set -o pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+# Record of a past call: the switch it A/Bs was removed from the sources after measuring slower (profiles/r4/README.md).
 # Round 4, call g11: fork form of the one-pass 1x1 kernel (DUAL_FORK) -- interleaved A/B x2 (default / DUAL_FORK
 # off / stage-2 plain kernel on the LDS weight panel) and a kernel trace of the default
 set -o pipefail

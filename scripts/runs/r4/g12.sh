@@ -1,4 +1,5 @@
 #!/bin/bash
+# Record of a past call: the switch it A/Bs was removed from the sources after measuring slower (profiles/r4/README.md).
 # Round 4, call g12: fork form with 64-row tiles -- dual tests, then interleaved A/B x2 (fork off = default / fork
 # on with 64-row tiles)
 set -o pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+# Record of a past call: the switch it A/Bs was removed from the sources after measuring slower (profiles/r4/README.md).
 # Round 4, call g17: relu(BN2) normalised on load by conv3 (LAZY_BN_ACT) -- kernel + model tests, then
 # interleaved A/B x2 (lazy on = new default / off)
 set -o pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+# Record of a past call: the switch it A/Bs was removed from the sources after measuring slower (profiles/r4/README.md).
 # Round 4, call g18: kernel traces with relu(BN2) normalised on load (LAZY_BN_ACT) and without
 set -o pipefail
 O=gpurun_out/g18

@@ -1,4 +1,5 @@
 #!/bin/bash
+# Record of a past call: the switch it A/Bs was removed from the sources after measuring slower (profiles/r4/README.md).
 # Round 4, call g19: relu(BN2) normalised on load, in the MFMA operand registers (no LDS pass) -- kernel + model tests, then
 # interleaved A/B x2 (default = lazy off / lazy on)
 set -o pipefail
