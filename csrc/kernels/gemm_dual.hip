@@ -54,7 +54,7 @@ struct DualCfg {
   static constexpr int TMW = CO / 64;                 // weight gradient: 16-row co fragments per wave
   static constexpr size_t Lds = (size_t)((kWReg ? 0 : KC * Panel) + NS * Stage) * sizeof(bf16_t);
   static_assert(Lds <= 160 * 1024, "dual 1x1 LDS budget");
-  static_assert(Slots >= 1 && (RF == 2 || RF == 4) && (NS == 2 || NS == 3), "tile configuration");
+  static_assert(Slots >= 1 && (RF == 2 || RF == 4) && NS >= 2 && NS <= 4, "tile configuration");
 };
 
 struct DualArgs {
@@ -356,6 +356,9 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout) {
 // plus 0.33 ms for the separate apply pass (profiles/r4/g08).
 bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout) { return Cout == 256 && conv1x1_dual_blocks(M, Cin, Cout) > 0; }
 
+static int g_dual512_stages = 3;  // A/B: ring depth of the Cout-512 kernel
+void set_dual512_stages(int n) { g_dual512_stages = n == 4 ? 4 : 3; }
+
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
                          int Cout, hipStream_t stream, const void* ybn, const uint8_t* mask, const float* ws) {
   const int mg = conv1x1_dual_groups(M, Cin, Cout);
@@ -373,6 +376,7 @@ bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx,
   }
   // Cout 512: weight fragments in registers + a 3-stage ring (the LDS-panel form fits only 2 stages: slower)
   if (Cout == 256) DLA_DUAL(256, 64, 3, false, false);
+  else if (g_dual512_stages == 4) DLA_DUAL(512, 32, 4, false, true);
   else DLA_DUAL(512, 32, 3, false, true);
 #undef DLA_DUAL
   return true;
