@@ -14,7 +14,7 @@
 //     block at the end, summed by splitk_reduce in fixed order (deterministic).
 // Wider Cin is split into 64-channel slices, one block each; the slice blocks of a row group sit on one XCD.
 // Served (launch_conv1x1_dual): (Cout, Cin) = (256, 64) with 64-row tiles; (512, 128 / 256) with 32-row tiles and
-// register-held weights; (256, 64) with the consuming BN's backward apply fused (kBN, the block-final BN).
+// register-held weights and a 4-stage ring; (256, 64) with the consuming BN's backward apply fused (kBN, the block-final BN).
 // A fork form for the block's first conv (BN apply with the ReLU recomputed + the identity gradient added in the
 // epilogue) measured slower (87.2-88.1 vs 84.2-84.5 ms per step, profiles/r4/g11-g12) and was removed.
 #include "dla_common.h"
@@ -356,9 +356,6 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout) {
 // plus 0.33 ms for the separate apply pass (profiles/r4/g08).
 bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout) { return Cout == 256 && conv1x1_dual_blocks(M, Cin, Cout) > 0; }
 
-static int g_dual512_stages = 3;  // A/B: ring depth of the Cout-512 kernel
-void set_dual512_stages(int n) { g_dual512_stages = n == 4 ? 4 : 3; }
-
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
                          int Cout, hipStream_t stream, const void* ybn, const uint8_t* mask, const float* ws) {
   const int mg = conv1x1_dual_groups(M, Cin, Cout);
@@ -374,10 +371,10 @@ bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx,
     DLA_DUAL(256, 32, 3, true, false);
     return true;
   }
-  // Cout 512: weight fragments in registers + a 3-stage ring (the LDS-panel form fits only 2 stages: slower)
+  // Cout 512: weight fragments in registers + a 4-stage ring (3 tiles in flight; 3 stages: +0.19 ms/step over
+  // 5 interleaved pairs, profiles/r4/g21; the LDS-panel form fits only 2 stages: slower)
   if (Cout == 256) DLA_DUAL(256, 64, 3, false, false);
-  else if (g_dual512_stages == 4) DLA_DUAL(512, 32, 4, false, true);
-  else DLA_DUAL(512, 32, 3, false, true);
+  else DLA_DUAL(512, 32, 4, false, true);
 #undef DLA_DUAL
   return true;
 }
