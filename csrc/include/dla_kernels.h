@@ -309,7 +309,6 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout);
 // ybn / mask / ws: dy is the incoming gradient of the BN(+residual)+ReLU that consumed the conv's output
 // (bit-mask ReLU, finalized workspace); its backward apply runs inside the kernel (Cout 256 only)
 bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout);
-void set_dualbn_form(int f);  // A/B: kBN kernel form
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
                          int Cout, hipStream_t stream, const void* ybn = nullptr, const uint8_t* mask = nullptr,
                          const float* ws = nullptr);

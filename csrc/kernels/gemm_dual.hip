@@ -356,9 +356,6 @@ int conv1x1_dual_groups(int64_t M, int Cin, int Cout) {
 // plus 0.33 ms for the separate apply pass (profiles/r4/g08).
 bool conv1x1_dual_bn_ok(int64_t M, int Cin, int Cout) { return Cout == 256 && conv1x1_dual_blocks(M, Cin, Cout) > 0; }
 
-static int g_dualbn_form = 0;  // A/B: 0 LDS weight panel + 3 stages, 1 register weights + 4 stages (kBN kernel)
-void set_dualbn_form(int f) { g_dualbn_form = f == 1 ? 1 : 0; }
-
 bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx, float* part, int64_t M, int Cin,
                          int Cout, hipStream_t stream, const void* ybn, const uint8_t* mask, const float* ws) {
   const int mg = conv1x1_dual_groups(M, Cin, Cout);
@@ -371,8 +368,7 @@ bool launch_conv1x1_dual(const void* dy, const void* x, const void* w, void* dx,
                      (DualCfg<CO_, R_, NS_, BN_, WR_>::Lds), stream, a)
   if (ybn) {
     if (!conv1x1_dual_bn_ok(M, Cin, Cout) || !mask || !ws) return false;
-    if (g_dualbn_form == 1) DLA_DUAL(256, 32, 4, true, true);
-    else DLA_DUAL(256, 32, 3, true, false);
+    DLA_DUAL(256, 32, 3, true, false);
     return true;
   }
   // Cout 512: weight fragments in registers + a 4-stage ring (3 tiles in flight; 3 stages: +0.19 ms/step over

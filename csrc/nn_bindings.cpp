@@ -1079,7 +1079,6 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("out_dtype") = at::kFloat,
         pybind11::arg("y_bn") = pybind11::none(), pybind11::arg("ws") = pybind11::none(),
         pybind11::arg("mask") = pybind11::none());
-  m.def("set_dualbn_form", &set_dualbn_form, "A/B: kBN one-pass kernel form (0 LDS panel + 3 stages, 1 registers + 4)");
   m.def("conv1x1_dual_bn_ok", [](int64_t M, int64_t Cin, int64_t Cout) { return conv1x1_dual_bn_ok(M, (int)Cin, (int)Cout); },
         "the one-pass 1x1 gradient kernel can also apply the consuming BN's backward for this shape");
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),
