@@ -44,7 +44,10 @@ def test_ipc_engine_two_processes(cuda):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "ipc_engine_check.py"), "--ranks", "2",
                         "--same_device", "1", "--timeout", "200"],
                        capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
-    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    if r.returncode != 0:  # pytest truncates long assertion messages: print the child's output in full first
+        print(r.stdout[-6000:])
+        print(r.stderr[-6000:], file=sys.stderr)
+    assert r.returncode == 0, r.returncode
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["ok"] and rec["world"] == 2 and rec["checked"] >= 100, rec
 
