@@ -190,8 +190,7 @@ def build_dp(model, reducer, cap_mb: float, dev, a, tune, world):
     if a.force_comm and world == 1:
         from distributed_learning_amd.parallel.executor import NativeStreamExecutor
 
-        dp.sync.executor = NativeStreamExecutor(reducer.engine, reducer.algorithm, passthrough=False)
-        dp.sync.passthrough = False
+        dp.sync.set_executor(NativeStreamExecutor(reducer.engine, reducer.algorithm, passthrough=False))
     if tune is not None:
         per_size = tune.run_buckets([b.flat.numel() for b in dp.sync.buckets])
         dp.sync.executor.per_bucket = {b.index: per_size[b.flat.numel()] for b in dp.sync.buckets}
@@ -200,15 +199,16 @@ def build_dp(model, reducer, cap_mb: float, dev, a, tune, world):
     return dp
 
 
-def time_steps(step, a, dev, engine, graphed, backend):
-    """W warmup steps, then exactly K timed steps between barrier + synchronize on both sides; the
-    elapsed time is the MAX over ranks."""
+def time_steps(step, a, dev, engine, graphed, backend, warmup=None):
+    """W warmup steps (``warmup``: those not already run, default all), then exactly K timed steps between
+    barrier + synchronize on both sides; the elapsed time is the MAX over ranks."""
+    warmup = a.warmup if warmup is None else warmup
     tele = {"before_warmup": telemetry.sample(dev.index or 0)}
     # one event per step boundary (warmup and timed): the per-step GPU-stream time distribution goes into
     # the record, so a slow first-steps ramp and a uniformly slow box can be told apart
-    wev = [torch.cuda.Event(enable_timing=True) for _ in range(a.warmup + 1)]
+    wev = [torch.cuda.Event(enable_timing=True) for _ in range(warmup + 1)]
     wev[0].record()
-    for i in range(a.warmup):
+    for i in range(warmup):
         step()
         wev[i + 1].record()
     torch.cuda.synchronize()
@@ -236,9 +236,30 @@ def time_steps(step, a, dev, engine, graphed, backend):
     step_ms = [tev[i].elapsed_time(tev[i + 1]) for i in range(a.steps)]
     srt = sorted(step_ms)
     return {"elapsed": float(t[0]), "comm_ms": float(t[1]), "loss": loss, "tele": tele,
-            "warm_ms": [round(wev[i].elapsed_time(wev[i + 1]), 2) for i in range(a.warmup)],
+            "warm_ms": [round(wev[i].elapsed_time(wev[i + 1]), 2) for i in range(warmup)],
             "step_ms": {"p50": round(srt[len(srt) // 2], 3), "min": round(srt[0], 3), "max": round(srt[-1], 3),
                         "seq": [round(x, 2) for x in step_ms] if a.steps <= 200 else None}}
+
+
+def measure_backward(data, opt, model, fwd_loss, dev, backend, n: int = 3) -> float:
+    """Seconds of one backward (compute stream, HIP events), the least of the last ``n - 1`` of
+    ``n`` eager steps (the first pays lazy setup), MAX over ranks. These are real steps."""
+    times = []
+    for _ in range(n):
+        x, y = data.next()
+        opt.zero_grad(set_to_none=True)
+        loss = fwd_loss(x, y)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        loss.backward()
+        e1.record()
+        model.sync_gradients()
+        opt.step()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1) * 1e-3)
+    t = torch.tensor([min(times[1:] or times)], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
 
 
 def phase_breakdown(parts, n: int, csv_path=None, name="bench"):
@@ -334,20 +355,31 @@ def main():
         engine.impl.set_force(True)  # the N>1 data path incl. fp32 staging, as a 1-rank collective
         engine.set_accum_fp32(True)
     grad_dtype = torch.bfloat16 if bf16 else torch.float32
+    graphed = a.graph == "on"
+    if graphed and comm_active and (engine.transport == "ipc" or a.algorithm.startswith("ipc_")):
+        # IPC barrier tokens are host-side launch arguments: a replayed graph would pass every barrier at
+        # once (engine.cpp allreduce_ipc refuses capture); the IPC transport runs eagerly
+        print("error: --graph on cannot capture the IPC transport; use --graph off", file=sys.stderr, flush=True)
+        sys.exit(2)
     if a.algorithm == "auto" and comm_active:
         from distributed_learning_amd.parallel import autotune as at
 
-        tune = at.Autotune(engine, grad_dtype, at.candidates(world, engine.transport))
+        def probe_engine():
+            e = engine.probe_clone(at.PROBE_TIMEOUT_S)
+            if a.force_comm and world == 1:
+                e.impl.set_force(True)
+                e.set_accum_fp32(True)
+            return e
+
+        tune = at.Autotune(engine, grad_dtype, at.candidates(world, engine.transport, include_ipc=not graphed),
+                           probe_factory=probe_engine)
         tune.run_grid()
         base_algo = tune.best_model()[0]
         reducer.algorithm = base_algo
+    # auto cap with a tuned model: provisional 8 MiB, then re-derived from the measured backward below
+    cap_from_backward = a.bucket_mb == "auto" and tune is not None
     if a.bucket_mb == "auto":
-        if tune is not None:
-            cpu_model = spec.build()
-            a.bucket_mb = tune.choose_cap(cpu_model, spec.input_shape, 0.028)
-            del cpu_model
-        else:
-            a.bucket_mb = 8.0
+        a.bucket_mb = 8.0
     a.bucket_mb = float(a.bucket_mb)
     sweep = [float(v) for v in a.bucket_mb_sweep.split(",")] if a.bucket_mb_sweep else None
     model = build_dp(base, reducer, sweep[0] if sweep else a.bucket_mb, dev, a, tune, world)
@@ -376,7 +408,21 @@ def main():
         opt.step()
         return loss
 
-    graphed = a.graph == "on"
+    warm_left = a.warmup
+    if cap_from_backward and not sweep and a.warmup > 0:
+        # the cap balances exposed collective time against the gradient-ready times of THIS step's
+        # backward: the first warmup steps measure it (eager, on the provisional buckets, MAX over ranks;
+        # they count as warmup steps), then the buckets are rebuilt. With no warmup the cap stays 8 MiB.
+        ncal = min(a.warmup, 3)
+        warm_left = a.warmup - ncal
+        bwd_s = measure_backward(data, opt, model, fwd_loss, dev, c.backend, n=ncal)
+        cpu_model = spec.build()
+        cap = float(tune.choose_cap(cpu_model, spec.input_shape, bwd_s))
+        del cpu_model
+        if abs(cap - a.bucket_mb) > 1e-9:
+            model.cleanup()
+            model = build_dp(base, reducer, cap, dev, a, tune, world)
+        a.bucket_mb = cap
     comm_ms_eager = None
     run_step = step
     if graphed:
@@ -416,7 +462,7 @@ def main():
     if gsync is not None:
         gsync.hook_s, gsync.hook_calls = 0.0, 0
     if not sweep:
-        res = time_steps(run_step, a, dev, engine, graphed, c.backend)
+        res = time_steps(run_step, a, dev, engine, graphed, c.backend, warmup=warm_left)
     elapsed = res["elapsed"]
     comm_ms = res["comm_ms"] if not graphed else comm_ms_eager
     final_loss = float(res["loss"].detach().float())
@@ -519,6 +565,8 @@ def main():
         torch.cuda.synchronize()
         torch.save(st, os.path.join(a.check_dir, f"rank{rank}.pt"))
     model.cleanup()
+    if tune is not None:
+        tune.close()
     ctxmod.shutdown()
 
 

@@ -183,7 +183,7 @@ class CommEngine {
     try {
       if (!aborted_ && comm_) {
         // bounded wait: a dead peer must not turn teardown into a hang
-        if (!wait_stream(std::min(comm_timeout_s(), 60.0), /*throw_on_fail=*/false)) abort_comms();
+        if (!wait_stream(std::min(timeout_s(), 60.0), /*throw_on_fail=*/false)) abort_comms();
       }
     } catch (...) {
       abort_comms();
@@ -239,7 +239,7 @@ class CommEngine {
   // communicators on error or after the deadline.
   void synchronize() {
     pybind11::gil_scoped_release nogil;
-    wait_stream(comm_timeout_s(), /*throw_on_fail=*/true);
+    wait_stream(timeout_s(), /*throw_on_fail=*/true);
   }
 
   // Current RCCL async error state of any communicator ("" = healthy).
@@ -254,6 +254,11 @@ class CommEngine {
   }
 
   void abort() { abort_comms(); }
+  // Deadline of this engine's waits and IPC barriers (<= 0: DLA_COMM_TIMEOUT_S, default 600 s). The
+  // autotuner's probe engine runs with a short one, so a candidate that hangs costs seconds and
+  // aborts only the probe communicator (parallel/autotune.py).
+  void set_timeout(double s) { timeout_s_ = s; }
+  double timeout_s() const { return timeout_s_ > 0 ? timeout_s_ : comm_timeout_s(); }
   bool aborted() const { return aborted_; }
 
   uintptr_t stream_handle() const { return reinterpret_cast<uintptr_t>(stream_->stream()); }
@@ -286,28 +291,47 @@ class CommEngine {
   int64_t ipc_capacity() const { return (int64_t)ipc_bytes_; }
   bool has_rccl() const { return comm_ != nullptr; }
 
-  pybind11::bytes ipc_alloc(int64_t bytes) {
+  // Window lifecycle. A grown window is allocated while the current one (and every earlier one not
+  // yet superseded by a verified mapping) stays allocated, so the new allocation can never reuse
+  // the address range a peer may still hold a mapping of; the owner stamps it with `nonce`. The
+  // retired windows are freed only once ipc_open has verified every peer's new mapping.
+  pybind11::bytes ipc_alloc(int64_t bytes, uint64_t nonce) {
     TORCH_CHECK(bytes > (int64_t)comm::kIpcHeaderBytes, "ipc_alloc: window too small");
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
-    ipc_release();
-    DLA_HIP_THROW(hipMalloc(&ipc_base_, (size_t)bytes));
-    DLA_HIP_THROW(hipMemset(ipc_base_, 0, (size_t)bytes));
-    DLA_HIP_THROW(hipDeviceSynchronize());
+    drain_stream_bounded();
+    void* p = nullptr;
+    DLA_HIP_THROW(hipMalloc(&p, (size_t)bytes));
+    if (ipc_base_) ipc_retired_.push_back(ipc_base_);
+    ipc_base_ = p;
     ipc_bytes_ = (size_t)bytes;
+    ipc_nonce_ = nonce;
+    DLA_HIP_THROW(hipMemset(ipc_base_, 0, (size_t)bytes));
+    DLA_HIP_THROW(hipMemcpy(static_cast<char*>(ipc_base_) + comm::kIpcNonceOffset, &nonce, sizeof(nonce),
+                            hipMemcpyHostToDevice));
+    DLA_HIP_THROW(hipDeviceSynchronize());
     hipIpcMemHandle_t h;
     DLA_HIP_THROW(hipIpcGetMemHandle(&h, ipc_base_));
     return pybind11::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
   }
 
-  void ipc_open(std::vector<pybind11::bytes> handles) {
-    TORCH_CHECK((int)handles.size() == topo_.world, "ipc_open: need one handle per rank");
+  // Map every peer's current window and read its nonce back through the mapping. Returns "" when
+  // every mapping shows its owner's nonce (the previous mappings are then closed and the retired
+  // windows freed); otherwise closes the new mappings, keeps the previous state and returns what
+  // was wrong -- the caller (NativeEngine._map_windows) then has every rank allocate again.
+  std::string ipc_open(std::vector<pybind11::bytes> handles, std::vector<uint64_t> nonces) {
+    TORCH_CHECK((int)handles.size() == topo_.world && (int)nonces.size() == topo_.world,
+                "ipc_open: need one handle and one nonce per rank");
     TORCH_CHECK(ipc_base_, "ipc_open: call ipc_alloc first");
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
-    ipc_close_peers();
-    ipc_peer_.assign(topo_.world, nullptr);
+    std::vector<char*> fresh(topo_.world, nullptr);
+    std::string bad;
+    auto close_fresh = [&] {
+      for (int r = 0; r < topo_.world; ++r)
+        if (r != topo_.rank && fresh[r]) hipIpcCloseMemHandle(fresh[r]);
+    };
     for (int r = 0; r < topo_.world; ++r) {
       if (r == topo_.rank) {
-        ipc_peer_[r] = static_cast<char*>(ipc_base_);
+        fresh[r] = static_cast<char*>(ipc_base_);
         continue;
       }
       std::string s = handles[r];
@@ -315,9 +339,32 @@ class CommEngine {
       hipIpcMemHandle_t h;
       std::memcpy(&h, s.data(), sizeof(h));
       void* p = nullptr;
-      DLA_HIP_THROW(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-      ipc_peer_[r] = static_cast<char*>(p);
+      const hipError_t oe = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+      if (oe != hipSuccess) {
+        close_fresh();
+        TORCH_CHECK(false, "ipc_open: hipIpcOpenMemHandle(rank ", r, "): ", hipGetErrorString(oe));
+      }
+      fresh[r] = static_cast<char*>(p);
+      uint64_t seen = 0;
+      DLA_HIP_THROW(hipMemcpy(&seen, fresh[r] + comm::kIpcNonceOffset, sizeof(seen), hipMemcpyDeviceToHost));
+      if (seen != nonces[r] && bad.empty()) {
+        char msg[160];
+        std::snprintf(msg, sizeof(msg), "rank %d's window maps to nonce %016llx, expected %016llx", r,
+                      (unsigned long long)seen, (unsigned long long)nonces[r]);
+        bad = msg;
+      }
     }
+    if (!bad.empty()) {
+      close_fresh();
+      ++ipc_stale_;
+      return bad;
+    }
+    ipc_close_peers();
+    ipc_peer_ = std::move(fresh);
+    for (void* w : ipc_retired_) hipFree(w);
+    ipc_retired_.clear();
+    ++ipc_generation_;
+    return "";
   }
 
   // 1 when a barrier timed out (a peer never arrived); valid after the comm stream drained
@@ -326,6 +373,20 @@ class CommEngine {
     int v = 0;
     DLA_HIP_THROW(hipMemcpy(&v, static_cast<char*>(ipc_base_) + comm::kIpcErrOffset, sizeof(int), hipMemcpyDeviceToHost));
     return v;
+  }
+
+  // What the first timed-out barrier waited for: (error, awaited token, peer flag seen, peer rank,
+  // host token counter, window generation, stale mappings refused so far).
+  std::vector<int64_t> ipc_error_info() {
+    std::vector<int64_t> out{0, 0, 0, -1, (int64_t)ipc_tok_, (int64_t)ipc_generation_, (int64_t)ipc_stale_};
+    if (!ipc_base_) return out;
+    uint64_t d[3] = {0, 0, 0};
+    out[0] = ipc_error();
+    DLA_HIP_THROW(hipMemcpy(d, static_cast<char*>(ipc_base_) + comm::kIpcDiagOffset, sizeof(d), hipMemcpyDeviceToHost));
+    out[1] = (int64_t)d[0];
+    out[2] = (int64_t)d[1];
+    out[3] = out[0] ? (int64_t)d[2] : -1;
+    return out;
   }
 
   // ---------------------------------------------------------------------------------------
@@ -366,6 +427,26 @@ class CommEngine {
     timed([&] { allreduce_on_stream(flat, algo, average, &grads, &offsets); });
   }
 
+  // Fusion-off launch group (reference main_overlap / main_onestep_overlap: one all-reduce per gradient
+  // tensor, /root/reference/src/main.py:168-179,222-230): the member buckets are slices of one `group`
+  // buffer at `starts` / `counts`. Every member keeps its own collective, but the group costs one event
+  // join, one gather launch of all members' gradients, one fp32 staging cast and -- on the RCCL built-in
+  // -- one ncclGroupStart/End around the members' ncclAllReduce calls (a single fused RCCL launch), then
+  // one cast back. Other schedules / the IPC transport run the members' plans one after another after
+  // the shared gather.
+  void bucket_allreduce_group(at::Tensor group, std::vector<int64_t> starts, std::vector<int64_t> counts, int algo,
+                              bool average, std::vector<at::Tensor> grads, std::vector<int64_t> offsets) {
+    check(group);
+    TORCH_CHECK(starts.size() == counts.size() && !starts.empty(), "bucket_allreduce_group: bad member spans");
+    for (size_t i = 0; i < starts.size(); ++i)
+      TORCH_CHECK(starts[i] >= 0 && counts[i] >= 0 && starts[i] + counts[i] <= group.numel(),
+                  "bucket_allreduce_group: member ", i, " outside the group buffer");
+    c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
+    join_current();
+    pybind11::gil_scoped_release nogil;
+    timed([&] { allreduce_group_on_stream(group, starts, counts, algo, average, grads, offsets); });
+  }
+
   void broadcast(at::Tensor t, int root) {
     check(t);
     TORCH_CHECK(comm_, "CommEngine.broadcast needs the RCCL communicator (IPC-only engine)");
@@ -397,7 +478,7 @@ class CommEngine {
   double consume_comm_ms() {
     pybind11::gil_scoped_release nogil;
     double total = 0.0;
-    wait_stream(comm_timeout_s(), /*throw_on_fail=*/true);
+    wait_stream(timeout_s(), /*throw_on_fail=*/true);
     for (size_t i = 0; i + 1 < used_timing_; i += 2) {
       float ms = 0.f;
       DLA_HIP_THROW(hipEventElapsedTime(&ms, timing_events_[i], timing_events_[i + 1]));
@@ -428,9 +509,13 @@ class CommEngine {
           // the IPC windows are out of step from here on (a barrier gave up), the RCCL communicator is not:
           // refuse further IPC collectives instead of aborting RCCL
           ipc_broken_ = true;
+          const std::vector<int64_t> d = ipc_error_info();
           if (throw_on_fail)
             throw std::runtime_error("CommEngine: an IPC peer did not reach a barrier within the timeout "
-                                     "(DLA_COMM_TIMEOUT_S; peer failure?); IPC transport disabled");
+                                     "(DLA_COMM_TIMEOUT_S; peer failure?): waited for token " + std::to_string(d[1]) +
+                                     " from rank " + std::to_string(d[3]) + ", whose flag held " + std::to_string(d[2]) +
+                                     " (host counter " + std::to_string(d[4]) + ", window generation " +
+                                     std::to_string(d[5]) + "); IPC transport disabled");
           return false;
         }
         return true;
@@ -464,14 +549,21 @@ class CommEngine {
     ipc_peer_.clear();
   }
 
-  // bounded drain of the comm stream, then unmap the peers and free the window
-  void ipc_release() {
-    if (!ipc_base_ && ipc_peer_.empty()) return;
+  void drain_stream_bounded() {
     const auto t0 = std::chrono::steady_clock::now();
+    const double limit = std::min(60.0, timeout_s());
     while (hipStreamQuery(stream_->stream()) == hipErrorNotReady &&
-           std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < 60.0)
+           std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < limit)
       std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+
+  // bounded drain of the comm stream, then unmap the peers and free the windows
+  void ipc_release() {
+    if (!ipc_base_ && ipc_peer_.empty() && ipc_retired_.empty()) return;
+    drain_stream_bounded();
     ipc_close_peers();
+    for (void* w : ipc_retired_) hipFree(w);
+    ipc_retired_.clear();
     if (ipc_base_) hipFree(ipc_base_);
     ipc_base_ = nullptr;
     ipc_bytes_ = 0;
@@ -645,6 +737,49 @@ class CommEngine {
     if (stg) launch_cast(flat.data_ptr(), kBF16, lay.data, kF32, n, 1.f, st);
   }
 
+  void allreduce_group_on_stream(const at::Tensor& group, const std::vector<int64_t>& starts,
+                                 const std::vector<int64_t>& counts, int algo, bool average,
+                                 const std::vector<at::Tensor>& grads, const std::vector<int64_t>& offsets) {
+    hipStream_t st = stream_->stream();
+    const int64_t n = group.numel();
+    const int dt = group.scalar_type() == at::kBFloat16 ? kBF16 : kF32;
+    if ((topo_.world == 1 && !force_) || n == 0) {
+      pack_tensors_on(grads, offsets, group, 1.f, st);
+      return;
+    }
+    const bool builtin_rccl = !uses_ipc(algo) && decode_algo(algo).algo == comm::kBuiltin;
+    if (!builtin_rccl) {
+      pack_tensors_on(grads, offsets, group, 1.f, st);
+      for (size_t i = 0; i < starts.size(); ++i)
+        if (counts[i] > 0) allreduce_on_stream(group.narrow(0, starts[i], counts[i]), algo, average, nullptr, nullptr);
+      return;
+    }
+    if (needs_reduce_kernel(algo))
+      TORCH_CHECK(group.scalar_type() == at::kFloat || group.scalar_type() == at::kBFloat16,
+                  "custom all-reduce algorithms support fp32/bf16 only");
+    const bool stg = staged(algo, dt) && group.scalar_type() == at::kBFloat16;
+    ensure_scratch(comm::staged_scratch_bytes(0, n, stg, dt));
+    char* data = stg ? static_cast<char*>(scratch_.data_ptr()) : static_cast<char*>(group.data_ptr());
+    const size_t esz = stg ? 4 : (size_t)group.element_size();
+    if (stg) {
+      // the slot padding between members is never gathered into: zero it so the cast back writes zeros
+      DLA_HIP_THROW(hipMemsetAsync(data, 0, (size_t)n * 4, st));
+      at::Tensor dst = at::from_blob(data, {n}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device_));
+      pack_tensors_on(grads, offsets, dst, 1.f, st);
+    } else {
+      pack_tensors_on(grads, offsets, group, 1.f, st);
+    }
+    const ncclDataType_t ndt = stg ? ncclFloat32 : nccl_dtype_of(group.scalar_type());
+    DLA_NCCL_CHECK(ncclGroupStart());
+    for (size_t i = 0; i < starts.size(); ++i) {
+      if (counts[i] == 0) continue;
+      void* p = data + (size_t)starts[i] * esz;
+      DLA_NCCL_CHECK(ncclAllReduce(p, p, counts[i], ndt, average ? ncclAvg : ncclSum, comm_, st));
+    }
+    DLA_NCCL_CHECK(ncclGroupEnd());
+    if (stg) launch_cast(group.data_ptr(), kBF16, data, kF32, n, 1.f, st);
+  }
+
   // The same Plan over peer-mapped windows (ipc.h): the bucket is staged into this rank's window
   // (fp32 for accum_fp32 bf16 buckets, else its own dtype), the plan runs there with pulls from the
   // peers' windows and flag barriers, and the result is cast / copied back into `flat`.
@@ -659,6 +794,13 @@ class CommEngine {
     const IpcEntry& e = ipc_entry(code, n);
     const size_t need = comm::kIpcHeaderBytes + (size_t)e.sched.total * esz;
     TORCH_CHECK(!ipc_broken_, "CommEngine: the IPC transport was disabled after a barrier timeout");
+    // The barrier tokens are host-side values baked into each barrier launch: a captured graph would
+    // replay stale tokens that every peer flag already satisfies, so the barriers would pass at once.
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    DLA_HIP_THROW(hipStreamIsCapturing(st, &cs));
+    TORCH_CHECK(cs == hipStreamCaptureStatusNone,
+                "CommEngine: IPC all-reduces cannot be captured into a HIP graph (host-side barrier tokens); "
+                "run the IPC transport eagerly (bench.py --graph off)");
     TORCH_CHECK(ipc_base_ && !ipc_peer_.empty() && need <= ipc_bytes_,
                 "CommEngine: the IPC window (", ipc_bytes_, " B) does not hold this all-reduce (", need,
                 " B); call reserve() with the bucket sizes first (NativeEngine.reserve maps the windows)");
@@ -699,10 +841,14 @@ class CommEngine {
       b.set = set;
       TORCH_CHECK((int)wait_ranks.size() <= kMaxIpcPeers, "IPC barrier: too many peers");
       b.npeers = (int)wait_ranks.size();
-      for (int i = 0; i < b.npeers; ++i) b.peer[i] = reinterpret_cast<const uint64_t*>(e.ipc_peer_[wait_ranks[i]]);
+      for (int i = 0; i < b.npeers; ++i) {
+        b.peer[i] = reinterpret_cast<const uint64_t*>(e.ipc_peer_[wait_ranks[i]]);
+        b.peer_rank[i] = wait_ranks[i];
+      }
       b.wait = wait;
       b.err = reinterpret_cast<int*>(e.ipc_peer_[e.topo_.rank] + comm::kIpcErrOffset);
-      b.timeout_ticks = (uint64_t)(comm_timeout_s() * (double)e.wall_khz_ * 1000.0);
+      b.diag = reinterpret_cast<uint64_t*>(e.ipc_peer_[e.topo_.rank] + comm::kIpcDiagOffset);
+      b.timeout_ticks = (uint64_t)(e.timeout_s() * (double)e.wall_khz_ * 1000.0);
       launch_ipc_barrier(b, iss.stream());
     }
     void copy(void* dst, const void* src, int64_t n) { iss.copy(dst, src, n); }
@@ -812,8 +958,13 @@ class CommEngine {
   void* ipc_base_ = nullptr;       // this rank's window (hipMalloc, exported)
   size_t ipc_bytes_ = 0, ipc_need_ = 0;
   std::vector<char*> ipc_peer_;    // every rank's window base as mapped here (mine = ipc_base_)
+  std::vector<void*> ipc_retired_;  // superseded windows, freed once the next mapping set is verified
+  uint64_t ipc_nonce_ = 0;         // identity stamp of the current window
+  int64_t ipc_generation_ = 0;     // verified mapping sets so far
+  int64_t ipc_stale_ = 0;          // mappings refused because they showed the wrong nonce
   uint64_t ipc_tok_ = 0;           // barrier token counter, identical sequence on every rank
   bool ipc_broken_ = false;        // a barrier timed out: tokens are out of step, no more IPC collectives
+  double timeout_s_ = 0.0;          // set_timeout
   int wall_khz_ = 100000;          // constant-clock rate for the barrier timeout
   at::Tensor scratch_;
   std::vector<hipEvent_t> ready_pool_;
@@ -1115,6 +1266,9 @@ void bind_comm(pybind11::module& m) {
            pybind11::arg("unpack_scale") = 1.0)
       .def("bucket_allreduce_list", &CommEngine::bucket_allreduce_list, pybind11::arg("flat"), pybind11::arg("algo"),
            pybind11::arg("average"), pybind11::arg("grads"), pybind11::arg("offsets"))
+      .def("bucket_allreduce_group", &CommEngine::bucket_allreduce_group, pybind11::arg("group"),
+           pybind11::arg("starts"), pybind11::arg("counts"), pybind11::arg("algo"), pybind11::arg("average"),
+           pybind11::arg("grads"), pybind11::arg("offsets"))
       .def("broadcast", &CommEngine::broadcast)
       .def("allgather", &CommEngine::allgather)
       .def("set_timing", &CommEngine::set_timing)
@@ -1124,7 +1278,10 @@ void bind_comm(pybind11::module& m) {
       .def("ipc_capacity", &CommEngine::ipc_capacity)
       .def("ipc_alloc", &CommEngine::ipc_alloc)
       .def("ipc_open", &CommEngine::ipc_open)
-      .def("ipc_error", &CommEngine::ipc_error);
+      .def("ipc_error", &CommEngine::ipc_error)
+      .def("ipc_error_info", &CommEngine::ipc_error_info)
+      .def("set_timeout", &CommEngine::set_timeout)
+      .def("timeout_s", &CommEngine::timeout_s);
   m.def("ipc_host_allreduce", &ipc_host_allreduce,
         "all-reduce CPU buffers with the IPC transport's pull/barrier protocol, one thread per rank",
         pybind11::arg("bufs"), pybind11::arg("algo"), pybind11::arg("average") = true, pybind11::arg("rings") = VV{},

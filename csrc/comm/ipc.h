@@ -48,8 +48,13 @@
 namespace dla {
 namespace comm {
 
-constexpr size_t kIpcHeaderBytes = 4096;  // flag u64 at 0, error word at 64
+// Window header: flag u64 at 0; barrier-timeout error word (int) at 64 and its record (awaited token,
+// last value seen, peer rank: u64 x3) at 72; the window's identity nonce (u64, written by the owner
+// when it allocates) at 128, which every importer reads back through its mapping before first use.
+constexpr size_t kIpcHeaderBytes = 4096;
 constexpr size_t kIpcErrOffset = 64;
+constexpr size_t kIpcDiagOffset = 72;
+constexpr size_t kIpcNonceOffset = 128;
 
 inline int64_t ipc_round64(int64_t v) { return (v + 63) / 64 * 64; }
 

@@ -96,15 +96,19 @@ void launch_cast(void* dst, int dst_dtype, const void* src, int src_dtype, int64
 // wrote before is visible to peers that observe it), then wait until every listed peer flag is
 // >= `wait` (system-scope acquire). A peer that never arrives ends the wait after `timeout_ticks`
 // of the constant 100 MHz clock with err[0] = 1 instead of spinning forever, so the grid always
-// drains; the host reads err after the stream completes.
+// drains; the host reads err after the stream completes. The first timeout also records what it
+// waited for in diag[0..2]: the awaited token, the value the peer's flag last held, and that peer's
+// global rank (engine.cpp ipc_error_info), so a failure names a stuck peer or a stale mapping.
 constexpr int kMaxIpcPeers = 16;
 struct IpcBarrier {
   uint64_t* mine;  // null: do not publish
   uint64_t set;
   const uint64_t* peer[kMaxIpcPeers];
+  int peer_rank[kMaxIpcPeers];
   int npeers;
   uint64_t wait;
   int* err;
+  uint64_t* diag;  // may be null
   uint64_t timeout_ticks;
 };
 void launch_ipc_barrier(const IpcBarrier& b, hipStream_t stream);

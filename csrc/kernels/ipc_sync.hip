@@ -15,9 +15,16 @@ __global__ __launch_bounds__(64) void ipc_barrier_kernel(IpcBarrier b) {
   if (b.mine) __hip_atomic_store(b.mine, b.set, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   const uint64_t t0 = wall_clock64();
   for (int i = 0; i < b.npeers; ++i) {
-    while (__hip_atomic_load(b.peer[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < b.wait) {
+    uint64_t seen;
+    while ((seen = __hip_atomic_load(b.peer[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) < b.wait) {
       if (wall_clock64() - t0 > b.timeout_ticks) {
-        __hip_atomic_store(b.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // keep the first failure's record: later barriers of a broken run time out too
+        if (b.diag && __hip_atomic_load(b.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+          __hip_atomic_store(b.diag, b.wait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(b.diag + 1, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(b.diag + 2, (uint64_t)b.peer_rank[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __hip_atomic_store(b.err, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
       }
       __builtin_amdgcn_s_sleep(8);

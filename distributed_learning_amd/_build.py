@@ -62,6 +62,27 @@ def _headers_digest() -> str:
     return h.hexdigest()
 
 
+def source_digest(root: Path | None = None) -> str:
+    """sha256 over every file the extension is built from (kernels, bindings, comm, headers), in a fixed
+    order. Embedded in _C.so at link time; ops/_ext.py compares it with the tree it runs from."""
+    csrc = (Path(root) if root is not None else ROOT) / "csrc"
+    files = sorted((csrc / "kernels").glob("*.hip")) + sorted(csrc.glob("*.cpp")) + sorted((csrc / "comm").glob("*.cpp"))
+    files += sorted((csrc / "include").glob("*.h")) + sorted((csrc / "comm").glob("*.h"))
+    h = hashlib.sha256()
+    for p in files:
+        h.update(str(p.relative_to(csrc)).encode())
+        h.update(b"\0")
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+def _hash_object(bflags, digest: str, force: bool, verbose: bool) -> Path:
+    src = OBJ_DIR / f"source_hash-{digest[:16]}.cpp"
+    if not src.exists():
+        src.write_text(f'extern "C" const char* dla_source_hash() {{ return "{digest}"; }}\n')
+    return _compile_one(src, [f for f in bflags if f.startswith(("-O", "-f", "--offload"))], "", force, verbose)
+
+
 def _flags(kind: str, tdir: Path, incs, abi: int, defines=()):
     common = [f"-D{d}" for d in defines] + [
         f"--offload-arch={ARCH}",
@@ -122,6 +143,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False, d
         futs = [ex.submit(_compile_one, s, kflags, hd, force, verbose) for s in kern]
         futs += [ex.submit(_compile_one, s, bflags, hd, force, verbose) for s in binds]
         objs = [f.result() for f in futs]
+    objs.append(_hash_object(bflags, source_digest(), force, verbose))
     tlib = tdir / "lib"
     link_key = hashlib.sha256(("".join(sorted(o.name for o in objs)) + str(out)).encode()).hexdigest()[:16]
     stamp = OBJ_DIR / f"link-{out.stem}-{link_key}.stamp"

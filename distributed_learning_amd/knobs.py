@@ -65,6 +65,7 @@ TABLE: Dict[str, Knob] = {
     # ---- build / load ------------------------------------------------------------------------------
     "AUTOBUILD": Knob("0", "ops/_ext.py", "1: build the extension on first import"),
     "EXT_SO": Knob("", "ops/_ext.py", "path of a variant _C.so (A/B builds, _build.py --out)"),
+    "ALLOW_STALE": Knob("0", "ops/_ext.py", "1: load a _C.so whose embedded source digest differs from csrc/"),
 }
 
 _CACHE: Dict[str, str] = {}

@@ -86,7 +86,7 @@ class _BNAct(torch.autograd.Function):
         # the producing 1x1 conv (the block's conv3) applies this BN's backward itself (ops/conv.py DualBNLink):
         # a bit-mask ReLU after the residual add, the residual gradient handed to the fork; bf16
         ok = (dlink is not None and x.dtype == torch.bfloat16 and ctx.mask_mode == MASK_BITS
-              and ctx.rlink is not None and m is not None)
+              and ctx.rlink is not None and m is not None and dlink.claim())
         ctx.dlink = dlink if ok else None
         return y
 
@@ -98,7 +98,7 @@ class _BNAct(torch.autograd.Function):
         C = _ext.require()
         ext = ctx.link.take(dy) if ctx.link is not None else None
         rl = ctx.rlink
-        if ctx.dlink is not None:
+        if ctx.dlink is not None and ctx.dlink.can_park(x):
             # reduction + finalize only; the conv backward applies (dy, x, mask, ws) in its own kernel
             dy = dy.contiguous(memory_format=torch.channels_last)
             _, _, dg, db = C.bn_act_bwd(dy, None, mask, x, ws, weight, ctx.mask_mode, False, ext, False)
@@ -134,14 +134,16 @@ class _BNDualAct(torch.autograd.Function):
         ctx.save_for_backward(x, ws, weight, xd, wsd, weight_d, mask if relu else None)
         # both inputs come from 1x1 convs that can apply their BN's backward themselves (ops/conv.py DualBNLink)
         ctx.dlinks = (dlink, dlink_d) if (dlink is not None and dlink_d is not None and relu and mask is not None
-                                           and mask.numel() and x.dtype == torch.bfloat16) else None
+                                           and mask.numel() and x.dtype == torch.bfloat16
+                                           and not dlink.claimed and not dlink_d.claimed
+                                           and dlink.claim() and dlink_d.claim()) else None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, ws, weight, xd, wsd, weight_d, mask = ctx.saved_tensors
         need = ctx.needs_input_grad
-        if ctx.dlinks is not None:
+        if ctx.dlinks is not None and ctx.dlinks[0].can_park(x) and ctx.dlinks[1].can_park(xd):
             dy = dy.contiguous(memory_format=torch.channels_last)
             _, dg, db, _, dgd, dbd = _ext.require().bn_dual_bwd(dy, mask, x, ws, weight, xd, wsd, weight_d, False)
             dx = ctx.dlinks[0].park(dy, x, ws, mask, weight, MASK_BITS)

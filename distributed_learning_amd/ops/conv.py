@@ -241,14 +241,35 @@ class DualBNLink:
     The BN backward returns a zero-stride placeholder as its input gradient and parks its incoming gradient,
     input, mask and finalized coefficients here; the conv backward recognises the placeholder and runs the
     one-pass kernel with the BN apply fused. If autograd summed the placeholder with other gradients of the
-    conv output (more consumers), the conv backward materialises the BN's gradient and adds it."""
+    conv output (more consumers), the conv backward materialises the BN's gradient and adds it.
 
-    __slots__ = ("ph", "dout", "ybn", "ws", "mask", "weight", "mode")
+    Guards: one link serves ONE BN -- the first BN to claim() it in its forward; a second BN on
+    the same conv output runs the normal path, so no parked gradient can be overwritten. And park()
+    is refused (can_park False: the BN computes its input gradient itself) when anything else observes the
+    conv output's gradient -- a tensor hook or retain_grad() on it -- since that observer would see the
+    placeholder's zeros."""
+
+    __slots__ = ("ph", "dout", "ybn", "ws", "mask", "weight", "mode", "claimed")
 
     def __init__(self):
         self.ph = self.dout = self.ybn = self.ws = self.mask = self.weight = self.mode = None
+        self.claimed = False
+
+    def claim(self) -> bool:
+        if self.claimed:
+            return False
+        self.claimed = True
+        return True
+
+    @staticmethod
+    def observed(y) -> bool:
+        return bool(y.retains_grad or getattr(y, "_backward_hooks", None))
+
+    def can_park(self, y) -> bool:
+        return self.ph is None and not self.observed(y)
 
     def park(self, dout, ybn, ws, mask, weight, mode=2):
+        assert self.can_park(ybn), "DualBNLink.park: check can_park first"
         self.dout, self.ybn, self.ws, self.mask, self.weight, self.mode = dout, ybn, ws, mask, weight, mode
         self.ph = torch.zeros((), dtype=ybn.dtype, device=ybn.device).expand(ybn.shape)
         return self.ph

@@ -17,18 +17,23 @@ first multi-GPU run measures them itself:
    own gradient-ready times);
 4. each actual bucket size is measured again for every verified algorithm and gets its fastest one.
 
+Isolation: ``builtin`` is measured first on the training engine; every other candidate runs on a
+probe engine with its own communicator and a 30 s deadline (ProbePool). A candidate that hangs,
+raises an RCCL async error or returns wrong numbers is excluded on every rank with its reason
+(``report()["excluded"]``), the probe communicator is aborted and replaced, and training continues
+on what passed -- the first 8-GPU run cannot be lost to one bad schedule.
+
 All ranks compute the same decision from the gathered table; rank 0's is broadcast anyway so a
 floating-point tie can never split the ranks (RCCL requires identical collective sequences).
 """
 from __future__ import annotations
 
 import math
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
 
-from .. import knobs
 from . import cost_model as cm
 
 MiB = 1024 * 1024
@@ -97,52 +102,111 @@ def _gather_max(table: Dict[str, Dict[int, float]], ok: Dict[str, bool], group) 
     return out, okk
 
 
+class ProbePool:
+    """The engine every non-builtin candidate is probed on: a clone of the training engine with its
+    own communicator and a short deadline (NativeEngine.probe_clone). A candidate that fails on
+    any rank gets the probe discarded (its communicator aborted) on every rank together, and the
+    next candidate gets a fresh one -- the training communicator never runs an unverified schedule
+    and is never aborted by probing. ``factory`` is collective; ``None`` probes on the engine itself
+    (stand-in engines of the CPU tests that have no communicator to lose)."""
+
+    def __init__(self, factory: Optional[Callable[[], object]] = None):
+        self.factory = factory
+        self.engine = None
+        self.created = 0
+        self.discarded = 0
+
+    def get(self, fallback):
+        if self.factory is None:
+            return fallback
+        if self.engine is None:
+            self.engine = self.factory()
+            self.created += 1
+        return self.engine
+
+    def discard(self) -> None:
+        if self.engine is not None:
+            try:
+                self.engine.discard()
+            except Exception:  # noqa: BLE001 -- an engine already broken is dropped all the same
+                pass
+            self.engine = None
+            self.discarded += 1
+
+    def close(self) -> None:
+        if self.engine is not None:
+            try:
+                self.engine.close()
+            except Exception:  # noqa: BLE001
+                try:
+                    self.engine.discard()
+                except Exception:  # noqa: BLE001
+                    pass
+            self.engine = None
+
+
+PROBE_TIMEOUT_S = 30.0
+
+
+def _agree(flag: bool, why: str, group) -> Tuple[bool, str]:
+    """Collective AND of ``flag`` with every failing rank's reason."""
+    objs: List[object] = [None] * dist.get_world_size(group)
+    dist.all_gather_object(objs, (bool(flag), why), group=group)
+    bad = [f"rank {r}: {w[:240]}" for r, (f, w) in enumerate(objs) if not f]
+    return (not bad), "; ".join(bad)[:1000]
+
+
 def measure(engine, algos: Sequence[str], sizes: Sequence[int], dtype: torch.dtype, reps: int = 5,
-            warmup: int = 2, verify: bool = True, group=None) -> Tuple[Dict[str, Dict[int, float]], Dict[str, bool]]:
+            warmup: int = 2, verify: bool = True, group=None, probe: Optional[ProbePool] = None,
+            reasons: Optional[Dict[str, str]] = None) -> Tuple[Dict[str, Dict[int, float]], Dict[str, bool]]:
     """Collective: algo -> {elements: ms (max over ranks)}, algo -> verified on every rank.
 
-    Algorithms whose setup fails (e.g. peer memory that cannot be mapped) are reported as not ok;
-    setup failures are agreed on across ranks before anything is timed, so no rank is left waiting
-    in a collective the others skipped."""
-    import os
-
+    ``builtin`` (RCCL's own all-reduce, what training falls back to) runs on ``engine``; every other
+    candidate runs on ``probe``'s engine (see ProbePool). Setup failures are agreed on across ranks
+    before anything is timed, and after every size all ranks agree whether the candidate is still
+    good, so a failure on one rank stops the candidate on every rank at the same point instead of
+    leaving the others waiting in barriers it will never reach. ``reasons`` collects why each
+    excluded candidate was excluded."""
     group = group if group is not None else engine.group
+    probe = probe if probe is not None else ProbePool(None)
+    reasons = reasons if reasons is not None else {}
     table: Dict[str, Dict[int, float]] = {}
     ok: Dict[str, bool] = {}
     for a in algos:
+        on_probe = a != "builtin" and probe.factory is not None
+        why = ""
         try:
-            engine.reserve(a, list(sizes), dtype)
+            eng = probe.get(engine) if on_probe else engine
+            eng.reserve(a, list(sizes), dtype)
             good = True
-        except Exception:  # noqa: BLE001 - a transport this node cannot run is excluded, not fatal
-            good = False
-        flags: List[object] = [None] * dist.get_world_size(group)
-        dist.all_gather_object(flags, good, group=group)
-        if not all(flags):
-            ok[a] = False
+        except Exception as e:  # noqa: BLE001 - a transport this node cannot run is excluded, not fatal
+            good, why = False, f"setup: {type(e).__name__}: {e}"
+        good, why = _agree(good, why, group)
+        if not good:
+            ok[a], reasons[a] = False, why
+            if on_probe:
+                probe.discard()
             continue
         row = {}
-        good = True
-        # an IPC barrier that never completes gives up after DLA_COMM_TIMEOUT_S: short while probing, so a
-        # transport that cannot synchronise on this node costs seconds and is excluded (the engine then
-        # refuses IPC; RCCL is untouched)
-        key = knobs.env_name("COMM_TIMEOUT_S")  # read by the engine at every barrier launch
-        old_to = os.environ.get(key)
-        if engine.uses_ipc(a) if hasattr(engine, "uses_ipc") else False:
-            os.environ[key] = "30"
-        try:
-            for n in sizes:
-                ms, v = _time_algo(engine, a, int(n), dtype, reps, warmup, verify)
-                row[int(n)] = ms
-                good = good and v
-        except Exception:  # noqa: BLE001
-            good = False
-        finally:
-            if old_to is None:
-                os.environ.pop(key, None)
-            else:
-                os.environ[key] = old_to
+        for n in sizes:
+            v, why = True, ""
+            try:
+                ms, v = _time_algo(eng, a, int(n), dtype, reps, warmup, verify)
+                if not v:
+                    why = f"wrong result at {int(n)} elements"
+            except Exception as e:  # noqa: BLE001 -- deadline / async error / transport refusal
+                v, why, ms = False, f"{type(e).__name__}: {e}", math.inf
+            v, why = _agree(v, why, group)
+            if not v:
+                good = False
+                break
+            row[int(n)] = ms
         if good:
             table[a] = row
+        else:
+            reasons[a] = why
+            if on_probe:
+                probe.discard()
         ok[a] = good
     return _gather_max(table, ok, group)
 
@@ -195,13 +259,18 @@ class Autotune:
     """The whole selection for one model (see the module docstring). ``report()`` is what the
     bench record carries."""
 
-    def __init__(self, engine, dtype: torch.dtype, algos: Sequence[str], reps: int = 5, warmup: int = 2):
+    def __init__(self, engine, dtype: torch.dtype, algos: Sequence[str], reps: int = 5, warmup: int = 2,
+                 probe_factory: Optional[Callable[[], object]] = None):
         self.engine = engine
         self.dtype = dtype
         self.esz = torch.tensor([], dtype=dtype).element_size()
         # what crosses the links: fp32 staging of bf16 buckets at N > 1 (engine accum_fp32)
         self.wire_esz = 4 if (dtype == torch.bfloat16 and engine.impl.accum_fp32()) else self.esz
-        self.algos = list(algos)
+        # builtin first: RCCL's own all-reduce is measured on the training engine before any custom
+        # schedule is probed (on the probe engine), so the fallback is known good whatever follows
+        self.algos = sorted(algos, key=lambda a: a != "builtin")
+        self.probe = ProbePool(probe_factory)
+        self.excluded: Dict[str, str] = {}
         self.reps, self.warmup = reps, warmup
         self.grid_table: Dict[str, Dict[int, float]] = {}
         self.ok: Dict[str, bool] = {}
@@ -210,10 +279,12 @@ class Autotune:
         self.per_size: Dict[int, str] = {}
         self.cap_mib: Optional[float] = None
         self.cap_rows: List[Dict[str, float]] = []
+        self.backward_s: Optional[float] = None
 
     def run_grid(self) -> None:
         sizes = [int(m * MiB) // self.esz for m in GRID_MIB]
-        self.grid_table, self.ok = measure(self.engine, self.algos, sizes, self.dtype, self.reps, self.warmup)
+        self.grid_table, self.ok = measure(self.engine, self.algos, sizes, self.dtype, self.reps, self.warmup,
+                                           probe=self.probe, reasons=self.excluded)
         self.models = {a: fit(row, self.wire_esz) for a, row in self.grid_table.items() if self.ok.get(a)}
 
     def best_model(self) -> Tuple[str, cm.CollectiveModel]:
@@ -225,7 +296,10 @@ class Autotune:
         return a, self.models[a]
 
     def choose_cap(self, cpu_model, input_shape, backward_s: float) -> float:
-        """Bucket cap (MiB of bucket dtype) from the fitted model of the best algorithm."""
+        """Bucket cap (MiB of bucket dtype) from the fitted model of the best algorithm, against a
+        backward of ``backward_s`` seconds (bench.py passes the warmup steps' measured backward,
+        MAX over ranks)."""
+        self.backward_s = float(backward_s)
         _, model = self.best_model()
         params = list(cpu_model.parameters())
         ready = cm.ready_times_from_flops(cpu_model, input_shape, backward_s)
@@ -238,7 +312,8 @@ class Autotune:
     def run_buckets(self, bucket_sizes: Sequence[int]) -> Dict[int, str]:
         sizes = sorted(set(int(s) for s in bucket_sizes))
         live = [a for a in self.algos if self.ok.get(a)]
-        self.bucket_table, ok = measure(self.engine, live, sizes, self.dtype, self.reps, self.warmup)
+        self.bucket_table, ok = measure(self.engine, live, sizes, self.dtype, self.reps, self.warmup,
+                                        probe=self.probe, reasons=self.excluded)
         for a, v in ok.items():
             self.ok[a] = self.ok.get(a, True) and v
         default = self.best_model()[0]
@@ -260,5 +335,12 @@ class Autotune:
             "bucket_ms": {a: {str(mib(n)): round(ms, 4) for n, ms in row.items()} for a, row in self.bucket_table.items()},
             "per_bucket_size": {str(mib(n)): a for n, a in self.per_size.items()},
             "cap_mib": self.cap_mib,
+            "cap_backward_ms": None if self.backward_s is None else round(self.backward_s * 1e3, 3),
             "size_unit": "MiB of bucket dtype",
+            "excluded": dict(self.excluded),
+            "probe_engines": {"created": self.probe.created, "discarded": self.probe.discarded},
         }
+
+    def close(self) -> None:
+        """Release the probe engine (its communicator and windows); the decisions stay."""
+        self.probe.close()

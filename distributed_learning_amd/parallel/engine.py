@@ -26,6 +26,7 @@ on a one-GPU box.
 from __future__ import annotations
 
 import functools
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -98,12 +99,15 @@ def topology(world: int, channels: int = 0, local_size: Optional[int] = None) ->
 class NativeEngine:
     """Wraps ``_C.CommEngine`` for one process group."""
 
+    MAP_ATTEMPTS = 3
+
     def __init__(self, impl, group, device: torch.device, channels: int, transport: str = "rccl"):
         self.impl = impl
         self.group = group
         self.device = device
         self.channels = channels
         self.transport = transport
+        self.stale_mappings = 0  # IPC mappings refused by the nonce check (re-allocated)
 
     @classmethod
     def create(cls, group=None, device: Optional[torch.device] = None, channels: int = 0,
@@ -136,6 +140,22 @@ class NativeEngine:
         impl.set_accum_fp32(n > 1 if accum_fp32 is None else bool(accum_fp32))
         return cls(impl, group, device, len(topo["rings"]), transport)
 
+    def probe_clone(self, timeout_s: float = 30.0) -> "NativeEngine":
+        """Collective: a second engine over the same group and topology with its OWN communicator
+        (a second ncclCommInitRank) and stream, and a short deadline. The autotuner runs every
+        non-builtin candidate here, so a schedule that hangs or raises an async error aborts this
+        communicator only -- never the one training uses (engine.cpp wait_stream aborts the
+        communicators of the engine that timed out)."""
+        e = NativeEngine.create(self.group, self.device, channels=self.channels,
+                                local_size=int(self.impl.local_size()), accum_fp32=bool(self.impl.accum_fp32()),
+                                transport=self.transport)
+        e.set_timeout(timeout_s)
+        return e
+
+    def set_timeout(self, seconds: float) -> None:
+        """Deadline of this engine's waits and IPC barriers (<= 0: ``DLA_COMM_TIMEOUT_S``)."""
+        self.impl.set_timeout(float(seconds))
+
     # -- setup -------------------------------------------------------------------------------
     def uses_ipc(self, algo: str) -> bool:
         return self.transport == "ipc" or parse_algo(algo)[2]
@@ -147,40 +167,70 @@ class NativeEngine:
         if self.uses_ipc(algo):
             self._map_windows()
 
-    def _map_windows(self) -> None:
+    def _map_windows(self, force: bool = False) -> None:
         """Collective: every rank calls it at the same point (the need is deterministic, so all
-        ranks agree on whether to grow; it is all-gathered anyway)."""
+        ranks agree on whether to grow; it is all-gathered anyway). ``force``: allocate and map a
+        new window generation even when the current one is large enough (tests cycle windows)."""
         need = int(self.impl.ipc_need())
         world = self.impl.world()
         needs: List[object] = [None] * world
         dist.all_gather_object(needs, need, group=self.group)
         need = max(int(x) for x in needs)
-        if need <= int(self.impl.ipc_capacity()):
+        if force:
+            need = max(need, int((int(self.impl.ipc_capacity()) - (1 << 20)) / 1.25), 1 << 16)
+        elif need <= int(self.impl.ipc_capacity()):
             return
         self.impl.synchronize()  # nothing of mine in flight reads a peer window
         dist.barrier(group=self.group)  # ... nor of any peer's that reads mine
         # every step below is agreed on across ranks before the next, so a rank whose allocation or
         # mapping fails (e.g. peer memory this node cannot map) raises on EVERY rank at the same point
-        # instead of leaving the others waiting in a collective
-        handle, err = None, ""
-        try:
-            handle = self.impl.ipc_alloc(int(need * 1.25) + (1 << 20))
-        except Exception as e:  # noqa: BLE001
-            err = f"ipc_alloc: {e}"
-        handles: List[object] = [None] * world
-        dist.all_gather_object(handles, (handle, err), group=self.group)
-        errs = [e for _, e in handles if e]
-        if errs:
-            raise RuntimeError("IPC window allocation failed: " + "; ".join(errs))
-        try:
-            self.impl.ipc_open([h for h, _ in handles])
-        except Exception as e:  # noqa: BLE001
-            err = f"ipc_open: {e}"
-        flags: List[object] = [None] * world
-        dist.all_gather_object(flags, err, group=self.group)
-        errs = [e for e in flags if e]
-        if errs:
-            raise RuntimeError("IPC window mapping failed: " + "; ".join(errs))
+        # instead of leaving the others waiting in a collective.
+        #
+        # Each new window carries a fresh random nonce that every importer reads back through its
+        # mapping (CommEngine.ipc_open). A mapping that shows another nonce is a stale view of an
+        # earlier window: pulls through it would read old data and its flag would never advance (the
+        # window lifecycle is the leading candidate for the round-4 g23 failure, profiles/r5/g02).
+        # All ranks then allocate again -- the superseded
+        # windows stay allocated until a verified set exists, so the retry lands on fresh addresses.
+        size = int(need * 1.25) + (1 << 20)
+        stale: List[str] = []
+        for attempt in range(self.MAP_ATTEMPTS):
+            nonce = int.from_bytes(os.urandom(8), "little") | 1
+            handle, err = None, ""
+            try:
+                handle = self.impl.ipc_alloc(size, nonce)
+            except Exception as e:  # noqa: BLE001
+                err = f"ipc_alloc: {e}"
+            handles: List[object] = [None] * world
+            dist.all_gather_object(handles, (handle, nonce, err), group=self.group)
+            errs = [e for _, _, e in handles if e]
+            if errs:
+                raise RuntimeError("IPC window allocation failed: " + "; ".join(errs))
+            bad = ""
+            try:
+                bad = self.impl.ipc_open([h for h, _, _ in handles], [n for _, n, _ in handles])
+            except Exception as e:  # noqa: BLE001
+                err = f"ipc_open: {e}"
+            flags: List[object] = [None] * world
+            dist.all_gather_object(flags, (err, bad), group=self.group)
+            errs = [e for e, _ in flags if e]
+            if errs:
+                raise RuntimeError("IPC window mapping failed: " + "; ".join(errs))
+            stale = [f"rank {r}: {b}" for r, (_, b) in enumerate(flags) if b]
+            if not stale:
+                return
+            self.stale_mappings += 1
+        raise RuntimeError(f"IPC window mapping stayed stale after {self.MAP_ATTEMPTS} attempts: " + "; ".join(stale))
+
+    def remap_windows(self) -> None:
+        """Collective: replace every rank's IPC window by a new generation of the same size."""
+        self._map_windows(force=True)
+
+    def ipc_error_info(self) -> Dict[str, int]:
+        """The first timed-out IPC barrier's record (error, awaited token, peer flag seen, peer rank),
+        the host token counter, the verified window generation and stale mappings refused."""
+        keys = ("error", "awaited", "seen", "peer", "host_token", "generation", "stale_refused")
+        return dict(zip(keys, (int(v) for v in self.impl.ipc_error_info())))
 
     def _lazy_reserve(self, algo: str, flat: torch.Tensor) -> None:
         """First use of a size the windows do not hold yet: grow them (collective -- the need is a
@@ -217,6 +267,13 @@ class NativeEngine:
         """Gather autograd-owned ``grads`` into ``flat`` at ``offsets`` on the comm stream, then reduce."""
         self.impl.bucket_allreduce_list(flat, algo_code(algo), average, list(grads), list(offsets))
 
+    def bucket_allreduce_group(self, group: torch.Tensor, starts, counts, algo: str, grads, offsets,
+                               average: bool = True) -> None:
+        """Per-tensor collectives of a fusion-off launch group (members are slices of ``group``): one
+        gather of ``grads`` at ``offsets`` (group-relative), one staging cast and one RCCL group."""
+        self.impl.bucket_allreduce_group(group, list(starts), list(counts), algo_code(algo), average, list(grads),
+                                         list(offsets))
+
     def broadcast(self, t: torch.Tensor, root: int = 0) -> None:
         self.impl.broadcast(t, root)
 
@@ -241,5 +298,13 @@ class NativeEngine:
             try:
                 if not self.impl.aborted():
                     self.impl.synchronize()
+            finally:
+                self.impl = None
+
+    def discard(self) -> None:
+        """Abort this engine's communicators (a failed probe) and drop it without waiting."""
+        if self.impl is not None:
+            try:
+                self.impl.abort()
             finally:
                 self.impl = None

@@ -207,6 +207,32 @@ class NativeStreamExecutor(Executor):
             return
         self._submit(b)
 
+    def submit_group(self, group) -> None:
+        """A fusion-off launch group (grad_sync.LaunchGroup): its buckets keep one collective each, issued
+        together (engine.bucket_allreduce_group)."""
+        if self.passthrough:
+            return
+        dev = group.buf.device
+        if _side_pending(dev):
+            j = self._join.get(dev)
+            if j is None:
+                j = self._join[dev] = torch.cuda.Stream(device=dev)
+            j.wait_stream(torch.cuda.current_stream(dev))
+            _late_wgrads_into(j, dev)
+            with torch.cuda.stream(j):
+                self._submit_group(group)
+            return
+        self._submit_group(group)
+
+    def _submit_group(self, group) -> None:
+        grads, offs = [], []
+        for b, start in zip(group.buckets, group.starts):
+            for g, o in (getattr(b, "stolen", None) or []):
+                grads.append(g)
+                offs.append(start + o)
+        algo = self.algorithm_for(group.buckets[0])
+        self.engine.bucket_allreduce_group(group.buf, group.starts, [b.numel for b in group.buckets], algo, grads, offs)
+
     def _submit(self, b: Bucket) -> None:
         algo = self.algorithm_for(b)
         stolen = getattr(b, "stolen", None)
@@ -227,6 +253,16 @@ class NativeStreamExecutor(Executor):
         for b in buckets:
             groups.setdefault((self.algorithm_for(b), b.flat.dtype), []).append(b.flat.numel())
         for (algo, dt), sizes in sorted(groups.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
+            self.engine.reserve(algo, sizes, dt)
+
+    def reserve_groups(self, groups) -> None:
+        """Staging for the fusion-off launch groups (their buffers are reduced as one staged region)."""
+        if self.passthrough:
+            return
+        by = {}
+        for g in groups:
+            by.setdefault((self.algorithm_for(g.buckets[0]), g.buf.dtype), []).append(g.buf.numel())
+        for (algo, dt), sizes in sorted(by.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
             self.engine.reserve(algo, sizes, dt)
 
     def finish(self) -> None:

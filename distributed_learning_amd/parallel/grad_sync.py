@@ -30,6 +30,8 @@ Fixes and MI355X design:
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
+
 from .. import knobs
 import contextlib
 from typing import Callable, Iterable, List, Optional, Sequence, Set
@@ -80,6 +82,50 @@ def find_unused_parameters(output, params: Sequence[torch.Tensor]) -> List[torch
     return [p for p in params if p.requires_grad and id(p) not in reached]
 
 
+# Fusion off (one bucket per tensor, the reference's main_overlap / main_onestep_overlap): per-tensor
+# buckets of one dtype form launch groups of at most LAUNCH_GROUP_BYTES / LAUNCH_GROUP_MAX tensors, whose
+# members lie within LAUNCH_GROUP_SPAN consecutive buckets (so a group never waits long for its last
+# member). Each tensor keeps its own collective; the group shares one event join, gather launch, staging
+# cast and RCCL group (engine.cpp bucket_allreduce_group). Groups launch in the order of their last
+# member, and the grouping is a pure function of the parameter list, so every rank issues the same
+# sequence. A tensor above the byte cap is a group of its own.
+LAUNCH_GROUP_BYTES = 1 << 20
+LAUNCH_GROUP_MAX = 16
+LAUNCH_GROUP_SPAN = 24
+
+
+@dataclass
+class LaunchGroup:
+    buckets: List[Bucket]
+    starts: List[int]       # element offset of each bucket's flat buffer in ``buf``
+    buf: torch.Tensor = None
+
+
+def launch_groups(buckets: Sequence[Bucket], max_bytes: int = LAUNCH_GROUP_BYTES, max_tensors: int = LAUNCH_GROUP_MAX,
+                  span: int = LAUNCH_GROUP_SPAN) -> List[List[Bucket]]:
+    """Per-dtype greedy grouping of buckets in index (backward) order; returned in launch order (by the
+    index of each group's last bucket)."""
+    done: List[List[Bucket]] = []
+    open_: dict = {}
+    for pos, b in enumerate(buckets):
+        dt = b.params[0].dtype
+        nb = b.padded_numel * b.params[0].element_size()
+        cur = open_.get(dt)
+        if cur is not None:
+            members, size, first = cur
+            if size + nb > max_bytes or len(members) >= max_tensors or pos - first >= span:
+                done.append(members)
+                cur = None
+        if cur is None:
+            open_[dt] = [[b], nb, pos]
+        else:
+            cur[0].append(b)
+            cur[1] += nb
+    done.extend(v[0] for v in open_.values())
+    pos_of = {id(b): i for i, b in enumerate(buckets)}
+    return sorted(done, key=lambda g: pos_of[id(g[-1])])
+
+
 class GradSync:
     """Owns buckets, hooks and an executor for a fixed parameter list."""
 
@@ -118,8 +164,13 @@ class GradSync:
         self.grad_as_bucket_view = grad_as_bucket_view
         self.buckets: List[Bucket] = bucketize(self.params, bucket_cap_bytes)
         self._owner = {}
+        # fusion off on the native engine: per-tensor buckets launched in groups (see LaunchGroup)
+        self.groups: List[LaunchGroup] = []
+        if grad_mode == "steal":
+            self._build_groups()
         for b in self.buckets:
-            b.flat = torch.zeros(b.padded_numel, dtype=comm_dtype or b.params[0].dtype, device=self.device)
+            if b.flat is None:
+                b.flat = torch.zeros(b.padded_numel, dtype=comm_dtype or b.params[0].dtype, device=self.device)
             for j, p in enumerate(b.params):
                 self._owner[id(p)] = (b, j)
         self._persistent_grads = {}
@@ -157,10 +208,53 @@ class GradSync:
         self.step_count = 0
         if hasattr(self.executor, "reserve"):
             self.executor.reserve(self.buckets)
+            if self.groups and hasattr(self.executor, "reserve_groups"):
+                self.executor.reserve_groups(self.groups)
 
     # -------------------------------------------------------------------------------------------
     # setup
     # -------------------------------------------------------------------------------------------
+    def _wants_groups(self) -> bool:
+        ex = self.executor
+        per_tensor = len(self.buckets) > 1 and all(len(b.params) == 1 for b in self.buckets)
+        return (per_tensor and self.comm_dtype is None and self.overlap and self.device.type == "cuda"
+                and getattr(ex, "supports_steal", False) and hasattr(ex, "submit_group")
+                and not getattr(ex, "passthrough", False))
+
+    def _build_groups(self) -> None:
+        self.groups = []
+        for b in self.buckets:
+            b.group = None
+        if not self._wants_groups():
+            return
+        for members in launch_groups(self.buckets):
+            starts, n = [], 0
+            for b in members:
+                starts.append(n)
+                n += b.padded_numel
+            g = LaunchGroup(members, starts, torch.zeros(n, dtype=members[0].params[0].dtype, device=self.device))
+            for b, st in zip(members, starts):
+                b.flat = g.buf[st:st + b.padded_numel]
+                b.group = g
+            self.groups.append(g)
+
+    def set_executor(self, executor: Executor) -> None:
+        """Replace the executor after construction (e.g. a forced full data path at one rank); the
+        fusion-off launch groups and the steal-mode views follow the new executor."""
+        self.executor = executor
+        self.passthrough = bool(getattr(executor, "passthrough", False))
+        if self.grad_mode == "steal":
+            had = bool(self.groups)
+            self._build_groups()
+            if had or self.groups:
+                for b in self.buckets:
+                    if b.group is None:
+                        b.flat = torch.zeros(b.padded_numel, dtype=b.params[0].dtype, device=self.device)
+                self._install_views(install=False)
+        if hasattr(executor, "reserve"):
+            executor.reserve(self.buckets)
+            if self.groups and hasattr(executor, "reserve_groups"):
+                executor.reserve_groups(self.groups)
     def _install_views(self, install: bool = True):
         for b in self.buckets:
             b.views = []
@@ -280,11 +374,26 @@ class GradSync:
         self._launch_in_order()
 
     def _launch_in_order(self) -> None:
+        if self.groups:
+            self._launch_groups_in_order()
+            return
         while self._next < len(self.buckets) and self.buckets[self._next].ready == len(self.buckets[self._next].params):
             b = self.buckets[self._next]
             b.launched = True
             self._next += 1
             self.executor.submit(b)
+
+    def _launch_groups_in_order(self) -> None:
+        # self._next counts groups (in launch order); a group goes out when all of its buckets are ready
+        # and every earlier group has gone out
+        while self._next < len(self.groups):
+            g = self.groups[self._next]
+            if any(b.ready != len(b.params) for b in g.buckets):
+                return
+            for b in g.buckets:
+                b.launched = True
+            self._next += 1
+            self.executor.submit_group(g)
 
     def flush(self) -> None:
         """Launch every bucket that has not been launched (zero-filling missing grads).
@@ -292,7 +401,7 @@ class GradSync:
         One rank with a pass-through executor reduces nothing, so parameters that got no gradient
         (GoogLeNet's unused aux heads) keep ``grad = None`` as in plain PyTorch, and optimizers skip
         them, instead of paying a zero-fill launch per tensor every step."""
-        for b in self.buckets[self._next:]:
+        for b in [b for b in self.buckets if not b.launched]:
             if b.ready < len(b.params):
                 if self.grad_mode == "steal":
                     if len(b.is_ready) != len(b.params):

@@ -91,6 +91,9 @@ def main():
                 if C.gemm_stream_rows(M, N, K, K, N, kmaj):
                     r["stream_forced_ms"] = timeit(lambda: C.gemm_nt(A, B, stats, None, kmaj, 0))
             C.set_gemm_stream(-1)
+            # the library GEMM (torch.matmul -> hipBLASLt) on the same operands, no BN-statistics epilogue
+            Bt = B.t() if kind == "fwd" else B
+            r["hipblaslt_ms"] = timeit(lambda: torch.matmul(A, Bt))
             r["auto_TBps"] = round(byts / r["auto_ms"] / 1e9, 2)
             r["auto_ms_per_step"] = round(r["auto_ms"] * calls, 4)
             rows.append(r)

@@ -43,7 +43,29 @@ def launch(a) -> int:
     return subprocess.run(cmd, env=env, timeout=a.timeout).returncode
 
 
+def _check(eng, c, dist, torch, algo, dtype, n, average, results, phase):
+    world, rank = c.world_size, c.rank
+    i = torch.arange(n, device=c.device, dtype=torch.int64)
+    pat = ((i % 7) - 3)
+    buf = (pat * (rank + 1)).to(dtype)
+    eng.allreduce(buf, algo, average)
+    eng.synchronize()
+    want = pat.double() * (world * (world + 1) / 2.0)
+    if average:
+        want = want / world
+    err = float((buf.double() - want).abs().max()) if n else 0.0
+    tol = 1e-6 if dtype == torch.float32 else float(want.abs().max()) * 2 ** -8 + 1e-6
+    # bitwise agreement across ranks: a checksum of the raw bytes
+    raw = buf.view(torch.int16 if dtype == torch.bfloat16 else torch.int32).long().sum().item()
+    raws = [None] * world
+    dist.all_gather_object(raws, raw)
+    results.append({"phase": phase, "algo": algo, "dtype": str(dtype).split(".")[-1], "n": n, "average": average,
+                    "max_err": err, "ok": err <= tol and len(set(raws)) == 1})
+
+
 def worker(a) -> None:
+    import traceback
+
     import torch
     import torch.distributed as dist
 
@@ -53,39 +75,50 @@ def worker(a) -> None:
     c = ctxmod.init(backend="gloo" if same else "nccl", same_device=same, transport="ipc")
     world, rank = c.world_size, c.rank
     local = int(os.environ.get("LOCAL_WORLD_SIZE", world))
-    results = []
-    for algo in a.algos.split(","):
-        ls = 2 if (algo.startswith("hier") and world % 2 == 0 and world > 2) else None
-        eng = c.engine(local_size=ls if ls else local, transport="ipc")
-        for dtype in (torch.float32, torch.bfloat16):
-            eng.set_accum_fp32(dtype == torch.bfloat16)
-            for n in SIZES:
-                for average in (True, False):
-                    i = torch.arange(n, device=c.device, dtype=torch.int64)
-                    pat = ((i % 7) - 3)
-                    buf = (pat * (rank + 1)).to(dtype)
-                    eng.allreduce(buf, algo, average)
-                    eng.synchronize()
-                    want = pat.double() * (world * (world + 1) / 2.0)
-                    if average:
-                        want = want / world
-                    err = float((buf.double() - want).abs().max())
-                    tol = 1e-6 if dtype == torch.float32 else float(want.abs().max()) * 2 ** -8 + 1e-6
-                    gathered = [None] * world
-                    dist.all_gather_object(gathered, buf.float().sum().item() if n else 0.0)
-                    # bitwise agreement: compare a checksum of the raw bytes too
-                    raw = buf.view(torch.int16 if dtype == torch.bfloat16 else torch.int32).long().sum().item()
-                    raws = [None] * world
-                    dist.all_gather_object(raws, raw)
-                    results.append({"algo": algo, "dtype": str(dtype).split(".")[-1], "n": n, "average": average,
-                                    "max_err": err, "ok": err <= tol and len(set(raws)) == 1})
+    results, engines, where = [], [], "setup"
+    try:
+        for algo in a.algos.split(","):
+            ls = 2 if (algo.startswith("hier") and world % 2 == 0 and world > 2) else None
+            eng = c.engine(local_size=ls if ls else local, transport="ipc")
+            if eng not in engines:
+                engines.append(eng)
+            for dtype in (torch.float32, torch.bfloat16):
+                eng.set_accum_fp32(dtype == torch.bfloat16)
+                for n in SIZES:
+                    for average in (True, False):
+                        where = f"{algo} {dtype} n={n} average={average}"
+                        _check(eng, c, dist, torch, algo, dtype, n, average, results, "sweep")
+        # window lifecycle: every cycle replaces all windows by a new generation (a fresh nonce each,
+        # read back through every peer's mapping) and runs two schedules through the new mappings
+        eng = engines[0]
+        for k in range(a.regrow):
+            where = f"regrow cycle {k}"
+            eng.remap_windows()
+            for algo in ("direct", "ring"):
+                _check(eng, c, dist, torch, algo, torch.float32, 4097 + 64 * k, True, results, f"regrow{k}")
+    except Exception as e:  # noqa: BLE001 -- report which call failed on THIS rank, with the engine's record
+        info = {}
+        for eng in engines:
+            try:
+                info = eng.ipc_error_info()
+            except Exception as e2:  # noqa: BLE001
+                info = {"unavailable": str(e2)}
+        print(json.dumps({"rank": rank, "failed_at": where, "error": f"{type(e).__name__}: {e}"[:2000],
+                          "ipc": info}), file=sys.stderr, flush=True)
+        traceback.print_exc()
+        sys.exit(2)
     torch.cuda.synchronize()
+    bad = [r for r in results if not r["ok"]]
+    gens = engines[0].ipc_error_info() if engines else {}
+    stale = sum(e.stale_mappings for e in engines)
+    if bad:  # every rank names its own mismatches (rank 0's view alone hid the cause in r4 g23)
+        print(json.dumps({"rank": rank, "failed": bad[:20], "ipc": gens}), file=sys.stderr, flush=True)
     if rank == 0:
-        bad = [r for r in results if not r["ok"]]
         print(json.dumps({"world": world, "same_device": same, "checked": len(results), "failed": bad[:20],
-                          "ok": not bad}), flush=True)
+                          "regrow_cycles": a.regrow, "window_generation": gens.get("generation"),
+                          "stale_mappings_refused": stale, "ok": not bad}), flush=True)
     ctxmod.shutdown()
-    if [r for r in results if not r["ok"]]:
+    if bad:
         sys.exit(1)
 
 
@@ -95,6 +128,7 @@ def main():
     ap.add_argument("--same_device", type=int, default=1)
     ap.add_argument("--algos", default=",".join(ALGOS))
     ap.add_argument("--timeout", type=float, default=600.0)
+    ap.add_argument("--regrow", type=int, default=8, help="window generations to cycle through after the sweep")
     a = ap.parse_args()
     if "WORLD_SIZE" not in os.environ:
         sys.exit(launch(a))

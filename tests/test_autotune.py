@@ -117,3 +117,95 @@ def test_per_size_choice_keeps_default_within_margin():
     # 3 % faster is noise at the default margin; 10 % faster switches; unverified never wins
     assert per == {1: "builtin", 2: "ring", 3: "builtin"}
     assert at.choose_per_size(table, ok, [1], "builtin", margin=0.0) == {1: "ring"}
+
+
+# ---- probe isolation ----------------------------------------------------
+# A stand-in with the failure modes of a real RCCL engine: a candidate that HANGS (every rank's wait
+# hits the probe deadline; engine.cpp wait_stream then aborts that engine's communicator) and one that
+# raises an ASYNC ERROR on one rank only (the other rank sits in the collective until its deadline).
+# The training engine must never run a non-builtin candidate and must never be aborted; the run has to
+# finish on builtin with identical decisions on every rank and both failures named in the report.
+
+ISO_COST = {"builtin": (20.0, 0.002), "hang": (1.0, 0.0001), "async_err": (1.0, 0.0001), "ring": (30.0, 0.003)}
+
+
+class IsoEngine(FakeEngine):
+    def __init__(self, rank, world, role, log):
+        super().__init__(rank, world)
+        self.role, self.log = role, log
+        self.aborted = False
+        self.pending = None
+
+    def reserve(self, algo, sizes, dtype):
+        pass
+
+    def allreduce(self, buf, algo, average=True):
+        assert not self.aborted, "a call on an aborted communicator"
+        self.log.append((self.role, algo))
+        if algo in ("hang", "async_err"):
+            self.pending = algo  # the collective never completes / errors asynchronously
+            return
+        dist.all_reduce(buf)
+        if average:
+            buf /= self.impl.world()
+        a, b = ISO_COST[algo]
+        if self._timing:
+            self._t += (a + b * buf.numel() * buf.element_size() / 1024) * 1e-3
+
+    def synchronize(self):
+        p, self.pending = self.pending, None
+        if p == "hang":
+            self.aborted = True
+            raise RuntimeError("CommEngine: communication did not complete within 30.000000 s (peer failure?); "
+                               "communicators aborted")
+        if p == "async_err":
+            self.aborted = True
+            if self.impl.rank() == 1:
+                raise RuntimeError("CommEngine: RCCL async error: unhandled system error (communicators aborted)")
+            raise RuntimeError("CommEngine: communication did not complete within 30.000000 s (peer failure?); "
+                               "communicators aborted")
+
+    def consume_comm_ms(self):
+        self.synchronize()
+        return super().consume_comm_ms()
+
+    def discard(self):
+        self.aborted = True
+
+
+def _tune_isolated(rank, world):
+    log = []
+    train = IsoEngine(rank, world, "train", log)
+    probes = []
+
+    def factory():
+        e = IsoEngine(rank, world, f"probe{len(probes)}", log)
+        probes.append(e)
+        return e
+
+    t = at.Autotune(train, torch.float32, ["hang", "ring", "async_err", "builtin"], reps=2, warmup=1,
+                    probe_factory=factory)
+    at.GRID_MIB = (0.25, 1.0)
+    t.run_grid()
+    per = t.run_buckets([4096, 1 << 20])
+    t.close()
+    return {"ok": t.ok, "per": per, "best": t.best_model()[0], "report": t.report(), "log": log,
+            "train_aborted": train.aborted, "probes": len(probes)}
+
+
+def test_autotune_isolates_hanging_and_erroring_candidates():
+    a, b = dist_util.run(_tune_isolated, 2)
+    assert a["per"] == b["per"] and a["best"] == b["best"] and a["ok"] == b["ok"]
+    assert a["ok"] == {"builtin": True, "hang": False, "ring": True, "async_err": False}
+    for r in (a, b):
+        assert not r["train_aborted"]
+        # builtin ran first, on the training engine; nothing else ever touched it
+        assert r["log"][0] == ("train", "builtin")
+        assert {alg for role, alg in r["log"] if role == "train"} == {"builtin"}
+        # the probe that hung and the one that errored were replaced: 3 probe engines in all
+        assert r["probes"] == 3 and r["report"]["probe_engines"] == {"created": 3, "discarded": 2}
+        ex = r["report"]["excluded"]
+        assert set(ex) == {"hang", "async_err"}
+        assert "did not complete" in ex["hang"]
+        assert "rank 1: RuntimeError: CommEngine: RCCL async error" in ex["async_err"]
+    assert a["best"] == "builtin" and set(a["per"].values()) <= {"builtin", "ring"}

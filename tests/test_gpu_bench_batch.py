@@ -165,3 +165,66 @@ def test_stage1_bn_at_bench_rows(cuda, native):
     assert _rel(x1.grad, x2.grad) < 2e-2
     assert _rel(bn.weight.grad, bn_ref.weight.grad) < 1e-2
     assert _rel(bn.bias.grad, bn_ref.bias.grad) < 1e-2
+
+
+M2 = BATCH * 28 * 28  # stage 2: 1,003,520 rows
+
+
+@pytest.mark.parametrize("M,ci,co", [(M1, 64, 256), (M2, 128, 512)])
+def test_one_pass_1x1_gradients_at_bench_rows(cuda, M, ci, co):
+    """gemm_dual.hip (both gradients of a stride-1 1x1 conv in one pass over dY) at the benchmarked row
+    counts: stage 1's 64 -> 256 conv3 at M = 4,014,080 (byte offsets up to 2.06e9, 4 % under the 2^31
+    out-of-range sentinel) and stage 2's Cout-512 form at M = 1,003,520, against fp32 torch. The last 4096
+    rows are checked on their own: dX directly, dW with dY zero everywhere else (the tail tiles' whole
+    contribution)."""
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    assert C.conv1x1_dual_blocks(M, ci, co) > 0
+    g = torch.Generator().manual_seed(M + co)
+    dy = torch.randn(M, co, generator=g).to(cuda, torch.bfloat16)
+    x = torch.randn(M, ci, generator=g).to(cuda, torch.bfloat16)
+    w = (torch.randn(co, ci, generator=g) * co ** -0.5).to(cuda, torch.bfloat16)
+    dx, dw = C.conv1x1_dual(dy, x, w, torch.float32)
+    torch.cuda.synchronize()
+    wf = w.float()
+    assert _rel(dx, dy.float() @ wf) < 5e-3
+    tail = slice(M - 4096, M)
+    assert _rel(dx[tail], dy[tail].float() @ wf) < 5e-3
+    assert _rel(dw, dy.float().t() @ x.float()) < 1e-4
+    dyt = torch.zeros_like(dy)
+    dyt[tail] = dy[tail]
+    _, dwt = C.conv1x1_dual(dyt, x, w, torch.float32)
+    assert _rel(dwt, dy[tail].float().t() @ x[tail].float()) < 1e-4
+
+
+def test_one_pass_1x1_with_bn_apply_at_bench_rows(cuda):
+    """The kBN form (the block-final BN's backward apply inside the one-pass kernel) at stage 1's M = 4,014,080:
+    against the BN apply of bn_act_bwd followed by fp32 torch products, tail rows separately."""
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    M, ci, co = M1, 64, 256
+    assert C.conv1x1_dual_bn_ok(M, ci, co)
+    g = torch.Generator().manual_seed(21)
+    dout = torch.randn(M, co, generator=g).to(cuda, torch.bfloat16)
+    ybn = (torch.randn(M, co, generator=g) * 2 + 0.5).to(cuda, torch.bfloat16)
+    x = torch.randn(M, ci, generator=g).to(cuda, torch.bfloat16)
+    w = (torch.randn(co, ci, generator=g) * co ** -0.5).to(cuda, torch.bfloat16)
+    mask = torch.randint(0, 256, ((M * co + 7) // 8,), generator=g, dtype=torch.uint8).to(cuda)
+    gamma = (torch.rand(co, generator=g) + 0.5).to(cuda)
+    ws = torch.zeros(7 * co, device=cuda)
+    ws[:co] = ybn.float().mean(0)
+    ws[co:2 * co] = (ybn.float().var(0, unbiased=False) + 1e-5).rsqrt()
+    ws_a, ws_b = ws.clone(), ws.clone()
+    dY, _, _, _ = C.bn_act_bwd(dout, None, mask, ybn, ws_a, gamma, 2, False, None)  # the separate apply
+    C.bn_act_bwd(dout, None, mask, ybn, ws_b, gamma, 2, False, None, False)  # reduction + finalize only
+    dx, dw = C.conv1x1_dual(dout, x, w, torch.float32, ybn, ws_b, mask)
+    torch.cuda.synchronize()
+    assert torch.equal(ws_a, ws_b)
+    del dout, ybn, mask
+    dYf = dY.float()
+    assert _rel(dx, dYf @ w.float()) < 5e-3
+    tail = slice(M - 4096, M)
+    assert _rel(dx[tail], dYf[tail] @ w.float()) < 5e-3
+    assert _rel(dw, dYf.t() @ x.float()) < 2e-3

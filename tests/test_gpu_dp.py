@@ -97,6 +97,44 @@ def test_native_engine_steal_path_matches_single_device(world1, arch, bf16, stag
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6, msg=n)
 
 
+@pytest.mark.parametrize("staged", [False, True])
+def test_fusion_off_launch_groups_match_single_device(world1, staged):
+    """Fusion off (one bucket per tensor) on the native engine: consecutive per-tensor buckets are launched
+    in groups (grad_sync.LaunchGroup -> engine.bucket_allreduce_group: one gather, one staging cast, one RCCL
+    group of per-tensor all-reduces, one cast back). The forced world-1 path must reproduce the single-device
+    update exactly, with fewer launches than tensors."""
+    from distributed_learning_amd.models import resnet18
+    from distributed_learning_amd.ops import nn as dnn
+    from distributed_learning_amd.parallel import PipelinedFusedDP, SingleDevice, make_reducer
+    from distributed_learning_amd.parallel.executor import NativeStreamExecutor
+
+    dnn.set_backend("native")
+    det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    seen = {}
+    try:
+        def wrap_dp(m):
+            red = make_reducer("immediate", "builtin", native=True)
+            w = PipelinedFusedDP(m, red, 0, broadcast=False)
+            if staged:
+                red.engine.impl.set_force(True)
+                red.engine.set_accum_fp32(True)
+            w.sync.set_executor(NativeStreamExecutor(red.engine, "builtin", passthrough=False))
+            seen["groups"], seen["buckets"] = len(w.sync.groups), len(w.sync.buckets)
+            assert w.sync.grad_mode == "steal"
+            return w
+
+        m1, l1 = _train(lambda: resnet18(10), wrap_dp, 4, True)
+        m2, l2 = _train(lambda: resnet18(10), SingleDevice, 4, True)
+    finally:
+        dnn.set_backend("torch")
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
+    assert 0 < seen["groups"] < seen["buckets"] == 62, seen
+    assert l1 == pytest.approx(l2, rel=1e-5, abs=1e-5)
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6, msg=n)
+
+
 def test_engine_algorithms_world1(world1):
     from distributed_learning_amd.parallel.engine import ALGO_CODES, NativeEngine
 

@@ -200,3 +200,65 @@ def test_bn_handoff_falls_back_when_output_has_other_consumers(cuda):
         assert float((a - b).norm() / b.norm().clamp_min(1e-20)) < 1e-2
     for a, b in zip(g_alone, g_ref_alone):
         assert float((a - b).norm() / b.norm().clamp_min(1e-20)) < 1e-2
+
+
+def _two_bn_setup(cuda):
+    import torch.nn as nn
+
+    CL = torch.channels_last
+    torch.manual_seed(1)
+    convs = [nn.Conv2d(256, 64, 1, bias=False), nn.Conv2d(256, 64, 1, bias=False), nn.Conv2d(64, 256, 1, bias=False)]
+    convs = [c.to(cuda).to(memory_format=CL) for c in convs]
+    for c in convs:
+        c.weight.data = c.weight.data.to(torch.bfloat16)
+    bns = [nn.BatchNorm2d(256).to(cuda), nn.BatchNorm2d(256).to(cuda)]
+    mk = lambda *s: torch.randn(*s, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)  # noqa: E731
+    return convs, bns, mk(24, 256, 56, 56), mk(24, 256, 56, 56), mk(24, 64, 56, 56), \
+        torch.randn(24, 256, 56, 56, device=cuda).contiguous(memory_format=CL)
+
+
+def test_bn_handoff_one_conv_output_two_bns(cuda):
+    """one conv output consumed by TWO fused BN(+residual)+ReLU calls. Only the first BN may claim the
+    conv's hand-off link (a second park would overwrite the first BN's parked gradient and lose it); the second
+    runs the normal path. Gradients must equal the run without the hand-off. With retain_grad() on the conv
+    output, nothing is handed off and the retained gradient is the real one, not the placeholder's zeros."""
+    from distributed_learning_amd.ops import bn_act
+    from distributed_learning_amd.ops import conv as nconv
+    from distributed_learning_amd.ops import nn as dnn
+
+    (c1a, c1b, c3), (bn1, bn2), xa0, xb0, h0, wgt = _two_bn_setup(cuda)
+
+    def run(flag, retain):
+        old = nconv.DUAL_BN
+        nconv.DUAL_BN = flag
+        try:
+            for p in (c1a.weight, c1b.weight, c3.weight, bn1.weight, bn1.bias, bn2.weight, bn2.bias):
+                p.grad = None
+            xa, xb, h = (t.clone().requires_grad_(True) for t in (xa0, xb0, h0))
+            _, _, ia, _ = nconv.conv1x1_fork(xa, c1a)
+            _, _, ib, _ = nconv.conv1x1_fork(xb, c1b)
+            y3, st = nconv.conv1x1(h, c3, want_stats=True)
+            if retain:
+                y3.retain_grad()
+            out = bn_act.fused_bn_act(y3, bn1, True, ia, st) + bn_act.fused_bn_act(y3, bn2, True, ib, st)
+            before = nconv.CALLS["1x1_dual_bn"]
+            (out.float() * wgt).sum().backward()
+            fused = nconv.CALLS["1x1_dual_bn"] - before
+            gs = [t.float().clone() for t in (xa.grad, xb.grad, h.grad, c3.weight.grad, bn1.weight.grad,
+                                              bn2.weight.grad, bn1.bias.grad, bn2.bias.grad)]
+            return fused, gs, (y3.grad.float().clone() if retain else None)
+        finally:
+            nconv.DUAL_BN = old
+
+    dnn.set_backend("native")
+    try:
+        n_on, g_on, _ = run(True, False)
+        n_ret, g_ret, y_ret = run(True, True)
+        _, g_ref, y_ref = run(False, True)
+    finally:
+        dnn.set_backend("torch")
+    assert n_on == 0 and n_ret == 0  # two consumers: the conv sees a summed gradient and materialises
+    for got in (g_on, g_ret):
+        for a, b in zip(got, g_ref):
+            assert float((a - b).norm() / b.norm().clamp_min(1e-20)) < 1e-2
+    assert float(y_ret.abs().max()) > 0 and float((y_ret - y_ref).norm() / y_ref.norm()) < 1e-2

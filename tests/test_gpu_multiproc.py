@@ -50,6 +50,9 @@ def test_ipc_engine_two_processes(cuda):
     assert r.returncode == 0, r.returncode
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["ok"] and rec["world"] == 2 and rec["checked"] >= 100, rec
+    # every regrow cycle mapped a new window generation whose nonce every peer read back (or re-allocated)
+    assert rec["regrow_cycles"] >= 8 and rec["window_generation"] >= rec["regrow_cycles"], rec
+    print("ipc check:", {k: rec[k] for k in ("checked", "window_generation", "stale_mappings_refused")})
 
 
 @pytest.fixture(scope="module")
@@ -170,3 +173,15 @@ def test_killed_rank_fails_the_job(cuda):
     assert "injected failure" in r.stderr
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert time.time() - t0 < 190
+
+
+def test_graph_capture_refused_on_ipc_transport(cuda):
+    """the IPC barrier tokens are host-side launch arguments, so a replayed HIP graph would
+    pass every barrier at once. bench.py refuses --graph on with the IPC transport before any step runs (and
+    CommEngine.allreduce_ipc refuses a capturing stream)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same_device", "1", "--batch", "8",
+           "--steps", "1", "--warmup", "0", "--graph", "on", "--launch_timeout", "150"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=200, env=_env(), cwd=ROOT)
+    assert r.returncode != 0
+    assert "cannot capture the IPC transport" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

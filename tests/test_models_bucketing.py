@@ -82,3 +82,34 @@ def test_bucket_rules():
     for b in bs:
         assert all(o % ALIGN_ELEMS == 0 for o in b.offsets)
         assert b.padded_numel >= b.numel
+
+
+def test_fusion_off_launch_groups_are_consecutive_and_capped():
+    """grad_sync.launch_groups: per-tensor buckets (fusion off) grouped per dtype, greedily in index order under
+    the byte / tensor / span caps; an oversize tensor is alone; groups come in the order of their last member;
+    a pure function of the parameter list."""
+    import torch
+
+    from distributed_learning_amd.models import resnet50
+    from distributed_learning_amd.ops import nn as dnn
+    from distributed_learning_amd.parallel.bucketing import bucketize
+    from distributed_learning_amd.parallel.grad_sync import (LAUNCH_GROUP_BYTES, LAUNCH_GROUP_MAX, LAUNCH_GROUP_SPAN,
+                                                             launch_groups)
+
+    m = resnet50()
+    dnn.bf16_weights(m)
+    bs = bucketize(m.parameters(), 0)
+    assert len(bs) == 161 and all(len(b.params) == 1 for b in bs)
+    gs = launch_groups(bs)
+    assert sorted(b.index for g in gs for b in g) == list(range(161))
+    assert [g[-1].index for g in gs] == sorted(g[-1].index for g in gs)
+    for g in gs:
+        idx = [b.index for b in g]
+        assert idx == sorted(idx) and idx[-1] - idx[0] < LAUNCH_GROUP_SPAN
+        assert len({b.params[0].dtype for b in g}) == 1 and len(g) <= LAUNCH_GROUP_MAX
+        nb = sum(b.padded_numel * b.params[0].element_size() for b in g)
+        assert nb <= LAUNCH_GROUP_BYTES or len(g) == 1
+    assert len(gs) < 161 / 2
+    assert [[b.index for b in g] for g in launch_groups(bucketize(m.parameters(), 0))] == \
+        [[b.index for b in g] for g in gs]
+    assert torch.bfloat16 in {g[0].params[0].dtype for g in gs} and torch.float32 in {g[0].params[0].dtype for g in gs}
