@@ -328,6 +328,10 @@ def main():
     c = ctxmod.init(backend="gloo" if same else "nccl", same_device=same, transport=a.transport)
     world, rank = c.world_size, c.rank
     dev = c.device
+    if knobs.get("COMPUTE_STREAM") == "high":
+        # the step's kernels (and, through autograd, its backward) on a high-priority queue: the late 3x3 weight
+        # gradients' side stream (normal priority) then fills in behind the critical path instead of sharing it
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     fp32 = a.precision == "fp32"
     bf16 = a.precision == "bf16"
     # the native kernels are bf16 kernels; the fp32 reference-precision path keeps NCHW on MIOpen / torch

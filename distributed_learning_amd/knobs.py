@@ -32,6 +32,8 @@ TABLE: Dict[str, Knob] = {
     "GRAPH": Knob("off", "bench.py", "on | off: HIP-graph capture of the whole step (bench --graph default)"),
     "SAME_DEVICE": Knob("0", "parallel/context.py", "1: every rank on cuda:0 (gloo + IPC transport)"),
     "TRANSPORT": Knob("", "parallel/context.py", "rccl | ipc gradient transport (default rccl; ipc with SAME_DEVICE)"),
+    "COMPUTE_STREAM": Knob("default", "bench.py", "high: the training step runs on a high-priority stream, so its "
+                                                  "kernels dispatch ahead of the late weight gradients' side stream"),
     "COMM_TIMEOUT_S": Knob("600", "csrc/comm/engine.cpp", "seconds before a collective / IPC barrier is declared dead"),
     # ---- scheduling of the backward ----------------------------------------------------------------
     "WGRAD_DEFER": Knob("3x3", "ops/conv.py", "3x3 | auto | all | 0: weight gradients on the side stream "
