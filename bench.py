@@ -100,7 +100,8 @@ def parse():
     ap.add_argument("--precision", default=knobs.get("PRECISION"), choices=["autocast", "bf16", "fp32"],
                     help="bf16: bf16 weights + fp32 master weights in the fused optimizer (no per-step weight casts, "
                          "bf16 gradients on the wire); autocast: fp32 params + bf16 autocast; fp32: the reference's "
-                         "precision (fp32 weights and activations, NCHW, MIOpen / torch kernels)")
+                         "precision (fp32 weights and activations; native BN/pool/loss/SGD kernels + MIOpen convs, "
+                         "or with --kernels torch the stock NCHW path)")
     ap.add_argument("--conv", default=knobs.get("CONV"), choices=["miopen", "native"],
                     help="1x1 convolutions on the native MFMA GEMMs (with fused BN statistics) or MIOpen")
     ap.add_argument("--graph", default=knobs.get("GRAPH"), choices=["on", "off"],
@@ -334,9 +335,17 @@ def main():
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     fp32 = a.precision == "fp32"
     bf16 = a.precision == "bf16"
-    # the native kernels are bf16 kernels; the fp32 reference-precision path keeps NCHW on MIOpen / torch
+    # fp32 (the reference's precision): with --kernels native the activations stay channels_last and the fused
+    # BN/residual/ReLU, pools, global-average pool, cross-entropy and SGD run on the native kernels' fp32 forms,
+    # the convolutions on MIOpen (the MFMA conv kernels are bf16); --kernels torch is the stock NCHW path
+    fp32_torch = fp32 and a.kernels == "torch"
+    # fp32 means fp32: no TF32-style reduced-precision convolutions / matmuls (torch enables them for MIOpen by
+    # default), and MIOpen's immediate mode instead of an exhaustive find over every fp32 conv shape
     torch.backends.cudnn.benchmark = not fp32
-    dnn.set_backend("torch" if fp32 else a.kernels)
+    if fp32:
+        torch.backends.cudnn.allow_tf32 = False
+        torch.backends.cuda.matmul.allow_tf32 = False
+    dnn.set_backend(a.kernels)
     dnn.set_native_conv(a.conv == "native" and not fp32)
     if a.wgrad_overlap_rows is not None:
         from distributed_learning_amd.ops import conv as nconv
@@ -346,7 +355,7 @@ def main():
     spec = get_spec(a.model)
     torch.manual_seed(1234)
     base = spec.build().to(dev)
-    if not fp32:
+    if not fp32_torch:
         base = base.to(memory_format=torch.channels_last)
     if bf16:
         dnn.bf16_weights(base)
@@ -390,7 +399,7 @@ def main():
     opt = FusedSGD(base.parameters(), lr=a.lr, momentum=a.momentum, master_weights=bf16)
     data = SyntheticBatches(a.batch, spec.input_shape, spec.num_classes, dev,
                             dtype=torch.bfloat16 if bf16 else torch.float32,
-                            seed=1234, rank=rank, channels_last=not fp32, device_step=a.graph == "on")
+                            seed=1234, rank=rank, channels_last=not fp32_torch, device_step=a.graph == "on")
     nstep = [0]
 
     def fwd_loss(x, y):
@@ -506,9 +515,10 @@ def main():
                 "bucket_mb": round(a.bucket_mb, 4),
                 "transport": engine.transport,
                 "same_device": same,
-                "kernels": "torch" if fp32 else a.kernels,
+                "kernels": a.kernels,
                 "precision": a.precision,
                 "conv1x1": "miopen" if fp32 else a.conv,
+                "layout": "nchw" if fp32_torch else "channels_last",
                 # 1x1 backward: both gradients in one pass over dY (gemm_dual.hip), the consuming BN's apply
                 # fused where served (ops/conv.py DUAL_*); what actually ran this process
                 "conv1x1_bwd": None if fp32 else {k: int(v) for k, v in _dual_calls().items()},
