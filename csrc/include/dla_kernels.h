@@ -360,6 +360,15 @@ void launch_stem_fwd(const void* xs, const void* wpk, void* y, int N, int H, int
 int stem_wgrad_splits(int N, int H, int W, int Cout);
 void launch_stem_wgrad(const void* dy, const void* xs, float* partial, int splits, void* dwpk, int out_dtype, int N,
                        int H, int W, int Cout, hipStream_t stream);
+// The stem weight gradient with the BatchNorm(+ReLU)+max-pool (3x3 / s2 / p1) backward APPLY computed on the fly
+// as its dY operand (stem.hip stem_wgrad_bn_kernel): dy_pool [N,OH,OW,64] and its argmax positions, x = the BN
+// input (the conv output [N,BH,BW,64], BH = (H + 1) / 2 = 2 OH), ws = the 7 x 64 coefficients the quad reduce +
+// finalize left (launch_bn_relu_maxpool_bwd with dx = nullptr). H, W: the stem INPUT image (as launch_stem_wgrad).
+bool stem_wgrad_bn_eligible(int N, int H, int W, int Cout, int OH, int OW);
+int stem_wgrad_bn_splits(int N, int H, int W);
+void launch_stem_wgrad_bn(const void* dy_pool, const uint8_t* pos, const void* x, const float* ws, const void* xs,
+                          float* partial, int splits, void* dwpk, int out_dtype, int N, int H, int W, int OH, int OW,
+                          hipStream_t stream);
 // Halo-tiled 64 -> 64 channel 3x3 / stride-1 weight gradient (conv_halo_wgrad.hip): persistent blocks over
 // a padded pixel space, x rows through an LDS ring; splits = partial slabs of [64][9][64] fp32.
 bool halo_wgrad_eligible(int Cin, int Cout, int W, int stride);

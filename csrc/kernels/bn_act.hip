@@ -1260,8 +1260,9 @@ void launch_bn_relu_maxpool_bwd(const void* dy_pool, const uint8_t* pos, const v
     const float* fp = bn_fold_rows(part, &nrb, C, stream);                                                            \
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<1>, dim3((C + 3) / 4), dim3(256), 0, stream, fp, nrb, M, C, gamma, ws, \
                        dgamma, dbeta);                                                                                \
-    hipLaunchKernelGGL(bn_pool_quad_apply_kernel<P_>, dim3(anct, anrb), dim3(kBNThreads), 0, stream, sq,             \
-                       (const bf16_t*)x, (const float*)ws, (bf16_t*)dx, Q, C, anrb, atpr);                            \
+    if (dx) /* dx null: reduce + finalize only; the stem weight gradient applies it (stem_wgrad_bn_kernel) */       \
+      hipLaunchKernelGGL(bn_pool_quad_apply_kernel<P_>, dim3(anct, anrb), dim3(kBNThreads), 0, stream, sq,           \
+                         (const bf16_t*)x, (const float*)ws, (bf16_t*)dx, Q, C, anrb, atpr);                          \
   }
     if (p == 1) DLA_QUAD(1) else DLA_QUAD(0)
 #undef DLA_QUAD

@@ -219,6 +219,228 @@ __global__ __launch_bounds__(kThreads, 2) void stem_wgrad_kernel(const bf16_t* _
   epilogue_f32<BM, BN>(acc, part + (int64_t)split * Cout * kStemK, Cout, kStemK, m0, n0);
 }
 
+// ---- fused backward: BN(+ReLU)+max-pool backward apply as the weight gradient's dY operand -------------------
+// The stem conv output's gradient dY is consumed by nothing but this weight gradient (the stem input is the data
+// batch), so instead of the quad apply pass writing dY (2 GB at batch 1280) and this GEMM reading it back, each
+// k-step computes its dY tile from what the apply would read: the conv output x, the pooled gradient and its
+// argmax window positions, and the finalized BN coefficients (bn_pool_quad_apply_kernel's arithmetic and bf16
+// rounding). The GEMM's K (pixels) runs in quad order -- k = 4 q + 2 dh + dw for the 2x2 quad q of conv-output
+// pixels -- which the sum over pixels does not care about: a 64-pixel k-step is 16 quads, and one thread turns the
+// 4 pooled windows covering its quad (for 8 channels) into the 4 pixels' dY values, as the quad apply does.
+//   A (dY)  [64 px][64 co] k-major: all threads, quad tid / 16, channels (tid % 16) * 4
+//   B (im2col of xs) [64 px][256 k] k-major: all threads, 8 chunks each = 128 contiguous bytes of xs
+// Register-staged: the next k-step's raw loads are in flight during this k-step's MFMAs; the dY arithmetic runs
+// between the MFMAs and the LDS stores. One fp32 [64][256] partial per split, summed by splitk_reduce.
+namespace {
+
+constexpr int kSBCo = 64;  // stem output channels served
+
+struct StemBnArgs {
+  const bf16_t* dyp;
+  const uint8_t* pos;
+  const bf16_t* x;
+  const float* ws;
+  const bf16_t* xs;
+  float* part;
+  int N, H, W, OH, OW;  // conv output (= folded image) and pooled sizes
+  FastDiv fQW, fQH;     // quads per row (W / 2), quad rows (H / 2)
+  int64_t Q;            // quads
+  int ksteps, kps;      // 16-quad k-steps in all, per split
+};
+
+struct KMajorTag {
+  static constexpr bool kKMajor = true;
+  static constexpr int kNT = kThreads;
+};
+
+__device__ __forceinline__ void quad_decode(const StemBnArgs& s, int64_t q, int& n, int& j, int& i) {
+  const uint32_t r = fdiv((uint32_t)q, s.fQW);
+  i = (int)q - (int)r * (s.W >> 1);
+  const uint32_t nn = fdiv(r, s.fQH);
+  j = (int)r - (int)nn * (s.H >> 1);
+  n = (int)nn;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kThreads, 2) void stem_wgrad_bn_kernel(const StemBnArgs s) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem_raw);  // [64 px][64 co] k-major image
+  bf16_t* Bs = As + kBK * kSBCo;                      // [64 px][256 k] k-major image
+  using AC = Acc<kSBCo, kStemK>;
+  constexpr int TM = AC::TM, TN = AC::TN, WM = AC::WM, WN = AC::WN;
+  const int tid = threadIdx.x, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN;
+  const int split = blockIdx.x;
+  const int kb = split * s.kps, ke = min(s.ksteps, kb + s.kps);
+  const int C = kSBCo;
+
+  // A role: quad qi of the k-step, channels c0 .. c0 + 3 (four channels keep the dY registers within budget
+  // next to the 64-float accumulator and the eight staged im2col chunks)
+  const int qi = tid >> 4, c0 = (tid & 15) * 4;
+  float mean[4], sc[4], sh[4], k1[4], m1[4], k2[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    mean[e] = s.ws[c0 + e];
+    sc[e] = s.ws[2 * C + c0 + e];
+    sh[e] = s.ws[3 * C + c0 + e];
+    k1[e] = s.ws[4 * C + c0 + e];
+    m1[e] = s.ws[5 * C + c0 + e];
+    k2[e] = s.ws[6 * C + c0 + e];
+  }
+  // B role: k-row (pixel) r = tid / 4 = quad qi, pixel sub = (tid / 4) % 4 of it (the A role's quad), filter row
+  // th = tid % 4: its 8 chunks are the 64 columns th * 64 .. +63 = taps tw 0..3 x channel halves, i.e. the 4
+  // consecutive folded pixels (ih, iw0 .. iw0 + 3): 128 contiguous bytes, one row test and one column test per tw
+  const int br = tid >> 2, bsub = br & 3, bth = tid & 3;
+  const int bdh = bth - 2 + (bsub >> 1), bdw = (bsub & 1) - 2;
+  // ds_write_b128 banks are (a / 4) mod 32 in groups of 8 lanes = 2 k-rows x 4 filter rows: the filter rows'
+  // 64-column offsets vanish mod 128 B, so each stores its chunks in its own order (chunk u ^ bsw at
+  // instruction u; bits 0 and 2, the row pair's swizzle differs in bit 1): 8 distinct 16-B slots per group
+  const int bsw = (bth & 1) | ((bth >> 1) << 2);
+
+  // buffer loads: an out-of-range operand (past the batch, conv padding) reads as zeros via an offset past
+  // num_records (kOOB) instead of an exec-masked branch; every tensor is < 2 GiB (stem_wgrad_bn_eligible)
+  const __amdgpu_buffer_rsrc_t srx = make_srd(s.x, (uint32_t)(s.Q * 4 * C * 2));
+  const __amdgpu_buffer_rsrc_t srs = make_srd(s.xs, (uint32_t)((int64_t)s.N * s.H * s.W * kStemC * 2));
+  ushort4_t rx[4], rd[4];
+  ushort8_t rb[8];
+  uint32_t rp[4];
+  bool wok[4];
+  bool qok = false;
+  auto issue = [&](int t) {
+    const int64_t q = (int64_t)t * 16 + qi;
+    qok = q < s.Q;
+    int n, j, i;
+    quad_decode(s, qok ? q : 0, n, j, i);
+    const uint32_t px = (uint32_t)(((n * s.H + 2 * j) * s.W + 2 * i) * C + c0) * 2u;  // bytes, < 2^31
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const uint32_t o = px + (uint32_t)(((p >> 1) * s.W + (p & 1)) * C * 2);
+      rx[p] = __builtin_bit_cast(ushort4_t, __builtin_amdgcn_raw_buffer_load_b64(srx, qok ? o : kOOB, 0, 0));
+    }
+    // pooled windows (j + a, i + b) cover the quad (pad 1); OH = H / 2, so only the far ones can fall outside
+    const bool aok = j + 1 < s.OH, bok = i + 1 < s.OW;
+    const int64_t pw0 = ((int64_t)n * s.OH + j) * s.OW + i;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const bool in = (!(w >> 1) || aok) && (!(w & 1) || bok);
+      wok[w] = qok && in;
+      const int64_t o = (in ? pw0 + (w >> 1) * s.OW + (w & 1) : pw0) * C + c0;
+      rp[w] = *reinterpret_cast<const uint32_t*>(s.pos + o);
+      rd[w] = *reinterpret_cast<const ushort4_t*>(s.dyp + o);
+    }
+    const int ih = 2 * j + bdh, iw0 = 2 * i + bdw;
+    const bool rok = qok && (unsigned)ih < (unsigned)s.H;
+    const int pix0 = (n * s.H + ih) * s.W + iw0;  // may be negative: only used where the tests pass
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {  // register u holds chunk u ^ bsw (see the LDS store)
+      const int c = u ^ bsw;
+      const bool ok = rok && (unsigned)(iw0 + (c >> 1)) < (unsigned)s.W;
+      const uint32_t o = (uint32_t)(pix0 * kStemC + c * 8) * 2u;
+      rb[u] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(srs, ok ? o : kOOB, 0, 0));
+    }
+  };
+  Acc<kSBCo, kStemK> acc;
+  acc.zero();
+  if (kb < ke) issue(kb);
+  for (int t = kb; t < ke; ++t) {
+    // dY of the quad's 4 pixels: g = sum of the pooled gradients whose argmax is the pixel, the forward's ReLU
+    // recomputed from x, then bn_pool_quad_apply_kernel's k1 (g - m1 - (x - mean) k2)
+    ushort4_t av[4];
+    {
+      float g[4][4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[p][e] = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+          for (int dw = 0; dw < 2; ++dw) {
+            const int ky = dh - 2 * (w >> 1) + 1, kx = dw - 2 * (w & 1) + 1;
+            if (ky < 0 || kx < 0) continue;  // compile-time after unrolling
+            const uint32_t tap = wok[w] ? (uint32_t)(ky * 3 + kx) : 0xffu;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t byte = (rp[w] >> (8 * e)) & 0xffu;
+              g[dh * 2 + dw][e] += byte == tap ? bf16_to_f32((bf16_t)rd[w][e]) : 0.f;
+            }
+          }
+      // past the last quad: x and the window gradients read as zeros, and a zero k1 zeroes dY (branch-free)
+      float kq[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) kq[e] = qok ? k1[e] : 0.f;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xv = bf16_to_f32((bf16_t)rx[p][e]);
+          const float gg = fmaf(xv, sc[e], sh[e]) > 0.f ? g[p][e] : 0.f;
+          av[p][e] = f32_to_bf16(kq[e] * (gg - m1[e] - (xv - mean[e]) * k2[e]));
+        }
+      }
+    }
+    __syncthreads();  // the previous k-step's fragment reads are done
+#pragma unroll
+    for (int p = 0; p < 4; ++p) *reinterpret_cast<ushort4_t*>(As + tr_off<kSBCo>(qi * 4 + p, c0)) = av[p];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) *reinterpret_cast<ushort8_t*>(Bs + tr_off<kStemK>(br, bth * 64 + (u ^ bsw) * 8)) = rb[u];
+    __syncthreads();
+    if (t + 1 < ke) issue(t + 1);  // in flight during the MFMAs
+#pragma unroll
+    for (int kk = 0; kk < kBK / kKS; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = tile_frag<kSBCo, KMajorTag>(As, wr * WM + i * kMS, kk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = tile_frag<kStemK, KMajorTag>(Bs, wc * WN + j * kMS, kk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
+    }
+  }
+  epilogue_f32<kSBCo, kStemK>(acc, s.part + (int64_t)split * kSBCo * kStemK, kSBCo, kStemK, 0, 0);
+}
+
+bool stem_wgrad_bn_eligible(int N, int H, int W, int Cout, int OH, int OW) {
+  const int BH = (H + 1) / 2, BW = (W + 1) / 2;  // conv output = folded image
+  return Cout == kSBCo && BH % 2 == 0 && BW % 2 == 0 && OH == BH / 2 && OW == BW / 2 &&
+         (int64_t)N * BH * BW < (1 << 24);
+}
+
+int stem_wgrad_bn_splits(int N, int H, int W) {
+  const int64_t Q = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) / 4;
+  const int ks = (int)((Q + 15) / 16);
+  return std::max(1, std::min(2 * 256, ks));  // two blocks per CU
+}
+
+void launch_stem_wgrad_bn(const void* dy_pool, const uint8_t* pos, const void* x, const float* ws, const void* xs,
+                          float* partial, int splits, void* dwpk, int out_dtype, int N, int H, int W, int OH, int OW,
+                          hipStream_t stream) {
+  StemBnArgs s{};
+  s.dyp = (const bf16_t*)dy_pool;
+  s.pos = pos;
+  s.x = (const bf16_t*)x;
+  s.ws = ws;
+  s.xs = (const bf16_t*)xs;
+  s.part = partial;
+  s.N = N;
+  s.H = (H + 1) / 2;
+  s.W = (W + 1) / 2;
+  s.OH = OH;
+  s.OW = OW;
+  s.fQW = make_fastdiv((uint32_t)(s.W / 2));
+  s.fQH = make_fastdiv((uint32_t)(s.H / 2));
+  s.Q = (int64_t)N * (s.H / 2) * (s.W / 2);
+  s.ksteps = (int)((s.Q + 15) / 16);
+  s.kps = (s.ksteps + splits - 1) / splits;
+  const size_t lds = (size_t)(kBK * kSBCo + kBK * kStemK) * sizeof(bf16_t);
+  hipLaunchKernelGGL(stem_wgrad_bn_kernel, dim3(splits), dim3(kThreads), lds, stream, s);
+  launch_splitk_reduce(partial, splits, (int64_t)kSBCo * kStemK, dwpk, out_dtype, 1.f, false, stream);
+}
+
 static StemGeom make_stem_geom(int N, int H, int W) {
   StemGeom g;
   g.N = N;

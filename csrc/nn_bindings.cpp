@@ -738,7 +738,8 @@ std::vector<at::Tensor> bn_relu_maxpool_fwd(at::Tensor x, c10::optional<at::Tens
 
 // Returns (dx, dgamma, dbeta) of the fused stem op, gathering dy from the pooled gradient.
 std::vector<at::Tensor> bn_relu_maxpool_bwd(at::Tensor dy_pool, at::Tensor pos, at::Tensor x, at::Tensor ws,
-                                            c10::optional<at::Tensor> weight, int64_t k, int64_t s, int64_t p) {
+                                            c10::optional<at::Tensor> weight, int64_t k, int64_t s, int64_t p,
+                                            bool want_dx) {
   dy_pool = dy_pool.contiguous(at::MemoryFormat::ChannelsLast).to(at::kBFloat16);
   check_act(x, "x");
   TORCH_CHECK(pos.scalar_type() == at::kByte && pos.sizes() == dy_pool.sizes() &&
@@ -749,10 +750,16 @@ std::vector<at::Tensor> bn_relu_maxpool_bwd(at::Tensor dy_pool, at::Tensor pos, 
   const int64_t M = (int64_t)N * H * W;
   auto f32 = x.options().dtype(at::kFloat);
   at::Tensor part = at::empty({bn_relu_maxpool_part_floats(M, C)}, f32);
-  at::Tensor dx = at::empty_like(x);
+  // want_dx false: the quad reduce + finalize only (ws then holds the backward coefficients); the stem weight
+  // gradient applies them itself (stem_wgrad_bn). Only the quad form (3x3 / s2, even input, OH = H / 2) stops there.
+  TORCH_CHECK(want_dx || (k == 3 && s == 2 && (p == 0 || p == 1) && H % 2 == 0 && W % 2 == 0 && OH == H / 2 &&
+                          OW == W / 2),
+              "bn_relu_maxpool_bwd: want_dx=False needs the quad form (3x3 / stride 2, even input)");
+  at::Tensor dx = want_dx ? at::empty_like(x) : at::Tensor();
   at::Tensor dg = at::empty({C}, f32), db = at::empty({C}, f32);
   const float* g = (weight.has_value() && weight->defined()) ? weight->data_ptr<float>() : nullptr;
-  launch_bn_relu_maxpool_bwd(dy_pool.data_ptr(), pos.data_ptr<uint8_t>(), x.data_ptr(), dx.data_ptr(), N, H, W, C, OH,
+  launch_bn_relu_maxpool_bwd(dy_pool.data_ptr(), pos.data_ptr<uint8_t>(), x.data_ptr(),
+                             want_dx ? dx.data_ptr() : nullptr, N, H, W, C, OH,
                              OW, (int)k, (int)s, (int)p, g, ws.data_ptr<float>(), part.data_ptr<float>(),
                              dg.data_ptr<float>(), db.data_ptr<float>(), current_stream(x));
   return {dx, dg, db};
@@ -818,6 +825,39 @@ std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor wpk, bool want_stats) 
   launch_stem_fwd(xs.data_ptr(), wpk.data_ptr(), y.data_ptr(), N, H, W, Cout,
                   want_stats ? stats.data_ptr<float>() : nullptr, current_stream(x));
   return {y, stats, xs};
+}
+
+// The stem weight gradient with the stem BN+ReLU+max-pool backward apply fused (stem.hip stem_wgrad_bn_kernel):
+// dy_pool / pos from the pooled op, x = the conv output (the BN input), ws = the coefficients a
+// bn_relu_maxpool_bwd(..., want_dx=False) finalized. The conv output's gradient is never materialised.
+at::Tensor stem_wgrad_bn(at::Tensor dy_pool, at::Tensor pos, at::Tensor x, at::Tensor ws, at::Tensor xs, int64_t H,
+                         int64_t W, c10::ScalarType out_dtype) {
+  dy_pool = dy_pool.contiguous(at::MemoryFormat::ChannelsLast).to(at::kBFloat16);
+  check_act(x, "x");
+  check_act(dy_pool, "dy_pool");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 4, "stem_wgrad_bn: x must be the bf16 conv output");
+  TORCH_CHECK(pos.scalar_type() == at::kByte && pos.sizes() == dy_pool.sizes() &&
+                  pos.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_wgrad_bn: pos must be the pooled op's positions");
+  TORCH_CHECK(xs.is_cuda() && xs.dim() == 4 && xs.size(3) == 16 && xs.scalar_type() == at::kBFloat16 &&
+                  xs.is_contiguous(),
+              "stem_wgrad_bn: xs must be the forward's folded [N, OH, OW, 16] input");
+  const int N = (int)x.size(0), Cout = (int)x.size(1), OH = (int)dy_pool.size(2), OW = (int)dy_pool.size(3);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() == 7 * (int64_t)Cout,
+              "stem_wgrad_bn: ws must be the 7C workspace");
+  TORCH_CHECK(xs.size(0) == N && xs.size(1) == (H + 1) / 2 && xs.size(2) == (W + 1) / 2 && x.size(2) == xs.size(1) &&
+                  x.size(3) == xs.size(2) && dy_pool.size(0) == N && dy_pool.size(1) == Cout,
+              "stem_wgrad_bn: x / xs / dy_pool / image size mismatch");
+  TORCH_CHECK(stem_wgrad_bn_eligible(N, (int)H, (int)W, Cout, OH, OW),
+              "stem_wgrad_bn: needs 64 channels, an even conv output and a 3x3 / s2 / p1 pool");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "stem_wgrad_bn: fp32/bf16 output");
+  const int splits = stem_wgrad_bn_splits(N, (int)H, (int)W);
+  at::Tensor part = at::empty({(int64_t)splits * Cout * 256}, xs.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({Cout, 256}, xs.options().dtype(out_dtype));
+  launch_stem_wgrad_bn(dy_pool.data_ptr(), pos.data_ptr<uint8_t>(), x.data_ptr(), ws.data_ptr<float>(), xs.data_ptr(),
+                       part.data_ptr<float>(), splits, dw.data_ptr(), out_dtype == at::kFloat ? kF32 : kBF16, N,
+                       (int)H, (int)W, OH, OW, current_stream(xs));
+  return dw;
 }
 
 at::Tensor stem_wgrad(at::Tensor dy, at::Tensor xs, int64_t H, int64_t W, c10::ScalarType out_dtype) {
@@ -1042,7 +1082,9 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("running_var"), pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("k"),
         pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("stats") = pybind11::none(),
         pybind11::arg("ceil_mode") = false);
-  m.def("bn_relu_maxpool_bwd", &bn_relu_maxpool_bwd, "stem BN+ReLU+max-pool backward (dy gathered from the pool)");
+  m.def("bn_relu_maxpool_bwd", &bn_relu_maxpool_bwd, "stem BN+ReLU+max-pool backward (dy gathered from the pool)",
+        pybind11::arg("dy_pool"), pybind11::arg("pos"), pybind11::arg("x"), pybind11::arg("ws"), pybind11::arg("weight"),
+        pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("want_dx") = true);
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC max pooling forward (+ argmax window positions)", pybind11::arg("x"),
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("ceil_mode") = false,
         pybind11::arg("need_pos") = true);
@@ -1054,6 +1096,8 @@ void bind_nn(pybind11::module& m) {
   m.def("gap_fwd", &gap_fwd, "NHWC global average pooling -> [N, C]");
   m.def("subsample2", &subsample2, "x[:, :, ::2, ::2] of a channels_last bf16 tensor, compact channels_last");
   m.def("stem_fwd", &stem_fwd, "7x7/s2/p3 stem conv, 3 input channels (space-to-depth + MFMA implicit GEMM, BN-statistics epilogue)");
+  m.def("stem_wgrad_bn", &stem_wgrad_bn,
+        "stem weight gradient with the BN+ReLU+max-pool backward apply fused (the conv-output gradient never stored)");
   m.def("stem_wgrad", &stem_wgrad, "7x7/s2/p3 stem conv weight gradient from the folded input (packed [Cout, 256] layout)");
   m.def("gap_bwd", &gap_bwd, "NHWC global average pooling backward (channels_last dx)");
   m.def("gemm_nt", &gemm_nt, "C = A @ B^T (bf16 MFMA), optional fused column statistics", pybind11::arg("A"),

@@ -42,6 +42,8 @@ TABLE: Dict[str, Knob] = {
     "WGRAD_DEFER_MIN_AI": Knob("200", "ops/conv.py", "WGRAD_DEFER=auto: 1x1 arithmetic-intensity threshold"),
     "BN_EPILOGUE": Knob("0", "ops/conv.py", "1 / stream: BN-backward partials in every / the streaming dgrad "
                                             "GEMM epilogue (profiles/r4/g02/, bn_epilogue_ab_bs512.jsonl)"),
+    "STEM_BN": Knob("1", "ops/conv.py", "0: stem BN+ReLU+max-pool backward apply as its own pass, not inside the "
+                                        "stem weight gradient (profiles/r5/g11/)"),
     # ---- GoogLeNet Inception fusions ---------------------------------------------------------------
     "BN_GROUPED": Knob("1", "ops/inception.py", "0: one BN launch chain per Inception branch (profiles/r3p/)"),
     "FANIN_CAT": Knob("1", "ops/inception.py", "0: three separate fan-in 1x1 GEMMs (profiles/r3y/)"),

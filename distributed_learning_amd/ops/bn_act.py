@@ -243,21 +243,34 @@ class _BNReluPool(torch.autograd.Function):
     activation and its gradient are never materialised."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p, stats=None, ceil=False):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p, stats=None, ceil=False,
+                slink=None):
         C = _ext.require()
         y, ws, pos = C.bn_relu_maxpool_fwd(x, weight, bias, running_mean, running_var, momentum, eps, k, s, p,
                                            stats, ceil)
         ctx.save_for_backward(x, ws, weight, pos)
         ctx.geom = (k, s, p)
+        # the producing stem conv applies this op's backward inside its weight gradient (ops/conv.py StemBNLink)
+        from .conv import stem_bn_fusable
+
+        ok = slink is not None and stem_bn_fusable(x, y.shape, k, s, p) and slink.claim()
+        ctx.slink = slink if ok else None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, ws, weight, pos = ctx.saved_tensors
         k, s, p = ctx.geom
-        dx, dg, db = _ext.require().bn_relu_maxpool_bwd(dy, pos, x, ws, weight, k, s, p)
         need = ctx.needs_input_grad
-        return dx, dg if need[1] else None, db if need[2] else None, None, None, None, None, None, None, None, None, None
+        C = _ext.require()
+        if ctx.slink is not None and ctx.slink.can_park(x):
+            # reduction + finalize only (ws then holds the backward coefficients); the stem weight gradient applies
+            dy = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
+            _, dg, db = C.bn_relu_maxpool_bwd(dy, pos, x, ws, weight, k, s, p, want_dx=False)
+            dx = ctx.slink.park(dy, pos, x, ws, weight, ctx.geom)
+        else:
+            dx, dg, db = C.bn_relu_maxpool_bwd(dy, pos, x, ws, weight, k, s, p)
+        return (dx, dg if need[1] else None, db if need[2] else None) + (None,) * 10
 
 
 def fused_bn_relu_maxpool(x: torch.Tensor, bn: nn.BatchNorm2d, pool: nn.MaxPool2d, stats=None):
@@ -279,4 +292,4 @@ def fused_bn_relu_maxpool(x: torch.Tensor, bn: nn.BatchNorm2d, pool: nn.MaxPool2
     if bn.track_running_stats:
         _PENDING_COUNTERS.append(bn.num_batches_tracked)
     return _BNReluPool.apply(x, bn.weight, bn.bias, rm, rv, float(bn.momentum), float(bn.eps), k, s, p, stats,
-                             bool(pool.ceil_mode))
+                             bool(pool.ceil_mode), getattr(x, "_dla_stem", None))

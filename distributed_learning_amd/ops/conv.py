@@ -655,6 +655,47 @@ def stem_unpack_grad(dwp: torch.Tensor) -> torch.Tensor:
     return g[:, :, 1:, 1:]
 
 
+# The stem BN+ReLU+max-pool backward apply inside the stem weight gradient (stem.hip stem_wgrad_bn_kernel): the
+# conv output's gradient (2 GB at batch 1280) is never written or read back.
+STEM_BN = knobs.flag("STEM_BN")
+
+
+class StemBNLink(DualBNLink):
+    """Hand-off from the stem BN+ReLU+max-pool (ops/bn_act.py _BNReluPool) to the stem conv's backward.
+
+    The pooled op's backward stops after its reduction + finalize, parks (pooled gradient, argmax positions,
+    conv output, coefficients) here and returns a zero-stride placeholder; the stem weight gradient computes the
+    conv output's gradient tile by tile from them. Same claim / observed guards as DualBNLink; a non-placeholder
+    gradient (other consumers of the conv output) materialises the parked gradient and adds it."""
+
+    __slots__ = ("pos", "geom")
+
+    def park(self, dout, pos, ybn, ws, weight, geom):
+        assert self.can_park(ybn), "StemBNLink.park: check can_park first"
+        self.dout, self.pos, self.ybn, self.ws, self.weight, self.geom = dout, pos, ybn, ws, weight, geom
+        self.ph = torch.zeros((), dtype=ybn.dtype, device=ybn.device).expand(ybn.shape)
+        return self.ph
+
+    def take(self):
+        out = (self.ph, self.dout, self.pos, self.ybn, self.ws, self.weight, self.geom)
+        self.ph = self.dout = self.pos = self.ybn = self.ws = self.weight = self.geom = None
+        return out
+
+    def materialise(self, C, dy, parked):
+        ph, dout, pos, ybn, ws, weight, (k, s, p) = parked
+        dbn = C.bn_relu_maxpool_bwd(dout, pos, ybn, ws, weight, k, s, p)[0]  # reduction re-run: same ws
+        is_ph = dy is not None and dy.data_ptr() == ph.data_ptr() and dy.stride() == ph.stride()
+        return dbn if (dy is None or is_ph) else dy + dbn
+
+
+def stem_bn_fusable(x: torch.Tensor, y_shape, k: int, s: int, p: int) -> bool:
+    """Whether the stem conv output ``x`` pooled 3x3 / s2 / p1 to ``y_shape`` is the quad form stem_wgrad_bn
+    serves (64 channels, even size, pooled to exactly half; < 2^24 pixels)."""
+    n, c, h, w = x.shape
+    return (k == 3 and s == 2 and p == 1 and c == 64 and h % 2 == 0 and w % 2 == 0
+            and tuple(y_shape[2:]) == (h // 2, w // 2) and n * h * w < (1 << 24))
+
+
 class _StemConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, want_stats: bool):
@@ -662,6 +703,7 @@ class _StemConv(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         y, stats, xs = C.stem_fwd(x, stem_pack_weight(weight), want_stats)
         ctx.save_for_backward(xs)
+        ctx.slink = StemBNLink() if STEM_BN and y.dtype == torch.bfloat16 else None
         ctx.hw = (x.shape[2], x.shape[3])
         ctx.wdtype = weight.dtype
         ctx.wfmt = torch.channels_last if weight.is_contiguous(memory_format=torch.channels_last) and \
@@ -678,6 +720,19 @@ class _StemConv(torch.autograd.Function):
             raise RuntimeError("native stem conv: no input gradient (the stem input is the data batch)")
         (xs,) = ctx.saved_tensors
         dw = None
+        sl = ctx.slink
+        if sl is not None and sl.ph is not None:
+            parked = sl.take()
+            ph, dout, pos, ybn, ws = parked[:5]
+            if not ctx.needs_input_grad[1]:
+                return None, None, None
+            if dy.data_ptr() == ph.data_ptr() and dy.stride() == ph.stride():
+                odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
+                CALLS["stem_bn"] += 1
+                dwp = _ext.require().stem_wgrad_bn(dout, pos, ybn, ws, xs, ctx.hw[0], ctx.hw[1], odt)
+                dw = stem_unpack_grad(dwp).to(ctx.wdtype).contiguous(memory_format=ctx.wfmt)
+                return None, dw, None
+            dy = sl.materialise(_ext.require(), dy, parked)
         if ctx.needs_input_grad[1]:
             odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
             dwp = _ext.require().stem_wgrad(dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16), xs,
@@ -690,5 +745,9 @@ def stem_conv(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False):
     """The ResNet stem conv on the native kernels. Returns (y, stats-or-None); stats are the
     [row_blocks, Cout, 2] (sum, sumsq) partials of y for the fused BatchNorm."""
     CALLS["stem"] += 1
-    return _StemConv.apply(x, conv.weight, want_stats)
+    y, stats = _StemConv.apply(x, conv.weight, want_stats)
+    sl = getattr(y.grad_fn, "slink", None) if y.grad_fn is not None else None
+    if sl is not None:
+        y._dla_stem = sl
+    return y, stats
 
