@@ -36,6 +36,9 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
 }
 
 constexpr int kThreads = 256;
+#ifndef DLA_KSTEP_PRE_FRAGS
+#define DLA_KSTEP_PRE_FRAGS 0  // kstep_mfma: fragment budget (both halves) for the pipelined form; 0 = off (r5 g18: 16 measured no faster)
+#endif
 constexpr int kBK = 64;
 
 // GEMM epilogues load their addends for all of a thread's rows before the store loop (1), or per row
@@ -571,6 +574,55 @@ __device__ __forceinline__ const void* loader_src(const L& l, int i, int k0, lon
 // terms are hoisted (loader_step), and each MFMA cluster runs at s_setprio 1 so a co-resident
 // wave's VALU/DMA issue does not preempt it (cdna_hip_programming.md T5). Same LDS images, same
 // counted-vmcnt + raw-barrier protocol as mainloop_glds.
+// The MFMAs of one staged k-step (kBK / kKS = 2 halves). s_setprio is a scheduling barrier, so the
+// plain form (read half kk's fragments, wait, MFMAs) exposes the LDS latency of every half to a wave
+// that has no other wave on its SIMD to cover it; where both halves' fragments fit (kPre), half 1's
+// reads are issued before half 0's MFMAs (counted lgkmcnt: half 0 waits only for its own reads).
+// mid() runs between the halves (the B-operand DMA of a later stage).
+template <int BM, int BN, int NT, class LA, class LB, class Mid>
+__device__ __forceinline__ void kstep_mfma(const bf16_t* As, const bf16_t* Bs, int wr, int wc, Acc<BM, BN, NT>& acc,
+                                           Mid&& mid) {
+  using AC = Acc<BM, BN, NT>;
+  constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN, KK = kBK / kKS;
+  constexpr bool kPre = (TM + TN) * KK <= DLA_KSTEP_PRE_FRAGS;
+  if constexpr (kPre) {
+    bf16x8_t af[KK][TM], bfr[KK][TN];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[kk][i] = glds_frag<BM, LA>(As, wr * WM + i * kMS, kk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[kk][j] = glds_frag<BN, LB>(Bs, wc * WN + j * kMS, kk);
+    }
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[kk][i], bfr[kk][j], acc.v[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      if (kk == 0) mid();
+    }
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = glds_frag<BM, LA>(As, wr * WM + i * kMS, kk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag<BN, LB>(Bs, wc * WN + j * kMS, kk);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      if (kk == 0) mid();
+    }
+  }
+}
+
 template <int BM, int BN, int NT, int NS, class LA, class LB>
 __device__ __forceinline__ void mainloop_glds2(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
                                                char* smem) {
@@ -626,21 +678,9 @@ __device__ __forceinline__ void mainloop_glds2(const LA& la, const LB& lb, int k
     if (more) issue_a(t + NS - 1);
     const bf16_t* As = base + (t % NS) * (SA + SB);
     const bf16_t* Bs = As + SA;
-#pragma unroll
-    for (int kk = 0; kk < kBK / kKS; ++kk) {
-      bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = glds_frag<BM, LA>(As, wr * WM + i * kMS, kk);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag<BN, LB>(Bs, wc * WN + j * kMS, kk);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-      if (kk == 0 && more) issue_b(t + NS - 1);
-    }
+    kstep_mfma<BM, BN, NT, LA, LB>(As, Bs, wr, wc, acc, [&] {
+      if (more) issue_b(t + NS - 1);
+    });
   }
   __syncthreads();  // every wave done with the stages before the epilogue reuses the LDS
 }
@@ -715,21 +755,9 @@ __device__ __forceinline__ void mainloop_bglds(const LA& la, const LB& lb, int k
     if (more) issue_a(t + NS - 1);
     const bf16_t* As = base + (t % NS) * (SA + SB);
     const bf16_t* Bs = As + SA;
-#pragma unroll
-    for (int kk = 0; kk < kBK / kKS; ++kk) {
-      bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = glds_frag<BM, LA>(As, wr * WM + i * kMS, kk);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag<BN, LB>(Bs, wc * WN + j * kMS, kk);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-      if (kk == 0 && more) issue_b(t + NS - 1);
-    }
+    kstep_mfma<BM, BN, NT, LA, LB>(As, Bs, wr, wc, acc, [&] {
+      if (more) issue_b(t + NS - 1);
+    });
   }
   __syncthreads();  // every wave done with the stages before the epilogue reuses the LDS
 }

@@ -129,32 +129,39 @@ __global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __r
     const char* pbuf = patch0 + b * kHPatchBytes;
     AC acc;
     acc.zero();
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
+    // 18 steps (tap t, k-half kk), software-pipelined: step u + 1's fragments are read before step u's
+    // MFMAs issue. With one wave per SIMD nothing else covers the LDS latency, and s_setprio is a
+    // scheduling barrier, so without this every step waited for its own reads (ISA: reads, wait, 8 MFMAs)
+    constexpr int kSteps = 9 * (kBK / kKS);
+    auto load_step = [&](int u, bf16x8_t (&af)[AC::TM], bf16x8_t (&bfr)[AC::TN]) {
+      const int t = u / (kBK / kKS), kk = u % (kBK / kKS);
       const int off = (t / 3) * W + (t % 3);
       const bf16_t* wt = reinterpret_cast<const bf16_t*>(wimg + t * kHTapImg * 2);
+      // fragment i reads patch pixel wr * 64 + i * 16 + (lane & 15) + off: the chunk swizzle
+      // (pixel & 7) does not depend on i, so every fragment is one base address plus an immediate
+      // offset of i * 2 KB; a padding tap selects a base that lands on the zero slot instead
+      const int sp0 = wr * AC::WM + (lane & 15) + off;
+      const char* a0 = pbuf + sp0 * 128 + (((kk * 4 + (lane >> 4)) ^ hswz(sp0)) << 4);
 #pragma unroll
-      for (int kk = 0; kk < kBK / kKS; ++kk) {
-        bf16x8_t af[AC::TM], bfr[AC::TN];
-        // fragment i reads patch pixel wr * 64 + i * 16 + (lane & 15) + off: the chunk swizzle
-        // (pixel & 7) does not depend on i, so every fragment is one base address plus an immediate
-        // offset of i * 2 KB; a padding tap selects a base that lands on the zero slot instead
-        const int sp0 = wr * AC::WM + (lane & 15) + off;
-        const char* a0 = pbuf + sp0 * 128 + (((kk * 4 + (lane >> 4)) ^ hswz(sp0)) << 4);
-#pragma unroll
-        for (int i = 0; i < AC::TM; ++i) {
-          const char* base = ((vmask[i] >> t) & 1u) ? a0 : zfrag - i * 2048;
-          af[i] = *reinterpret_cast<const bf16x8_t*>(base + i * 2048);
-        }
-#pragma unroll
-        for (int j = 0; j < AC::TN; ++j) bfr[j] = rm_glds_frag(wt, wc * AC::WN + j * 16, kk);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < AC::TM; ++i)
-#pragma unroll
-          for (int j = 0; j < AC::TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
-        __builtin_amdgcn_s_setprio(0);
+      for (int i = 0; i < AC::TM; ++i) {
+        const char* base = ((vmask[i] >> t) & 1u) ? a0 : zfrag - i * 2048;
+        af[i] = *reinterpret_cast<const bf16x8_t*>(base + i * 2048);
       }
+#pragma unroll
+      for (int j = 0; j < AC::TN; ++j) bfr[j] = rm_glds_frag(wt, wc * AC::WN + j * 16, kk);
+    };
+    bf16x8_t af[2][AC::TM], bfr[2][AC::TN];
+    load_step(0, af[0], bfr[0]);
+#pragma unroll
+    for (int u = 0; u < kSteps; ++u) {
+      const int cb = u & 1;
+      if (u + 1 < kSteps) load_step(u + 1, af[cb ^ 1], bfr[cb ^ 1]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < AC::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < AC::TN; ++j) acc.v[i][j] = mfma(af[cb][i], bfr[cb][j], acc.v[i][j]);
+      __builtin_amdgcn_s_setprio(0);
     }
     ColStats<kHBM, kHC, kHNT> st;
     st.zero();
