@@ -247,7 +247,11 @@ class DualBNLink:
     the same conv output runs the normal path, so no parked gradient can be overwritten. And park()
     is refused (can_park False: the BN computes its input gradient itself) when anything else observes the
     conv output's gradient -- a tensor hook or retain_grad() on it -- since that observer would see the
-    placeholder's zeros."""
+    placeholder's zeros. Not detectable from inside the backward: ``torch.autograd.grad(..., inputs=[y])``
+    with the conv output itself as an input (the engine captures the placeholder; its introspection,
+    ``torch._C._will_engine_execute_node``, reports the producing node as executed either way). Code that
+    differentiates with respect to a conv output turns the hand-offs off (``DUAL_BN`` / ``STEM_BN`` here,
+    ``DLA_STEM_BN=0``) or registers a hook on it."""
 
     __slots__ = ("ph", "dout", "ybn", "ws", "mask", "weight", "mode", "claimed")
 
