@@ -263,23 +263,27 @@ __device__ __forceinline__ void quad_decode(const StemBnArgs& s, int64_t q, int&
 
 }  // namespace
 
-__global__ __launch_bounds__(kThreads, 2) void stem_wgrad_bn_kernel(const StemBnArgs s) {
+// 8 waves per block (2 blocks per CU: four waves per SIMD to cover the loads' latency; the 4-wave form held
+// 226 VGPRs, two waves per SIMD, and waited on memory: profiles/r5/g11): wave (wr, wc) owns output channels
+// 32 wr .. + 31 x GEMM columns 64 wc .. + 63 (TM = 2, TN = 4). A role: quad tid / 32, channels (tid % 32) * 2;
+// B role: k-row tid / 8 (that quad's pixel (tid / 8) % 4), filter row th = (tid % 8) / 2, half-run hs = tid % 2:
+// taps 2 hs, 2 hs + 1 x 2 channel halves = 64 contiguous bytes of xs.
+constexpr int kSBNT = 512;
+__global__ __launch_bounds__(kSBNT, 4) void stem_wgrad_bn_kernel(const StemBnArgs s) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem_raw);  // [64 px][64 co] k-major image
   bf16_t* Bs = As + kBK * kSBCo;                      // [64 px][256 k] k-major image
-  using AC = Acc<kSBCo, kStemK>;
-  constexpr int TM = AC::TM, TN = AC::TN, WM = AC::WM, WN = AC::WN;
-  const int tid = threadIdx.x, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN;
+  constexpr int TM = 2, TN = 4, WM = 32, WN = 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 2, wc = wid & 3;
   const int split = blockIdx.x;
   const int kb = split * s.kps, ke = min(s.ksteps, kb + s.kps);
   const int C = kSBCo;
 
-  // A role: quad qi of the k-step, channels c0 .. c0 + 3 (four channels keep the dY registers within budget
-  // next to the 64-float accumulator and the eight staged im2col chunks)
-  const int qi = tid >> 4, c0 = (tid & 15) * 4;
-  float mean[4], sc[4], sh[4], k1[4], m1[4], k2[4];
+  // A role: quad qi of the k-step, channels c0, c0 + 1
+  const int qi = tid >> 5, c0 = (tid & 31) * 2;
+  float mean[2], sc[2], sh[2], k1[2], m1[2], k2[2];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < 2; ++e) {
     mean[e] = s.ws[c0 + e];
     sc[e] = s.ws[2 * C + c0 + e];
     sh[e] = s.ws[3 * C + c0 + e];
@@ -287,24 +291,21 @@ __global__ __launch_bounds__(kThreads, 2) void stem_wgrad_bn_kernel(const StemBn
     m1[e] = s.ws[5 * C + c0 + e];
     k2[e] = s.ws[6 * C + c0 + e];
   }
-  // B role: k-row (pixel) r = tid / 4 = quad qi, pixel sub = (tid / 4) % 4 of it (the A role's quad), filter row
-  // th = tid % 4: its 8 chunks are the 64 columns th * 64 .. +63 = taps tw 0..3 x channel halves, i.e. the 4
-  // consecutive folded pixels (ih, iw0 .. iw0 + 3): 128 contiguous bytes, one row test and one column test per tw
-  const int br = tid >> 2, bsub = br & 3, bth = tid & 3;
-  const int bdh = bth - 2 + (bsub >> 1), bdw = (bsub & 1) - 2;
-  // ds_write_b128 banks are (a / 4) mod 32 in groups of 8 lanes = 2 k-rows x 4 filter rows: the filter rows'
-  // 64-column offsets vanish mod 128 B, so each stores its chunks in its own order (chunk u ^ bsw at
-  // instruction u; bits 0 and 2, the row pair's swizzle differs in bit 1): 8 distinct 16-B slots per group
-  const int bsw = (bth & 1) | ((bth >> 1) << 2);
+  // B role. ds_write_b128 banks are (a / 4) mod 32 in groups of 8 lanes = one k-row: the filter rows'
+  // 64-column offsets vanish mod 128 B, so register u holds chunk hs * 4 + ((u + th) & 3) -- 8 distinct
+  // 16-byte slots per group
+  const int br = tid >> 3, bsub = br & 3, bth = (tid & 7) >> 1, bhs = tid & 1;
+  const int bdh = bth - 2 + (bsub >> 1), bdw = (bsub & 1) - 2 + 2 * bhs;
 
   // buffer loads: an out-of-range operand (past the batch, conv padding) reads as zeros via an offset past
   // num_records (kOOB) instead of an exec-masked branch; every tensor is < 2 GiB (stem_wgrad_bn_eligible)
   const __amdgpu_buffer_rsrc_t srx = make_srd(s.x, (uint32_t)(s.Q * 4 * C * 2));
   const __amdgpu_buffer_rsrc_t srs = make_srd(s.xs, (uint32_t)((int64_t)s.N * s.H * s.W * kStemC * 2));
-  ushort4_t rx[4], rd[4];
-  ushort8_t rb[8];
-  uint32_t rp[4];
-  bool wok[4];
+  const int64_t npool = (int64_t)s.N * s.OH * s.OW * C;  // pooled elements, < 2^29
+  const __amdgpu_buffer_rsrc_t srp = make_srd(s.pos, (uint32_t)npool);
+  const __amdgpu_buffer_rsrc_t srd = make_srd(s.dyp, (uint32_t)(npool * 2));
+  uint32_t rx[4], rd[4], rp[4];
+  ushort8_t rb[4];
   bool qok = false;
   auto issue = [&](int t) {
     const int64_t q = (int64_t)t * 16 + qi;
@@ -315,43 +316,44 @@ __global__ __launch_bounds__(kThreads, 2) void stem_wgrad_bn_kernel(const StemBn
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const uint32_t o = px + (uint32_t)(((p >> 1) * s.W + (p & 1)) * C * 2);
-      rx[p] = __builtin_bit_cast(ushort4_t, __builtin_amdgcn_raw_buffer_load_b64(srx, qok ? o : kOOB, 0, 0));
+      rx[p] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(srx, qok ? o : kOOB, 0, 0);
     }
-    // pooled windows (j + a, i + b) cover the quad (pad 1); OH = H / 2, so only the far ones can fall outside
+    // pooled windows (j + a, i + b) cover the quad (pad 1); OH = H / 2, so only the far ones can fall outside.
+    // A window outside (or past the batch) reads position 0 and gradient 0 (kOOB): it adds nothing
     const bool aok = j + 1 < s.OH, bok = i + 1 < s.OW;
-    const int64_t pw0 = ((int64_t)n * s.OH + j) * s.OW + i;
+    const uint32_t pw0 = (uint32_t)(((n * s.OH + j) * s.OW + i) * C + c0);
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      const bool in = (!(w >> 1) || aok) && (!(w & 1) || bok);
-      wok[w] = qok && in;
-      const int64_t o = (in ? pw0 + (w >> 1) * s.OW + (w & 1) : pw0) * C + c0;
-      rp[w] = *reinterpret_cast<const uint32_t*>(s.pos + o);
-      rd[w] = *reinterpret_cast<const ushort4_t*>(s.dyp + o);
+      const bool in = qok && (!(w >> 1) || aok) && (!(w & 1) || bok);
+      const uint32_t o = pw0 + (uint32_t)(((w >> 1) * s.OW + (w & 1)) * C);
+      rp[w] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(srp, in ? o : kOOB, 0, 0);
+      rd[w] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(srd, in ? 2 * o : kOOB, 0, 0);
     }
     const int ih = 2 * j + bdh, iw0 = 2 * i + bdw;
     const bool rok = qok && (unsigned)ih < (unsigned)s.H;
     const int pix0 = (n * s.H + ih) * s.W + iw0;  // may be negative: only used where the tests pass
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {  // register u holds chunk u ^ bsw (see the LDS store)
-      const int c = u ^ bsw;
-      const bool ok = rok && (unsigned)(iw0 + (c >> 1)) < (unsigned)s.W;
-      const uint32_t o = (uint32_t)(pix0 * kStemC + c * 8) * 2u;
+    for (int u = 0; u < 4; ++u) {
+      const int v = (u + bth) & 3;  // chunk v of the 64-byte run: tap 2 hs + v / 2, channel half v % 2
+      const bool ok = rok && (unsigned)(iw0 + (v >> 1)) < (unsigned)s.W;
+      const uint32_t o = (uint32_t)(pix0 * kStemC + v * 8) * 2u;
       rb[u] = __builtin_bit_cast(ushort8_t, __builtin_amdgcn_raw_buffer_load_b128(srs, ok ? o : kOOB, 0, 0));
     }
   };
-  Acc<kSBCo, kStemK> acc;
-  acc.zero();
+  accv_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = accv_t{};
   if (kb < ke) issue(kb);
   for (int t = kb; t < ke; ++t) {
     // dY of the quad's 4 pixels: g = sum of the pooled gradients whose argmax is the pixel, the forward's ReLU
     // recomputed from x, then bn_pool_quad_apply_kernel's k1 (g - m1 - (x - mean) k2)
-    ushort4_t av[4];
+    uint32_t av[4];
     {
-      float g[4][4];
+      float g[4][2];
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) g[p][e] = 0.f;
+      for (int p = 0; p < 4; ++p) g[p][0] = g[p][1] = 0.f;
 #pragma unroll
       for (int w = 0; w < 4; ++w)
 #pragma unroll
@@ -360,32 +362,38 @@ __global__ __launch_bounds__(kThreads, 2) void stem_wgrad_bn_kernel(const StemBn
           for (int dw = 0; dw < 2; ++dw) {
             const int ky = dh - 2 * (w >> 1) + 1, kx = dw - 2 * (w & 1) + 1;
             if (ky < 0 || kx < 0) continue;  // compile-time after unrolling
-            const uint32_t tap = wok[w] ? (uint32_t)(ky * 3 + kx) : 0xffu;
+            const uint32_t tap = (uint32_t)(ky * 3 + kx);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
+            for (int e = 0; e < 2; ++e) {
               const uint32_t byte = (rp[w] >> (8 * e)) & 0xffu;
-              g[dh * 2 + dw][e] += byte == tap ? bf16_to_f32((bf16_t)rd[w][e]) : 0.f;
+              g[dh * 2 + dw][e] += byte == tap ? bf16_to_f32((bf16_t)(rd[w] >> (16 * e))) : 0.f;
             }
           }
       // past the last quad: x and the window gradients read as zeros, and a zero k1 zeroes dY (branch-free)
-      float kq[4];
+      float kq[2];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) kq[e] = qok ? k1[e] : 0.f;
+      for (int e = 0; e < 2; ++e) kq[e] = qok ? k1[e] : 0.f;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
+        uint32_t packed = 0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float xv = bf16_to_f32((bf16_t)rx[p][e]);
+        for (int e = 0; e < 2; ++e) {
+          const float xv = bf16_to_f32((bf16_t)(rx[p] >> (16 * e)));
           const float gg = fmaf(xv, sc[e], sh[e]) > 0.f ? g[p][e] : 0.f;
-          av[p][e] = f32_to_bf16(kq[e] * (gg - m1[e] - (xv - mean[e]) * k2[e]));
+          packed |= (uint32_t)f32_to_bf16(kq[e] * (gg - m1[e] - (xv - mean[e]) * k2[e])) << (16 * e);
         }
+        av[p] = packed;
       }
     }
     __syncthreads();  // the previous k-step's fragment reads are done
 #pragma unroll
-    for (int p = 0; p < 4; ++p) *reinterpret_cast<ushort4_t*>(As + tr_off<kSBCo>(qi * 4 + p, c0)) = av[p];
+    for (int p = 0; p < 4; ++p)
+      *reinterpret_cast<uint32_t*>(As + tr_off<kSBCo>(qi * 4 + p, c0 & ~3) + (c0 & 3)) = av[p];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) *reinterpret_cast<ushort8_t*>(Bs + tr_off<kStemK>(br, bth * 64 + (u ^ bsw) * 8)) = rb[u];
+    for (int u = 0; u < 4; ++u) {
+      const int v = (u + bth) & 3;
+      *reinterpret_cast<ushort8_t*>(Bs + tr_off<kStemK>(br, bth * 64 + (bhs * 4 + v) * 8)) = rb[u];
+    }
     __syncthreads();
     if (t + 1 < ke) issue(t + 1);  // in flight during the MFMAs
 #pragma unroll
@@ -398,10 +406,18 @@ __global__ __launch_bounds__(kThreads, 2) void stem_wgrad_bn_kernel(const StemBn
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma(af[i], bfr[j], acc[i][j]);
     }
   }
-  epilogue_f32<kSBCo, kStemK>(acc, s.part + (int64_t)split * kSBCo * kStemK, kSBCo, kStemK, 0, 0);
+  // fp32 partial [64 co][256 k] of this split: lane (row acc_row, column acc_col) of each 16 x 16 fragment
+  float* out = s.part + (int64_t)split * kSBCo * kStemK;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        out[(wr * WM + i * kMS + acc_row(lane, r)) * kStemK + wc * WN + j * kMS + acc_col(lane)] = acc[i][j][r];
 }
 
 bool stem_wgrad_bn_eligible(int N, int H, int W, int Cout, int OH, int OW) {
@@ -413,7 +429,7 @@ bool stem_wgrad_bn_eligible(int N, int H, int W, int Cout, int OH, int OW) {
 int stem_wgrad_bn_splits(int N, int H, int W) {
   const int64_t Q = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) / 4;
   const int ks = (int)((Q + 15) / 16);
-  return std::max(1, std::min(2 * 256, ks));  // two blocks per CU
+  return std::max(1, std::min(2 * 256, ks));  // two 8-wave blocks per CU
 }
 
 void launch_stem_wgrad_bn(const void* dy_pool, const uint8_t* pos, const void* x, const float* ws, const void* xs,
@@ -437,7 +453,7 @@ void launch_stem_wgrad_bn(const void* dy_pool, const uint8_t* pos, const void* x
   s.ksteps = (int)((s.Q + 15) / 16);
   s.kps = (s.ksteps + splits - 1) / splits;
   const size_t lds = (size_t)(kBK * kSBCo + kBK * kStemK) * sizeof(bf16_t);
-  hipLaunchKernelGGL(stem_wgrad_bn_kernel, dim3(splits), dim3(kThreads), lds, stream, s);
+  hipLaunchKernelGGL(stem_wgrad_bn_kernel, dim3(splits), dim3(kSBNT), lds, stream, s);
   launch_splitk_reduce(partial, splits, (int64_t)kSBCo * kStemK, dwpk, out_dtype, 1.f, false, stream);
 }
 
