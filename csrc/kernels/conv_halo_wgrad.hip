@@ -123,6 +123,24 @@ __global__ __launch_bounds__(256, 1) void conv3x3_halo_wgrad_kernel(const HaloWg
     issue_strip(s_begin);
     issue_strip(s_begin + 1);  // past the end: zero rows / zero dy (contributes nothing)
   }
+  // LDS byte offsets (within the ring) of the two transposing reads of each (k-step, tap) step u of a strip:
+  // the XOR swizzle depends on ring-row bits 1 and 3 only, so the next strip's offsets are these plus 128 rows
+  // (16 KB) mod the 64 KB ring -- two VALU per offset per strip instead of the row wrap and swizzle per read
+  constexpr int kSteps = kWS / 32 * 9;
+  const int xg = lane >> 4, xqq = (lane & 15) >> 2, xp = lane & 3;
+  const int xcn = wave * 16 + 4 * xp;
+  uint32_t xo[kSteps][2];
+  {
+    const int rb0 = (int)(((int64_t)s_begin * kWS + 8 * xg + xqq + ring_off - (Wp + 1)) & (kWRing - 1));
+#pragma unroll
+    for (int u = 0; u < kSteps; ++u) {
+      const int kk = u / 9, t = u % 9;
+      const int o = kk * 32 + (t / 3) * Wp + (t % 3);
+      const int r0 = (rb0 + o) & (kWRing - 1), r1 = (rb0 + o + 4) & (kWRing - 1);
+      xo[u][0] = (uint32_t)tr_off<kWC>(r0, xcn) * 2u;
+      xo[u][1] = (uint32_t)tr_off<kWC>(r1, xcn) * 2u;
+    }
+  }
   for (int s = s_begin; s < s_end; ++s) {
     // strip s's group is done once only strip s+1's group (8 DMAs per thread) is younger
     vm_wait<8>();
@@ -134,11 +152,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_halo_wgrad_kernel(const HaloWg
 
     const int64_t q0 = (int64_t)s * kWS;
     const bf16_t* dyb = dys + (s % kWDySlots) * (kWDyBytes / 2);
-    const int g = lane >> 4, qq = (lane & 15) >> 2, p = lane & 3;
-    const int cn = wave * 16 + 4 * p;  // this wave's 16 input channels
-    // ring row of this lane's first transposing read at k-step 0, tap (0, 0): later k-steps and taps
-    // add compile-time row offsets (32 kk + shift), wrapped into the ring
-    const int rbase = (int)((q0 + 8 * g + qq + ring_off - (Wp + 1)) & (kWRing - 1));
+    const int g = xg, qq = xqq, p = xp;
+    (void)q0;
     // The 36 (k-step, tap) steps of the strip run as one unrolled sequence: step u's 4 MFMAs issue while
     // the x fragment of step u + 2 (and, in the last 4 taps of a k-step, one dy fragment of the next
     // k-step) is read. One wave per SIMD, so nothing else hides the LDS latency; and lgkmcnt is a 4-bit
@@ -149,12 +164,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3_halo_wgrad_kernel(const HaloWg
       af[b][i] = tr_frag(dyb + tr_off<kWC>(kr, 16 * i + 4 * p), dyb + tr_off<kWC>(kr + 4, 16 * i + 4 * p));
     };
     auto load_x = [&](int u) {
-      const int kk = u / 9, t = u % 9;
-      const int o = kk * 32 + (t / 3) * Wp + (t % 3);  // shift + (Wp + 1) >= 0
-      const int r0 = (rbase + o) & (kWRing - 1), r1 = (rbase + o + 4) & (kWRing - 1);
-      bx[u % 3] = tr_frag(ring + tr_off<kWC>(r0, cn), ring + tr_off<kWC>(r1, cn));
+      const char* rg = reinterpret_cast<const char*>(ring);
+      bx[u % 3] = tr_frag(reinterpret_cast<const bf16_t*>(rg + xo[u][0]), reinterpret_cast<const bf16_t*>(rg + xo[u][1]));
     };
-    constexpr int kSteps = kWS / 32 * 9;
 #pragma unroll
     for (int i = 0; i < 4; ++i) load_a(0, 0, i);
     load_x(0);
@@ -174,6 +186,11 @@ __global__ __launch_bounds__(256, 1) void conv3x3_halo_wgrad_kernel(const HaloWg
         else __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kSteps; ++u) {
+      xo[u][0] = (xo[u][0] + kWS * kWC * 2u) & (uint32_t)(kWRingBytes - 1);
+      xo[u][1] = (xo[u][1] + kWS * kWC * 2u) & (uint32_t)(kWRingBytes - 1);
     }
   }
   vm_wait<0>();  // no LDS-DMA may land after the block's LDS is released
