@@ -850,22 +850,45 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN,
             fr = acc_col(lane);
   bf16_t* Cs = reinterpret_cast<bf16_t*>(smem);
+  // accumulator registers in pairs (r, r + 1): one v_cvt_pk_bf16_f32 per pair, and the statistics of the
+  // stored (bf16-rounded) values in packed fp32 (v_pk_add_f32 / v_pk_fma_f32); the per-row range test
+  // only in a tile that crosses M. ~2.5 VALU per output element instead of ~11 (profiles/r5/g31/).
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  static_assert(kAccN % 2 == 0, "accumulator pairs");
+  const bool full = row0 + BM <= M;
+  f32x2_t ps[TN], pq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) ps[j] = pq[j] = f32x2_t{0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < kAccN; ++r) {
-        const int m = wr * WM + i * kMS + acc_row(lane, r);
+      for (int r = 0; r < kAccN; r += 2) {
+        const int m0 = wr * WM + i * kMS + acc_row(lane, r), m1 = wr * WM + i * kMS + acc_row(lane, r + 1);
         const int n = wc * WN + j * kMS + fr;
-        const bf16_t h = f32_to_bf16(acc.v[i][j][r]);
-        Cs[m * LDS_C + n] = h;
-        if constexpr (kStats) {
-          const float v = (row0 + m < M) ? bf16_to_f32(h) : 0.f;  // statistics of the stored values
-          st.s[j] += v;
-          st.q[j] = fmaf(v, v, st.q[j]);
+        const uint32_t u = __builtin_bit_cast(
+            uint32_t, __builtin_convertvector((f32x2_t{acc.v[i][j][r], acc.v[i][j][r + 1]}), bf16x2_t));
+        Cs[m0 * LDS_C + n] = (bf16_t)(u & 0xffffu);
+        Cs[m1 * LDS_C + n] = (bf16_t)(u >> 16);
+        if constexpr (kStats) {  // statistics of the stored values
+          f32x2_t v{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
+          if (!full) {
+            v.x = row0 + m0 < M ? v.x : 0.f;
+            v.y = row0 + m1 < M ? v.y : 0.f;
+          }
+          ps[j] += v;
+          pq[j] = __builtin_elementwise_fma(v, v, pq[j]);
         }
       }
+  if constexpr (kStats) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      st.s[j] += ps[j].x + ps[j].y;
+      st.q[j] += pq[j].x + pq[j].y;
+    }
+  }
   __syncthreads();
   constexpr int CPR = BN / 8;
   static_assert(NT % CPR == 0, "a thread keeps one 8-column group in the store loop");
