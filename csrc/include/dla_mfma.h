@@ -7,8 +7,8 @@
 // v_mfma_f32_16x16x32_bf16 (fp32 accumulate), kBK = 64 deep K steps staged through LDS with the
 // next step's global loads in flight during the current step's MFMAs (T14 register staging).
 // Operand tiles live in LDS either
-//   * row-major  [W][kBK + 8]  (operand is K-contiguous in memory; fragments by ds_read_b128,
-//                               rows padded by 16 B -> conflict-free), or
+//   * row-major  [W][kBK] (operand is K-contiguous in memory; fragments by ds_read_b128 from
+//                               XOR-swizzled 16-byte chunks -> conflict-free; DLA_RM_SWIZZLE), or
 //   * k-major    [kBK][W]      (operand is K-strided; fragments by ds_read_b64_tr_b16 through the
 //                               XOR-swizzled tr_off image -> conflict-free).
 // C/D fragment map of 16x16x32: col = lane & 15, row = 4 * (lane >> 4) + reg.
@@ -36,6 +36,13 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
 }
 
 constexpr int kThreads = 256;
+// Register-staged row-major operand tiles: 1 = the XOR-swizzled 128-byte rows of the LDS-DMA image, 0 = rows
+// padded by 16 B. The padding assumed 16 contiguous lanes per ds_read_b128 cycle; the instruction's lane groups
+// are {0-3, 12-15, 20-27}, ..., on which the padded rows pair up 2-way (profiles/r5/g32: 3.6e8 conflict cycles
+// in the 128x128 1x1 GEMM); the swizzled rows hit 16 distinct 16-byte slots.
+#ifndef DLA_RM_SWIZZLE
+#define DLA_RM_SWIZZLE 1
+#endif
 #ifndef DLA_KSTEP_PRE_FRAGS
 #define DLA_KSTEP_PRE_FRAGS 0  // kstep_mfma: fragment budget (both halves) for the pipelined form; 0 = off (r5 g18: 16 measured no faster)
 #endif
@@ -386,6 +393,8 @@ __device__ __forceinline__ void tile_store(bf16_t* s, const ushort8_t (&r)[TileG
     const int c = threadIdx.x + i * L::kNT;
     if constexpr (L::kKMajor)
       *reinterpret_cast<ushort8_t*>(s + tr_off<W>(c / TileGeom<W>::KPR, (c % TileGeom<W>::KPR) * 8)) = r[i];
+    else if constexpr (DLA_RM_SWIZZLE)  // the LDS-DMA row-major image (rm_glds_frag reads it)
+      *reinterpret_cast<ushort8_t*>(s + (c >> 3) * kBK + (((c & 7) ^ ((c >> 4) & 7)) << 3)) = r[i];
     else
       *reinterpret_cast<ushort8_t*>(s + (c >> 3) * (kBK + 8) + (c & 7) * 8) = r[i];
   }
@@ -408,6 +417,10 @@ __device__ __forceinline__ bf16x8_t tile_frag(const bf16_t* s, int r0, int kk) {
     }
     return tr_frag(s + tr_off<W>(kr, cn), s + tr_off<W>(kr + 4, cn));
   } else {
+    if constexpr (DLA_RM_SWIZZLE) {
+      const int r = r0 + (lane & (kMS - 1)), lc = kk * (kKS / 8) + lane / kMS;
+      return *reinterpret_cast<const bf16x8_t*>(s + r * kBK + ((lc ^ ((r >> 1) & 7)) << 3));
+    }
     return *reinterpret_cast<const bf16x8_t*>(s + (r0 + (lane & (kMS - 1))) * (kBK + 8) + kk * kKS +
                                               8 * (lane / kMS));
   }
