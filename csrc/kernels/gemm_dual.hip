@@ -73,8 +73,28 @@ struct DualArgs {
 // image row of panel-local weight row p (gemm_stream.hip): MFMA A-operand row 16 i + 4 g + r holds output
 // column 16 g + 4 i + r, so lane group g accumulates columns 16 g .. 16 g + 15
 __device__ __forceinline__ int uperm64(int p) { return 16 * ((p >> 2) & 3) + 4 * (p >> 4) + (p & 3); }
-// element offset of (row, 8-element chunk lc) in a [rows][64] LDS-DMA image (rm_glds_frag's swizzle)
-__device__ __forceinline__ int uimg(int row, int lc) { return row * kBK + ((lc ^ ((row >> 1) & 7)) << 3); }
+// The tile images are read two ways: row fragments by ds_read_b128 (data gradient) and transposed fragments by
+// ds_read_b64_tr_b16 (weight gradient). The LDS-DMA image's chunk XOR ((row >> 1) & 7) is conflict-free for the
+// first but pairs the transposed reads' 16-byte chunks 2-way (rows 2 apart XOR to adjacent chunks; r5 g37:
+// 6.4e8 conflict cycles per 5 steps in the Cout-256 kernel). The XOR below (bit 1 of the row -> chunk bit 1,
+// bit 3 -> chunk bit 2; found by exhaustive search over the two instructions' lane groups) serves both.
+#ifndef DLA_DUAL_SWZ
+#define DLA_DUAL_SWZ 2
+#endif
+__device__ __forceinline__ int usw(int row) {
+  if constexpr (DLA_DUAL_SWZ == 2) return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2);
+  else return (row >> 1) & 7;
+}
+// element offset of (row, 8-element chunk lc) in a [rows][64] tile image
+__device__ __forceinline__ int uimg(int row, int lc) { return row * kBK + ((lc ^ usw(row)) << 3); }
+// logical k of LDS-DMA slot c (row c >> 3, physical chunk c & 7) of that image
+__device__ __forceinline__ int uimg_kc(int c) { return ((c & 7) ^ usw(c >> 3)) << 3; }
+// 16 x 32 row fragment (rm_glds_frag's operand layout) from that image
+__device__ __forceinline__ bf16x8_t urm_frag(const bf16_t* s, int r0, int kk) {
+  const int lane = threadIdx.x & 63;
+  const int r = r0 + (lane & (kMS - 1)), lc = kk * (kKS / 8) + lane / kMS;
+  return *reinterpret_cast<const bf16x8_t*>(s + uimg(r, lc));
+}
 // element offset of (row, col), col % 4 == 0, in the same image: 4 consecutive columns are contiguous
 __device__ __forceinline__ int urm_off(int row, int col) { return uimg(row, col >> 3) + (col & 7); }
 
@@ -109,7 +129,7 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
 
   // data gradient of this wave: row fragment rf, channel fragments cf0 .. cf0 + NCF - 1 of the slice
   const int rf = wave % G::RF, cf0 = (wave / G::RF) * G::NCF;
-  // kWReg: this wave's W^T fragments (what rm_glds_frag would read from the panel below), loaded once
+  // kWReg: this wave's W^T fragments (what urm_frag would read from the panel below), loaded once
   bf16x8_t wreg[kWReg ? G::NCF : 1][kWReg ? 2 * G::KC : 1];
   if constexpr (kWReg) {
 #pragma unroll
@@ -157,8 +177,8 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
   for (int i = 0; i < G::Slots; ++i) {
     const int c = tid + i * 256, r = c >> 3;
     vr[i] = r;
-    vdy[i] = (uint32_t)((r * CO + rm_glds_kc(c)) * 2);
-    vx[i] = (uint32_t)((r * CI + ci0 + rm_glds_kc(c)) * 2);
+    vdy[i] = (uint32_t)((r * CO + uimg_kc(c)) * 2);
+    vx[i] = (uint32_t)((r * CI + ci0 + uimg_kc(c)) * 2);
   }
   const uint32_t ring0 = lds_addr(ring) + (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
   auto issue = [&](int t) {
@@ -277,9 +297,9 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
 #pragma unroll
         for (int i = 0; i < G::NCF; ++i) {
           if constexpr (kWReg) wf[i] = wreg[i][2 * kc + kk];
-          else wf[i] = rm_glds_frag(Ws + kc * G::Panel, 16 * (cf0 + i), kk);
+          else wf[i] = urm_frag(Ws + kc * G::Panel, 16 * (cf0 + i), kk);
         }
-        const bf16x8_t yf = rm_glds_frag(Ds + kc * G::Sub, 16 * rf, kk);
+        const bf16x8_t yf = urm_frag(Ds + kc * G::Sub, 16 * rf, kk);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < G::NCF; ++i) ad[i] = mfma(wf[i], yf, ad[i]);
