@@ -564,6 +564,9 @@ def main():
             f.write("\n\n")
             f.write(prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=40,
                                                                 max_name_column_width=60, max_src_column_width=400))
+            f.write("\n\n")  # the many small ops (memsets, copies) by call count, with their Python stacks
+            f.write(prof.key_averages(group_by_stack_n=8).table(sort_by="count", row_limit=60,
+                                                                max_name_column_width=60, max_src_column_width=500))
     if a.check_dir:
         os.makedirs(a.check_dir, exist_ok=True)
         names = dict((id(p), n) for n, p in base.named_parameters())
