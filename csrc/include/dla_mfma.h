@@ -43,6 +43,9 @@ constexpr int kThreads = 256;
 #ifndef DLA_RM_SWIZZLE
 #define DLA_RM_SWIZZLE 1
 #endif
+#ifndef DLA_EPI_SWZ
+#define DLA_EPI_SWZ 1  // epilogue_bf16 C staging layout (1 = swizzled unpadded rows, 0 = padded rows)
+#endif
 #ifndef DLA_KSTEP_PRE_FRAGS
 #define DLA_KSTEP_PRE_FRAGS 0  // kstep_mfma: fragment budget (both halves) for the pipelined form; 0 = off (r5 g18: 16 measured no faster)
 #endif
@@ -859,7 +862,17 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
   const bf16_t* __restrict__ d2 = (kEpi && epi) ? epi->d2 : nullptr;
   using AC = Acc<BM, BN, NT>;
   constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
-  constexpr int LDS_C = BN + 8;
+  // C staging: unpadded BN-wide rows, 16-byte chunk XOR ((m >> 2) & 1) << 1 (DLA_EPI_SWZ; else rows padded by
+  // 8 elements). The fragment writes (ds_write_b16, rows m and m + 4 in one 32-lane half) then land in different
+  // 32-byte units, and the row read-out (ds_read_b128 lane groups {0-3, 12-15, 20-27}, ...) covers 16 distinct
+  // slots; the padded rows conflicted 2-way on the read-out (tests/test_lds_swizzle.py)
+  static_assert(!DLA_EPI_SWZ || BN >= 32, "the staging XOR needs 4 chunks per row");
+  constexpr int LDS_C = DLA_EPI_SWZ ? BN : BN + 8;
+  auto cs_off = [](int m, int n) {
+    if constexpr (DLA_EPI_SWZ) return m * BN + ((((n >> 3) ^ (((m >> 2) & 1) << 1))) << 3) + (n & 7);
+    else return m * (BN + 8) + n;
+  };
+  (void)LDS_C;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN,
             fr = acc_col(lane);
   bf16_t* Cs = reinterpret_cast<bf16_t*>(smem);
@@ -883,8 +896,8 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
         const int n = wc * WN + j * kMS + fr;
         const uint32_t u = __builtin_bit_cast(
             uint32_t, __builtin_convertvector((f32x2_t{acc.v[i][j][r], acc.v[i][j][r + 1]}), bf16x2_t));
-        Cs[m0 * LDS_C + n] = (bf16_t)(u & 0xffffu);
-        Cs[m1 * LDS_C + n] = (bf16_t)(u >> 16);
+        Cs[cs_off(m0, n)] = (bf16_t)(u & 0xffffu);
+        Cs[cs_off(m1, n)] = (bf16_t)(u >> 16);
         if constexpr (kStats) {  // statistics of the stored values
           f32x2_t v{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
           if (!full) {
@@ -977,7 +990,7 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
     const int64_t gm = row0 + r;
     const int gn = col0 + cc;
     if (gm < M && gn < N) {
-      ushort8_t v = *reinterpret_cast<ushort8_t*>(Cs + r * LDS_C + cc);
+      ushort8_t v = *reinterpret_cast<ushort8_t*>(Cs + cs_off(r, cc));
       if (D) {
         const ushort8_t d = kPre ? dr[it] : *reinterpret_cast<const ushort8_t*>(D + gm * ldd + gn);
         const uint32_t db = kPre ? dbr[it] : (dmask ? (uint32_t)dmask[(gm * ldd + gn) >> 3] : 0xffu);

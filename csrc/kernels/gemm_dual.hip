@@ -230,8 +230,14 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
   // kBN: this thread's 8 channels (chunk column tid % (CO / 8)) in every row it converts
   constexpr int kCpr = CO / 8;  // 8-channel chunks per row
   float bmean[kBN ? 8 : 1], bk1[kBN ? 8 : 1], bm1[kBN ? 8 : 1], bk2[kBN ? 8 : 1];
+  // kBN pass lane map (conflict-free for both its ds_read_b128 and ds_write_b128 under the usw image, found by
+  // search, tests/test_lds_swizzle.py): a wave covers 2 rows x 32 chunks per step, row = lane bit 3, chunk =
+  // lane bits 0-2 (chunk in sub-image) and 4-5 (sub-image); the straight map (32 lanes per row) read the 4
+  // sub-images' same chunk positions from one bank slot: 2-way (r5 g41: 3.3e8 conflict cycles per 5 steps)
+  static_assert(!kBN || (kCpr == 32 && R % 8 == 0), "kBN lane map: Cout 256, whole 8-row steps");
+  const int bcg = (lane & 7) | (((lane >> 4) & 3) << 3), brb = (lane >> 3) & 1;
   if constexpr (kBN) {
-    const int c0 = (tid % kCpr) * 8;
+    const int c0 = bcg * 8;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       bmean[j] = s.ws[c0 + j];
@@ -263,10 +269,10 @@ __global__ __launch_bounds__(256, 1) void conv1x1_dual_kernel(const DualArgs s) 
       const bf16_t* Ys = Ds + G::KC * G::Sub;
       const uint8_t* Ms = reinterpret_cast<const uint8_t*>(Ds + G::MaskAt);
       constexpr int kPer = R * kCpr / 256;  // chunks per thread
-      const int cg = tid % kCpr, sub = cg >> 3, lc = cg & 7;
+      const int cg = bcg, sub = cg >> 3, lc = cg & 7;
 #pragma unroll
       for (int k = 0; k < kPer; ++k) {
-        const int r = tid / kCpr + k * (256 / kCpr);
+        const int r = 2 * (wave + 4 * k) + brb;
         const int o = sub * G::Sub + uimg(r, lc);
         const ushort8_t gv = *reinterpret_cast<const ushort8_t*>(Ds + o);
         const ushort8_t yv = *reinterpret_cast<const ushort8_t*>(Ys + o);

@@ -85,3 +85,71 @@ def test_register_staged_store_matches_fragment_reads():
     for c in range(1024):
         row, lc = c >> 3, c & 7
         assert ((c & 7) ^ ((c >> 4) & 7)) == (lc ^ lds_dma_sw(row))
+
+
+def epi_off(bn, m, n, swz=True):
+    """epilogue_bf16's C staging element offset (dla_mfma.h cs_off)."""
+    if swz:
+        return m * bn + (((n >> 3) ^ (((m >> 2) & 1) << 1)) << 3) + (n & 7)
+    return m * (bn + 8) + n
+
+
+def conflicts32(accesses):
+    """ds_write_b16 / b32: bank = (address / 4) mod 32 within each 32-lane half; one dword shared by two lanes
+    is one access."""
+    banks = {}
+    for addr in accesses:
+        banks.setdefault((addr // 4) % 32, set()).add(addr // 4)
+    return max(len(v) for v in banks.values()) - 1
+
+
+@pytest.mark.parametrize("bn", [64, 128, 256])
+@pytest.mark.parametrize("swz", [True, False])
+def test_epilogue_staging_layout(bn, swz):
+    # fragment writes: 32 lanes = columns c0 + (lane & 15) of rows m and m + 4 (lane >> 4), 2-byte stores
+    worst_w = 0
+    for m in range(0, 64, 16):
+        for r in range(4):
+            for c0 in range(0, bn, 16):
+                acc = [epi_off(bn, m + 4 * (l >> 4) + r, c0 + (l & 15), swz) * 2 for l in range(32)]
+                worst_w = max(worst_w, conflicts32(acc))
+    # read-out: thread c -> row c / (bn / 8), 16-byte chunk c % (bn / 8), ds_read_b128 lane groups
+    cpr = bn // 8
+    worst_r = 0
+    for base in range(0, 512, 64):
+        for g in B128_GROUPS:
+            acc = []
+            for l in g:
+                c = base + l
+                acc.append((epi_off(bn, c // cpr, (c % cpr) * 8, swz) * 2, 16))
+            worst_r = max(worst_r, conflicts(acc))
+    if swz:
+        assert worst_w == 0 and worst_r == 0, (bn, worst_w, worst_r)
+    else:  # the padded layout conflicted on the read-out at 64- and 128-wide tiles
+        assert worst_r >= (1 if bn <= 128 else 0)
+
+
+def test_dual_bn_pass_lane_map():
+    """gemm_dual.hip kBN in-place pass: lane -> (row bit 3, chunk bits 0-2 | 4-5 << 3) over four [64][64]
+    sub-images in the usw image: conflict-free for its row reads (ds_read_b128) and writes (ds_write_b128,
+    8 contiguous lanes, bank mod 32); the straight 32-lanes-per-row map was 2-way on the reads."""
+    sub_elems = 32 * 64  # the kBN kernel's 32-row tiles (any multiple of 4 rows: sub-images stay 256-byte aligned)
+
+    def addr(r, cg):
+        return (cg >> 3) * sub_elems * 2 + uimg_bytes(r, cg & 7)
+
+    def uimg_bytes(r, lc):
+        return (r * 64 + ((lc ^ dual_sw(r)) << 3)) * 2
+
+    def worst(mapf):
+        w = 0
+        for r0 in range(0, 64, 2):
+            for g in B128_GROUPS:
+                w = max(w, conflicts([(addr(r0 + mapf(l)[0], mapf(l)[1]), 16) for l in g]))
+            for g0 in range(0, 64, 8):
+                w = max(w, conflicts32([addr(r0 + mapf(l)[0], mapf(l)[1]) + 4 * d for l in range(g0, g0 + 8)
+                                        for d in range(4)]))
+        return w
+
+    assert worst(lambda l: ((l >> 3) & 1, (l & 7) | (((l >> 4) & 3) << 3))) == 0
+    assert worst(lambda l: (l >> 5, l & 31)) >= 1
