@@ -489,10 +489,12 @@ void launch_stem_fwd(const void* xs, const void* wpk, void* y, int N, int H, int
                      std::max(run_mainloop_lds_bytes<P_, 128, 64, StemRowLoader<128>, RowLoader<64>>(),          \
                               epilogue_lds_bytes<128, 64, S_>()),                                                \
                      stream, (const bf16_t*)xs, (const bf16_t*)wpk, (bf16_t*)y, g, Cout, stats)
-  if (pipe == 0) {
-    if (stats) DLA_STEM(true, 0); else DLA_STEM(false, 0);
-  } else {
-    if (stats) DLA_STEM(true, 2); else DLA_STEM(false, 2);
+  switch (pipe) {  // A/B: 0 register staging, 2 / 3 LDS-DMA stages, 4 / 5 the v2 LDS-DMA schedule
+    case 0: if (stats) DLA_STEM(true, 0); else DLA_STEM(false, 0); break;
+    case 3: if (stats) DLA_STEM(true, 3); else DLA_STEM(false, 3); break;
+    case 4: if (stats) DLA_STEM(true, 4); else DLA_STEM(false, 4); break;
+    case 5: if (stats) DLA_STEM(true, 5); else DLA_STEM(false, 5); break;
+    default: if (stats) DLA_STEM(true, 2); else DLA_STEM(false, 2); break;
   }
 #undef DLA_STEM
 }
