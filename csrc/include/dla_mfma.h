@@ -46,9 +46,7 @@ constexpr int kThreads = 256;
 #ifndef DLA_EPI_SWZ
 #define DLA_EPI_SWZ 1  // epilogue_bf16 C staging layout (1 = swizzled unpadded rows, 0 = padded rows)
 #endif
-#ifndef DLA_KSTEP_PRE_FRAGS
-#define DLA_KSTEP_PRE_FRAGS 0  // kstep_mfma: fragment budget (both halves) for the pipelined form; 0 = off (r5 g18: 16 measured no faster)
-#endif
+
 constexpr int kBK = 64;
 
 // GEMM epilogues load their addends for all of a thread's rows before the store loop (1), or per row
@@ -590,52 +588,28 @@ __device__ __forceinline__ const void* loader_src(const L& l, int i, int k0, lon
 // terms are hoisted (loader_step), and each MFMA cluster runs at s_setprio 1 so a co-resident
 // wave's VALU/DMA issue does not preempt it (cdna_hip_programming.md T5). Same LDS images, same
 // counted-vmcnt + raw-barrier protocol as mainloop_glds.
-// The MFMAs of one staged k-step (kBK / kKS = 2 halves). s_setprio is a scheduling barrier, so the
-// plain form (read half kk's fragments, wait, MFMAs) exposes the LDS latency of every half to a wave
-// that has no other wave on its SIMD to cover it; where both halves' fragments fit (kPre), half 1's
-// reads are issued before half 0's MFMAs (counted lgkmcnt: half 0 waits only for its own reads).
-// mid() runs between the halves (the B-operand DMA of a later stage).
+// The MFMAs of one staged k-step (kBK / kKS = 2 halves); mid() runs between the halves (the B-operand DMA of a
+// later stage). (Reading both halves' fragments before the first half's MFMAs measured no faster in these
+// two-waves-per-SIMD loops and was removed: profiles/r5/g18.)
 template <int BM, int BN, int NT, class LA, class LB, class Mid>
 __device__ __forceinline__ void kstep_mfma(const bf16_t* As, const bf16_t* Bs, int wr, int wc, Acc<BM, BN, NT>& acc,
                                            Mid&& mid) {
   using AC = Acc<BM, BN, NT>;
   constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN, KK = kBK / kKS;
-  constexpr bool kPre = (TM + TN) * KK <= DLA_KSTEP_PRE_FRAGS;
-  if constexpr (kPre) {
-    bf16x8_t af[KK][TM], bfr[KK][TN];
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
+  for (int kk = 0; kk < KK; ++kk) {
+    bf16x8_t af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[kk][i] = glds_frag<BM, LA>(As, wr * WM + i * kMS, kk);
+    for (int i = 0; i < TM; ++i) af[i] = glds_frag<BM, LA>(As, wr * WM + i * kMS, kk);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[kk][j] = glds_frag<BN, LB>(Bs, wc * WN + j * kMS, kk);
-    }
+    for (int j = 0; j < TN; ++j) bfr[j] = glds_frag<BN, LB>(Bs, wc * WN + j * kMS, kk);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      __builtin_amdgcn_s_setprio(1);
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[kk][i], bfr[kk][j], acc.v[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-      if (kk == 0) mid();
-    }
-  } else {
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = glds_frag<BM, LA>(As, wr * WM + i * kMS, kk);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag<BN, LB>(Bs, wc * WN + j * kMS, kk);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-      if (kk == 0) mid();
-    }
+      for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    if (kk == 0) mid();
   }
 }
 
