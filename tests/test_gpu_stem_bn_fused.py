@@ -12,18 +12,19 @@ def _stem_bn_case(cuda, n, h, w, seed=0):
     from distributed_learning_amd.ops.conv import stem_pack_weight
 
     C = _ext.require()
-    g = torch.Generator(device="cpu").manual_seed(seed)
-    x = torch.randn(n, 3, h, w, generator=g).to(cuda, torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    wt = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(cuda, torch.bfloat16)
+    g = torch.Generator(device=cuda).manual_seed(seed)  # device-side draws: the bench-batch case is 2 GB of dY
+    x = torch.randn(n, 3, h, w, generator=g, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(64, 3, 7, 7, generator=g, device=cuda) * 0.1).to(torch.bfloat16)
     y, stats, xs = C.stem_fwd(x, stem_pack_weight(wt), True)
-    gamma = (torch.rand(64, generator=g) + 0.5).to(cuda)
-    beta = (torch.rand(64, generator=g) - 0.5).to(cuda)
+    gamma = torch.rand(64, generator=g, device=cuda) + 0.5
+    beta = torch.rand(64, generator=g, device=cuda) - 0.5
     yp, ws, pos = C.bn_relu_maxpool_fwd(y, gamma, beta, None, None, 0.1, 1e-5, 3, 2, 1, stats, False)
-    dyp = torch.randn(yp.shape, generator=g).to(cuda, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dyp = torch.randn(yp.shape, generator=g, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     return C, x, wt, y, xs, gamma, ws, pos, dyp
 
 
-@pytest.mark.parametrize("shape", [(4, 224, 224), (3, 100, 100), (2, 64, 96), (1, 8, 8)])
+@pytest.mark.parametrize("shape", [(4, 224, 224), (3, 100, 100), (2, 64, 96), (1, 8, 8),
+                                   (1280, 224, 224)])  # bench.py's batch: 512 splits, 16 M conv-output pixels
 def test_stem_wgrad_bn_matches_unfused_and_torch(cuda, shape):
     from distributed_learning_amd.ops.conv import stem_unpack_grad
 
