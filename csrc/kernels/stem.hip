@@ -226,11 +226,12 @@ __global__ __launch_bounds__(kThreads, 2) void stem_wgrad_kernel(const bf16_t* _
 // argmax window positions, and the finalized BN coefficients (bn_pool_quad_apply_kernel's arithmetic and bf16
 // rounding). The GEMM's K (pixels) runs in quad order -- k = 4 q + 2 dh + dw for the 2x2 quad q of conv-output
 // pixels -- which the sum over pixels does not care about: a 64-pixel k-step is 16 quads, and one thread turns the
-// 4 pooled windows covering its quad (for 8 channels) into the 4 pixels' dY values, as the quad apply does.
-//   A (dY)  [64 px][64 co] k-major: all threads, quad tid / 16, channels (tid % 16) * 4
-//   B (im2col of xs) [64 px][256 k] k-major: all threads, 8 chunks each = 128 contiguous bytes of xs
-// Register-staged: the next k-step's raw loads are in flight during this k-step's MFMAs; the dY arithmetic runs
-// between the MFMAs and the LDS stores. One fp32 [64][256] partial per split, summed by splitk_reduce.
+// 4 pooled windows covering its quad (for 2 channels) into the 4 pixels' dY values, as the quad apply does.
+//   A (dY)  [64 px][64 co] k-major: all threads, quad tid / 32, channels (tid % 32) * 2
+//   B (im2col of xs) [64 px][256 k] k-major: all threads, 4 chunks each = 64 contiguous bytes of xs
+// Register-staged: the next k-step's raw loads (buffer loads; out of range reads zeros) are in flight during this
+// k-step's MFMAs; the dY arithmetic runs between the MFMAs and the LDS stores. One fp32 [64][256] partial per
+// split, summed by splitk_reduce. Kernel revisions and counters: profiles/r5/g11/README.md.
 namespace {
 
 constexpr int kSBCo = 64;  // stem output channels served
