@@ -43,6 +43,20 @@ __device__ __forceinline__ void block_rows(int64_t M, int nrb, int64_t& r0, int6
   r0 = (int64_t)blockIdx.y * per;
   r1 = min(M, r0 + per);
 }
+// The same row blocks dispatched last-to-first, for a pass that reads a tensor the previous kernel finished
+// writing (or reading) in row order: its first blocks then find the most recently touched rows still in the
+// 256 MB Infinity Cache (MALL) instead of evicting them on the way up. Used by the forward apply (after the
+// GEMM wrote x) and the backward reductions (after the data-gradient GEMM wrote dy); the backward apply then
+// runs first-to-last, after the reduction's last-to-first pass. Partial rows keep their blockIdx.y slot (each
+// block still writes one distinct partial; only the fixed summation order changes). DLA_BN_REV=0: off (A/B).
+#ifndef DLA_BN_REV
+#define DLA_BN_REV 1
+#endif
+__device__ __forceinline__ void block_rows_rev(int64_t M, int nrb, int64_t& r0, int64_t& r1) {
+  const int64_t per = (M + nrb - 1) / nrb;
+  r0 = (int64_t)(DLA_BN_REV ? nrb - 1 - (int)blockIdx.y : (int)blockIdx.y) * per;
+  r1 = min(M, r0 + per);
+}
 
 // Reduce 8 channels x 2 sums across the rpi row groups of the block (LDS), then thread row-group 0
 // writes the block partial. `red` holds rpi x ct x 2 floats.
@@ -293,7 +307,7 @@ __device__ __forceinline__ void bn_apply_body(int bx, const T* __restrict__ x, c
   const int c0 = bx * ct + (threadIdx.x % tpr) * 8;
   const int rg = threadIdx.x / tpr;
   int64_t r0, r1;
-  block_rows(M, nrb, r0, r1);
+  block_rows_rev(M, nrb, r0, r1);
   float sc[8], sh[8], sc2[8], sh2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -487,7 +501,7 @@ __device__ __forceinline__ void bn_bwd_reduce_body(int bx, DY dy, const T* __res
   const int c0 = c_base + (threadIdx.x % tpr) * 8;
   const int rg = threadIdx.x / tpr;
   int64_t r0, r1;
-  block_rows(M, nrb, r0, r1);
+  block_rows_rev(M, nrb, r0, r1);
   float mean[8], sc[8], sh[8], s[8], q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -689,7 +703,7 @@ __global__ __launch_bounds__(kBNThreads) void bn_bwd_dual_reduce_kernel(const T*
   const int c0 = c_base + (threadIdx.x % tpr) * 8;
   const int rg = threadIdx.x / tpr;
   int64_t r0, r1;
-  block_rows(M, nrb, r0, r1);
+  block_rows_rev(M, nrb, r0, r1);
   float mean[8], meand[8], s[8], q[8], qd[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
