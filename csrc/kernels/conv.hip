@@ -608,7 +608,10 @@ __global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void conv3x3_wgrad_k
 // ---------------------------------------------------------------------------------------------
 // Main loop of the 3x3 kernels when not forced (set_mfma_pipeline): per-layer A/B at ResNet-50
 // bs512 (profiles/r2v): forward and data gradient fastest on the buffer-DMA loop (PIPE 6: 2.62 /
-// 2.83 ms vs 2.69 / 2.95 on PIPE 2), the weight gradient on the v2 schedule (PIPE 4: 3.06 vs 3.20)
+// 2.83 ms vs 2.69 / 2.95 on PIPE 2). The weight gradient ran on the v2 schedule (PIPE 4: 3.06 vs 3.20 then);
+// after the round-5 swizzled operand images the 2-stage LDS-DMA loop is as fast or faster at every 3x3 weight
+// gradient of the bs1280 step (profiles/r5/g50: stage 2 0.393 vs 0.428 ms stride 1, 0.441 vs 0.463 stride 2;
+// 256x256 tiles equal or -3 %), so PIPE 2 is the weight-gradient default
 static int conv_pipeline(int K, int deep) {
   const int forced = mfma_pipeline();
   if (forced >= 0) return forced;
@@ -829,7 +832,7 @@ void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int spl
                      stream, (const bf16_t*)dy, (const bf16_t*)x, g, partial, kps,                                  \
                      ((Mo + BM_ - 1) / BM_) * ((No + 127) / 128), (int)splitk_xcd_remap())
 #define DLA_WG_P(BM_)                   \
-  switch (conv_pipeline(kps, 4)) {      \
+  switch (conv_pipeline(kps, 2)) {      \
     case 0: DLA_WG(BM_, 0); break;      \
     case 3: DLA_WG(BM_, 3); break;      \
     case 4: DLA_WG(BM_, 4); break;      \
@@ -837,7 +840,7 @@ void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int spl
   }
   if (wgrad_wide(Cin, Cout)) {
     const int nt = (Mo / 256) * (No / 256);
-    const int pipe = conv_pipeline(kps, 4) == 2 ? 2 : 4;
+    const int pipe = conv_pipeline(kps, 2) == 4 ? 4 : 2;
 #define DLA_WG8(P_)                                                                                             \
   hipLaunchKernelGGL((conv3x3_wgrad_kernel<256, 256, P_, 512>), dim3(nt * splits), dim3(512),                   \
                      (run_mainloop_lds_bytes<P_, 256, 256, KLoader<256, 512>, Im2colKLoader<256, true, 512>>()), \
