@@ -248,7 +248,11 @@ enum TileCfg : int {
   // 8 waves (4 x 2) of 64 x 128, 2-stage buffer-DMA pipeline (128 KB LDS), one block per CU: per MAC
   // 25 % fewer LDS fragment reads than the 64 x 64 wave tiles and half the DMA writes of two 128x128
   // blocks, for the compute-bound shapes where the 128x128 loop is LDS-bandwidth co-bound
-  kTile256x256 = 8
+  kTile256x256 = 8,
+  // 3x3 convs only: 8 waves (4 x 2) of 128 x 64 over 512 output pixels x 128 channels, 2-stage buffer-DMA
+  // pipeline (160 KB LDS, all of it), one block per CU: the per-MAC LDS fragment reads of the 256x256 tile's
+  // 64 x 128 wave tiles for the Cout = 128 layers that tile cannot serve (conv.hip pick_conv_tile)
+  kTile512x128 = 9
 };
 // K: reduction length (0 = unknown); wide_ok: the kernel family can run the 8-wave tiles (3x3 convs
 // need a channel count % 64 on the loaded side)
@@ -256,12 +260,14 @@ int pick_tile(int64_t M, int N, int tile, int K = 0, bool wide_ok = true);
 bool tile256_enabled();  // DLA_TILE256 != 0: 256x256 tiles for the compute-bound fwd / dgrad shapes
 bool tn256_enabled();    // ... and for the split-K weight gradients (also DLA_TN256 != 0)
 inline int tile_bm(int cfg) {
+  if (cfg == kTile512x128) return 512;
   return cfg == kTile64x64 ? 64
                            : ((cfg == kTile256x128 || cfg == kTile256x128w4 || cfg == kTile256x64 || cfg == kTile256x256)
                                   ? 256
                                   : 128);
 }
 inline int tile_bn(int cfg) {
+  if (cfg == kTile512x128) return 128;
   return (cfg == kTile128x256w4 || cfg == kTile256x256) ? 256
                                                        : ((cfg == kTile128x128 || cfg == kTile256x128 || cfg == kTile256x128w4) ? 128 : 64);
 }
@@ -334,6 +340,8 @@ void launch_gemm_nt_splitk(const void* A, int64_t lda, const void* B, int64_t ld
 // dgrad: stride 1 only, dx [N,H,W,Cin] (+ optional addend). wgrad: stride 1 or 2, split-K fp32
 // partials (splits * Cout * 9*Cin floats) reduced into dw [Cout][9*Cin] (fp32 or bf16).
 int conv3x3_stats_rows(int64_t P, int Cout, int tile = kTileAuto, int K = 0, bool wide_ok = true);
+// tile of a stride-1/2 3x3 forward or data-gradient launch (pick_tile plus the conv-only kTile512x128)
+int pick_conv_tile(int64_t P, int N, int tile, int K, bool wide_ok);
 // halo-tiled 64 -> 64 channel 3x3 / stride-1 conv (conv_halo.hip): persistent strips of 128 pixels,
 // weights resident in LDS; stats partial rows as the 128x64 tile (ceil(P / 128)). DLA_HALO: 0 off,
 // 1 data gradient only, 2 (default) also the forward.

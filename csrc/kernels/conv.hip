@@ -651,7 +651,7 @@ static void launch_fwd_p(const bf16_t* x, const bf16_t* w, bf16_t* y, const Conv
 template <int BM, int BN, bool S, int NTW = kThreads>
 static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGeom& g, float* stats,
                        hipStream_t stream) {
-  if constexpr (NTW == 512 && BM * BN > 256 * 128) {  // 256x256: 2 stages fill 128 KB of LDS
+  if constexpr (NTW == 512 && BM * BN > 256 * 128) {  // 256x256 / 512x128: 2 stages fill 128 / 160 KB of LDS
     if (mfma_pipeline() == 2) launch_fwd_p<BM, BN, S, 2, 512>(x, w, y, g, stats, stream);
     else launch_fwd_p<BM, BN, S, 6, 512>(x, w, y, g, stats, stream);
   } else if constexpr (NTW == 512) {  // 8-wave tile: 3-stage LDS-DMA pipeline, one block per CU
@@ -674,8 +674,26 @@ static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGe
   }
 }
 
+// 512x128 tiles for the Cout = 128 passes (ResNet stage 2): 128 x 64 wave tiles read as few LDS fragment bytes
+// per MFMA as the 256x256 tiles' 64 x 128 ones, which the 128x128 tile's 64 x 64 waves do not. At least 4 tiles
+// per CU (one block per CU, so the last wave of tiles is a small fraction). DLA_TILE512=1: on (A/B)
+static bool tile512_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DLA_TILE512");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+int pick_conv_tile(int64_t P, int N, int tile, int K, bool wide_ok) {
+  if (tile == kTileAuto && wide_ok && tile256_enabled() && tile512_enabled() && N == 128 && K >= 1024 &&
+      (P + 511) / 512 >= 1024)
+    return kTile512x128;
+  return pick_tile(P, N, tile, K, wide_ok);
+}
+
 int conv3x3_stats_rows(int64_t P, int Cout, int tile, int K, bool wide_ok) {
-  const int bm = tile_bm(pick_tile(P, Cout, tile, K, wide_ok));
+  const int bm = tile_bm(pick_conv_tile(P, Cout, tile, K, wide_ok));
   return (int)((P + bm - 1) / bm);
 }
 
@@ -693,7 +711,8 @@ void launch_conv3x3_fwd(const void* x, const void* w, void* y, int N, int H, int
   if (stats) launch_fwd<BM_, BN_, true, NT_>(xp, wp, yp, g, stats, stream);   \
   else launch_fwd<BM_, BN_, false, NT_>(xp, wp, yp, g, stats, stream);
 #define DLA_CF(BM_, BN_) DLA_CFW(BM_, BN_, kThreads)
-  switch (pick_tile((int64_t)g.N * g.OH * g.OW, Cout, tile, 9 * Cin, Cin % 64 == 0)) {
+  switch (pick_conv_tile((int64_t)g.N * g.OH * g.OW, Cout, tile, 9 * Cin, Cin % 64 == 0)) {
+    case kTile512x128: DLA_CFW(512, 128, 512) break;
     case kTile256x256: DLA_CFW(256, 256, 512) break;
     case kTile256x128: DLA_CFW(256, 128, 512) break;
     case kTile256x128w4: DLA_CF(256, 128) break;
@@ -759,7 +778,8 @@ void launch_conv3x3_dgrad(const void* dy, const void* w, void* dx, int N, int H,
   const bf16_t* d = (const bf16_t*)dy;
   const bf16_t* wp = (const bf16_t*)w;
   const bf16_t* ad = (const bf16_t*)addend;
-  switch (pick_tile((int64_t)N * H * W, Cin, tile, 9 * Cout, Cout % 64 == 0)) {
+  switch (pick_conv_tile((int64_t)N * H * W, Cin, tile, 9 * Cout, Cout % 64 == 0)) {
+    case kTile512x128: launch_dgrad<512, 128, 512>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile256x256: launch_dgrad<256, 256, 512>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile256x128: launch_dgrad<256, 128, 512>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;
     case kTile256x128w4: launch_dgrad<256, 128>(d, wp, (bf16_t*)dx, g, ad, bnb, stream); break;

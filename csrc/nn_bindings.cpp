@@ -934,7 +934,7 @@ static void check_conv3(const at::Tensor& x, const at::Tensor& w) {
 
 // 3x3 / pad 1 convolution forward (stride 1 or 2). Returns (y, stats-or-undefined).
 std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, bool stats, int64_t tile) {
-  TORCH_CHECK(tile >= 0 && tile <= kTile256x256, "conv3x3: tile config 0..8");
+  TORCH_CHECK(tile >= 0 && tile <= kTile512x128, "conv3x3: tile config 0..9");
   check_conv3(x, w);
   TORCH_CHECK(stride == 1 || stride == 2, "conv3x3: stride 1 or 2");
   TORCH_CHECK(x.size(1) % 64 == 0 || tile_bm(tile) * tile_bn(tile) <= 128 * 128,
@@ -952,7 +952,7 @@ std::vector<at::Tensor> conv3x3_fwd(at::Tensor x, at::Tensor w, int64_t stride, 
 
 // stride-1 data gradient (+ optional fused addend, same shape as dx)
 at::Tensor conv3x3_dgrad(at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> addend, int64_t tile) {
-  TORCH_CHECK(tile >= 0 && tile <= kTile256x256, "conv3x3: tile config 0..8");
+  TORCH_CHECK(tile >= 0 && tile <= kTile512x128, "conv3x3: tile config 0..9");
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(dy.dim() == 4 && dy.size(1) == w.size(0), "conv3x3_dgrad: dy/w mismatch");
   const int N = (int)dy.size(0), Cout = (int)w.size(0), Cin = (int)w.size(1), H = (int)dy.size(2), W = (int)dy.size(3);
@@ -1109,6 +1109,8 @@ void bind_nn(pybind11::module& m) {
         "split count gemm_nt uses for this shape (1 = tile kernel)");
   m.def("pick_tile", [](int64_t M, int64_t N, int64_t K, bool wide_ok) { return pick_tile(M, (int)N, kTileAuto, (int)K, wide_ok); },
         "tile config the auto policy picks for an M x N GEMM with reduction K (TileCfg: 1 = 128x128, 2 = 128x64, 8 = 256x256)");
+  m.def("pick_conv_tile", [](int64_t P, int64_t N, int64_t K, bool wide_ok) { return pick_conv_tile(P, (int)N, kTileAuto, (int)K, wide_ok); },
+        "tile of a 3x3 forward / data-gradient launch (pick_tile + the conv-only 512x128 tile)");
   m.def("gemm_tn_splits", [](int64_t Mo, int64_t No, int64_t K) { return gemm_tn_splits((int)Mo, (int)No, (int)K); },
         "split-K count of a weight-gradient gemm_tn launch");
   m.def("set_halo_wgrad", &set_halo_wgrad, "halo 64-channel 3x3 weight gradient: -1 environment (default on), 0 off, 1 on");

@@ -17,7 +17,8 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-TILES = {"auto": 0, "128x128": 1, "128x64": 2, "256x128": 4, "256x128w4": 5, "128x256w4": 6, "256x256": 8}
+TILES = {"auto": 0, "128x128": 1, "128x64": 2, "256x128": 4, "256x128w4": 5, "128x256w4": 6, "256x256": 8,
+         "512x128": 9}
 
 
 def timeit(fn, iters=15):
@@ -59,6 +60,8 @@ def main() -> None:
         r = {"C": C_, "H": H, "M": N * H * H, "gflop": round(gflop, 1)}
         for name, t in TILES.items():
             if t == 8 and C_ % 256:
+                continue
+            if t == 9 and C_ != 128:
                 continue
             if t == 2 and C_ > 64:
                 continue

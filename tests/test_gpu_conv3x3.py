@@ -99,7 +99,7 @@ def test_conv3x3_asymmetric_weights(cuda, Cin, Cout):
         torch.testing.assert_close(dw.float(), refw, rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 8])
+@pytest.mark.parametrize("tile", [1, 2, 3, 8, 9])
 @pytest.mark.parametrize("ch", [128, 256])
 def test_conv3x3_tile_configs(cuda, tile, ch):
     C = _C()
@@ -112,6 +112,35 @@ def test_conv3x3_tile_configs(cuda, tile, ch):
     torch.testing.assert_close(s.sum(0), s_ref.sum(0), rtol=1e-5, atol=1e-3)
     dy = torch.randn_like(y)
     assert torch.equal(C.conv3x3_dgrad(dy, w, None, tile), C.conv3x3_dgrad(dy, w, None, 1))
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv3x3_512x128_tile_at_stage2_rows(cuda, stride):
+    """The 512x128 tile (Cout = 128, >= 1024 row tiles: ResNet stage 2 at the bench batch) against fp32 torch,
+    with the BN-statistics epilogue, a partial last row tile (548,800 rows = 1071 x 512 + 448) and the data
+    gradient with a fused addend."""
+    C = _C()
+    torch.manual_seed(0)
+    N, H = 700, 28 * stride
+    x = torch.randn(N, 128, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(128, 128, 3, 3, device=cuda) * (2.0 / (9 * 128)) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    yr = F.conv2d(x.float(), w.float(), None, stride, 1)
+    y, stats = C.conv3x3_fwd(x, w, stride, True, 9)
+    assert stats.shape[0] == (N * 28 * 28 + 511) // 512
+    assert _rel(y, yr) < 1e-2
+    y1, s1 = C.conv3x3_fwd(x, w, stride, True, 1)
+    assert torch.equal(y, y1)
+    torch.testing.assert_close(stats.sum(0), s1.sum(0), rtol=1e-4, atol=1.0)
+    yf = y.float()
+    torch.testing.assert_close(stats.sum(0)[:, 0], yf.sum((0, 2, 3)), rtol=1e-3, atol=1.0)
+    if stride == 1:
+        dy = torch.randn(y.shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+        add = torch.randn_like(x)
+        dx = C.conv3x3_dgrad(dy, w, add, 9)
+        ref = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), 1, 1) + add.float()
+        assert _rel(dx, ref) < 1e-2
+        assert torch.equal(dx, C.conv3x3_dgrad(dy, w, add, 1))
 
 
 @pytest.mark.parametrize("pipe", [0, 2, 3, 4, 5, 6])

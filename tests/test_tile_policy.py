@@ -31,6 +31,14 @@ def test_pick_tile_wide_gate():
     assert C.pick_tile(100352, 256, 2304, False) == T128
 
 
+def test_conv_tile_512x128():
+    C = _ext.require()
+    # the 512x128 8-wave tile is opt-in (DLA_TILE512=1, unset in the test process): the auto policy is unchanged
+    assert C.pick_conv_tile(1003520, 128, 1152, True) == T128
+    assert C.pick_conv_tile(1003520, 256, 2304, True) == T256
+    assert C.pick_tile(1003520, 128, 1152, True) == T128  # the 1x1 GEMMs never get it
+
+
 def test_gemm_tn_splits_targets():
     C = _ext.require()
     # 256x256 weight-gradient tiles (both dims % 256): ~256 blocks, >= 16 k-steps per split
