@@ -676,11 +676,13 @@ static void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const ConvGe
 
 // 512x128 tiles for the Cout = 128 passes (ResNet stage 2): 128 x 64 wave tiles read as few LDS fragment bytes
 // per MFMA as the 256x256 tiles' 64 x 128 ones, which the 128x128 tile's 64 x 64 waves do not. At least 4 tiles
-// per CU (one block per CU, so the last wave of tiles is a small fraction). DLA_TILE512=1: on (A/B)
+// per CU (one block per CU, so the last wave of tiles is a small fraction). Stage 2 at bs1280 (profiles/r5/g54):
+// forward 0.359 -> 0.340 ms, data gradient 0.347 -> 0.341, stride-2 forward equal; step 82.54 -> 82.27 ms same
+// box. DLA_TILE512=0: off (A/B)
 static bool tile512_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("DLA_TILE512");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return v;
 }

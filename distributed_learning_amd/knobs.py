@@ -49,7 +49,7 @@ TABLE: Dict[str, Knob] = {
     "FANIN_CAT": Knob("1", "ops/inception.py", "0: three separate fan-in 1x1 GEMMs (profiles/r3y/)"),
     # ---- kernel selection (C++) --------------------------------------------------------------------
     "TILE256": Knob("1", "csrc/kernels/gemm.hip", "0: no 256x256 tiles for fwd / dgrad (profiles/r5a/)"),
-    "TILE512": Knob("0", "csrc/kernels/conv.hip", "1: 512x128 tiles for the Cout-128 3x3 fwd / dgrad (stage 2 at bs1280)"),
+    "TILE512": Knob("1", "csrc/kernels/conv.hip", "0: no 512x128 tiles for the Cout-128 3x3 fwd / dgrad (profiles/r5/g54/)"),
     "TN256": Knob("1", "csrc/kernels/gemm.hip", "0: no 256x256 weight-gradient tiles (profiles/r5c/, r5d/)"),
     "SPLITK_XCD": Knob("1", "csrc/kernels/gemm.hip", "0: no XCD-aware split-K grids (round-2 README row)"),
     "SPLITK_BLOCKS": Knob("512", "csrc/kernels/gemm.hip", "split-K grid target in blocks"),

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5, call g54: 512x128 conv tile for the Cout-128 3x3 passes: conv GPU tests, stage-2 timing vs 128x128
+# Round 5, call g54: 512x128 conv tile for the Cout-128 3x3 passes (then opt-in): conv GPU tests, stage-2 timing vs 128x128, step A/B
 set -o pipefail
 O=gpurun_out/r5/g54
 mkdir -p $O

@@ -122,6 +122,7 @@ def test_conv3x3_512x128_tile_at_stage2_rows(cuda, stride):
     C = _C()
     torch.manual_seed(0)
     N, H = 700, 28 * stride
+    assert C.pick_conv_tile(N * 28 * 28, 128, 9 * 128, True) == 9  # the auto pick at these rows
     x = torch.randn(N, 128, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
     w = (torch.randn(128, 128, 3, 3, device=cuda) * (2.0 / (9 * 128)) ** 0.5).to(torch.bfloat16)
     w = w.contiguous(memory_format=CL)

@@ -33,8 +33,10 @@ def test_pick_tile_wide_gate():
 
 def test_conv_tile_512x128():
     C = _ext.require()
-    # the 512x128 8-wave tile is opt-in (DLA_TILE512=1, unset in the test process): the auto policy is unchanged
-    assert C.pick_conv_tile(1003520, 128, 1152, True) == T128
+    # Cout = 128 3x3 passes with >= 1024 row tiles of 512 (ResNet-50 stage 2 at bs1280): the 512x128 8-wave tile
+    assert C.pick_conv_tile(1003520, 128, 1152, True) == 9
+    assert C.pick_conv_tile(401408, 128, 1152, True) == T128   # 784 tiles (bs512): stays on 128x128
+    assert C.pick_conv_tile(1003520, 128, 1152, False) == T128  # no 8-wave path
     assert C.pick_conv_tile(1003520, 256, 2304, True) == T256
     assert C.pick_tile(1003520, 128, 1152, True) == T128  # the 1x1 GEMMs never get it
 
