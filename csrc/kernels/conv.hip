@@ -808,6 +808,17 @@ void launch_conv3x3s2_dgrad(const void* dy, const void* w, void* dx, int N, int 
                        stream, (const bf16_t*)dy, (const bf16_t*)w, (bf16_t*)dx, g);
     return;
   }
+  // 512x128 8-wave tiles for Cin = 128 (stage 2's strided conv2) with >= 1024 tiles over the 4 parity classes,
+  // as pick_conv_tile does for the stride-1 passes; 2 stages fill all 160 KB of LDS. DLA_TILE512=0 turns them off
+  if (tile256_enabled() && tile512_enabled() && Cin == 128 && Cout % 64 == 0 && 4 * ((P + 511) / 512) >= 1024) {
+    const int pc = (int)((P + 511) / 512);
+    hipLaunchKernelGGL((conv3x3s2_dgrad_kernel<512, 128, 2, 512>), dim3(4 * pc), dim3(512),
+                       std::max(run_mainloop_lds_bytes<2, 512, 128, S2DgradRowLoader<512, 512>,
+                                                       S2WeightKLoader<128, 512>>(),
+                                epilogue_lds_bytes<512, 128, false, 512>()),
+                       stream, (const bf16_t*)dy, (const bf16_t*)w, (bf16_t*)dx, g);
+    return;
+  }
   const int bn = Cin <= 64 ? 64 : 128;
   const int per_class = (int)((P + 127) / 128) * ((Cin + bn - 1) / bn);
 #define DLA_S2(BN_, P_)                                                                                          \

@@ -61,7 +61,8 @@ def test_conv3x3_fwd_dgrad_wgrad(cuda, N, Cin, H, W, Cout, stride):
 
 
 @pytest.mark.parametrize("N,Cin,H,W,Cout", [(2, 64, 8, 6, 64), (1, 128, 14, 14, 64), (3, 64, 4, 10, 128),
-                                           (64, 256, 28, 28, 256)])  # 256x256 8-wave tiles
+                                           (64, 256, 28, 28, 256),  # 256x256 8-wave tiles
+                                           (333, 128, 56, 56, 128)])  # 512x128: 4 x 511 tiles, partial last
 def test_conv3x3s2_dgrad_every_tap(cuda, N, Cin, H, W, Cout):
     """Stride-2 data gradient (parity classes): one-hot weights per tap, exact against fp32."""
     C = _C()
