@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Stage-2 3x3 passes (Cout = 128, 28x28 output, bs1280) on the 512x128 tile vs the 128x128 tile: forward with the
 BN-statistics epilogue (stride 1 and 2) and data gradient, interleaved, medians of 30 after a warm-up pass.
-usage: python scripts/probe_tile512.py"""
+usage: [PROBE_N=512] python scripts/probe_tile512.py  (explicit tiles: the auto-pick threshold does not apply)"""
 import json
 import os
 import sys
@@ -18,7 +18,7 @@ def main():
     C = _ext.require()
     dev = torch.device("cuda:0")
     CL = torch.channels_last
-    N = 1280
+    N = int(os.environ.get("PROBE_N", "1280"))
     w = (torch.randn(128, 128, 3, 3, device=dev) * 0.03).to(torch.bfloat16).contiguous(memory_format=CL)
     for stride in (1, 2):
         H = 28 * stride
