@@ -195,6 +195,7 @@ def build_dp(model, reducer, cap_mb: float, dev, a, tune, world):
     if tune is not None:
         per_size = tune.run_buckets([b.flat.numel() for b in dp.sync.buckets])
         dp.sync.executor.per_bucket = {b.index: per_size[b.flat.numel()] for b in dp.sync.buckets}
+        dp.sync.regroup()  # fusion-off launch groups never span two algorithms (advisor r5)
     if world > 1 or a.force_comm:
         dp.sync.executor.reserve(dp.sync.buckets)
     return dp
@@ -215,6 +216,7 @@ def time_steps(step, a, dev, engine, graphed, backend, warmup=None):
     torch.cuda.synchronize()
     engine.consume_comm_ms()
     engine.set_timing(not graphed)
+    engine.impl.collective_counts(True)
     tele["before_timed"] = telemetry.sample(dev.index or 0)
     tev = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
     dist.barrier()
@@ -232,11 +234,14 @@ def time_steps(step, a, dev, engine, graphed, backend, warmup=None):
     tele["after_timed"] = telemetry.sample(dev.index or 0)
     comm_ms = engine.consume_comm_ms() / max(1, a.steps)
     engine.set_timing(False)
+    ncoll, nunits = (int(v) for v in engine.impl.collective_counts(True))
     t = torch.tensor([elapsed, comm_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     step_ms = [tev[i].elapsed_time(tev[i + 1]) for i in range(a.steps)]
     srt = sorted(step_ms)
     return {"elapsed": float(t[0]), "comm_ms": float(t[1]), "loss": loss, "tele": tele,
+            # host-side issue counts (engine.cpp collective_counts): member collectives and submission units
+            "collectives_per_step": ncoll / max(1, a.steps), "launch_units_per_step": nunits / max(1, a.steps),
             "warm_ms": [round(wev[i].elapsed_time(wev[i + 1]), 2) for i in range(warmup)],
             "step_ms": {"p50": round(srt[len(srt) // 2], 3), "min": round(srt[0], 3), "max": round(srt[-1], 3),
                         "seq": [round(x, 2) for x in step_ms] if a.steps <= 200 else None}}
@@ -426,16 +431,19 @@ def main():
         # the cap balances exposed collective time against the gradient-ready times of THIS step's
         # backward: the first warmup steps measure it (eager, on the provisional buckets, MAX over ranks;
         # they count as warmup steps), then the buckets are rebuilt. With no warmup the cap stays 8 MiB.
+        # the first eager step pays lazy setup (plans, first-call kernel setup): at least two calibration
+        # steps, the least of the later ones counts; with fewer warmup steps the provisional cap stays
         ncal = min(a.warmup, 3)
-        warm_left = a.warmup - ncal
-        bwd_s = measure_backward(data, opt, model, fwd_loss, dev, c.backend, n=ncal)
-        cpu_model = spec.build()
-        cap = float(tune.choose_cap(cpu_model, spec.input_shape, bwd_s))
-        del cpu_model
-        if abs(cap - a.bucket_mb) > 1e-9:
-            model.cleanup()
-            model = build_dp(base, reducer, cap, dev, a, tune, world)
-        a.bucket_mb = cap
+        if ncal >= 2:
+            warm_left = a.warmup - ncal
+            bwd_s = measure_backward(data, opt, model, fwd_loss, dev, c.backend, n=ncal)
+            cpu_model = spec.build()
+            cap = float(tune.choose_cap(cpu_model, spec.input_shape, bwd_s))
+            del cpu_model
+            if abs(cap - a.bucket_mb) > 1e-9:
+                model.cleanup()
+                model = build_dp(base, reducer, cap, dev, a, tune, world)
+            a.bucket_mb = cap
     comm_ms_eager = None
     run_step = step
     if graphed:
@@ -528,7 +536,12 @@ def main():
             },
             "knobs": knobs.non_default(),
             "allreduce_ms_per_step": round(comm_ms, 3),
-            "comm_world": int(engine.impl.world()),
+            # the rank count RCCL's own communicator reports (ncclCommCount), not WORLD_SIZE; the IPC-only
+            # transport has no communicator and reports its window group
+            "comm_world": int(engine.impl.rccl_count()) if engine.impl.has_rccl() else int(engine.impl.world()),
+            "comm_world_src": "ncclCommCount" if engine.impl.has_rccl() else "ipc window group",
+            "collectives_per_step": res["collectives_per_step"],
+            "launch_units_per_step": res["launch_units_per_step"],
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
             "final_loss": round(final_loss, 4),
             "baseline_ref": {"value": REFERENCE_IMG_S.get(world),
@@ -543,8 +556,14 @@ def main():
             rec["bucket_sweep"] = sweep_rows
         if phases is not None:
             rec["latency_breakdown_ms"] = phases
+        if gsync is not None and comm_active:
+            per_tensor = len(gsync.buckets) > 1 and all(len(b.params) == 1 for b in gsync.buckets)
+            if per_tensor:  # fusion off: which form ran (the strict one is the reference's semantics)
+                rec["fusion_off"] = {"mode": "grouped" if gsync.groups else "strict",
+                                     "tensors": len(gsync.buckets), "launch_groups": len(gsync.groups)}
         if tune is not None:
             rec["allreduce_table"] = tune.report()
+            rec["autotune_s"] = round(tune.spent_s, 3)
             ex = model.sync.executor
             rec["allreduce_per_bucket"] = [ex.algorithm_for(b) for b in model.sync.buckets]
         if gsync is not None and gsync.hook_calls:

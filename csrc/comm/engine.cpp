@@ -31,6 +31,7 @@
 // with a deadline (DLA_COMM_TIMEOUT_S, default 600 s) and aborts the communicators
 // (ncclCommAbort) on error or timeout instead of blocking forever; the destructor never waits
 // unboundedly on a comm stream whose peer may be dead.
+#include <atomic>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPStream.h>
@@ -290,6 +291,13 @@ class CommEngine {
   int64_t ipc_need() const { return (int64_t)ipc_need_; }
   int64_t ipc_capacity() const { return (int64_t)ipc_bytes_; }
   bool has_rccl() const { return comm_ != nullptr; }
+  // ranks of the RCCL communicator as RCCL itself reports them (ncclCommCount), -1 without one (IPC-only)
+  int rccl_count() const {
+    if (!comm_) return -1;
+    int n = -1;
+    DLA_NCCL_CHECK(ncclCommCount(comm_, &n));
+    return n;
+  }
 
   // Window lifecycle. A grown window is allocated while the current one (and every earlier one not
   // yet superseded by a verified mapping) stays allocated, so the new allocation can never reuse
@@ -301,16 +309,20 @@ class CommEngine {
     drain_stream_bounded();
     void* p = nullptr;
     DLA_HIP_THROW(hipMalloc(&p, (size_t)bytes));
-    if (ipc_base_) ipc_retired_.push_back(ipc_base_);
-    ipc_base_ = p;
-    ipc_bytes_ = (size_t)bytes;
-    ipc_nonce_ = nonce;
-    DLA_HIP_THROW(hipMemset(ipc_base_, 0, (size_t)bytes));
-    DLA_HIP_THROW(hipMemcpy(static_cast<char*>(ipc_base_) + comm::kIpcNonceOffset, &nonce, sizeof(nonce),
+    // The new window stays PENDING until ipc_open has verified every peer's mapping of it: the committed
+    // window (ipc_base_ / ipc_bytes_, what ipc_capacity() reports and allreduce_ipc checks against) and the
+    // peer mappings change together, so a failed or stale open leaves a consistent, smaller state that the
+    // next reserve grows again. An earlier pending window that never got verified is retired.
+    if (ipc_pend_base_) ipc_retired_.push_back(ipc_pend_base_);
+    ipc_pend_base_ = p;
+    ipc_pend_bytes_ = (size_t)bytes;
+    ipc_pend_nonce_ = nonce;
+    DLA_HIP_THROW(hipMemset(p, 0, (size_t)bytes));
+    DLA_HIP_THROW(hipMemcpy(static_cast<char*>(p) + comm::kIpcNonceOffset, &nonce, sizeof(nonce),
                             hipMemcpyHostToDevice));
     DLA_HIP_THROW(hipDeviceSynchronize());
     hipIpcMemHandle_t h;
-    DLA_HIP_THROW(hipIpcGetMemHandle(&h, ipc_base_));
+    DLA_HIP_THROW(hipIpcGetMemHandle(&h, p));
     return pybind11::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
   }
 
@@ -321,7 +333,7 @@ class CommEngine {
   std::string ipc_open(std::vector<pybind11::bytes> handles, std::vector<uint64_t> nonces) {
     TORCH_CHECK((int)handles.size() == topo_.world && (int)nonces.size() == topo_.world,
                 "ipc_open: need one handle and one nonce per rank");
-    TORCH_CHECK(ipc_base_, "ipc_open: call ipc_alloc first");
+    TORCH_CHECK(ipc_pend_base_, "ipc_open: call ipc_alloc first");
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
     std::vector<char*> fresh(topo_.world, nullptr);
     std::string bad;
@@ -331,7 +343,7 @@ class CommEngine {
     };
     for (int r = 0; r < topo_.world; ++r) {
       if (r == topo_.rank) {
-        fresh[r] = static_cast<char*>(ipc_base_);
+        fresh[r] = static_cast<char*>(ipc_pend_base_);
         continue;
       }
       std::string s = handles[r];
@@ -361,6 +373,12 @@ class CommEngine {
     }
     ipc_close_peers();
     ipc_peer_ = std::move(fresh);
+    if (ipc_base_) ipc_retired_.push_back(ipc_base_);
+    ipc_base_ = ipc_pend_base_;
+    ipc_bytes_ = ipc_pend_bytes_;
+    ipc_nonce_ = ipc_pend_nonce_;
+    ipc_pend_base_ = nullptr;
+    ipc_pend_bytes_ = 0;
     for (void* w : ipc_retired_) hipFree(w);
     ipc_retired_.clear();
     ++ipc_generation_;
@@ -394,6 +412,7 @@ class CommEngine {
   // ---------------------------------------------------------------------------------------
   void allreduce(at::Tensor flat, int algo, bool average) {
     check(flat);
+    ++n_units_;
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
     join_current();
     pybind11::gil_scoped_release nogil;
@@ -405,6 +424,7 @@ class CommEngine {
   void bucket_allreduce(at::Tensor flat, int algo, bool average, PackTable* table, double pack_scale,
                         double unpack_scale) {
     check(flat);
+    ++n_units_;
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
     join_current();
     pybind11::gil_scoped_release nogil;
@@ -421,6 +441,7 @@ class CommEngine {
   void bucket_allreduce_list(at::Tensor flat, int algo, bool average, std::vector<at::Tensor> grads,
                              std::vector<int64_t> offsets) {
     check(flat);
+    ++n_units_;
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
     join_current();
     pybind11::gil_scoped_release nogil;
@@ -441,6 +462,7 @@ class CommEngine {
     for (size_t i = 0; i < starts.size(); ++i)
       TORCH_CHECK(starts[i] >= 0 && counts[i] >= 0 && starts[i] + counts[i] <= group.numel(),
                   "bucket_allreduce_group: member ", i, " outside the group buffer");
+    ++n_units_;
     c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
     join_current();
     pybind11::gil_scoped_release nogil;
@@ -470,6 +492,17 @@ class CommEngine {
   }
 
   std::string describe_plan(int algo, int64_t n) { return comm::describe(plan_for(algo, n)); }
+
+  // Host-side issue counters: [member collectives issued (one per reduced bucket / group member, world > 1 or
+  // forced), submission units (one per allreduce / bucket / group call)]; reset after reading when asked.
+  std::vector<int64_t> collective_counts(bool reset) {
+    std::vector<int64_t> out{n_coll_.load(), n_units_.load()};
+    if (reset) {
+      n_coll_ = 0;
+      n_units_ = 0;
+    }
+    return out;
+  }
 
   // ---------------------------------------------------------------------------------------
   // Comm-stream timing (true communication ms, SURVEY.md §7.3 hard part 6).
@@ -559,14 +592,15 @@ class CommEngine {
 
   // bounded drain of the comm stream, then unmap the peers and free the windows
   void ipc_release() {
-    if (!ipc_base_ && ipc_peer_.empty() && ipc_retired_.empty()) return;
+    if (!ipc_base_ && !ipc_pend_base_ && ipc_peer_.empty() && ipc_retired_.empty()) return;
     drain_stream_bounded();
     ipc_close_peers();
     for (void* w : ipc_retired_) hipFree(w);
     ipc_retired_.clear();
     if (ipc_base_) hipFree(ipc_base_);
-    ipc_base_ = nullptr;
-    ipc_bytes_ = 0;
+    if (ipc_pend_base_) hipFree(ipc_pend_base_);
+    ipc_base_ = ipc_pend_base_ = nullptr;
+    ipc_bytes_ = ipc_pend_bytes_ = 0;
   }
 
   void abort_comms() {
@@ -713,6 +747,7 @@ class CommEngine {
       if (grads) pack_tensors_on(*grads, *offsets, flat, 1.f, st);
       return;
     }
+    ++n_coll_;
     if (uses_ipc(algo)) {
       allreduce_ipc(flat, algo, average, grads, offsets);
       return;
@@ -773,6 +808,7 @@ class CommEngine {
     DLA_NCCL_CHECK(ncclGroupStart());
     for (size_t i = 0; i < starts.size(); ++i) {
       if (counts[i] == 0) continue;
+      ++n_coll_;
       void* p = data + (size_t)starts[i] * esz;
       DLA_NCCL_CHECK(ncclAllReduce(p, p, counts[i], ndt, average ? ncclAvg : ncclSum, comm_, st));
     }
@@ -952,6 +988,7 @@ class CommEngine {
   bool aborted_ = false;
   bool accum_fp32_ = false;
   bool force_ = false;
+  std::atomic<int64_t> n_coll_{0}, n_units_{0};  // collective_counts() (hooks issue from the autograd thread)
   std::unique_ptr<c10::hip::HIPStream> stream_;
   std::map<std::pair<int, int64_t>, Plan> plans_;
   std::map<std::pair<int, int64_t>, IpcEntry> ipc_entries_;
@@ -960,6 +997,9 @@ class CommEngine {
   std::vector<char*> ipc_peer_;    // every rank's window base as mapped here (mine = ipc_base_)
   std::vector<void*> ipc_retired_;  // superseded windows, freed once the next mapping set is verified
   uint64_t ipc_nonce_ = 0;         // identity stamp of the current window
+  void* ipc_pend_base_ = nullptr;  // allocated by ipc_alloc, committed by a verified ipc_open
+  size_t ipc_pend_bytes_ = 0;
+  uint64_t ipc_pend_nonce_ = 0;
   int64_t ipc_generation_ = 0;     // verified mapping sets so far
   int64_t ipc_stale_ = 0;          // mappings refused because they showed the wrong nonce
   uint64_t ipc_tok_ = 0;           // barrier token counter, identical sequence on every rank
@@ -1273,7 +1313,9 @@ void bind_comm(pybind11::module& m) {
       .def("allgather", &CommEngine::allgather)
       .def("set_timing", &CommEngine::set_timing)
       .def("consume_comm_ms", &CommEngine::consume_comm_ms)
+      .def("collective_counts", &CommEngine::collective_counts, pybind11::arg("reset") = false)
       .def("has_rccl", &CommEngine::has_rccl)
+      .def("rccl_count", &CommEngine::rccl_count)
       .def("ipc_need", &CommEngine::ipc_need)
       .def("ipc_capacity", &CommEngine::ipc_capacity)
       .def("ipc_alloc", &CommEngine::ipc_alloc)

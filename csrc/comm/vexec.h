@@ -283,7 +283,9 @@ class VirtualRun {
   }
 
   const std::vector<Plan>& plans_;
-  const Topology& t_;
+  // by value: a caller may construct the run from a temporary topology (the sanitizer build of
+  // csrc/tests/host_check.cpp caught a dangling reference in exactly that use)
+  const Topology t_;
   Backend& be_;
 };
 

@@ -288,6 +288,14 @@ bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, 
                         int M, int N, int K, float* stats, hipStream_t stream, const void* addend = nullptr,
                         int64_t ldd = 0, const uint8_t* addend_mask = nullptr, const BnBwdArgs* bn_bwd = nullptr);
 void set_gemm_stream(int mode);
+// 128x128 1x1 GEMM tiles stored straight from the accumulators (gemm_direct.hip): the transposed product,
+// lane-exchange to 16-byte chunks, statistics by DPP row sums; same outputs / statistics layout as
+// launch_gemm_nt's 128x128 tile. set_gemm_direct: -1 environment (DLA_GEMM_DIRECT, default off), 0 / 1.
+bool gemm_direct_ok(int N, int64_t ldc, const void* addend, int64_t ldd);
+void launch_gemm_direct(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
+                        int M, int N, int K, float* stats, const void* addend, int64_t ldd,
+                        const uint8_t* addend_mask, hipStream_t stream);
+void set_gemm_direct(int mode);
 // BatchNorm-backward reduction fused into a bf16-output GEMM epilogue (the output is the BN's dy):
 // x = the BN input [M, N], ws = its 7N workspace, mask/mode as launch_bn_bwd (0, 1 or 2),
 // part = [stats_rows][N][2] partial (sum dy', sum dy'(x - mean)).

@@ -89,6 +89,14 @@ __device__ __forceinline__ accv_t mfma(const bf16x8_t& a, const bf16x8_t& b, con
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 #endif
 }
+// Main loops compute acc[i][j] += A-frag i x B-frag j (kT = false: output rows = A rows) or, with kT, the
+// transposed product B-frag j x A-frag i (output rows = B rows, e.g. a 1x1 conv's channels, columns = A rows,
+// its pixels): a lane then holds 4 consecutive channels of one pixel per fragment (gemm_direct.hip).
+template <bool kT>
+__device__ __forceinline__ accv_t mfma_t(const bf16x8_t& a, const bf16x8_t& b, const accv_t& c) {
+  if constexpr (kT) return mfma(b, a, c);
+  else return mfma(a, b, c);
+}
 // C/D fragment position of accumulator register `reg` of `lane` (16x16x32: col = lane & 15,
 // row = 4 * (lane >> 4) + reg; 32x32x16: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5))
 __device__ __forceinline__ int acc_row(int lane, int reg) {
@@ -428,7 +436,7 @@ __device__ __forceinline__ bf16x8_t tile_frag(const bf16_t* s, int r0, int kk) {
 }
 
 // acc += A[BM rows, k in [kbeg, kend)] * B[BN cols, same k]^T
-template <int BM, int BN, int NT, class LA, class LB>
+template <int BM, int BN, int NT, bool kT = false, class LA, class LB>
 __device__ __forceinline__ void mainloop(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
                                          char* smem) {
   static_assert(LA::kNT == NT && LB::kNT == NT, "loaders built for another block size");
@@ -464,7 +472,7 @@ __device__ __forceinline__ void mainloop(const LA& la, const LB& lb, int kbeg, i
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
+        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma_t<kT>(af[i], bfr[j], acc.v[i][j]);
     }
     __syncthreads();
     if (t + 1 < nk) {
@@ -497,7 +505,7 @@ __host__ __device__ constexpr size_t glds_lds_bytes() {
 // barrier per k-step. Iteration t: wait until this wave's DMAs for tile t are done (the younger
 // stages may stay outstanding: counted vmcnt), barrier (everyone's tile t has landed AND everyone
 // finished tile t-1, whose stage the next DMA overwrites), issue tile t+NS-1, multiply tile t.
-template <int BM, int BN, int NT, int NS, class LA, class LB>
+template <int BM, int BN, int NT, int NS, bool kT = false, class LA, class LB>
 __device__ __forceinline__ void mainloop_glds(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
                                               char* smem) {
   static_assert(NS == 2 || NS == 3, "2 or 3 stages");
@@ -558,7 +566,7 @@ __device__ __forceinline__ void mainloop_glds(const LA& la, const LB& lb, int kb
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
+        for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma_t<kT>(af[i], bfr[j], acc.v[i][j]);
     }
   }
   __syncthreads();  // every wave done with the stages before the epilogue reuses the LDS
@@ -591,7 +599,7 @@ __device__ __forceinline__ const void* loader_src(const L& l, int i, int k0, lon
 // The MFMAs of one staged k-step (kBK / kKS = 2 halves); mid() runs between the halves (the B-operand DMA of a
 // later stage). (Reading both halves' fragments before the first half's MFMAs measured no faster in these
 // two-waves-per-SIMD loops and was removed: profiles/r5/g18.)
-template <int BM, int BN, int NT, class LA, class LB, class Mid>
+template <int BM, int BN, int NT, class LA, class LB, bool kT = false, class Mid>
 __device__ __forceinline__ void kstep_mfma(const bf16_t* As, const bf16_t* Bs, int wr, int wc, Acc<BM, BN, NT>& acc,
                                            Mid&& mid) {
   using AC = Acc<BM, BN, NT>;
@@ -607,13 +615,13 @@ __device__ __forceinline__ void kstep_mfma(const bf16_t* As, const bf16_t* Bs, i
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma(af[i], bfr[j], acc.v[i][j]);
+      for (int j = 0; j < TN; ++j) acc.v[i][j] = mfma_t<kT>(af[i], bfr[j], acc.v[i][j]);
     __builtin_amdgcn_s_setprio(0);
     if (kk == 0) mid();
   }
 }
 
-template <int BM, int BN, int NT, int NS, class LA, class LB>
+template <int BM, int BN, int NT, int NS, bool kT = false, class LA, class LB>
 __device__ __forceinline__ void mainloop_glds2(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
                                                char* smem) {
   static_assert(NS == 2 || NS == 3, "2 or 3 stages");
@@ -668,7 +676,7 @@ __device__ __forceinline__ void mainloop_glds2(const LA& la, const LB& lb, int k
     if (more) issue_a(t + NS - 1);
     const bf16_t* As = base + (t % NS) * (SA + SB);
     const bf16_t* Bs = As + SA;
-    kstep_mfma<BM, BN, NT, LA, LB>(As, Bs, wr, wc, acc, [&] {
+    kstep_mfma<BM, BN, NT, LA, LB, kT>(As, Bs, wr, wc, acc, [&] {
       if (more) issue_b(t + NS - 1);
     });
   }
@@ -692,7 +700,7 @@ __device__ __forceinline__ void bissue(const L& l, int k0, uint32_t lds) {
   bglds<CH, NT * 16>(vo, l.bsrd, (uint32_t)__builtin_amdgcn_readfirstlane(l.bsoff(k0)), lds);
 }
 
-template <int BM, int BN, int NT, int NS, class LA, class LB>
+template <int BM, int BN, int NT, int NS, bool kT = false, class LA, class LB>
 __device__ __forceinline__ void mainloop_bglds(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
                                                char* smem) {
   static_assert(NS == 2 || NS == 3, "2 or 3 stages");
@@ -745,7 +753,7 @@ __device__ __forceinline__ void mainloop_bglds(const LA& la, const LB& lb, int k
     if (more) issue_a(t + NS - 1);
     const bf16_t* As = base + (t % NS) * (SA + SB);
     const bf16_t* Bs = As + SA;
-    kstep_mfma<BM, BN, NT, LA, LB>(As, Bs, wr, wc, acc, [&] {
+    kstep_mfma<BM, BN, NT, LA, LB, kT>(As, Bs, wr, wc, acc, [&] {
       if (more) issue_b(t + NS - 1);
     });
   }
@@ -755,13 +763,13 @@ __device__ __forceinline__ void mainloop_bglds(const LA& la, const LB& lb, int k
 // Pipeline selection shared by all MFMA kernels: 0 = register staging (one k-step in flight,
 // 3 blocks/CU), 2 / 3 = LDS-DMA with 2 / 3 stages, 4 / 5 = the v2 LDS-DMA schedule with 2 / 3 stages,
 // 6 / 7 = the v3 buffer-DMA schedule with 2 / 3 stages (loaders with a buffer form only).
-template <int PIPE, int BM, int BN, int NT, class LA, class LB>
+template <int PIPE, bool kT = false, int BM, int BN, int NT, class LA, class LB>
 __device__ __forceinline__ void run_mainloop(const LA& la, const LB& lb, int kbeg, int kend, Acc<BM, BN, NT>& acc,
                                              char* smem) {
-  if constexpr (PIPE == 0) mainloop<BM, BN, NT>(la, lb, kbeg, kend, acc, smem);
-  else if constexpr (PIPE >= 6) mainloop_bglds<BM, BN, NT, PIPE - 4>(la, lb, kbeg, kend, acc, smem);
-  else if constexpr (PIPE >= 4) mainloop_glds2<BM, BN, NT, PIPE - 2>(la, lb, kbeg, kend, acc, smem);
-  else mainloop_glds<BM, BN, NT, PIPE>(la, lb, kbeg, kend, acc, smem);
+  if constexpr (PIPE == 0) mainloop<BM, BN, NT, kT>(la, lb, kbeg, kend, acc, smem);
+  else if constexpr (PIPE >= 6) mainloop_bglds<BM, BN, NT, PIPE - 4, kT>(la, lb, kbeg, kend, acc, smem);
+  else if constexpr (PIPE >= 4) mainloop_glds2<BM, BN, NT, PIPE - 2, kT>(la, lb, kbeg, kend, acc, smem);
+  else mainloop_glds<BM, BN, NT, PIPE, kT>(la, lb, kbeg, kend, acc, smem);
 }
 
 template <int PIPE, int BM, int BN, class LA, class LB>

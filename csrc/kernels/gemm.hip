@@ -328,7 +328,15 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
     if (b_kmajor) DLA_NT(BM_, BN_, false, true, NT_); else DLA_NT(BM_, BN_, false, false, NT_);  \
   }
 #define DLA_NT_ST(BM_, BN_) DLA_NT_STW(BM_, BN_, kThreads)
-  switch (pick_tile(M, N, tile, K)) {
+  const int cfg = pick_tile(M, N, tile, K);
+  // the 128x128 tile without the BN-backward / stride-2 epilogue features: stored from the registers
+  // (gemm_direct.hip); tile = kTile128x128 forced by a caller keeps the LDS-staged kernel (A/B)
+  if (cfg == kTile128x128 && tile == kTileAuto && !bn_bwd && !addend2_s2 && !(stats && addend) &&
+      gemm_direct_ok(N, ldc, addend, ld_addend)) {
+    launch_gemm_direct(A, lda, B, ldb, b_kmajor, C, ldc, M, N, K, stats, addend, ld_addend, addend_mask, stream);
+    return;
+  }
+  switch (cfg) {
     case kTile256x256: DLA_NT_STW(256, 256, 512) break;
     case kTile256x128: DLA_NT_STW(256, 128, 512) break;
     case kTile256x128w4: DLA_NT_ST(256, 128) break;

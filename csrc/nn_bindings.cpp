@@ -1059,6 +1059,7 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("mask"), pybind11::arg("mode"));
   m.def("set_mfma_pipeline", &set_mfma_pipeline, "MFMA main loop: 0 register staging, 2/3 LDS-DMA stages, -1 per-shape auto");
   m.def("set_gemm_stream", &set_gemm_stream, "persistent streaming 1x1 GEMM: -1 environment (default on), 0 off, 1 on");
+  m.def("set_gemm_direct", &set_gemm_direct, "register-stored 128x128 1x1 GEMM tiles: -1 environment (default off), 0 / 1");
   m.def("gemm_stream_rows", &gemm_stream_rows, "BN-statistics partial rows of the streaming GEMM (0: shape not served)",
         pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("lda"), pybind11::arg("ldc"), pybind11::arg("b_kmajor") = false,
         pybind11::arg("add") = false, pybind11::arg("bnb") = false);

@@ -169,6 +169,27 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False, d
     return out
 
 
+SANITIZE_DIR = ROOT / "build" / "sanitize"
+
+
+def sanitize_check(run: bool = True) -> int:
+    """CPU AddressSanitizer + UndefinedBehaviorSanitizer build of the comm engine's host C++ (plan builder,
+    virtual-rank host executor, IPC host protocol; csrc/tests/host_check.cpp) -- the GPU pool runs no
+    sanitizers, so this is where they apply. Returns the check's exit status (0 = clean)."""
+    SANITIZE_DIR.mkdir(parents=True, exist_ok=True)
+    exe = SANITIZE_DIR / "host_check"
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+           "-fno-omit-frame-pointer", "-pthread", str(CSRC / "tests" / "host_check.cpp"), str(CSRC / "comm" / "plan.cpp"),
+           "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"sanitizer build failed:\n{r.stdout}\n{r.stderr}")
+    if not run:
+        return 0
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    return subprocess.run([str(exe)], env=env).returncode
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("-j", "--jobs", type=int, default=None)
@@ -176,7 +197,11 @@ def main(argv=None):
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("-D", "--define", action="append", default=[], help="extra -D for a variant build")
     ap.add_argument("--out", default=None, help="output .so (variant builds)")
+    ap.add_argument("--sanitize", action="store_true",
+                    help="build and run the ASan/UBSan CPU check of the host-side comm C++ instead")
     a = ap.parse_args(argv)
+    if a.sanitize:
+        return sanitize_check()
     out = build(a.jobs, a.force, a.verbose, tuple(a.define), a.out)
     print(f"built {out}")
 

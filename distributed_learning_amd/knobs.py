@@ -34,6 +34,10 @@ TABLE: Dict[str, Knob] = {
     "TRANSPORT": Knob("", "parallel/context.py", "rccl | ipc gradient transport (default rccl; ipc with SAME_DEVICE)"),
     "COMPUTE_STREAM": Knob("default", "bench.py", "high: the training step runs on a high-priority stream, so its "
                                                   "kernels dispatch ahead of the late weight gradients' side stream"),
+    "LAUNCH_GROUPS": Knob("1", "parallel/grad_sync.py", "0: fusion off (bucket cap 0) issues one collective launch per "
+                                                        "gradient tensor, the reference's semantics (main.py:168-179); 1: "
+                                                        "the per-tensor collectives launch in groups (profiles/r5/g04/)"),
+    "AUTOTUNE_BUDGET_S": Knob("90", "parallel/autotune.py", "wall-clock budget of the all-reduce selection at N > 1"),
     "COMM_TIMEOUT_S": Knob("600", "csrc/comm/engine.cpp", "seconds before a collective / IPC barrier is declared dead"),
     # ---- scheduling of the backward ----------------------------------------------------------------
     "WGRAD_DEFER": Knob("3x3", "ops/conv.py", "3x3 | auto | all | 0: weight gradients on the side stream "
@@ -55,6 +59,8 @@ TABLE: Dict[str, Knob] = {
     "SPLITK_BLOCKS": Knob("512", "csrc/kernels/gemm.hip", "split-K grid target in blocks"),
     "SPLITK_SG": Knob("1", "csrc/kernels/gemm.hip", "0: no split-group split-K reduce (profiles/r3n/)"),
     "GEMM_SPLITK": Knob("1", "csrc/nn_bindings.cpp", "0: no split-K for the FC heads"),
+    "GEMM_DIRECT": Knob("0", "csrc/kernels/gemm_direct.hip", "1: 128x128 1x1 GEMM tiles stored straight from the "
+                                                             "registers, not staged through LDS (neutral: profiles/r6/g03/)"),
     "GEMM_STREAM": Knob("1", "csrc/kernels/gemm_stream.hip", "0: no persistent streaming 1x1 GEMM (profiles/r3/)"),
     "CONV_PIPE": Knob("-1", "csrc/kernels/conv.hip", "3x3 conv main-loop pipeline for K >= 256 (-1: per shape)"),
     "HALO": Knob("2", "csrc/kernels/conv_halo.hip", "0 off, 1 dgrad only, 2 fwd + dgrad halo-tiled 64-ch 3x3 (r5l/)"),

@@ -171,14 +171,18 @@ class NativeEngine:
         """Collective: every rank calls it at the same point (the need is deterministic, so all
         ranks agree on whether to grow; it is all-gathered anyway). ``force``: allocate and map a
         new window generation even when the current one is large enough (tests cycle windows)."""
-        need = int(self.impl.ipc_need())
         world = self.impl.world()
-        needs: List[object] = [None] * world
-        dist.all_gather_object(needs, need, group=self.group)
-        need = max(int(x) for x in needs)
+        # need AND verified capacity are agreed on: a rank whose last mapping attempt failed reports the
+        # capacity it has verified (engine.cpp commits a window only in a clean ipc_open), so every rank
+        # takes the same branch even after a failed growth that a caller caught
+        mine = (int(self.impl.ipc_need()), int(self.impl.ipc_capacity()))
+        both: List[object] = [None] * world
+        dist.all_gather_object(both, mine, group=self.group)
+        need = max(int(n) for n, _ in both)
+        cap = min(int(c) for _, c in both)
         if force:
-            need = max(need, int((int(self.impl.ipc_capacity()) - (1 << 20)) / 1.25), 1 << 16)
-        elif need <= int(self.impl.ipc_capacity()):
+            need = max(need, int((cap - (1 << 20)) / 1.25), 1 << 16)
+        elif need <= cap:
             return
         self.impl.synchronize()  # nothing of mine in flight reads a peer window
         dist.barrier(group=self.group)  # ... nor of any peer's that reads mine
@@ -265,12 +269,15 @@ class NativeEngine:
 
     def bucket_allreduce_list(self, flat: torch.Tensor, algo: str, grads, offsets, average: bool = True) -> None:
         """Gather autograd-owned ``grads`` into ``flat`` at ``offsets`` on the comm stream, then reduce."""
+        self._lazy_reserve(algo, flat)
         self.impl.bucket_allreduce_list(flat, algo_code(algo), average, list(grads), list(offsets))
 
     def bucket_allreduce_group(self, group: torch.Tensor, starts, counts, algo: str, grads, offsets,
                                average: bool = True) -> None:
         """Per-tensor collectives of a fusion-off launch group (members are slices of ``group``): one
-        gather of ``grads`` at ``offsets`` (group-relative), one staging cast and one RCCL group."""
+        gather of ``grads`` at ``offsets`` (group-relative), one staging cast and one RCCL group. IPC schedules
+        stage the whole group buffer, so their windows are grown for it first (advisor r5)."""
+        self._lazy_reserve(algo, group)
         self.impl.bucket_allreduce_group(group, list(starts), list(counts), algo_code(algo), average, list(grads),
                                          list(offsets))
 

@@ -102,13 +102,15 @@ class LaunchGroup:
 
 
 def launch_groups(buckets: Sequence[Bucket], max_bytes: int = LAUNCH_GROUP_BYTES, max_tensors: int = LAUNCH_GROUP_MAX,
-                  span: int = LAUNCH_GROUP_SPAN) -> List[List[Bucket]]:
-    """Per-dtype greedy grouping of buckets in index (backward) order; returned in launch order (by the
-    index of each group's last bucket)."""
+                  span: int = LAUNCH_GROUP_SPAN, key=None) -> List[List[Bucket]]:
+    """Greedy grouping of buckets in index (backward) order, per dtype and per ``key(bucket)`` (the executor's
+    algorithm for the bucket: a group runs ONE algorithm for all members, so members never mix schedules whose
+    plans / IPC windows were sized for another); returned in launch order (by the index of each group's last
+    bucket)."""
     done: List[List[Bucket]] = []
     open_: dict = {}
     for pos, b in enumerate(buckets):
-        dt = b.params[0].dtype
+        dt = (b.params[0].dtype, key(b) if key is not None else None)
         nb = b.padded_numel * b.params[0].element_size()
         cur = open_.get(dt)
         if cur is not None:
@@ -217,7 +219,8 @@ class GradSync:
     def _wants_groups(self) -> bool:
         ex = self.executor
         per_tensor = len(self.buckets) > 1 and all(len(b.params) == 1 for b in self.buckets)
-        return (per_tensor and self.comm_dtype is None and self.overlap and self.device.type == "cuda"
+        # DLA_LAUNCH_GROUPS=0: strict fusion off -- every tensor its own collective launch, as the reference
+        return (knobs.flag("LAUNCH_GROUPS") and per_tensor and self.comm_dtype is None and self.overlap and self.device.type == "cuda"
                 and getattr(ex, "supports_steal", False) and hasattr(ex, "submit_group")
                 and not getattr(ex, "passthrough", False))
 
@@ -227,7 +230,8 @@ class GradSync:
             b.group = None
         if not self._wants_groups():
             return
-        for members in launch_groups(self.buckets):
+        algo_for = getattr(self.executor, "algorithm_for", None)
+        for members in launch_groups(self.buckets, key=algo_for):
             starts, n = [], 0
             for b in members:
                 starts.append(n)
@@ -255,6 +259,11 @@ class GradSync:
             executor.reserve(self.buckets)
             if self.groups and hasattr(executor, "reserve_groups"):
                 executor.reserve_groups(self.groups)
+    def regroup(self) -> None:
+        """Rebuild the fusion-off launch groups and re-reserve after the executor's per-bucket algorithms were
+        set (the autotuner runs after construction; a group must not span two algorithms)."""
+        self.set_executor(self.executor)
+
     def _install_views(self, install: bool = True):
         for b in self.buckets:
             b.views = []

@@ -209,3 +209,102 @@ def test_autotune_isolates_hanging_and_erroring_candidates():
         assert "did not complete" in ex["hang"]
         assert "rank 1: RuntimeError: CommEngine: RCCL async error" in ex["async_err"]
     assert a["best"] == "builtin" and set(a["per"].values()) <= {"builtin", "ring"}
+
+
+# ---- robust per-bucket decisions ---------------------------------------------
+# Ground truth: 'builtin' (low alpha, low bandwidth) and 'ring' (high alpha, twice the bandwidth) cross near
+# 19.5 MiB; 'twin' costs exactly what builtin costs. Every repetition carries +-5 % seeded jitter (rank-
+# dependent) and one rep in 8 a 3x outlier, as comm-stream timings do. Whatever the seed, the decision must be
+# the same, twin must never be picked, and along increasing bucket size the choice may change only once.
+
+JIT_COST = {"builtin": (20.0, 0.004), "ring": (60.0, 0.002), "twin": (20.0, 0.004)}  # (alpha us, us per KiB)
+
+
+class JitterEngine(FakeEngine):
+    def __init__(self, rank, world, seed):
+        super().__init__(rank, world)
+        import random
+
+        self.rng = random.Random(seed * 7919 + rank)
+
+    def allreduce(self, buf, algo, average=True):
+        dist.all_reduce(buf)
+        if average:
+            buf /= self.impl.world()
+        a, b = JIT_COST[algo]
+        # the buffers are SCALE x smaller than the sizes they stand for (a CPU gloo all-reduce of 256 MiB per rep
+        # would dominate the test); the simulated time is that of the full size
+        ms = (a + b * SCALE * buf.numel() * buf.element_size() / 1024) * 1e-3
+        ms *= 1.0 + self.rng.uniform(-0.05, 0.05)
+        if self.rng.random() < 0.125:
+            ms *= 3.0
+        if self._timing:
+            self._t += ms
+
+
+SIZES_MIB = (0.25, 1.0, 4.0, 5.91, 6.11, 8.0, 16.0, 96.0, 128.0, 256.0)
+SCALE = 4096
+
+
+def _tune_jitter(rank, world, seed):
+    eng = JitterEngine(rank, world, seed)
+    at.GRID_MIB = tuple(m / SCALE for m in (0.25, 1.0, 4.0, 16.0, 64.0))
+    t = at.Autotune(eng, torch.float32, list(JIT_COST))
+    t.run_grid()
+    sizes = [int(m * (1 << 20) / SCALE) // 4 for m in SIZES_MIB]
+    per = t.run_buckets(sizes)
+    return [per[n] for n in sizes]
+
+
+def test_per_bucket_decision_is_stable_under_jitter():
+    decisions = [dist_util.run(_tune_jitter, 2, seed) for seed in range(4)]
+    for d in decisions:
+        assert d[0] == d[1]  # ranks agree
+    first = decisions[0][0]
+    for d in decisions[1:]:
+        assert d[0] == first, (first, d[0])  # identical across seeds
+    assert "twin" not in first
+    changes = sum(1 for x, y in zip(first, first[1:]) if x != y)
+    assert changes <= 1, first
+    assert first[:7] == ["builtin"] * 7 and first[-1] == "ring", first
+
+
+def test_noise_winner_within_spread_is_not_chosen():
+    ok = {"builtin": True, "ring": True}
+    table = {"builtin": {1: 1.00}, "ring": {1: 0.90}}
+    assert at.choose_per_size(table, ok, [1], "builtin") == {1: "ring"}
+    spread = {"builtin": {1: 0.05}, "ring": {1: 0.01}}  # 10 % faster, but within 3 x the 5 % spread (MAD)
+    assert at.choose_per_size(table, ok, [1], "builtin", spread=spread) == {1: "builtin"}
+    # the fitted lines disagree with the measurement: stays on the default
+    models = {"builtin": at.cm.CollectiveModel("fit", 0.0, 1e-9), "ring": at.cm.CollectiveModel("fit", 0.0, 2e-9)}
+    assert at.choose_per_size(table, ok, [1], "builtin", models=models) == {1: "builtin"}
+
+
+# ---- time budget -------------------------------------------------------------
+
+class SlowEngine(JitterEngine):
+    def reserve(self, algo, sizes, dtype):
+        if algo == "twin":
+            import time
+
+            time.sleep(1.5)  # a candidate whose setup (e.g. probe communicator, IPC mapping) is slow
+
+
+def _tune_budget(rank, world):
+    eng = SlowEngine(rank, world, 0)
+    at.GRID_MIB = tuple(m / SCALE for m in (0.25, 1.0, 4.0))
+    t = at.Autotune(eng, torch.float32, ["builtin", "twin", "ring"], reps=3, budget_s=1.0)
+    t.run_grid()
+    per = t.run_buckets([256, 4096])
+    return {"per": per, "report": t.report(), "ok": t.ok}
+
+
+def test_budget_skips_remaining_candidates_and_finishes_on_builtin():
+    a, b = dist_util.run(_tune_budget, 2)
+    for r in (a, b):
+        ex = r["report"]["excluded"]
+        assert set(ex) == {"twin", "ring"}, ex
+        assert all(v.startswith("budget") for v in ex.values()), ex
+        assert set(r["per"].values()) == {"builtin"}
+        assert r["report"]["autotune_s"] >= 1.0 and r["report"]["budget_s"] == 1.0
+    assert a["per"] == b["per"]

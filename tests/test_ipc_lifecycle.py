@@ -21,7 +21,8 @@ class _FakeImpl:
     def __init__(self, rank, world, stale_opens):
         self.r, self.w = rank, world
         self.stale_opens = stale_opens  # this rank's first N opens see a stale peer mapping
-        self.cap = 0
+        self.cap = 0      # committed (verified) window bytes -- what ipc_capacity() reports
+        self.pending = 0  # allocated, not yet verified (engine.cpp ipc_alloc -> ipc_open commits it)
         self.allocs = []
         self.opens = 0
 
@@ -40,7 +41,7 @@ class _FakeImpl:
     def ipc_alloc(self, size, nonce):
         assert nonce & 1 and 0 < nonce < 1 << 64
         self.allocs.append(nonce)
-        self.cap = size
+        self.pending = size
         return f"handle-{self.r}-{len(self.allocs)}-{nonce}".encode()
 
     def ipc_open(self, handles, nonces):
@@ -49,6 +50,7 @@ class _FakeImpl:
             assert h.decode().endswith(f"-{n}"), "ipc_open got a nonce that is not the owner's stamp"
         if self.opens <= self.stale_opens:
             return f"rank {(self.r + 1) % self.w}'s window maps to nonce 0, expected {nonces[(self.r + 1) % self.w]:x}"
+        self.cap, self.pending = self.pending, 0
         return ""
 
 
@@ -60,7 +62,12 @@ def _map(rank, world, stale_on_rank1):
         eng._map_windows()
     except RuntimeError as e:
         out["raised"] = str(e)
-    out.update(allocs=len(impl.allocs), stale=eng.stale_mappings, opens=impl.opens)
+    out.update(allocs=len(impl.allocs), stale=eng.stale_mappings, opens=impl.opens, cap=impl.ipc_capacity(), rank=rank)
+    if out["raised"] is not None:  # a caller that caught the failure reserves again: every rank re-maps
+        impl.stale_opens = 0
+        before = len(impl.allocs)
+        eng._map_windows()
+        out["agreed_remap"] = len(impl.allocs) == before + 1 and impl.ipc_capacity() > 0
     # the next growth starts from an agreed state: a forced new generation works on every rank
     if out["raised"] is None:
         impl.stale_opens = 0
@@ -82,6 +89,12 @@ def test_persistently_stale_mapping_raises_everywhere():
     for r in res:
         assert r["raised"] and "stale" in r["raised"], r
         assert r["allocs"] == NativeEngine.MAP_ATTEMPTS, r
+        # advisor r5: a window that was never verified is not reported as capacity, so the next reserve
+        # maps again (or refuses) instead of running collectives past the old, smaller mapping
+        # rank 0 verified its own mappings; rank 1 never did: rank 1 reports no capacity, and the next
+        # _map_windows on both ranks sees the agreed minimum and maps again together
+        assert r["cap"] == (0 if r["rank"] == 1 else r["cap"]), r
+        assert r["agreed_remap"], r
 
 
 def test_clean_mapping_maps_once():
