@@ -135,6 +135,61 @@ def test_fusion_off_launch_groups_match_single_device(world1, staged):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6, msg=n)
 
 
+def test_fusion_off_strict_one_collective_per_tensor(world1):
+    """DLA_LAUNCH_GROUPS=0, the reference's fusion-off semantics (/root/reference/src/main.py:168-179,222-230;
+    ourdist.py:54-68 with grouping_size=0): every gradient tensor is its own collective AND its own launch. On
+    the forced world-1 data path (fp32 staging, RCCL 1-rank all-reduce) the engine's issue counters must show
+    N launches of N collectives per step for N tensors in strict mode, fewer launches of the same N collectives
+    in the grouped mode, and the two trainings must agree bit for bit."""
+    from distributed_learning_amd import knobs
+    from distributed_learning_amd.models import resnet18
+    from distributed_learning_amd.ops import nn as dnn
+    from distributed_learning_amd.parallel import PipelinedFusedDP, make_reducer
+    from distributed_learning_amd.parallel.executor import NativeStreamExecutor
+
+    dnn.set_backend("native")
+    det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    saved = knobs._CACHE.get("LAUNCH_GROUPS")
+    out = {}
+    try:
+        for mode in ("1", "0"):
+            knobs._CACHE["LAUNCH_GROUPS"] = mode
+            seen = {}
+
+            def wrap_dp(m, seen=seen):
+                red = make_reducer("immediate", "builtin", native=True)
+                w = PipelinedFusedDP(m, red, 0, broadcast=False)
+                red.engine.impl.set_force(True)
+                red.engine.set_accum_fp32(True)
+                w.sync.set_executor(NativeStreamExecutor(red.engine, "builtin", passthrough=False))
+                red.engine.impl.collective_counts(True)
+                seen.update(groups=len(w.sync.groups), tensors=len(w.sync.buckets), engine=red.engine)
+                return w
+
+            m, losses = _train(lambda: resnet18(10), wrap_dp, 3, True)
+            torch.cuda.synchronize()
+            coll, units = (int(v) for v in seen["engine"].impl.collective_counts(True))
+            out[mode] = dict(seen, coll=coll, units=units, losses=losses,
+                             params=[p.detach().clone() for p in m.parameters()])
+    finally:
+        if saved is None:
+            knobs._CACHE.pop("LAUNCH_GROUPS", None)
+        else:
+            knobs._CACHE["LAUNCH_GROUPS"] = saved
+        dnn.set_backend("torch")
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
+    g, s = out["1"], out["0"]
+    n = s["tensors"]
+    assert n == g["tensors"] == 62
+    assert s["groups"] == 0 and 0 < g["groups"] < n
+    assert s["coll"] == 3 * n and s["units"] == 3 * n, s  # strict: one launch per tensor per step
+    assert g["coll"] == 3 * n and g["units"] == 3 * g["groups"], g  # grouped: same collectives, fewer launches
+    assert s["losses"] == g["losses"]
+    for a, b in zip(s["params"], g["params"]):
+        assert torch.equal(a, b)
+
+
 def test_engine_algorithms_world1(world1):
     from distributed_learning_amd.parallel.engine import ALGO_CODES, NativeEngine
 
