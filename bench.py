@@ -100,7 +100,7 @@ def parse():
     ap.add_argument("--precision", default=knobs.get("PRECISION"), choices=["autocast", "bf16", "fp32"],
                     help="bf16: bf16 weights + fp32 master weights in the fused optimizer (no per-step weight casts, "
                          "bf16 gradients on the wire); autocast: fp32 params + bf16 autocast; fp32: the reference's "
-                         "precision (fp32 weights and activations; native BN/pool/loss/SGD kernels + MIOpen convs, "
+                         "precision (fp32 weights and activations; native BN/pool/loss/SGD kernels + fp32 MFMA convs, "
                          "or with --kernels torch the stock NCHW path)")
     ap.add_argument("--conv", default=knobs.get("CONV"), choices=["miopen", "native"],
                     help="1x1 convolutions on the native MFMA GEMMs (with fused BN statistics) or MIOpen")
@@ -352,6 +352,8 @@ def main():
         torch.backends.cuda.matmul.allow_tf32 = False
     dnn.set_backend(a.kernels)
     dnn.set_native_conv(a.conv == "native" and not fp32)
+    # fp32 convolutions on the fp32 matrix-core kernels (ops/conv_f32.py) instead of MIOpen
+    dnn.set_native_conv_f32(fp32 and a.conv == "native" and a.kernels == "native")
     if a.wgrad_overlap_rows is not None:
         from distributed_learning_amd.ops import conv as nconv
 
@@ -525,7 +527,7 @@ def main():
                 "same_device": same,
                 "kernels": a.kernels,
                 "precision": a.precision,
-                "conv1x1": "miopen" if fp32 else a.conv,
+                "conv1x1": ("native-f32" if dnn.native_conv_f32() else "miopen") if fp32 else a.conv,
                 "layout": "nchw" if fp32_torch else "channels_last",
                 # 1x1 backward: both gradients in one pass over dY (gemm_dual.hip), the consuming BN's apply
                 # fused where served (ops/conv.py DUAL_*); what actually ran this process

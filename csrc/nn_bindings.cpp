@@ -636,6 +636,58 @@ std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at:
   return {C, part};
 }
 
+// ---- fp32 convolutions (conv_f32.hip) ------------------------------------------------------------------------
+// x: [N, C, H, W] in channels_last memory (NHWC), fp32; w: [Cout, R, S, C] contiguous fp32 (OHWI). Returns y [N, Cout,
+// OH, OW] channels_last, or adds into `out` (same shape / layout) when given.
+static void check_nhwc_f32(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.scalar_type() == at::kFloat, what, ": 4-D fp32 CUDA tensor");
+  TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), what, ": channels_last memory");
+  check_span(t, what);
+}
+
+at::Tensor conv_f32_fwd(at::Tensor x, at::Tensor w, int64_t pad, int64_t stride, c10::optional<at::Tensor> out) {
+  check_nhwc_f32(x, "conv_f32_fwd x");
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.scalar_type() == at::kFloat && w.is_contiguous(),
+              "conv_f32_fwd: w must be a contiguous fp32 [Cout, R, S, C] tensor");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int Cout = (int)w.size(0), R = (int)w.size(1), S = (int)w.size(2);
+  TORCH_CHECK(w.size(3) == C, "conv_f32_fwd: weight channels ", w.size(3), " != input channels ", C);
+  TORCH_CHECK(stride >= 1 && pad >= 0, "conv_f32_fwd: bad stride / padding");
+  const int OH = (H + 2 * (int)pad - R) / (int)stride + 1, OW = (W + 2 * (int)pad - S) / (int)stride + 1;
+  TORCH_CHECK(OH > 0 && OW > 0, "conv_f32_fwd: empty output");
+  TORCH_CHECK(conv_f32_supported(C, Cout, (int64_t)N * OH * OW, R * S * C),
+              "conv_f32_fwd: needs C % 4 == 0, Cout % 4 == 0 and fewer than 2^24 output pixels");
+  at::Tensor y;
+  if (out.has_value() && out->defined()) {
+    y = *out;
+    check_nhwc_f32(y, "conv_f32_fwd out");
+    TORCH_CHECK(y.size(0) == N && y.size(1) == Cout && y.size(2) == OH && y.size(3) == OW, "conv_f32_fwd: out shape");
+  } else {
+    y = at::empty({N, Cout, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  }
+  launch_conv_f32_fwd(x.data_ptr<float>(), N, H, W, C, w.data_ptr<float>(), Cout, R, S, (int)pad, (int)stride,
+                      y.data_ptr<float>(), out.has_value() && out->defined(), current_stream(x));
+  return y;
+}
+
+// dw [Cout, R, S, C] of a conv with input x (channels_last fp32) and output gradient dy (channels_last fp32)
+at::Tensor conv_f32_wgrad(at::Tensor dy, at::Tensor x, int64_t R, int64_t S, int64_t pad, int64_t stride) {
+  check_nhwc_f32(dy, "conv_f32_wgrad dy");
+  check_nhwc_f32(x, "conv_f32_wgrad x");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Cout = (int)dy.size(1);
+  const int OH = (H + 2 * (int)pad - (int)R) / (int)stride + 1, OW = (W + 2 * (int)pad - (int)S) / (int)stride + 1;
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == OH && dy.size(3) == OW, "conv_f32_wgrad: dy shape does not match x");
+  const int64_t M = (int64_t)N * OH * OW;
+  const int K = (int)(R * S * C);
+  TORCH_CHECK(conv_f32_supported(C, Cout, M, K), "conv_f32_wgrad: needs C % 4 == 0, Cout % 4 == 0, M < 2^24");
+  at::Tensor dw = at::empty({Cout, R, S, C}, x.options());
+  const int splits = conv_f32_wgrad_splits(M, Cout, K);
+  at::Tensor part = at::empty({(int64_t)splits * Cout * K}, x.options());
+  launch_conv_f32_wgrad(dy.data_ptr<float>(), x.data_ptr<float>(), N, H, W, C, Cout, (int)R, (int)S, (int)pad,
+                        (int)stride, part.data_ptr<float>(), splits, dw.data_ptr<float>(), false, current_stream(x));
+  return dw;
+}
+
 // out = scale * A^T @ B with A [K, Mo], B [K, No] (reduction over the long row dim, split-K).
 at::Tensor gemm_tn(at::Tensor A, at::Tensor B, c10::ScalarType out_dtype, double scale) {
   check_mat(A, "A");
@@ -1128,6 +1180,13 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("mask") = pybind11::none());
   m.def("conv1x1_dual_bn_ok", [](int64_t M, int64_t Cin, int64_t Cout) { return conv1x1_dual_bn_ok(M, (int)Cin, (int)Cout); },
         "the one-pass 1x1 gradient kernel can also apply the consuming BN's backward for this shape");
+  m.def("conv_f32_fwd", &conv_f32_fwd, "fp32 implicit-GEMM convolution (v_mfma_f32_16x16x4_f32), NHWC / OHWI",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("pad"), pybind11::arg("stride") = 1,
+        pybind11::arg("out") = c10::nullopt);
+  m.def("set_conv_f32_buffers", &set_conv_f32_buffers, "fp32 conv main loop: 1 or 2 (default) LDS buffers");
+  m.def("conv_f32_wgrad", &conv_f32_wgrad, "fp32 convolution weight gradient [Cout, R, S, C] (split over pixels)",
+        pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("pad"),
+        pybind11::arg("stride") = 1);
   m.def("gemm_tn", &gemm_tn, "A^T @ B (bf16 MFMA, split-K over rows)", pybind11::arg("A"), pybind11::arg("B"),
         pybind11::arg("out_dtype") = at::kFloat, pybind11::arg("scale") = 1.0);
   m.def("bn_act_fwd", &bn_act_fwd, "fused BatchNorm(+residual)(+ReLU) forward, NHWC", pybind11::arg("x"),

@@ -87,6 +87,33 @@ def native_conv() -> bool:
     return _NATIVE_CONV
 
 
+# fp32 convolutions on the fp32 matrix-core kernels (ops/conv_f32.py) -- the --precision fp32 path
+_NATIVE_F32 = False
+
+
+def set_native_conv_f32(on: bool) -> None:
+    global _NATIVE_F32
+    if on:
+        from . import _ext
+
+        _ext.require()
+    _NATIVE_F32 = bool(on)
+
+
+def native_conv_f32() -> bool:
+    return _NATIVE_F32
+
+
+def _conv(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    """``conv(x)``: fp32 inputs on the native fp32 MFMA kernels when switched on and supported."""
+    if _NATIVE_F32 and _BACKEND == "native" and x.is_cuda and x.dtype == torch.float32:
+        from . import conv_f32
+
+        if conv_f32.supported(x, conv):
+            return conv_f32.conv(x, conv)
+    return conv(x)
+
+
 def linear(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
     """``fc(x)``; with the native backend and native convs, on the MFMA GEMMs (ops/linear.py)."""
     if _BACKEND == "native" and _NATIVE_CONV and x.is_cuda:
@@ -121,7 +148,7 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
     if presubsampled:
         y = F.conv2d(x, conv.weight, conv.bias, 1, conv.padding, conv.dilation, conv.groups)
         return bn_act(y, bn, relu, residual)
-    return bn_act(conv(x), bn, relu, residual)
+    return bn_act(_conv(x, conv), bn, relu, residual)
 
 
 def _native_conv_stats(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool, presubsampled: bool = False):
@@ -179,7 +206,7 @@ def conv_bn_act_maxpool(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, po
             r = _native_conv_stats(x, conv, bn.training)
             if r is not None:
                 return fused_bn_relu_maxpool(r[0], bn, pool, r[1])
-        return fused_bn_relu_maxpool(conv(x), bn, pool)
+        return fused_bn_relu_maxpool(_conv(x, conv), bn, pool)
     return pool(conv_bn_act(x, conv, bn, relu=True))
 
 
