@@ -300,12 +300,14 @@ void set_gemm_direct(int mode);
 // [N][OH][OW][Cout]; C % 4 == 0, Cout % 4 == 0, N * OH * OW < 2^24. accumulate: y += conv instead of y = conv.
 bool conv_f32_supported(int C, int Cout, int64_t M, int K);
 void set_conv_f32_buffers(int nb);  // 1 or 2 (default) LDS buffers of the fp32 GEMM main loop (A/B)
-void launch_conv_f32_fwd(const float* x, int N, int H, int W, int C, const float* w, int Cout, int R, int S, int pad,
-                         int stride, float* y, bool accumulate, hipStream_t st);
+// ldx: elements between consecutive pixels of x (C, or more when x is a channel slice of a wider NHWC tensor)
+void launch_conv_f32_fwd(const float* x, int64_t ldx, int N, int H, int W, int C, const float* w, int Cout, int R,
+                         int S, int pad, int stride, float* y, bool accumulate, hipStream_t st);
 // dw [Cout][R][S][C] (+)= sum over pixels of dy [N * OH * OW][Cout] x im2col(x); partial: splits * Cout * R * S * C floats
 int conv_f32_wgrad_splits(int64_t M, int Cout, int K);
-void launch_conv_f32_wgrad(const float* dy, const float* x, int N, int H, int W, int C, int Cout, int R, int S, int pad,
-                           int stride, float* partial, int splits, float* dw, bool accumulate, hipStream_t st);
+void launch_conv_f32_wgrad(const float* dy, const float* x, int64_t ldx, int N, int H, int W, int C, int Cout, int R,
+                           int S, int pad, int stride, float* partial, int splits, float* dw, bool accumulate,
+                           hipStream_t st);
 // BatchNorm-backward reduction fused into a bf16-output GEMM epilogue (the output is the BN's dy):
 // x = the BN input [M, N], ws = its 7N workspace, mask/mode as launch_bn_bwd (0, 1 or 2),
 // part = [stats_rows][N][2] partial (sum dy', sum dy'(x - mean)).

@@ -7,7 +7,7 @@
 //   forward   Y[m, co]           = sum_(tap, ci) X[pixel(m) + tap, ci] W[co, tap, ci]          (A = im2col X, B = W)
 //   dgrad     dX = the forward of dY with the flipped, transposed weights (stride 1 only; the host transforms W)
 //   wgrad     dW[co, (tap, ci)]  = sum_m dY[m, co] X[pixel(m) + tap, ci]                      (split over m)
-// NHWC (channels_last) activations, OHWI weights ([co][R][S][ci], k = tap * C + ci), C % 4 == 0 (16-byte chunks never
+// NHWC (channels_last) activations -- the input may be a channel slice of a wider tensor (pixel stride ldx) --, OHWI weights ([co][R][S][ci], k = tap * C + ci), C % 4 == 0 (16-byte chunks never
 // cross a tap), any R x S, padding, stride (the 7x7/s2 stem after a zero channel pads its 3 input channels to 4).
 //
 // Kernel: 256 threads = 2 x 2 waves, BM x BN tile (128 x 128 or 64 x 64), 32-deep k-steps staged through LDS with
@@ -52,6 +52,7 @@ __device__ __forceinline__ int km_off(int k, int col) {
 // Stride-s implicit-GEMM geometry over an NHWC fp32 input
 struct ConvGeomF {
   const float* x;
+  int64_t ldp;  // elements between consecutive pixels of x (C, or the width of the tensor x is a channel slice of)
   int N, H, W, C;
   int R, S, pad, stride;
   int OH, OW;
@@ -85,7 +86,7 @@ struct AConv {
       if (m < g.M) pixel_of(g, m, n, oh, ow);
       ih0[i] = m < g.M ? oh * g.stride - g.pad : -(1 << 28);  // out-of-range rows fail the bounds test
       iw0[i] = ow * g.stride - g.pad;
-      base[i] = (((int64_t)n * g.H) * g.W) * g.C;
+      base[i] = (((int64_t)n * g.H) * g.W) * g.ldp;
     }
   }
   __device__ void load(int k0, f32x4_t (&r)[CH]) const {
@@ -101,7 +102,7 @@ struct AConv {
     for (int i = 0; i < CH; ++i) {
       const int ih = ih0[i] + rr, iw = iw0[i] + ss;
       const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-      r[i] = ok ? *reinterpret_cast<const f32x4_t*>(g.x + base[i] + ((int64_t)ih * g.W + iw) * g.C + c) : zero4();
+      r[i] = ok ? *reinterpret_cast<const f32x4_t*>(g.x + base[i] + ((int64_t)ih * g.W + iw) * g.ldp + c) : zero4();
     }
   }
   __device__ void store(float* s, const f32x4_t (&r)[CH]) const {
@@ -193,7 +194,7 @@ struct KConv {
       if (mok) pixel_of(g, m, n, oh, ow);
       const int ih = oh * g.stride + dh, iw = ow * g.stride + dw;
       const bool ok = mok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-      r[i] = ok ? *reinterpret_cast<const f32x4_t*>(g.x + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + c) : zero4();
+      r[i] = ok ? *reinterpret_cast<const f32x4_t*>(g.x + (((int64_t)n * g.H + ih) * g.W + iw) * g.ldp + c) : zero4();
     }
   }
   __device__ void store(float* s, const f32x4_t (&r)[CH]) const {
@@ -308,9 +309,10 @@ __global__ __launch_bounds__(kFT, 2) void gemm_f32_kernel(LA la, LB lb, float* _
     }
 }
 
-ConvGeomF make_geom(const float* x, int N, int H, int W, int C, int R, int S, int pad, int stride) {
+ConvGeomF make_geom(const float* x, int64_t ldp, int N, int H, int W, int C, int R, int S, int pad, int stride) {
   ConvGeomF g;
   g.x = x;
+  g.ldp = ldp;
   g.N = N, g.H = H, g.W = W, g.C = C, g.R = R, g.S = S, g.pad = pad, g.stride = stride;
   g.OH = (H + 2 * pad - R) / stride + 1;
   g.OW = (W + 2 * pad - S) / stride + 1;
@@ -378,9 +380,9 @@ bool conv_f32_supported(int C, int Cout, int64_t M, int K) {
   return C % 4 == 0 && Cout % 4 == 0 && M > 0 && M < (int64_t(1) << 24) && K < (1 << 24);
 }
 
-void launch_conv_f32_fwd(const float* x, int N, int H, int W, int C, const float* w, int Cout, int R, int S, int pad,
-                         int stride, float* y, bool accumulate, hipStream_t st) {
-  const ConvGeomF g = make_geom(x, N, H, W, C, R, S, pad, stride);
+void launch_conv_f32_fwd(const float* x, int64_t ldx, int N, int H, int W, int C, const float* w, int Cout, int R,
+                         int S, int pad, int stride, float* y, bool accumulate, hipStream_t st) {
+  const ConvGeomF g = make_geom(x, ldx, N, H, W, C, R, S, pad, stride);
   const int bn = pick_f32_width(Cout), bm = pick_f32_rows(g.M, Cout, bn);
   const int acc = accumulate ? 1 : 0;
 #define DLA_F32F(BM_, BN_) \
@@ -404,9 +406,10 @@ int conv_f32_wgrad_splits(int64_t M, int Cout, int K) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(by_k, std::max(1, 512 / tiles)));
 }
 
-void launch_conv_f32_wgrad(const float* dy, const float* x, int N, int H, int W, int C, int Cout, int R, int S, int pad,
-                           int stride, float* partial, int splits, float* dw, bool accumulate, hipStream_t st) {
-  const ConvGeomF g = make_geom(x, N, H, W, C, R, S, pad, stride);
+void launch_conv_f32_wgrad(const float* dy, const float* x, int64_t ldx, int N, int H, int W, int C, int Cout, int R,
+                           int S, int pad, int stride, float* partial, int splits, float* dw, bool accumulate,
+                           hipStream_t st) {
+  const ConvGeomF g = make_geom(x, ldx, N, H, W, C, R, S, pad, stride);
   int64_t kps = (g.M + splits - 1) / splits;
   kps = (kps + kFK - 1) / kFK * kFK;
   splits = (int)((g.M + kps - 1) / kps);

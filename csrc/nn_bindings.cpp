@@ -637,7 +637,8 @@ std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at:
 }
 
 // ---- fp32 convolutions (conv_f32.hip) ------------------------------------------------------------------------
-// x: [N, C, H, W] in channels_last memory (NHWC), fp32; w: [Cout, R, S, C] contiguous fp32 (OHWI). Returns y [N, Cout,
+// x: [N, C, H, W] in channels_last memory (NHWC) or a channel slice of such a tensor, fp32; w: [Cout, R, S, C]
+// contiguous fp32 (OHWI). Returns y [N, Cout,
 // OH, OW] channels_last, or adds into `out` (same shape / layout) when given.
 static void check_nhwc_f32(const at::Tensor& t, const char* what) {
   TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.scalar_type() == at::kFloat, what, ": 4-D fp32 CUDA tensor");
@@ -645,8 +646,21 @@ static void check_nhwc_f32(const at::Tensor& t, const char* what) {
   check_span(t, what);
 }
 
+// channels_last, or a channel slice of a channels_last tensor: unit channel stride, pixel stride ldp >= C (a multiple of
+// 4, 16-byte aligned base); returns ldp
+static int64_t check_nhwc_f32_slice(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.scalar_type() == at::kFloat, what, ": 4-D fp32 CUDA tensor");
+  const int64_t ldp = t.stride(3);
+  const bool ok = t.stride(1) == 1 && ldp >= t.size(1) && t.stride(2) == ldp * t.size(3) &&
+                  t.stride(0) == t.stride(2) * t.size(2) && ldp % 4 == 0 && (uintptr_t)t.data_ptr() % 16 == 0;
+  TORCH_CHECK(ok || t.is_contiguous(at::MemoryFormat::ChannelsLast), what,
+              ": channels_last memory or a 16-byte aligned channel slice of it");
+  check_span(t, what);
+  return t.is_contiguous(at::MemoryFormat::ChannelsLast) ? t.size(1) : ldp;
+}
+
 at::Tensor conv_f32_fwd(at::Tensor x, at::Tensor w, int64_t pad, int64_t stride, c10::optional<at::Tensor> out) {
-  check_nhwc_f32(x, "conv_f32_fwd x");
+  const int64_t ldx = check_nhwc_f32_slice(x, "conv_f32_fwd x");
   TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.scalar_type() == at::kFloat && w.is_contiguous(),
               "conv_f32_fwd: w must be a contiguous fp32 [Cout, R, S, C] tensor");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
@@ -665,7 +679,7 @@ at::Tensor conv_f32_fwd(at::Tensor x, at::Tensor w, int64_t pad, int64_t stride,
   } else {
     y = at::empty({N, Cout, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   }
-  launch_conv_f32_fwd(x.data_ptr<float>(), N, H, W, C, w.data_ptr<float>(), Cout, R, S, (int)pad, (int)stride,
+  launch_conv_f32_fwd(x.data_ptr<float>(), ldx, N, H, W, C, w.data_ptr<float>(), Cout, R, S, (int)pad, (int)stride,
                       y.data_ptr<float>(), out.has_value() && out->defined(), current_stream(x));
   return y;
 }
@@ -673,7 +687,7 @@ at::Tensor conv_f32_fwd(at::Tensor x, at::Tensor w, int64_t pad, int64_t stride,
 // dw [Cout, R, S, C] of a conv with input x (channels_last fp32) and output gradient dy (channels_last fp32)
 at::Tensor conv_f32_wgrad(at::Tensor dy, at::Tensor x, int64_t R, int64_t S, int64_t pad, int64_t stride) {
   check_nhwc_f32(dy, "conv_f32_wgrad dy");
-  check_nhwc_f32(x, "conv_f32_wgrad x");
+  const int64_t ldx = check_nhwc_f32_slice(x, "conv_f32_wgrad x");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Cout = (int)dy.size(1);
   const int OH = (H + 2 * (int)pad - (int)R) / (int)stride + 1, OW = (W + 2 * (int)pad - (int)S) / (int)stride + 1;
   TORCH_CHECK(dy.size(0) == N && dy.size(2) == OH && dy.size(3) == OW, "conv_f32_wgrad: dy shape does not match x");
@@ -683,7 +697,7 @@ at::Tensor conv_f32_wgrad(at::Tensor dy, at::Tensor x, int64_t R, int64_t S, int
   at::Tensor dw = at::empty({Cout, R, S, C}, x.options());
   const int splits = conv_f32_wgrad_splits(M, Cout, K);
   at::Tensor part = at::empty({(int64_t)splits * Cout * K}, x.options());
-  launch_conv_f32_wgrad(dy.data_ptr<float>(), x.data_ptr<float>(), N, H, W, C, Cout, (int)R, (int)S, (int)pad,
+  launch_conv_f32_wgrad(dy.data_ptr<float>(), x.data_ptr<float>(), ldx, N, H, W, C, Cout, (int)R, (int)S, (int)pad,
                         (int)stride, part.data_ptr<float>(), splits, dw.data_ptr<float>(), false, current_stream(x));
   return dw;
 }

@@ -53,6 +53,11 @@ class Inception(nn.Module):
 
             if ninc.supported(self, x):  # no concat copy, no autograd sum of x's four gradients
                 return ninc.inception_forward(self, x)
+        if dnn.get_backend() == "native" and dnn.native_conv_f32() and x.is_cuda:
+            from ..ops import inception_f32
+
+            if inception_f32.supported(self, x):  # the three 1x1 convs on x as one fp32 GEMM, one BN pass
+                return inception_f32.forward(self, x)
         return torch.cat([self.branch1(x), self.branch2(x), self.branch3(x), self.branch4(x)], 1)
 
 

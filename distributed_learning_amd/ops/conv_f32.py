@@ -47,6 +47,16 @@ def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     return x.shape[0] * oh * ow < (1 << 24) and x.numel() * 4 < (1 << 31)
 
 
+def nhwc_view_ok(x: torch.Tensor) -> bool:
+    """channels_last, or a 16-byte aligned channel slice of a channels_last tensor (what the kernels read in place)."""
+    if x.is_contiguous(memory_format=CL):
+        return True
+    n, c, h, w = x.shape
+    ldp = x.stride(3)
+    return (x.stride(1) == 1 and ldp >= c and ldp % 4 == 0 and x.stride(2) == ldp * w and x.stride(0) == ldp * w * h
+            and x.data_ptr() % 16 == 0)
+
+
 def _ohwi(w: torch.Tensor) -> torch.Tensor:
     """[Cout, Cin, R, S] -> [Cout, R, S, Cin] contiguous (a view when w is channels_last)."""
     return w.permute(0, 2, 3, 1).contiguous()
@@ -64,7 +74,7 @@ class _ConvF32(torch.autograd.Function):
     def forward(ctx, x, weight, pad: int, stride: int):
         C = _ext.require()
         cin = x.shape[1]
-        xs = x.contiguous(memory_format=CL)
+        xs = x if nhwc_view_ok(x) else x.contiguous(memory_format=CL)
         w = _ohwi(weight)
         if cin % 4:  # the stem: 3 channels -> 4, zero channel and zero weights
             xs = _pad_channels(xs, 4)
@@ -100,3 +110,8 @@ class _ConvF32(torch.autograd.Function):
 def conv(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     """``conv(x)`` on the fp32 matrix-core kernels (caller checked :func:`supported`)."""
     return _ConvF32.apply(x, conv.weight, conv.padding[0], conv.stride[0])
+
+
+def conv_w(x: torch.Tensor, weight: torch.Tensor, pad: int = 0, stride: int = 1) -> torch.Tensor:
+    """The same with an explicit weight tensor (e.g. several convs' weights concatenated along Cout)."""
+    return _ConvF32.apply(x, weight, pad, stride)

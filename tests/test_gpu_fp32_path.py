@@ -3,7 +3,8 @@
 The reference trains fp32 GoogLeNet (/root/reference/src/network.py:33-54, main.py:36); BASELINE.md calls that
 the apples-to-apples comparison. ``bench.py --precision fp32`` runs it channels_last with the fused BN /
 residual / ReLU, max-pool, global-average-pool, cross-entropy and SGD kernels in their fp32 forms and the
-convolutions on MIOpen (TF32 off).
+convolutions on the fp32 matrix-core kernels (csrc/kernels/conv_f32.hip; the Inception blocks' three 1x1 convs on x
+as one GEMM, ops/inception_f32.py); ``native_f32=False`` keeps the round-5 form with MIOpen convolutions (TF32 off).
 
 Whole-model check: one GoogLeNet training step from the same weights and batch on (a) the native fp32 path,
 (b) the stock fp32 PyTorch path (MIOpen BN, torch pools / loss) and (c) stock PyTorch in float64, the
@@ -26,12 +27,13 @@ def _rel(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
-def _step(model, x, y, native: bool):
+def _step(model, x, y, native: bool, native_f32: bool = False):
     from distributed_learning_amd.ops import nn as dnn
     from distributed_learning_amd.ops.loss import cross_entropy
 
     dnn.set_backend("native" if native else "torch")
     dnn.set_native_conv(False)
+    dnn.set_native_conv_f32(native and native_f32)
     try:
         model.zero_grad(set_to_none=True)
         out = model(x)
@@ -42,9 +44,11 @@ def _step(model, x, y, native: bool):
                                       if p.grad is not None}
     finally:
         dnn.set_backend("torch")
+        dnn.set_native_conv_f32(False)
 
 
-def test_googlenet_fp32_native_as_accurate_as_stock(cuda):
+@pytest.mark.parametrize("native_f32", [False, True])
+def test_googlenet_fp32_native_as_accurate_as_stock(cuda, native_f32):
     from distributed_learning_amd.models import googlenet
 
     torch.manual_seed(0)
@@ -69,11 +73,14 @@ def test_googlenet_fp32_native_as_accurate_as_stock(cuda):
 
         with profile(activities=[ProfilerActivity.CUDA]) as prof:
             l_nat, g_nat = _step(copy.deepcopy(base).to(memory_format=torch.channels_last),
-                                 x.contiguous(memory_format=torch.channels_last), y, native=True)
+                                 x.contiguous(memory_format=torch.channels_last), y, native=True, native_f32=native_f32)
     finally:
         (torch.backends.cudnn.deterministic, torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32,
          torch.backends.cudnn.benchmark) = flags
-    assert any("dla::" in e.key for e in prof.key_averages()), "the fp32 native step ran no dla:: kernel"
+    keys = [e.key for e in prof.key_averages()]
+    assert any("dla::" in k for k in keys), "the fp32 native step ran no dla:: kernel"
+    if native_f32:
+        assert sum("gemm_f32_kernel" in k for k in keys) >= 4, "the fp32 convolutions did not run on conv_f32.hip"
     assert abs(l_nat - l64) <= 1e-4 * max(1.0, abs(l64)) and abs(l_ref - l64) <= 1e-4 * max(1.0, abs(l64))
     assert g_nat.keys() == g_ref.keys() == g64.keys()
     e_nat = sorted(_rel(g_nat[n], g64[n]) for n in g64)
