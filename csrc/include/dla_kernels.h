@@ -256,7 +256,8 @@ enum TileCfg : int {
 };
 // K: reduction length (0 = unknown); wide_ok: the kernel family can run the 8-wave tiles (3x3 convs
 // need a channel count % 64 on the loaded side)
-int pick_tile(int64_t M, int N, int tile, int K = 0, bool wide_ok = true);
+int pick_tile(int64_t M, int N, int tile, int K = 0, bool wide_ok = true, bool stats = false);
+void set_tile256_min_k_stats(int k);  // smallest K of the auto 256x256 tiles for statistics forwards (A/B)
 bool tile256_enabled();  // DLA_TILE256 != 0: 256x256 tiles for the compute-bound fwd / dgrad shapes
 bool tn256_enabled();    // ... and for the split-K weight gradients (also DLA_TN256 != 0)
 inline int tile_bm(int cfg) {
@@ -272,7 +273,9 @@ inline int tile_bn(int cfg) {
                                                        : ((cfg == kTile128x128 || cfg == kTile256x128 || cfg == kTile256x128w4) ? 128 : 64);
 }
 // rows of BN-statistics partials ([rows][N][2]) a stats-producing launch writes (one per row tile)
-int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto, int K = 0);
+// stats_fwd: the launch carries the forward statistics epilogue without an addend (its tile policy differs from
+// the data gradients' whose BN-backward partials also come one row per row tile)
+int gemm_nt_stats_rows(int M, int N, int tile = kTileAuto, int K = 0, bool stats_fwd = true);
 void set_tile256_min_k(int k);  // smallest K of the auto 256x256 tiles (A/B runs; <= 0 restores the default)
 // Persistent streaming 1x1 GEMM (gemm_stream.hip) for K in {64, 128, 256}, N % 64 == 0, long M: the
 // number of BN-statistics partial rows it writes (0 = shape not served: use launch_gemm_nt), and the
@@ -296,6 +299,8 @@ void launch_gemm_direct(const void* A, int64_t lda, const void* B, int64_t ldb, 
                         int M, int N, int K, float* stats, const void* addend, int64_t ldd,
                         const uint8_t* addend_mask, hipStream_t stream);
 void set_gemm_direct(int mode);
+// the register-stored tiles as a persistent kernel with n blocks per CU (0: one block per tile; -1: DLA_GEMM_PERSIST)
+void set_gemm_persist(int blocks_per_cu);
 // fp32 convolutions on v_mfma_f32_16x16x4_f32 (conv_f32.hip): x NHWC [N][H][W][C], w OHWI [Cout][R][S][C], y NHWC
 // [N][OH][OW][Cout]; C % 4 == 0, Cout % 4 == 0, N * OH * OW < 2^24. accumulate: y += conv instead of y = conv.
 bool conv_f32_supported(int C, int Cout, int64_t M, int K);

@@ -280,18 +280,29 @@ bool tile256_enabled() {
 // K >= 256 wins per shape in isolation (profiles/r4/g04) but not in the step (g05: +0.1 ms): 1024 stays
 static int g_tile256_min_k = 1024;  // A/B setter (set_tile256_min_k)
 void set_tile256_min_k(int k) { g_tile256_min_k = k > 0 ? k : 1024; }
+// forwards with the BN-statistics epilogue (no addend): their 256x256 tiles win from K = 256 in isolation
+// (profiles/r6/g10: stage-3 conv3 0.270 vs 0.299 ms, stage-4 conv3 0.202 vs 0.229 ms) while the data gradients
+// with the identity addend lose (0.397 vs 0.354). In the step, interleaved x3 on one box (profiles/r6/g11):
+// 82.30 ms (256) vs 82.40 (512) vs 82.53 (1024). set_tile256_min_k_stats / DLA_TILE256_MIN_K_STATS for A/B
+static int g_tile256_min_k_stats = [] {
+  const char* e = std::getenv("DLA_TILE256_MIN_K_STATS");
+  const int v = e ? std::atoi(e) : 0;
+  return v > 0 ? v : 256;
+}();
+void set_tile256_min_k_stats(int k) { g_tile256_min_k_stats = k > 0 ? k : 256; }
 
-int pick_tile(int64_t M, int N, int tile, int K, bool wide_ok) {
+int pick_tile(int64_t M, int N, int tile, int K, bool wide_ok, bool stats) {
   if (tile != kTileAuto) return tile;
-  if (wide_ok && tile256_enabled() && K >= g_tile256_min_k && N % 256 == 0 && ((M + 255) / 256) * (N / 256) >= 192)
+  const int min_k = stats ? std::min(g_tile256_min_k, g_tile256_min_k_stats) : g_tile256_min_k;
+  if (wide_ok && tile256_enabled() && K >= min_k && N % 256 == 0 && ((M + 255) / 256) * (N / 256) >= 192)
     return kTile256x256;
   // the 128-row tiles win at every other ResNet shape, including the small-M layers, so the narrow
   // tile is used only when N itself is narrow (scripts/bench_gemm.py, bench_conv.py)
   return N <= 64 ? kTile128x64 : kTile128x128;
 }
 
-int gemm_nt_stats_rows(int M, int N, int tile, int K) {
-  const int bm = tile_bm(pick_tile(M, N, tile, K));
+int gemm_nt_stats_rows(int M, int N, int tile, int K, bool stats_fwd) {
+  const int bm = tile_bm(pick_tile(M, N, tile, K, true, stats_fwd));
   return (M + bm - 1) / bm;
 }
 
@@ -328,7 +339,7 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
     if (b_kmajor) DLA_NT(BM_, BN_, false, true, NT_); else DLA_NT(BM_, BN_, false, false, NT_);  \
   }
 #define DLA_NT_ST(BM_, BN_) DLA_NT_STW(BM_, BN_, kThreads)
-  const int cfg = pick_tile(M, N, tile, K);
+  const int cfg = pick_tile(M, N, tile, K, true, stats != nullptr && addend == nullptr);
   // the 128x128 tile without the BN-backward / stride-2 epilogue features: stored from the registers
   // (gemm_direct.hip); tile = kTile128x128 forced by a caller keeps the LDS-staged kernel (A/B)
   if (cfg == kTile128x128 && tile == kTileAuto && !bn_bwd && !addend2_s2 && !(stats && addend) &&

@@ -70,15 +70,14 @@ __device__ __forceinline__ uint32_t add_pair(uint32_t u, uint32_t d, uint32_t bi
   return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
 }
 
+// One 128 x 128 tile: main loop, then the register-stored epilogue. Ends with every LDS access done (a caller
+// looping over tiles may start the next tile's main loop right away).
 template <bool kStats, bool kBT, bool kAdd, int PIPE>
-__global__ __launch_bounds__(256, 2) void gemm_direct_kernel(const bf16_t* __restrict__ A, int64_t lda,
-                                                             const bf16_t* __restrict__ B, int64_t ldb,
-                                                             bf16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
-                                                             float* __restrict__ stats, const bf16_t* __restrict__ D,
-                                                             int64_t ldd, const uint8_t* __restrict__ dmask) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+__device__ __forceinline__ void direct_tile(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
+                                            int64_t ldb, bf16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
+                                            float* __restrict__ stats, const bf16_t* __restrict__ D, int64_t ldd,
+                                            const uint8_t* __restrict__ dmask, int tile, char* smem_raw) {
   const int nbn = (N + kDB - 1) / kDB;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int bm = tile / nbn, bn = tile % nbn;
   const int64_t row0 = (int64_t)bm * kDB;
   const int col0 = bn * kDB;
@@ -201,6 +200,49 @@ __global__ __launch_bounds__(256, 2) void gemm_direct_kernel(const bf16_t* __res
   }
 }
 
+template <bool kStats, bool kBT, bool kAdd, int PIPE>
+__global__ __launch_bounds__(256, 2) void gemm_direct_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                             const bf16_t* __restrict__ B, int64_t ldb,
+                                                             bf16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
+                                                             float* __restrict__ stats, const bf16_t* __restrict__ D,
+                                                             int64_t ldd, const uint8_t* __restrict__ dmask) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  direct_tile<kStats, kBT, kAdd, PIPE>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, dmask,
+                                       xcd_remap(blockIdx.x, gridDim.x), smem_raw);
+}
+
+// Persistent form: a fixed grid of blocks walks the tiles (block b takes virtual slots b, b + grid, ...; the
+// XCD-aware remap of the virtual slot keeps the blocks of one XCD on consecutive tiles, i.e. on the column tiles
+// of the same rows). No block launch / retirement per tile: a block's stores drain while it already loads its
+// next tile. Every block runs the same number of slots; slots past the last tile do nothing, so every wave
+// reaches the end.
+template <bool kStats, bool kBT, bool kAdd, int PIPE>
+__global__ __launch_bounds__(256, 2) void gemm_direct_persist_kernel(
+    const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb, bf16_t* __restrict__ C,
+    int64_t ldc, int M, int N, int K, float* __restrict__ stats, const bf16_t* __restrict__ D, int64_t ldd,
+    const uint8_t* __restrict__ dmask, int tiles, int slots) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int total = slots * (int)gridDim.x;
+  for (int it = 0; it < slots; ++it) {
+    const int tile = xcd_remap(it * (int)gridDim.x + (int)blockIdx.x, total);
+    if (tile < tiles) {
+      direct_tile<kStats, kBT, kAdd, PIPE>(A, lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, dmask, tile, smem_raw);
+    }
+    __syncthreads();  // the statistics combine's LDS reads are done before the next tile's stores into LDS
+  }
+}
+
+// 0 = one block per tile (gemm_direct_kernel); n > 0 = the persistent kernel with n blocks per CU
+static int g_persist = -1;  // -1: environment (DLA_GEMM_PERSIST, default 0)
+int gemm_persist_blocks() {
+  if (g_persist >= 0) return g_persist;
+  static const int env = [] {
+    const char* e = std::getenv("DLA_GEMM_PERSIST");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
+  return env;
+}
+
 template <bool S, bool BT, bool ADD, int PIPE>
 void launch_direct_p(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M, int N,
                      int K, float* stats, const bf16_t* D, int64_t ldd, const uint8_t* dmask, hipStream_t stream) {
@@ -208,6 +250,14 @@ void launch_direct_p(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
   size_t lds = BT ? run_mainloop_lds_bytes<PIPE, kDB, kDB, RowLoader<kDB>, KLoader<kDB>>()
                   : run_mainloop_lds_bytes<PIPE, kDB, kDB, RowLoader<kDB>, RowLoader<kDB>>();
   if (S) lds = std::max(lds, (size_t)2 * kDB * 2 * sizeof(float));
+  const int per_cu = gemm_persist_blocks();
+  if (per_cu > 0 && tiles > 256 * per_cu) {
+    const int grid = 256 * per_cu;  // a multiple of the 8 XCDs
+    const int slots = (tiles + grid - 1) / grid;
+    hipLaunchKernelGGL((gemm_direct_persist_kernel<S, BT, ADD, PIPE>), dim3(grid), dim3(256), lds, stream, A, lda, B,
+                       ldb, C, ldc, M, N, K, stats, D, ldd, dmask, tiles, slots);
+    return;
+  }
   hipLaunchKernelGGL((gemm_direct_kernel<S, BT, ADD, PIPE>), dim3(tiles), dim3(256), lds, stream, A, lda, B, ldb, C,
                      ldc, M, N, K, stats, D, ldd, dmask);
 }
@@ -227,6 +277,7 @@ void launch_direct(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, b
 // -1: environment (DLA_GEMM_DIRECT, default OFF: same step time as the staged tile, profiles/r6/g03), 0 off, 1 on
 static int g_direct = -1;
 void set_gemm_direct(int mode) { g_direct = mode < 0 ? -1 : (mode ? 1 : 0); }
+void set_gemm_persist(int blocks_per_cu) { g_persist = blocks_per_cu; }
 bool gemm_direct_enabled() {
   static const bool env = [] {
     const char* e = std::getenv("DLA_GEMM_DIRECT");

@@ -573,7 +573,7 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
                 "gemm_nt: streaming kernel refused a shape it planned");
     return {C, S};
   }
-  if (stats) S = at::empty({gemm_nt_stats_rows(M, N, (int)tile, K), N, 2},
+  if (stats) S = at::empty({gemm_nt_stats_rows(M, N, (int)tile, K, !add), N, 2},
                            A.options().dtype(at::kFloat));
   // split-K only for the fully connected heads' shape class: no epilogue features beyond a bias row
   // (a full addend is a conv dgrad's residual sum, whose bitwise result must not depend on which
@@ -628,7 +628,7 @@ std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at:
                            add ? addend->stride(0) : 0, addend_mask_ptr(addend_mask, M, N, add), &sb))
       return {C, part};
   }
-  const BnBwdArgs bnb = make_bn_bwd(x_bn, ws, mask, mode, M, N, gemm_nt_stats_rows(M, N, kTileAuto, K), part);
+  const BnBwdArgs bnb = make_bn_bwd(x_bn, ws, mask, mode, M, N, gemm_nt_stats_rows(M, N, kTileAuto, K, false), part);
   launch_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), M, N, K, nullptr,
                  current_stream(A), add ? addend->data_ptr() : nullptr, add ? addend->stride(0) : 0, b_kmajor,
                  kTileAuto, &bnb, addend_mask_ptr(addend_mask, M, N, add), addend2_ptr(addend2, M, N, H, W), (int)H,
@@ -1125,11 +1125,13 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("mask"), pybind11::arg("mode"));
   m.def("set_mfma_pipeline", &set_mfma_pipeline, "MFMA main loop: 0 register staging, 2/3 LDS-DMA stages, -1 per-shape auto");
   m.def("set_gemm_stream", &set_gemm_stream, "persistent streaming 1x1 GEMM: -1 environment (default on), 0 off, 1 on");
+  m.def("set_gemm_persist", &set_gemm_persist, "persistent register-stored 1x1 GEMM: blocks per CU (0 off, -1 env)");
   m.def("set_gemm_direct", &set_gemm_direct, "register-stored 128x128 1x1 GEMM tiles: -1 environment (default off), 0 / 1");
   m.def("gemm_stream_rows", &gemm_stream_rows, "BN-statistics partial rows of the streaming GEMM (0: shape not served)",
         pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("lda"), pybind11::arg("ldc"), pybind11::arg("b_kmajor") = false,
         pybind11::arg("add") = false, pybind11::arg("bnb") = false);
   m.def("mfma_pipeline", &mfma_pipeline);
+  m.def("set_tile256_min_k_stats", &set_tile256_min_k_stats, "smallest K of the auto 256x256 tiles of statistics forwards (A/B)");
   m.def("set_tile256_min_k", &set_tile256_min_k, "smallest K of the auto 256x256 gemm_nt / conv tiles (A/B; <= 0 default 1024)");
   m.def("set_tn256", &set_tn256, "256x256 weight-gradient tiles: -1 environment (DLA_TN256, default on), 0 off, 1 on");
   m.def("set_splitk_blocks", &set_splitk_blocks, "split-K weight-gradient block target (0 = default / DLA_SPLITK_BLOCKS)");

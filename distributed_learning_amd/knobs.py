@@ -54,6 +54,8 @@ TABLE: Dict[str, Knob] = {
     # ---- kernel selection (C++) --------------------------------------------------------------------
     "TILE256": Knob("1", "csrc/kernels/gemm.hip", "0: no 256x256 tiles for fwd / dgrad (profiles/r5a/)"),
     "TILE512": Knob("1", "csrc/kernels/conv.hip", "0: no 512x128 tiles for the Cout-128 3x3 fwd / dgrad (profiles/r5/g54/)"),
+    "TILE256_MIN_K_STATS": Knob("256", "csrc/kernels/gemm.hip", "smallest K of the 256x256 tiles for the forward GEMMs "
+                                                                  "with BN statistics (profiles/r6/g11/)"),
     "TN256": Knob("1", "csrc/kernels/gemm.hip", "0: no 256x256 weight-gradient tiles (profiles/r5c/, r5d/)"),
     "SPLITK_XCD": Knob("1", "csrc/kernels/gemm.hip", "0: no XCD-aware split-K grids (round-2 README row)"),
     "SPLITK_BLOCKS": Knob("512", "csrc/kernels/gemm.hip", "split-K grid target in blocks"),
@@ -61,6 +63,8 @@ TABLE: Dict[str, Knob] = {
     "GEMM_SPLITK": Knob("1", "csrc/nn_bindings.cpp", "0: no split-K for the FC heads"),
     "GEMM_DIRECT": Knob("0", "csrc/kernels/gemm_direct.hip", "1: 128x128 1x1 GEMM tiles stored straight from the "
                                                              "registers, not staged through LDS (neutral: profiles/r6/g03/)"),
+    "GEMM_PERSIST": Knob("0", "csrc/kernels/gemm_direct.hip", "n > 0: the register-stored 128x128 tiles (GEMM_DIRECT=1) as a "
+                                                              "persistent kernel with n blocks per CU"),
     "GEMM_STREAM": Knob("1", "csrc/kernels/gemm_stream.hip", "0: no persistent streaming 1x1 GEMM (profiles/r3/)"),
     "CONV_PIPE": Knob("-1", "csrc/kernels/conv.hip", "3x3 conv main-loop pipeline for K >= 256 (-1: per shape)"),
     "HALO": Knob("2", "csrc/kernels/conv_halo.hip", "0 off, 1 dgrad only, 2 fwd + dgrad halo-tiled 64-ch 3x3 (r5l/)"),

@@ -23,6 +23,10 @@ def main() -> None:
     iters = int(sys.argv[5]) if len(sys.argv) > 5 else 20
     tile = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     C = _ext.require()
+    if os.environ.get("STALL_PIPE"):  # MFMA main-loop pipeline override (A/B)
+        C.set_mfma_pipeline(int(os.environ["STALL_PIPE"]))
+    if os.environ.get("STALL_STREAM"):  # streaming-kernel mode override (1: every K <= 256)
+        C.set_gemm_stream(int(os.environ["STALL_STREAM"]))
     dev = torch.device("cuda:0")
     A = torch.randn(M, K, device=dev).to(torch.bfloat16)
     fwd = kind.startswith("fwd")
