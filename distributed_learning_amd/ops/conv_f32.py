@@ -23,9 +23,11 @@ from . import _ext
 
 CL = torch.channels_last
 
-# The stem (3 input channels, 7x7 / stride 2) on these kernels: its 3 channels pad to 4 and each 16-byte chunk is a
-# different tap, so the loads scatter; MIOpen's stem is ~2x faster (profiles/r6/g06), so it stays there by default.
-STEM_NATIVE = False
+# The stem (3 input channels, 7x7 / stride 2) on these kernels. Generic form: 3 channels padded to 4, each 16-byte
+# chunk a different tap, scattered loads (~1.2x MIOpen's time, profiles/r6/g07). Space-to-depth form (stem_s2d):
+# the padded image regrouped into 2x2 pixel blocks of 12 channels makes the conv a 4x4 / stride-1 one over the
+# block image, whose k-steps read 128 contiguous bytes; STEM_NATIVE routes the model's stem to it.
+STEM_NATIVE = True
 
 
 def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -38,6 +40,8 @@ def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     if conv.kernel_size[0] != conv.kernel_size[1] or conv.stride[0] != conv.stride[1] or conv.padding[0] != conv.padding[1]:
         return False
     cin, cout = x.shape[1], conv.out_channels
+    if cin == 3 and STEM_NATIVE and stem_s2d_ok(x, conv):
+        return True
     if cout % 4 or not (cin % 4 == 0 or (cin == 3 and STEM_NATIVE)):
         return False
     if conv.stride[0] != 1 and x.requires_grad:
@@ -107,8 +111,63 @@ class _ConvF32(torch.autograd.Function):
         return dx, dw, None, None
 
 
+def stem_s2d_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    return (x.shape[1] == 3 and conv.kernel_size == (7, 7) and conv.stride == (2, 2) and conv.padding == (3, 3)
+            and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and not x.requires_grad and conv.out_channels % 4 == 0)
+
+
+def _s2d_image(x: torch.Tensor) -> torch.Tensor:
+    """[N, 3, H, W] -> the zero-padded (3 px) image as 2x2 pixel blocks: [N, 12, (H+6)/2, (W+6)/2] channels_last,
+    channel (dh, dw, c)."""
+    n, c, h, w = x.shape
+    xp = F.pad(x, (3, 3, 3, 3))
+    hb, wb = (h + 6) // 2, (w + 6) // 2
+    img = xp.reshape(n, c, hb, 2, wb, 2).permute(0, 2, 4, 3, 5, 1).reshape(n, hb, wb, 4 * c)
+    return img.permute(0, 3, 1, 2)  # channels_last view of the contiguous [N, hb, wb, 12] image
+
+
+def _s2d_weight(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, 3, 7, 7] -> [Cout, 4, 4, 12] (taps over 2x2 blocks, channel (dh, dw, c)); the 8th row / column are 0."""
+    co, c = w.shape[0], w.shape[1]
+    wp = F.pad(w, (0, 1, 0, 1))  # [co, c, 8, 8]
+    return wp.reshape(co, c, 4, 2, 4, 2).permute(0, 2, 4, 3, 5, 1).reshape(co, 4, 4, 4 * c).contiguous()
+
+
+def _s2d_grad(g: torch.Tensor, c: int) -> torch.Tensor:
+    """inverse of _s2d_weight for the gradient: [Cout, 4, 4, 12] -> [Cout, 3, 7, 7]"""
+    co = g.shape[0]
+    return g.reshape(co, 4, 4, 2, 2, c).permute(0, 5, 1, 3, 2, 4).reshape(co, c, 8, 8)[:, :, :7, :7]
+
+
+class _StemS2D(torch.autograd.Function):
+    """The 7x7 / stride-2 stem as a 4x4 / stride-1 conv over the space-to-depth image (no input gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        C = _ext.require()
+        img = _s2d_image(x)
+        y = C.conv_f32_fwd(img, _s2d_weight(weight), 0, 1)
+        ctx.save_for_backward(img)
+        ctx.cin = weight.shape[1]
+        ctx.wlayout = weight.is_contiguous(memory_format=CL)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.require()
+        (img,) = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=CL)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = _s2d_grad(C.conv_f32_wgrad(dy, img, 4, 4, 0, 1), ctx.cin)
+            dw = dw.contiguous(memory_format=CL) if ctx.wlayout else dw.contiguous()
+        return None, dw
+
+
 def conv(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     """``conv(x)`` on the fp32 matrix-core kernels (caller checked :func:`supported`)."""
+    if x.shape[1] == 3 and STEM_NATIVE and stem_s2d_ok(x, conv):
+        return _StemS2D.apply(x, conv.weight)
     return _ConvF32.apply(x, conv.weight, conv.padding[0], conv.stride[0])
 
 

@@ -7,7 +7,8 @@ order, so they are checked against the column sums of the stored output. Shapes 
 partly out of range), a column tile partly past N, the register-staged main loop (K <= 512), the 2-stage
 LDS-DMA loop (K > 512) and the buffer-DMA loop (forced PIPE 6), weights [N][K] (forward) and k-major [K][N]
 (data gradient), with and without the masked identity-gradient addend. The streaming kernel is turned off so
-the short-K shapes reach the tile dispatch.
+the short-K shapes reach the tile dispatch, and the statistics forwards are held on the 128x128 tiles (their
+default moves to 256x256 from K = 256).
 """
 import pytest
 import torch
@@ -26,7 +27,9 @@ def C():
 
     C = _ext.require()
     C.set_gemm_stream(0)
+    C.set_tile256_min_k_stats(1 << 30)  # keep the statistics forwards on the 128x128 tiles under test
     yield C
+    C.set_tile256_min_k_stats(-1)
     C.set_gemm_stream(-1)
     C.set_gemm_direct(-1)
     C.set_mfma_pipeline(-1)

@@ -66,7 +66,7 @@ def test_want_dx_false_refused_outside_quad_form(cuda):
         C.bn_relu_maxpool_bwd(dyp, pos, y, ws, gamma, 3, 2, 0, want_dx=False)
 
 
-def _model_step(cuda, fused: bool, observe: bool = False):
+def _model_step(cuda, fused: bool, observe: bool = False, second: bool = False):
     from distributed_learning_amd.ops import conv as nconv
     from distributed_learning_amd.ops import nn as dnn
     from distributed_learning_amd.ops.bn_act import fused_bn_relu_maxpool
@@ -84,13 +84,19 @@ def _model_step(cuda, fused: bool, observe: bool = False):
     dnn.set_native_conv(True)
     seen = []
     try:
+        extra = None
         if observe:  # a hook on the conv output must see the real gradient, so the fusion stands down
             y, stats = nconv.stem_conv(x, conv, want_stats=True)
             y.register_hook(lambda g: seen.append(g.float().norm().item()))
             out = fused_bn_relu_maxpool(y, bn, pool, stats)
+        elif second:  # the conv output also feeds another consumer: its gradient adds to the parked one
+            y, stats = nconv.stem_conv(x, conv, want_stats=True)
+            out = fused_bn_relu_maxpool(y, bn, pool, stats)
+            extra = y.float().mul(torch.linspace(-0.5, 0.5, y.numel(), device=cuda).reshape(y.shape)).sum()
         else:
             out = dnn.conv_bn_act_maxpool(x, conv, bn, pool)
-        out.float().mul(torch.linspace(-1, 1, out.numel(), device=cuda).reshape(out.shape)).sum().backward()
+        loss = out.float().mul(torch.linspace(-1, 1, out.numel(), device=cuda).reshape(out.shape)).sum()
+        (loss if extra is None else loss + extra).backward()
         torch.cuda.synchronize()
     finally:
         dnn.set_backend("torch")
@@ -112,3 +118,14 @@ def test_stem_bn_fusion_stands_down_for_observed_output(cuda):
     gw_u, _, _, _ = _model_step(cuda, False)
     assert used_o == 0 and len(seen) == 1 and seen[0] > 0
     assert ((gw_o - gw_u).norm() / gw_u.norm()).item() < 1e-4
+
+
+def test_stem_bn_fusion_with_a_second_consumer_of_the_conv_output(cuda):
+    """advisor r5: the stem conv output feeds the fused BN+ReLU+max-pool AND a second consumer. The parked gradient
+    is materialised (StemBNLink.materialise re-runs the quad apply on the already finalized workspace) and added to
+    the other consumer's gradient: dW and dgamma must match the unfused path."""
+    gw_f, gg_f, used_f, _ = _model_step(cuda, True, second=True)
+    gw_u, gg_u, used_u, _ = _model_step(cuda, False, second=True)
+    assert used_u == 0
+    torch.testing.assert_close(gg_f, gg_u, rtol=0, atol=0)
+    assert ((gw_f - gw_u).norm() / gw_u.norm()).item() < 1e-4
