@@ -299,6 +299,15 @@ void launch_gemm_direct(const void* A, int64_t lda, const void* B, int64_t ldb, 
                         int M, int N, int K, float* stats, const void* addend, int64_t ldd,
                         const uint8_t* addend_mask, hipStream_t stream);
 void set_gemm_direct(int mode);
+// 1x1-conv forward whose input is a deferred act(BN(y) + r) (gemm_apply.hip): y, r, out [M][K] bf16 contiguous,
+// ws / ws2 the 7K BN workspaces (ws2 non-null: r is the shortcut BN's input), mask the ReLU bits; C [M][N]
+// (row stride N), B [N][K]; statistics [gemm_apply_rows(M)][N][2] when stats is non-null. Writes out + mask
+// and C in one pass.
+constexpr int kGemmApplyMaxK = 512;
+bool gemm_apply_ok(int64_t M, int N, int K);
+int gemm_apply_rows(int64_t M);
+void launch_gemm_apply(const void* y, const void* r, const float* ws, const float* ws2, void* out, uint8_t* mask,
+                       const void* B, int64_t ldb, void* C, int M, int N, int K, float* stats, hipStream_t stream);
 // the register-stored tiles as a persistent kernel with n blocks per CU (0: one block per tile; -1: DLA_GEMM_PERSIST)
 void set_gemm_persist(int blocks_per_cu);
 // fp32 convolutions on v_mfma_f32_16x16x4_f32 (conv_f32.hip): x NHWC [N][H][W][C], w OHWI [Cout][R][S][C], y NHWC

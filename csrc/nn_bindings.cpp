@@ -61,7 +61,7 @@ std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> resid
                                    c10::optional<at::Tensor> bias, c10::optional<at::Tensor> running_mean,
                                    c10::optional<at::Tensor> running_var, bool training, double momentum, double eps,
                                    bool relu, c10::optional<at::Tensor> stats, c10::optional<at::Tensor> out,
-                                   int64_t out_channel) {
+                                   int64_t out_channel, bool defer) {
   check_act(x, "x");
   const int C = (int)x.size(1);
   const int64_t M = rows_of(x);
@@ -118,7 +118,11 @@ std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> resid
   }
   at::Tensor mask;
   if (training && relu && res) mask = at::empty({(M * C + 7) / 8}, x.options().dtype(at::kByte));
-  launch_bn_fwd(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), M, C, dtype_code(x), g, b, (float)eps,
+  // defer: statistics and coefficients only; y (and the mask) are written later by the consumer's GEMM
+  // (gemm_nt_apply) or by bn_apply_deferred
+  TORCH_CHECK(!defer || (training && ldy == 0 && x.scalar_type() == at::kBFloat16),
+              "bn_act_fwd: defer needs training mode, bf16 and a fresh output");
+  launch_bn_fwd(x.data_ptr(), res ? res->data_ptr() : nullptr, defer ? nullptr : y.data_ptr(), M, C, dtype_code(x), g, b, (float)eps,
                 (float)momentum, training ? rm : nullptr, training ? rv : nullptr, ws.data_ptr<float>(),
                 part.data_ptr<float>(), relu, training, current_stream(x), ext ? stats->data_ptr<float>() : nullptr,
                 ext ? (int)stats->size(0) : 0, mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, ldy);
@@ -135,7 +139,7 @@ std::vector<at::Tensor> bn_dual_fwd(at::Tensor x, at::Tensor xd, c10::optional<a
                                     c10::optional<at::Tensor> bias_d, c10::optional<at::Tensor> running_mean_d,
                                     c10::optional<at::Tensor> running_var_d, double momentum, double momentum_d,
                                     double eps, double eps_d, bool relu, c10::optional<at::Tensor> stats,
-                                    c10::optional<at::Tensor> stats_d) {
+                                    c10::optional<at::Tensor> stats_d, bool defer) {
   check_act(x, "x");
   check_act(xd, "xd");
   TORCH_CHECK(xd.sizes() == x.sizes() && xd.scalar_type() == x.scalar_type(), "bn_dual: x / xd mismatch");
@@ -167,9 +171,35 @@ std::vector<at::Tensor> bn_dual_fwd(at::Tensor x, at::Tensor xd, c10::optional<a
   at::Tensor y = at::empty_like(x);
   at::Tensor mask;
   if (relu) mask = at::empty({(M * C + 7) / 8}, x.options().dtype(at::kByte));
-  launch_bn_dual_apply(x.data_ptr(), xd.data_ptr(), y.data_ptr(), ws.data_ptr<float>(), wsd.data_ptr<float>(), M, C,
-                       dtype_code(x), relu, relu ? mask.data_ptr<uint8_t>() : nullptr, current_stream(x));
+  if (!defer)
+    launch_bn_dual_apply(x.data_ptr(), xd.data_ptr(), y.data_ptr(), ws.data_ptr<float>(), wsd.data_ptr<float>(), M, C,
+                         dtype_code(x), relu, relu ? mask.data_ptr<uint8_t>() : nullptr, current_stream(x));
   return {y, ws, wsd, mask};
+}
+
+// The apply pass a deferred bn_act_fwd / bn_dual_fwd skipped: y = act(BN(x) + r) (r a BN input too when wsd is
+// given), mask = its ReLU bits. For a deferred output whose consumer is not a gemm_nt_apply.
+void bn_apply_deferred(at::Tensor x, at::Tensor r, at::Tensor ws, c10::optional<at::Tensor> wsd, at::Tensor y,
+                       at::Tensor mask) {
+  check_act(x, "x");
+  check_act(r, "r");
+  check_act(y, "y");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && r.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 &&
+                  r.sizes() == x.sizes() && y.sizes() == x.sizes(),
+              "bn_apply_deferred: x, r, y must be bf16 tensors of one shape");
+  const int C = (int)x.size(1);
+  const int64_t M = rows_of(x);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() == 7 * (int64_t)C, "ws: 7C fp32");
+  TORCH_CHECK(mask.scalar_type() == at::kByte && mask.numel() * 8 >= M * C, "mask: one bit per element");
+  const bool dual = wsd.has_value() && wsd->defined();
+  if (dual) {
+    TORCH_CHECK(wsd->scalar_type() == at::kFloat && wsd->is_contiguous() && wsd->numel() == 7 * (int64_t)C, "wsd: 7C fp32");
+    launch_bn_dual_apply(x.data_ptr(), r.data_ptr(), y.data_ptr(), ws.data_ptr<float>(), wsd->data_ptr<float>(), M, C,
+                         kBF16, true, mask.data_ptr<uint8_t>(), current_stream(x));
+  } else {
+    launch_bn_fwd(x.data_ptr(), r.data_ptr(), y.data_ptr(), M, C, kBF16, nullptr, nullptr, 0.f, 0.f, nullptr, nullptr,
+                  ws.data_ptr<float>(), nullptr, true, false, current_stream(x), nullptr, 0, mask.data_ptr<uint8_t>(), 0);
+  }
 }
 
 // Backward of bn_dual_fwd: returns (dx, dgamma, dbeta, dxd, dgamma_d, dbeta_d).
@@ -595,6 +625,37 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
                    addend2_ptr(addend2, M, N, H, W), (int)H, (int)W);
   return {C, S};
 }
+
+// 1x1-conv forward over a deferred act(BN(y) + r) (gemm_apply.hip): writes out (the BN's output) and its ReLU
+// mask, returns (C = out @ B^T, statistics [gemm_apply_rows][N][2] or undefined). y, r, out: bf16 [M, K]
+// contiguous rows; B [N, K]; ws / wsd the 7K workspaces (wsd: r is the shortcut BN's input).
+std::vector<at::Tensor> gemm_nt_apply(at::Tensor y, at::Tensor r, at::Tensor ws, c10::optional<at::Tensor> wsd,
+                                      at::Tensor B, bool stats, at::Tensor out, at::Tensor mask) {
+  check_mat(y, "y");
+  check_mat(r, "r");
+  check_mat(out, "out");
+  check_mat(B, "B");
+  const int64_t M = y.size(0);
+  const int K = (int)y.size(1), N = (int)B.size(0);
+  TORCH_CHECK(y.is_contiguous() && r.is_contiguous() && out.is_contiguous() && B.is_contiguous() &&
+                  r.sizes() == y.sizes() && out.sizes() == y.sizes() && B.size(1) == K,
+              "gemm_nt_apply: y, r, out contiguous [M, K], B contiguous [N, K]");
+  TORCH_CHECK(gemm_apply_ok(M, N, K), "gemm_nt_apply: shape not served (check gemm_apply_ok)");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() == 7 * (int64_t)K, "ws: 7K fp32");
+  const bool dual = wsd.has_value() && wsd->defined();
+  if (dual)
+    TORCH_CHECK(wsd->scalar_type() == at::kFloat && wsd->is_contiguous() && wsd->numel() == 7 * (int64_t)K, "wsd: 7K fp32");
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kByte && mask.numel() * 8 >= M * K, "mask: one bit per element");
+  at::Tensor C = at::empty({M, N}, y.options());
+  at::Tensor S;
+  if (stats) S = at::empty({gemm_apply_rows(M), N, 2}, y.options().dtype(at::kFloat));
+  launch_gemm_apply(y.data_ptr(), r.data_ptr(), ws.data_ptr<float>(), dual ? wsd->data_ptr<float>() : nullptr,
+                    out.data_ptr(), mask.data_ptr<uint8_t>(), B.data_ptr(), B.stride(0), C.data_ptr(), (int)M, N, K,
+                    stats ? S.data_ptr<float>() : nullptr, current_stream(y));
+  return {C, S};
+}
+
+bool gemm_nt_apply_ok(int64_t M, int64_t N, int64_t K) { return gemm_apply_ok(M, (int)N, (int)K); }
 
 // gemm_nt whose output is the dy of a fused BN: also returns that BN's backward-reduction partials.
 std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at::Tensor> addend, bool b_kmajor,
@@ -1158,7 +1219,20 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("p"), pybind11::arg("ceil_mode") = false,
         pybind11::arg("need_pos") = true);
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC max pooling backward (gather form)");
-  m.def("bn_dual_fwd", &bn_dual_fwd, "training act(BN(x) + BN_d(xd)) in one apply pass (downsample residual)");
+  m.def("bn_dual_fwd", &bn_dual_fwd, "training act(BN(x) + BN_d(xd)) in one apply pass (downsample residual)",
+        pybind11::arg("x"), pybind11::arg("xd"), pybind11::arg("weight"), pybind11::arg("bias"),
+        pybind11::arg("running_mean"), pybind11::arg("running_var"), pybind11::arg("weight_d"), pybind11::arg("bias_d"),
+        pybind11::arg("running_mean_d"), pybind11::arg("running_var_d"), pybind11::arg("momentum"),
+        pybind11::arg("momentum_d"), pybind11::arg("eps"), pybind11::arg("eps_d"), pybind11::arg("relu"),
+        pybind11::arg("stats"), pybind11::arg("stats_d"), pybind11::arg("defer") = false);
+  m.def("bn_apply_deferred", &bn_apply_deferred, "the apply pass of a deferred bn_act_fwd / bn_dual_fwd (ReLU, residual)",
+        pybind11::arg("x"), pybind11::arg("r"), pybind11::arg("ws"), pybind11::arg("wsd"), pybind11::arg("y"),
+        pybind11::arg("mask"));
+  m.def("gemm_nt_apply", &gemm_nt_apply,
+        "1x1-conv forward over a deferred act(BN(y) + r): writes the BN output + mask and returns (C, stats)",
+        pybind11::arg("y"), pybind11::arg("r"), pybind11::arg("ws"), pybind11::arg("wsd"), pybind11::arg("B"),
+        pybind11::arg("stats"), pybind11::arg("out"), pybind11::arg("mask"));
+  m.def("gemm_nt_apply_ok", &gemm_nt_apply_ok, "shapes gemm_nt_apply serves (M rows, N outputs, K channels)");
   m.def("bn_dual_bwd", &bn_dual_bwd, "backward of bn_dual_fwd (one dy read for both BatchNorms)", pybind11::arg("dy"),
         pybind11::arg("mask"), pybind11::arg("x"), pybind11::arg("ws"), pybind11::arg("weight"), pybind11::arg("xd"),
         pybind11::arg("wsd"), pybind11::arg("weight_d"), pybind11::arg("want_dx") = true);
@@ -1209,7 +1283,7 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("residual"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"),
         pybind11::arg("running_var"), pybind11::arg("training"), pybind11::arg("momentum"), pybind11::arg("eps"),
         pybind11::arg("relu"), pybind11::arg("stats") = pybind11::none(), pybind11::arg("out") = pybind11::none(),
-        pybind11::arg("out_channel") = 0);
+        pybind11::arg("out_channel") = 0, pybind11::arg("defer") = false);
   m.def("bn_concat_fwd", &bn_concat_fwd, "grouped training BN+ReLU of concatenated branches into one NHWC output");
   m.def("bn_concat_bwd", &bn_concat_bwd, "backward of bn_concat_fwd (dy slices read in place)", pybind11::arg("dout"),
         pybind11::arg("ys"), pybind11::arg("weights"), pybind11::arg("wss"),

@@ -22,6 +22,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import nn as dnn
+from ..ops.bn_act import deferral_scope, ensure
 from ..ops.pool import MaxPool2d, global_avg_pool
 
 
@@ -65,6 +66,7 @@ class Bottleneck(nn.Module):
         self.bn3 = nn.BatchNorm2d(planes * self.expansion)
         self.downsample = downsample
         self.stride = stride
+        self.defer_output = False  # set by ResNet for every bottleneck followed by another
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         # conv1 forwards x as a second output that feeds the identity branch (or the downsample conv),
@@ -78,13 +80,17 @@ class Bottleneck(nn.Module):
             out, xa = dnn.conv_bn_act_fork(x, self.conv1, self.bn1, relu=True)
             xs = None
         out = dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True)
+        # a block whose output goes straight into the next bottleneck (ResNet.forward) leaves the final apply
+        # pass to that block's conv1 GEMM (ops/bn_act.py PendingApply); nothing else may observe it
+        defer = self.defer_output and not (self._forward_hooks or self._forward_pre_hooks)
         if self.downsample is None:
-            return dnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=xa)
+            return dnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=xa, defer=defer)
         # the shortcut BN is applied inside the block's final apply pass (never materialised)
         ds_conv, ds_bn = self.downsample[0], self.downsample[1]
         if xs is not None:
-            return dnn.conv_bn_add_conv_bn_act(out, self.conv3, self.bn3, xs, ds_conv, ds_bn, presubsampled=True)
-        return dnn.conv_bn_add_conv_bn_act(out, self.conv3, self.bn3, xa, ds_conv, ds_bn)
+            return dnn.conv_bn_add_conv_bn_act(out, self.conv3, self.bn3, xs, ds_conv, ds_bn, presubsampled=True,
+                                               defer=defer)
+        return dnn.conv_bn_add_conv_bn_act(out, self.conv3, self.bn3, xa, ds_conv, ds_bn, defer=defer)
 
 
 class Downsample(nn.Sequential):
@@ -118,6 +124,7 @@ class ResNet(nn.Module):
         self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
         self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
         self.fc = nn.Linear(512 * block.expansion, num_classes)
+        self._chain_bottlenecks()
 
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
@@ -142,12 +149,23 @@ class ResNet(nn.Module):
             layers.append(block(self.inplanes, planes))
         return nn.Sequential(*layers)
 
+    def _chain_bottlenecks(self) -> None:
+        """Mark every bottleneck whose output feeds another bottleneck (all but the network's last)."""
+        blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
+        for b, nxt in zip(blocks, blocks[1:]):
+            if isinstance(b, Bottleneck):
+                b.defer_output = isinstance(nxt, Bottleneck)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = dnn.conv_bn_act_maxpool(x, self.conv1, self.bn1, self.maxpool)
-        x = self.layer1(x)
-        x = self.layer2(x)
-        x = self.layer3(x)
-        x = self.layer4(x)
+        # block outputs consumed only by the next bottleneck's conv1 may be written by that conv's GEMM
+        # (deferral_scope: anything still unwritten at its exit is materialised)
+        with deferral_scope():
+            x = self.layer1(x)
+            x = self.layer2(x)
+            x = self.layer3(x)
+            x = self.layer4(x)
+            ensure(x)
         x = global_avg_pool(x) if isinstance(self.avgpool, nn.AdaptiveAvgPool2d) else torch.flatten(self.avgpool(x), 1)
         return dnn.linear(x, self.fc)
 

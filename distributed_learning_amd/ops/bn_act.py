@@ -11,6 +11,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from .. import knobs
 from . import _ext
 from . import limits as _limits
 
@@ -58,6 +59,77 @@ class ResidualLink:
         self.dy = self.mask = None
 
 
+class PendingApply:
+    """A BN(+residual)+ReLU output whose apply pass was deferred to its consumer.
+
+    The block-final BN of a bottleneck finalizes its statistics but does not write its output ``y``: the next
+    block's conv1 GEMM (ops/conv.py::_Conv1x1Fork, csrc/kernels/gemm_apply.hip) reads the BN input ``x`` and the
+    residual ``r`` itself, writes ``y`` and the ReLU mask while staging its operand, and multiplies -- the block
+    output is never re-read. Any other consumer calls :func:`ensure` first (one apply pass, as without the
+    deferral). Deferral only happens inside :func:`deferral_scope` (ResNet.forward), whose exit materialises
+    whatever is still pending, so no code outside the model's own forward can see an unwritten output."""
+
+    __slots__ = ("x", "r", "ws", "wsd", "y", "mask")
+
+    def __init__(self, x, r, ws, wsd, y, mask):
+        self.x, self.r, self.ws, self.wsd, self.y, self.mask = x, r, ws, wsd, y, mask
+
+    def materialise(self) -> None:
+        if self.y is not None:
+            _ext.require().bn_apply_deferred(self.x, self.r, self.ws, self.wsd, self.y, self.mask)
+            CALLS["materialised"] += 1
+        self.clear()
+
+    def clear(self) -> None:
+        if self.y is not None:
+            self.y._dla_pending = None
+        self.x = self.r = self.ws = self.wsd = self.y = self.mask = None
+
+
+CALLS = {"deferred": 0, "fused": 0, "materialised": 0}
+_SCOPE: list = []  # open deferral scopes, each the list of the outputs it deferred
+
+
+def pending_of(t):
+    """The PendingApply of a deferred, not yet written BN output (None for any other tensor)."""
+    p = getattr(t, "_dla_pending", None) if t is not None else None
+    return p if p is not None and p.y is not None else None
+
+
+def ensure(t):
+    """Write a deferred BN output now (a no-op for every other tensor); returns ``t``."""
+    p = pending_of(t)
+    if p is not None:
+        p.materialise()
+    return t
+
+
+class deferral_scope:
+    """Context in which the bottleneck blocks may defer their final apply pass (DLA_DEFER_APPLY)."""
+
+    def __enter__(self):
+        _SCOPE.append([])
+        return self
+
+    def __exit__(self, *exc):
+        for p in _SCOPE.pop():
+            p.materialise()
+        return False
+
+
+def deferral_active() -> bool:
+    return bool(_SCOPE) and knobs.flag("DEFER_APPLY")
+
+
+def _defer_record(y, p) -> None:
+    y._dla_pending = p
+    _SCOPE[-1].append(p)
+    CALLS["deferred"] += 1
+
+
+_HANDOFF: list = [None]  # a deferring forward's PendingApply, picked up by its wrapper
+
+
 def fork_link_of(t):
     return getattr(t, "_dla_fork", None) if t is not None else None
 
@@ -70,10 +142,12 @@ def bn_link_of(t: torch.Tensor):
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu, stats,
-                rlink=None, dlink=None):
+                rlink=None, dlink=None, defer=False):
         C = _ext.require()
         y, ws, mask = C.bn_act_fwd(x, residual, weight, bias, running_mean, running_var, training, momentum, eps,
-                                   relu, stats)
+                                   relu, stats, None, 0, defer)
+        if defer:  # y and mask are written by the consumer (PendingApply)
+            _HANDOFF[0] = PendingApply(x, residual, ws, None, y, mask)
         ctx.has_res = residual is not None
         ctx.training = training
         ctx.rlink = rlink if (rlink is not None and residual is not None and training) else None
@@ -107,7 +181,7 @@ class _BNAct(torch.autograd.Function):
                 rl.dy, rl.mask = dy, mask
             need = ctx.needs_input_grad
             return (dx, dg if need[1] else None, db if need[2] else None, None,
-                    None, None, None, None, None, None, None, None, None)
+                    None, None, None, None, None, None, None, None, None, None)
         dx, dres, dg, db = C.bn_act_bwd(dy, None, mask, x, ws, weight, ctx.mask_mode, ctx.has_res and rl is None, ext)
         if rl is not None:  # the forking conv adds dy (masked) in its dgrad epilogue
             rl.dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
@@ -115,7 +189,7 @@ class _BNAct(torch.autograd.Function):
             dres = None
         need = ctx.needs_input_grad
         return (dx, dg if need[1] else None, db if need[2] else None, dres if ctx.has_res else None,
-                None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None)
 
 
 class _BNDualAct(torch.autograd.Function):
@@ -126,10 +200,12 @@ class _BNDualAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, xd, weight_d, bias_d, rm, rv, rmd, rvd, momentum, momentum_d, eps, eps_d,
-                relu, stats, stats_d, dlink=None, dlink_d=None):
+                relu, stats, stats_d, dlink=None, dlink_d=None, defer=False):
         C = _ext.require()
         y, ws, wsd, mask = C.bn_dual_fwd(x, xd, weight, bias, rm, rv, weight_d, bias_d, rmd, rvd, momentum,
-                                         momentum_d, eps, eps_d, relu, stats, stats_d)
+                                         momentum_d, eps, eps_d, relu, stats, stats_d, defer)
+        if defer:
+            _HANDOFF[0] = PendingApply(x, xd, ws, wsd, y, mask)
         ctx.relu = relu
         ctx.save_for_backward(x, ws, weight, xd, wsd, weight_d, mask if relu else None)
         # both inputs come from 1x1 convs that can apply their BN's backward themselves (ops/conv.py DualBNLink)
@@ -151,7 +227,7 @@ class _BNDualAct(torch.autograd.Function):
         else:
             dx, dg, db, dxd, dgd, dbd = _ext.require().bn_dual_bwd(dy, mask, x, ws, weight, xd, wsd, weight_d)
         return (dx, dg if need[1] else None, db if need[2] else None, dxd, dgd if need[4] else None,
-                dbd if need[5] else None) + (None,) * 13
+                dbd if need[5] else None) + (None,) * 14
 
 
 def dual_supported(x: torch.Tensor, bn: nn.BatchNorm2d, xd: torch.Tensor, bnd: nn.BatchNorm2d) -> bool:
@@ -160,9 +236,26 @@ def dual_supported(x: torch.Tensor, bn: nn.BatchNorm2d, xd: torch.Tensor, bnd: n
             and bn.momentum is not None and bnd.momentum is not None)
 
 
+def _can_defer(x, relu: bool, *others) -> bool:
+    return (relu and x.dtype == torch.bfloat16 and deferral_active() and torch.is_grad_enabled()
+            and any(t is not None and t.requires_grad for t in (x,) + others))
+
+
+def _apply_deferred(fn, *args):
+    """Run a deferring autograd Function and attach its PendingApply to the output."""
+    _HANDOFF[0] = None
+    y = fn.apply(*args)
+    p, _HANDOFF[0] = _HANDOFF[0], None
+    if p is not None:
+        _defer_record(y, p)
+        p.y = y
+    return y
+
+
 def fused_bn_add_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, xd: torch.Tensor, bnd: nn.BatchNorm2d,
-                        relu: bool = True, stats=None, stats_d=None) -> torch.Tensor:
-    """``act(bn(x) + bnd(xd))`` (training mode); falls back to the two-step form when unsupported."""
+                        relu: bool = True, stats=None, stats_d=None, defer: bool = False) -> torch.Tensor:
+    """``act(bn(x) + bnd(xd))`` (training mode); falls back to the two-step form when unsupported.
+    ``defer``: the output may be left for its consumer to write (PendingApply; inside a deferral_scope)."""
     if not dual_supported(x, bn, xd, bnd):
         return fused_bn_act(x, bn, relu, fused_bn_act(xd, bnd, False, None, stats_d), stats)
     running = []
@@ -172,9 +265,10 @@ def fused_bn_add_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, xd: torch.Tensor, b
             _PENDING_COUNTERS.append(b.num_batches_tracked)
     if len(_PENDING_COUNTERS) >= 1024:
         flush_bn_counters()
-    return _BNDualAct.apply(x, bn.weight, bn.bias, xd, bnd.weight, bnd.bias, *running, float(bn.momentum),
-                            float(bnd.momentum), float(bn.eps), float(bnd.eps), relu, stats, stats_d,
-                            getattr(x, "_dla_dual", None), getattr(xd, "_dla_dual", None))
+    defer = defer and _can_defer(x, relu, xd, bn.weight, bnd.weight)
+    return _apply_deferred(_BNDualAct, x, bn.weight, bn.bias, xd, bnd.weight, bnd.bias, *running, float(bn.momentum),
+                           float(bnd.momentum), float(bn.eps), float(bnd.eps), relu, stats, stats_d,
+                           getattr(x, "_dla_dual", None), getattr(xd, "_dla_dual", None), defer)
 
 
 # num_batches_tracked increments are batched into one multi-tensor launch per forward instead of
@@ -206,9 +300,10 @@ def supported(x: torch.Tensor, bn: nn.BatchNorm2d, residual) -> bool:
 
 
 def fused_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residual: torch.Tensor | None = None,
-                 stats: torch.Tensor | None = None):
+                 stats: torch.Tensor | None = None, defer: bool = False):
     """``stats``: optional [row_blocks, C, 2] (sum, sumsq) partials of ``x`` produced by the conv GEMM
-    epilogue (training mode only) — the statistics pass over ``x`` is then skipped."""
+    epilogue (training mode only) — the statistics pass over ``x`` is then skipped. ``defer``: with a residual
+    and ReLU, the output may be left for its consumer to write (PendingApply; inside a deferral_scope)."""
     if not supported(x, bn, residual):
         y = bn(x)
         if residual is not None:
@@ -229,8 +324,10 @@ def fused_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residua
     if rlink is not None and residual.dtype != torch.bfloat16:  # the epilogue addend is bf16
         rlink = None
     dlink = getattr(x, "_dla_dual", None) if training else None
-    y = _BNAct.apply(x, bn.weight, bn.bias, residual, rm, rv, training, float(bn.momentum or 0.0),
-                     float(bn.eps), relu, stats if training else None, rlink, dlink)
+    defer = (defer and training and residual is not None and residual.dtype == x.dtype
+             and _can_defer(x, relu, residual, bn.weight))
+    y = _apply_deferred(_BNAct, x, bn.weight, bn.bias, residual, rm, rv, training, float(bn.momentum or 0.0),
+                        float(bn.eps), relu, stats if training else None, rlink, dlink, defer)
     if y.grad_fn is not None:
         link = getattr(y.grad_fn, "link", None)
         if link is not None:

@@ -23,6 +23,7 @@ import torch.nn.functional as F
 from . import _ext
 from . import limits as _limits
 from .bn_act import ResidualLink
+from .bn_act import pending_of
 from .bn_act import bn_link_of as _bn_link_of
 
 # Fuse the backward reduction of a producing BatchNorm into this conv's dgrad epilogue (BNLink).
@@ -397,20 +398,29 @@ class _Conv1x1Fork(torch.autograd.Function):
     elementwise kernel over the block-input tensor (the autograd sum of the two uses of ``x``)."""
 
     @staticmethod
-    def forward(ctx, x, weight, want_stats: bool, rlink, sub: bool = False):
+    def forward(ctx, x, weight, want_stats: bool, rlink, sub: bool = False, pending=None):
         C = _ext.require()
         ctx.set_materialize_grads(False)
         ctx.rlink = rlink
         n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        w2 = weight.reshape(cout, cin).to(torch.bfloat16).contiguous()
+        if pending is not None:
+            # x is a deferred BN(+residual)+ReLU output: this GEMM writes it (and its ReLU mask) while staging
+            # its operand from the BN's input and the residual (gemm_apply.hip), then multiplies
+            p = pending
+            y2, stats = C.gemm_nt_apply(_rows(p.x), _rows(p.r), p.ws, p.wsd, w2, want_stats, _rows(x), p.mask)
+            p.clear()
+            CALLS["1x1_apply"] += 1
+        else:
+            y2, stats = C.gemm_nt(_rows(x), w2, want_stats)
         # sub: also hand on the stride-2 subsample of x (the downsample conv's input); its compact
-        # gradient is added at the even pixels inside the dgrad epilogue (no zero-filled scatter)
+        # gradient is added at the even pixels inside the dgrad epilogue (no zero-filled scatter). After the
+        # GEMM: a deferred x is written by it
         xs = None
         if sub:
             xs = C.subsample2(x) if (x.dtype == torch.bfloat16 and cin % 8 == 0) else \
                 x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last)
-        cout = weight.shape[0]
-        w2 = weight.reshape(cout, cin).to(torch.bfloat16).contiguous()
-        y2, stats = C.gemm_nt(_rows(x), w2, want_stats)
         y = y2.view(n, h, w, cout).permute(0, 3, 1, 2)
         ctx.save_for_backward(x, w2)
         ctx.wdtype = weight.dtype
@@ -449,7 +459,7 @@ class _Conv1x1Fork(torch.autograd.Function):
                 full = torch.zeros_like(x) if dident is None else dident.clone()
                 full[:, :, ::2, ::2] += dsub
                 dident = full
-            return dident, None, None, None, None
+            return dident, None, None, None, None, None
         odt = ctx.wdtype if ctx.wdtype in (torch.float32, torch.bfloat16) else torch.float32
         dy = dy.contiguous(memory_format=torch.channels_last).to(torch.bfloat16)
         dy2 = _rows(dy)
@@ -482,7 +492,7 @@ class _Conv1x1Fork(torch.autograd.Function):
             dw = _wgrad_after_dgrad(wgrad, ctx, (dy, x), dy.device)
         if wg is not None:
             dw = wg.result()
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 def _unpack_bits(mask: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
@@ -506,7 +516,13 @@ def conv1x1_fork(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False, sub
     and ``x_sub`` (= x[:, :, ::2, ::2], with sub) as a stride-2 downsample conv's input."""
     CALLS["1x1_fork"] += 1
     rlink = ResidualLink() if RESIDUAL_HANDOFF and x.requires_grad else None
-    y, stats, xa, xs = _Conv1x1Fork.apply(x, conv.weight, want_stats, rlink, sub)
+    pending = pending_of(x)
+    if pending is not None and not (x.is_contiguous(memory_format=torch.channels_last)
+                                    and _ext.require().gemm_nt_apply_ok(x.numel() // x.shape[1], conv.out_channels,
+                                                                        x.shape[1])):
+        pending.materialise()
+        pending = None
+    y, stats, xa, xs = _Conv1x1Fork.apply(x, conv.weight, want_stats, rlink, sub, pending)
     if rlink is not None:
         xa._dla_fork = rlink
     return y, stats, xa, xs

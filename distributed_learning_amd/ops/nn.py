@@ -124,11 +124,12 @@ def linear(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
 
 
 def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool = True,
-                residual: torch.Tensor | None = None, presubsampled: bool = False):
+                residual: torch.Tensor | None = None, presubsampled: bool = False, defer: bool = False):
     """``act(BN(conv(x)) [+ residual])``. With the native backend and native convs, a 1x1 conv runs as
     an MFMA GEMM whose epilogue also produces BN's batch statistics (one pass over the conv output
     saved). ``presubsampled``: ``x`` is already the stride-2 subsample a strided 1x1 ``conv`` would
-    take (conv_bn_act_fork(..., subsample=True)), so the conv runs with stride 1."""
+    take (conv_bn_act_fork(..., subsample=True)), so the conv runs with stride 1. ``defer``: the result
+    feeds only the next bottleneck's conv_bn_act_fork, which may write it itself (ops/bn_act.py PendingApply)."""
     if _BACKEND == "native" and _NATIVE_CONV and x.is_cuda:
         from . import conv as nconv
         from .bn_act import fused_bn_act, supported as bn_supported
@@ -138,7 +139,7 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
             y, stats = nconv.conv1x1(x, conv, want_stats=bn.training, stride=stride)
             if stats is not None and not bn_supported(y, bn, residual):
                 stats = None
-            return fused_bn_act(y, bn, relu, residual, stats)
+            return fused_bn_act(y, bn, relu, residual, stats, defer=defer)
         if nconv.supported3x3(x, conv):
             want = bn.training and nconv.CONV3_POLICY["fwd"] == "native"
             y, stats = nconv.conv3x3(x, conv, want_stats=want)
@@ -168,7 +169,7 @@ DUAL_RESIDUAL = True
 
 def conv_bn_add_conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, xd: torch.Tensor,
                             conv_d: nn.Conv2d, bn_d: nn.BatchNorm2d, relu: bool = True,
-                            presubsampled: bool = False) -> torch.Tensor:
+                            presubsampled: bool = False, defer: bool = False) -> torch.Tensor:
     """``act(BN(conv(x)) + BN_d(conv_d(xd)))`` — a residual block's last conv plus its downsample
     shortcut. Native path: both convs emit their BN statistics and one apply pass reads both conv
     outputs (the shortcut BN's output is never written). ``presubsampled``: ``xd`` is already the
@@ -180,7 +181,7 @@ def conv_bn_add_conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d
         a = _native_conv_stats(x, conv, True)
         b = _native_conv_stats(xd, conv_d, True, presubsampled) if a is not None else None
         if a is not None and b is not None and dual_supported(a[0], bn, b[0], bn_d):
-            return fused_bn_add_bn_act(a[0], bn, b[0], bn_d, relu, a[1], b[1])
+            return fused_bn_add_bn_act(a[0], bn, b[0], bn_d, relu, a[1], b[1], defer=defer)
         if a is not None and b is not None:  # convs done; BN the plain way
             from .bn_act import fused_bn_act
 
@@ -225,16 +226,19 @@ def conv_bn_act_fork(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu:
     ``x[:, :, ::2, ::2]`` for a stride-2 downsample conv (``conv_bn_act(..., presubsampled=True)``),
     whose compact gradient the same epilogue adds at the even pixels; None when the native path
     does not apply (then subsample inside the downsample conv as usual)."""
+    from .bn_act import ensure
+
     if _BACKEND == "native" and _NATIVE_CONV and x.is_cuda:
         from . import conv as nconv
         from .bn_act import fused_bn_act, supported as bn_supported
 
         sub_ok = subsample and FORK_SUBSAMPLE and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0
-        if nconv.fork_supported(x, conv):
+        if nconv.fork_supported(x, conv):  # writes a deferred x itself (or materialises it first)
             y, stats, ident, xs = nconv.conv1x1_fork(x, conv, want_stats=bn.training, sub=sub_ok)
             if stats is not None and not bn_supported(y, bn, None):
                 stats = None
             out = fused_bn_act(y, bn, relu, None, stats)
             return (out, ident, xs if sub_ok else None) if subsample else (out, ident)
+    ensure(x)
     out = conv_bn_act(x, conv, bn, relu)
     return (out, x, None) if subsample else (out, x)
