@@ -37,7 +37,7 @@ TABLE: Dict[str, Knob] = {
     "LAUNCH_GROUPS": Knob("1", "parallel/grad_sync.py", "0: fusion off (bucket cap 0) issues one collective launch per "
                                                         "gradient tensor, the reference's semantics (main.py:168-179); 1: "
                                                         "the per-tensor collectives launch in groups (profiles/r5/g04/)"),
-    "DEFER_APPLY": Knob("0", "ops/bn_act.py", "1: a bottleneck block's final BN(+residual)+ReLU output is written by the "
+    "DEFER_APPLY": Knob("1", "ops/bn_act.py", "1: a bottleneck block's final BN(+residual)+ReLU output is written by the "
                                               "next block's conv1 GEMM (gemm_apply.hip) instead of its own apply pass"),
     "AUTOTUNE_BUDGET_S": Knob("90", "parallel/autotune.py", "wall-clock budget of the all-reduce selection at N > 1"),
     "COMM_TIMEOUT_S": Knob("600", "csrc/comm/engine.cpp", "seconds before a collective / IPC barrier is declared dead"),
