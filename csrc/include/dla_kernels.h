@@ -303,8 +303,9 @@ void set_gemm_direct(int mode);
 // ws / ws2 the 7K BN workspaces (ws2 non-null: r is the shortcut BN's input), mask the ReLU bits; C [M][N]
 // (row stride N), B [N][K]; statistics [gemm_apply_rows(M)][N][2] when stats is non-null. Writes out + mask
 // and C in one pass.
-constexpr int kGemmApplyMaxK = 512;
+constexpr int kGemmApplyMaxK = 2048;  // coefficient table: 4 x K fp32 of LDS (dual)
 bool gemm_apply_ok(int64_t M, int N, int K);
+void set_gemm_apply_max_k(int k);  // <= 0: DLA_APPLY_MAX_K / default 512
 int gemm_apply_rows(int64_t M);
 void launch_gemm_apply(const void* y, const void* r, const float* ws, const float* ws2, void* out, uint8_t* mask,
                        const void* B, int64_t ldb, void* C, int M, int N, int K, float* stats, hipStream_t stream);

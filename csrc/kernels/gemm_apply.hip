@@ -17,6 +17,7 @@
 // (and to HBM) after them, so the loads stay in flight under the MFMAs. The per-channel coefficients sit in
 // LDS for the whole K.
 #include <algorithm>
+#include <cstdlib>
 
 #include "dla_common.h"
 #include "dla_kernels.h"
@@ -166,8 +167,18 @@ void launch_apply(const ApplyArgs& ap, const bf16_t* B, int64_t ldb, bf16_t* C, 
 
 }  // namespace
 
+// Largest K served (the consumer's conv1 input channels): 512 covers stages 1-2 and the stage-2 -> 3 transition,
+// where the 128-row register-staged tile is also the unfused GEMM's; above it the unfused forward runs on the
+// 256x256 LDS-DMA tile. DLA_APPLY_MAX_K / set_gemm_apply_max_k (<= kGemmApplyMaxK) for A/B.
+static int g_apply_max_k = [] {
+  const char* e = std::getenv("DLA_APPLY_MAX_K");
+  const int v = e ? std::atoi(e) : 0;
+  return v > 0 ? std::min(v, kGemmApplyMaxK) : 512;
+}();
+void set_gemm_apply_max_k(int k) { g_apply_max_k = k > 0 ? std::min(k, kGemmApplyMaxK) : 512; }
+
 bool gemm_apply_ok(int64_t M, int N, int K) {
-  return M > 0 && K % kBK == 0 && K >= kBK && K <= kGemmApplyMaxK && N % 64 == 0 && N > 0 &&
+  return M > 0 && K % kBK == 0 && K >= kBK && K <= g_apply_max_k && N % 64 == 0 && N > 0 &&
          M * (int64_t)K * 2 < ((int64_t)1 << 31) && M * (int64_t)N * 2 < ((int64_t)1 << 31);
 }
 

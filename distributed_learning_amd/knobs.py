@@ -39,6 +39,8 @@ TABLE: Dict[str, Knob] = {
                                                         "the per-tensor collectives launch in groups (profiles/r5/g04/)"),
     "DEFER_APPLY": Knob("1", "ops/bn_act.py", "1: a bottleneck block's final BN(+residual)+ReLU output is written by the "
                                               "next block's conv1 GEMM (gemm_apply.hip) instead of its own apply pass"),
+    "APPLY_MAX_K": Knob("512", "csrc/kernels/gemm_apply.hip", "largest conv1 input width whose deferred block-final "
+                                                               "apply the conv1 GEMM writes (<= 2048)"),
     "AUTOTUNE_BUDGET_S": Knob("90", "parallel/autotune.py", "wall-clock budget of the all-reduce selection at N > 1"),
     "COMM_TIMEOUT_S": Knob("600", "csrc/comm/engine.cpp", "seconds before a collective / IPC barrier is declared dead"),
     # ---- scheduling of the backward ----------------------------------------------------------------

@@ -39,9 +39,22 @@ def _as4d(t):  # [M, K] rows as a channels_last [1, K, M, 1] tensor (bn_apply_de
     return t.view(1, M, 1, K).permute(0, 3, 1, 2)
 
 
+@pytest.fixture
+def wide_k():
+    """Serve K up to 2048 and keep the unfused reference GEMM on the same register-staged main loop."""
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    C.set_gemm_apply_max_k(2048)
+    C.set_mfma_pipeline(0)
+    yield
+    C.set_gemm_apply_max_k(-1)
+    C.set_mfma_pipeline(-1)
+
+
 @pytest.mark.parametrize("dual", [False, True])
-@pytest.mark.parametrize("shape", SHAPES)
-def test_apply_gemm_matches_unfused_and_torch(cuda, shape, dual):
+@pytest.mark.parametrize("shape", SHAPES + [(4097, 1024, 256), (3001, 2048, 512), (1000, 1024, 512)])
+def test_apply_gemm_matches_unfused_and_torch(cuda, wide_k, shape, dual):
     from distributed_learning_amd.ops import _ext
 
     C = _ext.require()
@@ -102,7 +115,7 @@ def test_apply_gemm_stage1_bench_shape(cuda):
     assert ((c[tail].float() - ref).norm() / ref.norm()).item() < 5e-3
 
 
-def _resnet_step(cuda, defer: bool):
+def _resnet_step(cuda, defer: bool, max_k: int = -1):
     from distributed_learning_amd import knobs
     from distributed_learning_amd.models.resnet import resnet50
     from distributed_learning_amd.ops import _ext
@@ -119,6 +132,9 @@ def _resnet_step(cuda, defer: bool):
     old = knobs._CACHE.get("DEFER_APPLY")
     knobs._CACHE["DEFER_APPLY"] = "1" if defer else "0"
     C.set_tile256_min_k_stats(1 << 30)  # the same statistics tiles on both paths (bitwise comparison)
+    C.set_gemm_apply_max_k(max_k)
+    if max_k > 512:
+        C.set_mfma_pipeline(0)  # the unfused K > 512 forwards on the fused kernel's main loop too
     dnn.set_backend("native")
     dnn.set_native_conv(True)
     before = dict(bn_act.CALLS), nconv.CALLS["1x1_apply"]
@@ -131,6 +147,8 @@ def _resnet_step(cuda, defer: bool):
         dnn.set_backend("torch")
         dnn.set_native_conv(False)
         C.set_tile256_min_k_stats(-1)
+        C.set_gemm_apply_max_k(-1)
+        C.set_mfma_pipeline(-1)
         if old is None:
             knobs._CACHE.pop("DEFER_APPLY", None)
         else:
@@ -148,6 +166,18 @@ def test_resnet50_step_with_deferred_apply_matches(cuda):
     # 15 block outputs feed a next bottleneck; the 7 with K <= 512 are written by their consumer's GEMM
     assert used_d["deferred"] == 15 and used_d["fused"] == 7 and used_d["materialised"] == 8, used_d
     assert used_u["deferred"] == 0 and used_u["fused"] == 0, used_u
+    assert loss_d == loss_u
+    assert torch.equal(out_d, out_u)
+    for a, b in zip(s_d, s_u):
+        assert torch.equal(a, b)
+    for i, (a, b) in enumerate(zip(g_d, g_u)):
+        assert torch.equal(a, b), i
+
+
+def test_resnet50_step_with_every_chained_output_deferred_matches(cuda):
+    out_d, loss_d, g_d, s_d, used_d = _resnet_step(cuda, True, 2048)
+    out_u, loss_u, g_u, s_u, used_u = _resnet_step(cuda, False, 2048)
+    assert used_d["deferred"] == 15 and used_d["fused"] == 15 and used_d["materialised"] == 0, used_d
     assert loss_d == loss_u
     assert torch.equal(out_d, out_u)
     for a, b in zip(s_d, s_u):
