@@ -305,7 +305,8 @@ void set_gemm_direct(int mode);
 // and C in one pass.
 constexpr int kGemmApplyMaxK = 2048;  // coefficient table: 4 x K fp32 of LDS (dual)
 bool gemm_apply_ok(int64_t M, int N, int K);
-void set_gemm_apply_max_k(int k);  // <= 0: DLA_APPLY_MAX_K / default 512
+void set_gemm_apply_max_k(int k);
+void set_wgrad_w4(int mode);  // 128x256 tiles for the Cout-128 3x3 weight gradients: -1 env (DLA_WGRAD_W4), 0, 1  // <= 0: DLA_APPLY_MAX_K / default 512
 int gemm_apply_rows(int64_t M);
 void launch_gemm_apply(const void* y, const void* r, const float* ws, const float* ws2, void* out, uint8_t* mask,
                        const void* B, int64_t ldb, void* C, int M, int N, int K, float* stats, hipStream_t stream);

@@ -840,14 +840,28 @@ void launch_conv3x3s2_dgrad(const void* dy, const void* w, void* dx, int N, int 
 // 256 (Cout and Cin in {256, 512, ...}: the compute-bound 14x14 / 7x7 layers), as for gemm_tn
 static bool wgrad_wide(int Cin, int Cout) { return tn256_enabled() && Cout % 256 == 0 && Cin % 256 == 0; }
 
+// 128 x 256 four-wave tiles (64 x 128 wave tiles: half the LDS fragment reads per MFMA of the 64 x 64 ones, one
+// block per CU) for the Cout = 128 weight gradients (stage 2), whose 9 * Cin columns the 256x256 tiles cannot
+// cover without wasting half the rows. DLA_WGRAD_W4=1 / set_wgrad_w4 (A/B; default off)
+static int g_wgrad_w4 = -1;
+void set_wgrad_w4(int mode) { g_wgrad_w4 = mode < 0 ? -1 : (mode ? 1 : 0); }
+static bool wgrad_w4(int Cin, int Cout) {
+  static const bool env = [] {
+    const char* e = std::getenv("DLA_WGRAD_W4");
+    return e && e[0] == '1';
+  }();
+  const bool on = g_wgrad_w4 < 0 ? env : g_wgrad_w4 == 1;
+  return on && !wgrad_wide(Cin, Cout) && Cout == 128 && Cin % 64 == 0;
+}
+
 int conv3x3_wgrad_splits(int N, int H, int W, int Cin, int Cout, int stride) {
   const ConvGeom g = make_geom(N, H, W, Cin, Cout, stride);
   const int P = g.N * g.OH * g.OW;
-  const bool wide = wgrad_wide(Cin, Cout);
-  const int bm = wide ? 256 : (Cout <= 64 ? 64 : 128), bn = wide ? 256 : 128;
+  const bool wide = wgrad_wide(Cin, Cout), w4 = wgrad_w4(Cin, Cout);
+  const int bm = wide ? 256 : (Cout <= 64 ? 64 : 128), bn = (wide || w4) ? 256 : 128;
   const int tiles = ((Cout + bm - 1) / bm) * ((9 * Cin + bn - 1) / bn);
-  // ~2 workgroups per CU (one per CU for the 8-wave tiles)
-  const int splits = std::max(1, (wide ? splitk_target_blocks() / 2 : splitk_target_blocks()) / std::max(1, tiles));
+  // ~2 workgroups per CU (one per CU for the 8-wave and the 128x256 tiles)
+  const int splits = std::max(1, (wide || w4 ? splitk_target_blocks() / 2 : splitk_target_blocks()) / std::max(1, tiles));
   const int max_splits = std::max(1, P / (8 * kBK));          // >= 8 k-steps per split
   return std::max(1, std::min(splits, max_splits));
 }
@@ -881,6 +895,11 @@ void launch_conv3x3_wgrad(const void* dy, const void* x, float* partial, int spl
     if (pipe == 2) DLA_WG8(2);
     else DLA_WG8(4);
 #undef DLA_WG8
+  } else if (wgrad_w4(Cin, Cout)) {
+    const int nt = (No + 255) / 256;
+    hipLaunchKernelGGL((conv3x3_wgrad_kernel<128, 256, 2>), dim3(nt * splits), dim3(kThreads),
+                       (run_mainloop_lds_bytes<2, 128, 256, KLoader<128>, Im2colKLoader<256, true>>()), stream,
+                       (const bf16_t*)dy, (const bf16_t*)x, g, partial, kps, nt, (int)splitk_xcd_remap());
   } else if (Cout <= 64) {
     DLA_WG_P(64)
   } else {

@@ -1233,6 +1233,7 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("y"), pybind11::arg("r"), pybind11::arg("ws"), pybind11::arg("wsd"), pybind11::arg("B"),
         pybind11::arg("stats"), pybind11::arg("out"), pybind11::arg("mask"));
   m.def("gemm_nt_apply_ok", &gemm_nt_apply_ok, "shapes gemm_nt_apply serves (M rows, N outputs, K channels)");
+  m.def("set_wgrad_w4", &set_wgrad_w4, "128x256 tiles for the Cout-128 3x3 weight gradients (-1 env, 0, 1)");
   m.def("set_gemm_apply_max_k", &set_gemm_apply_max_k, "largest K gemm_nt_apply serves (<= 0: environment / 512)");
   m.def("bn_dual_bwd", &bn_dual_bwd, "backward of bn_dual_fwd (one dy read for both BatchNorms)", pybind11::arg("dy"),
         pybind11::arg("mask"), pybind11::arg("x"), pybind11::arg("ws"), pybind11::arg("weight"), pybind11::arg("xd"),

@@ -41,6 +41,7 @@ TABLE: Dict[str, Knob] = {
                                               "next block's conv1 GEMM (gemm_apply.hip) instead of its own apply pass"),
     "APPLY_MAX_K": Knob("512", "csrc/kernels/gemm_apply.hip", "largest conv1 input width whose deferred block-final "
                                                                "apply the conv1 GEMM writes (<= 2048)"),
+    "WGRAD_W4": Knob("0", "csrc/kernels/conv.hip", "1: 128x256 four-wave tiles for the Cout-128 3x3 weight gradients"),
     "AUTOTUNE_BUDGET_S": Knob("90", "parallel/autotune.py", "wall-clock budget of the all-reduce selection at N > 1"),
     "COMM_TIMEOUT_S": Knob("600", "csrc/comm/engine.cpp", "seconds before a collective / IPC barrier is declared dead"),
     # ---- scheduling of the backward ----------------------------------------------------------------

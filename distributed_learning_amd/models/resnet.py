@@ -82,7 +82,8 @@ class Bottleneck(nn.Module):
         out = dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True)
         # a block whose output goes straight into the next bottleneck (ResNet.forward) leaves the final apply
         # pass to that block's conv1 GEMM (ops/bn_act.py PendingApply); nothing else may observe it
-        defer = self.defer_output and not (self._forward_hooks or self._forward_pre_hooks)
+        defer = self.defer_output and not (self._forward_hooks or self._forward_pre_hooks
+                                           or nn.modules.module._global_forward_hooks)
         if self.downsample is None:
             return dnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=xa, defer=defer)
         # the shortcut BN is applied inside the block's final apply pass (never materialised)

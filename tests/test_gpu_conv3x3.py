@@ -208,3 +208,25 @@ def test_conv3x3_halo_c64(cuda, version):
     r = subprocess.run([sys.executable, "-c", _HALO_SCRIPT % root], env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0 and "halo ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+@pytest.mark.parametrize("N,H,stride", [(2, 28, 1), (3, 13, 1), (2, 56, 2), (64, 28, 1)])
+def test_conv3x3_wgrad_128x256_tiles(cuda, N, H, stride):
+    """128x256 four-wave weight-gradient tiles for Cout = 128 (set_wgrad_w4): the last column tile covers taps
+    past the 9th (masked), against fp32 PyTorch and the 128x128 tiles."""
+    C = _C()
+    torch.manual_seed(0)
+    x = torch.randn(N, 128, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    oh = (H - 1) // stride + 1
+    dy = torch.randn(N, 128, oh, oh, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL)
+    try:
+        C.set_wgrad_w4(0)
+        ref_tile = C.conv3x3_wgrad(dy, x, stride, torch.float32)
+        C.set_wgrad_w4(1)
+        got = C.conv3x3_wgrad(dy, x, stride, torch.float32)
+    finally:
+        C.set_wgrad_w4(-1)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (128, 128, 3, 3), dy.float(), stride, 1)
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=CL)
+    assert _rel(got, ref) < 1e-2
+    assert _rel(got, ref_tile) < 1e-5  # same products, another split of the pixel sum
