@@ -308,8 +308,10 @@ bool gemm_apply_ok(int64_t M, int N, int K);
 void set_gemm_apply_max_k(int k);
 void set_wgrad_w4(int mode);  // 128x256 tiles for the Cout-128 3x3 weight gradients: -1 env (DLA_WGRAD_W4), 0, 1  // <= 0: DLA_APPLY_MAX_K / default 512
 int gemm_apply_rows(int64_t M);
+// xs (optional): also write out's stride-2 subsample [n][H/2][W/2][K] (rows m = (n H + h) W + w; H, W even)
 void launch_gemm_apply(const void* y, const void* r, const float* ws, const float* ws2, void* out, uint8_t* mask,
-                       const void* B, int64_t ldb, void* C, int M, int N, int K, float* stats, hipStream_t stream);
+                       const void* B, int64_t ldb, void* C, int M, int N, int K, float* stats, hipStream_t stream,
+                       void* xs = nullptr, int H = 0, int W = 0);
 // the register-stored tiles as a persistent kernel with n blocks per CU (0: one block per tile; -1: DLA_GEMM_PERSIST)
 void set_gemm_persist(int blocks_per_cu);
 // fp32 convolutions on v_mfma_f32_16x16x4_f32 (conv_f32.hip): x NHWC [N][H][W][C], w OHWI [Cout][R][S][C], y NHWC

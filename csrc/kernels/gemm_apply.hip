@@ -36,6 +36,10 @@ struct ApplyArgs {
   const float* ws2;  // kDual: the shortcut BN's
   bf16_t* out;       // act(BN(y) + r) [M][K]
   uint8_t* mask;     // its ReLU bits: bit j of byte e >> 3 for element e = m * K + k
+  // optional stride-2 subsample of out, [n][H/2][W/2][K] for rows m = (n H + h) W + w (the downsample conv's input
+  // at a stage transition; written from the same registers instead of a second pass over out)
+  bf16_t* xs;
+  int H, W;
 };
 
 template <int BM, int BN, bool kStats, bool kDual>
@@ -70,13 +74,19 @@ __global__ __launch_bounds__(kThreads, blocks_per_cu(BM, BN, kThreads)) void gem
   const int wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN;
   // chunk i of this thread: row (tid + i * NT) >> 3, the same 8 channels kc .. kc + 7 in every chunk and k-step
   const int kc = (tid & 7) * 8;
-  int64_t off[GA::CH];
+  int64_t off[GA::CH], xoff[GA::CH];
   bool ok[GA::CH];
 #pragma unroll
   for (int i = 0; i < GA::CH; ++i) {
     const int64_t gr = row0 + ((tid + i * kThreads) >> 3);
     ok[i] = gr < M;
     off[i] = (ok[i] ? gr : 0) * K + kc;
+    xoff[i] = -1;
+    if (ap.xs && ok[i]) {  // even (h, w): its position in the subsample
+      const int64_t q = gr / ap.W, w = gr - q * ap.W;
+      const int64_t n = q / ap.H, h = q - n * ap.H;
+      if (!((h | w) & 1)) xoff[i] = ((n * (ap.H >> 1) + (h >> 1)) * (ap.W >> 1) + (w >> 1)) * K + kc;
+    }
   }
   ushort8_t ya[GA::CH], ra[GA::CH], rb[GB::CH];
   auto fetch = [&](int k0) {
@@ -114,6 +124,7 @@ __global__ __launch_bounds__(kThreads, blocks_per_cu(BM, BN, kThreads)) void gem
       if (writer && ok[i]) {
         *reinterpret_cast<ushort8_t*>(ap.out + off[i] + k0) = o;
         ap.mask[(off[i] + k0) >> 3] = (uint8_t)bits;
+        if (xoff[i] >= 0) *reinterpret_cast<ushort8_t*>(ap.xs + xoff[i] + k0) = o;
       }
     }
     tile_store<BM, LA>(As, ta);
@@ -185,8 +196,9 @@ bool gemm_apply_ok(int64_t M, int N, int K) {
 int gemm_apply_rows(int64_t M) { return (int)((M + 127) / 128); }
 
 void launch_gemm_apply(const void* y, const void* r, const float* ws, const float* ws2, void* out, uint8_t* mask,
-                       const void* B, int64_t ldb, void* C, int M, int N, int K, float* stats, hipStream_t stream) {
-  const ApplyArgs ap{(const bf16_t*)y, (const bf16_t*)r, ws, ws2, (bf16_t*)out, mask};
+                       const void* B, int64_t ldb, void* C, int M, int N, int K, float* stats, hipStream_t stream,
+                       void* xs, int H, int W) {
+  const ApplyArgs ap{(const bf16_t*)y, (const bf16_t*)r, ws, ws2, (bf16_t*)out, mask, (bf16_t*)xs, H, W};
   const bf16_t* b = (const bf16_t*)B;
   bf16_t* c = (bf16_t*)C;
 #define DLA_APPLY(BN_)                                                                          \

@@ -630,7 +630,8 @@ std::vector<at::Tensor> gemm_nt(at::Tensor A, at::Tensor B, bool stats, c10::opt
 // mask, returns (C = out @ B^T, statistics [gemm_apply_rows][N][2] or undefined). y, r, out: bf16 [M, K]
 // contiguous rows; B [N, K]; ws / wsd the 7K workspaces (wsd: r is the shortcut BN's input).
 std::vector<at::Tensor> gemm_nt_apply(at::Tensor y, at::Tensor r, at::Tensor ws, c10::optional<at::Tensor> wsd,
-                                      at::Tensor B, bool stats, at::Tensor out, at::Tensor mask) {
+                                      at::Tensor B, bool stats, at::Tensor out, at::Tensor mask,
+                                      c10::optional<at::Tensor> xs, int64_t H, int64_t W) {
   check_mat(y, "y");
   check_mat(r, "r");
   check_mat(out, "out");
@@ -646,12 +647,22 @@ std::vector<at::Tensor> gemm_nt_apply(at::Tensor y, at::Tensor r, at::Tensor ws,
   if (dual)
     TORCH_CHECK(wsd->scalar_type() == at::kFloat && wsd->is_contiguous() && wsd->numel() == 7 * (int64_t)K, "wsd: 7K fp32");
   TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kByte && mask.numel() * 8 >= M * K, "mask: one bit per element");
+  const bool sub = xs.has_value() && xs->defined();
+  if (sub) {
+    TORCH_CHECK(H > 0 && W > 0 && H % 2 == 0 && W % 2 == 0 && M % (H * W) == 0, "gemm_nt_apply: xs needs even H, W");
+    TORCH_CHECK(xs->is_cuda() && xs->scalar_type() == at::kBFloat16 && xs->dim() == 4 &&
+                    xs->is_contiguous(at::MemoryFormat::ChannelsLast) && xs->size(0) == M / (H * W) &&
+                    xs->size(1) == K && xs->size(2) == H / 2 && xs->size(3) == W / 2 &&
+                    (reinterpret_cast<uintptr_t>(xs->data_ptr()) & 15) == 0,
+                "gemm_nt_apply: xs must be a channels_last bf16 [n, K, H/2, W/2] tensor");
+  }
   at::Tensor C = at::empty({M, N}, y.options());
   at::Tensor S;
   if (stats) S = at::empty({gemm_apply_rows(M), N, 2}, y.options().dtype(at::kFloat));
   launch_gemm_apply(y.data_ptr(), r.data_ptr(), ws.data_ptr<float>(), dual ? wsd->data_ptr<float>() : nullptr,
                     out.data_ptr(), mask.data_ptr<uint8_t>(), B.data_ptr(), B.stride(0), C.data_ptr(), (int)M, N, K,
-                    stats ? S.data_ptr<float>() : nullptr, current_stream(y));
+                    stats ? S.data_ptr<float>() : nullptr, current_stream(y), sub ? xs->data_ptr() : nullptr, (int)H,
+                    (int)W);
   return {C, S};
 }
 
@@ -1231,7 +1242,8 @@ void bind_nn(pybind11::module& m) {
   m.def("gemm_nt_apply", &gemm_nt_apply,
         "1x1-conv forward over a deferred act(BN(y) + r): writes the BN output + mask and returns (C, stats)",
         pybind11::arg("y"), pybind11::arg("r"), pybind11::arg("ws"), pybind11::arg("wsd"), pybind11::arg("B"),
-        pybind11::arg("stats"), pybind11::arg("out"), pybind11::arg("mask"));
+        pybind11::arg("stats"), pybind11::arg("out"), pybind11::arg("mask"), pybind11::arg("xs") = pybind11::none(),
+        pybind11::arg("H") = 0, pybind11::arg("W") = 0);
   m.def("gemm_nt_apply_ok", &gemm_nt_apply_ok, "shapes gemm_nt_apply serves (M rows, N outputs, K channels)");
   m.def("set_wgrad_w4", &set_wgrad_w4, "128x256 tiles for the Cout-128 3x3 weight gradients (-1 env, 0, 1)");
   m.def("set_gemm_apply_max_k", &set_gemm_apply_max_k, "largest K gemm_nt_apply serves (<= 0: environment / 512)");

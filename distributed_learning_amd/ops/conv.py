@@ -405,20 +405,24 @@ class _Conv1x1Fork(torch.autograd.Function):
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         w2 = weight.reshape(cout, cin).to(torch.bfloat16).contiguous()
+        # sub: also hand on the stride-2 subsample of x (the downsample conv's input); its compact
+        # gradient is added at the even pixels inside the dgrad epilogue (no zero-filled scatter)
+        xs = None
         if pending is not None:
-            # x is a deferred BN(+residual)+ReLU output: this GEMM writes it (and its ReLU mask) while staging
-            # its operand from the BN's input and the residual (gemm_apply.hip), then multiplies
+            # x is a deferred BN(+residual)+ReLU output: this GEMM writes it (and its ReLU mask, and with sub its
+            # stride-2 subsample) while staging its operand from the BN's input and the residual (gemm_apply.hip),
+            # then multiplies
             p = pending
-            y2, stats = C.gemm_nt_apply(_rows(p.x), _rows(p.r), p.ws, p.wsd, w2, want_stats, _rows(x), p.mask)
+            if sub and knobs.flag("APPLY_SUBSAMPLE"):
+                xs = torch.empty((n, cin, h // 2, w // 2), dtype=x.dtype, device=x.device,
+                                 memory_format=torch.channels_last)
+            y2, stats = C.gemm_nt_apply(_rows(p.x), _rows(p.r), p.ws, p.wsd, w2, want_stats, _rows(x), p.mask,
+                                        xs, h if xs is not None else 0, w if xs is not None else 0)
             p.clear()
             CALLS["1x1_apply"] += 1
         else:
             y2, stats = C.gemm_nt(_rows(x), w2, want_stats)
-        # sub: also hand on the stride-2 subsample of x (the downsample conv's input); its compact
-        # gradient is added at the even pixels inside the dgrad epilogue (no zero-filled scatter). After the
-        # GEMM: a deferred x is written by it
-        xs = None
-        if sub:
+        if sub and xs is None:
             xs = C.subsample2(x) if (x.dtype == torch.bfloat16 and cin % 8 == 0) else \
                 x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last)
         y = y2.view(n, h, w, cout).permute(0, 3, 1, 2)

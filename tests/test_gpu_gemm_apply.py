@@ -90,6 +90,27 @@ def test_apply_gemm_matches_unfused_and_torch(cuda, wide_k, shape, dual):
     assert torch.allclose(st[:, :, 0].sum(0), csum, rtol=1e-3, atol=1e-2 * csum.abs().max().item())
 
 
+@pytest.mark.parametrize("n,H,W,K,N,dual", [(3, 14, 10, 256, 128, False), (2, 28, 28, 512, 256, True),
+                                            (5, 6, 8, 256, 64, False)])
+def test_apply_gemm_writes_stride2_subsample(cuda, n, H, W, K, N, dual):
+    """At a stage transition the fused kernel also writes out[:, ::2, ::2] (the downsample conv's input)."""
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    M = n * H * W
+    y, r, ws, wsd, w = _case(cuda, M, K, N, dual, seed=3)
+    out = torch.empty((M, K), device=cuda, dtype=torch.bfloat16)
+    mask = torch.empty((M * K + 7) // 8, device=cuda, dtype=torch.uint8)
+    xs = torch.full((n, K, H // 2, W // 2), float("nan"), device=cuda, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    c, st = C.gemm_nt_apply(y, r, ws, wsd, w, True, out, mask, xs, H, W)
+    c0, st0 = C.gemm_nt_apply(y, r, ws, wsd, w, True, torch.empty_like(out), torch.empty_like(mask))
+    torch.cuda.synchronize()
+    ref = out.view(n, H, W, K)[:, ::2, ::2].permute(0, 3, 1, 2)
+    assert torch.equal(xs, ref)
+    assert torch.equal(c, c0) and torch.equal(st, st0)
+
+
 def test_apply_gemm_stage1_bench_shape(cuda):
     """conv1 of ResNet-50 layer1 blocks 2-3 at bench.py's batch (M = 1280 x 56 x 56, K 256, N 64)."""
     from distributed_learning_amd.ops import _ext
@@ -99,11 +120,13 @@ def test_apply_gemm_stage1_bench_shape(cuda):
     y, r, ws, wsd, w = _case(cuda, M, K, N, False, seed=1)
     out = torch.empty((M, K), device=cuda, dtype=torch.bfloat16)
     mask = torch.empty((M * K + 7) // 8, device=cuda, dtype=torch.uint8)
-    c, st = C.gemm_nt_apply(y, r, ws, None, w, True, out, mask)
+    xs = torch.empty((1280, K, 28, 28), device=cuda, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    c, st = C.gemm_nt_apply(y, r, ws, None, w, True, out, mask, xs, 56, 56)
     out_u = torch.empty_like(out)
     mask_u = torch.empty_like(mask)
     C.bn_apply_deferred(_as4d(y), _as4d(r), ws, None, _as4d(out_u), mask_u)
     del y, r
+    assert torch.equal(xs, C.subsample2(out_u.view(1280, 56, 56, K).permute(0, 3, 1, 2)))
     c_u, st_u = C.gemm_nt(out_u, w, True, None, False, 2)
     torch.cuda.synchronize()
     assert torch.equal(out, out_u)
