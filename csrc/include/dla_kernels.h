@@ -287,9 +287,12 @@ int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_k
 struct BnBwdArgs;
 // bn_bwd (k-major data gradients): the output is the dy of a fused BN; its backward-reduction partials
 // [gemm_stream_rows][N][2] are written to bn_bwd->part instead of statistics.
+// apply_ws (forwards with statistics): A is the input of a deferred BN+ReLU (7K workspace apply_ws); the kernel
+// multiplies relu(A * scale + shift) and writes it to apply_out (A's layout)
 bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
                         int M, int N, int K, float* stats, hipStream_t stream, const void* addend = nullptr,
-                        int64_t ldd = 0, const uint8_t* addend_mask = nullptr, const BnBwdArgs* bn_bwd = nullptr);
+                        int64_t ldd = 0, const uint8_t* addend_mask = nullptr, const BnBwdArgs* bn_bwd = nullptr,
+                        const float* apply_ws = nullptr, void* apply_out = nullptr);
 void set_gemm_stream(int mode);
 // 128x128 1x1 GEMM tiles stored straight from the accumulators (gemm_direct.hip): the transposed product,
 // lane-exchange to 16-byte chunks, statistics by DPP row sums; same outputs / statistics layout as

@@ -69,6 +69,11 @@ struct StreamArgs {
   const float* bws;
   const uint8_t* bmask;
   int bmode;
+  // deferred BN+ReLU of the A operand (kAp, forwards): A = y, the BN's input; the kernel multiplies
+  // relu(y * scale + shift) (scale / shift at aws[2K, 3K) / [3K, 4K) of the BN's 7K workspace) and writes it to aout
+  // (row stride lda) from the column panel 0 blocks
+  const float* aws;
+  bf16_t* aout;
 };
 
 // image row of panel-local weight row p (0..63 within a wave's 64 columns): the MFMA A-operand row
@@ -88,9 +93,13 @@ typedef int i32x4_t __attribute__((ext_vector_type(4)));
 // 4-chunk ring of the other variants.
 __host__ __device__ constexpr bool stream_two_blocks(bool add, bool bnb) { return add && !bnb; }
 
-template <int BN, int KC, bool kBT, bool kStats, bool kAdd = false, int kBM = -1>
+// kAp: the A operand is a deferred BN+ReLU output (ops/bn_act.py PendingApply): each thread transforms the 16-byte
+// pieces its own LDS-DMA brought in (after its vmcnt wait, before the barrier that publishes the chunk), writes
+// them back in place and stores them to aout: the BN's apply pass and the GEMM's re-read of its output disappear.
+template <int BN, int KC, bool kBT, bool kStats, bool kAdd = false, int kBM = -1, bool kAp = false>
 __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) void gemm_stream_kernel(const StreamArgs s) {
   constexpr bool kBnb = kBM >= 0;
+  static_assert(!kAp || (!kBT && !kAdd && !kBnb), "apply-on-load: forwards only");
   static_assert(!(kStats && kBnb), "the partials buffer holds either the statistics or the BN-backward sums");
   constexpr int kSP = stream_lookahead(KC, stream_two_blocks(kAdd, kBnb));
   constexpr int kSS = kSP + 1;
@@ -107,13 +116,16 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
   // ops issued after chunk q before its wait. The epilogue's operand loads are waited for by their use
   // (which drains everything older, chunk q included), so a count clamped to the 6-bit field is only
   // stricter than necessary, never too weak
-  constexpr int kVmAfter = ((kSP - 1) * 4 + Q * (E + F)) < 63 ? ((kSP - 1) * 4 + Q * (E + F)) : 63;
-  static_assert(kBnb || (kSP - 1) * 4 + Q * (E + F) <= 63, "vmcnt is a 6-bit count");
+  // (kAp: each iteration also stores its chunk's D transformed pieces before issuing the next chunk)
+  constexpr int kVmRaw = (kSP - 1) * (kAp ? 2 * D : D) + Q * (E + F);
+  constexpr int kVmAfter = kVmRaw < 63 ? kVmRaw : 63;
+  static_assert(kBnb || kVmRaw <= 63, "vmcnt is a 6-bit count");
   constexpr int kPanelElems = BN * kBK;     // one weight sub-image [BN][64]
 
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16_t* Bs = reinterpret_cast<bf16_t*>(smem_raw);  // KC sub-images [BN][64]
   bf16_t* ring = Bs + KC * kPanelElems;              // kSS slots [128][64]
+  float* coef = reinterpret_cast<float*>(ring + kSS * kChunkElems);  // kAp: [scale | shift] x KC * 64
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave % WGN, wm = wave / WGN;
@@ -188,7 +200,11 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
                        ring0 + (uint32_t)((q % kSS) * kChunkElems * 2));
   };
 
-  // the weight panel's plain loads and LDS writes must be complete before the ring starts counting
+  if constexpr (kAp) {
+    for (int i = tid; i < 2 * KC * kBK; i += 256) coef[i] = s.aws[2 * KC * kBK + i];
+  }
+  // the weight panel's (and coefficient table's) plain loads and LDS writes must be complete before the ring
+  // starts counting
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -251,6 +267,12 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
   for (int q = 0; q < kSP; ++q) issue(q);
 
   const __amdgpu_buffer_rsrc_t rc = make_srd(s.c, (uint32_t)((int64_t)M * s.ldc * 2));
+  // kAp: the pieces of every chunk this thread DMAs share one logical 8-channel group (rm_glds_kc(tid + 256 i) does
+  // not depend on i); only column panel 0 writes the transformed operand
+  const __amdgpu_buffer_rsrc_t rao = make_srd(kAp ? (void*)s.aout : (void*)s.c,
+                                              kAp ? (uint32_t)((int64_t)M * s.lda * 2) : 0u);
+  const int alk = rm_glds_kc(tid);
+  const bool awriter = bn == 0;
   float st_s[4][4], st_q[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -264,6 +286,29 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
     // after chunk q was issued
     if (q < kSP) vm_wait<(kSP - 1) * D>();
     else vm_wait<kVmAfter>();
+    if constexpr (kAp) {  // this thread's pieces of chunk q have landed: BN + ReLU in place, store the result
+      const int kc = q % KC;
+      const int64_t arow0 = (int64_t)(grp + (q / KC) * s.mg) * kSBM;
+      bf16_t* slot = ring + (q % kSS) * kChunkElems;
+      float sc[8], sh[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sc[j] = coef[kc * kBK + alk + j];
+        sh[j] = coef[KC * kBK + kc * kBK + alk + j];
+      }
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const int c = tid + i * 256;
+        const int64_t gr = arow0 + vr[i];
+        const ushort8_t v = *reinterpret_cast<const ushort8_t*>(slot + c * 8);
+        ushort8_t o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = gr < M ? f32_to_bf16(fmaxf(fmaf(bf16_to_f32(v[j]), sc[j], sh[j]), 0.f)) : 0;
+        *reinterpret_cast<ushort8_t*>(slot + c * 8) = o;
+        const uint32_t off = (awriter && gr < M) ? (uint32_t)((gr * s.lda + kc * kBK + alk) * 2) : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, o), rao, off, 0, 0);
+      }
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: slot (q-1) % kSS is refilled below
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -375,9 +420,10 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
   }
 }
 
-template <int BN, int KC, bool kTwo>
+template <int BN, int KC, bool kTwo, bool kAp = false>
 constexpr size_t stream_lds_bytes() {
-  return (size_t)(KC * BN * kBK + (stream_lookahead(KC, kTwo) + 1) * kChunkElems) * sizeof(bf16_t);
+  return (size_t)(KC * BN * kBK + (stream_lookahead(KC, kTwo) + 1) * kChunkElems) * sizeof(bf16_t) +
+         (kAp ? (size_t)2 * KC * kBK * sizeof(float) : 0);
 }
 
 int g_stream_mode = -1;  // -1: environment (DLA_GEMM_STREAM, default on), 0 off, 1 on (every K <= 256)
@@ -424,6 +470,11 @@ StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b
 template <int BN, int KC>
 void launch_stream_kc(const StreamArgs& a, int grid, bool kmajor, bool stats, bool add, hipStream_t stream) {
   const dim3 g(grid), b(256);
+  if (a.aws) {  // forward over a deferred BN+ReLU output (always with statistics: the consumer's BN)
+    hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, false, true, false, -1, true>), g, b,
+                       (stream_lds_bytes<BN, KC, false, true>()), stream, a);
+    return;
+  }
   const int bm = a.bx != nullptr ? a.bmode : -1;
 #define DLA_SBN(ADD_, M_)                                                                                         \
   hipLaunchKernelGGL((gemm_stream_kernel<BN, KC, true, false, ADD_, M_>), g, b,                                  \
@@ -468,9 +519,11 @@ int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_k
 
 bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, bool b_kmajor, void* C, int64_t ldc,
                         int M, int N, int K, float* stats, hipStream_t stream, const void* addend, int64_t ldd,
-                        const uint8_t* addend_mask, const BnBwdArgs* bn_bwd) {
+                        const uint8_t* addend_mask, const BnBwdArgs* bn_bwd, const float* apply_ws,
+                        void* apply_out) {
   const StreamPlan p = stream_plan(M, N, K, lda, ldc, b_kmajor, addend != nullptr, bn_bwd != nullptr);
   if (!p.mg) return false;
+  if (apply_ws && (b_kmajor || !stats || addend || bn_bwd || !apply_out)) return false;
   if (addend && (stats || !b_kmajor || ldd % 8 != 0 || (int64_t)M * ldd * 2 >= (int64_t)kOOB)) return false;
   if (bn_bwd) {  // partials go where the statistics would: [mg][N][2]
     const int64_t ldbx = bn_bwd->ldx ? bn_bwd->ldx : ldc;
@@ -479,7 +532,8 @@ bool launch_gemm_stream(const void* A, int64_t lda, const void* B, int64_t ldb, 
   StreamArgs a{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, p.mg, p.per_xcd,
                bn_bwd ? bn_bwd->part : stats, (const bf16_t*)addend, ldd, addend_mask,
                bn_bwd ? (const bf16_t*)bn_bwd->x : nullptr, bn_bwd ? (bn_bwd->ldx ? bn_bwd->ldx : ldc) : 0,
-               bn_bwd ? bn_bwd->ws : nullptr, bn_bwd ? bn_bwd->mask : nullptr, bn_bwd ? bn_bwd->mode : 0};
+               bn_bwd ? bn_bwd->ws : nullptr, bn_bwd ? bn_bwd->mask : nullptr, bn_bwd ? bn_bwd->mode : 0,
+               apply_ws, (bf16_t*)apply_out};
   const int kc = K / kBK;
   if (p.bn == 128) {
     if (kc == 1) launch_stream_kc<128, 1>(a, p.grid, b_kmajor, stats != nullptr, addend != nullptr, stream);

@@ -179,17 +179,25 @@ std::vector<at::Tensor> bn_dual_fwd(at::Tensor x, at::Tensor xd, c10::optional<a
 
 // The apply pass a deferred bn_act_fwd / bn_dual_fwd skipped: y = act(BN(x) + r) (r a BN input too when wsd is
 // given), mask = its ReLU bits. For a deferred output whose consumer is not a gemm_nt_apply.
-void bn_apply_deferred(at::Tensor x, at::Tensor r, at::Tensor ws, c10::optional<at::Tensor> wsd, at::Tensor y,
-                       at::Tensor mask) {
+void bn_apply_deferred(at::Tensor x, c10::optional<at::Tensor> r_, at::Tensor ws, c10::optional<at::Tensor> wsd,
+                       at::Tensor y, c10::optional<at::Tensor> mask_) {
   check_act(x, "x");
-  check_act(r, "r");
   check_act(y, "y");
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && r.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 &&
-                  r.sizes() == x.sizes() && y.sizes() == x.sizes(),
-              "bn_apply_deferred: x, r, y must be bf16 tensors of one shape");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 && y.sizes() == x.sizes(),
+              "bn_apply_deferred: x, y must be bf16 tensors of one shape");
   const int C = (int)x.size(1);
   const int64_t M = rows_of(x);
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() == 7 * (int64_t)C, "ws: 7C fp32");
+  if (!(r_.has_value() && r_->defined())) {  // relu(BN(x)), no residual (its backward recomputes the ReLU from x)
+    launch_bn_fwd(x.data_ptr(), nullptr, y.data_ptr(), M, C, kBF16, nullptr, nullptr, 0.f, 0.f, nullptr, nullptr,
+                  ws.data_ptr<float>(), nullptr, true, false, current_stream(x), nullptr, 0, nullptr, 0);
+    return;
+  }
+  at::Tensor r = *r_;
+  check_act(r, "r");
+  TORCH_CHECK(r.scalar_type() == at::kBFloat16 && r.sizes() == x.sizes(), "bn_apply_deferred: r like x");
+  TORCH_CHECK(mask_.has_value() && mask_->defined(), "bn_apply_deferred: a residual needs the ReLU mask");
+  at::Tensor mask = *mask_;
   TORCH_CHECK(mask.scalar_type() == at::kByte && mask.numel() * 8 >= M * C, "mask: one bit per element");
   const bool dual = wsd.has_value() && wsd->defined();
   if (dual) {
@@ -667,6 +675,33 @@ std::vector<at::Tensor> gemm_nt_apply(at::Tensor y, at::Tensor r, at::Tensor ws,
 }
 
 bool gemm_nt_apply_ok(int64_t M, int64_t N, int64_t K) { return gemm_apply_ok(M, (int)N, (int)K); }
+
+// 1x1-conv forward with statistics over a deferred BN+ReLU output on the streaming GEMM (gemm_stream.hip kAp):
+// y the BN input [M, K] (contiguous), ws its 7K workspace; writes out = relu(BN(y)) and returns (C, statistics
+// [gemm_stream_rows][N][2]). Only shapes the streaming kernel plans (gemm_stream_rows(M, N, K, K, N, false) > 0).
+std::vector<at::Tensor> gemm_nt_stream_apply(at::Tensor y, at::Tensor ws, at::Tensor B, at::Tensor out) {
+  check_mat(y, "y");
+  check_mat(B, "B");
+  check_mat(out, "out");
+  const int64_t M = y.size(0);
+  const int K = (int)y.size(1), N = (int)B.size(0);
+  TORCH_CHECK(y.is_contiguous() && out.is_contiguous() && out.sizes() == y.sizes() && B.size(1) == K,
+              "gemm_nt_stream_apply: y, out contiguous [M, K], B [N, K]");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() == 7 * (int64_t)K, "ws: 7K fp32");
+  const int rows = gemm_stream_rows(M, N, K, K, N, false, false, false);
+  TORCH_CHECK(rows > 0, "gemm_nt_stream_apply: shape not served by the streaming kernel");
+  at::Tensor C = at::empty({M, N}, y.options());
+  at::Tensor S = at::empty({rows, N, 2}, y.options().dtype(at::kFloat));
+  TORCH_CHECK(launch_gemm_stream(y.data_ptr(), K, B.data_ptr(), B.stride(0), false, C.data_ptr(), N, (int)M, N, K,
+                                 S.data_ptr<float>(), current_stream(y), nullptr, 0, nullptr, nullptr,
+                                 ws.data_ptr<float>(), out.data_ptr()),
+              "gemm_nt_stream_apply: the streaming kernel refused a shape it planned");
+  return {C, S};
+}
+
+bool gemm_nt_stream_apply_ok(int64_t M, int64_t N, int64_t K) {
+  return M > 0 && K % 8 == 0 && gemm_stream_rows(M, (int)N, (int)K, K, N, false, false, false) > 0;
+}
 
 // gemm_nt whose output is the dy of a fused BN: also returns that BN's backward-reduction partials.
 std::vector<at::Tensor> gemm_nt_bn(at::Tensor A, at::Tensor B, c10::optional<at::Tensor> addend, bool b_kmajor,
@@ -1245,6 +1280,10 @@ void bind_nn(pybind11::module& m) {
         pybind11::arg("stats"), pybind11::arg("out"), pybind11::arg("mask"), pybind11::arg("xs") = pybind11::none(),
         pybind11::arg("H") = 0, pybind11::arg("W") = 0);
   m.def("gemm_nt_apply_ok", &gemm_nt_apply_ok, "shapes gemm_nt_apply serves (M rows, N outputs, K channels)");
+  m.def("gemm_nt_stream_apply", &gemm_nt_stream_apply,
+        "streaming 1x1-conv forward over a deferred BN+ReLU output: writes relu(BN(y)) and returns (C, stats)",
+        pybind11::arg("y"), pybind11::arg("ws"), pybind11::arg("B"), pybind11::arg("out"));
+  m.def("gemm_nt_stream_apply_ok", &gemm_nt_stream_apply_ok, "shapes gemm_nt_stream_apply serves (M, N, K)");
   m.def("set_wgrad_w4", &set_wgrad_w4, "128x256 tiles for the Cout-128 3x3 weight gradients (-1 env, 0, 1)");
   m.def("set_gemm_apply_max_k", &set_gemm_apply_max_k, "largest K gemm_nt_apply serves (<= 0: environment / 512)");
   m.def("bn_dual_bwd", &bn_dual_bwd, "backward of bn_dual_fwd (one dy read for both BatchNorms)", pybind11::arg("dy"),

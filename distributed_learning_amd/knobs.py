@@ -42,6 +42,8 @@ TABLE: Dict[str, Knob] = {
     "APPLY_MAX_K": Knob("512", "csrc/kernels/gemm_apply.hip", "largest conv1 input width whose deferred block-final "
                                                                "apply the conv1 GEMM writes (<= 2048)"),
     "WGRAD_W4": Knob("0", "csrc/kernels/conv.hip", "1: 128x256 four-wave tiles for the Cout-128 3x3 weight gradients"),
+    "DEFER_MID": Knob("0", "models/resnet.py", "1: a bottleneck's bn2+ReLU output is written by conv3's streaming GEMM "
+                                              "(gemm_stream.hip kAp) at the short-K stages instead of its own apply pass; measured slower, profiles/r6/g22/"),
     "APPLY_SUBSAMPLE": Knob("1", "ops/conv.py", "1: at a stage transition the fused conv1 apply also writes the stride-2 "
                                                 "subsample of the block output (no subsample2 pass)"),
     "AUTOTUNE_BUDGET_S": Knob("90", "parallel/autotune.py", "wall-clock budget of the all-reduce selection at N > 1"),

@@ -21,6 +21,7 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
+from .. import knobs
 from ..ops import nn as dnn
 from ..ops.bn_act import deferral_scope, ensure
 from ..ops.pool import MaxPool2d, global_avg_pool
@@ -79,11 +80,12 @@ class Bottleneck(nn.Module):
         else:
             out, xa = dnn.conv_bn_act_fork(x, self.conv1, self.bn1, relu=True)
             xs = None
-        out = dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True)
         # a block whose output goes straight into the next bottleneck (ResNet.forward) leaves the final apply
-        # pass to that block's conv1 GEMM (ops/bn_act.py PendingApply); nothing else may observe it
-        defer = self.defer_output and not (self._forward_hooks or self._forward_pre_hooks
-                                           or nn.modules.module._global_forward_hooks)
+        # pass to that block's conv1 GEMM (ops/bn_act.py PendingApply); nothing else may observe it. The same for
+        # bn2, whose only consumer is conv3 (the streaming GEMM applies it at stages 1-2)
+        observed = bool(self._forward_hooks or self._forward_pre_hooks or nn.modules.module._global_forward_hooks)
+        defer = self.defer_output and not observed
+        out = dnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, defer=not observed and knobs.flag("DEFER_MID"))
         if self.downsample is None:
             return dnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=xa, defer=defer)
         # the shortcut BN is applied inside the block's final apply pass (never materialised)

@@ -302,8 +302,9 @@ def supported(x: torch.Tensor, bn: nn.BatchNorm2d, residual) -> bool:
 def fused_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residual: torch.Tensor | None = None,
                  stats: torch.Tensor | None = None, defer: bool = False):
     """``stats``: optional [row_blocks, C, 2] (sum, sumsq) partials of ``x`` produced by the conv GEMM
-    epilogue (training mode only) — the statistics pass over ``x`` is then skipped. ``defer``: with a residual
-    and ReLU, the output may be left for its consumer to write (PendingApply; inside a deferral_scope)."""
+    epilogue (training mode only) — the statistics pass over ``x`` is then skipped. ``defer``: with ReLU (and
+    optionally a residual), the output may be left for its consumer to write (PendingApply; inside a
+    deferral_scope)."""
     if not supported(x, bn, residual):
         y = bn(x)
         if residual is not None:
@@ -324,7 +325,7 @@ def fused_bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, relu: bool = True, residua
     if rlink is not None and residual.dtype != torch.bfloat16:  # the epilogue addend is bf16
         rlink = None
     dlink = getattr(x, "_dla_dual", None) if training else None
-    defer = (defer and training and residual is not None and residual.dtype == x.dtype
+    defer = (defer and training and (residual is None or residual.dtype == x.dtype)
              and _can_defer(x, relu, residual, bn.weight))
     y = _apply_deferred(_BNAct, x, bn.weight, bn.bias, residual, rm, rv, training, float(bn.momentum or 0.0),
                         float(bn.eps), relu, stats if training else None, rlink, dlink, defer)

@@ -294,7 +294,7 @@ class DualBNLink:
 
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride: int, want_stats: bool):
+    def forward(ctx, x, weight, stride: int, want_stats: bool, pending=None):
         C = _ext.require()
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         ctx.wstride = weight.stride()
@@ -304,7 +304,14 @@ class _Conv1x1(torch.autograd.Function):
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         w2 = weight.reshape(cout, cin).to(torch.bfloat16).contiguous()
-        y2, stats = C.gemm_nt(_rows(x), w2, want_stats)
+        if pending is not None:
+            # x is a deferred BN+ReLU output: the streaming GEMM applies it to its operand chunks in LDS, writes x
+            # and multiplies (gemm_stream.hip kAp)
+            y2, stats = C.gemm_nt_stream_apply(_rows(pending.x), pending.ws, w2, _rows(x))
+            pending.clear()
+            CALLS["1x1_stream_apply"] += 1
+        else:
+            y2, stats = C.gemm_nt(_rows(x), w2, want_stats)
         y = y2.view(n, h, w, cout).permute(0, 3, 1, 2)
         ctx.save_for_backward(x, w2)
         ctx.dlink = DualBNLink() if (DUAL_1X1 and DUAL_BN and stride == 1 and x.dtype == torch.bfloat16
@@ -336,11 +343,11 @@ class _Conv1x1(torch.autograd.Function):
                     CALLS["1x1_dual_bn"] += 1
                     n, cin, h, w = x.shape
                     dx = out[0].view(n, h, w, cin).permute(0, 3, 1, 2)
-                    return dx, _as_param_layout(out[1].to(ctx.wdtype), ctx.wshape, ctx.wstride), None, None
+                    return dx, _as_param_layout(out[1].to(ctx.wdtype), ctx.wshape, ctx.wstride), None, None, None
             # materialise the BN's input gradient (its reduction is re-run: ws is recomputed identically)
             dy = dl.materialise(C, dy, parked)
         if dy is None:
-            return None, None, None, None
+            return None, None, None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
         if dy.dtype != torch.bfloat16:
             dy = dy.to(torch.bfloat16)
@@ -363,7 +370,7 @@ class _Conv1x1(torch.autograd.Function):
                 CALLS["1x1_dual"] += 1
                 n, cin, h, w = x.shape
                 dx = out[0].view(n, h, w, cin).permute(0, 3, 1, 2)
-                return dx, _as_param_layout(out[1].to(ctx.wdtype), ctx.wshape, ctx.wstride), None, None
+                return dx, _as_param_layout(out[1].to(ctx.wdtype), ctx.wshape, ctx.wstride), None, None, None
         if ctx.needs_input_grad[1] and not defer:
             wg = _SideWork(wgrad, dy2.shape[0], dy.device)
         if ctx.needs_input_grad[0]:
@@ -388,7 +395,7 @@ class _Conv1x1(torch.autograd.Function):
             dw = _wgrad_after_dgrad(wgrad, ctx, (dy, x), dy.device)
         if wg is not None:
             dw = wg.result()
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 class _Conv1x1Fork(torch.autograd.Function):
@@ -521,7 +528,7 @@ def conv1x1_fork(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False, sub
     CALLS["1x1_fork"] += 1
     rlink = ResidualLink() if RESIDUAL_HANDOFF and x.requires_grad else None
     pending = pending_of(x)
-    if pending is not None and not (x.is_contiguous(memory_format=torch.channels_last)
+    if pending is not None and not (pending.r is not None and x.is_contiguous(memory_format=torch.channels_last)
                                     and _ext.require().gemm_nt_apply_ok(x.numel() // x.shape[1], conv.out_channels,
                                                                         x.shape[1])):
         pending.materialise()
@@ -540,7 +547,14 @@ def conv1x1(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool = False, stride: 
     if x.shape[2] % s or x.shape[3] % s:
         # odd spatial size with stride 2 (output ceil) — keep F.conv2d semantics exactly
         return F.conv2d(x, conv.weight.to(x.dtype), None, s), None
-    y, stats = _Conv1x1.apply(x, conv.weight, s, want_stats)
+    pending = pending_of(x)
+    if pending is not None and not (pending.r is None and s == 1 and want_stats
+                                    and x.is_contiguous(memory_format=torch.channels_last)
+                                    and _ext.require().gemm_nt_stream_apply_ok(x.numel() // x.shape[1],
+                                                                              conv.out_channels, x.shape[1])):
+        pending.materialise()
+        pending = None
+    y, stats = _Conv1x1.apply(x, conv.weight, s, want_stats, pending)
     dl = getattr(y.grad_fn, "dlink", None) if y.grad_fn is not None else None
     if dl is not None:
         y._dla_dual = dl

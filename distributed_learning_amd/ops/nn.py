@@ -130,6 +130,8 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
     saved). ``presubsampled``: ``x`` is already the stride-2 subsample a strided 1x1 ``conv`` would
     take (conv_bn_act_fork(..., subsample=True)), so the conv runs with stride 1. ``defer``: the result
     feeds only the next bottleneck's conv_bn_act_fork, which may write it itself (ops/bn_act.py PendingApply)."""
+    from .bn_act import ensure
+
     if _BACKEND == "native" and _NATIVE_CONV and x.is_cuda:
         from . import conv as nconv
         from .bn_act import fused_bn_act, supported as bn_supported
@@ -140,12 +142,14 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
             if stats is not None and not bn_supported(y, bn, residual):
                 stats = None
             return fused_bn_act(y, bn, relu, residual, stats, defer=defer)
+        ensure(x)  # a deferred BN output is written by a 1x1 consumer's GEMM only
         if nconv.supported3x3(x, conv):
             want = bn.training and nconv.CONV3_POLICY["fwd"] == "native"
             y, stats = nconv.conv3x3(x, conv, want_stats=want)
             if stats is not None and not bn_supported(y, bn, residual):
                 stats = None
-            return fused_bn_act(y, bn, relu, residual, stats)
+            return fused_bn_act(y, bn, relu, residual, stats, defer=defer)
+    ensure(x)
     if presubsampled:
         y = F.conv2d(x, conv.weight, conv.bias, 1, conv.padding, conv.dilation, conv.groups)
         return bn_act(y, bn, relu, residual)
@@ -155,9 +159,11 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool
 def _native_conv_stats(x: torch.Tensor, conv: nn.Conv2d, want_stats: bool, presubsampled: bool = False):
     """(y, stats-or-None) from a native 1x1 / 3x3 conv, or None when neither applies."""
     from . import conv as nconv
+    from .bn_act import ensure
 
     if nconv.supported(x, conv):
         return nconv.conv1x1(x, conv, want_stats=want_stats, stride=1 if presubsampled else None)
+    ensure(x)
     if not presubsampled and nconv.supported3x3(x, conv):
         want = want_stats and nconv.CONV3_POLICY["fwd"] == "native"
         return nconv.conv3x3(x, conv, want_stats=want)

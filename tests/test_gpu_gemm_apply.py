@@ -138,7 +138,34 @@ def test_apply_gemm_stage1_bench_shape(cuda):
     assert ((c[tail].float() - ref).norm() / ref.norm()).item() < 5e-3
 
 
-def _resnet_step(cuda, defer: bool, max_k: int = -1):
+@pytest.mark.parametrize("M,K,N", [(20000, 64, 256), (50001, 128, 512), (1280 * 56 * 56, 64, 256)])
+def test_stream_apply_matches_unfused_and_torch(cuda, M, K, N):
+    """The streaming GEMM with a deferred BN+ReLU on its operand (gemm_stream.hip kAp): the written operand, the
+    output and the statistics equal the apply pass + the same streaming kernel bit for bit."""
+    from distributed_learning_amd.ops import _ext
+
+    C = _ext.require()
+    assert C.gemm_nt_stream_apply_ok(M, N, K)
+    y, _, ws, _, w = _case(cuda, M, K, N, False, seed=5)
+    out = torch.full((M, K), float("nan"), device=cuda, dtype=torch.bfloat16)
+    c, st = C.gemm_nt_stream_apply(y, ws, w, out)
+    out_u = torch.empty_like(out)
+    C.bn_apply_deferred(_as4d(y), None, ws, None, _as4d(out_u), None)
+    c_u, st_u = C.gemm_nt(out_u, w, True)  # the same streaming kernel without the transform
+    torch.cuda.synchronize()
+    assert torch.equal(out, out_u)
+    assert torch.equal(c, c_u)
+    assert st.shape == st_u.shape and torch.equal(st, st_u)
+    rows = slice(M - 500, M)  # the last (partial) row tile against fp32
+    ref_out = torch.relu(y[rows].float() * ws[2 * K:3 * K] + ws[3 * K:4 * K])
+    assert ((out[rows].float() - ref_out).abs().max() <= 1e-2 * ref_out.abs().max()).item()
+    ref_c = out[rows].float() @ w.float().t()
+    assert ((c[rows].float() - ref_c).norm() / ref_c.norm()).item() < 5e-3
+    csum = c.float().sum(0)
+    assert torch.allclose(st[:, :, 0].sum(0), csum, rtol=1e-3, atol=1e-2 * csum.abs().max().item())
+
+
+def _resnet_step(cuda, defer: bool, max_k: int = -1, mid: bool = False):
     from distributed_learning_amd import knobs
     from distributed_learning_amd.models.resnet import resnet50
     from distributed_learning_amd.ops import _ext
@@ -152,15 +179,16 @@ def _resnet_step(cuda, defer: bool, max_k: int = -1):
     dnn.bf16_weights(model)
     x = torch.randn(16, 3, 96, 96, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     tgt = torch.randint(0, 100, (16,), device=cuda)
-    old = knobs._CACHE.get("DEFER_APPLY")
+    old = knobs._CACHE.get("DEFER_APPLY"), knobs._CACHE.get("DEFER_MID")
     knobs._CACHE["DEFER_APPLY"] = "1" if defer else "0"
+    knobs._CACHE["DEFER_MID"] = "1" if mid else "0"
     C.set_tile256_min_k_stats(1 << 30)  # the same statistics tiles on both paths (bitwise comparison)
     C.set_gemm_apply_max_k(max_k)
     if max_k > 512:
         C.set_mfma_pipeline(0)  # the unfused K > 512 forwards on the fused kernel's main loop too
     dnn.set_backend("native")
     dnn.set_native_conv(True)
-    before = dict(bn_act.CALLS), nconv.CALLS["1x1_apply"]
+    before = dict(bn_act.CALLS), nconv.CALLS["1x1_apply"], nconv.CALLS["1x1_stream_apply"]
     try:
         out = model(x)
         loss = torch.nn.functional.cross_entropy(out.float(), tgt)
@@ -172,12 +200,14 @@ def _resnet_step(cuda, defer: bool, max_k: int = -1):
         C.set_tile256_min_k_stats(-1)
         C.set_gemm_apply_max_k(-1)
         C.set_mfma_pipeline(-1)
-        if old is None:
-            knobs._CACHE.pop("DEFER_APPLY", None)
-        else:
-            knobs._CACHE["DEFER_APPLY"] = old
+        for k, v in zip(("DEFER_APPLY", "DEFER_MID"), old):
+            if v is None:
+                knobs._CACHE.pop(k, None)
+            else:
+                knobs._CACHE[k] = v
     used = {k: bn_act.CALLS[k] - before[0][k] for k in bn_act.CALLS}
     used["fused"] = nconv.CALLS["1x1_apply"] - before[1]
+    used["stream_fused"] = nconv.CALLS["1x1_stream_apply"] - before[2]
     grads = [p.grad.float().clone() for p in model.parameters()]
     stats = [b.clone() for b in model.buffers()]
     return out.float(), loss.item(), grads, stats, used
@@ -209,6 +239,21 @@ def test_resnet50_step_with_every_chained_output_deferred_matches(cuda):
         assert torch.equal(a, b), i
 
 
+def test_resnet50_step_with_deferred_mid_bn_matches(cuda):
+    """bn2 + ReLU written by conv3's streaming GEMM as well (DLA_DEFER_MID): bitwise the undeferred step."""
+    out_d, loss_d, g_d, s_d, used_d = _resnet_step(cuda, True, mid=True)
+    out_u, loss_u, g_u, s_u, used_u = _resnet_step(cuda, False, mid=False)
+    # 16 bn2 outputs deferred on top of the 15 block outputs; the streaming kernel serves the stage-1 / 2 conv3s
+    assert used_d["deferred"] == 31 and used_d["fused"] == 7 and used_d["stream_fused"] > 0, used_d
+    assert used_d["materialised"] == 31 - 7 - used_d["stream_fused"], used_d
+    assert loss_d == loss_u
+    assert torch.equal(out_d, out_u)
+    for a, b in zip(s_d, s_u):
+        assert torch.equal(a, b)
+    for i, (a, b) in enumerate(zip(g_d, g_u)):
+        assert torch.equal(a, b), i
+
+
 def test_deferred_output_is_materialised_for_other_consumers(cuda):
     """A bottleneck called on its own (outside ResNet.forward's deferral scope) never defers, and a hook on a
     chained block makes it write its output itself."""
@@ -223,8 +268,9 @@ def test_deferred_output_is_materialised_for_other_consumers(cuda):
     from distributed_learning_amd import knobs
 
     seen = []
-    old = knobs._CACHE.get("DEFER_APPLY")
+    old = knobs._CACHE.get("DEFER_APPLY"), knobs._CACHE.get("DEFER_MID")
     knobs._CACHE["DEFER_APPLY"] = "1"
+    knobs._CACHE["DEFER_MID"] = "0"  # count the block outputs only
     dnn.set_backend("native")
     dnn.set_native_conv(True)
     try:
@@ -244,10 +290,11 @@ def test_deferred_output_is_materialised_for_other_consumers(cuda):
     finally:
         dnn.set_backend("torch")
         dnn.set_native_conv(False)
-        if old is None:
-            knobs._CACHE.pop("DEFER_APPLY", None)
-        else:
-            knobs._CACHE["DEFER_APPLY"] = old
+        for k, v in zip(("DEFER_APPLY", "DEFER_MID"), old):
+            if v is None:
+                knobs._CACHE.pop(k, None)
+            else:
+                knobs._CACHE[k] = v
     assert deferred == 14  # the hooked block wrote its own output
     assert alone == 0 and bn_act.pending_of(o) is None
     assert seen and all(v == v and v > 0 for v in seen)
