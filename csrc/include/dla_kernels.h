@@ -400,8 +400,14 @@ void launch_conv3x3s2_dgrad(const void* dy, const void* w, void* dx, int N, int 
 // ---- 7x7 / stride-2 / pad-3 stem conv, Cin = 3 (stem.hip) ------------------------------------------
 // x [N,H,W,3] bf16 -> fold: xs [N,(H+1)/2,(W+1)/2,16] (space-to-depth, 4 zero channels);
 // wpk = packed weight [Cout][256] (k = (th * 4 + tw) * 16 + (ph * 2 + pw) * 3 + c, see stem.hip);
-// y [N,OH,OW,Cout] with optional BN-statistics partials stats[stem_stats_rows(P)][Cout][2].
-int stem_stats_rows(int64_t P);
+// y [N,OH,OW,Cout] with optional BN-statistics partials stats[stem_stats_rows(P, Cout)][Cout][2].
+int stem_stats_rows(int64_t P, int Cout = 64);
+// the stem forward with statistics on the persistent streaming GEMM (gemm_stream.hip kStem): its partial rows
+// (0: not used -- DLA_STEM_STREAM / set_stem_stream off, or the shape is not served)
+int stem_stream_rows(int64_t P, int Cout);
+bool launch_stem_stream(const void* xs, const void* wpk, void* y, int N, int BH, int BW, float* stats,
+                        hipStream_t stream);
+void set_stem_stream(int mode);
 
 void launch_stem_fold(const void* x, void* xs, int N, int H, int W, hipStream_t stream);
 void launch_stem_fwd(const void* xs, const void* wpk, void* y, int N, int H, int W, int Cout, float* stats,

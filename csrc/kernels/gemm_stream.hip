@@ -74,6 +74,12 @@ struct StreamArgs {
   // (row stride lda) from the column panel 0 blocks
   const float* aws;
   bf16_t* aout;
+  // kStem: A is the ResNet stem's implicit im2col over the space-to-depth image xs [n][BH][BW][16] (stem.hip):
+  // row = output pixel (n, oh, ow), 64-deep k-step th = filter row, logical 16-byte chunk (tw, channel half) =
+  // folded pixel (oh - 2 + th, ow - 2 + tw); pieces outside the image read zeros (buffer offset kOOB)
+  int sBH, sBW;
+  FastDiv sfW, sfH;
+  uint32_t a_bytes;  // kStem: bytes of xs
 };
 
 // image row of panel-local weight row p (0..63 within a wave's 64 columns): the MFMA A-operand row
@@ -96,9 +102,11 @@ __host__ __device__ constexpr bool stream_two_blocks(bool add, bool bnb) { retur
 // kAp: the A operand is a deferred BN+ReLU output (ops/bn_act.py PendingApply): each thread transforms the 16-byte
 // pieces its own LDS-DMA brought in (after its vmcnt wait, before the barrier that publishes the chunk), writes
 // them back in place and stores them to aout: the BN's apply pass and the GEMM's re-read of its output disappear.
-template <int BN, int KC, bool kBT, bool kStats, bool kAdd = false, int kBM = -1, bool kAp = false>
+template <int BN, int KC, bool kBT, bool kStats, bool kAdd = false, int kBM = -1, bool kAp = false,
+          bool kStem = false>
 __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) void gemm_stream_kernel(const StreamArgs s) {
   constexpr bool kBnb = kBM >= 0;
+  static_assert(!kStem || (!kBT && !kAdd && !kBnb && !kAp && KC == 4), "stem: the K = 256 forward");
   static_assert(!kAp || (!kBT && !kAdd && !kBnb), "apply-on-load: forwards only");
   static_assert(!(kStats && kBnb), "the partials buffer holds either the statistics or the BN-backward sums");
   constexpr int kSP = stream_lookahead(KC, stream_two_blocks(kAdd, kBnb));
@@ -179,7 +187,12 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
   }
 
   // ---- A ring: chunk q = (tile q / KC, k-chunk q % KC) -> slot q % kSS ------------------------------
-  const __amdgpu_buffer_rsrc_t ra = make_srd(s.a, (uint32_t)((int64_t)M * s.lda * 2));
+  const __amdgpu_buffer_rsrc_t ra = make_srd(s.a, kStem ? s.a_bytes : (uint32_t)((int64_t)M * s.lda * 2));
+  // kStem: per row slot of the tile being issued, the folded-pixel element index at th = 0 and the bit mask of the
+  // filter rows th inside the image (0: the row or its column tw is outside); this thread's (tw, half) is fixed
+  int sbase[kStem ? D : 1];
+  uint32_t smsk[kStem ? D : 1];
+  const int stw = rm_glds_kc(tid) >> 4, shalf = rm_glds_kc(tid) & 8;
   uint32_t vo[D];
   int vr[D];
 #pragma unroll
@@ -193,9 +206,37 @@ __global__ __launch_bounds__(256, stream_two_blocks(kAdd, kBM >= 0) ? 2 : 1) voi
     const int t = q / KC, kc = q % KC;
     const int64_t row0 = (int64_t)(grp + t * s.mg) * kSBM;  // past the end for q >= nchunk: all OOB
     uint32_t o[D];
+    uint32_t soff;
+    if constexpr (kStem) {
+      if (kc == 0) {  // a new tile: its rows' pixels (issue runs in chunk order)
 #pragma unroll
-    for (int i = 0; i < D; ++i) o[i] = row0 + vr[i] < M ? vo[i] : kOOB;
-    const uint32_t soff = row0 < M ? (uint32_t)((row0 * s.lda + kc * kBK) * 2) : 0u;
+        for (int i = 0; i < D; ++i) {
+          const int64_t p = row0 + vr[i];
+          smsk[i] = 0u;
+          sbase[i] = 0;
+          if (p < M) {
+            const uint32_t q2 = fdiv((uint32_t)p, s.sfW);
+            const int ow = (int)p - (int)q2 * s.sBW;
+            const uint32_t nn = fdiv(q2, s.sfH);
+            const int oh = (int)q2 - (int)nn * s.sBH;
+            const int bw = ow - 2 + stw;
+            if ((unsigned)bw < (unsigned)s.sBW) {
+#pragma unroll
+              for (int th = 0; th < 4; ++th) smsk[i] |= ((unsigned)(oh - 2 + th) < (unsigned)s.sBH) ? (1u << th) : 0u;
+              sbase[i] = (((int)nn * s.sBH + oh - 2) * s.sBW + bw) * 16 + shalf;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+        o[i] = ((smsk[i] >> kc) & 1u) ? (uint32_t)(sbase[i] + kc * s.sBW * 16) * 2u : kOOB;
+      soff = 0u;
+    } else {
+#pragma unroll
+      for (int i = 0; i < D; ++i) o[i] = row0 + vr[i] < M ? vo[i] : kOOB;
+      soff = row0 < M ? (uint32_t)((row0 * s.lda + kc * kBK) * 2) : 0u;
+    }
     bglds<D, 256 * 16>(o, ra, (uint32_t)__builtin_amdgcn_readfirstlane(soff),
                        ring0 + (uint32_t)((q % kSS) * kChunkElems * 2));
   };
@@ -445,6 +486,8 @@ struct StreamPlan {
 // win or tie everywhere (fwd K 64 x N 256 -11 %, dgrad K 128 x N 256 -45 %); at K = 256 only the data
 // gradient (k-major weights) wins (-11 % at N 512); the forward K = 256 shapes lose 1-12 % (N >= 512 at
 // M <= 802k: the tile kernel's 2-4 co-resident blocks beat one 4-wave block per CU there).
+StreamPlan stream_geometry(int64_t M, int N, bool add, bool bnb);
+
 StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor, bool add = false,
                        bool bnb = false) {
   StreamPlan p;
@@ -453,6 +496,12 @@ StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b
   if (K != 64 && K != 128 && !(K == 256 && (b_kmajor || g_stream_mode == 1))) return p;
   if (N % 64 != 0 || lda % 8 != 0 || ldc % 8 != 0) return p;
   if (M * lda * 2 >= (int64_t)kOOB || M * ldc * 2 >= (int64_t)kOOB) return p;
+  return stream_geometry(M, N, add, bnb);
+}
+
+// blocks of the persistent grid for M rows x N columns (one block per CU; N / BN panels per row group)
+StreamPlan stream_geometry(int64_t M, int N, bool add, bool bnb) {
+  StreamPlan p;
   p.bn = N % 128 == 0 ? 128 : 64;
   const int nbn = N / p.bn;
   const int mt = (int)((M + kSBM - 1) / kSBM);
@@ -465,6 +514,19 @@ StreamPlan stream_plan(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b
   p.mg = 8 * per_xcd;
   p.grid = p.mg * nbn;
   return p;
+}
+
+// The ResNet stem forward (7x7 / s2 over 3 channels, stem.hip) on this kernel: K = 256 over the space-to-depth
+// image, Cout = 64 (one 64-column panel), BN statistics in registers. DLA_STEM_STREAM / set_stem_stream (default
+// off: the 128x64 implicit-GEMM tile kernel)
+int g_stem_stream = -1;
+bool stem_stream_enabled() {
+  if (g_stem_stream >= 0) return g_stem_stream == 1;
+  static const bool v = [] {
+    const char* e = std::getenv("DLA_STEM_STREAM");
+    return e && e[0] == '1';
+  }();
+  return v;
 }
 
 template <int BN, int KC>
@@ -512,6 +574,41 @@ void launch_stream_kc(const StreamArgs& a, int grid, bool kmajor, bool stats, bo
 }  // namespace
 
 void set_gemm_stream(int mode) { g_stream_mode = mode < 0 ? -1 : (mode ? 1 : 0); }
+void set_stem_stream(int mode) { g_stem_stream = mode < 0 ? -1 : (mode ? 1 : 0); }
+
+int stem_stream_rows(int64_t P, int Cout) {
+  if (!stem_stream_enabled() || Cout != 64 || P <= 0 || P >= (1 << 24)) return 0;
+  return stream_geometry(P, 64, false, false).mg;
+}
+
+bool launch_stem_stream(const void* xs, const void* wpk, void* y, int N, int BH, int BW, float* stats,
+                        hipStream_t stream) {
+  const int64_t P = (int64_t)N * BH * BW;
+  const StreamPlan p = stream_geometry(P, 64, false, false);
+  if (!stats || stem_stream_rows(P, 64) != p.mg || !p.mg) return false;
+  const int64_t xs_bytes = P * 16 * 2;
+  if (xs_bytes >= (int64_t)kOOB || P * 64 * 2 >= (int64_t)kOOB) return false;
+  StreamArgs a{};
+  a.a = (const bf16_t*)xs;
+  a.lda = 256;
+  a.b = (const bf16_t*)wpk;
+  a.ldb = 256;
+  a.c = (bf16_t*)y;
+  a.ldc = 64;
+  a.M = (int)P;
+  a.N = 64;
+  a.mg = p.mg;
+  a.per_xcd = p.per_xcd;
+  a.stats = stats;
+  a.sBH = BH;
+  a.sBW = BW;
+  a.sfW = make_fastdiv((uint32_t)BW);
+  a.sfH = make_fastdiv((uint32_t)BH);
+  a.a_bytes = (uint32_t)xs_bytes;
+  hipLaunchKernelGGL((gemm_stream_kernel<64, 4, false, true, false, -1, false, true>), dim3(p.grid), dim3(256),
+                     (stream_lds_bytes<64, 4, false>()), stream, a);
+  return true;
+}
 
 int gemm_stream_rows(int64_t M, int N, int K, int64_t lda, int64_t ldc, bool b_kmajor, bool add, bool bnb) {
   return stream_plan(M, N, K, lda, ldc, b_kmajor, add, bnb).mg;

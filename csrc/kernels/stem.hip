@@ -468,7 +468,10 @@ static StemGeom make_stem_geom(int N, int H, int W) {
   return g;
 }
 
-int stem_stats_rows(int64_t P) { return (int)((P + 127) / 128); }
+int stem_stats_rows(int64_t P, int Cout) {
+  const int rows = stem_stream_rows(P, Cout);  // the persistent streaming kernel (gemm_stream.hip kStem)
+  return rows > 0 ? rows : (int)((P + 127) / 128);
+}
 
 void launch_stem_fold(const void* x, void* xs, int N, int H, int W, hipStream_t stream) {
   const StemGeom g = make_stem_geom(N, H, W);
@@ -483,6 +486,7 @@ void launch_stem_fwd(const void* xs, const void* wpk, void* y, int N, int H, int
                      hipStream_t stream) {
   const StemGeom g = make_stem_geom(N, H, W);
   const int64_t P = (int64_t)N * g.BH * g.BW;
+  if (stats && stem_stream_rows(P, Cout) > 0 && launch_stem_stream(xs, wpk, y, N, g.BH, g.BW, stats, stream)) return;
   const int tiles = (int)((P + 127) / 128) * ((Cout + 63) / 64);
   const int pipe = mfma_pipeline() >= 0 ? mfma_pipeline() : 2;
 #define DLA_STEM(S_, P_)                                                                                         \

@@ -994,7 +994,7 @@ std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor wpk, bool want_stats) 
   launch_stem_fold(x.data_ptr(), xs.data_ptr(), N, H, W, current_stream(x));
   at::Tensor y = at::empty({N, Cout, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor stats;
-  if (want_stats) stats = at::empty({stem_stats_rows(P), Cout, 2}, x.options().dtype(at::kFloat));
+  if (want_stats) stats = at::empty({stem_stats_rows(P, Cout), Cout, 2}, x.options().dtype(at::kFloat));
   launch_stem_fwd(xs.data_ptr(), wpk.data_ptr(), y.data_ptr(), N, H, W, Cout,
                   want_stats ? stats.data_ptr<float>() : nullptr, current_stream(x));
   return {y, stats, xs};
@@ -1284,6 +1284,7 @@ void bind_nn(pybind11::module& m) {
         "streaming 1x1-conv forward over a deferred BN+ReLU output: writes relu(BN(y)) and returns (C, stats)",
         pybind11::arg("y"), pybind11::arg("ws"), pybind11::arg("B"), pybind11::arg("out"));
   m.def("gemm_nt_stream_apply_ok", &gemm_nt_stream_apply_ok, "shapes gemm_nt_stream_apply serves (M, N, K)");
+  m.def("set_stem_stream", &set_stem_stream, "stem forward on the persistent streaming GEMM (-1 env, 0, 1)");
   m.def("set_wgrad_w4", &set_wgrad_w4, "128x256 tiles for the Cout-128 3x3 weight gradients (-1 env, 0, 1)");
   m.def("set_gemm_apply_max_k", &set_gemm_apply_max_k, "largest K gemm_nt_apply serves (<= 0: environment / 512)");
   m.def("bn_dual_bwd", &bn_dual_bwd, "backward of bn_dual_fwd (one dy read for both BatchNorms)", pybind11::arg("dy"),
