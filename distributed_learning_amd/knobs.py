@@ -50,7 +50,8 @@ TABLE: Dict[str, Knob] = {
     "COMM_TIMEOUT_S": Knob("600", "csrc/comm/engine.cpp", "seconds before a collective / IPC barrier is declared dead"),
     # ---- scheduling of the backward ----------------------------------------------------------------
     "WGRAD_DEFER": Knob("3x3", "ops/conv.py", "3x3 | auto | all | 0: weight gradients on the side stream "
-                                              "(profiles/r3/g18_g19_wgrad_defer.md, g47_defer_batch_ab.md)"),
+                                              "(profiles/r3/g18_g19_wgrad_defer.md, g47_defer_batch_ab.md; 'all' "
+                                              "stalls for seconds at bs1280, profiles/r6/g27/)"),
     "WGRAD_JOIN": Knob("end", "ops/conv.py", "end | conv: where the compute stream joins the side stream"),
     "WGRAD_DEFER_MIN_AI": Knob("200", "ops/conv.py", "WGRAD_DEFER=auto: 1x1 arithmetic-intensity threshold"),
     "BN_EPILOGUE": Knob("0", "ops/conv.py", "1 / stream: BN-backward partials in every / the streaming dgrad "
