@@ -20,7 +20,7 @@ iters = int(sys.argv[6]) if len(sys.argv) > 6 else 50
 if len(sys.argv) > 7:
     C.set_mfma_pipeline(int(sys.argv[7]))
 tile = int(sys.argv[8]) if len(sys.argv) > 8 else 0
-N = 256
+N = int(os.environ.get("CONV_ONE_N", "256"))  # batch (the bench runs 1280)
 if op == "gemm":
     M, Cin, Cout = a, b, c
     X = torch.randn(M, Cin, device=dev).to(torch.bfloat16)
