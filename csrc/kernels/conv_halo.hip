@@ -54,7 +54,8 @@ __global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __r
                                                                bf16_t* __restrict__ y, int H, int W, int P,
                                                                int nstrips, int per_block,
                                                                float* __restrict__ stats,
-                                                               const bf16_t* __restrict__ addend) {
+                                                               const bf16_t* __restrict__ addend, FastDiv fW,
+                                                               FastDiv fH, int fast) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   using AC = Acc<kHBM, kHC, kHNT>;
   static_assert(AC::TM == 4 && AC::TN == 2 && AC::WM == 64 && AC::WN == 32, "2x2 waves of 64 x 32");
@@ -116,7 +117,19 @@ __global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __r
     for (int i = 0; i < AC::TM; ++i) {
       const int64_t p = row0 + wr * AC::WM + i * 16 + (lane & 15);
       const int pp = (int)(p < P ? p : 0);
-      const int q = pp / W, ow = pp - q * W, oh = q % H;
+      // (oh, ow) of the pixel: multiply-shift divisions (exact below 2^24 pixels, checked on the host) instead of
+      // two 32-bit integer divisions per fragment before the strip's first MFMA (one wave per SIMD: on the
+      // critical path; profiles/r6/g29 counters)
+      int q, ow, oh;
+      if (fast) {
+        q = (int)fdiv((uint32_t)pp, fW);
+        ow = pp - q * W;
+        oh = q - (int)fdiv((uint32_t)q, fH) * H;
+      } else {
+        q = pp / W;
+        ow = pp - q * W;
+        oh = q % H;
+      }
       uint32_t m = 0;
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh)
@@ -186,7 +199,8 @@ __global__ __launch_bounds__(kHNT, 2) void conv3x3_halo_rb_kernel(const bf16_t* 
                                                                   bf16_t* __restrict__ y, int H, int W, int P,
                                                                   int nstrips, int per_block,
                                                                   float* __restrict__ stats,
-                                                                  const bf16_t* __restrict__ addend) {
+                                                                  const bf16_t* __restrict__ addend, FastDiv fW,
+                                                                  FastDiv fH, int fast) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   constexpr int TM = kHBM / 16;  // 8 fragments along M per wave
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -237,7 +251,19 @@ __global__ __launch_bounds__(kHNT, 2) void conv3x3_halo_rb_kernel(const bf16_t* 
     for (int i = 0; i < TM; ++i) {
       const int64_t p = row0 + i * 16 + (lane & 15);
       const int pp = (int)(p < P ? p : 0);
-      const int q = pp / W, ow = pp - q * W, oh = q % H;
+      // (oh, ow) of the pixel: multiply-shift divisions (exact below 2^24 pixels, checked on the host) instead of
+      // two 32-bit integer divisions per fragment before the strip's first MFMA (one wave per SIMD: on the
+      // critical path; profiles/r6/g29 counters)
+      int q, ow, oh;
+      if (fast) {
+        q = (int)fdiv((uint32_t)pp, fW);
+        ow = pp - q * W;
+        oh = q - (int)fdiv((uint32_t)q, fH) * H;
+      } else {
+        q = pp / W;
+        ow = pp - q * W;
+        oh = q % H;
+      }
       uint32_t m = 0;
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh)
@@ -368,20 +394,27 @@ void launch_conv3x3_halo(const void* x, const void* w, void* y, int N, int H, in
   const bf16_t* wp = (const bf16_t*)w;
   const bf16_t* ap = (const bf16_t*)addend;
   bf16_t* yp = (bf16_t*)y;
+  // DLA_HALO_FASTDIV=0: the integer-division form of the per-strip tap masks (A/B)
+  static const int fast = [] {
+    const char* e = std::getenv("DLA_HALO_FASTDIV");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  const FastDiv fW = make_fastdiv((uint32_t)W), fH = make_fastdiv((uint32_t)H);
+  const int use_fast = (P < (1 << 24) && W < (1 << 16) && H < (1 << 16)) ? fast : 0;  // fdiv's exact range
   if (ver == 1) {
     if (stats)
       hipLaunchKernelGGL(conv3x3_halo_kernel<true>, dim3(grid), dim3(kHNT), kHLds, stream, xp, wp, yp, H, W, P,
-                         nstrips, per_block, stats, ap);
+                         nstrips, per_block, stats, ap, fW, fH, use_fast);
     else
       hipLaunchKernelGGL(conv3x3_halo_kernel<false>, dim3(grid), dim3(kHNT), kHLds, stream, xp, wp, yp, H, W, P,
-                         nstrips, per_block, stats, ap);
+                         nstrips, per_block, stats, ap, fW, fH, use_fast);
   } else {
     if (stats)
       hipLaunchKernelGGL(conv3x3_halo_rb_kernel<true>, dim3(grid), dim3(kHNT), kH2Lds, stream, xp, wp, yp, H, W,
-                         P, nstrips, per_block, stats, ap);
+                         P, nstrips, per_block, stats, ap, fW, fH, use_fast);
     else
       hipLaunchKernelGGL(conv3x3_halo_rb_kernel<false>, dim3(grid), dim3(kHNT), kH2Lds, stream, xp, wp, yp, H, W,
-                         P, nstrips, per_block, stats, ap);
+                         P, nstrips, per_block, stats, ap, fW, fH, use_fast);
   }
 }
 

@@ -81,6 +81,8 @@ TABLE: Dict[str, Knob] = {
     "CONV_PIPE": Knob("-1", "csrc/kernels/conv.hip", "3x3 conv main-loop pipeline for K >= 256 (-1: per shape)"),
     "HALO": Knob("2", "csrc/kernels/conv_halo.hip", "0 off, 1 dgrad only, 2 fwd + dgrad halo-tiled 64-ch 3x3 (r5l/)"),
     "HALO_V": Knob("1", "csrc/kernels/conv_halo.hip", "halo kernel version (1 / 2)"),
+    "HALO_FASTDIV": Knob("1", "csrc/kernels/conv_halo.hip", "0: integer divisions for the halo conv's per-strip tap masks "
+                                                            "(A/B of the multiply-shift form, profiles/r6/g30/)"),
     "HALO_WGRAD": Knob("1", "csrc/kernels/conv_halo_wgrad.hip", "0: implicit-GEMM 64-ch 3x3 weight gradient"),
     "POOL3_SEP": Knob("4", "csrc/kernels/pool.hip", "separable 3x3 stride-1 max-pool variant (4 / 7; other: off; r3w/)"),
     "BN_RED_BLOCKS": Knob("1024", "csrc/kernels/bn_act.hip", "BN reduction-pass block target"),
