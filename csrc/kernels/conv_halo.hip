@@ -381,12 +381,17 @@ void launch_conv3x3_halo(const void* x, const void* w, void* y, int N, int H, in
     hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     return n > 0 ? n : 256;
   }();
-  // DLA_HALO_V: 1 (default) the one-block-per-CU variant with LDS-resident weights, 2 the two-blocks-
-  // per-CU variant with VGPR-resident weights (forward -4 %, dgrad +5 % vs variant 1: profiles/r5j)
-  static const int ver = [] {
+  // DLA_HALO_V: 1 the one-block-per-CU variant with LDS-resident weights, 2 the two-blocks-per-CU variant with
+  // VGPR-resident weights (forward -4 %, dgrad +5 % vs variant 1: profiles/r5j), 3 (default) 2 for the forward, 1 for
+  // the data gradient
+  // DLA_HALO_V=3: variant 2 for the forward (it carries the statistics epilogue), variant 1 for the data gradient
+  // -- the per-direction winners of profiles/r5j (forward 0.228-0.231 vs 0.238-0.246 ms, data gradient 0.209-0.221
+  // vs 0.221-0.233 ms at bs512)
+  static const int ver_env = [] {
     const char* e = std::getenv("DLA_HALO_V");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 3;  // default 3 since profiles/r6/g32 (step 80.17 vs 80.33 ms median, interleaved x3)
   }();
+  const int ver = ver_env == 3 ? (stats ? 2 : 1) : ver_env;
   const int slots = ver == 1 ? cus : 2 * cus;
   const int per_block = (nstrips + slots - 1) / slots;
   const int grid = (nstrips + per_block - 1) / per_block;

@@ -80,7 +80,8 @@ TABLE: Dict[str, Knob] = {
     "GEMM_STREAM": Knob("1", "csrc/kernels/gemm_stream.hip", "0: no persistent streaming 1x1 GEMM (profiles/r3/)"),
     "CONV_PIPE": Knob("-1", "csrc/kernels/conv.hip", "3x3 conv main-loop pipeline for K >= 256 (-1: per shape)"),
     "HALO": Knob("2", "csrc/kernels/conv_halo.hip", "0 off, 1 dgrad only, 2 fwd + dgrad halo-tiled 64-ch 3x3 (r5l/)"),
-    "HALO_V": Knob("1", "csrc/kernels/conv_halo.hip", "halo kernel version (1 / 2)"),
+    "HALO_V": Knob("3", "csrc/kernels/conv_halo.hip", "halo kernel version (1 / 2 / 3 = 2 forward + 1 data "
+                                                    "gradient, profiles/r6/g32/)"),
     "HALO_FASTDIV": Knob("1", "csrc/kernels/conv_halo.hip", "0: integer divisions for the halo conv's per-strip tap masks "
                                                             "(A/B of the multiply-shift form, profiles/r6/g30/)"),
     "HALO_WGRAD": Knob("1", "csrc/kernels/conv_halo_wgrad.hip", "0: implicit-GEMM 64-ch 3x3 weight gradient"),

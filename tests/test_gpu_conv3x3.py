@@ -194,7 +194,7 @@ print("halo ok")
 """
 
 
-@pytest.mark.parametrize("version", ["1", "2"])
+@pytest.mark.parametrize("version", ["1", "2", "3"])  # 3: variant 2 forward, variant 1 data gradient
 def test_conv3x3_halo_c64(cuda, version):
     """64 -> 64 channel stride-1 3x3 convs on the halo-tiled persistent kernel, forward and data
     gradient, both kernel variants (a fresh process with DLA_HALO=2, read once): forward bitwise equal to the
