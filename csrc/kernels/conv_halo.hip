@@ -48,7 +48,11 @@ __device__ __forceinline__ int hswz(int s) { return s & 7; }  // chunk XOR of pa
 
 }  // namespace
 
-template <bool kStats>
+// kDirect (no statistics): the product is computed transposed (weights as the MFMA A operand, dla_mfma.h mfma_t)
+// so a lane holds 4 consecutive output channels of one pixel per fragment; one v_permlane16_swap per register pair
+// makes them 8 channels (16 bytes), stored straight from the registers -- no LDS staging, no epilogue barrier
+// (gemm_direct.hip's mapping). With one wave per SIMD nothing hides the staged epilogue (profiles/r6/g29).
+template <bool kStats, bool kDirect = false>
 __global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __restrict__ x,
                                                                const bf16_t* __restrict__ w,
                                                                bf16_t* __restrict__ y, int H, int W, int P,
@@ -173,13 +177,60 @@ __global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __r
 #pragma unroll
       for (int i = 0; i < AC::TM; ++i)
 #pragma unroll
-        for (int j = 0; j < AC::TN; ++j) acc.v[i][j] = mfma(af[cb][i], bfr[cb][j], acc.v[i][j]);
+        for (int j = 0; j < AC::TN; ++j) acc.v[i][j] = mfma_t<kDirect>(af[cb][i], bfr[cb][j], acc.v[i][j]);
       __builtin_amdgcn_s_setprio(0);
     }
-    ColStats<kHBM, kHC, kHNT> st;
-    st.zero();
-    epilogue_bf16<kHBM, kHC, kStats, false, kHNT>(acc, y, kHC, P, kHC, row0, 0, st, addend, kHC, stage);
-    if constexpr (kStats) stats_flush<kHBM, kHC, kHNT>(st, stats + (int64_t)s * kHC * 2, kHC, 0, stage);
+    if constexpr (kDirect) {
+      static_assert(!kStats && AC::TM == 4 && AC::TN == 2, "direct stores: 64 x 32 wave tiles, no statistics");
+      // acc.v[i][j][r]: pixel 16 i + p of the wave's 64 rows, channel 16 j + 4 g + r of its 32 columns; after the
+      // swap the lane holds channels n .. n + 7 of each of its 4 pixels
+      const int g = lane >> 4, p = lane & 15;
+      const int64_t pix0 = row0 + wr * AC::WM + p;
+      const int n = wc * AC::WN + 16 * (g & 1) + 8 * (g >> 1);
+      typedef float f32x2_t __attribute__((ext_vector_type(2)));
+      typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+      typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+      auto pack = [](float a, float b) {
+        return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{a, b}), bf16x2_t));
+      };
+      u32x4_t dv[AC::TM];
+      if (addend) {  // C = bf16(bf16(acc) + D), the staged epilogue's unfused add; all loads before the packing
+#pragma unroll
+        for (int i = 0; i < AC::TM; ++i) {
+          const int64_t m = pix0 + 16 * i;
+          dv[i] = m < P ? *reinterpret_cast<const u32x4_t*>(addend + m * kHC + n) : u32x4_t{0u, 0u, 0u, 0u};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < AC::TM; ++i) {
+        uint32_t u0[2], u1[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          u0[h] = pack(acc.v[i][0][2 * h], acc.v[i][0][2 * h + 1]);
+          u1[h] = pack(acc.v[i][1][2 * h], acc.v[i][1][2 * h + 1]);
+          const auto r = __builtin_amdgcn_permlane16_swap(u0[h], u1[h], false, false);
+          u0[h] = r[0];
+          u1[h] = r[1];
+        }
+        u32x4_t v{u0[0], u0[1], u1[0], u1[1]};
+        if (addend) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float lo = __builtin_bit_cast(float, v[e] << 16) + __builtin_bit_cast(float, dv[i][e] << 16);
+            const float hi = __builtin_bit_cast(float, v[e] & 0xffff0000u) +
+                             __builtin_bit_cast(float, dv[i][e] & 0xffff0000u);
+            v[e] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+          }
+        }
+        const int64_t m = pix0 + 16 * i;
+        if (m < P) *reinterpret_cast<u32x4_t*>(y + m * kHC + n) = v;
+      }
+    } else {
+      ColStats<kHBM, kHC, kHNT> st;
+      st.zero();
+      epilogue_bf16<kHBM, kHC, kStats, false, kHNT>(acc, y, kHC, P, kHC, row0, 0, st, addend, kHC, stage);
+      if constexpr (kStats) stats_flush<kHBM, kHC, kHNT>(st, stats + (int64_t)s * kHC * 2, kHC, 0, stage);
+    }
   }
 }
 
@@ -406,10 +457,19 @@ void launch_conv3x3_halo(const void* x, const void* w, void* y, int N, int H, in
   }();
   const FastDiv fW = make_fastdiv((uint32_t)W), fH = make_fastdiv((uint32_t)H);
   const int use_fast = (P < (1 << 24) && W < (1 << 16) && H < (1 << 16)) ? fast : 0;  // fdiv's exact range
+  // the variant-1 data gradient stores from registers (kDirect; default since profiles/r6/g34: -0.14 ms/step,
+  // interleaved x3); DLA_HALO_DIRECT=0 restores the LDS-staged epilogue
+  static const bool direct = [] {
+    const char* e = std::getenv("DLA_HALO_DIRECT");
+    return !(e && e[0] == '0');
+  }();
   if (ver == 1) {
     if (stats)
       hipLaunchKernelGGL(conv3x3_halo_kernel<true>, dim3(grid), dim3(kHNT), kHLds, stream, xp, wp, yp, H, W, P,
                          nstrips, per_block, stats, ap, fW, fH, use_fast);
+    else if (direct)
+      hipLaunchKernelGGL((conv3x3_halo_kernel<false, true>), dim3(grid), dim3(kHNT), kHLds, stream, xp, wp, yp, H, W,
+                         P, nstrips, per_block, stats, ap, fW, fH, use_fast);
     else
       hipLaunchKernelGGL(conv3x3_halo_kernel<false>, dim3(grid), dim3(kHNT), kHLds, stream, xp, wp, yp, H, W, P,
                          nstrips, per_block, stats, ap, fW, fH, use_fast);
