@@ -244,7 +244,10 @@ __global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __r
 // columns, so the BN statistics need no cross-wave combine.
 constexpr int kH2Lds = kHPatchBytes + kHStageBytes;
 
-template <bool kStats>
+// kDirect: the product computed transposed, so a lane holds 4 consecutive output channels of one pixel per
+// fragment: the tile leaves as 8-byte stores straight from the registers, the statistics are an in-lane sum over
+// the 8 fragments plus a 16-lane DPP row sum (a wave owns its 16 channels), no LDS staging, no epilogue barriers.
+template <bool kStats, bool kDirect = false>
 __global__ __launch_bounds__(kHNT, 2) void conv3x3_halo_rb_kernel(const bf16_t* __restrict__ x,
                                                                   const bf16_t* __restrict__ w,
                                                                   bf16_t* __restrict__ y, int H, int W, int P,
@@ -291,7 +294,8 @@ __global__ __launch_bounds__(kHNT, 2) void conv3x3_halo_rb_kernel(const bf16_t* 
 
   for (int s = s_begin; s < s_end; ++s) {
     if (s == s_begin) vm_wait<0>();
-    else vm_wait<4>();  // the patch DMA is older than the previous strip's 4 tile stores
+    else vm_wait<kDirect ? TM : 4>();  // the patch DMA is older than the previous strip's tile stores (4 staged
+                                       // 16-byte / TM direct 8-byte stores per lane; addend loads are waited by use)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -345,7 +349,7 @@ __global__ __launch_bounds__(kHNT, 2) void conv3x3_halo_rb_kernel(const bf16_t* 
         }
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) acc[i] = mfma(af[i], bw[t][kk], acc[i]);
+        for (int i = 0; i < TM; ++i) acc[i] = mfma_t<kDirect>(af[i], bw[t][kk], acc[i]);
         __builtin_amdgcn_s_setprio(0);
       }
     }
@@ -354,6 +358,67 @@ __global__ __launch_bounds__(kHNT, 2) void conv3x3_halo_rb_kernel(const bf16_t* 
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (s + 1 < s_end) issue_patch(s + 1);
+
+    if constexpr (kDirect) {
+      // acc[i][r]: channel wave * 16 + 4 g + r of pixel row0 + 16 i + p
+      const int g = lane >> 4, p = lane & 15;
+      const int ch = wave * 16 + 4 * g;
+      typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+      typedef float f32x2_t __attribute__((ext_vector_type(2)));
+      typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+      auto pack = [](float a, float b) {
+        return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{a, b}), bf16x2_t));
+      };
+      u32x2_t dv[TM];
+      if (addend) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int64_t m = row0 + 16 * i + p;
+          dv[i] = m < P ? *reinterpret_cast<const u32x2_t*>(addend + m * kHC + ch) : u32x2_t{0u, 0u};
+        }
+      }
+      float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int64_t m = row0 + 16 * i + p;
+        u32x2_t v{pack(acc[i][0], acc[i][1]), pack(acc[i][2], acc[i][3])};
+        if constexpr (kStats) {  // statistics of the stored (bf16-rounded) values; rows past P count 0
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t w2 = v[r >> 1];
+            const float f = m < P ? __builtin_bit_cast(float, (r & 1) ? (w2 & 0xffff0000u) : (w2 << 16)) : 0.f;
+            cs[r] += f;
+            cq[r] = fmaf(f, f, cq[r]);
+          }
+        }
+        if (addend) {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float lo = __builtin_bit_cast(float, v[e] << 16) + __builtin_bit_cast(float, dv[i][e] << 16);
+            const float hi = __builtin_bit_cast(float, v[e] & 0xffff0000u) +
+                             __builtin_bit_cast(float, dv[i][e] & 0xffff0000u);
+            v[e] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+          }
+        }
+        if (m < P) *reinterpret_cast<u32x2_t*>(y + m * kHC + ch) = v;
+      }
+      if constexpr (kStats) {  // sum the 16 pixel lanes of each row: lane p = 0 of row g holds its 4 channels
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int x = 1; x < 16; x <<= 1) {
+            cs[r] += __shfl_xor(cs[r], x, kWave);
+            cq[r] += __shfl_xor(cq[r], x, kWave);
+          }
+        }
+        if (p == 0) {
+          float* dst = stats + ((int64_t)s * kHC + ch) * 2;
+          *reinterpret_cast<float4_t*>(dst) = float4_t{cs[0], cq[0], cs[1], cq[1]};
+          *reinterpret_cast<float4_t*>(dst + 4) = float4_t{cs[2], cq[2], cs[3], cq[3]};
+        }
+      }
+      continue;
+    }
 
     // epilogue: bf16 tile -> LDS (pitch 72) -> 16-byte row stores (+ addend); per-column statistics of
     // the stored values straight from the accumulators (a lane owns one column of each fragment)
@@ -463,6 +528,11 @@ void launch_conv3x3_halo(const void* x, const void* w, void* y, int N, int H, in
     const char* e = std::getenv("DLA_HALO_DIRECT");
     return !(e && e[0] == '0');
   }();
+  // DLA_HALO_DIRECT_FWD=1: the variant-2 forward stores from registers as well (A/B)
+  static const bool direct_fwd = [] {
+    const char* e = std::getenv("DLA_HALO_DIRECT_FWD");
+    return e && e[0] == '1';
+  }();
   if (ver == 1) {
     if (stats)
       hipLaunchKernelGGL(conv3x3_halo_kernel<true>, dim3(grid), dim3(kHNT), kHLds, stream, xp, wp, yp, H, W, P,
@@ -474,7 +544,10 @@ void launch_conv3x3_halo(const void* x, const void* w, void* y, int N, int H, in
       hipLaunchKernelGGL(conv3x3_halo_kernel<false>, dim3(grid), dim3(kHNT), kHLds, stream, xp, wp, yp, H, W, P,
                          nstrips, per_block, stats, ap, fW, fH, use_fast);
   } else {
-    if (stats)
+    if (stats && direct_fwd)
+      hipLaunchKernelGGL((conv3x3_halo_rb_kernel<true, true>), dim3(grid), dim3(kHNT), kH2Lds, stream, xp, wp, yp, H,
+                         W, P, nstrips, per_block, stats, ap, fW, fH, use_fast);
+    else if (stats)
       hipLaunchKernelGGL(conv3x3_halo_rb_kernel<true>, dim3(grid), dim3(kHNT), kH2Lds, stream, xp, wp, yp, H, W,
                          P, nstrips, per_block, stats, ap, fW, fH, use_fast);
     else

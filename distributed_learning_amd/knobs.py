@@ -87,6 +87,8 @@ TABLE: Dict[str, Knob] = {
     "HALO_DIRECT": Knob("1", "csrc/kernels/conv_halo.hip", "1: the variant-1 halo data gradient stores its tile from "
                                                            "registers (transposed product) instead of through LDS "
                                                            "(profiles/r6/g34/)"),
+    "HALO_DIRECT_FWD": Knob("0", "csrc/kernels/conv_halo.hip", "1: the variant-2 halo forward stores its tile and "
+                                                               "statistics from registers"),
     "HALO_WGRAD": Knob("1", "csrc/kernels/conv_halo_wgrad.hip", "0: implicit-GEMM 64-ch 3x3 weight gradient"),
     "POOL3_SEP": Knob("4", "csrc/kernels/pool.hip", "separable 3x3 stride-1 max-pool variant (4 / 7; other: off; r3w/)"),
     "BN_RED_BLOCKS": Knob("1024", "csrc/kernels/bn_act.hip", "BN reduction-pass block target"),

@@ -194,8 +194,9 @@ print("halo ok")
 """
 
 
-# 3: variant 2 forward, variant 1 data gradient; "1d" / "3d": the variant-1 data gradient stored from registers
-@pytest.mark.parametrize("version", ["1", "2", "3", "1d", "3d"])
+# 3: variant 2 forward, variant 1 data gradient; "d": the variant-1 data gradient stored from registers, "f": the
+# variant-2 forward (tile and statistics) from registers
+@pytest.mark.parametrize("version", ["1", "2", "3", "1d", "3d", "2f", "3df"])
 def test_conv3x3_halo_c64(cuda, version):
     """64 -> 64 channel stride-1 3x3 convs on the halo-tiled persistent kernel, forward and data
     gradient, both kernel variants (a fresh process with DLA_HALO=2, read once): forward bitwise equal to the
@@ -205,7 +206,8 @@ def test_conv3x3_halo_c64(cuda, version):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, DLA_HALO="2", DLA_HALO_V=version[0], DLA_HALO_DIRECT="1" if version.endswith("d") else "0")
+    env = dict(os.environ, DLA_HALO="2", DLA_HALO_V=version[0], DLA_HALO_DIRECT="1" if "d" in version else "0",
+               DLA_HALO_DIRECT_FWD="1" if "f" in version else "0")
     r = subprocess.run([sys.executable, "-c", _HALO_SCRIPT % root], env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0 and "halo ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
