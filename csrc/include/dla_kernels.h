@@ -309,6 +309,9 @@ void set_gemm_direct(int mode);
 constexpr int kGemmApplyMaxK = 2048;  // coefficient table: 4 x K fp32 of LDS (dual)
 bool gemm_apply_ok(int64_t M, int N, int K);
 void set_gemm_apply_max_k(int k);
+// 256x256 statistics forwards stored from the registers (dla_mfma.h epilogue_direct): -1 env (DLA_GEMM256_DIRECT), 0, 1
+void set_gemm256_direct(int mode);
+bool gemm256_direct_enabled();
 void set_wgrad_w4(int mode);  // 128x256 tiles for the Cout-128 3x3 weight gradients: -1 env (DLA_WGRAD_W4), 0, 1  // <= 0: DLA_APPLY_MAX_K / default 512
 int gemm_apply_rows(int64_t M);
 // xs (optional): also write out's stride-2 subsample [n][H/2][W/2][K] (rows m = (n H + h) W + w; H, W even)

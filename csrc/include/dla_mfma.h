@@ -1037,6 +1037,107 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
   }
 }
 
+// Register-direct epilogue for a main loop run with the transposed product (run_mainloop<PIPE, true>):
+// acc.v[i][j][r] holds output row wr * WM + 16 i + p and column wc * WN + 16 j + 4 g + r (p = lane & 15,
+// g = lane >> 4). One v_permlane16_swap per register pair of a fragment column pair gives every lane 8
+// consecutive columns (16 bytes) of its rows, stored straight from the registers -- no C staging through LDS, no
+// staging barriers (gemm_direct.hip, conv_halo.hip kDirect). With stats_row: the [N][2] (sum, sumsq) partial row of
+// the tile's stored (bf16-rounded) values, summed in registers over the lane's rows, over the 16 lanes of a DPP
+// row, and over the WGM M-waves through 2 * WGM * BN floats of LDS (the main loop's image bytes, free by then).
+template <int CTRL>
+__device__ __forceinline__ float epi_dpp_add(float v) {
+  const int o = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false);
+  return v + __builtin_bit_cast(float, o);
+}
+__device__ __forceinline__ float epi_row16_sum(float v) {  // pairs {i, 15-i}, {i, 7-i}, xor 2, xor 1
+  v = epi_dpp_add<0x140>(v);
+  v = epi_dpp_add<0x141>(v);
+  v = epi_dpp_add<0x4E>(v);
+  return epi_dpp_add<0xB1>(v);
+}
+
+template <int BM, int BN, bool kStats, int NT = kThreads>
+__device__ __forceinline__ void epilogue_direct(const Acc<BM, BN, NT>& acc, bf16_t* __restrict__ C, int64_t ldc,
+                                                int64_t M, int N, int64_t row0, int col0,
+                                                float* __restrict__ stats_row, char* smem) {
+  using AC = Acc<BM, BN, NT>;
+  constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
+  static_assert(kMS == 16 && TN % 2 == 0, "16x16 fragments in column pairs");
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN;
+  const int g = lane >> 4, p = lane & 15;
+  const int64_t pix0 = row0 + wr * WM + p;  // + 16 i
+  uint32_t u[TM][TN][2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        u[i][j][h] = __builtin_bit_cast(
+            uint32_t, __builtin_convertvector((f32x2_t{acc.v[i][j][2 * h], acc.v[i][j][2 * h + 1]}), bf16x2_t));
+  if constexpr (kStats) {
+    float* red = reinterpret_cast<float*>(smem);  // [WGM][BN][2]
+    __syncthreads();  // every wave's main-loop LDS reads are done before the bytes are reused
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float s4[4], q4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sv = 0.f, qv = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const uint32_t w2 = u[i][j][r >> 1];
+          const float f = pix0 + 16 * i < M ? __builtin_bit_cast(float, (r & 1) ? (w2 & 0xffff0000u) : (w2 << 16))
+                                            : 0.f;
+          sv += f;
+          qv = fmaf(f, f, qv);
+        }
+        s4[r] = epi_row16_sum(sv);
+        q4[r] = epi_row16_sum(qv);
+      }
+      if (p == 0) {
+        float* dst = red + (wr * BN + wc * WN + 16 * j + 4 * g) * 2;
+        *reinterpret_cast<float4_t*>(dst) = float4_t{s4[0], q4[0], s4[1], q4[1]};
+        *reinterpret_cast<float4_t*>(dst + 4) = float4_t{s4[2], q4[2], s4[3], q4[3]};
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < AC::WGM; ++w) {
+        a += red[(w * BN + c) * 2];
+        b += red[(w * BN + c) * 2 + 1];
+      }
+      if (col0 + c < N) *reinterpret_cast<f32x2_t*>(stats_row + (int64_t)(col0 + c) * 2) = f32x2_t{a, b};
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int jp = 0; jp < TN; jp += 2)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const auto r = __builtin_amdgcn_permlane16_swap(u[i][jp][h], u[i][jp + 1][h], false, false);
+        u[i][jp][h] = r[0];
+        u[i][jp + 1][h] = r[1];
+      }
+  const int cb = col0 + wc * WN + 16 * (g & 1) + 8 * (g >> 1);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int64_t m = pix0 + 16 * i;
+#pragma unroll
+    for (int hh = 0; hh < TN / 2; ++hh) {
+      const int n = cb + 32 * hh;
+      const u32x4_t v{u[i][2 * hh][0], u[i][2 * hh][1], u[i][2 * hh + 1][0], u[i][2 * hh + 1][1]};
+      if (m < M && n < N) *reinterpret_cast<u32x4_t*>(C + m * ldc + n) = v;
+    }
+  }
+}
+
 // Writes a block's accumulated column statistics as one partial row: out[N][2] at columns col0..
 // (the 4 lane groups sharing a column combine by xor-shuffles, the 2 M-waves through LDS).
 template <int BM, int BN, int NT = kThreads>

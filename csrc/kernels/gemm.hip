@@ -33,7 +33,9 @@ using namespace mm;
 // C[M,N] = A[M,K] * B[N,K]^T   (A K-contiguous; B K-contiguous, or k-major [K][N] when kBT),
 // bf16 in/out, fp32 accumulate, optional fused addend and BN-statistics epilogue.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, bool kStats, bool kBT, int PIPE, int NT>
+// kD: the product computed transposed and the tile stored from the registers (dla_mfma.h epilogue_direct);
+// forwards without addend / BN-backward features only
+template <int BM, int BN, bool kStats, bool kBT, int PIPE, int NT, bool kD = false>
 __global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void gemm_nt_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               bf16_t* __restrict__ C, int64_t ldc, int M, int N, int K,
@@ -52,13 +54,18 @@ __global__ __launch_bounds__(NT, blocks_per_cu(BM, BN, NT)) void gemm_nt_kernel(
   const RowLoader<BM, NT> la{A, lda, row0, M, K};
   if constexpr (kBT) {
     const KLoader<BN, NT> lb{B, ldb, col0, N, K};
-    run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
+    run_mainloop<PIPE, kD>(la, lb, 0, K, acc, smem_raw);
   } else {
     const RowLoader<BN, NT> lb{B, ldb, (int64_t)col0, N, K};
-    run_mainloop<PIPE>(la, lb, 0, K, acc, smem_raw);
+    run_mainloop<PIPE, kD>(la, lb, 0, K, acc, smem_raw);
   }
-  epilogue_bf16<BM, BN, kStats, !kStats, NT>(acc, C, ldc, M, N, row0, col0, st, D, ldd, smem_raw, &bnb, bm);
-  if constexpr (kStats) stats_flush<BM, BN, NT>(st, stats + (int64_t)bm * N * 2, N, col0, smem_raw);
+  if constexpr (kD) {
+    epilogue_direct<BM, BN, kStats, NT>(acc, C, ldc, M, N, row0, col0, kStats ? stats + (int64_t)bm * N * 2 : nullptr,
+                                        smem_raw);
+  } else {
+    epilogue_bf16<BM, BN, kStats, !kStats, NT>(acc, C, ldc, M, N, row0, col0, st, D, ldd, smem_raw, &bnb, bm);
+    if constexpr (kStats) stats_flush<BM, BN, NT>(st, stats + (int64_t)bm * N * 2, N, col0, smem_raw);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -225,7 +232,7 @@ void set_mfma_pipeline(int p) { g_pipe = (p == 0 || (p >= 2 && p <= 7)) ? p : -1
 int mfma_pipeline() { return g_pipe; }
 int mfma_pipeline_for(int K) { return g_pipe >= 0 ? g_pipe : (K >= 256 ? 2 : 0); }
 
-template <int BM, int BN, bool S, bool BT, int PIPE, int NT>
+template <int BM, int BN, bool S, bool BT, int PIPE, int NT, bool kD = false>
 static void launch_nt_p(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
                         int N, int K, float* stats, const bf16_t* D, int64_t ldd, const BnBwdEpi& bnb,
                         hipStream_t stream) {
@@ -233,7 +240,7 @@ static void launch_nt_p(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t l
   const size_t ab = BT ? run_mainloop_lds_bytes<PIPE, BM, BN, RowLoader<BM, NT>, KLoader<BN, NT>>()
                        : run_mainloop_lds_bytes<PIPE, BM, BN, RowLoader<BM, NT>, RowLoader<BN, NT>>();
   const size_t cs = epilogue_lds_bytes<BM, BN, S, NT>();
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, S, BT, PIPE, NT>), dim3(tiles), dim3(NT), std::max(ab, cs), stream, A,
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, S, BT, PIPE, NT, kD>), dim3(tiles), dim3(NT), std::max(ab, cs), stream, A,
                      lda, B, ldb, C, ldc, M, N, K, stats, D, ldd, bnb);
 }
 
@@ -291,6 +298,17 @@ static int g_tile256_min_k_stats = [] {
 }();
 void set_tile256_min_k_stats(int k) { g_tile256_min_k_stats = k > 0 ? k : 256; }
 
+static int g_gemm256_direct = -1;  // -1: DLA_GEMM256_DIRECT (default off), 0 / 1
+void set_gemm256_direct(int mode) { g_gemm256_direct = mode < 0 ? -1 : (mode ? 1 : 0); }
+bool gemm256_direct_enabled() {
+  if (g_gemm256_direct >= 0) return g_gemm256_direct == 1;
+  static const bool v = [] {
+    const char* e = std::getenv("DLA_GEMM256_DIRECT");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 int pick_tile(int64_t M, int N, int tile, int K, bool wide_ok, bool stats) {
   if (tile != kTileAuto) return tile;
   const int min_k = stats ? std::min(g_tile256_min_k, g_tile256_min_k_stats) : g_tile256_min_k;
@@ -345,6 +363,14 @@ void launch_gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void
   if (cfg == kTile128x128 && tile == kTileAuto && !bn_bwd && !addend2_s2 && !(stats && addend) &&
       gemm_direct_ok(N, ldc, addend, ld_addend)) {
     launch_gemm_direct(A, lda, B, ldb, b_kmajor, C, ldc, M, N, K, stats, addend, ld_addend, addend_mask, stream);
+    return;
+  }
+  // the 256x256 statistics forwards stored from the registers (DLA_GEMM256_DIRECT / set_gemm256_direct, A/B)
+  if (cfg == kTile256x256 && stats && !b_kmajor && !addend && !bn_bwd && !addend2_s2 && gemm256_direct_enabled()) {
+    if (mfma_pipeline() == 2)
+      launch_nt_p<256, 256, true, false, 2, 512, true>(a, lda, b, ldb, c, ldc, M, N, K, stats, d, ld_addend, bnb, stream);
+    else
+      launch_nt_p<256, 256, true, false, 6, 512, true>(a, lda, b, ldb, c, ldc, M, N, K, stats, d, ld_addend, bnb, stream);
     return;
   }
   switch (cfg) {

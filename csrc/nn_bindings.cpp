@@ -1284,6 +1284,7 @@ void bind_nn(pybind11::module& m) {
         "streaming 1x1-conv forward over a deferred BN+ReLU output: writes relu(BN(y)) and returns (C, stats)",
         pybind11::arg("y"), pybind11::arg("ws"), pybind11::arg("B"), pybind11::arg("out"));
   m.def("gemm_nt_stream_apply_ok", &gemm_nt_stream_apply_ok, "shapes gemm_nt_stream_apply serves (M, N, K)");
+  m.def("set_gemm256_direct", &set_gemm256_direct, "256x256 statistics forwards stored from registers (-1 env, 0, 1)");
   m.def("set_stem_stream", &set_stem_stream, "stem forward on the persistent streaming GEMM (-1 env, 0, 1)");
   m.def("set_wgrad_w4", &set_wgrad_w4, "128x256 tiles for the Cout-128 3x3 weight gradients (-1 env, 0, 1)");
   m.def("set_gemm_apply_max_k", &set_gemm_apply_max_k, "largest K gemm_nt_apply serves (<= 0: environment / 512)");

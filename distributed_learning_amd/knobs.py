@@ -64,6 +64,8 @@ TABLE: Dict[str, Knob] = {
     # ---- kernel selection (C++) --------------------------------------------------------------------
     "STEM_STREAM": Knob("0", "csrc/kernels/gemm_stream.hip", "1: the stem forward (with BN statistics) on the persistent "
                                                              "streaming GEMM instead of the 128x64 tile kernel"),
+    "GEMM256_DIRECT": Knob("0", "csrc/kernels/gemm.hip", "1: the 256x256 statistics forwards store their tile and "
+                                                          "statistics from registers (dla_mfma.h epilogue_direct)"),
     "TILE256": Knob("1", "csrc/kernels/gemm.hip", "0: no 256x256 tiles for fwd / dgrad (profiles/r5a/)"),
     "TILE512": Knob("1", "csrc/kernels/conv.hip", "0: no 512x128 tiles for the Cout-128 3x3 fwd / dgrad (profiles/r5/g54/)"),
     "TILE256_MIN_K_STATS": Knob("256", "csrc/kernels/gemm.hip", "smallest K of the 256x256 tiles for the forward GEMMs "
