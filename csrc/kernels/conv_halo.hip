@@ -180,8 +180,10 @@ __global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __r
         for (int j = 0; j < AC::TN; ++j) acc.v[i][j] = mfma_t<kDirect>(af[cb][i], bfr[cb][j], acc.v[i][j]);
       __builtin_amdgcn_s_setprio(0);
     }
-    if constexpr (kDirect) {
-      static_assert(!kStats && AC::TM == 4 && AC::TN == 2, "direct stores: 64 x 32 wave tiles, no statistics");
+    if constexpr (kDirect && kStats) {  // the forward: the generic register-direct epilogue with statistics
+      epilogue_direct<kHBM, kHC, true, kHNT>(acc, y, kHC, P, kHC, row0, 0, stats + (int64_t)s * kHC * 2, stage);
+    } else if constexpr (kDirect) {
+      static_assert(AC::TM == 4 && AC::TN == 2, "direct stores: 64 x 32 wave tiles");
       // acc.v[i][j][r]: pixel 16 i + p of the wave's 64 rows, channel 16 j + 4 g + r of its 32 columns; after the
       // swap the lane holds channels n .. n + 7 of each of its 4 pixels
       const int g = lane >> 4, p = lane & 15;
@@ -534,7 +536,10 @@ void launch_conv3x3_halo(const void* x, const void* w, void* y, int N, int H, in
     return e && e[0] == '1';
   }();
   if (ver == 1) {
-    if (stats)
+    if (stats && direct_fwd && !addend)
+      hipLaunchKernelGGL((conv3x3_halo_kernel<true, true>), dim3(grid), dim3(kHNT), kHLds, stream, xp, wp, yp, H, W,
+                         P, nstrips, per_block, stats, ap, fW, fH, use_fast);
+    else if (stats)
       hipLaunchKernelGGL(conv3x3_halo_kernel<true>, dim3(grid), dim3(kHNT), kHLds, stream, xp, wp, yp, H, W, P,
                          nstrips, per_block, stats, ap, fW, fH, use_fast);
     else if (direct)

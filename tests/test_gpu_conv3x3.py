@@ -195,8 +195,8 @@ print("halo ok")
 
 
 # 3: variant 2 forward, variant 1 data gradient; "d": the variant-1 data gradient stored from registers, "f": the
-# variant-2 forward (tile and statistics) from registers
-@pytest.mark.parametrize("version", ["1", "2", "3", "1d", "3d", "2f", "3df"])
+# forward (tile and statistics) from registers (variant 2, or variant 1 through dla_mfma.h epilogue_direct)
+@pytest.mark.parametrize("version", ["1", "2", "3", "1d", "3d", "2f", "3df", "1f", "1df"])
 def test_conv3x3_halo_c64(cuda, version):
     """64 -> 64 channel stride-1 3x3 convs on the halo-tiled persistent kernel, forward and data
     gradient, both kernel variants (a fresh process with DLA_HALO=2, read once): forward bitwise equal to the
