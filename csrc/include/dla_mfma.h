@@ -1044,6 +1044,7 @@ __device__ __forceinline__ void epilogue_bf16(const Acc<BM, BN, NT>& acc, bf16_t
 // staging barriers (gemm_direct.hip, conv_halo.hip kDirect). With stats_row: the [N][2] (sum, sumsq) partial row of
 // the tile's stored (bf16-rounded) values, summed in registers over the lane's rows, over the 16 lanes of a DPP
 // row, and over the WGM M-waves through 2 * WGM * BN floats of LDS (the main loop's image bytes, free by then).
+// D (optional, no statistics): C = bf16(bf16(acc) + D), the staged epilogue's unfused add, D [M][N] row stride ldd.
 template <int CTRL>
 __device__ __forceinline__ float epi_dpp_add(float v) {
   const int o = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false);
@@ -1059,7 +1060,8 @@ __device__ __forceinline__ float epi_row16_sum(float v) {  // pairs {i, 15-i}, {
 template <int BM, int BN, bool kStats, int NT = kThreads>
 __device__ __forceinline__ void epilogue_direct(const Acc<BM, BN, NT>& acc, bf16_t* __restrict__ C, int64_t ldc,
                                                 int64_t M, int N, int64_t row0, int col0,
-                                                float* __restrict__ stats_row, char* smem) {
+                                                float* __restrict__ stats_row, char* smem,
+                                                const bf16_t* __restrict__ D = nullptr, int64_t ldd = 0) {
   using AC = Acc<BM, BN, NT>;
   constexpr int WM = AC::WM, WN = AC::WN, TM = AC::TM, TN = AC::TN;
   static_assert(kMS == 16 && TN % 2 == 0, "16x16 fragments in column pairs");
@@ -1069,6 +1071,19 @@ __device__ __forceinline__ void epilogue_direct(const Acc<BM, BN, NT>& acc, bf16
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid / AC::WGN, wc = wid % AC::WGN;
   const int g = lane >> 4, p = lane & 15;
   const int64_t pix0 = row0 + wr * WM + p;  // + 16 i
+  const int cb = col0 + wc * WN + 16 * (g & 1) + 8 * (g >> 1);  // + 32 hh: the lane's 16-byte chunks after the swap
+  u32x4_t dv[kStats ? 1 : TM][TN / 2];
+  if (!kStats && D) {  // every addend chunk in flight before the packing
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int hh = 0; hh < TN / 2; ++hh) {
+        const int64_t m = pix0 + 16 * i;
+        const int n = cb + 32 * hh;
+        dv[kStats ? 0 : i][hh] = (m < M && n < N) ? *reinterpret_cast<const u32x4_t*>(D + m * ldd + n)
+                                                   : u32x4_t{0u, 0u, 0u, 0u};
+      }
+  }
   uint32_t u[TM][TN][2];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -1125,14 +1140,22 @@ __device__ __forceinline__ void epilogue_direct(const Acc<BM, BN, NT>& acc, bf16
         u[i][jp][h] = r[0];
         u[i][jp + 1][h] = r[1];
       }
-  const int cb = col0 + wc * WN + 16 * (g & 1) + 8 * (g >> 1);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int64_t m = pix0 + 16 * i;
 #pragma unroll
     for (int hh = 0; hh < TN / 2; ++hh) {
       const int n = cb + 32 * hh;
-      const u32x4_t v{u[i][2 * hh][0], u[i][2 * hh][1], u[i][2 * hh + 1][0], u[i][2 * hh + 1][1]};
+      u32x4_t v{u[i][2 * hh][0], u[i][2 * hh][1], u[i][2 * hh + 1][0], u[i][2 * hh + 1][1]};
+      if (!kStats && D) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t d = dv[kStats ? 0 : i][hh][e];
+          const float lo = __builtin_bit_cast(float, v[e] << 16) + __builtin_bit_cast(float, d << 16);
+          const float hi = __builtin_bit_cast(float, v[e] & 0xffff0000u) + __builtin_bit_cast(float, d & 0xffff0000u);
+          v[e] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+        }
+      }
       if (m < M && n < N) *reinterpret_cast<u32x4_t*>(C + m * ldc + n) = v;
     }
   }

@@ -182,51 +182,8 @@ __global__ __launch_bounds__(kHNT, 1) void conv3x3_halo_kernel(const bf16_t* __r
     }
     if constexpr (kDirect && kStats) {  // the forward: the generic register-direct epilogue with statistics
       epilogue_direct<kHBM, kHC, true, kHNT>(acc, y, kHC, P, kHC, row0, 0, stats + (int64_t)s * kHC * 2, stage);
-    } else if constexpr (kDirect) {
-      static_assert(AC::TM == 4 && AC::TN == 2, "direct stores: 64 x 32 wave tiles");
-      // acc.v[i][j][r]: pixel 16 i + p of the wave's 64 rows, channel 16 j + 4 g + r of its 32 columns; after the
-      // swap the lane holds channels n .. n + 7 of each of its 4 pixels
-      const int g = lane >> 4, p = lane & 15;
-      const int64_t pix0 = row0 + wr * AC::WM + p;
-      const int n = wc * AC::WN + 16 * (g & 1) + 8 * (g >> 1);
-      typedef float f32x2_t __attribute__((ext_vector_type(2)));
-      typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-      typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-      auto pack = [](float a, float b) {
-        return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{a, b}), bf16x2_t));
-      };
-      u32x4_t dv[AC::TM];
-      if (addend) {  // C = bf16(bf16(acc) + D), the staged epilogue's unfused add; all loads before the packing
-#pragma unroll
-        for (int i = 0; i < AC::TM; ++i) {
-          const int64_t m = pix0 + 16 * i;
-          dv[i] = m < P ? *reinterpret_cast<const u32x4_t*>(addend + m * kHC + n) : u32x4_t{0u, 0u, 0u, 0u};
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < AC::TM; ++i) {
-        uint32_t u0[2], u1[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          u0[h] = pack(acc.v[i][0][2 * h], acc.v[i][0][2 * h + 1]);
-          u1[h] = pack(acc.v[i][1][2 * h], acc.v[i][1][2 * h + 1]);
-          const auto r = __builtin_amdgcn_permlane16_swap(u0[h], u1[h], false, false);
-          u0[h] = r[0];
-          u1[h] = r[1];
-        }
-        u32x4_t v{u0[0], u0[1], u1[0], u1[1]};
-        if (addend) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float lo = __builtin_bit_cast(float, v[e] << 16) + __builtin_bit_cast(float, dv[i][e] << 16);
-            const float hi = __builtin_bit_cast(float, v[e] & 0xffff0000u) +
-                             __builtin_bit_cast(float, dv[i][e] & 0xffff0000u);
-            v[e] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
-          }
-        }
-        const int64_t m = pix0 + 16 * i;
-        if (m < P) *reinterpret_cast<u32x4_t*>(y + m * kHC + n) = v;
-      }
+    } else if constexpr (kDirect) {  // the data gradient (+ its plain addend), same epilogue
+      epilogue_direct<kHBM, kHC, false, kHNT>(acc, y, kHC, P, kHC, row0, 0, nullptr, stage, addend, kHC);
     } else {
       ColStats<kHBM, kHC, kHNT> st;
       st.zero();

@@ -49,19 +49,8 @@ __device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
 __device__ __forceinline__ f32x2_t unpack_bf16(uint32_t u) {
   return f32x2_t{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
 }
-// v + the value of the DPP-permuted lane (ctrl: row_mirror 0x140, row_half_mirror 0x141, quad_perm)
-template <int CTRL>
-__device__ __forceinline__ float dpp_add(float v) {
-  const int o = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false);
-  return v + __builtin_bit_cast(float, o);
-}
-// sum over the 16 lanes of a DPP row: pairs {i, 15-i}, {i, 7-i} within halves, xor 2, xor 1
-__device__ __forceinline__ float row16_sum(float v) {
-  v = dpp_add<0x140>(v);
-  v = dpp_add<0x141>(v);
-  v = dpp_add<0x4E>(v);
-  return dpp_add<0xB1>(v);
-}
+// sum over the 16 lanes of a DPP row (dla_mfma.h epi_row16_sum)
+__device__ __forceinline__ float row16_sum(float v) { return epi_row16_sum(v); }
 
 // bf16(x) + (bit ? d : 0) rounded to bf16, for the 2 packed values of u and d
 __device__ __forceinline__ uint32_t add_pair(uint32_t u, uint32_t d, uint32_t bits) {
